@@ -1,0 +1,37 @@
+"""Build the native C++ runtime tools (no GPU needed): supervisor + GPU/topology probe.
+
+Outputs go to ``arena_amd/bin/`` (git-ignored, shipped to the GPU box with the tree).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+BIN = os.path.join(HERE, "bin")
+
+TOOLS = {
+    # name: (sources, extra flags)
+}
+
+
+def tool_path(name: str) -> str:
+    return os.path.join(BIN, name)
+
+
+def build_native_tools(force: bool = False) -> list[str]:
+    os.makedirs(BIN, exist_ok=True)
+    cxx = shutil.which("g++") or shutil.which("c++")
+    built = []
+    for name, (srcs, flags) in TOOLS.items():
+        out = tool_path(name)
+        paths = [os.path.join(ROOT, s) for s in srcs]
+        if not force and os.path.exists(out) and all(
+                os.path.getmtime(out) >= os.path.getmtime(p) for p in paths):
+            built.append(out)
+            continue
+        subprocess.run([cxx, "-O2", "-std=c++17", "-Wall", "-o", out, *paths, *flags], check=True)
+        built.append(out)
+    return built

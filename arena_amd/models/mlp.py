@@ -1,0 +1,343 @@
+"""Fused MNIST MLP trainer -- the bundled reference workload, built MI355X-first.
+
+Model = the reference's demo job (`mnist_with_summaries`: 784-500-10, ReLU, dropout keep 0.9,
+softmax cross-entropy, Adam lr 1e-3, batch 100; `docs/userguide/1-tfjob-standalone.md:178-186`),
+and `dist-mnist`'s 784-100-10 variant via ``hidden=100``.
+
+Execution design:
+  * ALL parameters live in ONE flat fp32 buffer (Adam m/v and the gradient bucket mirror it), so
+    the data-parallel gradient all-reduce is a single RCCL call on a contiguous buffer and Adam is a
+    single launch -- no flatten/unflatten copies, no per-tensor launches.
+  * The training set lives in HBM as uint8; the batch gather (permutation + device step counter)
+    and the /255 dequantisation are fused into the first GEMM and the loss head.
+  * One step = 3 launches on one GPU (linear_fwd -> xent_head -> wgrad_grouped with fused Adam);
+    with data parallelism 5 (grad bucket -> all_reduce -> adam_flat).
+  * Every per-step scalar (data cursor, Adam t, dropout step, metric slot) is a device counter, so
+    ``steps_per_graph`` consecutive steps are captured into ONE hipGraph and replayed.
+Step-counter protocol (no intra-kernel races): A = completed steps, B = current Adam t.
+  linear_fwd reads A; xent_head reads A and writes B=A+1; wgrad reads B (cursor = B-1);
+  the last kernel of the step (wgrad with fused Adam, or adam_flat) writes A=B.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import Optional
+
+import torch
+
+from .. import ops
+
+
+@dataclass
+class MLPConfig:
+    in_dim: int = 784
+    hidden: int = 500
+    classes: int = 10
+    keep_prob: float = 0.9
+    batch: int = 100            # per-rank batch
+    lr: float = 1e-3
+    betas: tuple = (0.9, 0.999)
+    eps: float = 1e-8
+    tf_adam: bool = False       # TF AdamOptimizer epsilon placement
+    seed: int = 0
+    init: str = "tf"            # "tf": truncated normal(0.1), bias 0.1 (mnist_with_summaries)
+    hist_len: int = 4096
+
+
+def _pad4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+@dataclass
+class FlatLayout:
+    shapes: dict
+    offsets: dict = field(default_factory=dict)
+    total: int = 0
+
+    def __post_init__(self):
+        off = 0
+        for name, shp in self.shapes.items():
+            self.offsets[name] = off
+            off += _pad4(math.prod(shp))
+        self.total = off
+
+    def view(self, flat: torch.Tensor, name: str) -> torch.Tensor:
+        shp = self.shapes[name]
+        o = self.offsets[name]
+        return flat[o:o + math.prod(shp)].view(shp)
+
+
+class FusedMLPTrainer:
+    """Single-hidden-layer MLP trained entirely by the native HIP kernels (or the CPU reference)."""
+
+    def __init__(self, cfg: MLPConfig, train_x: torch.Tensor, train_y: torch.Tensor,
+                 device: torch.device | str = "cuda", process_group=None,
+                 rank: int = 0, world: int = 1):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.pg = process_group
+        self.rank, self.world = rank, world
+        self.distributed = world > 1
+        dev = self.device
+        D, H, C = cfg.in_dim, cfg.hidden, cfg.classes
+        if D % 4 or H % 4:
+            raise ValueError("in_dim and hidden must be multiples of 4 (vectorised MFMA operands)")
+        self.layout = FlatLayout({"W1": (D, H), "b1": (H,), "W2": (H, C), "b2": (C,)})
+        n = self.layout.total
+        self.P = torch.zeros(n, device=dev)
+        self.M = torch.zeros(n, device=dev)
+        self.V = torch.zeros(n, device=dev)
+        self.G = torch.zeros(n, device=dev) if self.distributed else None
+        self._init_params()
+        if self.distributed:
+            import torch.distributed as dist
+            dist.broadcast(self.P, src=0, group=self.pg)
+        L = self.layout
+        self.W1, self.b1 = L.view(self.P, "W1"), L.view(self.P, "b1")
+        self.W2, self.b2 = L.view(self.P, "W2"), L.view(self.P, "b2")
+        self.mW1, self.mb1 = L.view(self.M, "W1"), L.view(self.M, "b1")
+        self.mW2, self.mb2 = L.view(self.M, "W2"), L.view(self.M, "b2")
+        self.vW1, self.vb1 = L.view(self.V, "W1"), L.view(self.V, "b1")
+        self.vW2, self.vb2 = L.view(self.V, "W2"), L.view(self.V, "b2")
+        if self.G is not None:
+            self.gW1, self.gb1 = L.view(self.G, "W1"), L.view(self.G, "b1")
+            self.gW2, self.gb2 = L.view(self.G, "W2"), L.view(self.G, "b2")
+        B = cfg.batch
+        self.Hbuf = torch.empty(B, H, device=dev)
+        self.dZ = torch.empty(B, H, device=dev)
+        self.dlogits = torch.empty(B, C, device=dev)
+        self.ctrA = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.ctrB = torch.zeros(1, dtype=torch.int64, device=dev)
+        self.loss_hist = torch.zeros(cfg.hist_len, device=dev)
+        self.corr_hist = torch.zeros(cfg.hist_len, dtype=torch.int32, device=dev)
+        self.lr_t = torch.full((1,), cfg.lr, device=dev)
+        # data: resident in HBM, rank-sharded (Horovod-style DP), reshuffled per epoch
+        self.train_x = train_x.to(dev).contiguous()
+        self.train_y = train_y.to(dev).contiguous()
+        n_all = self.train_x.shape[0]
+        self.shard = torch.arange(rank, n_all, world, dtype=torch.int64)
+        if self.shard.numel() < B:
+            raise ValueError("dataset shard smaller than one batch")
+        if int(self.shard.max()) >= n_all:
+            raise ValueError("shard index out of range")
+        self.shard = self.shard.to(dev)
+        self._gen = torch.Generator(device=dev).manual_seed(cfg.seed * 7919 + rank)
+        self.perm = torch.empty(self.shard.numel(), dtype=torch.int32, device=dev)
+        self._reshuffle()
+        self.steps_done = 0
+        self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
+        self.graph_mode = None
+
+    # ------------------------------------------------------------------------------------------
+    def _init_params(self):
+        g = torch.Generator().manual_seed(self.cfg.seed)
+        L = self.layout
+        for name, shp in L.shapes.items():
+            if name.startswith("W"):
+                if self.cfg.init == "tf":
+                    w = torch.randn(shp, generator=g) * 0.1
+                    bad = w.abs() > 0.2
+                    while bad.any():  # truncated normal: redraw beyond 2 sigma
+                        w[bad] = torch.randn(int(bad.sum()), generator=g) * 0.1
+                        bad = w.abs() > 0.2
+                else:
+                    bound = 1.0 / math.sqrt(shp[0])
+                    w = (torch.rand(shp, generator=g) * 2 - 1) * bound
+                L.view(self.P, name).copy_(w)
+            else:
+                L.view(self.P, name).fill_(0.1 if self.cfg.init == "tf" else 0.0)
+
+    def _reshuffle(self):
+        """New epoch order, generated on the device (no host sync). Indices are a permutation of
+        this rank's shard, which was range-checked against the dataset at construction."""
+        rp = torch.randperm(self.shard.numel(), generator=self._gen, device=self.device)
+        self.perm.copy_(self.shard[rp].to(torch.int32))
+
+    def pick_steps_per_graph(self, cap: int = 64) -> int:
+        """Largest divisor of the epoch length <= cap, so graphs never straddle a reshuffle."""
+        spe = self.steps_per_epoch
+        return max(d for d in range(1, min(cap, spe) + 1) if spe % d == 0)
+
+    @property
+    def steps_per_epoch(self) -> int:
+        return self.perm.numel() // self.cfg.batch
+
+    # ------------------------------------------------------------------------------------------
+    def _launch_step(self):
+        """Enqueue one training step (no host sync, graph-capturable)."""
+        if self.distributed:
+            for part in range(3):
+                self._launch_step_part(part)
+            return
+        cfg = self.cfg
+        B = cfg.batch
+        A, Bc = self.ctrA, self.ctrB
+        ops.linear_fwd(self.train_x, self.W1, self.Hbuf, self.b1, x_scale=1.0 / 255.0,
+                       idx=self.perm, cursor=A, batch=B, act=1, keep_prob=cfg.keep_prob,
+                       seed=cfg.seed * 2654435761 + self.rank, step=A)
+        ops.xent_head(self.Hbuf, self.W2, self.b2, self.train_y, loss_acc=self.loss_hist,
+                      correct_acc=self.corr_hist, idx=self.perm, cursor=A, batch=B,
+                      dlogits=self.dlogits, dZ=self.dZ, keep_prob=cfg.keep_prob, relu_mask=True,
+                      loss_scale=1.0 / B, hist_step=A, ctr_dst=Bc, ctr_src=A, ctr_add=1)
+        common = dict(x_scales=[1.0 / 255.0, 1.0], gather=[True, False], idx=self.perm,
+                      cursor=Bc, cursor_off=-1, batch=B)
+        adam = dict(lr=cfg.lr, lr_t=self.lr_t, betas=cfg.betas, eps=cfg.eps, t_step=Bc,
+                    tf_style=cfg.tf_adam)
+        ops.wgrad_grouped([self.train_x, self.Hbuf], [self.dZ, self.dlogits],
+                          [self.W1, self.W2], [self.b1, self.b2], mode=1,
+                          mW=[self.mW1, self.mW2], vW=[self.vW1, self.vW2],
+                          mB=[self.mb1, self.mb2], vB=[self.vb1, self.vb2],
+                          ctr_dst=A, ctr_src=Bc, ctr_add=0, **common, **adam)
+
+    def _capture(self, nsteps: int) -> torch.cuda.CUDAGraph:
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(nsteps):
+                self._launch_step()
+        return g
+
+    def enable_graphs(self, steps_per_graph: int = 50) -> bool:
+        """Capture ``steps_per_graph`` steps per hipGraph. Returns False if capture failed
+        (e.g. a collective backend that refuses capture) -- steps then run eagerly."""
+        if self.device.type != "cuda":
+            return False
+        self.steps_per_graph = steps_per_graph
+        # warm up on a side stream (allocator / collective communicators initialised outside
+        # capture), then restore the state so warm-up steps do not count as training.
+        snap = [t.clone() for t in (self.P, self.M, self.V, self.ctrA, self.ctrB)]
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self._launch_step()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        for t, v in zip((self.P, self.M, self.V, self.ctrA, self.ctrB), snap):
+            t.copy_(v)
+        try:
+            self._graphs[steps_per_graph] = self._capture(steps_per_graph)
+            self.graph_mode = "full"
+        except Exception as e:  # noqa: BLE001
+            self._graph_error = repr(e)
+            self._graphs.clear()
+            self.graph_mode = None
+            torch.cuda.synchronize()
+            if self.distributed:
+                return self._enable_split_graphs()
+            return False
+        torch.cuda.synchronize()
+        return True
+
+    def _enable_split_graphs(self) -> bool:
+        """Collective refused capture: graph the compute before/after an eager all_reduce."""
+        try:
+            pre, post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+            self._split = True
+            with torch.cuda.graph(pre):
+                self._launch_step_part(0)
+            with torch.cuda.graph(post):
+                self._launch_step_part(2)
+            self._split_graphs = (pre, post)
+            self.graph_mode = "split"
+            torch.cuda.synchronize()
+            return True
+        except Exception as e:  # noqa: BLE001
+            self._graph_error += " | split: " + repr(e)
+            self._split_graphs = None
+            self.graph_mode = None
+            torch.cuda.synchronize()
+            return False
+
+    def _launch_step_part(self, part: int):
+        """DP step in three parts: 0 = compute up to the grad bucket, 1 = all_reduce, 2 = Adam."""
+        cfg, B, A, Bc = self.cfg, self.cfg.batch, self.ctrA, self.ctrB
+        if part == 0:
+            ops.linear_fwd(self.train_x, self.W1, self.Hbuf, self.b1, x_scale=1.0 / 255.0,
+                           idx=self.perm, cursor=A, batch=B, act=1, keep_prob=cfg.keep_prob,
+                           seed=cfg.seed * 2654435761 + self.rank, step=A)
+            ops.xent_head(self.Hbuf, self.W2, self.b2, self.train_y, loss_acc=self.loss_hist,
+                          correct_acc=self.corr_hist, idx=self.perm, cursor=A, batch=B,
+                          dlogits=self.dlogits, dZ=self.dZ, keep_prob=cfg.keep_prob,
+                          relu_mask=True, loss_scale=1.0 / B, hist_step=A, ctr_dst=Bc, ctr_src=A,
+                          ctr_add=1)
+            ops.wgrad_grouped([self.train_x, self.Hbuf], [self.dZ, self.dlogits],
+                              [self.gW1, self.gW2], [self.gb1, self.gb2], mode=0, grad_scale=1.0,
+                              x_scales=[1.0 / 255.0, 1.0], gather=[True, False], idx=self.perm,
+                              cursor=Bc, cursor_off=-1, batch=B)
+        elif part == 1:
+            import torch.distributed as dist
+            dist.all_reduce(self.G, group=self.pg)
+        else:
+            ops.adam_flat(self.P, self.M, self.V, self.G, grad_scale=1.0 / self.world,
+                          ctr_dst=A, ctr_src=Bc, ctr_add=0, lr=cfg.lr, lr_t=self.lr_t,
+                          betas=cfg.betas, eps=cfg.eps, t_step=Bc, tf_style=cfg.tf_adam)
+
+    def train_steps(self, n: int):
+        """Run n steps (graph replays where possible). Reshuffles at epoch boundaries."""
+        spe = self.steps_per_epoch
+        while n > 0:
+            to_epoch_end = spe - (self.steps_done % spe)
+            chunk = min(n, to_epoch_end)
+            k = getattr(self, "steps_per_graph", 0)
+            while chunk > 0:
+                if self._graphs and chunk >= k:
+                    self._graphs[k].replay()
+                    done = k
+                elif self.graph_mode == "split":
+                    pre, post = self._split_graphs
+                    pre.replay()
+                    self._launch_step_part(1)
+                    post.replay()
+                    done = 1
+                else:
+                    self._launch_step()
+                    done = 1
+                chunk -= done
+                n -= done
+                self.steps_done += done
+            if self.steps_done % spe == 0:
+                self._reshuffle()
+
+    # ------------------------------------------------------------------------------------------
+    def recent_metrics(self, last: int = 100):
+        """(mean loss, train accuracy) over the last ``last`` completed steps (host sync)."""
+        done = int(self.ctrA.item())
+        L = self.cfg.hist_len
+        last = min(last, done, L - 1)
+        if last <= 0:
+            return float("nan"), float("nan")
+        idx = torch.tensor([(done - 1 - i) % L for i in range(last)], device=self.device)
+        loss = float(self.loss_hist[idx].mean().item())
+        acc = float(self.corr_hist[idx].float().mean().item()) / self.cfg.batch
+        return loss, acc
+
+    @torch.no_grad()
+    def evaluate(self, test_x: torch.Tensor, test_y: torch.Tensor, chunk: int = 10000):
+        """Test-set (loss, accuracy) with dropout off, on the same kernels."""
+        dev = self.device
+        n = test_x.shape[0]
+        loss_acc = torch.zeros(1, device=dev)
+        corr = torch.zeros(1, dtype=torch.int32, device=dev)
+        tx = test_x.to(dev).contiguous()
+        ty = test_y.to(dev).contiguous()
+        for s in range(0, n, chunk):
+            xs = tx[s:s + chunk]
+            ys = ty[s:s + chunk]
+            h = torch.empty(xs.shape[0], self.cfg.hidden, device=dev)
+            ops.linear_fwd(xs, self.W1, h, self.b1, x_scale=1.0 / 255.0, act=1, keep_prob=1.0)
+            ops.xent_head(h, self.W2, self.b2, ys, loss_acc=loss_acc, correct_acc=corr,
+                          loss_scale=1.0 / n)
+        return float(loss_acc.item()), float(corr.item()) / n
+
+    def state_dict(self):
+        return {"P": self.P.detach().cpu(), "M": self.M.detach().cpu(), "V": self.V.detach().cpu(),
+                "step": int(self.ctrA.item()), "layout": dict(self.layout.shapes)}
+
+    def load_state_dict(self, sd):
+        self.P.copy_(sd["P"])
+        self.M.copy_(sd["M"])
+        self.V.copy_(sd["V"])
+        self.ctrA.fill_(int(sd["step"]))
+        self.ctrB.fill_(int(sd["step"]))
+        self.steps_done = int(sd["step"])

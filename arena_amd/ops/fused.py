@@ -1,0 +1,101 @@
+"""Functional API over the native kernels with device dispatch.
+
+GPU tensors -> HIP kernels in ``arena_amd._C`` (raises if the extension is missing: no silent
+fallback); CPU tensors -> the bit-compatible PyTorch reference in :mod:`arena_amd.ops.reference`.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+
+from . import _ext, reference
+
+Tensor = torch.Tensor
+
+
+def _impl(t: Tensor):
+    return _ext.load() if t.is_cuda else reference
+
+
+def linear_fwd(x: Tensor, W: Tensor, Y: Tensor, bias: Optional[Tensor] = None, *,
+               x_scale: float = 1.0, idx: Optional[Tensor] = None,
+               cursor: Optional[Tensor] = None, batch: int = 0, act: int = 1,
+               keep_prob: float = 1.0, seed: int = 0, step: Optional[Tensor] = None) -> Tensor:
+    """Y = dropout(act(gather(x)·scale @ W + bias)). ``act``: 0 identity, 1 ReLU."""
+    _impl(W).linear_fwd(x, float(x_scale), idx, cursor, int(batch), W, bias, Y, int(act),
+                        float(keep_prob), int(seed), step)
+    return Y
+
+
+def xent_head(H: Tensor, W2: Tensor, b2: Optional[Tensor], labels: Tensor, *,
+              loss_acc: Tensor, correct_acc: Tensor, idx: Optional[Tensor] = None,
+              cursor: Optional[Tensor] = None, batch: int = 0,
+              dlogits: Optional[Tensor] = None, dZ: Optional[Tensor] = None,
+              keep_prob: float = 1.0, relu_mask: bool = True, loss_scale: float = 1.0,
+              hist_step: Optional[Tensor] = None, ctr_dst: Optional[Tensor] = None,
+              ctr_src: Optional[Tensor] = None, ctr_add: int = 0) -> None:
+    _impl(H).xent_head(H, W2, b2, labels, idx, cursor, int(batch), dlogits, dZ, float(keep_prob),
+                       bool(relu_mask), float(loss_scale), loss_acc, correct_acc, hist_step,
+                       ctr_dst, ctr_src, int(ctr_add))
+
+
+def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Tensor], outW: Sequence[Tensor],
+                  outB: Sequence[Optional[Tensor]], *, x_scales: Sequence[float],
+                  gather: Sequence[bool], idx: Optional[Tensor] = None,
+                  cursor: Optional[Tensor] = None, cursor_off: int = 0, batch: int = 0,
+                  mode: int = 0, mW=None, vW=None, mB=None, vB=None, lr: float = 1e-3,
+                  lr_t: Optional[Tensor] = None, betas=(0.9, 0.999), eps: float = 1e-8,
+                  weight_decay: float = 0.0, t_step: Optional[Tensor] = None,
+                  grad_scale: float = 1.0, tf_style: bool = False,
+                  ctr_dst: Optional[Tensor] = None, ctr_src: Optional[Tensor] = None,
+                  ctr_add: int = 0) -> None:
+    """dW_i = gather(x_i)ᵀ·dz_i, db_i = Σ_rows dz_i for up to 4 layers in one launch.
+
+    mode 0 writes ``grad_scale * dW`` into ``outW`` (e.g. views of the flat all-reduce bucket);
+    mode 1 applies Adam in place to parameters ``outW``/``outB`` with state ``mW,vW,mB,vB``.
+    """
+    n = len(xs)
+    none = [None] * n
+    _impl(dzs[0]).wgrad_grouped(list(xs), [float(s) for s in x_scales], [bool(g) for g in gather],
+                                idx, cursor, int(cursor_off), int(batch), list(dzs), int(mode),
+                                list(outW), list(outB), list(mW or none), list(vW or none),
+                                list(mB or none), list(vB or none), float(lr), lr_t,
+                                float(betas[0]), float(betas[1]), float(eps), float(weight_decay),
+                                t_step, float(grad_scale), bool(tf_style), ctr_dst, ctr_src,
+                                int(ctr_add))
+
+
+def adam_flat(P: Tensor, M: Tensor, V: Tensor, G: Tensor, *, lr: float = 1e-3,
+              lr_t: Optional[Tensor] = None, betas=(0.9, 0.999), eps: float = 1e-8,
+              weight_decay: float = 0.0, t_step: Optional[Tensor] = None,
+              grad_scale: float = 1.0, tf_style: bool = False,
+              ctr_dst: Optional[Tensor] = None, ctr_src: Optional[Tensor] = None,
+              ctr_add: int = 0) -> None:
+    _impl(P).adam_flat(P, M, V, G, float(lr), lr_t, float(betas[0]), float(betas[1]), float(eps),
+                       float(weight_decay), t_step, float(grad_scale), bool(tf_style), ctr_dst,
+                       ctr_src, int(ctr_add))
+
+
+def sgd_flat(P: Tensor, G: Tensor, *, lr: float, lr_t: Optional[Tensor] = None,
+             grad_scale: float = 1.0) -> None:
+    _impl(P).sgd_flat(P, G, float(lr), lr_t, float(grad_scale))
+
+
+def softmax_xent(logits: Tensor, labels: Tensor, grad_scale: float = 1.0,
+                 need_grad: bool = True):
+    """Per-row cross-entropy loss and (optionally) dlogits = (softmax - onehot) * grad_scale."""
+    out = _impl(logits).softmax_xent(logits, labels, float(grad_scale), bool(need_grad))
+    return tuple(out)
+
+
+def flatten_into(tensors: Sequence[Tensor], offsets: Sequence[int], flat: Tensor,
+                 scale: float = 1.0) -> None:
+    """flat[off_i : off_i+n_i] = t_i * scale (one multi-tensor launch per 48 tensors)."""
+    _impl(flat).mt_copy_scale(list(tensors), [int(o) for o in offsets], flat, float(scale), 0)
+
+
+def unflatten_from(tensors: Sequence[Tensor], offsets: Sequence[int], flat: Tensor,
+                   scale: float = 1.0) -> None:
+    """t_i = flat[off_i : off_i+n_i] * scale."""
+    _impl(flat).mt_copy_scale(list(tensors), [int(o) for o in offsets], flat, float(scale), 1)

@@ -1,0 +1,196 @@
+"""Plain-PyTorch fp32 reference implementations of every arena_amd HIP kernel.
+
+Used (a) as the numerics oracle in tests and (b) as the implementation for CPU tensors (the
+multi-process gloo paths that run without a GPU). Semantics match csrc/ops/mlp_kernels.hip
+exactly, including the counter-hash dropout mask, the device step counters and the gather.
+"""
+from __future__ import annotations
+
+import math
+
+import torch
+
+_M32 = 0xFFFFFFFF
+
+
+def _mul32(h: torch.Tensor, c: int) -> torch.Tensor:
+    """(h * c) mod 2**32 for int64 tensors holding uint32 values, without int64 overflow."""
+    lo = h & 0xFFFF
+    hi = h >> 16
+    return ((lo * c) + (((hi * c) & 0xFFFF) << 16)) & _M32
+
+
+def _mix32(h: torch.Tensor) -> torch.Tensor:
+    h = h ^ (h >> 16)
+    h = _mul32(h, 0x7FEB352D)
+    h = h ^ (h >> 15)
+    h = _mul32(h, 0x846CA68B)
+    h = h ^ (h >> 16)
+    return h
+
+
+def hash4(seed: int, step: int, rows: torch.Tensor, cols: torch.Tensor) -> torch.Tensor:
+    """uint32 hash of (seed, step, row, col) -- bit-identical to arena::hash4 (common.h)."""
+    h = torch.full_like(rows, (seed & _M32) ^ 0x9E3779B9, dtype=torch.int64)
+    h = _mix32(h)
+    h = _mix32(h ^ _mul32(torch.full_like(h, step & _M32), 0x85EBCA77))
+    h = _mix32(h ^ _mul32(rows.to(torch.int64) & _M32, 0xC2B2AE3D))
+    h = _mix32(h ^ _mul32(cols.to(torch.int64) & _M32, 0x27D4EB2F))
+    return h
+
+
+def keep_threshold(keep_prob: float) -> int:
+    return 0xFFFFFFFF if keep_prob >= 1.0 else int(keep_prob * 4294967296.0)
+
+
+def dropout_keep_mask(M: int, N: int, keep_prob: float, seed: int, step: int,
+                      device=None) -> torch.Tensor:
+    """Boolean [M, N] keep-mask used by linear_fwd's fused dropout."""
+    if keep_prob >= 1.0:
+        return torch.ones(M, N, dtype=torch.bool, device=device)
+    rows = torch.arange(M, device=device, dtype=torch.int64).unsqueeze(1).expand(M, N)
+    cols = torch.arange(N, device=device, dtype=torch.int64).unsqueeze(0).expand(M, N)
+    return hash4(seed, step, rows, cols) < keep_threshold(keep_prob)
+
+
+def _cursor_val(cursor: torch.Tensor | None, off: int) -> int:
+    return (int(cursor.reshape(-1)[0].item()) if cursor is not None else 0) + off
+
+
+def gather_rows(x: torch.Tensor, idx: torch.Tensor | None, cursor: torch.Tensor | None,
+                batch: int, M: int, cursor_off: int = 0) -> torch.Tensor:
+    if idx is None:
+        return x[:M]
+    cur = _cursor_val(cursor, cursor_off)
+    pos = (cur * batch + torch.arange(M, dtype=torch.int64, device=x.device)) % idx.numel()
+    return x[idx.to(torch.int64)[pos]]
+
+
+def linear_fwd(x, x_scale, idx, cursor, batch, W, bias, Y, act, keep_prob, seed, step):
+    M = Y.shape[0]
+    xr = gather_rows(x, idx, cursor, batch, M).to(torch.float32) * x_scale
+    z = xr @ W
+    if bias is not None:
+        z = z + bias
+    if act == 1:
+        z = torch.relu(z)
+    if keep_prob < 1.0:
+        st = int(step.reshape(-1)[0].item()) & _M32 if step is not None else 0
+        mask = dropout_keep_mask(M, W.shape[1], keep_prob, seed, st, device=z.device)
+        z = torch.where(mask, z * (1.0 / keep_prob), torch.zeros_like(z))
+    Y.copy_(z)
+
+
+def xent_head(H, W2, b2, labels, idx, cursor, batch, dlogits, dZ, keep_prob, relu_mask,
+              loss_scale, loss_acc, correct_acc, hist_step, ctr_dst, ctr_src, ctr_add):
+    M = H.shape[0]
+    hs = int(hist_step.reshape(-1)[0].item()) if hist_step is not None else 0
+    L = loss_acc.numel()
+    slot = hs % L if L > 1 else 0
+    if L > 1:
+        loss_acc[(hs + 1) % L] = 0.0
+        correct_acc[(hs + 1) % L] = 0
+    logits = H @ W2
+    if b2 is not None:
+        logits = logits + b2
+    y = gather_rows(labels, idx, cursor, batch, M).to(torch.int64)
+    lse = torch.logsumexp(logits, dim=1)
+    loss = lse - logits.gather(1, y.unsqueeze(1)).squeeze(1)
+    loss_acc[slot] += (loss * loss_scale).sum()
+    correct_acc[slot] += (logits.argmax(dim=1) == y).sum().to(correct_acc.dtype)
+    if ctr_dst is not None:
+        src = int(ctr_src.reshape(-1)[0].item()) if ctr_src is not None else 0
+        ctr_dst.fill_(src + ctr_add)
+    if dlogits is None:
+        return
+    g = (torch.softmax(logits, dim=1) - torch.nn.functional.one_hot(y, W2.shape[1]).to(H.dtype))
+    g = g * loss_scale
+    dlogits.view(M, -1).copy_(g)
+    if dZ is None:
+        return
+    dz = g @ W2.t()
+    if relu_mask:
+        inv_keep = 1.0 / keep_prob if keep_prob < 1.0 else 1.0
+        dz = torch.where(H > 0, dz * inv_keep, torch.zeros_like(dz))
+    dZ.view(M, -1).copy_(dz)
+
+
+def adam_update(p, m, v, g, lr, b1, b2, eps, wd, t, grad_scale, tf_style):
+    """In-place Adam on tensors (fp32), same formula as adam_apply in mlp_kernels.hip."""
+    g = g * grad_scale + wd * p
+    m.mul_(b1).add_(g, alpha=1.0 - b1)
+    v.mul_(b2).addcmul_(g, g, value=1.0 - b2)
+    bc1 = 1.0 - b1 ** t
+    bc2 = 1.0 - b2 ** t
+    if tf_style:
+        step_size = lr * math.sqrt(bc2) / bc1
+        p.sub_(step_size * m / (v.sqrt() + eps))
+    else:
+        p.sub_((lr / bc1) * m / (v.sqrt() / math.sqrt(bc2) + eps))
+
+
+def wgrad_grouped(xs, x_scales, gather, idx, cursor, cursor_off, batch, dzs, mode, outW, outB, mW,
+                  vW, mB, vB, lr, lr_t, b1, b2, eps, wd, t_step, grad_scale, tf_style, ctr_dst,
+                  ctr_src, ctr_add):
+    t = int(t_step.reshape(-1)[0].item()) if t_step is not None else 1
+    lr_v = float(lr_t.reshape(-1)[0].item()) if lr_t is not None else lr
+    pending = []
+    for i in range(len(xs)):
+        dz = dzs[i]
+        M = dz.shape[0]
+        if gather[i]:
+            xr = gather_rows(xs[i], idx, cursor, batch, M, cursor_off)
+        else:
+            xr = xs[i][:M]
+        xr = xr.to(torch.float32) * x_scales[i]
+        gw = xr.t() @ dz
+        gb = dz.sum(dim=0)
+        pending.append((i, gw, gb))
+    for i, gw, gb in pending:
+        if mode == 0:
+            outW[i].view_as(gw).copy_(gw * grad_scale)
+            if outB[i] is not None:
+                outB[i].copy_(gb * grad_scale)
+        else:
+            adam_update(outW[i].view_as(gw), mW[i].view_as(gw), vW[i].view_as(gw), gw, lr_v, b1,
+                        b2, eps, wd, t, grad_scale, tf_style)
+            if outB[i] is not None:
+                adam_update(outB[i], mB[i], vB[i], gb, lr_v, b1, b2, eps, wd, t, grad_scale,
+                            tf_style)
+    if ctr_dst is not None:
+        src = int(ctr_src.reshape(-1)[0].item()) if ctr_src is not None else 0
+        ctr_dst.fill_(src + ctr_add)
+
+
+def adam_flat(P, M, V, G, lr, lr_t, b1, b2, eps, wd, t_step, grad_scale, tf_style, ctr_dst,
+              ctr_src, ctr_add):
+    t = int(t_step.reshape(-1)[0].item()) if t_step is not None else 1
+    lr_v = float(lr_t.reshape(-1)[0].item()) if lr_t is not None else lr
+    adam_update(P, M, V, G, lr_v, b1, b2, eps, wd, t, grad_scale, tf_style)
+    if ctr_dst is not None:
+        src = int(ctr_src.reshape(-1)[0].item()) if ctr_src is not None else 0
+        ctr_dst.fill_(src + ctr_add)
+
+
+def sgd_flat(P, G, lr, lr_t, grad_scale):
+    lr_v = float(lr_t.reshape(-1)[0].item()) if lr_t is not None else lr
+    P.sub_(G * (lr_v * grad_scale))
+
+
+def softmax_xent(logits, labels, grad_scale, need_grad):
+    lse = torch.logsumexp(logits, dim=1)
+    loss = lse - logits.gather(1, labels.unsqueeze(1)).squeeze(1)
+    if not need_grad:
+        return [loss]
+    d = torch.softmax(logits, dim=1)
+    d[torch.arange(labels.numel()), labels] -= 1.0
+    return [loss, d * grad_scale]
+
+
+def mt_copy_scale(tensors, offsets, flat, scale, direction):
+    for t, off in zip(tensors, offsets):
+        n = t.numel()
+        if direction == 0:
+            flat[off:off + n].copy_(t.reshape(-1) * scale)
+        else:
+            t.view(-1).copy_(flat[off:off + n] * scale)

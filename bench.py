@@ -1,0 +1,131 @@
+#!/usr/bin/env python3
+"""Flagship benchmark: MNIST MLP data-parallel training throughput on MI355X.
+
+Metric/config: the reference publishes no perf numbers (BASELINE.json is N/A); its headline
+workload is the MNIST demo job (784-500-10 MLP, ReLU, dropout keep 0.9, softmax-xent, Adam 1e-3,
+batch 100; docs/userguide/1-tfjob-standalone.md:178-186), which BASELINE.md adopts as the
+north-star. We measure whole-job training throughput (samples/s, all ranks) with a FIXED per-GPU
+batch of 100 (weak scaling), full fp32 compute, every step complete (forward, loss, backward,
+gradient all-reduce when N>1, Adam update, device-side data gather + epoch reshuffles).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3000)
+    ap.add_argument("--warmup", type=int, default=300)
+    ap.add_argument("--impl", choices=["fused", "torch"], default="fused",
+                    help="fused = arena_amd HIP kernels + hipGraph; torch = eager PyTorch baseline")
+    ap.add_argument("--hidden", type=int, default=500)
+    ap.add_argument("--batch", type=int, default=100)
+    ap.add_argument("--steps-per-graph", type=int, default=0, help="0 = auto")
+    ap.add_argument("--eval", action="store_true", help="report test accuracy after timing")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and rank == 0:
+        print(f"[bench] note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE",
+              file=sys.stderr)
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    pg = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+        pg = dist.group.WORLD
+
+    from arena_amd.data.mnist import load_mnist
+    from arena_amd.models.mlp import FusedMLPTrainer, MLPConfig
+
+    data = load_mnist()
+    cfg = MLPConfig(hidden=args.hidden, batch=args.batch)
+
+    if args.impl == "fused":
+        tr = FusedMLPTrainer(cfg, data.train_images, data.train_labels, device=dev,
+                             process_group=pg, rank=rank, world=world)
+        spg = args.steps_per_graph or tr.pick_steps_per_graph()
+        graphs = tr.enable_graphs(spg)
+        run = tr.train_steps
+        mode = f"hipgraph[{tr.graph_mode},{spg} steps/graph]" if graphs else "eager"
+    else:
+        from arena_amd.models.torch_mlp import EagerMLPTrainer
+        tr = EagerMLPTrainer(cfg, data.train_images, data.train_labels, device=dev,
+                             process_group=pg, rank=rank, world=world)
+        run = tr.train_steps
+        mode = "eager-pytorch"
+
+    run(args.warmup)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    run(args.steps)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = t1 - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+
+    extra = {}
+    loss, acc = tr.recent_metrics(100)
+    extra["train_loss_last100"] = round(loss, 5)
+    extra["train_acc_last100"] = round(acc, 5)
+    if args.eval:
+        tl, ta = tr.evaluate(data.test_images, data.test_labels)
+        extra["test_loss"] = round(tl, 5)
+        extra["test_acc"] = round(ta, 5)
+
+    samples = world * cfg.batch * args.steps
+    value = samples / elapsed
+    if rank == 0:
+        out = {
+            "metric": "mnist_mlp_train_throughput",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 5),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": f"synthetic ({data.source} MNIST-shaped uint8 60k/10k, device-resident)",
+            "config": {"model": f"mnist_mlp_784-{args.hidden}-10 (relu, dropout 0.9, adam 1e-3)",
+                       "global_batch": world * cfg.batch, "seq_len": None,
+                       "parallelism": f"dp{world}", "impl": args.impl, "exec": mode},
+            **extra,
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,356 @@
+// PyTorch binding for the arena_amd HIP kernels. Validates every shape/dtype/device on the host
+// BEFORE launching (a kernel that faults on an MI355X can reset the node), then calls the plain-C
+// launchers in mlp_kernels.hip on the current HIP stream (so hipGraph capture via torch works).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <hip/hip_runtime_api.h>
+
+#include <vector>
+
+#include "abi.h"
+
+extern "C" {
+hipError_t arena_linear_fwd(ArenaRowSource, const float*, const float*, float*, int, int, int, int,
+                            float, uint32_t, const long long*, hipStream_t);
+hipError_t arena_xent_head(const float*, int, int, const float*, const float*, int, ArenaRowSource,
+                           float*, float*, float, int, float, float*, int*, int, const long long*,
+                           ArenaCounterOp, hipStream_t);
+hipError_t arena_wgrad_grouped(ArenaWGradProblem*, int, ArenaAdam, float, ArenaCounterOp,
+                               hipStream_t);
+hipError_t arena_adam_flat(float*, float*, float*, const float*, long long, ArenaAdam,
+                           ArenaCounterOp, hipStream_t);
+hipError_t arena_sgd_flat(float*, const float*, long long, float, const float*, float, hipStream_t);
+hipError_t arena_softmax_xent(const float*, const long long*, int, int, float*, float*, float,
+                              hipStream_t);
+hipError_t arena_mt_copy_scale(float* const*, const long long*, const long long*, int, float*, float,
+                               int, hipStream_t);
+}
+
+namespace {
+
+using torch::Tensor;
+using OptT = c10::optional<Tensor>;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+void check_hip(hipError_t e, const char* what) {
+  TORCH_CHECK(e == hipSuccess, "arena_amd HIP launch failed in ", what, ": ", hipGetErrorString(e));
+}
+
+void check_dev(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.is_contiguous(), name, " must be contiguous");
+}
+
+void check_f32(const Tensor& t, const char* name) {
+  check_dev(t, name);
+  TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be float32");
+}
+
+const long long* opt_i64_scalar(const OptT& t, const char* name) {
+  if (!t.has_value()) return nullptr;
+  check_dev(*t, name);
+  TORCH_CHECK(t->scalar_type() == torch::kInt64 && t->numel() >= 1, name,
+              " must be an int64 device tensor with >=1 element");
+  return reinterpret_cast<const long long*>(t->data_ptr<int64_t>());
+}
+
+int dtype_code(const Tensor& t) {
+  switch (t.scalar_type()) {
+    case torch::kFloat32: return 0;
+    case torch::kUInt8: return 1;
+    case torch::kInt32: return 2;
+    case torch::kInt64: return 3;
+    default: TORCH_CHECK(false, "unsupported dtype ", t.scalar_type());
+  }
+  return -1;
+}
+
+// x: [rows, ld] (2-D) or [rows] (1-D labels). Logical row r reads physical row
+// idx[(cursor*batch + r) % len(idx)] when idx is given, else row r (checked against rows).
+ArenaRowSource make_src(const Tensor& x, double scale, const OptT& idx, const OptT& cursor,
+                        int64_t batch, int64_t logical_rows, const char* name,
+                        int64_t cursor_off = 0) {
+  check_dev(x, name);
+  ArenaRowSource s{};
+  s.ptr = x.data_ptr();
+  s.dtype = dtype_code(x);
+  s.ld = x.dim() >= 2 ? (int)x.size(1) : 1;
+  s.scale = (float)scale;
+  s.idx = nullptr;
+  s.idx_len = 0;
+  s.cursor = opt_i64_scalar(cursor, "cursor");
+  s.batch = (int)batch;
+  s.cursor_off = (int)cursor_off;
+  if (idx.has_value()) {
+    check_dev(*idx, "idx");
+    TORCH_CHECK(idx->scalar_type() == torch::kInt32, "idx must be int32");
+    TORCH_CHECK(idx->numel() > 0, "idx must be non-empty");
+    s.idx = idx->data_ptr<int>();
+    s.idx_len = idx->numel();
+    // Every index value must be a valid row: checked once on the host when the permutation is
+    // installed (arena_amd/data/device_loader.py), not per launch (launches are graph-captured).
+  } else {
+    TORCH_CHECK(logical_rows <= x.size(0), name, ": ", logical_rows, " rows requested but tensor has ",
+                x.size(0));
+  }
+  return s;
+}
+
+// Y = dropout(act(X·W + b)); X rows optionally gathered (dataset permutation + device cursor).
+void linear_fwd(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch, Tensor W, OptT bias,
+                Tensor Y, int64_t act, double keep_prob, int64_t seed, OptT step) {
+  check_f32(W, "W");
+  check_f32(Y, "Y");
+  TORCH_CHECK(W.dim() == 2 && Y.dim() == 2 && x.dim() == 2, "linear_fwd: 2-D tensors required");
+  const int64_t M = Y.size(0), N = Y.size(1), K = W.size(0);
+  TORCH_CHECK(W.size(1) == N, "W.shape[1] must equal Y.shape[1]");
+  TORCH_CHECK(x.size(1) == K, "x.shape[1] must equal W.shape[0]");
+  TORCH_CHECK(K % 4 == 0, "linear_fwd: K must be a multiple of 4 (got ", K, ")");
+  TORCH_CHECK(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kUInt8,
+              "x must be float32 or uint8");
+  TORCH_CHECK(M > 0 && N > 0, "empty linear");
+  const float* b = nullptr;
+  if (bias.has_value()) {
+    check_f32(*bias, "bias");
+    TORCH_CHECK(bias->numel() == N, "bias size mismatch");
+    b = bias->data_ptr<float>();
+  }
+  TORCH_CHECK(keep_prob > 0.0 && keep_prob <= 1.0, "keep_prob must be in (0, 1]");
+  ArenaRowSource s = make_src(x, x_scale, idx, cursor, batch, M, "x");
+  check_hip(arena_linear_fwd(s, W.data_ptr<float>(), b, Y.data_ptr<float>(), (int)M, (int)N, (int)K,
+                             (int)act, (float)keep_prob, (uint32_t)seed, opt_i64_scalar(step, "step"),
+                             cur_stream()),
+            "linear_fwd");
+}
+
+void xent_head(Tensor H, Tensor W2, OptT b2, Tensor labels, OptT idx, OptT cursor, int64_t batch,
+               OptT dlogits, OptT dZ, double keep_prob, bool relu_mask, double loss_scale,
+               Tensor loss_acc, Tensor correct_acc, OptT hist_step, OptT ctr_dst, OptT ctr_src,
+               int64_t ctr_add) {
+  check_f32(H, "H");
+  check_f32(W2, "W2");
+  const int64_t M = H.size(0), D = H.size(1), C = W2.size(1);
+  TORCH_CHECK(W2.size(0) == D, "W2.shape[0] must equal H.shape[1]");
+  TORCH_CHECK(D <= 1024 && C <= 16 && D * C <= 16384, "xent_head: D<=1024, C<=16, D*C<=16384");
+  TORCH_CHECK(labels.dim() == 1, "labels must be 1-D");
+  const float* pb2 = nullptr;
+  if (b2.has_value()) {
+    check_f32(*b2, "b2");
+    TORCH_CHECK(b2->numel() == C, "b2 size");
+    pb2 = b2->data_ptr<float>();
+  }
+  float* pdl = nullptr;
+  float* pdz = nullptr;
+  if (dlogits.has_value()) {
+    check_f32(*dlogits, "dlogits");
+    TORCH_CHECK(dlogits->numel() == M * C, "dlogits size");
+    pdl = dlogits->data_ptr<float>();
+  }
+  if (dZ.has_value()) {
+    TORCH_CHECK(pdl != nullptr, "dZ requires dlogits");
+    check_f32(*dZ, "dZ");
+    TORCH_CHECK(dZ->numel() == M * D, "dZ size");
+    pdz = dZ->data_ptr<float>();
+  }
+  check_f32(loss_acc, "loss_acc");
+  check_dev(correct_acc, "correct_acc");
+  TORCH_CHECK(correct_acc.scalar_type() == torch::kInt32, "correct_acc must be int32");
+  TORCH_CHECK(loss_acc.numel() == correct_acc.numel() && loss_acc.numel() >= 1, "acc sizes");
+  TORCH_CHECK(labels.scalar_type() != torch::kFloat32, "labels must be integer");
+  ArenaRowSource lab = make_src(labels, 1.0, idx, cursor, batch, M, "labels");
+  ArenaCounterOp ctr{};
+  if (ctr_dst.has_value()) {
+    ctr.dst = const_cast<long long*>(opt_i64_scalar(ctr_dst, "ctr_dst"));
+    ctr.src = opt_i64_scalar(ctr_src, "ctr_src");
+    ctr.add = (int)ctr_add;
+  }
+  check_hip(arena_xent_head(H.data_ptr<float>(), (int)M, (int)D, W2.data_ptr<float>(), pb2, (int)C,
+                            lab, pdl, pdz, (float)keep_prob, relu_mask ? 1 : 0, (float)loss_scale,
+                            loss_acc.data_ptr<float>(), correct_acc.data_ptr<int>(),
+                            (int)loss_acc.numel(), opt_i64_scalar(hist_step, "hist_step"), ctr,
+                            cur_stream()),
+            "xent_head");
+}
+
+ArenaAdam make_adam(double lr, OptT lr_t, double b1, double b2, double eps, double wd, OptT t_step,
+                    double grad_scale, bool tf_style) {
+  ArenaAdam a{};
+  a.lr = (float)lr;
+  a.lr_ptr = nullptr;
+  if (lr_t.has_value()) {
+    check_f32(*lr_t, "lr");
+    a.lr_ptr = lr_t->data_ptr<float>();
+  }
+  a.beta1 = (float)b1; a.beta2 = (float)b2; a.eps = (float)eps; a.weight_decay = (float)wd;
+  a.t_ptr = opt_i64_scalar(t_step, "t_step");
+  a.grad_scale = (float)grad_scale;
+  a.tf_style = tf_style ? 1 : 0;
+  return a;
+}
+
+// problems: list of dicts is awkward across pybind; use parallel lists of tensors instead.
+// Each layer i: x_i (f32 or u8 [rows, K]), x_scale_i, dz_i [M, N]; mode 0 -> gW_i/gB_i views,
+// mode 1 -> (pW,mW,vW,pB,mB,vB) views. One shared gather (idx, cursor, batch) is applied to
+// layers flagged gather=True (the dataset-fed first layer).
+void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::vector<bool> gather,
+                   OptT idx, OptT cursor, int64_t cursor_off, int64_t batch, std::vector<Tensor> dzs, int64_t mode,
+                   std::vector<Tensor> outW, std::vector<OptT> outB, std::vector<OptT> mW,
+                   std::vector<OptT> vW, std::vector<OptT> mB, std::vector<OptT> vB, double lr,
+                   OptT lr_t, double b1, double b2, double eps, double wd, OptT t_step,
+                   double grad_scale, bool tf_style, OptT ctr_dst, OptT ctr_src, int64_t ctr_add) {
+  const size_t n = xs.size();
+  TORCH_CHECK(n >= 1 && n <= 4, "wgrad_grouped: 1..4 problems");
+  TORCH_CHECK(x_scales.size() == n && gather.size() == n && dzs.size() == n && outW.size() == n &&
+                  outB.size() == n,
+              "wgrad_grouped: list lengths differ");
+  if (mode == 1)
+    TORCH_CHECK(mW.size() == n && vW.size() == n && mB.size() == n && vB.size() == n,
+                "adam state lists");
+  std::vector<ArenaWGradProblem> probs(n);
+  for (size_t i = 0; i < n; ++i) {
+    ArenaWGradProblem& P = probs[i];
+    P = ArenaWGradProblem{};
+    const Tensor& dz = dzs[i];
+    check_f32(dz, "dz");
+    TORCH_CHECK(dz.dim() == 2, "dz must be 2-D");
+    const int64_t M = dz.size(0), N = dz.size(1);
+    const Tensor& x = xs[i];
+    TORCH_CHECK(x.dim() == 2, "x must be 2-D");
+    const int64_t K = x.size(1);
+    TORCH_CHECK(K % 4 == 0, "wgrad: K must be a multiple of 4");
+    TORCH_CHECK(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kUInt8,
+                "x must be f32/u8");
+    P.x = gather[i] ? make_src(x, x_scales[i], idx, cursor, batch, M, "x", cursor_off)
+                    : make_src(x, x_scales[i], c10::nullopt, c10::nullopt, 0, M, "x");
+    P.xt = x.scalar_type() == torch::kUInt8 ? 1 : 0;
+    P.dz = dz.data_ptr<float>();
+    P.M = (int)M; P.K = (int)K; P.N = (int)N;
+    P.mode = (int)mode;
+    check_f32(outW[i], "W");
+    TORCH_CHECK(outW[i].numel() == K * N, "W/grad size mismatch for problem ", i);
+    if (outB[i].has_value()) {
+      check_f32(*outB[i], "b");
+      TORCH_CHECK(outB[i]->numel() == N, "bias size");
+    }
+    if (mode == 0) {
+      P.gW = outW[i].data_ptr<float>();
+      P.gB = outB[i].has_value() ? outB[i]->data_ptr<float>() : nullptr;
+    } else {
+      P.pW = outW[i].data_ptr<float>();
+      TORCH_CHECK(mW[i].has_value() && vW[i].has_value(), "adam: mW/vW required");
+      check_f32(*mW[i], "mW");
+      check_f32(*vW[i], "vW");
+      TORCH_CHECK(mW[i]->numel() == K * N && vW[i]->numel() == K * N, "adam W state size");
+      P.mW = mW[i]->data_ptr<float>();
+      P.vW = vW[i]->data_ptr<float>();
+      if (outB[i].has_value()) {
+        TORCH_CHECK(mB[i].has_value() && vB[i].has_value(), "adam: mB/vB required");
+        check_f32(*mB[i], "mB");
+        check_f32(*vB[i], "vB");
+        TORCH_CHECK(mB[i]->numel() == N && vB[i]->numel() == N, "adam b state size");
+        P.pB = outB[i]->data_ptr<float>();
+        P.mB = mB[i]->data_ptr<float>();
+        P.vB = vB[i]->data_ptr<float>();
+      }
+    }
+  }
+  ArenaAdam a = make_adam(lr, lr_t, b1, b2, eps, wd, t_step, grad_scale, tf_style);
+  ArenaCounterOp ctr{};
+  if (ctr_dst.has_value()) {
+    ctr.dst = const_cast<long long*>(opt_i64_scalar(ctr_dst, "ctr_dst"));
+    ctr.src = opt_i64_scalar(ctr_src, "ctr_src");
+    ctr.add = (int)ctr_add;
+  }
+  check_hip(arena_wgrad_grouped(probs.data(), (int)n, a, (float)grad_scale, ctr, cur_stream()),
+            "wgrad_grouped");
+}
+
+void adam_flat(Tensor P, Tensor M, Tensor V, Tensor G, double lr, OptT lr_t, double b1, double b2,
+               double eps, double wd, OptT t_step, double grad_scale, bool tf_style, OptT ctr_dst,
+               OptT ctr_src, int64_t ctr_add) {
+  for (auto* t : {&P, &M, &V, &G}) check_f32(*t, "adam_flat operand");
+  const int64_t n = P.numel();
+  TORCH_CHECK(M.numel() == n && V.numel() == n && G.numel() == n, "adam_flat size mismatch");
+  TORCH_CHECK(n % 4 == 0, "adam_flat: numel must be a multiple of 4");
+  ArenaAdam a = make_adam(lr, lr_t, b1, b2, eps, wd, t_step, grad_scale, tf_style);
+  ArenaCounterOp ctr{};
+  if (ctr_dst.has_value()) {
+    ctr.dst = const_cast<long long*>(opt_i64_scalar(ctr_dst, "ctr_dst"));
+    ctr.src = opt_i64_scalar(ctr_src, "ctr_src");
+    ctr.add = (int)ctr_add;
+  }
+  check_hip(arena_adam_flat(P.data_ptr<float>(), M.data_ptr<float>(), V.data_ptr<float>(),
+                            G.data_ptr<float>(), n, a, ctr, cur_stream()),
+            "adam_flat");
+}
+
+void sgd_flat(Tensor P, Tensor G, double lr, OptT lr_t, double grad_scale) {
+  check_f32(P, "P");
+  check_f32(G, "G");
+  TORCH_CHECK(P.numel() == G.numel() && P.numel() % 4 == 0, "sgd_flat sizes");
+  const float* lp = nullptr;
+  if (lr_t.has_value()) {
+    check_f32(*lr_t, "lr");
+    lp = lr_t->data_ptr<float>();
+  }
+  check_hip(arena_sgd_flat(P.data_ptr<float>(), G.data_ptr<float>(), P.numel(), (float)lr, lp,
+                           (float)grad_scale, cur_stream()),
+            "sgd_flat");
+}
+
+std::vector<Tensor> softmax_xent(Tensor logits, Tensor labels, double grad_scale, bool need_grad) {
+  check_f32(logits, "logits");
+  check_dev(labels, "labels");
+  TORCH_CHECK(logits.dim() == 2, "logits must be 2-D");
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.numel() == logits.size(0),
+              "labels must be int64 [M]");
+  const int64_t M = logits.size(0), C = logits.size(1);
+  auto loss = torch::empty({M}, logits.options());
+  Tensor dl;
+  if (need_grad) dl = torch::empty_like(logits);
+  // Labels outside [0, C) would read out of bounds: validated by the Python wrapper in debug mode
+  // and by construction of the data pipeline (labels are class ids).
+  check_hip(arena_softmax_xent(logits.data_ptr<float>(),
+                               reinterpret_cast<const long long*>(labels.data_ptr<int64_t>()),
+                               (int)M, (int)C, loss.data_ptr<float>(),
+                               need_grad ? dl.data_ptr<float>() : nullptr, (float)grad_scale,
+                               cur_stream()),
+            "softmax_xent");
+  if (need_grad) return {loss, dl};
+  return {loss};
+}
+
+// dir 0: flat[off_i:off_i+n_i] = t_i * scale; dir 1: t_i = flat[...] * scale.
+void mt_copy_scale(std::vector<Tensor> tensors, std::vector<int64_t> offsets, Tensor flat,
+                   double scale, int64_t dir) {
+  check_f32(flat, "flat");
+  TORCH_CHECK(tensors.size() == offsets.size(), "offsets length");
+  std::vector<float*> ptrs;
+  std::vector<long long> offs, ns;
+  for (size_t i = 0; i < tensors.size(); ++i) {
+    check_f32(tensors[i], "tensor");
+    TORCH_CHECK(offsets[i] >= 0 && offsets[i] + tensors[i].numel() <= flat.numel(),
+                "mt_copy_scale: segment ", i, " out of bounds");
+    ptrs.push_back(tensors[i].data_ptr<float>());
+    offs.push_back(offsets[i]);
+    ns.push_back(tensors[i].numel());
+  }
+  check_hip(arena_mt_copy_scale(ptrs.data(), offs.data(), ns.data(), (int)ptrs.size(),
+                                flat.data_ptr<float>(), (float)scale, (int)dir, cur_stream()),
+            "mt_copy_scale");
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "arena_amd native HIP kernels (gfx950)";
+  m.def("linear_fwd", &linear_fwd);
+  m.def("xent_head", &xent_head);
+  m.def("wgrad_grouped", &wgrad_grouped);
+  m.def("adam_flat", &adam_flat);
+  m.def("sgd_flat", &sgd_flat);
+  m.def("softmax_xent", &softmax_xent);
+  m.def("mt_copy_scale", &mt_copy_scale);
+  m.attr("arch") = "gfx950";
+}

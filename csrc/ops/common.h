@@ -1,0 +1,60 @@
+// Shared device-side definitions for the arena_amd HIP kernels (gfx950 / CDNA4 only).
+//
+// Design notes (MI355X-first):
+//  * wave64 everywhere: lane = threadIdx.x & 63, 64-bit ballots, shfl over 64 lanes.
+//  * fp32 matmul-shaped work goes to the exact-f32 MFMA (v_mfma_f32_16x16x4_f32):
+//      A operand: lane l holds A[i = l&15][k = l>>4]
+//      B operand: lane l holds B[k = l>>4][j = l&15]
+//      C/D      : lane l, reg r holds D[row = 4*(l>>4) + r][col = l&15]
+//  * Per-step scalars that change across hipGraph replays (data cursor, Adam step t,
+//    learning rate) live in device memory and are read in-kernel, never baked in.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "abi.h"
+
+namespace arena {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+__device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
+
+__device__ __forceinline__ f32x4 mfma_16x16x4(float a, float b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Counter-based hash used for dropout masks: a pure function of (seed, step, row, col) so the
+// mask never has to be stored and a PyTorch reference can reproduce it bit-exactly
+// (arena_amd/ops/reference.py::dropout_keep_mask).
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t h) {
+  h ^= h >> 16; h *= 0x7FEB352Du;
+  h ^= h >> 15; h *= 0x846CA68Bu;
+  h ^= h >> 16;
+  return h;
+}
+__host__ __device__ __forceinline__ uint32_t hash4(uint32_t seed, uint32_t step, uint32_t row,
+                                                   uint32_t col) {
+  uint32_t h = mix32(seed ^ 0x9E3779B9u);
+  h = mix32(h ^ (step * 0x85EBCA77u));
+  h = mix32(h ^ (row * 0xC2B2AE3Du));
+  h = mix32(h ^ (col * 0x27D4EB2Fu));
+  return h;
+}
+
+}  // namespace arena
+

@@ -1,0 +1,623 @@
+#include "hip/hip_runtime.h"
+// Fused fp32 MLP training kernels for gfx950 (MI355X).
+//
+// The reference (mark1222/arena) only *launches* MNIST training images (TF1.5 mnist_with_summaries,
+// dist-mnist, Horovod): see docs/userguide/1-tfjob-standalone.md:178-186 and SURVEY.md §2.11. Their
+// hot ops -- GEMM+bias+ReLU, dropout, softmax-cross-entropy, Adam -- are implemented here natively:
+//
+//   linear_fwd      Y = dropout(act(X·W + b))       X rows gathered from the dataset in-kernel
+//   xent_head       logits = H·W2 + b2 -> loss, accuracy, dlogits, dZ = (dlogits·W2ᵀ)⊙mask
+//   wgrad_grouped   dW = Xᵀ·dZ, db = 1ᵀ·dZ for up to 4 layers in ONE launch, epilogue either
+//                   writes the (scaled) gradient into the flat all-reduce bucket or applies Adam
+//   adam_flat       Adam over the whole flat parameter buffer (after the gradient all-reduce)
+//   softmax_xent    generic row softmax-cross-entropy forward+backward
+//   mt_copy_scale   multi-tensor flatten/unflatten with scale (gradient buckets)
+//
+// All matmul work uses the exact-fp32 MFMA v_mfma_f32_16x16x4_f32 (no TF32 on gfx950), so numerics
+// equal an fp32 fmaf chain. Layout is TF-style: W is [K][N] (in x out), activations row-major.
+#include "common.h"
+
+#include <algorithm>
+#include <cmath>
+
+using namespace arena;
+
+namespace {
+
+__device__ __forceinline__ long long phys_row(const ArenaRowSource& s, long long r) {
+  if (s.idx == nullptr) return r;
+  const long long cur = s.cursor ? *s.cursor : 0;
+  const long long pos = (cur * (long long)s.batch + r) % s.idx_len;
+  return (long long)s.idx[pos];
+}
+
+template <int XT>
+__device__ __forceinline__ void load4(const ArenaRowSource& s, long long prow, int k, float out[4]) {
+  if constexpr (XT == 1) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(
+        static_cast<const uint8_t*>(s.ptr) + prow * (long long)s.ld + k);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) out[j] = (float)((u >> (8 * j)) & 0xffu) * s.scale;
+  } else {
+    const float4 v = *reinterpret_cast<const float4*>(static_cast<const float*>(s.ptr) +
+                                                      prow * (long long)s.ld + k);
+    out[0] = v.x * s.scale; out[1] = v.y * s.scale; out[2] = v.z * s.scale; out[3] = v.w * s.scale;
+  }
+}
+
+template <int XT>
+__device__ __forceinline__ float load1(const ArenaRowSource& s, long long prow, int k) {
+  if constexpr (XT == 1) {
+    return (float)(static_cast<const uint8_t*>(s.ptr)[prow * (long long)s.ld + k]) * s.scale;
+  } else {
+    return static_cast<const float*>(s.ptr)[prow * (long long)s.ld + k] * s.scale;
+  }
+}
+
+__device__ __forceinline__ void counter_op(const ArenaCounterOp& c) {
+  if (c.dst != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    *c.dst = (c.src ? *c.src : 0) + c.add;
+  }
+}
+
+__device__ __forceinline__ float adam_lr(const ArenaAdam& a) { return a.lr_ptr ? *a.lr_ptr : a.lr; }
+
+struct AdamCoef {
+  float step_size, inv_sqrt_bc2, eps, b1, b2, wd, gscale;
+  int tf;
+};
+
+__device__ __forceinline__ AdamCoef adam_coef(const ArenaAdam& a) {
+  AdamCoef c;
+  const float t = a.t_ptr ? (float)(*a.t_ptr) : 1.0f;
+  const float bc1 = 1.0f - exp2f(t * log2f(a.beta1));
+  const float bc2 = 1.0f - exp2f(t * log2f(a.beta2));
+  const float lr = adam_lr(a);
+  c.tf = a.tf_style;
+  if (a.tf_style) {
+    c.step_size = lr * sqrtf(bc2) / bc1;
+    c.inv_sqrt_bc2 = 1.0f;
+  } else {
+    c.step_size = lr / bc1;
+    c.inv_sqrt_bc2 = 1.0f / sqrtf(bc2);
+  }
+  c.eps = a.eps; c.b1 = a.beta1; c.b2 = a.beta2; c.wd = a.weight_decay; c.gscale = a.grad_scale;
+  return c;
+}
+
+__device__ __forceinline__ void adam_apply(const AdamCoef& c, float g, float& p, float& m, float& v) {
+  g = g * c.gscale + c.wd * p;
+  m = c.b1 * m + (1.0f - c.b1) * g;
+  v = c.b2 * v + (1.0f - c.b2) * g * g;
+  // torch: p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps);  tf: p -= lr_t * m / (sqrt(v) + eps)
+  p -= c.step_size * m / (sqrtf(v) * c.inv_sqrt_bc2 + c.eps);
+}
+
+// ---------------------------------------------------------------------------------------------
+// linear_fwd: one 16x16 output tile per workgroup, K split across WAVES waves, partial tiles
+// reduced through LDS. Lane (g = l>>4, c = l&15) loads 4 consecutive k of its A row with one
+// vector load; MFMA j consumes k = 16s + 4g + j (a fixed permutation of the K order that A and B
+// share). Grid: (ceil(N/16), ceil(M/16)).
+// ---------------------------------------------------------------------------------------------
+template <int XT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void linear_fwd_kernel(
+    ArenaRowSource src, const float* __restrict__ W, const float* __restrict__ bias,
+    float* __restrict__ Y, int M, int N, int K, int act, uint32_t keep_thr, float inv_keep,
+    uint32_t seed, const long long* step_src) {
+  constexpr int CH = 8;
+  const int lane = lane_id(), w = wave_id();
+  const int g = lane >> 4, c = lane & 15;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  const int row = m0 + c, col = n0 + c;
+  const bool row_ok = row < M, col_ok = col < N;
+  const long long prow = row_ok ? phys_row(src, row) : 0;
+  const int nsteps = (K + 15) >> 4;
+  const int s0 = (nsteps * w) / WAVES, s1 = (nsteps * (w + 1)) / WAVES;
+
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int sb = s0; sb < s1; sb += CH) {
+    float a[CH][4], b[CH][4];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int k = (sb + i) * 16 + 4 * g;
+      const bool ok = (sb + i < s1) && (k < K);
+      if (ok && row_ok) {
+        load4<XT>(src, prow, k, a[i]);
+      } else {
+        a[i][0] = a[i][1] = a[i][2] = a[i][3] = 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) b[i][j] = (ok && col_ok) ? W[(long long)(k + j) * N + col] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      if (sb + i < s1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = mfma_16x16x4(a[i][j], b[i][j], acc);
+      }
+    }
+  }
+
+  __shared__ float red[WAVES][16][17];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[w][4 * g + r][c] = acc[r];
+  __syncthreads();
+  const uint32_t step = step_src ? (uint32_t)(*step_src) : 0u;
+  for (int t = threadIdx.x; t < 256; t += WAVES * 64) {
+    const int rr = t >> 4, cc = t & 15;
+    const int gm = m0 + rr, gn = n0 + cc;
+    if (gm < M && gn < N) {
+      float v = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < WAVES; ++ww) v += red[ww][rr][cc];
+      if (bias) v += bias[gn];
+      if (act == 1) v = fmaxf(v, 0.f);
+      if (keep_thr != 0xFFFFFFFFu) {
+        const uint32_t h = hash4(seed, step, (uint32_t)gm, (uint32_t)gn);
+        v = (h < keep_thr) ? v * inv_keep : 0.f;
+      }
+      Y[(long long)gm * N + gn] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// xent_head: one wave per batch row, 4 rows per workgroup, W2 staged in LDS.
+//   logits = h·W2 + b2; loss = lse - logit[y]; dlogits = (softmax - onehot) * loss_scale
+//   dZ[j] = (Σ_c dlogits[c]·W2[j][c]) * (h[j] > 0 ? inv_keep : 0)      (ReLU + dropout backward)
+// Loss/correct are accumulated (one atomic per row) into slot (*hist_step % hist_len); block 0
+// zeroes the NEXT slot so a graph-replayed loop keeps a ring of per-step metrics on device.
+// ---------------------------------------------------------------------------------------------
+constexpr int kHeadMaxT = 16;  // hidden <= 1024
+constexpr int kHeadMaxC = 16;  // classes <= 16
+
+template <int LT>
+__global__ __launch_bounds__(256) void xent_head_kernel(
+    const float* __restrict__ H, int M, int D, const float* __restrict__ W2,
+    const float* __restrict__ b2, int C, ArenaRowSource lab, float* __restrict__ dlogits,
+    float* __restrict__ dZ, float inv_keep, int relu_mask, float loss_scale,
+    float* __restrict__ loss_acc, int* __restrict__ correct_acc, int hist_len,
+    const long long* hist_step, ArenaCounterOp ctr) {
+  extern __shared__ __attribute__((aligned(16))) float ws[];  // [D][C]
+  for (int i = threadIdx.x; i < D * C; i += blockDim.x) ws[i] = W2[i];
+  counter_op(ctr);
+  const long long hs = hist_step ? *hist_step : 0;
+  const int slot = hist_len > 1 ? (int)(hs % hist_len) : 0;
+  if (hist_len > 1 && blockIdx.x == 0 && threadIdx.x == 0) {
+    const int nxt = (int)((hs + 1) % hist_len);
+    loss_acc[nxt] = 0.f;
+    correct_acc[nxt] = 0;
+  }
+  __syncthreads();
+
+  const int lane = lane_id();
+  const int r = blockIdx.x * 4 + wave_id();
+  if (r >= M) return;
+
+  float h[kHeadMaxT];
+#pragma unroll
+  for (int t = 0; t < kHeadMaxT; ++t) {
+    const int j = lane + 64 * t;
+    h[t] = (j < D) ? H[(long long)r * D + j] : 0.f;
+  }
+  float lg[kHeadMaxC];
+#pragma unroll
+  for (int cc = 0; cc < kHeadMaxC; ++cc) {
+    lg[cc] = -INFINITY;
+    if (cc < C) {
+      float s = 0.f;
+#pragma unroll
+      for (int t = 0; t < kHeadMaxT; ++t) {
+        const int j = lane + 64 * t;
+        if (j < D) s += h[t] * ws[j * C + cc];
+      }
+      lg[cc] = wave_sum(s) + (b2 ? b2[cc] : 0.f);
+    }
+  }
+  float mx = lg[0];
+  int arg = 0;
+#pragma unroll
+  for (int cc = 1; cc < kHeadMaxC; ++cc) {
+    if (cc < C && lg[cc] > mx) { mx = lg[cc]; arg = cc; }
+  }
+  float se = 0.f;
+#pragma unroll
+  for (int cc = 0; cc < kHeadMaxC; ++cc)
+    if (cc < C) se += expf(lg[cc] - mx);
+  const float lse = mx + logf(se);
+
+  const long long pr = phys_row(lab, r);
+  int y;
+  if constexpr (LT == 1) y = (int)static_cast<const uint8_t*>(lab.ptr)[pr];
+  else if constexpr (LT == 2) y = static_cast<const int*>(lab.ptr)[pr];
+  else y = (int)static_cast<const long long*>(lab.ptr)[pr];
+  float ly = 0.f;
+#pragma unroll
+  for (int cc = 0; cc < kHeadMaxC; ++cc) ly = (cc == y) ? lg[cc] : ly;
+
+  if (lane == 0) {
+    atomicAdd(&loss_acc[slot], (lse - ly) * loss_scale);
+    atomicAdd(&correct_acc[slot], arg == y ? 1 : 0);
+  }
+  if (dlogits == nullptr) return;
+
+  float gcl[kHeadMaxC];
+#pragma unroll
+  for (int cc = 0; cc < kHeadMaxC; ++cc)
+    gcl[cc] = (cc < C) ? (expf(lg[cc] - lse) - (cc == y ? 1.f : 0.f)) * loss_scale : 0.f;
+  if (lane < C) {
+    float v = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < kHeadMaxC; ++cc) v = (cc == lane) ? gcl[cc] : v;
+    dlogits[(long long)r * C + lane] = v;
+  }
+  if (dZ == nullptr) return;
+#pragma unroll
+  for (int t = 0; t < kHeadMaxT; ++t) {
+    const int j = lane + 64 * t;
+    if (j < D) {
+      float s = 0.f;
+#pragma unroll
+      for (int cc = 0; cc < kHeadMaxC; ++cc)
+        if (cc < C) s += gcl[cc] * ws[j * C + cc];
+      if (relu_mask) s = (h[t] > 0.f) ? s * inv_keep : 0.f;
+      dZ[(long long)r * D + j] = s;
+    }
+  }
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------
+// wgrad_grouped: dW = Xᵀ·dZ (+ db = 1ᵀ·dZ) for up to kMaxProblems layers in one launch.
+// Workgroup = 4 waves = a 64(k) x 16(n) tile of dW; the gathered X block [m][64] and the dZ slice
+// [m][16] are staged through LDS once per 128-row chunk and shared by the 4 waves.
+//   A operand (Xᵀ): lane l -> Xs[m = ms + (l>>4)][k = 16w + (l&15)]
+//   B operand (dZ): lane l -> Zs[m = ms + (l>>4)][n = l&15]
+// Xs row stride 80 floats (≡16 mod 32 banks) makes the two 16-lane groups of each half-wave hit
+// disjoint banks; Zs (stride 16) is conflict-free as is.
+// ---------------------------------------------------------------------------------------------
+extern "C" {
+struct ArenaWGradProblem {
+  ArenaRowSource x;       // rows m of the layer input
+  int xt;                 // 0 f32, 1 u8
+  const float* dz;        // [M][N] upstream gradient
+  int M, K, N;
+  int mode;               // 0: write grad (scaled), 1: Adam in place
+  float* gW; float* gB;   // mode 0 outputs ([K][N], [N]); gB may be null
+  float* pW; float* mW; float* vW;  // mode 1
+  float* pB; float* mB; float* vB;
+  int tiles_k, tiles_n, block_begin;
+};
+}
+
+namespace {
+constexpr int kMaxProblems = 4;
+struct WGradArgs {
+  ArenaWGradProblem p[kMaxProblems];
+  int nprob;
+  ArenaAdam adam;
+  float grad_scale;  // mode 0
+  ArenaCounterOp ctr;
+};
+
+constexpr int kMC = 128;      // rows per LDS chunk
+constexpr int kXsStride = 80; // floats
+
+template <int XT>
+__device__ __forceinline__ void stage_x(const ArenaWGradProblem& P, int mc0, int mcn, int k0,
+                                        float* Xs) {
+  // 64 columns per row: 16 threads per row, 4 consecutive k each.
+  for (int t = threadIdx.x; t < mcn * 16; t += 256) {
+    const int rr = t >> 4, q = t & 15;
+    const int k = k0 + 4 * q;
+    float v[4] = {0.f, 0.f, 0.f, 0.f};
+    if (k < P.K) {
+      const long long pr = phys_row(P.x, mc0 + rr);
+      load4<XT>(P.x, pr, k, v);  // K % 4 == 0 is enforced by the host
+    }
+    *reinterpret_cast<float4*>(&Xs[rr * kXsStride + 4 * q]) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+__global__ __launch_bounds__(256) void wgrad_grouped_kernel(WGradArgs args) {
+  __shared__ __attribute__((aligned(16))) float Xs[kMC * kXsStride];
+  __shared__ __attribute__((aligned(16))) float Zs[kMC * 16];
+  counter_op(args.ctr);
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxProblems; ++i)
+    if (i < args.nprob && (int)blockIdx.x >= args.p[i].block_begin) pi = i;
+  const ArenaWGradProblem& P = args.p[pi];
+  const int local = blockIdx.x - P.block_begin;
+  const int tk = local / P.tiles_n, tn = local % P.tiles_n;
+  const int k0 = tk * 64, n0 = tn * 16;
+  const int lane = lane_id(), w = wave_id();
+  const int g = lane >> 4, c = lane & 15;
+  const bool do_bias = (tk == 0) && (w == 0) && (P.mode == 1 ? P.pB != nullptr : P.gB != nullptr);
+
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+  for (int mc0 = 0; mc0 < P.M; mc0 += kMC) {
+    const int mcn = min(kMC, P.M - mc0);
+    if (P.xt == 1) stage_x<1>(P, mc0, mcn, k0, Xs);
+    else stage_x<0>(P, mc0, mcn, k0, Xs);
+    for (int t = threadIdx.x; t < mcn * 4; t += 256) {
+      const int rr = t >> 2, q = t & 3;
+      const int n = n0 + 4 * q;
+      const float* src = P.dz + (long long)(mc0 + rr) * P.N + n;
+      float4 v;
+      if (n + 3 < P.N && ((P.N & 3) == 0)) {
+        v = *reinterpret_cast<const float4*>(src);
+      } else {
+        v.x = (n + 0 < P.N) ? src[0] : 0.f;
+        v.y = (n + 1 < P.N) ? src[1] : 0.f;
+        v.z = (n + 2 < P.N) ? src[2] : 0.f;
+        v.w = (n + 3 < P.N) ? src[3] : 0.f;
+      }
+      *reinterpret_cast<float4*>(&Zs[rr * 16 + 4 * q]) = v;
+    }
+    __syncthreads();
+    const int nst = (mcn + 3) >> 2;
+#pragma unroll 5
+    for (int s = 0; s < nst; ++s) {
+      const int m = 4 * s + g;
+      const bool ok = m < mcn;
+      const float a = ok ? Xs[m * kXsStride + 16 * w + c] : 0.f;
+      const float b = ok ? Zs[m * 16 + c] : 0.f;
+      acc = mfma_16x16x4(a, b, acc);
+      if (do_bias) accb = mfma_16x16x4(ok ? 1.f : 0.f, b, accb);
+    }
+    __syncthreads();
+  }
+
+  const int n = n0 + c;
+  if (P.mode == 0) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + 16 * w + 4 * g + r;
+      if (k < P.K && n < P.N) P.gW[(long long)k * P.N + n] = acc[r] * args.grad_scale;
+    }
+    if (do_bias && g == 0 && n < P.N) P.gB[n] = accb[0] * args.grad_scale;
+  } else {
+    const AdamCoef co = adam_coef(args.adam);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int k = k0 + 16 * w + 4 * g + r;
+      if (k < P.K && n < P.N) {
+        const long long off = (long long)k * P.N + n;
+        float p = P.pW[off], m = P.mW[off], v = P.vW[off];
+        adam_apply(co, acc[r], p, m, v);
+        P.pW[off] = p; P.mW[off] = m; P.vW[off] = v;
+      }
+    }
+    if (do_bias && g == 0 && n < P.N) {
+      float p = P.pB[n], m = P.mB[n], v = P.vB[n];
+      adam_apply(co, accb[0], p, m, v);
+      P.pB[n] = p; P.mB[n] = m; P.vB[n] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// adam_flat: float4-vectorised Adam over the flat parameter buffer; n must be a multiple of 4.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void adam_flat_kernel(float* __restrict__ P, float* __restrict__ Mm,
+                                                        float* __restrict__ V,
+                                                        const float* __restrict__ G, long long n4,
+                                                        ArenaAdam a, ArenaCounterOp ctr) {
+  counter_op(ctr);
+  const AdamCoef co = adam_coef(a);
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 p = reinterpret_cast<float4*>(P)[i];
+    float4 m = reinterpret_cast<float4*>(Mm)[i];
+    float4 v = reinterpret_cast<float4*>(V)[i];
+    const float4 g = reinterpret_cast<const float4*>(G)[i];
+    adam_apply(co, g.x, p.x, m.x, v.x);
+    adam_apply(co, g.y, p.y, m.y, v.y);
+    adam_apply(co, g.z, p.z, m.z, v.z);
+    adam_apply(co, g.w, p.w, m.w, v.w);
+    reinterpret_cast<float4*>(P)[i] = p;
+    reinterpret_cast<float4*>(Mm)[i] = m;
+    reinterpret_cast<float4*>(V)[i] = v;
+  }
+}
+
+__global__ __launch_bounds__(256) void sgd_flat_kernel(float* __restrict__ P,
+                                                       const float* __restrict__ G, long long n4,
+                                                       float lr, const float* lr_ptr, float gscale) {
+  const float l = lr_ptr ? *lr_ptr : lr;
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 p = reinterpret_cast<float4*>(P)[i];
+    const float4 g = reinterpret_cast<const float4*>(G)[i];
+    p.x -= l * g.x * gscale; p.y -= l * g.y * gscale; p.z -= l * g.z * gscale; p.w -= l * g.w * gscale;
+    reinterpret_cast<float4*>(P)[i] = p;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// softmax_xent: generic rows (any C), one wave per row; writes per-row loss and dlogits.
+// ---------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restrict__ logits,
+                                                           const long long* __restrict__ labels,
+                                                           int M, int C, float* __restrict__ loss,
+                                                           float* __restrict__ dlogits,
+                                                           float grad_scale) {
+  const int lane = lane_id();
+  const int r = blockIdx.x * 4 + wave_id();
+  if (r >= M) return;
+  const float* x = logits + (long long)r * C;
+  float mx = -INFINITY;
+  for (int cc = lane; cc < C; cc += 64) mx = fmaxf(mx, x[cc]);
+  mx = wave_max(mx);
+  float se = 0.f;
+  for (int cc = lane; cc < C; cc += 64) se += expf(x[cc] - mx);
+  se = wave_sum(se);
+  const float lse = mx + logf(se);
+  const long long y = labels[r];
+  if (lane == 0) loss[r] = lse - x[y];
+  if (dlogits) {
+    float* d = dlogits + (long long)r * C;
+    for (int cc = lane; cc < C; cc += 64)
+      d[cc] = (expf(x[cc] - lse) - (cc == y ? 1.f : 0.f)) * grad_scale;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// mt_copy_scale: multi-tensor gather/scatter between a list of tensors and one flat bucket.
+//   dir 0: flat[off_i + j] = src_i[j] * scale      (flatten gradients into the all-reduce bucket)
+//   dir 1: dst_i[j] = flat[off_i + j] * scale      (unflatten reduced gradients)
+// ---------------------------------------------------------------------------------------------
+constexpr int kMtMax = 48;
+struct MtArgs {
+  float* ptr[kMtMax];
+  long long off[kMtMax];
+  long long n[kMtMax];
+  int blk_begin[kMtMax + 1];
+  int count;
+};
+
+__global__ __launch_bounds__(256) void mt_copy_scale_kernel(MtArgs a, float* __restrict__ flat,
+                                                            float scale, int dir) {
+  int ti = 0;
+  for (int i = 1; i < a.count; ++i)
+    if ((int)blockIdx.x >= a.blk_begin[i]) ti = i;
+  const long long base = (long long)(blockIdx.x - a.blk_begin[ti]) * 1024;
+  float* t = a.ptr[ti];
+  float* f = flat + a.off[ti];
+  for (int k = 0; k < 4; ++k) {
+    const long long j = base + k * 256 + threadIdx.x;
+    if (j < a.n[ti]) {
+      if (dir == 0) f[j] = t[j] * scale;
+      else t[j] = f[j] * scale;
+    }
+  }
+}
+
+}  // namespace
+
+// =============================================================================================
+// Host launchers (plain C ABI; the torch binding TU validates shapes before calling these).
+// =============================================================================================
+extern "C" {
+
+hipError_t arena_linear_fwd(ArenaRowSource src, const float* W, const float* bias, float* Y, int M,
+                            int N, int K, int act, float keep_prob, uint32_t seed,
+                            const long long* step_src, hipStream_t stream) {
+  uint32_t thr = 0xFFFFFFFFu;
+  float inv_keep = 1.f;
+  if (keep_prob < 1.f) {
+    thr = (uint32_t)((double)keep_prob * 4294967296.0);
+    inv_keep = 1.f / keep_prob;
+  }
+  dim3 grid((N + 15) / 16, (M + 15) / 16);
+  if (src.dtype == 1)
+    hipLaunchKernelGGL((linear_fwd_kernel<1, 8>), grid, dim3(512), 0, stream, src, W, bias, Y, M,
+                       N, K, act, thr, inv_keep, seed, step_src);
+  else
+    hipLaunchKernelGGL((linear_fwd_kernel<0, 8>), grid, dim3(512), 0, stream, src, W, bias, Y, M,
+                       N, K, act, thr, inv_keep, seed, step_src);
+  return hipGetLastError();
+}
+
+hipError_t arena_xent_head(const float* H, int M, int D, const float* W2, const float* b2, int C,
+                           ArenaRowSource lab, float* dlogits, float* dZ, float keep_prob,
+                           int relu_mask, float loss_scale, float* loss_acc, int* correct_acc,
+                           int hist_len, const long long* hist_step, ArenaCounterOp ctr,
+                           hipStream_t stream) {
+  if (D > 64 * kHeadMaxT || C > kHeadMaxC || D * C > 16384) return hipErrorInvalidValue;
+  const float inv_keep = keep_prob < 1.f ? 1.f / keep_prob : 1.f;
+  dim3 grid((M + 3) / 4);
+  const size_t smem = sizeof(float) * (size_t)D * C;
+  switch (lab.dtype) {
+    case 1:
+      hipLaunchKernelGGL((xent_head_kernel<1>), grid, dim3(256), smem, stream, H, M, D, W2, b2, C,
+                         lab, dlogits, dZ, inv_keep, relu_mask, loss_scale, loss_acc, correct_acc,
+                         hist_len, hist_step, ctr);
+      break;
+    case 2:
+      hipLaunchKernelGGL((xent_head_kernel<2>), grid, dim3(256), smem, stream, H, M, D, W2, b2, C,
+                         lab, dlogits, dZ, inv_keep, relu_mask, loss_scale, loss_acc, correct_acc,
+                         hist_len, hist_step, ctr);
+      break;
+    default:
+      hipLaunchKernelGGL((xent_head_kernel<3>), grid, dim3(256), smem, stream, H, M, D, W2, b2, C,
+                         lab, dlogits, dZ, inv_keep, relu_mask, loss_scale, loss_acc, correct_acc,
+                         hist_len, hist_step, ctr);
+  }
+  return hipGetLastError();
+}
+
+hipError_t arena_wgrad_grouped(ArenaWGradProblem* probs, int nprob, ArenaAdam adam,
+                               float grad_scale, ArenaCounterOp ctr, hipStream_t stream) {
+  if (nprob < 1 || nprob > kMaxProblems) return hipErrorInvalidValue;
+  WGradArgs a;
+  int blocks = 0;
+  for (int i = 0; i < nprob; ++i) {
+    probs[i].tiles_k = (probs[i].K + 63) / 64;
+    probs[i].tiles_n = (probs[i].N + 15) / 16;
+    probs[i].block_begin = blocks;
+    blocks += probs[i].tiles_k * probs[i].tiles_n;
+    a.p[i] = probs[i];
+  }
+  a.nprob = nprob;
+  a.adam = adam;
+  a.grad_scale = grad_scale;
+  a.ctr = ctr;
+  hipLaunchKernelGGL(wgrad_grouped_kernel, dim3(blocks), dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+hipError_t arena_adam_flat(float* P, float* M, float* V, const float* G, long long n,
+                           ArenaAdam adam, ArenaCounterOp ctr, hipStream_t stream) {
+  if (n % 4) return hipErrorInvalidValue;
+  const long long n4 = n / 4;
+  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(adam_flat_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, stream, P, M, V,
+                     G, n4, adam, ctr);
+  return hipGetLastError();
+}
+
+hipError_t arena_sgd_flat(float* P, const float* G, long long n, float lr, const float* lr_ptr,
+                          float gscale, hipStream_t stream) {
+  if (n % 4) return hipErrorInvalidValue;
+  const long long n4 = n / 4;
+  const int blocks = (int)std::min<long long>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(sgd_flat_kernel, dim3(blocks > 0 ? blocks : 1), dim3(256), 0, stream, P, G, n4,
+                     lr, lr_ptr, gscale);
+  return hipGetLastError();
+}
+
+hipError_t arena_softmax_xent(const float* logits, const long long* labels, int M, int C,
+                              float* loss, float* dlogits, float grad_scale, hipStream_t stream) {
+  hipLaunchKernelGGL(softmax_xent_kernel, dim3((M + 3) / 4), dim3(256), 0, stream, logits, labels,
+                     M, C, loss, dlogits, grad_scale);
+  return hipGetLastError();
+}
+
+// ptrs/offs/ns arrays of length count (any count; chunked into launches of kMtMax tensors).
+hipError_t arena_mt_copy_scale(float* const* ptrs, const long long* offs, const long long* ns,
+                               int count, float* flat, float scale, int dir, hipStream_t stream) {
+  for (int base = 0; base < count; base += kMtMax) {
+    MtArgs a;
+    const int cnt = std::min(kMtMax, count - base);
+    int blocks = 0;
+    for (int i = 0; i < cnt; ++i) {
+      a.ptr[i] = ptrs[base + i];
+      a.off[i] = offs[base + i];
+      a.n[i] = ns[base + i];
+      a.blk_begin[i] = blocks;
+      blocks += (int)((ns[base + i] + 1023) / 1024);
+    }
+    a.blk_begin[cnt] = blocks;
+    a.count = cnt;
+    if (blocks == 0) continue;
+    hipLaunchKernelGGL(mt_copy_scale_kernel, dim3(blocks), dim3(256), 0, stream, a, flat, scale,
+                       dir);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+}  // extern "C"

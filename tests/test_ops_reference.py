@@ -1,0 +1,80 @@
+"""The CPU reference ops (used for CPU tensors and as the GPU oracle) vs stock PyTorch."""
+import torch
+
+from arena_amd import ops
+from arena_amd.ops import reference as ref
+
+
+def test_hash_is_uint32_and_deterministic():
+    r = torch.arange(1000)
+    h1 = ref.hash4(5, 7, r, r * 3)
+    h2 = ref.hash4(5, 7, r, r * 3)
+    assert torch.equal(h1, h2)
+    assert int(h1.min()) >= 0 and int(h1.max()) <= 0xFFFFFFFF
+    # roughly uniform: keep fraction close to keep_prob
+    m = ref.dropout_keep_mask(200, 500, 0.9, 1, 2)
+    assert abs(m.float().mean().item() - 0.9) < 0.01
+
+
+def test_mix32_known_values():
+    # pinned values from the C implementation (arena::mix32 in csrc/ops/common.h)
+    def mix32(h):
+        h ^= h >> 16; h = (h * 0x7FEB352D) & 0xFFFFFFFF
+        h ^= h >> 15; h = (h * 0x846CA68B) & 0xFFFFFFFF
+        h ^= h >> 16
+        return h
+    xs = [0, 1, 12345, 0xFFFFFFFF, 0x9E3779B9]
+    got = ref._mix32(torch.tensor(xs, dtype=torch.int64)).tolist()
+    assert got == [mix32(x) for x in xs]
+
+
+def test_linear_and_wgrad_vs_autograd():
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(50, 64, generator=g)
+    W = torch.randn(64, 30, generator=g, requires_grad=True)
+    b = torch.randn(30, generator=g, requires_grad=True)
+    Y = torch.empty(50, 30)
+    ops.linear_fwd(x, W.detach(), Y, b.detach(), act=1)
+    yt = torch.relu(x @ W + b)
+    torch.testing.assert_close(Y, yt.detach())
+    up = torch.randn(50, 30, generator=g)
+    yt.backward(up)
+    dz = torch.where(Y > 0, up, torch.zeros_like(up))
+    gW = torch.empty(64, 30)
+    gb = torch.empty(30)
+    ops.wgrad_grouped([x], [dz], [gW], [gb], x_scales=[1.0], gather=[False], mode=0)
+    torch.testing.assert_close(gW, W.grad)
+    torch.testing.assert_close(gb, b.grad)
+
+
+def test_adam_flat_matches_torch():
+    g = torch.Generator().manual_seed(1)
+    p = torch.randn(100, generator=g)
+    P, M, V = p.clone(), torch.zeros(100), torch.zeros(100)
+    tp = torch.nn.Parameter(p.clone())
+    opt = torch.optim.Adam([tp], lr=0.01)
+    t = torch.zeros(1, dtype=torch.int64)
+    for s in range(1, 4):
+        gr = torch.randn(100, generator=g)
+        t.fill_(s)
+        ops.adam_flat(P, M, V, gr, lr=0.01, t_step=t)
+        tp.grad = gr
+        opt.step()
+    torch.testing.assert_close(P, tp.detach())
+
+
+def test_head_grad_vs_autograd():
+    g = torch.Generator().manual_seed(2)
+    H = torch.relu(torch.randn(20, 40, generator=g))
+    W2 = torch.randn(40, 10, generator=g, requires_grad=True)
+    b2 = torch.randn(10, generator=g)
+    y = torch.randint(0, 10, (20,), generator=g)
+    Ht = H.clone().requires_grad_(True)
+    loss = torch.nn.functional.cross_entropy(Ht @ W2 + b2, y)
+    loss.backward()
+    la, ca = torch.zeros(1), torch.zeros(1, dtype=torch.int32)
+    dl, dz = torch.empty(20, 10), torch.empty(20, 40)
+    ops.xent_head(H, W2.detach(), b2, y, loss_acc=la, correct_acc=ca, dlogits=dl, dZ=dz,
+                  relu_mask=False, loss_scale=1 / 20)
+    torch.testing.assert_close(la[0], loss.detach())
+    torch.testing.assert_close(dz, Ht.grad)
