@@ -7,6 +7,7 @@ PyTorch (the round-end GPU check records which ``.so`` files were actually loade
 from __future__ import annotations
 
 import importlib
+import os
 
 _EXT = None
 _ERR: Exception | None = None
@@ -26,7 +27,16 @@ def load():
             "arena_amd._C is not built (run `python setup.py build_ext --inplace` or "
             f"`python -c 'import __graft_entry__ as g; g.build()'`): {_ERR}")
     try:
-        _EXT = importlib.import_module("arena_amd._C")
+        mod = importlib.import_module("arena_amd._C")
+        src = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+            os.path.abspath(__file__)))), "csrc", "ops")
+        if os.path.isdir(src):
+            from ._srchash import source_hash
+            want = source_hash(src)
+            if getattr(mod, "src_hash", None) != want:
+                raise RuntimeError(f"stale build: extension built from sources {mod.src_hash}, "
+                                   f"tree has {want}")
+        _EXT = mod
     except Exception as e:  # noqa: BLE001 - report any import failure verbatim
         _ERR = e
         return load()

@@ -353,4 +353,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent", &softmax_xent);
   m.def("mt_copy_scale", &mt_copy_scale);
   m.attr("arch") = "gfx950";
+#ifndef ARENA_SRC_HASH
+#define ARENA_SRC_HASH "unknown"
+#endif
+  m.attr("src_hash") = ARENA_SRC_HASH;
 }

@@ -1,40 +1,79 @@
 """Build script for arena_amd's native components (in-tree).
 
-    PYTORCH_ROCM_ARCH=gfx950 python setup.py build_ext --inplace
+    python setup.py build_ext --inplace
 
-builds ``arena_amd/_C*.so`` (HIP kernels + torch bindings, gfx950 only). The C++ runtime tools
-(supervisor, GPU probe) are built by ``arena_amd/_build.py`` with plain g++ (no GPU needed).
+builds ``arena_amd/_C*.so``: the HIP kernels (``csrc/ops/*.hip``) are compiled by ``hipcc
+--offload-arch=gfx950`` straight from source (no hipify pass, no CUDA sources anywhere) and linked
+with the host-only torch binding TU. The C++ runtime tools (supervisor, GPU probe) are built by
+``arena_amd/_build.py`` with plain g++ (no GPU needed).
 """
 import os
+import subprocess
+import sys
 
 from setuptools import find_packages, setup
 
-os.environ.setdefault("PYTORCH_ROCM_ARCH", "gfx950")
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+if ARCH != "gfx950":
+    raise SystemExit(f"arena_amd targets MI355X only (gfx950); PYTORCH_ROCM_ARCH={ARCH}")
+
+HIP_SOURCES = ["csrc/ops/mlp_kernels.hip"]
+CPP_SOURCES = ["csrc/ops/bindings.cpp"]
 
 ext_modules = []
 cmdclass = {}
 try:
-    from torch.utils.cpp_extension import BuildExtension, CUDAExtension
+    from torch.utils.cpp_extension import BuildExtension, CppExtension
 
-    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(HERE, "arena_amd", "ops"))
+    from _srchash import source_hash  # noqa: E402
+
+    src_hash = source_hash(os.path.join(HERE, "csrc", "ops"))
+    obj_dir = os.path.join(HERE, "build", "hip_objs")
+    hip_objs = [os.path.join(obj_dir, os.path.basename(s).replace(".hip", ".o"))
+                for s in HIP_SOURCES]
+
+    class HipBuildExt(BuildExtension):
+        """Compile .hip kernels with hipcc for gfx950, then link them into the torch extension."""
+
+        def build_extensions(self):
+            os.makedirs(obj_dir, exist_ok=True)
+            hipcc = os.path.join(ROCM, "bin", "hipcc")
+            for src, obj in zip(HIP_SOURCES, hip_objs):
+                srcp = os.path.join(HERE, src)
+                deps = [srcp] + [os.path.join(HERE, "csrc", "ops", h) for h in ("abi.h", "common.h")]
+                if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d)
+                                               for d in deps):
+                    continue
+                cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+                       "-ffp-contract=fast", "-I", os.path.join(HERE, "csrc", "ops"), "-c", srcp,
+                       "-o", obj]
+                print(" ".join(cmd), flush=True)
+                subprocess.run(cmd, check=True)
+            super().build_extensions()
+
     ext_modules = [
-        CUDAExtension(
+        CppExtension(
             "arena_amd._C",
-            sources=["csrc/ops/bindings.cpp", "csrc/ops/mlp_kernels.hip"],
-            include_dirs=[os.path.join(here, "csrc", "ops")],
-            extra_compile_args={
-                "cxx": ["-O3", "-std=c++17"],
-                "nvcc": ["-O3", "--offload-arch=gfx950", "-std=c++17", "-ffp-contract=fast"],
-            },
+            sources=CPP_SOURCES,
+            include_dirs=[os.path.join(HERE, "csrc", "ops"), os.path.join(ROCM, "include")],
+            extra_objects=hip_objs,
+            library_dirs=[os.path.join(ROCM, "lib")],
+            libraries=["amdhip64", "c10_hip", "torch_hip"],
+            define_macros=[("ARENA_SRC_HASH", f'"{src_hash}"'), ("__HIP_PLATFORM_AMD__", "1"),
+                           ("USE_ROCM", "1")],
+            extra_compile_args=["-O3", "-std=c++17"],
         )
     ]
-    cmdclass = {"build_ext": BuildExtension.with_options(use_ninja=True)}
+    cmdclass = {"build_ext": HipBuildExt.with_options(use_ninja=True)}
 except ImportError:  # pragma: no cover - torch is always present in this image
     pass
 
 setup(
     name="arena_amd",
-    version=open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "VERSION")).read().strip(),
+    version=open(os.path.join(HERE, "VERSION")).read().strip(),
     packages=find_packages(include=["arena_amd", "arena_amd.*"]),
     ext_modules=ext_modules,
     cmdclass=cmdclass,
