@@ -83,7 +83,7 @@ class FusedMLPTrainer:
         D, H, C = cfg.in_dim, cfg.hidden, cfg.classes
         if D % 4 or H % 4:
             raise ValueError("in_dim and hidden must be multiples of 4 (vectorised MFMA operands)")
-        self.layout = FlatLayout({"W1": (D, H), "b1": (H,), "W2": (H, C), "b2": (C,)})
+        self.layout = FlatLayout({"W1": (H, D), "b1": (H,), "W2": (C, H), "b2": (C,)})  # [out, in]
         n = self.layout.total
         self.P = torch.zeros(n, device=dev)
         self.M = torch.zeros(n, device=dev)
@@ -142,7 +142,7 @@ class FusedMLPTrainer:
                         w[bad] = torch.randn(int(bad.sum()), generator=g) * 0.1
                         bad = w.abs() > 0.2
                 else:
-                    bound = 1.0 / math.sqrt(shp[0])
+                    bound = 1.0 / math.sqrt(shp[1])
                     w = (torch.rand(shp, generator=g) * 2 - 1) * bound
                 L.view(self.P, name).copy_(w)
             else:

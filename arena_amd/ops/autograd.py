@@ -1,8 +1,7 @@
 """Autograd wrappers so ordinary PyTorch models can use the fused HIP kernels.
 
-``FusedLinear``: y = dropout(relu(x @ W + b)) with W stored [in, out] (TF layout, as in the
-reference's TF workloads). Forward = one linear_fwd launch; backward = wgrad_grouped (dW, db in one
-launch) + a plain library GEMM for dX (hipBLASLt via torch.mm).
+``FusedLinear``: y = dropout(relu(x @ Wᵀ + b)) with W stored [out, in]. Forward = one linear_fwd launch; backward = wgrad_grouped (dW, db in one
+launch) + a plain library GEMM for dX (hipBLASLt via torch.mm). W is [out, in] (nn.Linear).
 """
 from __future__ import annotations
 
@@ -15,7 +14,7 @@ from . import fused
 
 
 def _kernel_ok(x: torch.Tensor, W: torch.Tensor) -> bool:
-    return (x.dim() == 2 and W.shape[0] % 4 == 0 and x.dtype in (torch.float32, torch.uint8)
+    return (x.dim() == 2 and W.shape[1] % 4 == 0 and x.dtype in (torch.float32, torch.uint8)
             and W.dtype == torch.float32)
 
 
@@ -23,7 +22,7 @@ class _FusedLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b, act, keep_prob, seed, step):
         x = x.contiguous()
-        Y = torch.empty(x.shape[0], W.shape[1], device=x.device, dtype=torch.float32)
+        Y = torch.empty(x.shape[0], W.shape[0], device=x.device, dtype=torch.float32)
         fused.linear_fwd(x, W, Y, b, act=act, keep_prob=keep_prob, seed=seed, step=step)
         ctx.save_for_backward(x, W, Y)
         ctx.act, ctx.keep_prob, ctx.has_bias = act, keep_prob, b is not None
@@ -39,9 +38,9 @@ class _FusedLinearFn(torch.autograd.Function):
         else:
             dZ = dY.contiguous()
         dW = torch.empty_like(W)
-        db = torch.empty(W.shape[1], device=W.device, dtype=torch.float32) if ctx.has_bias else None
+        db = torch.empty(W.shape[0], device=W.device, dtype=torch.float32) if ctx.has_bias else None
         fused.wgrad_grouped([x], [dZ], [dW], [db], x_scales=[1.0], gather=[False], mode=0)
-        dx = dZ @ W.t() if ctx.needs_input_grad[0] else None
+        dx = dZ @ W if ctx.needs_input_grad[0] else None
         return dx, dW, db, None, None, None, None
 
 
@@ -50,7 +49,7 @@ def fused_linear(x, W, b=None, act: int = 1, keep_prob: float = 1.0, seed: int =
     if act == 0 and keep_prob < 1.0:
         raise ValueError("fused dropout requires act=relu (mask is recovered from the output)")
     if not _kernel_ok(x, W):
-        z = x.float() @ W
+        z = x.float() @ W.t()
         if b is not None:
             z = z + b
         if act == 1:
@@ -60,12 +59,12 @@ def fused_linear(x, W, b=None, act: int = 1, keep_prob: float = 1.0, seed: int =
 
 
 class FusedLinear(nn.Module):
-    """Linear(+ReLU)(+dropout) layer on the fused HIP kernels; weight is [in, out]."""
+    """Linear(+ReLU)(+dropout) layer on the fused HIP kernels; weight is [out, in]."""
 
     def __init__(self, in_features: int, out_features: int, bias: bool = True,
                  activation: str = "relu", keep_prob: float = 1.0, seed: int = 0):
         super().__init__()
-        self.weight = nn.Parameter(torch.empty(in_features, out_features))
+        self.weight = nn.Parameter(torch.empty(out_features, in_features))
         self.bias = nn.Parameter(torch.zeros(out_features)) if bias else None
         self.act = {"relu": 1, "none": 0, None: 0}[activation]
         self.keep_prob = keep_prob

@@ -69,14 +69,14 @@ def gather_rows(x: torch.Tensor, idx: torch.Tensor | None, cursor: torch.Tensor 
 def linear_fwd(x, x_scale, idx, cursor, batch, W, bias, Y, act, keep_prob, seed, step):
     M = Y.shape[0]
     xr = gather_rows(x, idx, cursor, batch, M).to(torch.float32) * x_scale
-    z = xr @ W
+    z = xr @ W.t()  # W is [out, in]
     if bias is not None:
         z = z + bias
     if act == 1:
         z = torch.relu(z)
     if keep_prob < 1.0:
         st = int(step.reshape(-1)[0].item()) & _M32 if step is not None else 0
-        mask = dropout_keep_mask(M, W.shape[1], keep_prob, seed, st, device=z.device)
+        mask = dropout_keep_mask(M, W.shape[0], keep_prob, seed, st, device=z.device)
         z = torch.where(mask, z * (1.0 / keep_prob), torch.zeros_like(z))
     Y.copy_(z)
 
@@ -90,7 +90,7 @@ def xent_head(H, W2, b2, labels, idx, cursor, batch, dlogits, dZ, keep_prob, rel
     if L > 1:
         loss_acc[(hs + 1) % L] = 0.0
         correct_acc[(hs + 1) % L] = 0
-    logits = H @ W2
+    logits = H @ W2.t()  # W2 is [classes, hidden]
     if b2 is not None:
         logits = logits + b2
     y = gather_rows(labels, idx, cursor, batch, M).to(torch.int64)
@@ -103,12 +103,12 @@ def xent_head(H, W2, b2, labels, idx, cursor, batch, dlogits, dZ, keep_prob, rel
         ctr_dst.fill_(src + ctr_add)
     if dlogits is None:
         return
-    g = (torch.softmax(logits, dim=1) - torch.nn.functional.one_hot(y, W2.shape[1]).to(H.dtype))
+    g = (torch.softmax(logits, dim=1) - torch.nn.functional.one_hot(y, W2.shape[0]).to(H.dtype))
     g = g * loss_scale
     dlogits.view(M, -1).copy_(g)
     if dZ is None:
         return
-    dz = g @ W2.t()
+    dz = g @ W2
     if relu_mask:
         inv_keep = 1.0 / keep_prob if keep_prob < 1.0 else 1.0
         dz = torch.where(H > 0, dz * inv_keep, torch.zeros_like(dz))
@@ -143,7 +143,7 @@ def wgrad_grouped(xs, x_scales, gather, idx, cursor, cursor_off, batch, dzs, mod
         else:
             xr = xs[i][:M]
         xr = xr.to(torch.float32) * x_scales[i]
-        gw = xr.t() @ dz
+        gw = dz.t() @ xr  # [N, K] = [out, in]
         gb = dz.sum(dim=0)
         pending.append((i, gw, gb))
     for i, gw, gb in pending:

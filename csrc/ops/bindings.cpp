@@ -103,9 +103,10 @@ void linear_fwd(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch, 
   check_f32(W, "W");
   check_f32(Y, "Y");
   TORCH_CHECK(W.dim() == 2 && Y.dim() == 2 && x.dim() == 2, "linear_fwd: 2-D tensors required");
-  const int64_t M = Y.size(0), N = Y.size(1), K = W.size(0);
-  TORCH_CHECK(W.size(1) == N, "W.shape[1] must equal Y.shape[1]");
-  TORCH_CHECK(x.size(1) == K, "x.shape[1] must equal W.shape[0]");
+  // W is [out, in] (nn.Linear layout)
+  const int64_t M = Y.size(0), N = Y.size(1), K = W.size(1);
+  TORCH_CHECK(W.size(0) == N, "W.shape[0] must equal Y.shape[1]");
+  TORCH_CHECK(x.size(1) == K, "x.shape[1] must equal W.shape[1]");
   TORCH_CHECK(K % 4 == 0, "linear_fwd: K must be a multiple of 4 (got ", K, ")");
   TORCH_CHECK(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kUInt8,
               "x must be float32 or uint8");
@@ -130,9 +131,11 @@ void xent_head(Tensor H, Tensor W2, OptT b2, Tensor labels, OptT idx, OptT curso
                int64_t ctr_add) {
   check_f32(H, "H");
   check_f32(W2, "W2");
-  const int64_t M = H.size(0), D = H.size(1), C = W2.size(1);
-  TORCH_CHECK(W2.size(0) == D, "W2.shape[0] must equal H.shape[1]");
-  TORCH_CHECK(D <= 1024 && C <= 16 && D * C <= 16384, "xent_head: D<=1024, C<=16, D*C<=16384");
+  // W2 is [classes, hidden]
+  const int64_t M = H.size(0), D = H.size(1), C = W2.size(0);
+  TORCH_CHECK(W2.size(1) == D, "W2.shape[1] must equal H.shape[1]");
+  TORCH_CHECK(D <= 1024 && C <= 16 && D * C <= 16384 && (D * C) % 4 == 0,
+              "xent_head: D<=1024, C<=16, D*C<=16384, D*C % 4 == 0");
   TORCH_CHECK(labels.dim() == 1, "labels must be 1-D");
   const float* pb2 = nullptr;
   if (b2.has_value()) {

@@ -4,16 +4,16 @@
 // dist-mnist, Horovod): see docs/userguide/1-tfjob-standalone.md:178-186 and SURVEY.md §2.11. Their
 // hot ops -- GEMM+bias+ReLU, dropout, softmax-cross-entropy, Adam -- are implemented here natively:
 //
-//   linear_fwd      Y = dropout(act(X·W + b))       X rows gathered from the dataset in-kernel
-//   xent_head       logits = H·W2 + b2 -> loss, accuracy, dlogits, dZ = (dlogits·W2ᵀ)⊙mask
-//   wgrad_grouped   dW = Xᵀ·dZ, db = 1ᵀ·dZ for up to 4 layers in ONE launch, epilogue either
+//   linear_fwd      Y = dropout(act(X·Wᵀ + b))      X rows gathered from the dataset in-kernel
+//   xent_head       logits = H·W2ᵀ + b2 -> loss, accuracy, dlogits, dZ = (dlogits·W2)⊙mask
+//   wgrad_grouped   dW = dZᵀ·X, db = dZᵀ·1 for up to 4 layers in ONE launch, epilogue either
 //                   writes the (scaled) gradient into the flat all-reduce bucket or applies Adam
 //   adam_flat       Adam over the whole flat parameter buffer (after the gradient all-reduce)
 //   softmax_xent    generic row softmax-cross-entropy forward+backward
 //   mt_copy_scale   multi-tensor flatten/unflatten with scale (gradient buckets)
 //
 // All matmul work uses the exact-fp32 MFMA v_mfma_f32_16x16x4_f32 (no TF32 on gfx950), so numerics
-// equal an fp32 fmaf chain. Layout is TF-style: W is [K][N] (in x out), activations row-major.
+// equal an fp32 fmaf chain. Weights are [out][in] (nn.Linear layout), activations row-major.
 #include "common.h"
 
 #include <algorithm>
@@ -22,13 +22,6 @@
 using namespace arena;
 
 namespace {
-
-__device__ __forceinline__ long long phys_row(const ArenaRowSource& s, long long r) {
-  if (s.idx == nullptr) return r;
-  const long long cur = (s.cursor ? *s.cursor : 0) + s.cursor_off;
-  const long long pos = (cur * (long long)s.batch + r) % s.idx_len;
-  return (long long)s.idx[pos];
-}
 
 template <int XT>
 __device__ __forceinline__ void load4(const ArenaRowSource& s, long long prow, int k, float out[4]) {
@@ -92,11 +85,24 @@ __device__ __forceinline__ void adam_apply(const AdamCoef& c, float g, float& p,
   p -= c.step_size * m / (sqrtf(v) * c.inv_sqrt_bc2 + c.eps);
 }
 
+// Data cursor (wave-uniform scalar load) and the gathered physical row of logical row r.
+__device__ __forceinline__ long long row_cursor(const ArenaRowSource& s) {
+  return (s.cursor ? *s.cursor : 0) + s.cursor_off;
+}
+__device__ __forceinline__ long long gather_row(const ArenaRowSource& s, long long cur,
+                                                long long r) {
+  if (s.idx == nullptr) return r;
+  return (long long)s.idx[(cur * (long long)s.batch + r) % s.idx_len];
+}
+
 // ---------------------------------------------------------------------------------------------
-// linear_fwd: one 16x16 output tile per workgroup, K split across WAVES waves, partial tiles
-// reduced through LDS. Lane (g = l>>4, c = l&15) loads 4 consecutive k of its A row with one
-// vector load; MFMA j consumes k = 16s + 4g + j (a fixed permutation of the K order that A and B
-// share). Grid: (ceil(N/16), ceil(M/16)).
+// linear_fwd: Y[M][N] = dropout(act(X·Wᵀ + b)), W stored [N][K] (out x in, nn.Linear layout).
+// One 16x16 output tile per workgroup; K split across WAVES waves, partial tiles reduced through
+// LDS. Lane (g = l>>4, c = l&15) loads 4 consecutive k of its A row (X) and of its B column (a W
+// row) with ONE vector load each; MFMA j consumes k = 16s + 4g + j (a K permutation shared by A
+// and B). Every load is unconditional on a clamped address (out-of-range operands are zeroed
+// AFTER the load): a branch around a load makes hipcc drain vmcnt per element.
+// Grid: (ceil(N/16), ceil(M/16)).
 // ---------------------------------------------------------------------------------------------
 template <int XT, int WAVES>
 __global__ __launch_bounds__(WAVES * 64) void linear_fwd_kernel(
@@ -107,9 +113,11 @@ __global__ __launch_bounds__(WAVES * 64) void linear_fwd_kernel(
   const int lane = lane_id(), w = wave_id();
   const int g = lane >> 4, c = lane & 15;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
-  const int row = m0 + c, col = n0 + c;
-  const bool row_ok = row < M, col_ok = col < N;
-  const long long prow = row_ok ? phys_row(src, row) : 0;
+  const int rowc = min(m0 + c, M - 1), colc = min(n0 + c, N - 1);
+  const long long cur = row_cursor(src);
+  const uint32_t step = step_src ? (uint32_t)(*step_src) : 0u;  // early: off the epilogue's path
+  const long long prow = gather_row(src, cur, rowc);
+  const float* wrow = W + (long long)colc * K;
   const int nsteps = (K + 15) >> 4;
   const int s0 = (nsteps * w) / WAVES, s1 = (nsteps * (w + 1)) / WAVES;
 
@@ -119,14 +127,16 @@ __global__ __launch_bounds__(WAVES * 64) void linear_fwd_kernel(
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int k = (sb + i) * 16 + 4 * g;
-      const bool ok = (sb + i < s1) && (k < K);
-      if (ok && row_ok) {
-        load4<XT>(src, prow, k, a[i]);
-      } else {
-        a[i][0] = a[i][1] = a[i][2] = a[i][3] = 0.f;
-      }
+      const int kc = min(k, K - 4);
+      load4<XT>(src, prow, kc, a[i]);
+      const float4 wv = *reinterpret_cast<const float4*>(wrow + kc);
+      b[i][0] = wv.x; b[i][1] = wv.y; b[i][2] = wv.z; b[i][3] = wv.w;
+    }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) b[i][j] = (ok && col_ok) ? W[(long long)(k + j) * N + col] : 0.f;
+    for (int i = 0; i < CH; ++i) {
+      const bool kv = ((sb + i) * 16 + 4 * g) < K;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[i][j] = kv ? a[i][j] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
@@ -141,7 +151,6 @@ __global__ __launch_bounds__(WAVES * 64) void linear_fwd_kernel(
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[w][4 * g + r][c] = acc[r];
   __syncthreads();
-  const uint32_t step = step_src ? (uint32_t)(*step_src) : 0u;
   for (int t = threadIdx.x; t < 256; t += WAVES * 64) {
     const int rr = t >> 4, cc = t & 15;
     const int gm = m0 + rr, gn = n0 + cc;
@@ -161,26 +170,57 @@ __global__ __launch_bounds__(WAVES * 64) void linear_fwd_kernel(
 }
 
 // ---------------------------------------------------------------------------------------------
-// xent_head: one wave per batch row, 4 rows per workgroup, W2 staged in LDS.
-//   logits = h·W2 + b2; loss = lse - logit[y]; dlogits = (softmax - onehot) * loss_scale
-//   dZ[j] = (Σ_c dlogits[c]·W2[j][c]) * (h[j] > 0 ? inv_keep : 0)      (ReLU + dropout backward)
-// Loss/correct are accumulated (one atomic per row) into slot (*hist_step % hist_len); block 0
-// zeroes the NEXT slot so a graph-replayed loop keeps a ring of per-step metrics on device.
+// xent_head: one wave per batch row, 4 rows per workgroup; W2 [C][D] staged in LDS by float4
+// loads that are all in flight at once (one round trip), concurrently with the row's H loads and
+// the label gather chain.
+//   logits = h·W2ᵀ + b2; loss = lse - logit[y]; dlogits = (softmax - onehot) * loss_scale
+//   dZ[j] = (Σ_c dlogits[c]·W2[c][j]) * (h[j] > 0 ? inv_keep : 0)      (ReLU + dropout backward)
+// Loss/correct go (one atomic per row) into slot (*hist_step % hist_len); block 0 zeroes the NEXT
+// slot, so a graph-replayed loop keeps a ring of per-step metrics on the device.
 // ---------------------------------------------------------------------------------------------
 constexpr int kHeadMaxT = 16;  // hidden <= 1024
 constexpr int kHeadMaxC = 16;  // classes <= 16
+constexpr int kHeadStage = 16; // max float4 staging loads per thread (D*C <= 16384)
 
-template <int LT>
-__global__ __launch_bounds__(256) void xent_head_kernel(
+template <int LT, int STAGE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void xent_head_kernel(
     const float* __restrict__ H, int M, int D, const float* __restrict__ W2,
     const float* __restrict__ b2, int C, ArenaRowSource lab, float* __restrict__ dlogits,
     float* __restrict__ dZ, float inv_keep, int relu_mask, float loss_scale,
     float* __restrict__ loss_acc, int* __restrict__ correct_acc, int hist_len,
     const long long* hist_step, ArenaCounterOp ctr) {
-  extern __shared__ __attribute__((aligned(16))) float ws[];  // [D][C]
-  for (int i = threadIdx.x; i < D * C; i += blockDim.x) ws[i] = W2[i];
-  counter_op(ctr);
+  extern __shared__ __attribute__((aligned(16))) float ws[];  // [C][D]
+  const int lane = lane_id();
+  const int r = blockIdx.x * 4 + wave_id();
+  const int rc = min(r, M - 1);
+  // (1) issue every independent global load up front
+  const long long cur = row_cursor(lab);
+  const long long pr = gather_row(lab, cur, rc);
+  int y;
+  if constexpr (LT == 1) y = (int)static_cast<const uint8_t*>(lab.ptr)[pr];
+  else if constexpr (LT == 2) y = static_cast<const int*>(lab.ptr)[pr];
+  else y = (int)static_cast<const long long*>(lab.ptr)[pr];
+  float h[kHeadMaxT];
+#pragma unroll
+  for (int t = 0; t < kHeadMaxT; ++t) h[t] = H[(long long)rc * D + min(lane + 64 * t, D - 1)];
+  const int n4 = (D * C) >> 2;  // host guarantees (D*C) % 4 == 0
+  float4 st[STAGE];
+#pragma unroll
+  for (int i = 0; i < STAGE; ++i)
+    st[i] = reinterpret_cast<const float4*>(W2)[min((int)threadIdx.x + 256 * i, n4 - 1)];
+  float bb[kHeadMaxC];
+#pragma unroll
+  for (int cc = 0; cc < kHeadMaxC; ++cc) bb[cc] = b2 ? b2[min(cc, C - 1)] : 0.f;
   const long long hs = hist_step ? *hist_step : 0;
+  // (2) stage, bookkeeping
+  // unconditional stores (out-of-range items go to a dummy slot at ws[4*n4]): a store guarded by
+  // a branch lets hipcc sink each load into the branch and wait for it there, serialising them.
+#pragma unroll
+  for (int i = 0; i < STAGE; ++i) {
+    const int q = threadIdx.x + 256 * i;
+    reinterpret_cast<float4*>(ws)[q < n4 ? q : n4] = st[i];
+  }
+  counter_op(ctr);
   const int slot = hist_len > 1 ? (int)(hs % hist_len) : 0;
   if (hist_len > 1 && blockIdx.x == 0 && threadIdx.x == 0) {
     const int nxt = (int)((hs + 1) % hist_len);
@@ -188,52 +228,39 @@ __global__ __launch_bounds__(256) void xent_head_kernel(
     correct_acc[nxt] = 0;
   }
   __syncthreads();
-
-  const int lane = lane_id();
-  const int r = blockIdx.x * 4 + wave_id();
   if (r >= M) return;
-
-  float h[kHeadMaxT];
 #pragma unroll
-  for (int t = 0; t < kHeadMaxT; ++t) {
-    const int j = lane + 64 * t;
-    h[t] = (j < D) ? H[(long long)r * D + j] : 0.f;
-  }
+  for (int t = 0; t < kHeadMaxT; ++t) h[t] = (lane + 64 * t < D) ? h[t] : 0.f;
+
+  // (3) logits: per-lane partial dot products, then 64-lane reductions (independent chains)
   float lg[kHeadMaxC];
 #pragma unroll
   for (int cc = 0; cc < kHeadMaxC; ++cc) {
-    lg[cc] = -INFINITY;
+    float s = 0.f;
     if (cc < C) {
-      float s = 0.f;
 #pragma unroll
       for (int t = 0; t < kHeadMaxT; ++t) {
         const int j = lane + 64 * t;
-        if (j < D) s += h[t] * ws[j * C + cc];
+        if (j < D) s += h[t] * ws[cc * D + j];
       }
-      lg[cc] = wave_sum(s) + (b2 ? b2[cc] : 0.f);
     }
+    lg[cc] = s;
   }
+#pragma unroll
+  for (int cc = 0; cc < kHeadMaxC; ++cc) lg[cc] = (cc < C) ? wave_sum(lg[cc]) + bb[cc] : -INFINITY;
   float mx = lg[0];
   int arg = 0;
 #pragma unroll
-  for (int cc = 1; cc < kHeadMaxC; ++cc) {
+  for (int cc = 1; cc < kHeadMaxC; ++cc)
     if (cc < C && lg[cc] > mx) { mx = lg[cc]; arg = cc; }
-  }
   float se = 0.f;
 #pragma unroll
   for (int cc = 0; cc < kHeadMaxC; ++cc)
     if (cc < C) se += expf(lg[cc] - mx);
   const float lse = mx + logf(se);
-
-  const long long pr = phys_row(lab, r);
-  int y;
-  if constexpr (LT == 1) y = (int)static_cast<const uint8_t*>(lab.ptr)[pr];
-  else if constexpr (LT == 2) y = static_cast<const int*>(lab.ptr)[pr];
-  else y = (int)static_cast<const long long*>(lab.ptr)[pr];
   float ly = 0.f;
 #pragma unroll
   for (int cc = 0; cc < kHeadMaxC; ++cc) ly = (cc == y) ? lg[cc] : ly;
-
   if (lane == 0) {
     atomicAdd(&loss_acc[slot], (lse - ly) * loss_scale);
     atomicAdd(&correct_acc[slot], arg == y ? 1 : 0);
@@ -258,26 +285,25 @@ __global__ __launch_bounds__(256) void xent_head_kernel(
       float s = 0.f;
 #pragma unroll
       for (int cc = 0; cc < kHeadMaxC; ++cc)
-        if (cc < C) s += gcl[cc] * ws[j * C + cc];
+        if (cc < C) s += gcl[cc] * ws[cc * D + j];
       if (relu_mask) s = (h[t] > 0.f) ? s * inv_keep : 0.f;
       dZ[(long long)r * D + j] = s;
     }
   }
 }
 
-}  // namespace
-
 // ---------------------------------------------------------------------------------------------
-// wgrad_grouped: dW = Xᵀ·dZ (+ db = 1ᵀ·dZ) for up to kMaxProblems layers in one launch.
-// Workgroup = 4 waves = a 64(k) x 16(n) tile of dW; the gathered X block [m][64] and the dZ slice
-// [m][16] are staged through LDS once per 128-row chunk and shared by the 4 waves.
-//   A operand (Xᵀ): lane l -> Xs[m = ms + (l>>4)][k = 16w + (l&15)]
-//   B operand (dZ): lane l -> Zs[m = ms + (l>>4)][n = l&15]
-// Xs row stride 80 floats (≡16 mod 32 banks) makes the two 16-lane groups of each half-wave hit
-// disjoint banks; Zs (stride 16) is conflict-free as is.
+// wgrad_grouped: dW[N][K] = dZᵀ·X (+ db = dZᵀ·1) for up to kMaxProblems layers in one launch.
+// Workgroup = 4 waves = a 16(n) x 64(k) tile of dW. Per 128-row chunk: (1) the gathered row ids
+// go to LDS (one dependent chain per row, once), (2) the X block [m][64] and the dZ slice [m][16]
+// are staged through LDS with every load of the block in flight at once, (3) 4 waves run the MFMA
+// K-loop over m. The Adam state of the tile is prefetched at kernel entry so its latency hides
+// under the staging.
+//   A operand (dZᵀ): lane l -> Zs[m = 4s + (l>>4)][n = l&15]         (stride 16: conflict-free)
+//   B operand (X)  : lane l -> Xs[m = 4s + (l>>4)][k = 16w + (l&15)] (stride 80 ≡ 16 mod 32 banks:
+//                    the two 16-lane groups of each half-wave hit disjoint banks)
+//   D              : lane l, reg r -> dW[n0 + 4(l>>4) + r][k0 + 16w + (l&15)]   (coalesced rows)
 // ---------------------------------------------------------------------------------------------
-
-namespace {
 constexpr int kMaxProblems = 4;
 struct WGradArgs {
   ArenaWGradProblem p[kMaxProblems];
@@ -287,26 +313,41 @@ struct WGradArgs {
   ArenaCounterOp ctr;
 };
 
-constexpr int kMC = 128;      // rows per LDS chunk
-constexpr int kXsStride = 80; // floats
+constexpr int kMC = 128;       // rows per LDS chunk
+constexpr int kXsStride = 80;  // floats
+constexpr int kXItems = (kMC * 16) / 256;  // X staging items per thread (16 per row)
+constexpr int kZItems = (kMC * 4) / 256;   // dZ staging items per thread (4 float4 per row)
+
+// Raw workgroup barrier for LDS hand-offs: waits only for this wave's LDS ops (lgkmcnt), NOT for
+// its outstanding global loads (__syncthreads() would emit vmcnt(0) and drain the prefetches).
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 template <int XT>
-__device__ __forceinline__ void stage_x(const ArenaWGradProblem& P, int mc0, int mcn, int k0,
-                                        float* Xs) {
-  // 64 columns per row: 16 threads per row, 4 consecutive k each.
-  for (int t = threadIdx.x; t < mcn * 16; t += 256) {
-    const int rr = t >> 4, q = t & 15;
-    const int k = k0 + 4 * q;
-    float v[4] = {0.f, 0.f, 0.f, 0.f};
-    if (k < P.K) {
-      const long long pr = phys_row(P.x, mc0 + rr);
-      load4<XT>(P.x, pr, k, v);  // K % 4 == 0 is enforced by the host
-    }
-    *reinterpret_cast<float4*>(&Xs[rr * kXsStride + 4 * q]) = make_float4(v[0], v[1], v[2], v[3]);
+__device__ __forceinline__ void load_x_items(const ArenaWGradProblem& P, long long cur, int mc0,
+                                             int mcn, int k0, float4 (&v)[kXItems]) {
+  // 16 items per row, item q = 4 consecutive k (one u32 of u8 pixels or one float4). Rows past
+  // mcn re-read row mcn-1 (finite data; their A operand is zeroed in the K-loop).
+  int prow[kXItems];
+#pragma unroll
+  for (int i = 0; i < kXItems; ++i) {
+    const int t = threadIdx.x + 256 * i;
+    prow[i] = (int)gather_row(P.x, cur, mc0 + min(t >> 4, mcn - 1));
+  }
+#pragma unroll
+  for (int i = 0; i < kXItems; ++i) {
+    const int q = (threadIdx.x + 256 * i) & 15;
+    float f[4];
+    load4<XT>(P.x, prow[i], min(k0 + 4 * q, P.K - 4), f);
+    v[i] = make_float4(f[0], f[1], f[2], f[3]);
   }
 }
 
-__global__ __launch_bounds__(256) void wgrad_grouped_kernel(WGradArgs args) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void wgrad_grouped_kernel(
+    WGradArgs args) {
   __shared__ __attribute__((aligned(16))) float Xs[kMC * kXsStride];
   __shared__ __attribute__((aligned(16))) float Zs[kMC * 16];
   counter_op(args.ctr);
@@ -316,71 +357,136 @@ __global__ __launch_bounds__(256) void wgrad_grouped_kernel(WGradArgs args) {
     if (i < args.nprob && (int)blockIdx.x >= args.p[i].block_begin) pi = i;
   const ArenaWGradProblem& P = args.p[pi];
   const int local = blockIdx.x - P.block_begin;
-  const int tk = local / P.tiles_n, tn = local % P.tiles_n;
-  const int k0 = tk * 64, n0 = tn * 16;
+  const int tn = local / P.tiles_k, tk = local % P.tiles_k;
+  const int n0 = tn * 16, k0 = tk * 64;
   const int lane = lane_id(), w = wave_id();
   const int g = lane >> 4, c = lane & 15;
-  const bool do_bias = (tk == 0) && (w == 0) && (P.mode == 1 ? P.pB != nullptr : P.gB != nullptr);
+  const int kk = k0 + 16 * w + c;
+  const int kkc = min(kk, P.K - 1);
+  const bool bias_wave = (tk == 0) && (w == 0);
+  const bool has_bias = P.mode == 1 ? P.pB != nullptr : P.gB != nullptr;
+  const long long cur = row_cursor(P.x);
+  const bool zvec = (P.N & 3) == 0;
+  AdamCoef co{};
+  if (P.mode == 1) co = adam_coef(args.adam);  // t / lr loads issued first, off the epilogue path
 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   f32x4 accb = {0.f, 0.f, 0.f, 0.f};
+  float pw[4], mw[4], vw[4], pb[4], mb[4], vb[4];
   for (int mc0 = 0; mc0 < P.M; mc0 += kMC) {
     const int mcn = min(kMC, P.M - mc0);
-    if (P.xt == 1) stage_x<1>(P, mc0, mcn, k0, Xs);
-    else stage_x<0>(P, mc0, mcn, k0, Xs);
-    for (int t = threadIdx.x; t < mcn * 4; t += 256) {
+    // (1) issue the chunk's loads: gathered X items, the dZ slice [m][16 n]
+    float4 xv[kXItems];
+    if (P.xt == 1) load_x_items<1>(P, cur, mc0, mcn, k0, xv);
+    else load_x_items<0>(P, cur, mc0, mcn, k0, xv);
+    float4 zv[kZItems];
+#pragma unroll
+    for (int i = 0; i < kZItems; ++i) {
+      const int t = threadIdx.x + 256 * i;
+      const int rr = min(t >> 2, mcn - 1), q = t & 3;
+      const int n = n0 + 4 * q;
+      const float* srcp = P.dz + (long long)(mc0 + rr) * P.N;
+      if (zvec) {
+        zv[i] = *reinterpret_cast<const float4*>(srcp + min(n, P.N - 4));
+      } else {
+        zv[i] = make_float4(srcp[min(n, P.N - 1)], srcp[min(n + 1, P.N - 1)],
+                            srcp[min(n + 2, P.N - 1)], srcp[min(n + 3, P.N - 1)]);
+      }
+    }
+    // (2) on the first chunk, prefetch the tile's Adam state behind them (in-order vmcnt lets the
+    //     staging waits below leave these in flight through the K-loop)
+    if (mc0 == 0 && P.mode == 1) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const long long off = (long long)min(n0 + 4 * g + r, P.N - 1) * P.K + kkc;
+        pw[r] = P.pW[off]; mw[r] = P.mW[off]; vw[r] = P.vW[off];
+      }
+      if (bias_wave && has_bias) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = min(n0 + 4 * g + r, P.N - 1);
+          pb[r] = P.pB[n]; mb[r] = P.mB[n]; vb[r] = P.vB[n];
+        }
+      }
+    }
+    // (3) LDS images; every store unconditional (no branch for hipcc to sink a load into)
+#pragma unroll
+    for (int i = 0; i < kXItems; ++i) {
+      const int t = threadIdx.x + 256 * i;
+      const int rr = t >> 4, q = t & 15;
+      const float4 o = (k0 + 4 * q < P.K) ? xv[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(&Xs[rr * kXsStride + 4 * q]) = o;
+    }
+#pragma unroll
+    for (int i = 0; i < kZItems; ++i) {
+      const int t = threadIdx.x + 256 * i;
       const int rr = t >> 2, q = t & 3;
       const int n = n0 + 4 * q;
-      const float* src = P.dz + (long long)(mc0 + rr) * P.N + n;
-      float4 v;
-      if (n + 3 < P.N && ((P.N & 3) == 0)) {
-        v = *reinterpret_cast<const float4*>(src);
-      } else {
-        v.x = (n + 0 < P.N) ? src[0] : 0.f;
-        v.y = (n + 1 < P.N) ? src[1] : 0.f;
-        v.z = (n + 2 < P.N) ? src[2] : 0.f;
-        v.w = (n + 3 < P.N) ? src[3] : 0.f;
+      float4 o = zv[i];
+      o.x = (n + 0 < P.N) ? o.x : 0.f;
+      o.y = (n + 1 < P.N) ? o.y : 0.f;
+      o.z = (n + 2 < P.N) ? o.z : 0.f;
+      o.w = (n + 3 < P.N) ? o.w : 0.f;
+      if (rr >= mcn) o = make_float4(0.f, 0.f, 0.f, 0.f);
+      *reinterpret_cast<float4*>(&Zs[rr * 16 + 4 * q]) = o;
+    }
+    lds_barrier();
+    // (4) K-loop over all kMC rows of the image (rows >= mcn: Zs zero, Xs finite), fully
+    //     unrolled so every LDS read is issued ahead of its MFMA
+    if (mcn > kMC / 2) {
+#pragma unroll
+      for (int s = 0; s < kMC / 4; ++s) {
+        const int m = 4 * s + g;
+        const float a = Zs[m * 16 + c];
+        const float b = Xs[m * kXsStride + 16 * w + c];
+        acc = mfma_16x16x4(a, b, acc);
+        if (bias_wave) accb = mfma_16x16x4(a, 1.f, accb);
       }
-      *reinterpret_cast<float4*>(&Zs[rr * 16 + 4 * q]) = v;
+    } else {
+      const int nst = (mcn + 3) >> 2;
+      for (int s = 0; s < nst; ++s) {
+        const int m = 4 * s + g;
+        const float a = Zs[m * 16 + c];
+        const float b = Xs[m * kXsStride + 16 * w + c];
+        acc = mfma_16x16x4(a, b, acc);
+        if (bias_wave) accb = mfma_16x16x4(a, 1.f, accb);
+      }
     }
-    __syncthreads();
-    const int nst = (mcn + 3) >> 2;
-#pragma unroll 5
-    for (int s = 0; s < nst; ++s) {
-      const int m = 4 * s + g;
-      const bool ok = m < mcn;
-      const float a = ok ? Xs[m * kXsStride + 16 * w + c] : 0.f;
-      const float b = ok ? Zs[m * 16 + c] : 0.f;
-      acc = mfma_16x16x4(a, b, acc);
-      if (do_bias) accb = mfma_16x16x4(ok ? 1.f : 0.f, b, accb);
-    }
-    __syncthreads();
+    if (mc0 + kMC < P.M) lds_barrier();  // before the next chunk overwrites the images
   }
 
-  const int n = n0 + c;
   if (P.mode == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      const int k = k0 + 16 * w + 4 * g + r;
-      if (k < P.K && n < P.N) P.gW[(long long)k * P.N + n] = acc[r] * args.grad_scale;
+      const int n = n0 + 4 * g + r;
+      if (kk < P.K && n < P.N) P.gW[(long long)n * P.K + kk] = acc[r] * args.grad_scale;
     }
-    if (do_bias && g == 0 && n < P.N) P.gB[n] = accb[0] * args.grad_scale;
-  } else {
-    const AdamCoef co = adam_coef(args.adam);
+    if (bias_wave && has_bias && c == 0) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int k = k0 + 16 * w + 4 * g + r;
-      if (k < P.K && n < P.N) {
-        const long long off = (long long)k * P.N + n;
-        float p = P.pW[off], m = P.mW[off], v = P.vW[off];
-        adam_apply(co, acc[r], p, m, v);
-        P.pW[off] = p; P.mW[off] = m; P.vW[off] = v;
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + 4 * g + r;
+        if (n < P.N) P.gB[n] = accb[r] * args.grad_scale;
       }
     }
-    if (do_bias && g == 0 && n < P.N) {
-      float p = P.pB[n], m = P.mB[n], v = P.vB[n];
-      adam_apply(co, accb[0], p, m, v);
-      P.pB[n] = p; P.mB[n] = m; P.vB[n] = v;
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int n = n0 + 4 * g + r;
+      if (kk < P.K && n < P.N) {
+        const long long off = (long long)n * P.K + kk;
+        adam_apply(co, acc[r], pw[r], mw[r], vw[r]);
+        P.pW[off] = pw[r]; P.mW[off] = mw[r]; P.vW[off] = vw[r];
+      }
+    }
+    if (bias_wave && has_bias && c == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int n = n0 + 4 * g + r;
+        if (n < P.N) {
+          adam_apply(co, accb[r], pb[r], mb[r], vb[r]);
+          P.pB[n] = pb[r]; P.mB[n] = mb[r]; P.vB[n] = vb[r];
+        }
+      }
     }
   }
 }
@@ -511,26 +617,22 @@ hipError_t arena_xent_head(const float* H, int M, int D, const float* W2, const 
                            int relu_mask, float loss_scale, float* loss_acc, int* correct_acc,
                            int hist_len, const long long* hist_step, ArenaCounterOp ctr,
                            hipStream_t stream) {
-  if (D > 64 * kHeadMaxT || C > kHeadMaxC || D * C > 16384) return hipErrorInvalidValue;
+  if (D > 64 * kHeadMaxT || C > kHeadMaxC || D * C > 1024 * kHeadStage || (D * C) % 4)
+    return hipErrorInvalidValue;
   const float inv_keep = keep_prob < 1.f ? 1.f / keep_prob : 1.f;
   dim3 grid((M + 3) / 4);
-  const size_t smem = sizeof(float) * (size_t)D * C;
+  const size_t smem = sizeof(float) * ((size_t)D * C + 4);  // + dummy float4 slot
+  const bool big = D * C > 1024 * 8;
+#define ARENA_HEAD(LT, ST)                                                                      \
+  hipLaunchKernelGGL((xent_head_kernel<LT, ST>), grid, dim3(256), smem, stream, H, M, D, W2, b2, \
+                     C, lab, dlogits, dZ, inv_keep, relu_mask, loss_scale, loss_acc,             \
+                     correct_acc, hist_len, hist_step, ctr)
   switch (lab.dtype) {
-    case 1:
-      hipLaunchKernelGGL((xent_head_kernel<1>), grid, dim3(256), smem, stream, H, M, D, W2, b2, C,
-                         lab, dlogits, dZ, inv_keep, relu_mask, loss_scale, loss_acc, correct_acc,
-                         hist_len, hist_step, ctr);
-      break;
-    case 2:
-      hipLaunchKernelGGL((xent_head_kernel<2>), grid, dim3(256), smem, stream, H, M, D, W2, b2, C,
-                         lab, dlogits, dZ, inv_keep, relu_mask, loss_scale, loss_acc, correct_acc,
-                         hist_len, hist_step, ctr);
-      break;
-    default:
-      hipLaunchKernelGGL((xent_head_kernel<3>), grid, dim3(256), smem, stream, H, M, D, W2, b2, C,
-                         lab, dlogits, dZ, inv_keep, relu_mask, loss_scale, loss_acc, correct_acc,
-                         hist_len, hist_step, ctr);
+    case 1: if (big) ARENA_HEAD(1, 16); else ARENA_HEAD(1, 8); break;
+    case 2: if (big) ARENA_HEAD(2, 16); else ARENA_HEAD(2, 8); break;
+    default: if (big) ARENA_HEAD(3, 16); else ARENA_HEAD(3, 8);
   }
+#undef ARENA_HEAD
   return hipGetLastError();
 }
 

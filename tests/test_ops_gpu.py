@@ -18,7 +18,7 @@ def _close(a, b, rtol=1e-4, atol=1e-5):
 def test_linear_fwd_f32(cuda, M, K, N, act):
     g = torch.Generator().manual_seed(M * 7 + K)
     x = torch.randn(M, K, generator=g).to(cuda)
-    W = (torch.randn(K, N, generator=g) * 0.1).to(cuda)
+    W = (torch.randn(N, K, generator=g) * 0.1).to(cuda)
     b = torch.randn(N, generator=g).to(cuda)
     Y = torch.empty(M, N, device=cuda)
     ops.linear_fwd(x, W, Y, b, act=act)
@@ -32,7 +32,7 @@ def test_linear_fwd_u8_gather_dropout(cuda):
     data = torch.randint(0, 256, (1000, 784), generator=g, dtype=torch.uint8).to(cuda)
     idx = torch.randperm(1000, generator=g).to(torch.int32).to(cuda)
     cursor = torch.tensor([7], dtype=torch.int64, device=cuda)
-    W = (torch.randn(784, 500, generator=g) * 0.05).to(cuda)
+    W = (torch.randn(500, 784, generator=g) * 0.05).to(cuda)
     b = torch.randn(500, generator=g).to(cuda)
     Y = torch.empty(100, 500, device=cuda)
     ops.linear_fwd(data, W, Y, b, x_scale=1 / 255.0, idx=idx, cursor=cursor, batch=100, act=1,
@@ -61,7 +61,7 @@ def test_dropout_hash_matches_reference(cuda):
 def test_xent_head(cuda, M, D, C):
     g = torch.Generator().manual_seed(D)
     H = torch.relu(torch.randn(M, D, generator=g)).to(cuda)
-    W2 = (torch.randn(D, C, generator=g) * 0.1).to(cuda)
+    W2 = (torch.randn(C, D, generator=g) * 0.1).to(cuda)
     b2 = torch.randn(C, generator=g).to(cuda)
     y = torch.randint(0, C, (M,), generator=g, dtype=torch.uint8).to(cuda)
     outs = {}
@@ -99,8 +99,8 @@ def test_wgrad_grouped(cuda, mode):
     dz2 = torch.randn(100, 10, generator=g).to(cuda)
     res = {}
     for impl in ("hip", "ref"):
-        W1 = (torch.randn(784, 500, generator=torch.Generator().manual_seed(1))).to(cuda)
-        W2 = (torch.randn(500, 10, generator=torch.Generator().manual_seed(2))).to(cuda)
+        W1 = (torch.randn(500, 784, generator=torch.Generator().manual_seed(1))).to(cuda)
+        W2 = (torch.randn(10, 500, generator=torch.Generator().manual_seed(2))).to(cuda)
         b1 = torch.zeros(500, device=cuda)
         b2 = torch.zeros(10, device=cuda)
         st = [torch.full_like(t, 0.01) for t in (W1, W2, b1, b2)] + \
@@ -175,12 +175,12 @@ def test_multi_tensor_flatten_roundtrip(cuda):
 def test_fused_linear_autograd(cuda):
     g = torch.Generator().manual_seed(0)
     x = torch.randn(64, 128, generator=g).to(cuda).requires_grad_(True)
-    W = (torch.randn(128, 32, generator=g) * 0.1).to(cuda).requires_grad_(True)
+    W = (torch.randn(32, 128, generator=g) * 0.1).to(cuda).requires_grad_(True)
     b = torch.randn(32, generator=g).to(cuda).requires_grad_(True)
     y = ops.fused_linear(x, W, b, act=1)
     (y * torch.arange(32, device=cuda)).sum().backward()
     x2, W2, b2 = (t.detach().clone().requires_grad_(True) for t in (x, W, b))
-    y2 = torch.relu(x2 @ W2 + b2)
+    y2 = torch.relu(x2 @ W2.t() + b2)
     (y2 * torch.arange(32, device=cuda)).sum().backward()
     _close(y, y2)
     _close(x.grad, x2.grad)

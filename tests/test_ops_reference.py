@@ -31,16 +31,16 @@ def test_mix32_known_values():
 def test_linear_and_wgrad_vs_autograd():
     g = torch.Generator().manual_seed(0)
     x = torch.randn(50, 64, generator=g)
-    W = torch.randn(64, 30, generator=g, requires_grad=True)
+    W = torch.randn(30, 64, generator=g, requires_grad=True)
     b = torch.randn(30, generator=g, requires_grad=True)
     Y = torch.empty(50, 30)
     ops.linear_fwd(x, W.detach(), Y, b.detach(), act=1)
-    yt = torch.relu(x @ W + b)
+    yt = torch.relu(x @ W.t() + b)
     torch.testing.assert_close(Y, yt.detach())
     up = torch.randn(50, 30, generator=g)
     yt.backward(up)
     dz = torch.where(Y > 0, up, torch.zeros_like(up))
-    gW = torch.empty(64, 30)
+    gW = torch.empty(30, 64)
     gb = torch.empty(30)
     ops.wgrad_grouped([x], [dz], [gW], [gb], x_scales=[1.0], gather=[False], mode=0)
     torch.testing.assert_close(gW, W.grad)
@@ -66,11 +66,11 @@ def test_adam_flat_matches_torch():
 def test_head_grad_vs_autograd():
     g = torch.Generator().manual_seed(2)
     H = torch.relu(torch.randn(20, 40, generator=g))
-    W2 = torch.randn(40, 10, generator=g, requires_grad=True)
+    W2 = torch.randn(10, 40, generator=g, requires_grad=True)
     b2 = torch.randn(10, generator=g)
     y = torch.randint(0, 10, (20,), generator=g)
     Ht = H.clone().requires_grad_(True)
-    loss = torch.nn.functional.cross_entropy(Ht @ W2 + b2, y)
+    loss = torch.nn.functional.cross_entropy(Ht @ W2.t() + b2, y)
     loss.backward()
     la, ca = torch.zeros(1), torch.zeros(1, dtype=torch.int32)
     dl, dz = torch.empty(20, 10), torch.empty(20, 40)
