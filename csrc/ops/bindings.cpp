@@ -88,6 +88,9 @@ ArenaRowSource make_src(const Tensor& x, double scale, const OptT& idx, const Op
     TORCH_CHECK(idx->numel() > 0, "idx must be non-empty");
     s.idx = idx->data_ptr<int>();
     s.idx_len = idx->numel();
+    TORCH_CHECK(logical_rows <= s.idx_len, name, ": batch rows (", logical_rows,
+                ") must not exceed the gather index length (", s.idx_len, ")");
+    TORCH_CHECK(batch >= 0, "batch must be >= 0");
     // Every index value must be a valid row: checked once on the host when the permutation is
     // installed (arena_amd/data/device_loader.py), not per launch (launches are graph-captured).
   } else {
@@ -160,6 +163,8 @@ void xent_head(Tensor H, Tensor W2, OptT b2, Tensor labels, OptT idx, OptT curso
   check_dev(correct_acc, "correct_acc");
   TORCH_CHECK(correct_acc.scalar_type() == torch::kInt32, "correct_acc must be int32");
   TORCH_CHECK(loss_acc.numel() == correct_acc.numel() && loss_acc.numel() >= 1, "acc sizes");
+  TORCH_CHECK((loss_acc.numel() & (loss_acc.numel() - 1)) == 0,
+              "metric history length must be a power of two");
   TORCH_CHECK(labels.scalar_type() != torch::kFloat32, "labels must be integer");
   ArenaRowSource lab = make_src(labels, 1.0, idx, cursor, batch, M, "labels");
   ArenaCounterOp ctr{};

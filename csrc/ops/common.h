@@ -27,6 +27,36 @@ __device__ __forceinline__ f32x4 mfma_16x16x4(float a, float b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// Full-wave reductions without LDS round trips: DPP quad_perm (xor 1, xor 2) and row_ror (4, 8)
+// inside each 16-lane row, ds_swizzle xor 16 across row pairs, then two v_readlane for the
+// halves. Result is wave-uniform. (The __shfl_xor form is 6 dependent ds_bpermute_b32.)
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float swz_xor16(float v) {
+  // ds_swizzle bit-mode: offset = xor_mask<<10 | or_mask<<5 | and_mask  (within 32-lane halves)
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(v), (0x10 << 10) | 0x1F));
+}
+__device__ __forceinline__ float wave_sum_fast(float v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x124>(v);  // row_ror:4
+  v += dpp_f<0x128>(v);  // row_ror:8
+  v += swz_xor16(v);
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)) +
+         __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+}
+__device__ __forceinline__ float wave_max_fast(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x124>(v));
+  v = fmaxf(v, dpp_f<0x128>(v));
+  v = fmaxf(v, swz_xor16(v));
+  return fmaxf(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0)),
+               __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32)));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

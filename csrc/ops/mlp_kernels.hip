@@ -85,14 +85,36 @@ __device__ __forceinline__ void adam_apply(const AdamCoef& c, float g, float& p,
   p -= c.step_size * m / (sqrtf(v) * c.inv_sqrt_bc2 + c.eps);
 }
 
-// Data cursor (wave-uniform scalar load) and the gathered physical row of logical row r.
-__device__ __forceinline__ long long row_cursor(const ArenaRowSource& s) {
-  return (s.cursor ? *s.cursor : 0) + s.cursor_off;
+// Batch gather: logical row r of this step -> dataset row idx[(cursor*batch + r) % len]. The
+// 64-bit modulo (a ~100-instruction software routine on CDNA) is done ONCE per wave on the
+// wave-uniform base; per row it is one add + one conditional subtract (host guarantees r < len).
+// x mod n for 0 <= x < 2^53 (exact in fp64) and 0 < n < 2^31 via fp64 division + correction:
+// branch-free, unlike the ~100-instruction 64-bit integer division routine.
+__device__ __forceinline__ long long mod_fp64(double x, long long n) {
+  const double dn = (double)n;
+  double r = x - floor(x / dn) * dn;
+  r = (r < 0.0) ? r + dn : r;
+  r = (r >= dn) ? r - dn : r;
+  return (long long)r;
 }
-__device__ __forceinline__ long long gather_row(const ArenaRowSource& s, long long cur,
-                                                long long r) {
-  if (s.idx == nullptr) return r;
-  return (long long)s.idx[(cur * (long long)s.batch + r) % s.idx_len];
+
+struct Gather {
+  const int* idx;
+  long long base, len;
+};
+__device__ __forceinline__ Gather make_gather(const ArenaRowSource& s) {
+  Gather gt{s.idx, 0, s.idx_len};
+  if (s.idx != nullptr) {
+    const long long cur = (s.cursor ? *s.cursor : 0) + s.cursor_off;
+    gt.base = mod_fp64((double)cur * (double)s.batch, s.idx_len);
+  }
+  return gt;
+}
+__device__ __forceinline__ int gather_row(const Gather& gt, int r) {
+  if (gt.idx == nullptr) return r;
+  long long p = gt.base + r;
+  p = (p >= gt.len) ? p - gt.len : p;
+  return gt.idx[p];
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -114,9 +136,9 @@ __global__ __launch_bounds__(WAVES * 64) void linear_fwd_kernel(
   const int g = lane >> 4, c = lane & 15;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
   const int rowc = min(m0 + c, M - 1), colc = min(n0 + c, N - 1);
-  const long long cur = row_cursor(src);
+  const Gather gt = make_gather(src);
   const uint32_t step = step_src ? (uint32_t)(*step_src) : 0u;  // early: off the epilogue's path
-  const long long prow = gather_row(src, cur, rowc);
+  const long long prow = gather_row(gt, rowc);
   const float* wrow = W + (long long)colc * K;
   const int nsteps = (K + 15) >> 4;
   const int s0 = (nsteps * w) / WAVES, s1 = (nsteps * (w + 1)) / WAVES;
@@ -182,113 +204,121 @@ constexpr int kHeadMaxT = 16;  // hidden <= 1024
 constexpr int kHeadMaxC = 16;  // classes <= 16
 constexpr int kHeadStage = 16; // max float4 staging loads per thread (D*C <= 16384)
 
-template <int LT, int STAGE>
+// CB/TB: compile-time bounds on classes and hidden/64 so the inner loops are straight-line code
+// (runtime C/D guards become selects on clamped LDS addresses, not branches).
+template <int LT, int STAGE, int CB, int TB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void xent_head_kernel(
     const float* __restrict__ H, int M, int D, const float* __restrict__ W2,
     const float* __restrict__ b2, int C, ArenaRowSource lab, float* __restrict__ dlogits,
     float* __restrict__ dZ, float inv_keep, int relu_mask, float loss_scale,
     float* __restrict__ loss_acc, int* __restrict__ correct_acc, int hist_len,
     const long long* hist_step, ArenaCounterOp ctr) {
-  extern __shared__ __attribute__((aligned(16))) float ws[];  // [C][D]
+  extern __shared__ __attribute__((aligned(16))) float ws[];  // [C][D] + one dummy float4
   const int lane = lane_id();
   const int r = blockIdx.x * 4 + wave_id();
   const int rc = min(r, M - 1);
   // (1) issue every independent global load up front
-  const long long cur = row_cursor(lab);
-  const long long pr = gather_row(lab, cur, rc);
+  const long long pr = gather_row(make_gather(lab), rc);
   int y;
   if constexpr (LT == 1) y = (int)static_cast<const uint8_t*>(lab.ptr)[pr];
   else if constexpr (LT == 2) y = static_cast<const int*>(lab.ptr)[pr];
   else y = (int)static_cast<const long long*>(lab.ptr)[pr];
-  float h[kHeadMaxT];
+  float h[TB];
 #pragma unroll
-  for (int t = 0; t < kHeadMaxT; ++t) h[t] = H[(long long)rc * D + min(lane + 64 * t, D - 1)];
+  for (int t = 0; t < TB; ++t) h[t] = H[(long long)rc * D + min(lane + 64 * t, D - 1)];
   const int n4 = (D * C) >> 2;  // host guarantees (D*C) % 4 == 0
   float4 st[STAGE];
 #pragma unroll
   for (int i = 0; i < STAGE; ++i)
     st[i] = reinterpret_cast<const float4*>(W2)[min((int)threadIdx.x + 256 * i, n4 - 1)];
-  float bb[kHeadMaxC];
-#pragma unroll
-  for (int cc = 0; cc < kHeadMaxC; ++cc) bb[cc] = b2 ? b2[min(cc, C - 1)] : 0.f;
+  // b2: one vector load (lane cc holds b2[cc]); broadcast later with readlane (no scalar chain)
+  const float bl = b2 ? b2[min(lane, C - 1)] : 0.f;
   const long long hs = hist_step ? *hist_step : 0;
-  // (2) stage, bookkeeping
-  // unconditional stores (out-of-range items go to a dummy slot at ws[4*n4]): a store guarded by
-  // a branch lets hipcc sink each load into the branch and wait for it there, serialising them.
+  // (2) stage W2; unconditional stores (out-of-range items go to the dummy slot ws[4*n4]): a
+  //     store guarded by a branch lets hipcc sink each load into it and wait there, serialising.
 #pragma unroll
   for (int i = 0; i < STAGE; ++i) {
     const int q = threadIdx.x + 256 * i;
     reinterpret_cast<float4*>(ws)[q < n4 ? q : n4] = st[i];
   }
   counter_op(ctr);
-  const int slot = hist_len > 1 ? (int)(hs % hist_len) : 0;
+  const int hmask = hist_len - 1;  // hist_len is a power of two (host-checked)
+  const int slot = (int)hs & hmask;
   if (hist_len > 1 && blockIdx.x == 0 && threadIdx.x == 0) {
-    const int nxt = (int)((hs + 1) % hist_len);
+    const int nxt = (int)(hs + 1) & hmask;
     loss_acc[nxt] = 0.f;
     correct_acc[nxt] = 0;
   }
   __syncthreads();
   if (r >= M) return;
+  int jo[TB];  // clamped LDS column per t; h zeroed past D
 #pragma unroll
-  for (int t = 0; t < kHeadMaxT; ++t) h[t] = (lane + 64 * t < D) ? h[t] : 0.f;
+  for (int t = 0; t < TB; ++t) {
+    const int j = lane + 64 * t;
+    jo[t] = min(j, D - 1);
+    h[t] = (j < D) ? h[t] : 0.f;
+  }
 
   // (3) logits: per-lane partial dot products, then 64-lane reductions (independent chains)
-  float lg[kHeadMaxC];
+  float lg[CB];
 #pragma unroll
-  for (int cc = 0; cc < kHeadMaxC; ++cc) {
+  for (int cc = 0; cc < CB; ++cc) {
+    const float* wr = ws + min(cc, C - 1) * D;
     float s = 0.f;
-    if (cc < C) {
 #pragma unroll
-      for (int t = 0; t < kHeadMaxT; ++t) {
-        const int j = lane + 64 * t;
-        if (j < D) s += h[t] * ws[cc * D + j];
-      }
-    }
+    for (int t = 0; t < TB; ++t) s += h[t] * wr[jo[t]];
     lg[cc] = s;
   }
 #pragma unroll
-  for (int cc = 0; cc < kHeadMaxC; ++cc) lg[cc] = (cc < C) ? wave_sum(lg[cc]) + bb[cc] : -INFINITY;
+  for (int cc = 0; cc < CB; ++cc) {  // all CB reductions unconditional -> interleaved DPP chains
+    const float tot = wave_sum_fast(lg[cc]) +
+                      __int_as_float(__builtin_amdgcn_readlane(__float_as_int(bl), cc));
+    lg[cc] = (cc < C) ? tot : -INFINITY;
+  }
   float mx = lg[0];
   int arg = 0;
 #pragma unroll
-  for (int cc = 1; cc < kHeadMaxC; ++cc)
-    if (cc < C && lg[cc] > mx) { mx = lg[cc]; arg = cc; }
+  for (int cc = 1; cc < CB; ++cc) {
+    const bool gt = lg[cc] > mx;
+    mx = gt ? lg[cc] : mx;
+    arg = gt ? cc : arg;
+  }
   float se = 0.f;
 #pragma unroll
-  for (int cc = 0; cc < kHeadMaxC; ++cc)
-    if (cc < C) se += expf(lg[cc] - mx);
+  for (int cc = 0; cc < CB; ++cc) se += (cc < C) ? expf(lg[cc] - mx) : 0.f;
   const float lse = mx + logf(se);
   float ly = 0.f;
 #pragma unroll
-  for (int cc = 0; cc < kHeadMaxC; ++cc) ly = (cc == y) ? lg[cc] : ly;
+  for (int cc = 0; cc < CB; ++cc) ly = (cc == y) ? lg[cc] : ly;
   if (lane == 0) {
     atomicAdd(&loss_acc[slot], (lse - ly) * loss_scale);
     atomicAdd(&correct_acc[slot], arg == y ? 1 : 0);
   }
   if (dlogits == nullptr) return;
 
-  float gcl[kHeadMaxC];
+  float gcl[CB];
 #pragma unroll
-  for (int cc = 0; cc < kHeadMaxC; ++cc)
+  for (int cc = 0; cc < CB; ++cc)
     gcl[cc] = (cc < C) ? (expf(lg[cc] - lse) - (cc == y ? 1.f : 0.f)) * loss_scale : 0.f;
   if (lane < C) {
     float v = 0.f;
 #pragma unroll
-    for (int cc = 0; cc < kHeadMaxC; ++cc) v = (cc == lane) ? gcl[cc] : v;
+    for (int cc = 0; cc < CB; ++cc) v = (cc == lane) ? gcl[cc] : v;
     dlogits[(long long)r * C + lane] = v;
   }
   if (dZ == nullptr) return;
+  float o[TB];
 #pragma unroll
-  for (int t = 0; t < kHeadMaxT; ++t) {
+  for (int t = 0; t < TB; ++t) {
+    float s = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < CB; ++cc) s += gcl[cc] * ws[min(cc, C - 1) * D + jo[t]];
+    o[t] = relu_mask ? ((h[t] > 0.f) ? s * inv_keep : 0.f) : s;
+  }
+#pragma unroll
+  for (int t = 0; t < TB; ++t) {
     const int j = lane + 64 * t;
-    if (j < D) {
-      float s = 0.f;
-#pragma unroll
-      for (int cc = 0; cc < kHeadMaxC; ++cc)
-        if (cc < C) s += gcl[cc] * ws[cc * D + j];
-      if (relu_mask) s = (h[t] > 0.f) ? s * inv_keep : 0.f;
-      dZ[(long long)r * D + j] = s;
-    }
+    if (j < D) dZ[(long long)r * D + j] = o[t];
   }
 }
 
@@ -327,7 +357,7 @@ __device__ __forceinline__ void lds_barrier() {
 }
 
 template <int XT>
-__device__ __forceinline__ void load_x_items(const ArenaWGradProblem& P, long long cur, int mc0,
+__device__ __forceinline__ void load_x_items(const ArenaWGradProblem& P, const Gather& gt, int mc0,
                                              int mcn, int k0, float4 (&v)[kXItems]) {
   // 16 items per row, item q = 4 consecutive k (one u32 of u8 pixels or one float4). Rows past
   // mcn re-read row mcn-1 (finite data; their A operand is zeroed in the K-loop).
@@ -335,7 +365,7 @@ __device__ __forceinline__ void load_x_items(const ArenaWGradProblem& P, long lo
 #pragma unroll
   for (int i = 0; i < kXItems; ++i) {
     const int t = threadIdx.x + 256 * i;
-    prow[i] = (int)gather_row(P.x, cur, mc0 + min(t >> 4, mcn - 1));
+    prow[i] = gather_row(gt, mc0 + min(t >> 4, mcn - 1));
   }
 #pragma unroll
   for (int i = 0; i < kXItems; ++i) {
@@ -365,7 +395,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
   const int kkc = min(kk, P.K - 1);
   const bool bias_wave = (tk == 0) && (w == 0);
   const bool has_bias = P.mode == 1 ? P.pB != nullptr : P.gB != nullptr;
-  const long long cur = row_cursor(P.x);
+  const Gather gt = make_gather(P.x);
   const bool zvec = (P.N & 3) == 0;
   AdamCoef co{};
   if (P.mode == 1) co = adam_coef(args.adam);  // t / lr loads issued first, off the epilogue path
@@ -377,8 +407,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
     const int mcn = min(kMC, P.M - mc0);
     // (1) issue the chunk's loads: gathered X items, the dZ slice [m][16 n]
     float4 xv[kXItems];
-    if (P.xt == 1) load_x_items<1>(P, cur, mc0, mcn, k0, xv);
-    else load_x_items<0>(P, cur, mc0, mcn, k0, xv);
+    if (P.xt == 1) load_x_items<1>(P, gt, mc0, mcn, k0, xv);
+    else load_x_items<0>(P, gt, mc0, mcn, k0, xv);
     float4 zv[kZItems];
 #pragma unroll
     for (int i = 0; i < kZItems; ++i) {
@@ -541,10 +571,10 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   const float* x = logits + (long long)r * C;
   float mx = -INFINITY;
   for (int cc = lane; cc < C; cc += 64) mx = fmaxf(mx, x[cc]);
-  mx = wave_max(mx);
+  mx = wave_max_fast(mx);
   float se = 0.f;
   for (int cc = lane; cc < C; cc += 64) se += expf(x[cc] - mx);
-  se = wave_sum(se);
+  se = wave_sum_fast(se);
   const float lse = mx + logf(se);
   const long long y = labels[r];
   if (lane == 0) loss[r] = lse - x[y];
@@ -623,15 +653,21 @@ hipError_t arena_xent_head(const float* H, int M, int D, const float* W2, const 
   dim3 grid((M + 3) / 4);
   const size_t smem = sizeof(float) * ((size_t)D * C + 4);  // + dummy float4 slot
   const bool big = D * C > 1024 * 8;
-#define ARENA_HEAD(LT, ST)                                                                      \
-  hipLaunchKernelGGL((xent_head_kernel<LT, ST>), grid, dim3(256), smem, stream, H, M, D, W2, b2, \
-                     C, lab, dlogits, dZ, inv_keep, relu_mask, loss_scale, loss_acc,             \
+  const bool small = C <= 10 && D <= 512 && !big;
+#define ARENA_HEAD(LT, ST, CB, TB)                                                               \
+  hipLaunchKernelGGL((xent_head_kernel<LT, ST, CB, TB>), grid, dim3(256), smem, stream, H, M, D, \
+                     W2, b2, C, lab, dlogits, dZ, inv_keep, relu_mask, loss_scale, loss_acc,     \
                      correct_acc, hist_len, hist_step, ctr)
+#define ARENA_HEAD_LT(LT)                \
+  if (small) ARENA_HEAD(LT, 8, 10, 8);   \
+  else if (big) ARENA_HEAD(LT, 16, 16, 16); \
+  else ARENA_HEAD(LT, 8, 16, 16);
   switch (lab.dtype) {
-    case 1: if (big) ARENA_HEAD(1, 16); else ARENA_HEAD(1, 8); break;
-    case 2: if (big) ARENA_HEAD(2, 16); else ARENA_HEAD(2, 8); break;
-    default: if (big) ARENA_HEAD(3, 16); else ARENA_HEAD(3, 8);
+    case 1: ARENA_HEAD_LT(1) break;
+    case 2: ARENA_HEAD_LT(2) break;
+    default: ARENA_HEAD_LT(3)
   }
+#undef ARENA_HEAD_LT
 #undef ARENA_HEAD
   return hipGetLastError();
 }
