@@ -10,12 +10,13 @@ Execution design:
     single launch -- no flatten/unflatten copies, no per-tensor launches.
   * The training set lives in HBM as uint8; the batch gather (permutation + device step counter)
     and the /255 dequantisation are fused into the first GEMM and the loss head.
-  * One step = 3 launches on one GPU (linear_fwd -> xent_head -> wgrad_grouped with fused Adam);
-    with data parallelism 5 (grad bucket -> all_reduce -> adam_flat).
+  * One step = 2 launches on one GPU: mlp_fwd_head (hidden layer + loss head, last-arriver
+    softmax) -> wgrad_grouped (dz recomputed in-kernel from dlogits, both layers' dW, fused Adam);
+    with data parallelism: mlp_fwd_head -> wgrad (grad bucket) -> all_reduce -> adam_flat.
   * Every per-step scalar (data cursor, Adam t, dropout step, metric slot) is a device counter, so
     ``steps_per_graph`` consecutive steps are captured into ONE hipGraph and replayed.
 Step-counter protocol (no intra-kernel races): A = completed steps, B = current Adam t.
-  linear_fwd reads A; xent_head reads A and writes B=A+1; wgrad reads B (cursor = B-1);
+  mlp_fwd_head reads A and writes B=A+1; wgrad reads B (cursor = B-1);
   the last kernel of the step (wgrad with fused Adam, or adam_flat) writes A=B.
 """
 from __future__ import annotations
@@ -105,8 +106,9 @@ class FusedMLPTrainer:
             self.gW2, self.gb2 = L.view(self.G, "W2"), L.view(self.G, "b2")
         B = cfg.batch
         self.Hbuf = torch.empty(B, H, device=dev)
-        self.dZ = torch.empty(B, H, device=dev)
         self.dlogits = torch.empty(B, C, device=dev)
+        self.W2snap = torch.empty(C, H, device=dev)
+        self.slabs, self.counters = ops.mlp_fwd_head_workspace(B, H, C, dev)
         self.ctrA = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ctrB = torch.zeros(1, dtype=torch.int64, device=dev)
         self.loss_hist = torch.zeros(cfg.hist_len, device=dev)
@@ -170,25 +172,38 @@ class FusedMLPTrainer:
             for part in range(3):
                 self._launch_step_part(part)
             return
-        cfg = self.cfg
-        B = cfg.batch
-        A, Bc = self.ctrA, self.ctrB
-        ops.linear_fwd(self.train_x, self.W1, self.Hbuf, self.b1, x_scale=1.0 / 255.0,
-                       idx=self.perm, cursor=A, batch=B, act=1, keep_prob=cfg.keep_prob,
-                       seed=cfg.seed * 2654435761 + self.rank, step=A)
-        ops.xent_head(self.Hbuf, self.W2, self.b2, self.train_y, loss_acc=self.loss_hist,
-                      correct_acc=self.corr_hist, idx=self.perm, cursor=A, batch=B,
-                      dlogits=self.dlogits, dZ=self.dZ, keep_prob=cfg.keep_prob, relu_mask=True,
-                      loss_scale=1.0 / B, hist_step=A, ctr_dst=Bc, ctr_src=A, ctr_add=1)
+        self._launch_fwd_head()
+        self._launch_wgrad(adam=True)
+
+    def _launch_fwd_head(self):
+        cfg, B, A, Bc = self.cfg, self.cfg.batch, self.ctrA, self.ctrB
+        ops.mlp_fwd_head(self.train_x, self.W1, self.b1, self.Hbuf, self.W2, self.b2,
+                         self.train_y, slabs=self.slabs, counters=self.counters,
+                         loss_acc=self.loss_hist, correct_acc=self.corr_hist,
+                         dlogits=self.dlogits, W2_copy=self.W2snap, x_scale=1.0 / 255.0,
+                         idx=self.perm, cursor=A, batch=B, keep_prob=cfg.keep_prob,
+                         seed=cfg.seed * 2654435761 + self.rank, step=A, loss_scale=1.0 / B,
+                         hist_step=A, ctr_dst=Bc, ctr_src=A, ctr_add=1)
+
+    def _launch_wgrad(self, adam: bool):
+        """dW1 (dz recomputed from dlogits, W2 snapshot and the H mask) and dW2 in one launch;
+        with ``adam`` the update is applied in the epilogue, else grads go to the flat bucket."""
+        cfg, B, A, Bc = self.cfg, self.cfg.batch, self.ctrA, self.ctrB
         common = dict(x_scales=[1.0 / 255.0, 1.0], gather=[True, False], idx=self.perm,
-                      cursor=Bc, cursor_off=-1, batch=B)
-        adam = dict(lr=cfg.lr, lr_t=self.lr_t, betas=cfg.betas, eps=cfg.eps, t_step=Bc,
-                    tf_style=cfg.tf_adam)
-        ops.wgrad_grouped([self.train_x, self.Hbuf], [self.dZ, self.dlogits],
-                          [self.W1, self.W2], [self.b1, self.b2], mode=1,
-                          mW=[self.mW1, self.mW2], vW=[self.vW1, self.vW2],
-                          mB=[self.mb1, self.mb2], vB=[self.vb1, self.vb2],
-                          ctr_dst=A, ctr_src=Bc, ctr_add=0, **common, **adam)
+                      cursor=Bc, cursor_off=-1, batch=B,
+                      head=[(self.dlogits, self.W2snap, self.Hbuf), None],
+                      head_keep_prob=cfg.keep_prob)
+        xs, dzs = [self.train_x, self.Hbuf], [None, self.dlogits]
+        if adam:
+            ops.wgrad_grouped(xs, dzs, [self.W1, self.W2], [self.b1, self.b2], mode=1,
+                              mW=[self.mW1, self.mW2], vW=[self.vW1, self.vW2],
+                              mB=[self.mb1, self.mb2], vB=[self.vb1, self.vb2],
+                              lr=cfg.lr, lr_t=self.lr_t, betas=cfg.betas, eps=cfg.eps,
+                              t_step=Bc, tf_style=cfg.tf_adam, ctr_dst=A, ctr_src=Bc, ctr_add=0,
+                              **common)
+        else:
+            ops.wgrad_grouped(xs, dzs, [self.gW1, self.gW2], [self.gb1, self.gb2], mode=0,
+                              grad_scale=1.0, **common)
 
     def _capture(self, nsteps: int) -> torch.cuda.CUDAGraph:
         g = torch.cuda.CUDAGraph()
@@ -251,20 +266,10 @@ class FusedMLPTrainer:
 
     def _launch_step_part(self, part: int):
         """DP step in three parts: 0 = compute up to the grad bucket, 1 = all_reduce, 2 = Adam."""
-        cfg, B, A, Bc = self.cfg, self.cfg.batch, self.ctrA, self.ctrB
+        cfg, A, Bc = self.cfg, self.ctrA, self.ctrB
         if part == 0:
-            ops.linear_fwd(self.train_x, self.W1, self.Hbuf, self.b1, x_scale=1.0 / 255.0,
-                           idx=self.perm, cursor=A, batch=B, act=1, keep_prob=cfg.keep_prob,
-                           seed=cfg.seed * 2654435761 + self.rank, step=A)
-            ops.xent_head(self.Hbuf, self.W2, self.b2, self.train_y, loss_acc=self.loss_hist,
-                          correct_acc=self.corr_hist, idx=self.perm, cursor=A, batch=B,
-                          dlogits=self.dlogits, dZ=self.dZ, keep_prob=cfg.keep_prob,
-                          relu_mask=True, loss_scale=1.0 / B, hist_step=A, ctr_dst=Bc, ctr_src=A,
-                          ctr_add=1)
-            ops.wgrad_grouped([self.train_x, self.Hbuf], [self.dZ, self.dlogits],
-                              [self.gW1, self.gW2], [self.gb1, self.gb2], mode=0, grad_scale=1.0,
-                              x_scales=[1.0 / 255.0, 1.0], gather=[True, False], idx=self.perm,
-                              cursor=Bc, cursor_off=-1, batch=B)
+            self._launch_fwd_head()
+            self._launch_wgrad(adam=False)
         elif part == 1:
             import torch.distributed as dist
             dist.all_reduce(self.G, group=self.pg)

@@ -115,6 +115,22 @@ def xent_head(H, W2, b2, labels, idx, cursor, batch, dlogits, dZ, keep_prob, rel
     dZ.view(M, -1).copy_(dz)
 
 
+def mlp_fwd_head(x, x_scale, idx, cursor, batch, W1, b1, H, keep_prob, seed, step, W2, b2, labels,
+                 slabs, counters, dlogits, W2_copy, loss_scale, loss_acc, correct_acc, hist_step,
+                 ctr_dst, ctr_src, ctr_add):
+    """Reference for the head-fused forward: linear_fwd + xent_head (no slab workspace needed)."""
+    if ctr_dst is not None:
+        src = int(ctr_src.reshape(-1)[0].item()) if ctr_src is not None else 0
+        ctr_new = src + ctr_add
+    linear_fwd(x, x_scale, idx, cursor, batch, W1, b1, H, 1, keep_prob, seed, step)
+    if W2_copy is not None:
+        W2_copy.view_as(W2).copy_(W2)
+    xent_head(H, W2, b2, labels, idx, cursor, batch, dlogits, None, keep_prob, True, loss_scale,
+              loss_acc, correct_acc, hist_step, None, None, 0)
+    if ctr_dst is not None:
+        ctr_dst.fill_(ctr_new)
+
+
 def adam_update(p, m, v, g, lr, b1, b2, eps, wd, t, grad_scale, tf_style):
     """In-place Adam on tensors (fp32), same formula as adam_apply in mlp_kernels.hip."""
     g = g * grad_scale + wd * p
@@ -129,15 +145,23 @@ def adam_update(p, m, v, g, lr, b1, b2, eps, wd, t, grad_scale, tf_style):
         p.sub_((lr / bc1) * m / (v.sqrt() / math.sqrt(bc2) + eps))
 
 
-def wgrad_grouped(xs, x_scales, gather, idx, cursor, cursor_off, batch, dzs, mode, outW, outB, mW,
-                  vW, mB, vB, lr, lr_t, b1, b2, eps, wd, t_step, grad_scale, tf_style, ctr_dst,
-                  ctr_src, ctr_add):
+def head_dz(dl, w2, h, keep_prob):
+    """dz = (dlogits · W2) ⊙ (h > 0) / keep -- ReLU + dropout backward through the head."""
+    dz = dl @ w2
+    inv_keep = 1.0 / keep_prob
+    return torch.where(h > 0, dz * inv_keep, torch.zeros_like(dz))
+
+
+def wgrad_grouped(xs, x_scales, gather, idx, cursor, cursor_off, batch, dzs, hd_dl, hd_w2, hd_h,
+                  hd_keep_prob, Ms, mode, outW, outB, mW, vW, mB, vB, lr, lr_t, b1, b2, eps, wd,
+                  t_step, grad_scale, tf_style, ctr_dst, ctr_src, ctr_add):
     t = int(t_step.reshape(-1)[0].item()) if t_step is not None else 1
     lr_v = float(lr_t.reshape(-1)[0].item()) if lr_t is not None else lr
     pending = []
     for i in range(len(xs)):
-        dz = dzs[i]
-        M = dz.shape[0]
+        dz = dzs[i] if dzs[i] is not None else head_dz(hd_dl[i], hd_w2[i], hd_h[i], hd_keep_prob)
+        M = Ms[i] if Ms[i] > 0 else dz.shape[0]
+        dz = dz[:M]
         if gather[i]:
             xr = gather_rows(xs[i], idx, cursor, batch, M, cursor_off)
         else:

@@ -42,13 +42,34 @@ struct ArenaAdam {
 struct ArenaWGradProblem {
   ArenaRowSource x;       // rows m of the layer input
   int xt;                 // 0 f32, 1 u8
-  const float* dz;        // [M][N] upstream gradient
+  const float* dz;        // [M][N] upstream gradient (null when recomputed from the head below)
+  // dz recomputed in-kernel from the softmax head (fused MLP step):
+  //   dz[m][n] = (Σ_c hd_dl[m][c] * hd_w2[c][n]) * (hd_h[m][n] > 0 ? hd_inv_keep : 0)
+  const float* hd_dl;     // [M][hd_c] dlogits
+  const float* hd_w2;     // [hd_c][N] next-layer weight
+  const float* hd_h;      // [M][N] this layer's (post-dropout) activation, for the ReLU/drop mask
+  int hd_c;
+  float hd_inv_keep;
   int M, K, N;
   int mode;               // 0: write grad (scaled), 1: Adam in place
   float* gW; float* gB;   // mode 0 outputs ([K][N], [N]); gB may be null
   float* pW; float* mW; float* vW;  // mode 1
   float* pB; float* mB; float* vB;
   int tiles_k, tiles_n, block_begin;
+};
+
+// Fused forward + loss head of a 1-hidden-layer MLP (mlp_fwd_head).
+struct ArenaFwdHead {
+  const float* W2;        // [C][N] output layer
+  const float* b2;        // [C]
+  int C;
+  ArenaRowSource lab;     // labels (same gather as x)
+  float* slabs;           // workspace [mtiles][ntiles][16][C] partial logits
+  int* counters;          // workspace [mtiles], zero-initialised once; reset by the last arriver
+  float* dlogits;         // [M][C] out (null: metrics only)
+  float* W2_copy;         // optional [C][N] snapshot of W2 (backward reads it while Adam updates W2)
+  float loss_scale;
+  float* loss_acc; int* correct_acc; int hist_len; const long long* hist_step;
 };
 
 }  // extern "C"

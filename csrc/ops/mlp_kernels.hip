@@ -376,10 +376,13 @@ __device__ __forceinline__ void load_x_items(const ArenaWGradProblem& P, const G
   }
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) void wgrad_grouped_kernel(
+// >= 2 waves/SIMD: 424 workgroups x 4 waves must be co-resident in ONE round on 1024 SIMDs.
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void wgrad_grouped_kernel(
     WGradArgs args) {
   __shared__ __attribute__((aligned(16))) float Xs[kMC * kXsStride];
   __shared__ __attribute__((aligned(16))) float Zs[kMC * 16];
+  __shared__ __attribute__((aligned(16))) float Ds[kMC * 16];  // head dlogits rows [m][c]
+  __shared__ __attribute__((aligned(16))) float W2s[16 * 16];  // head W2 slice [c][n]
   counter_op(args.ctr);
   int pi = 0;
 #pragma unroll
@@ -397,6 +400,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
   const bool has_bias = P.mode == 1 ? P.pB != nullptr : P.gB != nullptr;
   const Gather gt = make_gather(P.x);
   const bool zvec = (P.N & 3) == 0;
+  const bool head = P.hd_dl != nullptr;  // host: head mode requires N % 4 == 0
   AdamCoef co{};
   if (P.mode == 1) co = adam_coef(args.adam);  // t / lr loads issued first, off the epilogue path
 
@@ -405,23 +409,45 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
   float pw[4], mw[4], vw[4], pb[4], mb[4], vb[4];
   for (int mc0 = 0; mc0 < P.M; mc0 += kMC) {
     const int mcn = min(kMC, P.M - mc0);
-    // (1) issue the chunk's loads: gathered X items, the dZ slice [m][16 n]
+    // (1) issue the chunk's loads: gathered X items; the dZ slice [m][16 n] -- or, in head mode,
+    //     the mask slice of H plus the dlogits rows and the W2 slice it is recomputed from
     float4 xv[kXItems];
     if (P.xt == 1) load_x_items<1>(P, gt, mc0, mcn, k0, xv);
     else load_x_items<0>(P, gt, mc0, mcn, k0, xv);
     float4 zv[kZItems];
+    constexpr int kDItems = (kMC * 16) / 256;
+    float dv[kDItems];
+    float wv = 0.f;
+    if (!head) {
 #pragma unroll
-    for (int i = 0; i < kZItems; ++i) {
-      const int t = threadIdx.x + 256 * i;
-      const int rr = min(t >> 2, mcn - 1), q = t & 3;
-      const int n = n0 + 4 * q;
-      const float* srcp = P.dz + (long long)(mc0 + rr) * P.N;
-      if (zvec) {
-        zv[i] = *reinterpret_cast<const float4*>(srcp + min(n, P.N - 4));
-      } else {
-        zv[i] = make_float4(srcp[min(n, P.N - 1)], srcp[min(n + 1, P.N - 1)],
-                            srcp[min(n + 2, P.N - 1)], srcp[min(n + 3, P.N - 1)]);
+      for (int i = 0; i < kZItems; ++i) {
+        const int t = threadIdx.x + 256 * i;
+        const int rr = min(t >> 2, mcn - 1), q = t & 3;
+        const int n = n0 + 4 * q;
+        const float* srcp = P.dz + (long long)(mc0 + rr) * P.N;
+        if (zvec) {
+          zv[i] = *reinterpret_cast<const float4*>(srcp + min(n, P.N - 4));
+        } else {
+          zv[i] = make_float4(srcp[min(n, P.N - 1)], srcp[min(n + 1, P.N - 1)],
+                              srcp[min(n + 2, P.N - 1)], srcp[min(n + 3, P.N - 1)]);
+        }
       }
+    } else {
+      const int C = P.hd_c;
+#pragma unroll
+      for (int i = 0; i < kZItems; ++i) {  // mask source (post-dropout activation)
+        const int t = threadIdx.x + 256 * i;
+        const int rr = min(t >> 2, mcn - 1), q = t & 3;
+        zv[i] = *reinterpret_cast<const float4*>(P.hd_h + (long long)(mc0 + rr) * P.N +
+                                                 min(n0 + 4 * q, P.N - 4));
+      }
+#pragma unroll
+      for (int i = 0; i < kDItems; ++i) {  // dlogits rows: item t -> (m = t>>4, c = t&15)
+        const int t = threadIdx.x + 256 * i;
+        dv[i] = P.hd_dl[(long long)(mc0 + min(t >> 4, mcn - 1)) * C + min(t & 15, C - 1)];
+      }
+      wv = P.hd_w2[(long long)min((int)threadIdx.x >> 4, C - 1) * P.N +
+                   min(n0 + ((int)threadIdx.x & 15), P.N - 1)];
     }
     // (2) on the first chunk, prefetch the tile's Adam state behind them (in-order vmcnt lets the
     //     staging waits below leave these in flight through the K-loop)
@@ -447,24 +473,59 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
       const float4 o = (k0 + 4 * q < P.K) ? xv[i] : make_float4(0.f, 0.f, 0.f, 0.f);
       *reinterpret_cast<float4*>(&Xs[rr * kXsStride + 4 * q]) = o;
     }
+    if (head) {
+      const int C = P.hd_c;
 #pragma unroll
-    for (int i = 0; i < kZItems; ++i) {
-      const int t = threadIdx.x + 256 * i;
-      const int rr = t >> 2, q = t & 3;
-      const int n = n0 + 4 * q;
-      float4 o = zv[i];
-      o.x = (n + 0 < P.N) ? o.x : 0.f;
-      o.y = (n + 1 < P.N) ? o.y : 0.f;
-      o.z = (n + 2 < P.N) ? o.z : 0.f;
-      o.w = (n + 3 < P.N) ? o.w : 0.f;
-      if (rr >= mcn) o = make_float4(0.f, 0.f, 0.f, 0.f);
-      *reinterpret_cast<float4*>(&Zs[rr * 16 + 4 * q]) = o;
+      for (int i = 0; i < kDItems; ++i) {
+        const int t = threadIdx.x + 256 * i;
+        Ds[t] = ((t & 15) < C) ? dv[i] : 0.f;
+      }
+      W2s[threadIdx.x] = (((int)threadIdx.x >> 4) < C) ? wv : 0.f;
+      lds_barrier();
+      // dz = (dlogits · W2[:, n-slice]) ⊙ mask, straight into the Zs image
+#pragma unroll
+      for (int i = 0; i < kZItems; ++i) {
+        const int t = threadIdx.x + 256 * i;
+        const int rr = t >> 2, q = t & 3;
+        float z[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int cc = 0; cc < 16; ++cc) {
+          const float d = Ds[rr * 16 + cc];
+          const float4 w4 = *reinterpret_cast<const float4*>(&W2s[cc * 16 + 4 * q]);
+          z[0] += d * w4.x; z[1] += d * w4.y; z[2] += d * w4.z; z[3] += d * w4.w;
+        }
+        const float4 hm = zv[i];
+        const float ik = P.hd_inv_keep;
+        float4 o = make_float4(hm.x > 0.f ? z[0] * ik : 0.f, hm.y > 0.f ? z[1] * ik : 0.f,
+                               hm.z > 0.f ? z[2] * ik : 0.f, hm.w > 0.f ? z[3] * ik : 0.f);
+        const int n = n0 + 4 * q;
+        o.x = (n + 0 < P.N) ? o.x : 0.f;
+        o.y = (n + 1 < P.N) ? o.y : 0.f;
+        o.z = (n + 2 < P.N) ? o.z : 0.f;
+        o.w = (n + 3 < P.N) ? o.w : 0.f;
+        if (rr >= mcn) o = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(&Zs[rr * 16 + 4 * q]) = o;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < kZItems; ++i) {
+        const int t = threadIdx.x + 256 * i;
+        const int rr = t >> 2, q = t & 3;
+        const int n = n0 + 4 * q;
+        float4 o = zv[i];
+        o.x = (n + 0 < P.N) ? o.x : 0.f;
+        o.y = (n + 1 < P.N) ? o.y : 0.f;
+        o.z = (n + 2 < P.N) ? o.z : 0.f;
+        o.w = (n + 3 < P.N) ? o.w : 0.f;
+        if (rr >= mcn) o = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(&Zs[rr * 16 + 4 * q]) = o;
+      }
     }
     lds_barrier();
     // (4) K-loop over all kMC rows of the image (rows >= mcn: Zs zero, Xs finite), fully
     //     unrolled so every LDS read is issued ahead of its MFMA
     if (mcn > kMC / 2) {
-#pragma unroll
+#pragma unroll 8
       for (int s = 0; s < kMC / 4; ++s) {
         const int m = 4 * s + g;
         const float a = Zs[m * 16 + c];
@@ -517,6 +578,178 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
           P.pB[n] = pb[r]; P.mB[n] = mb[r]; P.vB[n] = vb[r];
         }
       }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// mlp_fwd_head: linear_fwd of the hidden layer with the loss head fused in.
+// Each (m-tile, n-tile) workgroup computes its 16x16 H tile (bias, ReLU, dropout), stores it, and
+// multiplies it by the matching 16-column slice of W2 -> a 16 x C partial-logit slab. The LAST
+// workgroup to finish an m-tile (agent-scope release -> arrival counter -> acquire; placement-
+// independent, cdna_hip_programming.md §6 G16) sums the slabs in a fixed order (bitwise
+// reproducible), and runs softmax-cross-entropy for its 16 rows: loss/accuracy into the metric
+// ring, dlogits for the backward pass. One launch replaces linear_fwd + xent_head.
+// ---------------------------------------------------------------------------------------------
+template <int XT, int WAVES>
+__global__ __launch_bounds__(WAVES * 64) void mlp_fwd_head_kernel(
+    ArenaRowSource src, const float* __restrict__ W, const float* __restrict__ bias,
+    float* __restrict__ Y, int M, int N, int K, uint32_t keep_thr, float inv_keep, uint32_t seed,
+    const long long* step_src, ArenaFwdHead hd, ArenaCounterOp ctr) {
+  constexpr int CH = 8;
+  const int lane = lane_id(), w = wave_id();
+  const int g = lane >> 4, c = lane & 15;
+  const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  const int ntiles = gridDim.x;
+  const int C = hd.C;
+  const int rowc = min(m0 + c, M - 1), colc = min(n0 + c, N - 1);
+  const Gather gt = make_gather(src);
+  const uint32_t step = step_src ? (uint32_t)(*step_src) : 0u;
+  const long long prow = gather_row(gt, rowc);
+  const float* wrow = W + (long long)colc * K;
+  // W2 slice [C][16] for the partial logits (thread t < 256: c = t>>4, n = t&15)
+  __shared__ float w2s[16][17];
+  __shared__ float hs[16][17];
+  __shared__ float red[WAVES][16][17];
+  __shared__ float lg[16][17];
+  __shared__ int s_last;
+  float w2v = 0.f;
+  if (threadIdx.x < 256)
+    w2v = hd.W2[(long long)min((int)threadIdx.x >> 4, C - 1) * N + min(n0 + ((int)threadIdx.x & 15), N - 1)];
+  counter_op(ctr);
+  if (hd.hist_len > 1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    const long long hs0 = hd.hist_step ? *hd.hist_step : 0;
+    const int nxt = (int)(hs0 + 1) & (hd.hist_len - 1);
+    hd.loss_acc[nxt] = 0.f;
+    hd.correct_acc[nxt] = 0;
+  }
+
+  const int nsteps = (K + 15) >> 4;
+  const int s0 = (nsteps * w) / WAVES, s1 = (nsteps * (w + 1)) / WAVES;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int sb = s0; sb < s1; sb += CH) {
+    float a[CH][4], b[CH][4];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int k = (sb + i) * 16 + 4 * g;
+      const int kc = min(k, K - 4);
+      load4<XT>(src, prow, kc, a[i]);
+      const float4 wv = *reinterpret_cast<const float4*>(wrow + kc);
+      b[i][0] = wv.x; b[i][1] = wv.y; b[i][2] = wv.z; b[i][3] = wv.w;
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const bool kv = ((sb + i) * 16 + 4 * g) < K;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[i][j] = kv ? a[i][j] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      if (sb + i < s1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = mfma_16x16x4(a[i][j], b[i][j], acc);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 4; ++r) red[w][4 * g + r][c] = acc[r];
+  if (threadIdx.x < 256) w2s[threadIdx.x >> 4][threadIdx.x & 15] = ((int)(threadIdx.x >> 4) < C) ? w2v : 0.f;
+  __syncthreads();
+  if (threadIdx.x < 256) {
+    const int rr = threadIdx.x >> 4, cc = threadIdx.x & 15;
+    const int gm = m0 + rr, gn = n0 + cc;
+    float v = 0.f;
+#pragma unroll
+    for (int ww = 0; ww < WAVES; ++ww) v += red[ww][rr][cc];
+    v += bias[min(gn, N - 1)];
+    v = fmaxf(v, 0.f);
+    if (keep_thr != 0xFFFFFFFFu) {
+      const uint32_t h = hash4(seed, step, (uint32_t)gm, (uint32_t)gn);
+      v = (h < keep_thr) ? v * inv_keep : 0.f;
+    }
+    const bool ok = gm < M && gn < N;
+    if (ok) Y[(long long)gm * N + gn] = v;
+    hs[rr][cc] = ok ? v : 0.f;
+  }
+  __syncthreads();
+  // partial logits of this tile: slab[mt][nt][r][cl] = Σ_n hs[r][n] * W2[cl][n0+n]
+  float* slab = hd.slabs + ((long long)blockIdx.y * ntiles + blockIdx.x) * 16 * C;
+  if (hd.W2_copy != nullptr && blockIdx.y == 0 && threadIdx.x < 256) {
+    const int cl = threadIdx.x >> 4, gn = n0 + (threadIdx.x & 15);
+    if (cl < C && gn < N) hd.W2_copy[(long long)cl * N + gn] = w2v;
+  }
+  if ((int)threadIdx.x < 16 * C) {
+    const int rr = threadIdx.x / C, cl = threadIdx.x % C;
+    float p = 0.f;
+#pragma unroll
+    for (int n = 0; n < 16; ++n) p += hs[rr][n] * w2s[cl][n];
+    slab[threadIdx.x] = p;
+  }
+  // ---- arrival: release the slab, count, the last arriver acquires and finishes the m-tile ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int prev = __hip_atomic_fetch_add(&hd.counters[blockIdx.y], 1, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT);
+    s_last = (prev == ntiles - 1);
+  }
+  __syncthreads();
+  if (!s_last) return;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __hip_atomic_store(&hd.counters[blockIdx.y], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const float* mslab = hd.slabs + (long long)blockIdx.y * ntiles * 16 * C;
+  if ((int)threadIdx.x < 16 * C) {
+    const int rr = threadIdx.x / C, cl = threadIdx.x % C;
+    float sacc = hd.b2 ? hd.b2[cl] : 0.f;
+    for (int nt = 0; nt < ntiles; ++nt) sacc += mslab[(long long)nt * 16 * C + threadIdx.x];
+    lg[rr][cl] = sacc;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {  // wave 0: lane r < 16 owns row m0 + r
+    const int r = threadIdx.x;
+    const int gm = m0 + r;
+    const bool ok = r < 16 && gm < M;
+    float loss = 0.f;
+    int correct = 0;
+    if (ok) {
+      const int y = [&] {
+        const long long pr = gather_row(make_gather(hd.lab), gm);
+        if (hd.lab.dtype == 1) return (int)static_cast<const uint8_t*>(hd.lab.ptr)[pr];
+        if (hd.lab.dtype == 2) return static_cast<const int*>(hd.lab.ptr)[pr];
+        return (int)static_cast<const long long*>(hd.lab.ptr)[pr];
+      }();
+      float mx = lg[r][0];
+      int arg = 0;
+      for (int cl = 1; cl < C; ++cl) {
+        const float v = lg[r][cl];
+        if (v > mx) { mx = v; arg = cl; }
+      }
+      float se = 0.f;
+      for (int cl = 0; cl < C; ++cl) se += expf(lg[r][cl] - mx);
+      const float lse = mx + logf(se);
+      float ly = 0.f;
+      for (int cl = 0; cl < C; ++cl) ly = (cl == y) ? lg[r][cl] : ly;
+      loss = (lse - ly) * hd.loss_scale;
+      correct = (arg == y) ? 1 : 0;
+      if (hd.dlogits) {
+        for (int cl = 0; cl < C; ++cl)
+          hd.dlogits[(long long)gm * C + cl] =
+              (expf(lg[r][cl] - lse) - (cl == y ? 1.f : 0.f)) * hd.loss_scale;
+      }
+    }
+    const float lsum = wave_sum_fast(loss);
+    const float csum = wave_sum_fast((float)correct);
+    if (threadIdx.x == 0) {
+      const long long hs0 = hd.hist_step ? *hd.hist_step : 0;
+      const int slot = (int)hs0 & (hd.hist_len - 1);
+      atomicAdd(&hd.loss_acc[slot], lsum);
+      atomicAdd(&hd.correct_acc[slot], (int)(csum + 0.5f));
     }
   }
 }
@@ -639,6 +872,27 @@ hipError_t arena_linear_fwd(ArenaRowSource src, const float* W, const float* bia
   else
     hipLaunchKernelGGL((linear_fwd_kernel<0, 8>), grid, dim3(512), 0, stream, src, W, bias, Y, M,
                        N, K, act, thr, inv_keep, seed, step_src);
+  return hipGetLastError();
+}
+
+hipError_t arena_mlp_fwd_head(ArenaRowSource src, const float* W, const float* bias, float* Y, int M,
+                              int N, int K, float keep_prob, uint32_t seed,
+                              const long long* step_src, ArenaFwdHead hd, ArenaCounterOp ctr,
+                              hipStream_t stream) {
+  if (hd.C < 1 || hd.C > 16 || K % 4) return hipErrorInvalidValue;
+  uint32_t thr = 0xFFFFFFFFu;
+  float inv_keep = 1.f;
+  if (keep_prob < 1.f) {
+    thr = (uint32_t)((double)keep_prob * 4294967296.0);
+    inv_keep = 1.f / keep_prob;
+  }
+  dim3 grid((N + 15) / 16, (M + 15) / 16);
+  if (src.dtype == 1)
+    hipLaunchKernelGGL((mlp_fwd_head_kernel<1, 8>), grid, dim3(512), 0, stream, src, W, bias, Y, M,
+                       N, K, thr, inv_keep, seed, step_src, hd, ctr);
+  else
+    hipLaunchKernelGGL((mlp_fwd_head_kernel<0, 8>), grid, dim3(512), 0, stream, src, W, bias, Y, M,
+                       N, K, thr, inv_keep, seed, step_src, hd, ctr);
   return hipGetLastError();
 }
 

@@ -51,10 +51,12 @@ def main():
         ops.linear_fwd(tr.train_x, tr.W1, tr.Hbuf, tr.b1, x_scale=1 / 255.0, idx=tr.perm,
                        cursor=A, batch=B, act=1, keep_prob=cfg.keep_prob, seed=1, step=A)
 
+    dZ = torch.empty_like(tr.Hbuf)
+
     def head():
         ops.xent_head(tr.Hbuf, tr.W2, tr.b2, tr.train_y, loss_acc=tr.loss_hist,
                       correct_acc=tr.corr_hist, idx=tr.perm, cursor=A, batch=B,
-                      dlogits=tr.dlogits, dZ=tr.dZ, keep_prob=cfg.keep_prob, relu_mask=True,
+                      dlogits=tr.dlogits, dZ=dZ, keep_prob=cfg.keep_prob, relu_mask=True,
                       loss_scale=1.0 / B, hist_step=A, ctr_dst=Bc, ctr_src=A, ctr_add=0)
 
     def head_nograd():
@@ -63,7 +65,7 @@ def main():
                       keep_prob=cfg.keep_prob, relu_mask=True, loss_scale=1.0 / B, hist_step=A)
 
     def wgrad_adam():
-        ops.wgrad_grouped([tr.train_x, tr.Hbuf], [tr.dZ, tr.dlogits], [tr.W1, tr.W2],
+        ops.wgrad_grouped([tr.train_x, tr.Hbuf], [dZ, tr.dlogits], [tr.W1, tr.W2],
                           [tr.b1, tr.b2], mode=1, mW=[tr.mW1, tr.mW2], vW=[tr.vW1, tr.vW2],
                           mB=[tr.mb1, tr.mb2], vB=[tr.vb1, tr.vb2], x_scales=[1 / 255.0, 1.0],
                           gather=[True, False], idx=tr.perm, cursor=Bc, cursor_off=-1, batch=B,
@@ -74,22 +76,56 @@ def main():
     gW1, gb1, gW2, gb2 = (L.view(G, n) for n in ("W1", "b1", "W2", "b2"))
 
     def wgrad_grad():
-        ops.wgrad_grouped([tr.train_x, tr.Hbuf], [tr.dZ, tr.dlogits], [gW1, gW2], [gb1, gb2],
+        ops.wgrad_grouped([tr.train_x, tr.Hbuf], [dZ, tr.dlogits], [gW1, gW2], [gb1, gb2],
                           mode=0, x_scales=[1 / 255.0, 1.0], gather=[True, False], idx=tr.perm,
                           cursor=Bc, cursor_off=-1, batch=B)
 
     def wgrad_l1_only():
-        ops.wgrad_grouped([tr.train_x], [tr.dZ], [gW1], [gb1], mode=0, x_scales=[1 / 255.0],
+        ops.wgrad_grouped([tr.train_x], [dZ], [gW1], [gb1], mode=0, x_scales=[1 / 255.0],
                           gather=[True], idx=tr.perm, cursor=Bc, cursor_off=-1, batch=B)
 
     def adam():
         ops.adam_flat(tr.P, tr.M, tr.V, G, lr=1e-9, t_step=Bc)
 
+    xf = (tr.train_x[:B].float() / 255.0).contiguous()
+    xu = tr.train_x[:B].contiguous()
+    yb = tr.train_y[:B].contiguous()
+
+    def fwd_f32_nogather():
+        ops.linear_fwd(xf, tr.W1, tr.Hbuf, tr.b1, act=1, keep_prob=cfg.keep_prob, seed=1, step=A)
+
+    def fwd_u8_nogather_nodrop():
+        ops.linear_fwd(xu, tr.W1, tr.Hbuf, tr.b1, x_scale=1 / 255.0, act=1)
+
+    def head_nogather():
+        ops.xent_head(tr.Hbuf, tr.W2, tr.b2, yb, loss_acc=tr.loss_hist, correct_acc=tr.corr_hist,
+                      dlogits=tr.dlogits, dZ=dZ, keep_prob=cfg.keep_prob, relu_mask=True,
+                      loss_scale=1.0 / B)
+
+    def wgrad_l1_nogather():
+        ops.wgrad_grouped([xu], [dZ], [gW1], [gb1], mode=0, x_scales=[1 / 255.0],
+                          gather=[False])
+
+    def wgrad_l2_only():
+        ops.wgrad_grouped([tr.Hbuf], [tr.dlogits], [gW2], [gb2], mode=0, x_scales=[1.0],
+                          gather=[False])
+
     Bc.fill_(1)
-    for name, fn in [("linear_fwd", fwd), ("xent_head", head), ("xent_head_nograd", head_nograd),
+    for name, fn in [("fwd_f32_nogather", fwd_f32_nogather),
+                     ("fwd_u8_nogather_nodrop", fwd_u8_nogather_nodrop),
+                     ("head_nogather", head_nogather), ("wgrad_l1_nogather", wgrad_l1_nogather),
+                     ("wgrad_l2_only", wgrad_l2_only),("linear_fwd", fwd), ("xent_head", head), ("xent_head_nograd", head_nograd),
                      ("wgrad_adam", wgrad_adam), ("wgrad_grad", wgrad_grad),
                      ("wgrad_l1_grad", wgrad_l1_only), ("adam_flat", adam)]:
         res[name] = bench(fn)
+    def fused_fwd_head():
+        tr._launch_fwd_head()
+
+    def fused_wgrad_adam():
+        tr._launch_wgrad(adam=True)
+
+    res["fused_fwd_head"] = bench(fused_fwd_head)
+    res["fused_wgrad_adam"] = bench(fused_wgrad_adam)
     tr.enable_graphs(60)
     res["full_step"] = bench(lambda: tr._launch_step(), reps=60)
     for k, v in res.items():
