@@ -610,12 +610,20 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_head_kernel(
   // W2 slice [C][16] for the partial logits (thread t < 256: c = t>>4, n = t&15)
   __shared__ float w2s[16][17];
   __shared__ float hs[16][17];
-  __shared__ float red[WAVES][16][17];
+  __shared__ float red[WAVES][16][17];  // WAVES*16*17 >= 4 * 16 * C floats (tail scratch)
   __shared__ float lg[16][17];
   __shared__ int s_last;
   float w2v = 0.f;
   if (threadIdx.x < 256)
     w2v = hd.W2[(long long)min((int)threadIdx.x >> 4, C - 1) * N + min(n0 + ((int)threadIdx.x & 15), N - 1)];
+  // labels of this m-tile, prefetched by wave 0 (used only if this block is the last arriver)
+  int y_pre = 0;
+  if (threadIdx.x < 64) {
+    const long long pr = gather_row(make_gather(hd.lab), min(m0 + (int)(threadIdx.x & 15), M - 1));
+    if (hd.lab.dtype == 1) y_pre = (int)static_cast<const uint8_t*>(hd.lab.ptr)[pr];
+    else if (hd.lab.dtype == 2) y_pre = static_cast<const int*>(hd.lab.ptr)[pr];
+    else y_pre = (int)static_cast<const long long*>(hd.lab.ptr)[pr];
+  }
   counter_op(ctr);
   if (hd.hist_len > 1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
     const long long hs0 = hd.hist_step ? *hd.hist_step : 0;
@@ -672,42 +680,57 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_head_kernel(
     hs[rr][cc] = ok ? v : 0.f;
   }
   __syncthreads();
-  // partial logits of this tile: slab[mt][nt][r][cl] = Σ_n hs[r][n] * W2[cl][n0+n]
+  // partial logits of this tile: slab[mt][nt][r][cl] = Σ_n hs[r][n] * W2[cl][n0+n], stored
+  // write-through (agent-scope relaxed atomic stores = sc1): no release fence / L2 writeback needed
   float* slab = hd.slabs + ((long long)blockIdx.y * ntiles + blockIdx.x) * 16 * C;
-  if (hd.W2_copy != nullptr && blockIdx.y == 0 && threadIdx.x < 256) {
-    const int cl = threadIdx.x >> 4, gn = n0 + (threadIdx.x & 15);
-    if (cl < C && gn < N) hd.W2_copy[(long long)cl * N + gn] = w2v;
-  }
   if ((int)threadIdx.x < 16 * C) {
     const int rr = threadIdx.x / C, cl = threadIdx.x % C;
     float p = 0.f;
 #pragma unroll
     for (int n = 0; n < 16; ++n) p += hs[rr][n] * w2s[cl][n];
-    slab[threadIdx.x] = p;
+    __hip_atomic_store(&slab[threadIdx.x], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  // ---- arrival: release the slab, count, the last arriver acquires and finishes the m-tile ----
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+  // ---- arrival: drain the write-through stores, count; the last arriver finishes the m-tile ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
   __syncthreads();
   if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int prev = __hip_atomic_fetch_add(&hd.counters[blockIdx.y], 1, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT);
     s_last = (prev == ntiles - 1);
   }
   __syncthreads();
   if (!s_last) return;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep loads below
+  if (threadIdx.x == 0)
     __hip_atomic_store(&hd.counters[blockIdx.y], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // slab reduction: S threads per (row, class), each summing every S-th tile with all its loads in
+  // flight at once (sc1 loads: every read of handed-off bytes bypasses this CU's stale L1), then a
+  // fixed-order combine -> bitwise reproducible logits
+  const float* mslab = hd.slabs + (long long)blockIdx.y * ntiles * 16 * C;
+  const int pairs = 16 * C;
+  const int S = min(4, (int)blockDim.x / pairs);
+  constexpr int kRedLoads = 16;
+  if ((int)threadIdx.x < pairs * S) {
+    const int pr = threadIdx.x % pairs, q = threadIdx.x / pairs;
+    float sacc = 0.f;
+    for (int base = q; base < ntiles; base += S * kRedLoads) {
+      float v[kRedLoads];
+#pragma unroll
+      for (int j = 0; j < kRedLoads; ++j) {
+        const int nt = min(base + j * S, ntiles - 1);
+        v[j] = __hip_atomic_load(&mslab[(long long)nt * pairs + pr], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int j = 0; j < kRedLoads; ++j) sacc += (base + j * S < ntiles) ? v[j] : 0.f;
+    }
+    red[q][pr / 16][pr % 16] = sacc;  // red is free again: reuse as [S][pairs] scratch
   }
   __syncthreads();
-  const float* mslab = hd.slabs + (long long)blockIdx.y * ntiles * 16 * C;
-  if ((int)threadIdx.x < 16 * C) {
+  if ((int)threadIdx.x < pairs) {
     const int rr = threadIdx.x / C, cl = threadIdx.x % C;
     float sacc = hd.b2 ? hd.b2[cl] : 0.f;
-    for (int nt = 0; nt < ntiles; ++nt) sacc += mslab[(long long)nt * 16 * C + threadIdx.x];
+    for (int q = 0; q < S; ++q) sacc += red[q][threadIdx.x / 16][threadIdx.x % 16];
     lg[rr][cl] = sacc;
   }
   __syncthreads();
@@ -718,12 +741,7 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_head_kernel(
     float loss = 0.f;
     int correct = 0;
     if (ok) {
-      const int y = [&] {
-        const long long pr = gather_row(make_gather(hd.lab), gm);
-        if (hd.lab.dtype == 1) return (int)static_cast<const uint8_t*>(hd.lab.ptr)[pr];
-        if (hd.lab.dtype == 2) return static_cast<const int*>(hd.lab.ptr)[pr];
-        return (int)static_cast<const long long*>(hd.lab.ptr)[pr];
-      }();
+      const int y = y_pre;
       float mx = lg[r][0];
       int arg = 0;
       for (int cl = 1; cl < C; ++cl) {
