@@ -10,13 +10,15 @@ Execution design:
     single launch -- no flatten/unflatten copies, no per-tensor launches.
   * The training set lives in HBM as uint8; the batch gather (permutation + device step counter)
     and the /255 dequantisation are fused into the first GEMM and the loss head.
-  * One step = 2 launches on one GPU: mlp_fwd_head (hidden layer + loss head, last-arriver
-    softmax) -> wgrad_grouped (dz recomputed in-kernel from dlogits, both layers' dW, fused Adam);
-    with data parallelism: mlp_fwd_head -> wgrad (grad bucket) -> all_reduce -> adam_flat.
+  * One step = 2 launches on one GPU: mlp_fwd_logits (hidden layer + per-tile partial logits,
+    atomically accumulated) -> wgrad_grouped (every workgroup recomputes the 100x10 softmax-xent,
+    derives dz in LDS, computes both layers' dW and applies Adam in its epilogue). No kernel
+    waits on another workgroup. With data parallelism: fwd -> wgrad (grad bucket) -> all_reduce
+    -> adam_flat.
   * Every per-step scalar (data cursor, Adam t, dropout step, metric slot) is a device counter, so
     ``steps_per_graph`` consecutive steps are captured into ONE hipGraph and replayed.
 Step-counter protocol (no intra-kernel races): A = completed steps, B = current Adam t.
-  mlp_fwd_head reads A and writes B=A+1; wgrad reads B (cursor = B-1);
+  mlp_fwd_logits reads A and writes B=A+1; wgrad reads B (cursor = B-1);
   the last kernel of the step (wgrad with fused Adam, or adam_flat) writes A=B.
 """
 from __future__ import annotations
@@ -108,7 +110,7 @@ class FusedMLPTrainer:
         self.Hbuf = torch.empty(B, H, device=dev)
         self.dlogits = torch.empty(B, C, device=dev)
         self.W2snap = torch.empty(C, H, device=dev)
-        self.slabs, self.counters = ops.mlp_fwd_head_workspace(B, H, C, dev)
+        self.logits2 = torch.zeros(2, B, C, device=dev)  # step-parity double buffer
         self.ctrA = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ctrB = torch.zeros(1, dtype=torch.int64, device=dev)
         self.loss_hist = torch.zeros(cfg.hist_len, device=dev)
@@ -176,24 +178,27 @@ class FusedMLPTrainer:
         self._launch_wgrad(adam=True)
 
     def _launch_fwd_head(self):
+        """Hidden layer + logits accumulation (one launch); writes B = A + 1."""
         cfg, B, A, Bc = self.cfg, self.cfg.batch, self.ctrA, self.ctrB
-        ops.mlp_fwd_head(self.train_x, self.W1, self.b1, self.Hbuf, self.W2, self.b2,
-                         self.train_y, slabs=self.slabs, counters=self.counters,
-                         loss_acc=self.loss_hist, correct_acc=self.corr_hist,
-                         dlogits=self.dlogits, W2_copy=self.W2snap, x_scale=1.0 / 255.0,
-                         idx=self.perm, cursor=A, batch=B, keep_prob=cfg.keep_prob,
-                         seed=cfg.seed * 2654435761 + self.rank, step=A, loss_scale=1.0 / B,
-                         hist_step=A, ctr_dst=Bc, ctr_src=A, ctr_add=1)
+        ops.mlp_fwd_logits(self.train_x, self.W1, self.b1, self.Hbuf, self.W2, self.logits2,
+                           W2_copy=self.W2snap, x_scale=1.0 / 255.0, idx=self.perm, cursor=A,
+                           batch=B, keep_prob=cfg.keep_prob,
+                           seed=cfg.seed * 2654435761 + self.rank, step=A, ctr_dst=Bc,
+                           ctr_src=A, ctr_add=1)
 
     def _launch_wgrad(self, adam: bool):
-        """dW1 (dz recomputed from dlogits, W2 snapshot and the H mask) and dW2 in one launch;
-        with ``adam`` the update is applied in the epilogue, else grads go to the flat bucket."""
+        """Softmax-xent recomputed per workgroup from the logits; dW1 (dz via the W2 snapshot and
+        the H mask) and dW2 in one launch. With ``adam`` the update is the epilogue (and A = B is
+        committed), else the grads go to the flat all-reduce bucket."""
         cfg, B, A, Bc = self.cfg, self.cfg.batch, self.ctrA, self.ctrB
         common = dict(x_scales=[1.0 / 255.0, 1.0], gather=[True, False], idx=self.perm,
-                      cursor=Bc, cursor_off=-1, batch=B,
-                      head=[(self.dlogits, self.W2snap, self.Hbuf), None],
-                      head_keep_prob=cfg.keep_prob)
-        xs, dzs = [self.train_x, self.Hbuf], [None, self.dlogits]
+                      cursor=Bc, cursor_off=-1, batch=B, head_modes=[2, 1],
+                      head_w2=[self.W2snap, None], head_h=[self.Hbuf, None],
+                      head_keep_prob=cfg.keep_prob, head_logits2=self.logits2, head_step=Bc,
+                      head_step_off=-1, head_b2=self.b2, head_labels=self.train_y,
+                      head_loss_scale=1.0 / B, head_loss_acc=self.loss_hist,
+                      head_correct_acc=self.corr_hist)
+        xs, dzs = [self.train_x, self.Hbuf], [None, None]
         if adam:
             ops.wgrad_grouped(xs, dzs, [self.W1, self.W2], [self.b1, self.b2], mode=1,
                               mW=[self.mW1, self.mW2], vW=[self.vW1, self.vW2],
@@ -220,7 +225,7 @@ class FusedMLPTrainer:
         self.steps_per_graph = steps_per_graph
         # warm up on a side stream (allocator / collective communicators initialised outside
         # capture), then restore the state so warm-up steps do not count as training.
-        snap = [t.clone() for t in (self.P, self.M, self.V, self.ctrA, self.ctrB)]
+        snap = [t.clone() for t in (self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2)]
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -228,7 +233,7 @@ class FusedMLPTrainer:
                 self._launch_step()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        for t, v in zip((self.P, self.M, self.V, self.ctrA, self.ctrB), snap):
+        for t, v in zip((self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2), snap):
             t.copy_(v)
         try:
             self._graphs[steps_per_graph] = self._capture(steps_per_graph)

@@ -40,35 +40,31 @@ def xent_head(H: Tensor, W2: Tensor, b2: Optional[Tensor], labels: Tensor, *,
                        ctr_dst, ctr_src, int(ctr_add))
 
 
-def mlp_fwd_head(x: Tensor, W1: Tensor, b1: Tensor, H: Tensor, W2: Tensor, b2: Optional[Tensor],
-                 labels: Tensor, *, slabs: Tensor, counters: Tensor, loss_acc: Tensor,
-                 correct_acc: Tensor, dlogits: Optional[Tensor] = None,
-                 W2_copy: Optional[Tensor] = None, x_scale: float = 1.0,
-                 idx: Optional[Tensor] = None, cursor: Optional[Tensor] = None, batch: int = 0,
-                 keep_prob: float = 1.0, seed: int = 0, step: Optional[Tensor] = None,
-                 loss_scale: float = 1.0, hist_step: Optional[Tensor] = None,
-                 ctr_dst: Optional[Tensor] = None, ctr_src: Optional[Tensor] = None,
-                 ctr_add: int = 0) -> None:
-    """H = dropout(relu(x·W1ᵀ+b1)); logits = H·W2ᵀ+b2 -> loss/accuracy metrics + dlogits, in ONE
-    launch (per-tile partial logits + deterministic last-arriver softmax)."""
-    _impl(H).mlp_fwd_head(x, float(x_scale), idx, cursor, int(batch), W1, b1, H, float(keep_prob),
-                          int(seed), step, W2, b2, labels, slabs, counters, dlogits, W2_copy,
-                          float(loss_scale), loss_acc, correct_acc, hist_step, ctr_dst, ctr_src,
-                          int(ctr_add))
+def mlp_fwd_logits(x: Tensor, W1: Tensor, b1: Tensor, H: Tensor, W2: Tensor, logits2: Tensor, *,
+                   W2_copy: Optional[Tensor] = None, x_scale: float = 1.0,
+                   idx: Optional[Tensor] = None, cursor: Optional[Tensor] = None, batch: int = 0,
+                   keep_prob: float = 1.0, seed: int = 0, step: Optional[Tensor] = None,
+                   ctr_dst: Optional[Tensor] = None, ctr_src: Optional[Tensor] = None,
+                   ctr_add: int = 0) -> None:
+    """H = dropout(relu(x·W1ᵀ+b1)) and logits2[step & 1] += H·W2ᵀ in ONE launch.
 
-
-def mlp_fwd_head_workspace(M: int, N: int, C: int, device) -> tuple:
-    """(slabs, counters) workspace for mlp_fwd_head; counters must start at zero."""
-    mt, nt = (M + 15) // 16, (N + 15) // 16
-    return (torch.empty(mt * nt * 16 * C, device=device),
-            torch.zeros(mt, dtype=torch.int32, device=device))
+    ``logits2`` is [2, M, C]; the consuming wgrad (head mode) zeroes the other buffer each step.
+    """
+    _impl(H).mlp_fwd_logits(x, float(x_scale), idx, cursor, int(batch), W1, b1, H,
+                            float(keep_prob), int(seed), step, W2, W2_copy, logits2, ctr_dst,
+                            ctr_src, int(ctr_add))
 
 
 def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Optional[Tensor]], outW: Sequence[Tensor],
                   outB: Sequence[Optional[Tensor]], *, x_scales: Sequence[float],
                   gather: Sequence[bool], idx: Optional[Tensor] = None,
-                  head: Optional[Sequence] = None, head_keep_prob: float = 1.0,
                   cursor: Optional[Tensor] = None, cursor_off: int = 0, batch: int = 0,
+                  head_modes: Optional[Sequence[int]] = None, head_w2=None, head_h=None,
+                  head_keep_prob: float = 1.0, head_logits2: Optional[Tensor] = None,
+                  head_step: Optional[Tensor] = None, head_step_off: int = 0,
+                  head_b2: Optional[Tensor] = None, head_labels: Optional[Tensor] = None,
+                  head_loss_scale: float = 1.0, head_loss_acc: Optional[Tensor] = None,
+                  head_correct_acc: Optional[Tensor] = None,
                   mode: int = 0, mW=None, vW=None, mB=None, vB=None, lr: float = 1e-3,
                   lr_t: Optional[Tensor] = None, betas=(0.9, 0.999), eps: float = 1e-8,
                   weight_decay: float = 0.0, t_step: Optional[Tensor] = None,
@@ -77,26 +73,24 @@ def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Optional[Tensor]], outW: S
                   ctr_add: int = 0) -> None:
     """dW_i = dz_iᵀ·gather(x_i), db_i = Σ_rows dz_i for up to 4 layers in one launch.
 
-    ``dzs[i]`` may be None with ``head[i] = (dlogits, W2, h)``: dz is then recomputed in-kernel as
-    (dlogits·W2) ⊙ (h > 0) / head_keep_prob (the ReLU+dropout backward of an MLP hidden layer).
+    Head modes (fused MLP step): every workgroup recomputes softmax-xent from ``head_logits2``
+    (+ ``head_b2``, ``head_labels``); ``head_modes[i]`` 1 -> dz = dlogits (output layer),
+    2 -> dz = (dlogits·head_w2[i]) ⊙ (head_h[i] > 0) / head_keep_prob (hidden layer).
     mode 0 writes ``grad_scale * dW`` into ``outW`` (e.g. views of the flat all-reduce bucket);
     mode 1 applies Adam in place to parameters ``outW``/``outB`` with state ``mW,vW,mB,vB``.
     """
     n = len(xs)
     none = [None] * n
-    head = list(head) if head is not None else none
-    hd_dl = [h[0] if h is not None else None for h in head]
-    hd_w2 = [h[1] if h is not None else None for h in head]
-    hd_h = [h[2] if h is not None else None for h in head]
-    ref_t = outW[0]
-    _impl(ref_t).wgrad_grouped(list(xs), [float(s) for s in x_scales], [bool(g) for g in gather],
-                                idx, cursor, int(cursor_off), int(batch), list(dzs), hd_dl, hd_w2,
-                                hd_h, float(head_keep_prob), [0] * n, int(mode),
-                                list(outW), list(outB), list(mW or none), list(vW or none),
-                                list(mB or none), list(vB or none), float(lr), lr_t,
-                                float(betas[0]), float(betas[1]), float(eps), float(weight_decay),
-                                t_step, float(grad_scale), bool(tf_style), ctr_dst, ctr_src,
-                                int(ctr_add))
+    hm = list(head_modes) if head_modes is not None else [0] * n
+    _impl(outW[0]).wgrad_grouped(
+        list(xs), [float(s) for s in x_scales], [bool(g) for g in gather], idx, cursor,
+        int(cursor_off), int(batch), list(dzs), [int(m) for m in hm], list(head_w2 or none),
+        list(head_h or none), float(head_keep_prob), head_logits2, head_step, int(head_step_off),
+        head_b2, head_labels, float(head_loss_scale), head_loss_acc, head_correct_acc, int(mode),
+        list(outW), list(outB), list(mW or none), list(vW or none), list(mB or none),
+        list(vB or none), float(lr), lr_t, float(betas[0]), float(betas[1]), float(eps),
+        float(weight_decay), t_step, float(grad_scale), bool(tf_style), ctr_dst, ctr_src,
+        int(ctr_add))
 
 
 def adam_flat(P: Tensor, M: Tensor, V: Tensor, G: Tensor, *, lr: float = 1e-3,

@@ -115,22 +115,6 @@ def xent_head(H, W2, b2, labels, idx, cursor, batch, dlogits, dZ, keep_prob, rel
     dZ.view(M, -1).copy_(dz)
 
 
-def mlp_fwd_head(x, x_scale, idx, cursor, batch, W1, b1, H, keep_prob, seed, step, W2, b2, labels,
-                 slabs, counters, dlogits, W2_copy, loss_scale, loss_acc, correct_acc, hist_step,
-                 ctr_dst, ctr_src, ctr_add):
-    """Reference for the head-fused forward: linear_fwd + xent_head (no slab workspace needed)."""
-    if ctr_dst is not None:
-        src = int(ctr_src.reshape(-1)[0].item()) if ctr_src is not None else 0
-        ctr_new = src + ctr_add
-    linear_fwd(x, x_scale, idx, cursor, batch, W1, b1, H, 1, keep_prob, seed, step)
-    if W2_copy is not None:
-        W2_copy.view_as(W2).copy_(W2)
-    xent_head(H, W2, b2, labels, idx, cursor, batch, dlogits, None, keep_prob, True, loss_scale,
-              loss_acc, correct_acc, hist_step, None, None, 0)
-    if ctr_dst is not None:
-        ctr_dst.fill_(ctr_new)
-
-
 def adam_update(p, m, v, g, lr, b1, b2, eps, wd, t, grad_scale, tf_style):
     """In-place Adam on tensors (fp32), same formula as adam_apply in mlp_kernels.hip."""
     g = g * grad_scale + wd * p
@@ -152,16 +136,62 @@ def head_dz(dl, w2, h, keep_prob):
     return torch.where(h > 0, dz * inv_keep, torch.zeros_like(dz))
 
 
-def wgrad_grouped(xs, x_scales, gather, idx, cursor, cursor_off, batch, dzs, hd_dl, hd_w2, hd_h,
-                  hd_keep_prob, Ms, mode, outW, outB, mW, vW, mB, vB, lr, lr_t, b1, b2, eps, wd,
-                  t_step, grad_scale, tf_style, ctr_dst, ctr_src, ctr_add):
+def mlp_fwd_logits(x, x_scale, idx, cursor, batch, W1, b1, H, keep_prob, seed, step, W2, W2_copy,
+                   logits2, ctr_dst, ctr_src, ctr_add):
+    """Reference for the logits-emitting forward: H and logits2[step & 1] += H·W2ᵀ."""
+    if ctr_dst is not None:
+        src = int(ctr_src.reshape(-1)[0].item()) if ctr_src is not None else 0
+        ctr_new = src + ctr_add
+    linear_fwd(x, x_scale, idx, cursor, batch, W1, b1, H, 1, keep_prob, seed, step)
+    if W2_copy is not None:
+        W2_copy.view_as(W2).copy_(W2)
+    st = int(step.reshape(-1)[0].item()) if step is not None else 0
+    logits2[st & 1] += H @ W2.t()
+    if ctr_dst is not None:
+        ctr_dst.fill_(ctr_new)
+
+
+def _head_dlogits(logits2, hd_step, hd_step_off, b2, labels, idx, cursor, cursor_off, batch,
+                  gather_any, loss_scale, loss_acc, correct_acc):
+    hstep = int(hd_step.reshape(-1)[0].item()) + hd_step_off
+    lg = logits2[hstep & 1].clone()
+    M, C = lg.shape
+    if b2 is not None:
+        lg = lg + b2
+    y = (gather_rows(labels, idx, cursor, batch, M, cursor_off) if gather_any
+         else labels[:M]).to(torch.int64)
+    lse = torch.logsumexp(lg, dim=1)
+    loss = lse - lg.gather(1, y.unsqueeze(1)).squeeze(1)
+    L = loss_acc.numel()
+    loss_acc[(hstep + 1) & (L - 1)] = 0.0
+    correct_acc[(hstep + 1) & (L - 1)] = 0
+    loss_acc[hstep & (L - 1)] += (loss * loss_scale).sum()
+    correct_acc[hstep & (L - 1)] += (lg.argmax(dim=1) == y).sum().to(correct_acc.dtype)
+    dl = (torch.softmax(lg, dim=1) - torch.nn.functional.one_hot(y, C).to(lg.dtype)) * loss_scale
+    logits2[(hstep + 1) & 1].zero_()
+    return dl
+
+
+def wgrad_grouped(xs, x_scales, gather, idx, cursor, cursor_off, batch, dzs, hd_modes, hd_w2, hd_h,
+                  hd_keep_prob, hd_logits2, hd_step, hd_step_off, hd_b2, hd_labels, hd_loss_scale,
+                  hd_loss_acc, hd_correct_acc, mode, outW, outB, mW, vW, mB, vB, lr, lr_t, b1, b2,
+                  eps, wd, t_step, grad_scale, tf_style, ctr_dst, ctr_src, ctr_add):
     t = int(t_step.reshape(-1)[0].item()) if t_step is not None else 1
     lr_v = float(lr_t.reshape(-1)[0].item()) if lr_t is not None else lr
+    dl = None
+    if any(m != 0 for m in hd_modes):
+        dl = _head_dlogits(hd_logits2, hd_step, hd_step_off, hd_b2, hd_labels, idx, cursor,
+                           cursor_off, batch, any(gather), hd_loss_scale, hd_loss_acc,
+                           hd_correct_acc)
     pending = []
     for i in range(len(xs)):
-        dz = dzs[i] if dzs[i] is not None else head_dz(hd_dl[i], hd_w2[i], hd_h[i], hd_keep_prob)
-        M = Ms[i] if Ms[i] > 0 else dz.shape[0]
-        dz = dz[:M]
+        if hd_modes[i] == 0:
+            dz = dzs[i]
+        elif hd_modes[i] == 1:
+            dz = dl
+        else:
+            dz = head_dz(dl, hd_w2[i], hd_h[i], hd_keep_prob)
+        M = dz.shape[0]
         if gather[i]:
             xr = gather_rows(xs[i], idx, cursor, batch, M, cursor_off)
         else:

@@ -42,34 +42,35 @@ struct ArenaAdam {
 struct ArenaWGradProblem {
   ArenaRowSource x;       // rows m of the layer input
   int xt;                 // 0 f32, 1 u8
-  const float* dz;        // [M][N] upstream gradient (null when recomputed from the head below)
-  // dz recomputed in-kernel from the softmax head (fused MLP step):
-  //   dz[m][n] = (Σ_c hd_dl[m][c] * hd_w2[c][n]) * (hd_h[m][n] > 0 ? hd_inv_keep : 0)
-  const float* hd_dl;     // [M][hd_c] dlogits
-  const float* hd_w2;     // [hd_c][N] next-layer weight
-  const float* hd_h;      // [M][N] this layer's (post-dropout) activation, for the ReLU/drop mask
-  int hd_c;
+  const float* dz;        // [M][N] upstream gradient (null when derived from the softmax head)
+  // Softmax-head modes (fused MLP step, see ArenaHead):
+  //   hd_mode 1: dz = dlogits                               (output layer, N == C)
+  //   hd_mode 2: dz = (dlogits · hd_w2) ⊙ (hd_h > 0) / keep  (hidden layer: ReLU+dropout bwd)
+  int hd_mode;
+  const float* hd_w2;     // [C][N] W2 snapshot (mode 2)
+  const float* hd_h;      // [M][N] post-dropout activation, mask source (mode 2)
   float hd_inv_keep;
   int M, K, N;
   int mode;               // 0: write grad (scaled), 1: Adam in place
-  float* gW; float* gB;   // mode 0 outputs ([K][N], [N]); gB may be null
+  float* gW; float* gB;   // mode 0 outputs ([N][K], [N]); gB may be null
   float* pW; float* mW; float* vW;  // mode 1
   float* pB; float* mB; float* vB;
   int tiles_k, tiles_n, block_begin;
 };
 
-// Fused forward + loss head of a 1-hidden-layer MLP (mlp_fwd_head).
-struct ArenaFwdHead {
-  const float* W2;        // [C][N] output layer
-  const float* b2;        // [C]
+// Softmax-cross-entropy head recomputed inside every wgrad workgroup from the raw logits that the
+// forward kernel accumulated (100 x 10 for MNIST: cheaper than any inter-workgroup hand-off).
+// logits2 is double-buffered by step parity: step t accumulates into buffer t&1 while the wgrad
+// of step t zeroes buffer (t+1)&1 for the next forward.
+struct ArenaHead {
+  float* logits2;           // [2][M][C] Σ over hidden tiles of H·W2ᵀ (no bias)
+  const long long* step;    // device step counter: (*step + step_off) = index of this step
+  int step_off;
+  const float* b2;          // [C]
   int C;
-  ArenaRowSource lab;     // labels (same gather as x)
-  float* slabs;           // workspace [mtiles][ntiles][16][C] partial logits
-  int* counters;          // workspace [mtiles], zero-initialised once; reset by the last arriver
-  float* dlogits;         // [M][C] out (null: metrics only)
-  float* W2_copy;         // optional [C][N] snapshot of W2 (backward reads it while Adam updates W2)
-  float loss_scale;
-  float* loss_acc; int* correct_acc; int hist_len; const long long* hist_step;
+  ArenaRowSource lab;       // labels (same gather as the layer input)
+  float loss_scale;         // 1/batch (mean loss)
+  float* loss_acc; int* correct_acc; int hist_len;  // metric ring (block 0), power of two
 };
 
 }  // extern "C"

@@ -12,13 +12,13 @@
 extern "C" {
 hipError_t arena_linear_fwd(ArenaRowSource, const float*, const float*, float*, int, int, int, int,
                             float, uint32_t, const long long*, hipStream_t);
-hipError_t arena_mlp_fwd_head(ArenaRowSource, const float*, const float*, float*, int, int, int, float,
-                              uint32_t, const long long*, ArenaFwdHead, ArenaCounterOp,
-                              hipStream_t);
+hipError_t arena_mlp_fwd_logits(ArenaRowSource, const float*, const float*, float*, int, int, int,
+                                float, uint32_t, const long long*, const float*, float*, int,
+                                float*, ArenaCounterOp, hipStream_t);
 hipError_t arena_xent_head(const float*, int, int, const float*, const float*, int, ArenaRowSource,
                            float*, float*, float, int, float, float*, int*, int, const long long*,
                            ArenaCounterOp, hipStream_t);
-hipError_t arena_wgrad_grouped(ArenaWGradProblem*, int, ArenaAdam, float, ArenaCounterOp,
+hipError_t arena_wgrad_grouped(ArenaWGradProblem*, int, ArenaAdam, float, ArenaCounterOp, ArenaHead,
                                hipStream_t);
 hipError_t arena_adam_flat(float*, float*, float*, const float*, long long, ArenaAdam,
                            ArenaCounterOp, hipStream_t);
@@ -131,62 +131,28 @@ void linear_fwd(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch, 
             "linear_fwd");
 }
 
-// Hidden layer forward with the softmax-xent head fused in (see mlp_fwd_head_kernel).
-void mlp_fwd_head(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch, Tensor W1,
-                  Tensor b1, Tensor H, double keep_prob, int64_t seed, OptT step, Tensor W2,
-                  OptT b2, Tensor labels, Tensor slabs, Tensor counters, OptT dlogits,
-                  OptT W2_copy, double loss_scale, Tensor loss_acc, Tensor correct_acc, OptT hist_step,
-                  OptT ctr_dst, OptT ctr_src, int64_t ctr_add) {
-  for (auto* t : {&W1, &b1, &H, &W2, &slabs}) check_f32(*t, "mlp_fwd_head operand");
+// Hidden layer forward that also accumulates the output layer's logits (mlp_fwd_logits_kernel).
+// logits2 [2, M, C] must be zero in buffer (step & 1) before the launch (the fused wgrad zeroes
+// the other buffer each step; zero both once at setup).
+void mlp_fwd_logits(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch, Tensor W1,
+                    Tensor b1, Tensor H, double keep_prob, int64_t seed, OptT step, Tensor W2,
+                    OptT W2_copy, Tensor logits2, OptT ctr_dst, OptT ctr_src, int64_t ctr_add) {
+  for (auto* t : {&W1, &b1, &H, &W2, &logits2}) check_f32(*t, "mlp_fwd_logits operand");
   const int64_t M = H.size(0), N = H.size(1), K = W1.size(1), C = W2.size(0);
   TORCH_CHECK(W1.dim() == 2 && W1.size(0) == N && x.dim() == 2 && x.size(1) == K,
-              "mlp_fwd_head: W1 [N, K], x [*, K], H [M, N]");
+              "mlp_fwd_logits: W1 [N, K], x [*, K], H [M, N]");
   TORCH_CHECK(K % 4 == 0, "K must be a multiple of 4");
   TORCH_CHECK(b1.numel() == N, "b1 size");
   TORCH_CHECK(W2.dim() == 2 && W2.size(1) == N && C >= 1 && C <= 16, "W2 must be [C<=16, N]");
+  TORCH_CHECK(logits2.numel() == 2 * M * C, "logits2 must be [2, M, C]");
   TORCH_CHECK(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kUInt8, "x dtype");
-  const int64_t mt = (M + 15) / 16, nt = (N + 15) / 16;
-  TORCH_CHECK(slabs.numel() >= mt * nt * 16 * C, "slabs workspace too small (need ",
-              mt * nt * 16 * C, ")");
-  check_dev(counters, "counters");
-  TORCH_CHECK(counters.scalar_type() == torch::kInt32 && counters.numel() >= mt,
-              "counters must be int32 with >= ceil(M/16) entries (zero-initialised)");
   TORCH_CHECK(keep_prob > 0.0 && keep_prob <= 1.0, "keep_prob in (0, 1]");
-  check_f32(loss_acc, "loss_acc");
-  check_dev(correct_acc, "correct_acc");
-  TORCH_CHECK(correct_acc.scalar_type() == torch::kInt32 && correct_acc.numel() == loss_acc.numel(),
-              "correct_acc int32, same length as loss_acc");
-  TORCH_CHECK((loss_acc.numel() & (loss_acc.numel() - 1)) == 0, "history length power of two");
-  ArenaFwdHead hd{};
-  hd.W2 = W2.data_ptr<float>();
-  hd.b2 = nullptr;
-  if (b2.has_value()) {
-    check_f32(*b2, "b2");
-    TORCH_CHECK(b2->numel() == C, "b2 size");
-    hd.b2 = b2->data_ptr<float>();
-  }
-  hd.C = (int)C;
-  TORCH_CHECK(labels.dim() == 1 && labels.scalar_type() != torch::kFloat32, "labels");
-  hd.lab = make_src(labels, 1.0, idx, cursor, batch, M, "labels");
-  hd.slabs = slabs.data_ptr<float>();
-  hd.counters = counters.data_ptr<int>();
-  hd.dlogits = nullptr;
-  if (dlogits.has_value()) {
-    check_f32(*dlogits, "dlogits");
-    TORCH_CHECK(dlogits->numel() == M * C, "dlogits size");
-    hd.dlogits = dlogits->data_ptr<float>();
-  }
-  hd.W2_copy = nullptr;
+  float* w2c = nullptr;
   if (W2_copy.has_value()) {
     check_f32(*W2_copy, "W2_copy");
     TORCH_CHECK(W2_copy->numel() == C * N, "W2_copy size");
-    hd.W2_copy = W2_copy->data_ptr<float>();
+    w2c = W2_copy->data_ptr<float>();
   }
-  hd.loss_scale = (float)loss_scale;
-  hd.loss_acc = loss_acc.data_ptr<float>();
-  hd.correct_acc = correct_acc.data_ptr<int>();
-  hd.hist_len = (int)loss_acc.numel();
-  hd.hist_step = opt_i64_scalar(hist_step, "hist_step");
   ArenaCounterOp ctr{};
   if (ctr_dst.has_value()) {
     ctr.dst = const_cast<long long*>(opt_i64_scalar(ctr_dst, "ctr_dst"));
@@ -194,10 +160,11 @@ void mlp_fwd_head(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch
     ctr.add = (int)ctr_add;
   }
   ArenaRowSource s = make_src(x, x_scale, idx, cursor, batch, M, "x");
-  check_hip(arena_mlp_fwd_head(s, W1.data_ptr<float>(), b1.data_ptr<float>(), H.data_ptr<float>(),
-                               (int)M, (int)N, (int)K, (float)keep_prob, (uint32_t)seed,
-                               opt_i64_scalar(step, "step"), hd, ctr, cur_stream()),
-            "mlp_fwd_head");
+  check_hip(arena_mlp_fwd_logits(s, W1.data_ptr<float>(), b1.data_ptr<float>(),
+                                 H.data_ptr<float>(), (int)M, (int)N, (int)K, (float)keep_prob,
+                                 (uint32_t)seed, opt_i64_scalar(step, "step"), W2.data_ptr<float>(),
+                                 w2c, (int)C, logits2.data_ptr<float>(), ctr, cur_stream()),
+            "mlp_fwd_logits");
 }
 
 void xent_head(Tensor H, Tensor W2, OptT b2, Tensor labels, OptT idx, OptT cursor, int64_t batch,
@@ -275,9 +242,11 @@ ArenaAdam make_adam(double lr, OptT lr_t, double b1, double b2, double eps, doub
 // layers flagged gather=True (the dataset-fed first layer).
 void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::vector<bool> gather,
                    OptT idx, OptT cursor, int64_t cursor_off, int64_t batch,
-                   std::vector<OptT> dzs, std::vector<OptT> hd_dl, std::vector<OptT> hd_w2,
-                   std::vector<OptT> hd_h, double hd_keep_prob, std::vector<int64_t> Ms,
-                   int64_t mode,
+                   std::vector<OptT> dzs, std::vector<int64_t> hd_modes,
+                   std::vector<OptT> hd_w2, std::vector<OptT> hd_h, double hd_keep_prob,
+                   OptT hd_logits2, OptT hd_step, int64_t hd_step_off, OptT hd_b2,
+                   OptT hd_labels, double hd_loss_scale, OptT hd_loss_acc,
+                   OptT hd_correct_acc, int64_t mode,
                    std::vector<Tensor> outW, std::vector<OptT> outB, std::vector<OptT> mW,
                    std::vector<OptT> vW, std::vector<OptT> mB, std::vector<OptT> vB, double lr,
                    OptT lr_t, double b1, double b2, double eps, double wd, OptT t_step,
@@ -285,8 +254,8 @@ void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::ve
   const size_t n = xs.size();
   TORCH_CHECK(n >= 1 && n <= 4, "wgrad_grouped: 1..4 problems");
   TORCH_CHECK(x_scales.size() == n && gather.size() == n && dzs.size() == n && outW.size() == n &&
-                  outB.size() == n && hd_dl.size() == n && hd_w2.size() == n &&
-                  hd_h.size() == n && Ms.size() == n,
+                  outB.size() == n && hd_modes.size() == n && hd_w2.size() == n &&
+                  hd_h.size() == n,
               "wgrad_grouped: list lengths differ");
   if (mode == 1)
     TORCH_CHECK(mW.size() == n && vW.size() == n && mB.size() == n && vB.size() == n,
@@ -297,7 +266,8 @@ void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::ve
     P = ArenaWGradProblem{};
     const Tensor& x = xs[i];
     int64_t M = 0, N = 0;
-    if (dzs[i].has_value()) {
+    if (hd_modes[i] == 0) {
+      TORCH_CHECK(dzs[i].has_value(), "wgrad_grouped: problem ", i, " needs dz");
       const Tensor& dz = *dzs[i];
       check_f32(dz, "dz");
       TORCH_CHECK(dz.dim() == 2, "dz must be 2-D");
@@ -305,34 +275,34 @@ void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::ve
       N = dz.size(1);
       P.dz = dz.data_ptr<float>();
     } else {
-      // dz recomputed from the softmax head: dz = (dl · W2) ⊙ (h > 0) / keep
-      TORCH_CHECK(hd_dl[i].has_value() && hd_w2[i].has_value() && hd_h[i].has_value(),
-                  "wgrad_grouped: problem ", i, " needs dz or (hd_dl, hd_w2, hd_h)");
-      const Tensor& dl = *hd_dl[i];
-      const Tensor& w2 = *hd_w2[i];
-      const Tensor& h = *hd_h[i];
-      check_f32(dl, "hd_dl");
-      check_f32(w2, "hd_w2");
-      check_f32(h, "hd_h");
-      M = h.size(0);
-      N = h.size(1);
-      TORCH_CHECK(dl.dim() == 2 && dl.size(0) == M && dl.size(1) <= 16, "hd_dl must be [M, C<=16]");
-      TORCH_CHECK(w2.dim() == 2 && w2.size(0) == dl.size(1) && w2.size(1) == N,
-                  "hd_w2 must be [C, N]");
-      TORCH_CHECK(N % 4 == 0, "head-recompute mode needs N % 4 == 0");
-      TORCH_CHECK(hd_keep_prob > 0.0 && hd_keep_prob <= 1.0, "hd_keep_prob in (0, 1]");
+      TORCH_CHECK(hd_logits2.has_value() && hd_labels.has_value() && hd_step.has_value() &&
+                      hd_loss_acc.has_value() && hd_correct_acc.has_value(),
+                  "head mode needs logits2, labels, step and metric buffers");
+      const int64_t C = hd_logits2->size(-1);
+      M = hd_logits2->size(-2);
+      TORCH_CHECK(hd_logits2->dim() == 3 && hd_logits2->size(0) == 2 && C >= 1 && C <= 16,
+                  "hd_logits2 must be [2, M, C<=16]");
       P.dz = nullptr;
-      P.hd_dl = dl.data_ptr<float>();
-      P.hd_w2 = w2.data_ptr<float>();
-      P.hd_h = h.data_ptr<float>();
-      P.hd_c = (int)dl.size(1);
+      P.hd_mode = (int)hd_modes[i];
+      if (hd_modes[i] == 1) {
+        N = C;
+      } else {
+        TORCH_CHECK(hd_modes[i] == 2 && hd_w2[i].has_value() && hd_h[i].has_value(),
+                    "hd_mode 2 needs hd_w2 and hd_h");
+        const Tensor& w2 = *hd_w2[i];
+        const Tensor& h = *hd_h[i];
+        check_f32(w2, "hd_w2");
+        check_f32(h, "hd_h");
+        TORCH_CHECK(h.dim() == 2 && h.size(0) == M, "hd_h must be [M, N]");
+        N = h.size(1);
+        TORCH_CHECK(w2.dim() == 2 && w2.size(0) == C && w2.size(1) == N, "hd_w2 must be [C, N]");
+        TORCH_CHECK(N % 4 == 0, "head mode 2 needs N % 4 == 0");
+        P.hd_w2 = w2.data_ptr<float>();
+        P.hd_h = h.data_ptr<float>();
+      }
+      TORCH_CHECK(hd_keep_prob > 0.0 && hd_keep_prob <= 1.0, "hd_keep_prob in (0, 1]");
       P.hd_inv_keep = (float)(1.0 / hd_keep_prob);
     }
-    if (Ms[i] > 0) {
-      TORCH_CHECK(Ms[i] <= M, "Ms[i] exceeds rows");
-      M = Ms[i];
-    }
-    TORCH_CHECK(x.dim() == 2, "x must be 2-D");
     const int64_t K = x.size(1);
     TORCH_CHECK(K % 4 == 0, "wgrad: K must be a multiple of 4");
     TORCH_CHECK(x.scalar_type() == torch::kFloat32 || x.scalar_type() == torch::kUInt8,
@@ -377,7 +347,43 @@ void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::ve
     ctr.src = opt_i64_scalar(ctr_src, "ctr_src");
     ctr.add = (int)ctr_add;
   }
-  check_hip(arena_wgrad_grouped(probs.data(), (int)n, a, (float)grad_scale, ctr, cur_stream()),
+  ArenaHead head{};
+  bool any_head = false;
+  for (auto m : hd_modes) any_head |= (m != 0);
+  if (any_head) {
+    check_f32(*hd_logits2, "hd_logits2");
+    head.logits2 = hd_logits2->data_ptr<float>();
+    head.step = opt_i64_scalar(hd_step, "hd_step");
+    head.step_off = (int)hd_step_off;
+    head.C = (int)hd_logits2->size(-1);
+    head.b2 = nullptr;
+    if (hd_b2.has_value()) {
+      check_f32(*hd_b2, "hd_b2");
+      TORCH_CHECK(hd_b2->numel() == head.C, "hd_b2 size");
+      head.b2 = hd_b2->data_ptr<float>();
+    }
+    const int64_t Mh = hd_logits2->size(1);
+    TORCH_CHECK(hd_labels->dim() == 1 && hd_labels->scalar_type() != torch::kFloat32, "labels");
+    // labels share the layer-input gather (first problem with gather=True), same cursor offset
+    int gi = -1;
+    for (size_t i = 0; i < n; ++i)
+      if (gather[i]) { gi = (int)i; break; }
+    head.lab = gi >= 0 ? make_src(*hd_labels, 1.0, idx, cursor, batch, Mh, "labels", cursor_off)
+                       : make_src(*hd_labels, 1.0, c10::nullopt, c10::nullopt, 0, Mh, "labels");
+    head.loss_scale = (float)hd_loss_scale;
+    check_f32(*hd_loss_acc, "hd_loss_acc");
+    check_dev(*hd_correct_acc, "hd_correct_acc");
+    TORCH_CHECK(hd_correct_acc->scalar_type() == torch::kInt32 &&
+                    hd_correct_acc->numel() == hd_loss_acc->numel(),
+                "metric buffers");
+    TORCH_CHECK((hd_loss_acc->numel() & (hd_loss_acc->numel() - 1)) == 0,
+                "metric history length must be a power of two");
+    head.loss_acc = hd_loss_acc->data_ptr<float>();
+    head.correct_acc = hd_correct_acc->data_ptr<int>();
+    head.hist_len = (int)hd_loss_acc->numel();
+  }
+  check_hip(arena_wgrad_grouped(probs.data(), (int)n, a, (float)grad_scale, ctr, head,
+                                cur_stream()),
             "wgrad_grouped");
 }
 
@@ -462,7 +468,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "arena_amd native HIP kernels (gfx950)";
   m.def("linear_fwd", &linear_fwd);
   m.def("xent_head", &xent_head);
-  m.def("mlp_fwd_head", &mlp_fwd_head);
+  m.def("mlp_fwd_logits", &mlp_fwd_logits);
   m.def("wgrad_grouped", &wgrad_grouped);
   m.def("adam_flat", &adam_flat);
   m.def("sgd_flat", &sgd_flat);

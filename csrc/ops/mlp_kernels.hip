@@ -138,6 +138,7 @@ __global__ __launch_bounds__(WAVES * 64) void linear_fwd_kernel(
   const int rowc = min(m0 + c, M - 1), colc = min(n0 + c, N - 1);
   const Gather gt = make_gather(src);
   const uint32_t step = step_src ? (uint32_t)(*step_src) : 0u;  // early: off the epilogue's path
+  const float bv = bias ? bias[min(n0 + (int)(threadIdx.x & 15), N - 1)] : 0.f;  // epilogue t&15
   const long long prow = gather_row(gt, rowc);
   const float* wrow = W + (long long)colc * K;
   const int nsteps = (K + 15) >> 4;
@@ -180,7 +181,7 @@ __global__ __launch_bounds__(WAVES * 64) void linear_fwd_kernel(
       float v = 0.f;
 #pragma unroll
       for (int ww = 0; ww < WAVES; ++ww) v += red[ww][rr][cc];
-      if (bias) v += bias[gn];
+      v += bv;  // thread t's prefetched bias[n0 + (t & 15)] == bias[gn]
       if (act == 1) v = fmaxf(v, 0.f);
       if (keep_thr != 0xFFFFFFFFu) {
         const uint32_t h = hash4(seed, step, (uint32_t)gm, (uint32_t)gn);
@@ -341,12 +342,15 @@ struct WGradArgs {
   ArenaAdam adam;
   float grad_scale;  // mode 0
   ArenaCounterOp ctr;
+  ArenaHead head;    // used by problems with hd_mode != 0
+  int head_block;    // first block of the first head-mode problem: zeroes + records metrics
 };
 
 constexpr int kMC = 128;       // rows per LDS chunk
 constexpr int kXsStride = 80;  // floats
 constexpr int kXItems = (kMC * 16) / 256;  // X staging items per thread (16 per row)
 constexpr int kZItems = (kMC * 4) / 256;   // dZ staging items per thread (4 float4 per row)
+constexpr int kDItems = (kMC * 16) / 256;  // head logits items per thread ([m][16])
 
 // Raw workgroup barrier for LDS hand-offs: waits only for this wave's LDS ops (lgkmcnt), NOT for
 // its outstanding global loads (__syncthreads() would emit vmcnt(0) and drain the prefetches).
@@ -376,19 +380,40 @@ __device__ __forceinline__ void load_x_items(const ArenaWGradProblem& P, const G
   }
 }
 
-// >= 2 waves/SIMD: 424 workgroups x 4 waves must be co-resident in ONE round on 1024 SIMDs.
+__device__ __forceinline__ int load_label(const ArenaRowSource& lab, long long pr) {
+  if (lab.dtype == 1) return (int)static_cast<const uint8_t*>(lab.ptr)[pr];
+  if (lab.dtype == 2) return static_cast<const int*>(lab.ptr)[pr];
+  return (int)static_cast<const long long*>(lab.ptr)[pr];
+}
+
+// ---------------------------------------------------------------------------------------------
+// wgrad_grouped: dW[N][K] = dZᵀ·X (+ db = dZᵀ·1) for up to kMaxProblems layers in one launch.
+// Workgroup = 4 waves = a 16(n) x 64(k) tile of dW. Per 128-row chunk: (1) every global load of the
+// chunk is issued at once (gathered X block, dZ slice -- or the softmax head's raw logits, labels
+// and the W2/H slices dZ is derived from -- then the tile's Adam state), (2) LDS images, (3) in
+// head mode each workgroup recomputes softmax-xent for the chunk's rows (cheap, removes a kernel)
+// and derives dZ, (4) 4 waves run the MFMA K-loop over m; the Adam update is the epilogue.
+//   A operand (dZᵀ): lane l -> Zs[m = 4s + (l>>4)][n = l&15]         (stride 16: conflict-free)
+//   B operand (X)  : lane l -> Xs[m = 4s + (l>>4)][k = 16w + (l&15)] (stride 80 ≡ 16 mod 32 banks:
+//                    the two 16-lane groups of each half-wave hit disjoint banks)
+//   D              : lane l, reg r -> dW[n0 + 4(l>>4) + r][k0 + 16w + (l&15)]   (coalesced rows)
+// >= 2 waves/SIMD so all 424 workgroups x 4 waves are co-resident in ONE round on 1024 SIMDs.
+// ---------------------------------------------------------------------------------------------
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void wgrad_grouped_kernel(
     WGradArgs args) {
   __shared__ __attribute__((aligned(16))) float Xs[kMC * kXsStride];
   __shared__ __attribute__((aligned(16))) float Zs[kMC * 16];
-  __shared__ __attribute__((aligned(16))) float Ds[kMC * 16];  // head dlogits rows [m][c]
-  __shared__ __attribute__((aligned(16))) float W2s[16 * 16];  // head W2 slice [c][n]
+  __shared__ __attribute__((aligned(16))) float Ds[kMC * 16];  // head: logits -> dlogits [m][c]
+  __shared__ __attribute__((aligned(16))) float W2s[16 * 16];  // head: W2 slice [c][n]
+  __shared__ int Ys[kMC];                                      // head: labels
+  __shared__ float B2s[16];
   counter_op(args.ctr);
   int pi = 0;
 #pragma unroll
   for (int i = 1; i < kMaxProblems; ++i)
     if (i < args.nprob && (int)blockIdx.x >= args.p[i].block_begin) pi = i;
   const ArenaWGradProblem& P = args.p[pi];
+  const ArenaHead& HD = args.head;
   const int local = blockIdx.x - P.block_begin;
   const int tn = local / P.tiles_k, tk = local % P.tiles_k;
   const int n0 = tn * 16, k0 = tk * 64;
@@ -400,25 +425,39 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
   const bool has_bias = P.mode == 1 ? P.pB != nullptr : P.gB != nullptr;
   const Gather gt = make_gather(P.x);
   const bool zvec = (P.N & 3) == 0;
-  const bool head = P.hd_dl != nullptr;  // host: head mode requires N % 4 == 0
+  const int hmode = P.hd_mode;
   AdamCoef co{};
   if (P.mode == 1) co = adam_coef(args.adam);  // t / lr loads issued first, off the epilogue path
+  const float* logits = nullptr;
+  long long hstep = 0;
+  if (hmode) {
+    hstep = *HD.step + HD.step_off;
+    logits = HD.logits2 + (long long)(hstep & 1) * P.M * HD.C;
+    if ((int)blockIdx.x == args.head_block) {  // zero the other buffer + next metric slot
+      float* nxt = HD.logits2 + (long long)((hstep + 1) & 1) * P.M * HD.C;
+      for (int i = threadIdx.x; i < P.M * HD.C; i += 256) nxt[i] = 0.f;
+      if (threadIdx.x == 0 && HD.hist_len > 1) {
+        const int ns = (int)(hstep + 1) & (HD.hist_len - 1);
+        HD.loss_acc[ns] = 0.f;
+        HD.correct_acc[ns] = 0;
+      }
+    }
+  }
 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   f32x4 accb = {0.f, 0.f, 0.f, 0.f};
   float pw[4], mw[4], vw[4], pb[4], mb[4], vb[4];
   for (int mc0 = 0; mc0 < P.M; mc0 += kMC) {
     const int mcn = min(kMC, P.M - mc0);
-    // (1) issue the chunk's loads: gathered X items; the dZ slice [m][16 n] -- or, in head mode,
-    //     the mask slice of H plus the dlogits rows and the W2 slice it is recomputed from
+    // (1) issue the chunk's loads
     float4 xv[kXItems];
     if (P.xt == 1) load_x_items<1>(P, gt, mc0, mcn, k0, xv);
     else load_x_items<0>(P, gt, mc0, mcn, k0, xv);
     float4 zv[kZItems];
-    constexpr int kDItems = (kMC * 16) / 256;
     float dv[kDItems];
-    float wv = 0.f;
-    if (!head) {
+    float wv = 0.f, bv = 0.f;
+    int yv = 0;
+    if (hmode == 0) {
 #pragma unroll
       for (int i = 0; i < kZItems; ++i) {
         const int t = threadIdx.x + 256 * i;
@@ -433,21 +472,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
         }
       }
     } else {
-      const int C = P.hd_c;
+      const int C = HD.C;
 #pragma unroll
-      for (int i = 0; i < kZItems; ++i) {  // mask source (post-dropout activation)
+      for (int i = 0; i < kDItems; ++i) {  // raw logits rows: item t -> (m = t>>4, c = t&15)
         const int t = threadIdx.x + 256 * i;
-        const int rr = min(t >> 2, mcn - 1), q = t & 3;
-        zv[i] = *reinterpret_cast<const float4*>(P.hd_h + (long long)(mc0 + rr) * P.N +
-                                                 min(n0 + 4 * q, P.N - 4));
+        dv[i] = logits[(long long)(mc0 + min(t >> 4, mcn - 1)) * C + min(t & 15, C - 1)];
       }
+      if ((int)threadIdx.x < kMC)
+        yv = load_label(HD.lab, gather_row(make_gather(HD.lab), mc0 + min((int)threadIdx.x, mcn - 1)));
+      bv = HD.b2 ? HD.b2[min((int)threadIdx.x & 15, C - 1)] : 0.f;
+      if (hmode == 2) {
 #pragma unroll
-      for (int i = 0; i < kDItems; ++i) {  // dlogits rows: item t -> (m = t>>4, c = t&15)
-        const int t = threadIdx.x + 256 * i;
-        dv[i] = P.hd_dl[(long long)(mc0 + min(t >> 4, mcn - 1)) * C + min(t & 15, C - 1)];
+        for (int i = 0; i < kZItems; ++i) {  // mask source (post-dropout activation)
+          const int t = threadIdx.x + 256 * i;
+          const int rr = min(t >> 2, mcn - 1), q = t & 3;
+          zv[i] = *reinterpret_cast<const float4*>(P.hd_h + (long long)(mc0 + rr) * P.N +
+                                                   min(n0 + 4 * q, P.N - 4));
+        }
+        wv = P.hd_w2[(long long)min((int)threadIdx.x >> 4, C - 1) * P.N +
+                     min(n0 + ((int)threadIdx.x & 15), P.N - 1)];
       }
-      wv = P.hd_w2[(long long)min((int)threadIdx.x >> 4, C - 1) * P.N +
-                   min(n0 + ((int)threadIdx.x & 15), P.N - 1)];
     }
     // (2) on the first chunk, prefetch the tile's Adam state behind them (in-order vmcnt lets the
     //     staging waits below leave these in flight through the K-loop)
@@ -473,40 +517,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
       const float4 o = (k0 + 4 * q < P.K) ? xv[i] : make_float4(0.f, 0.f, 0.f, 0.f);
       *reinterpret_cast<float4*>(&Xs[rr * kXsStride + 4 * q]) = o;
     }
-    if (head) {
-      const int C = P.hd_c;
-#pragma unroll
-      for (int i = 0; i < kDItems; ++i) {
-        const int t = threadIdx.x + 256 * i;
-        Ds[t] = ((t & 15) < C) ? dv[i] : 0.f;
-      }
-      W2s[threadIdx.x] = (((int)threadIdx.x >> 4) < C) ? wv : 0.f;
-      lds_barrier();
-      // dz = (dlogits · W2[:, n-slice]) ⊙ mask, straight into the Zs image
-#pragma unroll
-      for (int i = 0; i < kZItems; ++i) {
-        const int t = threadIdx.x + 256 * i;
-        const int rr = t >> 2, q = t & 3;
-        float z[4] = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int cc = 0; cc < 16; ++cc) {
-          const float d = Ds[rr * 16 + cc];
-          const float4 w4 = *reinterpret_cast<const float4*>(&W2s[cc * 16 + 4 * q]);
-          z[0] += d * w4.x; z[1] += d * w4.y; z[2] += d * w4.z; z[3] += d * w4.w;
-        }
-        const float4 hm = zv[i];
-        const float ik = P.hd_inv_keep;
-        float4 o = make_float4(hm.x > 0.f ? z[0] * ik : 0.f, hm.y > 0.f ? z[1] * ik : 0.f,
-                               hm.z > 0.f ? z[2] * ik : 0.f, hm.w > 0.f ? z[3] * ik : 0.f);
-        const int n = n0 + 4 * q;
-        o.x = (n + 0 < P.N) ? o.x : 0.f;
-        o.y = (n + 1 < P.N) ? o.y : 0.f;
-        o.z = (n + 2 < P.N) ? o.z : 0.f;
-        o.w = (n + 3 < P.N) ? o.w : 0.f;
-        if (rr >= mcn) o = make_float4(0.f, 0.f, 0.f, 0.f);
-        *reinterpret_cast<float4*>(&Zs[rr * 16 + 4 * q]) = o;
-      }
-    } else {
+    if (hmode == 0) {
 #pragma unroll
       for (int i = 0; i < kZItems; ++i) {
         const int t = threadIdx.x + 256 * i;
@@ -520,10 +531,84 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
         if (rr >= mcn) o = make_float4(0.f, 0.f, 0.f, 0.f);
         *reinterpret_cast<float4*>(&Zs[rr * 16 + 4 * q]) = o;
       }
+    } else {
+      const int C = HD.C;
+#pragma unroll
+      for (int i = 0; i < kDItems; ++i) Ds[threadIdx.x + 256 * i] = dv[i];
+      if ((int)threadIdx.x < kMC) Ys[threadIdx.x] = yv;
+      if (threadIdx.x < 16) B2s[threadIdx.x] = bv;
+      W2s[threadIdx.x] = (((int)threadIdx.x >> 4) < C) ? wv : 0.f;
+      lds_barrier();
+      // softmax-xent per row (thread = row): Ds row -> dlogits; block 0 also records metrics
+      float loss = 0.f, corr = 0.f;
+      if ((int)threadIdx.x < mcn) {
+        float* row = &Ds[threadIdx.x * 16];
+        const int y = Ys[threadIdx.x];
+        float lgv[16];
+        float mx = -INFINITY;
+        int arg = 0;
+#pragma unroll
+        for (int cc = 0; cc < 16; ++cc) {
+          lgv[cc] = row[cc] + B2s[cc];
+          const bool better = cc < C && lgv[cc] > mx;
+          mx = better ? lgv[cc] : mx;
+          arg = better ? cc : arg;
+        }
+        float se = 0.f;
+#pragma unroll
+        for (int cc = 0; cc < 16; ++cc) se += (cc < C) ? expf(lgv[cc] - mx) : 0.f;
+        const float lse = mx + logf(se);
+        float ly = 0.f;
+#pragma unroll
+        for (int cc = 0; cc < 16; ++cc) {
+          ly = (cc == y) ? lgv[cc] : ly;
+          row[cc] = (cc < C) ? (expf(lgv[cc] - lse) - (cc == y ? 1.f : 0.f)) * HD.loss_scale : 0.f;
+        }
+        loss = (lse - ly) * HD.loss_scale;
+        corr = (arg == y) ? 1.f : 0.f;
+      }
+      if ((int)blockIdx.x == args.head_block) {
+        const float ls = wave_sum_fast(loss), cs = wave_sum_fast(corr);
+        if (lane == 0 && w * 64 < mcn) {
+          const int slot = (int)hstep & (HD.hist_len - 1);
+          atomicAdd(&HD.loss_acc[slot], ls);
+          atomicAdd(&HD.correct_acc[slot], (int)(cs + 0.5f));
+        }
+      }
+      lds_barrier();
+      // derive dZ for this tile into the Zs image
+#pragma unroll
+      for (int i = 0; i < kZItems; ++i) {
+        const int t = threadIdx.x + 256 * i;
+        const int rr = t >> 2, q = t & 3;
+        const int n = n0 + 4 * q;
+        float z[4];
+        if (hmode == 1) {  // output layer: dz = dlogits (N == C <= 16, single n tile)
+          const float4 d4 = *reinterpret_cast<const float4*>(&Ds[rr * 16 + 4 * q]);
+          z[0] = d4.x; z[1] = d4.y; z[2] = d4.z; z[3] = d4.w;
+        } else {           // hidden layer: dz = (dlogits · W2) ⊙ (h > 0) / keep
+          z[0] = z[1] = z[2] = z[3] = 0.f;
+#pragma unroll
+          for (int cc = 0; cc < 16; ++cc) {
+            const float d = Ds[rr * 16 + cc];
+            const float4 w4 = *reinterpret_cast<const float4*>(&W2s[cc * 16 + 4 * q]);
+            z[0] += d * w4.x; z[1] += d * w4.y; z[2] += d * w4.z; z[3] += d * w4.w;
+          }
+          const float4 hm = zv[i];
+          const float ik = P.hd_inv_keep;
+          z[0] = hm.x > 0.f ? z[0] * ik : 0.f;
+          z[1] = hm.y > 0.f ? z[1] * ik : 0.f;
+          z[2] = hm.z > 0.f ? z[2] * ik : 0.f;
+          z[3] = hm.w > 0.f ? z[3] * ik : 0.f;
+        }
+        float4 o = make_float4((n + 0 < P.N) ? z[0] : 0.f, (n + 1 < P.N) ? z[1] : 0.f,
+                               (n + 2 < P.N) ? z[2] : 0.f, (n + 3 < P.N) ? z[3] : 0.f);
+        if (rr >= mcn) o = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(&Zs[rr * 16 + 4 * q]) = o;
+      }
     }
     lds_barrier();
-    // (4) K-loop over all kMC rows of the image (rows >= mcn: Zs zero, Xs finite), fully
-    //     unrolled so every LDS read is issued ahead of its MFMA
+    // (4) K-loop over all kMC rows of the image (rows >= mcn: Zs zero, Xs finite)
     if (mcn > kMC / 2) {
 #pragma unroll 8
       for (int s = 0; s < kMC / 4; ++s) {
@@ -583,54 +668,38 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
 }
 
 // ---------------------------------------------------------------------------------------------
-// mlp_fwd_head: linear_fwd of the hidden layer with the loss head fused in.
-// Each (m-tile, n-tile) workgroup computes its 16x16 H tile (bias, ReLU, dropout), stores it, and
-// multiplies it by the matching 16-column slice of W2 -> a 16 x C partial-logit slab. The LAST
-// workgroup to finish an m-tile (agent-scope release -> arrival counter -> acquire; placement-
-// independent, cdna_hip_programming.md §6 G16) sums the slabs in a fixed order (bitwise
-// reproducible), and runs softmax-cross-entropy for its 16 rows: loss/accuracy into the metric
-// ring, dlogits for the backward pass. One launch replaces linear_fwd + xent_head.
+// mlp_fwd_logits: linear_fwd of the hidden layer (bias, ReLU, dropout) that also emits the
+// output layer's logits: each (m, n) tile multiplies its 16x16 H tile by the matching 16-column
+// slice of W2 and atomically adds the 16 x C partial into logits2[step&1] (no-return f32 atomics;
+// 32 hidden tiles per logit, so the sum order -- and the last bit -- may vary run to run). The
+// m-tile-0 workgroups also snapshot W2 for the backward pass (which updates W2 in place). The
+// softmax itself is recomputed by every wgrad workgroup: no intra-kernel hand-off anywhere.
 // ---------------------------------------------------------------------------------------------
 template <int XT, int WAVES>
-__global__ __launch_bounds__(WAVES * 64) void mlp_fwd_head_kernel(
+__global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
     ArenaRowSource src, const float* __restrict__ W, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int K, uint32_t keep_thr, float inv_keep, uint32_t seed,
-    const long long* step_src, ArenaFwdHead hd, ArenaCounterOp ctr) {
+    const long long* step_src, const float* __restrict__ W2, float* __restrict__ W2_copy, int C,
+    float* __restrict__ logits2, ArenaCounterOp ctr) {
   constexpr int CH = 8;
   const int lane = lane_id(), w = wave_id();
   const int g = lane >> 4, c = lane & 15;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
-  const int ntiles = gridDim.x;
-  const int C = hd.C;
   const int rowc = min(m0 + c, M - 1), colc = min(n0 + c, N - 1);
   const Gather gt = make_gather(src);
-  const uint32_t step = step_src ? (uint32_t)(*step_src) : 0u;
+  const long long stepv = step_src ? *step_src : 0;
+  const uint32_t step = (uint32_t)stepv;
   const long long prow = gather_row(gt, rowc);
   const float* wrow = W + (long long)colc * K;
-  // W2 slice [C][16] for the partial logits (thread t < 256: c = t>>4, n = t&15)
   __shared__ float w2s[16][17];
   __shared__ float hs[16][17];
-  __shared__ float red[WAVES][16][17];  // WAVES*16*17 >= 4 * 16 * C floats (tail scratch)
-  __shared__ float lg[16][17];
-  __shared__ int s_last;
-  float w2v = 0.f;
-  if (threadIdx.x < 256)
-    w2v = hd.W2[(long long)min((int)threadIdx.x >> 4, C - 1) * N + min(n0 + ((int)threadIdx.x & 15), N - 1)];
-  // labels of this m-tile, prefetched by wave 0 (used only if this block is the last arriver)
-  int y_pre = 0;
-  if (threadIdx.x < 64) {
-    const long long pr = gather_row(make_gather(hd.lab), min(m0 + (int)(threadIdx.x & 15), M - 1));
-    if (hd.lab.dtype == 1) y_pre = (int)static_cast<const uint8_t*>(hd.lab.ptr)[pr];
-    else if (hd.lab.dtype == 2) y_pre = static_cast<const int*>(hd.lab.ptr)[pr];
-    else y_pre = (int)static_cast<const long long*>(hd.lab.ptr)[pr];
+  __shared__ float red[WAVES][16][17];
+  float w2v = 0.f, bv = 0.f;
+  if (threadIdx.x < 256) {
+    w2v = W2[(long long)min((int)threadIdx.x >> 4, C - 1) * N + min(n0 + ((int)threadIdx.x & 15), N - 1)];
+    bv = bias[min(n0 + ((int)threadIdx.x & 15), N - 1)];
   }
   counter_op(ctr);
-  if (hd.hist_len > 1 && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
-    const long long hs0 = hd.hist_step ? *hd.hist_step : 0;
-    const int nxt = (int)(hs0 + 1) & (hd.hist_len - 1);
-    hd.loss_acc[nxt] = 0.f;
-    hd.correct_acc[nxt] = 0;
-  }
 
   const int nsteps = (K + 15) >> 4;
   const int s0 = (nsteps * w) / WAVES, s1 = (nsteps * (w + 1)) / WAVES;
@@ -661,15 +730,15 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_head_kernel(
   }
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[w][4 * g + r][c] = acc[r];
-  if (threadIdx.x < 256) w2s[threadIdx.x >> 4][threadIdx.x & 15] = ((int)(threadIdx.x >> 4) < C) ? w2v : 0.f;
+  if (threadIdx.x < 256)
+    w2s[threadIdx.x >> 4][threadIdx.x & 15] = ((int)(threadIdx.x >> 4) < C) ? w2v : 0.f;
   __syncthreads();
   if (threadIdx.x < 256) {
     const int rr = threadIdx.x >> 4, cc = threadIdx.x & 15;
     const int gm = m0 + rr, gn = n0 + cc;
-    float v = 0.f;
+    float v = bv;
 #pragma unroll
     for (int ww = 0; ww < WAVES; ++ww) v += red[ww][rr][cc];
-    v += bias[min(gn, N - 1)];
     v = fmaxf(v, 0.f);
     if (keep_thr != 0xFFFFFFFFu) {
       const uint32_t h = hash4(seed, step, (uint32_t)gm, (uint32_t)gn);
@@ -678,97 +747,17 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_head_kernel(
     const bool ok = gm < M && gn < N;
     if (ok) Y[(long long)gm * N + gn] = v;
     hs[rr][cc] = ok ? v : 0.f;
+    if (W2_copy != nullptr && blockIdx.y == 0 && rr < C && gn < N)
+      W2_copy[(long long)rr * N + gn] = w2v;  // thread (rr, cc) holds W2[rr][n0 + cc]
   }
   __syncthreads();
-  // partial logits of this tile: slab[mt][nt][r][cl] = Σ_n hs[r][n] * W2[cl][n0+n], stored
-  // write-through (agent-scope relaxed atomic stores = sc1): no release fence / L2 writeback needed
-  float* slab = hd.slabs + ((long long)blockIdx.y * ntiles + blockIdx.x) * 16 * C;
+  float* lg = logits2 + (long long)(stepv & 1) * M * C;
   if ((int)threadIdx.x < 16 * C) {
     const int rr = threadIdx.x / C, cl = threadIdx.x % C;
     float p = 0.f;
 #pragma unroll
     for (int n = 0; n < 16; ++n) p += hs[rr][n] * w2s[cl][n];
-    __hip_atomic_store(&slab[threadIdx.x], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  // ---- arrival: drain the write-through stores, count; the last arriver finishes the m-tile ----
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int prev = __hip_atomic_fetch_add(&hd.counters[blockIdx.y], 1, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_AGENT);
-    s_last = (prev == ntiles - 1);
-  }
-  __syncthreads();
-  if (!s_last) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // compiler-only: keep loads below
-  if (threadIdx.x == 0)
-    __hip_atomic_store(&hd.counters[blockIdx.y], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  // slab reduction: S threads per (row, class), each summing every S-th tile with all its loads in
-  // flight at once (sc1 loads: every read of handed-off bytes bypasses this CU's stale L1), then a
-  // fixed-order combine -> bitwise reproducible logits
-  const float* mslab = hd.slabs + (long long)blockIdx.y * ntiles * 16 * C;
-  const int pairs = 16 * C;
-  const int S = min(4, (int)blockDim.x / pairs);
-  constexpr int kRedLoads = 16;
-  if ((int)threadIdx.x < pairs * S) {
-    const int pr = threadIdx.x % pairs, q = threadIdx.x / pairs;
-    float sacc = 0.f;
-    for (int base = q; base < ntiles; base += S * kRedLoads) {
-      float v[kRedLoads];
-#pragma unroll
-      for (int j = 0; j < kRedLoads; ++j) {
-        const int nt = min(base + j * S, ntiles - 1);
-        v[j] = __hip_atomic_load(&mslab[(long long)nt * pairs + pr], __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int j = 0; j < kRedLoads; ++j) sacc += (base + j * S < ntiles) ? v[j] : 0.f;
-    }
-    red[q][pr / 16][pr % 16] = sacc;  // red is free again: reuse as [S][pairs] scratch
-  }
-  __syncthreads();
-  if ((int)threadIdx.x < pairs) {
-    const int rr = threadIdx.x / C, cl = threadIdx.x % C;
-    float sacc = hd.b2 ? hd.b2[cl] : 0.f;
-    for (int q = 0; q < S; ++q) sacc += red[q][threadIdx.x / 16][threadIdx.x % 16];
-    lg[rr][cl] = sacc;
-  }
-  __syncthreads();
-  if (threadIdx.x < 64) {  // wave 0: lane r < 16 owns row m0 + r
-    const int r = threadIdx.x;
-    const int gm = m0 + r;
-    const bool ok = r < 16 && gm < M;
-    float loss = 0.f;
-    int correct = 0;
-    if (ok) {
-      const int y = y_pre;
-      float mx = lg[r][0];
-      int arg = 0;
-      for (int cl = 1; cl < C; ++cl) {
-        const float v = lg[r][cl];
-        if (v > mx) { mx = v; arg = cl; }
-      }
-      float se = 0.f;
-      for (int cl = 0; cl < C; ++cl) se += expf(lg[r][cl] - mx);
-      const float lse = mx + logf(se);
-      float ly = 0.f;
-      for (int cl = 0; cl < C; ++cl) ly = (cl == y) ? lg[r][cl] : ly;
-      loss = (lse - ly) * hd.loss_scale;
-      correct = (arg == y) ? 1 : 0;
-      if (hd.dlogits) {
-        for (int cl = 0; cl < C; ++cl)
-          hd.dlogits[(long long)gm * C + cl] =
-              (expf(lg[r][cl] - lse) - (cl == y ? 1.f : 0.f)) * hd.loss_scale;
-      }
-    }
-    const float lsum = wave_sum_fast(loss);
-    const float csum = wave_sum_fast((float)correct);
-    if (threadIdx.x == 0) {
-      const long long hs0 = hd.hist_step ? *hd.hist_step : 0;
-      const int slot = (int)hs0 & (hd.hist_len - 1);
-      atomicAdd(&hd.loss_acc[slot], lsum);
-      atomicAdd(&hd.correct_acc[slot], (int)(csum + 0.5f));
-    }
+    if (m0 + rr < M) atomicAdd(&lg[(long long)(m0 + rr) * C + cl], p);
   }
 }
 
@@ -893,11 +882,11 @@ hipError_t arena_linear_fwd(ArenaRowSource src, const float* W, const float* bia
   return hipGetLastError();
 }
 
-hipError_t arena_mlp_fwd_head(ArenaRowSource src, const float* W, const float* bias, float* Y, int M,
-                              int N, int K, float keep_prob, uint32_t seed,
-                              const long long* step_src, ArenaFwdHead hd, ArenaCounterOp ctr,
-                              hipStream_t stream) {
-  if (hd.C < 1 || hd.C > 16 || K % 4) return hipErrorInvalidValue;
+hipError_t arena_mlp_fwd_logits(ArenaRowSource src, const float* W, const float* bias, float* Y,
+                                int M, int N, int K, float keep_prob, uint32_t seed,
+                                const long long* step_src, const float* W2, float* W2_copy, int C,
+                                float* logits2, ArenaCounterOp ctr, hipStream_t stream) {
+  if (C < 1 || C > 16 || K % 4) return hipErrorInvalidValue;
   uint32_t thr = 0xFFFFFFFFu;
   float inv_keep = 1.f;
   if (keep_prob < 1.f) {
@@ -906,11 +895,11 @@ hipError_t arena_mlp_fwd_head(ArenaRowSource src, const float* W, const float* b
   }
   dim3 grid((N + 15) / 16, (M + 15) / 16);
   if (src.dtype == 1)
-    hipLaunchKernelGGL((mlp_fwd_head_kernel<1, 8>), grid, dim3(512), 0, stream, src, W, bias, Y, M,
-                       N, K, thr, inv_keep, seed, step_src, hd, ctr);
+    hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8>), grid, dim3(512), 0, stream, src, W, bias, Y,
+                       M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2, ctr);
   else
-    hipLaunchKernelGGL((mlp_fwd_head_kernel<0, 8>), grid, dim3(512), 0, stream, src, W, bias, Y, M,
-                       N, K, thr, inv_keep, seed, step_src, hd, ctr);
+    hipLaunchKernelGGL((mlp_fwd_logits_kernel<0, 8>), grid, dim3(512), 0, stream, src, W, bias, Y,
+                       M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2, ctr);
   return hipGetLastError();
 }
 
@@ -945,7 +934,8 @@ hipError_t arena_xent_head(const float* H, int M, int D, const float* W2, const 
 }
 
 hipError_t arena_wgrad_grouped(ArenaWGradProblem* probs, int nprob, ArenaAdam adam,
-                               float grad_scale, ArenaCounterOp ctr, hipStream_t stream) {
+                               float grad_scale, ArenaCounterOp ctr, ArenaHead head,
+                               hipStream_t stream) {
   if (nprob < 1 || nprob > kMaxProblems) return hipErrorInvalidValue;
   WGradArgs a;
   int blocks = 0;
@@ -957,9 +947,13 @@ hipError_t arena_wgrad_grouped(ArenaWGradProblem* probs, int nprob, ArenaAdam ad
     a.p[i] = probs[i];
   }
   a.nprob = nprob;
+  a.head_block = -1;
+  for (int i = 0; i < nprob; ++i)
+    if (probs[i].hd_mode != 0) { a.head_block = probs[i].block_begin; break; }
   a.adam = adam;
   a.grad_scale = grad_scale;
   a.ctr = ctr;
+  a.head = head;
   hipLaunchKernelGGL(wgrad_grouped_kernel, dim3(blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }

@@ -190,74 +190,80 @@ def test_fused_linear_autograd(cuda):
 
 
 @pytest.mark.parametrize("M,N,C", [(100, 500, 10), (37, 100, 10), (16, 64, 3)])
-def test_mlp_fwd_head_matches_reference(cuda, M, N, C):
+def test_mlp_fwd_logits_matches_reference(cuda, M, N, C):
     g = torch.Generator().manual_seed(N + C)
     data = torch.randint(0, 256, (400, 784), generator=g, dtype=torch.uint8).to(cuda)
-    labels = torch.randint(0, C, (400,), generator=g, dtype=torch.uint8).to(cuda)
     idx = torch.randperm(400, generator=g).to(torch.int32).to(cuda)
     W1 = (torch.randn(N, 784, generator=g) * 0.05).to(cuda)
     b1 = (torch.randn(N, generator=g) * 0.1).to(cuda)
     W2 = (torch.randn(C, N, generator=g) * 0.1).to(cuda)
-    b2 = torch.randn(C, generator=g).to(cuda)
     out = {}
     for impl in ("hip", "ref"):
         A = torch.tensor([3], dtype=torch.int64, device=cuda)
         Bc = torch.zeros(1, dtype=torch.int64, device=cuda)
         H = torch.empty(M, N, device=cuda)
-        dl = torch.empty(M, C, device=cuda)
         w2c = torch.empty(C, N, device=cuda)
-        la = torch.zeros(4, device=cuda)
-        ca = torch.zeros(4, dtype=torch.int32, device=cuda)
-        slabs, cnt = ops.mlp_fwd_head_workspace(M, N, C, cuda)
-        args = (data, 1 / 255.0, idx, A, M, W1, b1, H, 0.9, 77, A, W2, b2, labels, slabs, cnt, dl,
-                w2c, 1.0 / M, la, ca, A, Bc, A, 1)
-        for _ in range(3 if impl == "hip" else 1):  # repeated launches: counters self-reset
-            if impl == "hip":
-                la.zero_()
-                ca.zero_()
-                from arena_amd.ops import _ext
-                _ext.load().mlp_fwd_head(*args)
-            else:
-                ref.mlp_fwd_head(*args)
+        lg2 = torch.zeros(2, M, C, device=cuda)
+        args = (data, 1 / 255.0, idx, A, M, W1, b1, H, 0.9, 77, A, W2, w2c, lg2, Bc, A, 1)
+        if impl == "hip":
+            from arena_amd.ops import _ext
+            _ext.load().mlp_fwd_logits(*args)
+        else:
+            ref.mlp_fwd_logits(*args)
         torch.cuda.synchronize()
-        out[impl] = (H, dl, la, ca, Bc, w2c, cnt)
+        out[impl] = (H, lg2, Bc, w2c)
     h, r = out["hip"], out["ref"]
     _close(h[0], r[0])
-    _close(h[1], r[1])
-    _close(h[2], r[2], rtol=1e-4, atol=1e-5)
-    assert torch.equal(h[3].cpu(), r[3].cpu())
-    assert int(h[4].item()) == 4
-    _close(h[5], W2)
-    assert int(h[6].abs().sum().item()) == 0
+    _close(h[1], r[1], rtol=1e-4, atol=1e-4)
+    assert float(h[1][0].abs().sum()) == 0.0  # step 3 -> buffer 1 only
+    assert int(h[2].item()) == 4
+    _close(h[3], W2)
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-def test_wgrad_head_recompute(cuda, mode):
+def test_wgrad_head_modes(cuda, mode):
+    """Both layers' grads from raw logits (softmax recomputed per workgroup) vs the reference."""
     g = torch.Generator().manual_seed(10 + mode)
     M, N, K, C = 100, 500, 784, 10
     data = torch.randint(0, 256, (300, K), generator=g, dtype=torch.uint8).to(cuda)
+    labels = torch.randint(0, C, (300,), generator=g, dtype=torch.uint8).to(cuda)
     idx = torch.randperm(300, generator=g).to(torch.int32).to(cuda)
-    cur = torch.tensor([2], dtype=torch.int64, device=cuda)
     Hh = torch.relu(torch.randn(M, N, generator=g)).to(cuda)
     Hh[Hh < 0.3] = 0.0
-    dl = (torch.randn(M, C, generator=g) * 0.01).to(cuda)
-    W2 = (torch.randn(C, N, generator=g) * 0.1).to(cuda)
+    W2c = (torch.randn(C, N, generator=g) * 0.1).to(cuda)
+    lg0 = torch.randn(M, C, generator=g).to(cuda)
+    b2v = torch.randn(C, generator=g).to(cuda)
     res = {}
     for impl in ("hip", "ref"):
+        cur = torch.tensor([6], dtype=torch.int64, device=cuda)  # B counter: step index 5
+        lg2 = torch.zeros(2, M, C, device=cuda)
+        lg2[1] = lg0
+        lg2[0] = 7.0  # must be zeroed by the launch
         W1 = torch.randn(N, K, generator=torch.Generator().manual_seed(1)).to(cuda) * 0.01
+        W2 = torch.randn(C, N, generator=torch.Generator().manual_seed(2)).to(cuda) * 0.01
         b1 = torch.zeros(N, device=cuda)
-        mW, vW = torch.full_like(W1, 1e-3), torch.full_like(W1, 1e-4)
-        mb, vb = torch.full_like(b1, 1e-3), torch.full_like(b1, 1e-4)
-        t = torch.tensor([7], dtype=torch.int64, device=cuda)
-        args = ([data], [1 / 255.0], [True], idx, cur, -1, M, [None], [dl], [W2], [Hh], 0.9, [0],
-                mode, [W1], [b1], [mW], [vW], [mb], [vb], 1e-3, None, 0.9, 0.999, 1e-8, 0.0, t,
-                1.0, False, None, None, 0)
+        b2 = b2v.clone()
+        st = [torch.full_like(t, 1e-3) for t in (W1, W2, b1, b2)] + \
+             [torch.full_like(t, 1e-4) for t in (W1, W2, b1, b2)]
+        la = torch.zeros(8, device=cuda)
+        ca = torch.zeros(8, dtype=torch.int32, device=cuda)
+        la[6] = 5.0
+        args = ([data, Hh], [1 / 255.0, 1.0], [True, False], idx, cur, -1, M, [None, None],
+                [2, 1], [W2c, None], [Hh, None], 0.9, lg2, cur, -1, b2v, labels, 1.0 / M, la,
+                ca, mode, [W1, W2], [b1, b2], [st[0], st[1]], [st[4], st[5]], [st[2], st[3]],
+                [st[6], st[7]], 1e-3, None, 0.9, 0.999, 1e-8, 0.0, cur, 1.0, False, None, None,
+                0)
         if impl == "hip":
             from arena_amd.ops import _ext
             _ext.load().wgrad_grouped(*args)
         else:
             ref.wgrad_grouped(*args)
         torch.cuda.synchronize()
-        res[impl] = (W1, b1, mW, vW)
-    for a, b in zip(res["hip"], res["ref"]):
+        res[impl] = (W1, W2, b1, b2, la, ca, lg2)
+    h, r = res["hip"], res["ref"]
+    for a, b in zip(h[:4], r[:4]):
         _close(a, b, rtol=2e-4, atol=1e-6)
+    _close(h[4], r[4], rtol=1e-4, atol=1e-5)
+    assert float(h[4][6]) == 0.0  # next slot zeroed
+    assert torch.equal(h[5].cpu(), r[5].cpu())
+    assert float(h[6][0].abs().sum()) == 0.0  # next logits buffer zeroed
