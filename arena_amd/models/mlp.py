@@ -111,6 +111,8 @@ class FusedMLPTrainer:
         self.dlogits = torch.empty(B, C, device=dev)
         self.W2snap = torch.empty(C, H, device=dev)
         self.logits2 = torch.zeros(2, B, C, device=dev)  # step-parity double buffer
+        self.xb = torch.zeros(B, D, dtype=torch.uint8, device=dev)  # this step's gathered batch
+        self.yb = torch.zeros(B, dtype=torch.int32, device=dev)
         self.ctrA = torch.zeros(1, dtype=torch.int64, device=dev)
         self.ctrB = torch.zeros(1, dtype=torch.int64, device=dev)
         self.loss_hist = torch.zeros(cfg.hist_len, device=dev)
@@ -181,7 +183,8 @@ class FusedMLPTrainer:
         """Hidden layer + logits accumulation (one launch); writes B = A + 1."""
         cfg, B, A, Bc = self.cfg, self.cfg.batch, self.ctrA, self.ctrB
         ops.mlp_fwd_logits(self.train_x, self.W1, self.b1, self.Hbuf, self.W2, self.logits2,
-                           W2_copy=self.W2snap, x_scale=1.0 / 255.0, idx=self.perm, cursor=A,
+                           W2_copy=self.W2snap, xb=self.xb, labels=self.train_y, yb=self.yb,
+                           x_scale=1.0 / 255.0, idx=self.perm, cursor=A,
                            batch=B, keep_prob=cfg.keep_prob,
                            seed=cfg.seed * 2654435761 + self.rank, step=A, ctr_dst=Bc,
                            ctr_src=A, ctr_add=1)
@@ -191,14 +194,14 @@ class FusedMLPTrainer:
         the H mask) and dW2 in one launch. With ``adam`` the update is the epilogue (and A = B is
         committed), else the grads go to the flat all-reduce bucket."""
         cfg, B, A, Bc = self.cfg, self.cfg.batch, self.ctrA, self.ctrB
-        common = dict(x_scales=[1.0 / 255.0, 1.0], gather=[True, False], idx=self.perm,
-                      cursor=Bc, cursor_off=-1, batch=B, head_modes=[2, 1],
+        # the batch rows/labels published by the forward: no gather chain in the backward
+        common = dict(x_scales=[1.0 / 255.0, 1.0], gather=[False, False], head_modes=[2, 1],
                       head_w2=[self.W2snap, None], head_h=[self.Hbuf, None],
                       head_keep_prob=cfg.keep_prob, head_logits2=self.logits2, head_step=Bc,
-                      head_step_off=-1, head_b2=self.b2, head_labels=self.train_y,
+                      head_step_off=-1, head_b2=self.b2, head_labels=self.yb,
                       head_loss_scale=1.0 / B, head_loss_acc=self.loss_hist,
                       head_correct_acc=self.corr_hist)
-        xs, dzs = [self.train_x, self.Hbuf], [None, None]
+        xs, dzs = [self.xb, self.Hbuf], [None, None]
         if adam:
             ops.wgrad_grouped(xs, dzs, [self.W1, self.W2], [self.b1, self.b2], mode=1,
                               mW=[self.mW1, self.mW2], vW=[self.vW1, self.vW2],

@@ -41,7 +41,9 @@ def xent_head(H: Tensor, W2: Tensor, b2: Optional[Tensor], labels: Tensor, *,
 
 
 def mlp_fwd_logits(x: Tensor, W1: Tensor, b1: Tensor, H: Tensor, W2: Tensor, logits2: Tensor, *,
-                   W2_copy: Optional[Tensor] = None, x_scale: float = 1.0,
+                   W2_copy: Optional[Tensor] = None, xb: Optional[Tensor] = None,
+                   labels: Optional[Tensor] = None, yb: Optional[Tensor] = None,
+                   x_scale: float = 1.0,
                    idx: Optional[Tensor] = None, cursor: Optional[Tensor] = None, batch: int = 0,
                    keep_prob: float = 1.0, seed: int = 0, step: Optional[Tensor] = None,
                    ctr_dst: Optional[Tensor] = None, ctr_src: Optional[Tensor] = None,
@@ -49,10 +51,12 @@ def mlp_fwd_logits(x: Tensor, W1: Tensor, b1: Tensor, H: Tensor, W2: Tensor, log
     """H = dropout(relu(x·W1ᵀ+b1)) and logits2[step & 1] += H·W2ᵀ in ONE launch.
 
     ``logits2`` is [2, M, C]; the consuming wgrad (head mode) zeroes the other buffer each step.
+    With ``xb``/``labels``/``yb`` the gathered u8 batch rows and their labels are published for the
+    backward kernel (so it skips the cursor -> permutation -> row dependency chain).
     """
     _impl(H).mlp_fwd_logits(x, float(x_scale), idx, cursor, int(batch), W1, b1, H,
-                            float(keep_prob), int(seed), step, W2, W2_copy, logits2, ctr_dst,
-                            ctr_src, int(ctr_add))
+                            float(keep_prob), int(seed), step, W2, W2_copy, logits2, xb, labels, yb,
+                            ctr_dst, ctr_src, int(ctr_add))
 
 
 def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Optional[Tensor]], outW: Sequence[Tensor],

@@ -137,12 +137,16 @@ def head_dz(dl, w2, h, keep_prob):
 
 
 def mlp_fwd_logits(x, x_scale, idx, cursor, batch, W1, b1, H, keep_prob, seed, step, W2, W2_copy,
-                   logits2, ctr_dst, ctr_src, ctr_add):
+                   logits2, xb, labels, yb, ctr_dst, ctr_src, ctr_add):
     """Reference for the logits-emitting forward: H and logits2[step & 1] += H·W2ᵀ."""
     if ctr_dst is not None:
         src = int(ctr_src.reshape(-1)[0].item()) if ctr_src is not None else 0
         ctr_new = src + ctr_add
     linear_fwd(x, x_scale, idx, cursor, batch, W1, b1, H, 1, keep_prob, seed, step)
+    if xb is not None:
+        M = H.shape[0]
+        xb.copy_(gather_rows(x, idx, cursor, batch, M))
+        yb.copy_(gather_rows(labels, idx, cursor, batch, M).to(yb.dtype))
     if W2_copy is not None:
         W2_copy.view_as(W2).copy_(W2)
     st = int(step.reshape(-1)[0].item()) if step is not None else 0

@@ -14,7 +14,8 @@ hipError_t arena_linear_fwd(ArenaRowSource, const float*, const float*, float*, 
                             float, uint32_t, const long long*, hipStream_t);
 hipError_t arena_mlp_fwd_logits(ArenaRowSource, const float*, const float*, float*, int, int, int,
                                 float, uint32_t, const long long*, const float*, float*, int,
-                                float*, ArenaCounterOp, hipStream_t);
+                                float*, uint8_t*, const void*, int, int*, ArenaCounterOp,
+                                hipStream_t);
 hipError_t arena_xent_head(const float*, int, int, const float*, const float*, int, ArenaRowSource,
                            float*, float*, float, int, float, float*, int*, int, const long long*,
                            ArenaCounterOp, hipStream_t);
@@ -136,7 +137,8 @@ void linear_fwd(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch, 
 // the other buffer each step; zero both once at setup).
 void mlp_fwd_logits(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch, Tensor W1,
                     Tensor b1, Tensor H, double keep_prob, int64_t seed, OptT step, Tensor W2,
-                    OptT W2_copy, Tensor logits2, OptT ctr_dst, OptT ctr_src, int64_t ctr_add) {
+                    OptT W2_copy, Tensor logits2, OptT xb, OptT labels, OptT yb, OptT ctr_dst,
+                    OptT ctr_src, int64_t ctr_add) {
   for (auto* t : {&W1, &b1, &H, &W2, &logits2}) check_f32(*t, "mlp_fwd_logits operand");
   const int64_t M = H.size(0), N = H.size(1), K = W1.size(1), C = W2.size(0);
   TORCH_CHECK(W1.dim() == 2 && W1.size(0) == N && x.dim() == 2 && x.size(1) == K,
@@ -159,11 +161,34 @@ void mlp_fwd_logits(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t bat
     ctr.src = opt_i64_scalar(ctr_src, "ctr_src");
     ctr.add = (int)ctr_add;
   }
+  // optional publication of the gathered batch (u8 rows -> xb [M, K], labels -> yb [M] int32)
+  uint8_t* pxb = nullptr;
+  int* pyb = nullptr;
+  const void* plab = nullptr;
+  int lab_dtype = 0;
+  if (xb.has_value()) {
+    check_dev(*xb, "xb");
+    TORCH_CHECK(x.scalar_type() == torch::kUInt8 && xb->scalar_type() == torch::kUInt8 &&
+                    xb->numel() == M * K,
+                "xb must be uint8 [M, K] (u8 input only)");
+    TORCH_CHECK(labels.has_value() && yb.has_value(), "xb requires labels and yb");
+    check_dev(*labels, "labels");
+    check_dev(*yb, "yb");
+    TORCH_CHECK(yb->scalar_type() == torch::kInt32 && yb->numel() == M, "yb must be int32 [M]");
+    TORCH_CHECK(labels->dim() == 1 && labels->size(0) >= x.size(0) &&
+                    labels->scalar_type() != torch::kFloat32,
+                "labels must be integer [rows of x]");
+    pxb = xb->data_ptr<uint8_t>();
+    pyb = yb->data_ptr<int>();
+    plab = labels->data_ptr();
+    lab_dtype = dtype_code(*labels);
+  }
   ArenaRowSource s = make_src(x, x_scale, idx, cursor, batch, M, "x");
   check_hip(arena_mlp_fwd_logits(s, W1.data_ptr<float>(), b1.data_ptr<float>(),
                                  H.data_ptr<float>(), (int)M, (int)N, (int)K, (float)keep_prob,
                                  (uint32_t)seed, opt_i64_scalar(step, "step"), W2.data_ptr<float>(),
-                                 w2c, (int)C, logits2.data_ptr<float>(), ctr, cur_stream()),
+                                 w2c, (int)C, logits2.data_ptr<float>(), pxb, plab, lab_dtype, pyb,
+                                 ctr, cur_stream()),
             "mlp_fwd_logits");
 }
 

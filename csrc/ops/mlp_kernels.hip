@@ -399,6 +399,7 @@ __device__ __forceinline__ int load_label(const ArenaRowSource& lab, long long p
 //   D              : lane l, reg r -> dW[n0 + 4(l>>4) + r][k0 + 16w + (l&15)]   (coalesced rows)
 // >= 2 waves/SIMD so all 424 workgroups x 4 waves are co-resident in ONE round on 1024 SIMDs.
 // ---------------------------------------------------------------------------------------------
+template <int CB>  // compile-time bound on head classes (C <= CB): 10 (MNIST) or 16
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void wgrad_grouped_kernel(
     WGradArgs args) {
   __shared__ __attribute__((aligned(16))) float Xs[kMC * kXsStride];
@@ -544,25 +545,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
       if ((int)threadIdx.x < mcn) {
         float* row = &Ds[threadIdx.x * 16];
         const int y = Ys[threadIdx.x];
-        float lgv[16];
+        float lgv[CB];
         float mx = -INFINITY;
         int arg = 0;
 #pragma unroll
-        for (int cc = 0; cc < 16; ++cc) {
+        for (int cc = 0; cc < CB; ++cc) {
           lgv[cc] = row[cc] + B2s[cc];
           const bool better = cc < C && lgv[cc] > mx;
           mx = better ? lgv[cc] : mx;
           arg = better ? cc : arg;
         }
+        float pe[CB];
         float se = 0.f;
 #pragma unroll
-        for (int cc = 0; cc < 16; ++cc) se += (cc < C) ? expf(lgv[cc] - mx) : 0.f;
+        for (int cc = 0; cc < CB; ++cc) {
+          pe[cc] = (cc < C) ? expf(lgv[cc] - mx) : 0.f;
+          se += pe[cc];
+        }
+        const float inv = 1.f / se;
         const float lse = mx + logf(se);
         float ly = 0.f;
 #pragma unroll
-        for (int cc = 0; cc < 16; ++cc) {
+        for (int cc = 0; cc < CB; ++cc) {
           ly = (cc == y) ? lgv[cc] : ly;
-          row[cc] = (cc < C) ? (expf(lgv[cc] - lse) - (cc == y ? 1.f : 0.f)) * HD.loss_scale : 0.f;
+          row[cc] = (pe[cc] * inv - (cc == y ? 1.f : 0.f)) * HD.loss_scale;
         }
         loss = (lse - ly) * HD.loss_scale;
         corr = (arg == y) ? 1.f : 0.f;
@@ -589,7 +595,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
         } else {           // hidden layer: dz = (dlogits · W2) ⊙ (h > 0) / keep
           z[0] = z[1] = z[2] = z[3] = 0.f;
 #pragma unroll
-          for (int cc = 0; cc < 16; ++cc) {
+          for (int cc = 0; cc < CB; ++cc) {
             const float d = Ds[rr * 16 + cc];
             const float4 w4 = *reinterpret_cast<const float4*>(&W2s[cc * 16 + 4 * q]);
             z[0] += d * w4.x; z[1] += d * w4.y; z[2] += d * w4.z; z[3] += d * w4.w;
@@ -680,7 +686,8 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
     ArenaRowSource src, const float* __restrict__ W, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int K, uint32_t keep_thr, float inv_keep, uint32_t seed,
     const long long* step_src, const float* __restrict__ W2, float* __restrict__ W2_copy, int C,
-    float* __restrict__ logits2, ArenaCounterOp ctr) {
+    float* __restrict__ logits2, uint8_t* __restrict__ xb, const void* __restrict__ lab_ptr,
+    int lab_dtype, int* __restrict__ yb, ArenaCounterOp ctr) {
   constexpr int CH = 8;
   const int lane = lane_id(), w = wave_id();
   const int g = lane >> 4, c = lane & 15;
@@ -691,6 +698,15 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
   const uint32_t step = (uint32_t)stepv;
   const long long prow = gather_row(gt, rowc);
   const float* wrow = W + (long long)colc * K;
+  // n-tile-0 workgroups publish the step's gathered batch (u8 rows + labels) so the backward
+  // kernel reads them directly instead of repeating the cursor -> index -> row chain
+  const bool publish = (xb != nullptr) && blockIdx.x == 0;
+  if (publish && w == 0 && g == 0 && m0 + c < M) {
+    const int y = (lab_dtype == 1) ? (int)static_cast<const uint8_t*>(lab_ptr)[prow]
+                : (lab_dtype == 2) ? static_cast<const int*>(lab_ptr)[prow]
+                                   : (int)static_cast<const long long*>(lab_ptr)[prow];
+    yb[m0 + c] = y;
+  }
   __shared__ float w2s[16][17];
   __shared__ float hs[16][17];
   __shared__ float red[WAVES][16][17];
@@ -706,13 +722,31 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int sb = s0; sb < s1; sb += CH) {
     float a[CH][4], b[CH][4];
+    uint32_t raw[CH];
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
       const int k = (sb + i) * 16 + 4 * g;
       const int kc = min(k, K - 4);
-      load4<XT>(src, prow, kc, a[i]);
+      if constexpr (XT == 1) {
+        raw[i] = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(src.ptr) +
+                                                    prow * (long long)src.ld + kc);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[i][j] = (float)((raw[i] >> (8 * j)) & 0xffu) * src.scale;
+      } else {
+        load4<XT>(src, prow, kc, a[i]);
+      }
       const float4 wv = *reinterpret_cast<const float4*>(wrow + kc);
       b[i][0] = wv.x; b[i][1] = wv.y; b[i][2] = wv.z; b[i][3] = wv.w;
+    }
+    if constexpr (XT == 1) {
+      if (publish && m0 + c < M) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int k = (sb + i) * 16 + 4 * g;
+          if (sb + i < s1 && k < K)  // stores only: the branch holds no load
+            *reinterpret_cast<uint32_t*>(xb + (long long)(m0 + c) * K + k) = raw[i];
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
@@ -885,7 +919,8 @@ hipError_t arena_linear_fwd(ArenaRowSource src, const float* W, const float* bia
 hipError_t arena_mlp_fwd_logits(ArenaRowSource src, const float* W, const float* bias, float* Y,
                                 int M, int N, int K, float keep_prob, uint32_t seed,
                                 const long long* step_src, const float* W2, float* W2_copy, int C,
-                                float* logits2, ArenaCounterOp ctr, hipStream_t stream) {
+                                float* logits2, uint8_t* xb, const void* lab_ptr, int lab_dtype,
+                                int* yb, ArenaCounterOp ctr, hipStream_t stream) {
   if (C < 1 || C > 16 || K % 4) return hipErrorInvalidValue;
   uint32_t thr = 0xFFFFFFFFu;
   float inv_keep = 1.f;
@@ -896,10 +931,12 @@ hipError_t arena_mlp_fwd_logits(ArenaRowSource src, const float* W, const float*
   dim3 grid((N + 15) / 16, (M + 15) / 16);
   if (src.dtype == 1)
     hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8>), grid, dim3(512), 0, stream, src, W, bias, Y,
-                       M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2, ctr);
+                       M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2, xb,
+                       lab_ptr, lab_dtype, yb, ctr);
   else
     hipLaunchKernelGGL((mlp_fwd_logits_kernel<0, 8>), grid, dim3(512), 0, stream, src, W, bias, Y,
-                       M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2, ctr);
+                       M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2, nullptr,
+                       lab_ptr, lab_dtype, yb, ctr);
   return hipGetLastError();
 }
 
@@ -954,7 +991,10 @@ hipError_t arena_wgrad_grouped(ArenaWGradProblem* probs, int nprob, ArenaAdam ad
   a.grad_scale = grad_scale;
   a.ctr = ctr;
   a.head = head;
-  hipLaunchKernelGGL(wgrad_grouped_kernel, dim3(blocks), dim3(256), 0, stream, a);
+  if (head.C <= 10)
+    hipLaunchKernelGGL(wgrad_grouped_kernel<10>, dim3(blocks), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(wgrad_grouped_kernel<16>, dim3(blocks), dim3(256), 0, stream, a);
   return hipGetLastError();
 }
 

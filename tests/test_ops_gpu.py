@@ -108,7 +108,8 @@ def test_wgrad_grouped(cuda, mode):
         t = torch.tensor([4], dtype=torch.int64, device=cuda)
         A = torch.zeros(1, dtype=torch.int64, device=cuda)
         args = ([data, Hh], [1 / 255.0, 1.0], [True, False], idx, cur, -1, 100, [dz1, dz2],
-                [None, None], [None, None], [None, None], 1.0, [0, 0], mode,
+                [0, 0], [None, None], [None, None], 1.0, None, None, 0, None, None, 1.0, None,
+                None, mode,
                 [W1, W2], [b1, b2], [st[0], st[1]], [st[4], st[5]], [st[2], st[3]],
                 [st[6], st[7]], 1e-3, None, 0.9, 0.999, 1e-8, 0.0, t, 0.5, False, A, t, 0)
         if impl == "hip":
@@ -204,15 +205,22 @@ def test_mlp_fwd_logits_matches_reference(cuda, M, N, C):
         H = torch.empty(M, N, device=cuda)
         w2c = torch.empty(C, N, device=cuda)
         lg2 = torch.zeros(2, M, C, device=cuda)
-        args = (data, 1 / 255.0, idx, A, M, W1, b1, H, 0.9, 77, A, W2, w2c, lg2, Bc, A, 1)
+        labels = torch.randint(0, C, (400,), generator=torch.Generator().manual_seed(5),
+                               dtype=torch.uint8).to(cuda)
+        xb = torch.zeros(M, 784, dtype=torch.uint8, device=cuda)
+        yb = torch.zeros(M, dtype=torch.int32, device=cuda)
+        args = (data, 1 / 255.0, idx, A, M, W1, b1, H, 0.9, 77, A, W2, w2c, lg2, xb, labels, yb,
+                Bc, A, 1)
         if impl == "hip":
             from arena_amd.ops import _ext
             _ext.load().mlp_fwd_logits(*args)
         else:
             ref.mlp_fwd_logits(*args)
         torch.cuda.synchronize()
-        out[impl] = (H, lg2, Bc, w2c)
+        out[impl] = (H, lg2, Bc, w2c, xb, yb)
     h, r = out["hip"], out["ref"]
+    assert torch.equal(h[4].cpu(), r[4].cpu())
+    assert torch.equal(h[5].cpu(), r[5].cpu())
     _close(h[0], r[0])
     _close(h[1], r[1], rtol=1e-4, atol=1e-4)
     assert float(h[1][0].abs().sum()) == 0.0  # step 3 -> buffer 1 only
