@@ -36,7 +36,8 @@ def test_graph_replay_equals_eager(cuda, small_data):
     a.train_steps(20)
     b.train_steps(20)
     torch.cuda.synchronize()
-    assert torch.equal(a.P, b.P)
+    # logits are accumulated with f32 atomics (order may differ run to run): equal to rounding
+    torch.testing.assert_close(a.P, b.P, rtol=1e-4, atol=1e-6)
     assert int(a.ctrA.item()) == 20
 
 
