@@ -14,6 +14,8 @@ BIN = os.path.join(HERE, "bin")
 
 TOOLS = {
     # name: (sources, extra flags)
+    "arena-supervisor": (["csrc/runtime/supervisor.cpp"], ["-Icsrc/runtime"]),
+    "arena-probe": (["csrc/runtime/probe.cpp"], ["-Icsrc/runtime"]),
 }
 
 
@@ -28,10 +30,21 @@ def build_native_tools(force: bool = False) -> list[str]:
     for name, (srcs, flags) in TOOLS.items():
         out = tool_path(name)
         paths = [os.path.join(ROOT, s) for s in srcs]
+        deps = paths + [os.path.join(ROOT, "csrc", "runtime", "json.h")]
         if not force and os.path.exists(out) and all(
-                os.path.getmtime(out) >= os.path.getmtime(p) for p in paths):
+                os.path.getmtime(out) >= os.path.getmtime(p) for p in deps):
             built.append(out)
             continue
-        subprocess.run([cxx, "-O2", "-std=c++17", "-Wall", "-o", out, *paths, *flags], check=True)
+        subprocess.run([cxx, "-O2", "-std=c++17", "-Wall", "-Wextra", "-o", out, *paths,
+                        *[f.replace("-Icsrc", "-I" + os.path.join(ROOT, "csrc")) for f in flags]],
+                       check=True)
         built.append(out)
     return built
+
+
+def ensure_tool(name: str) -> str:
+    """Path to a native tool, building it on first use (g++ only, seconds)."""
+    path = tool_path(name)
+    if not os.path.exists(path):
+        build_native_tools()
+    return path

@@ -91,7 +91,8 @@ class ClusterState:
                 created += [job, pod]
             elif kind == "StatefulSet":
                 ss = StatefulSet(meta=self._meta(md), replicas=int(spec.get("replicas", 0)),
-                                 template=spec.get("template") or {})
+                                 template={**(spec.get("template") or {}),
+                                           "serviceName": spec.get("serviceName", "")})
                 self.statefulsets[(ns, ss.name)] = ss
                 created.append(ss)
                 for i in range(ss.replicas):

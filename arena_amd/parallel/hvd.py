@@ -1,0 +1,240 @@
+"""Horovod-style data-parallel API on torch.distributed (RCCL over xGMI on MI355X, gloo on CPU).
+
+The reference's allreduce jobs run Horovod images (DistributedOptimizer
+gradient allreduce with a 64 MB tensor-fusion buffer, broadcast_global_variables(0), allgather).
+This module provides the same user-facing calls, designed for one process per GPU:
+
+    import arena_amd.parallel.hvd as hvd
+    hvd.init()                                   # env:// rendezvous (RANK/WORLD_SIZE/MASTER_*)
+    torch.cuda.set_device(hvd.local_rank())
+    hvd.broadcast_parameters(model.state_dict(), root_rank=0)
+    opt = hvd.DistributedOptimizer(opt, named_parameters=model.named_parameters())
+
+``DistributedOptimizer`` packs gradients into flat fp32 buckets with the native multi-tensor
+kernel as soon as each bucket's last gradient is produced (post-accumulate hooks), launches an
+async all_reduce per bucket so communication overlaps the rest of backward, and unpacks the
+averaged result (the 1/N scale fused into the unpack kernel) in ``step()``. Bucket size defaults
+to 32 MB: on a fully connected 8x MI355X node each ring hop is one ~153 GB/s xGMI link, so
+32-64 MB buckets amortise the per-collective latency while leaving several buckets to overlap.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Iterable, List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .. import ops
+
+_STATE = {"pg": None, "local_rank": 0, "local_size": 1}
+
+
+def init(backend: Optional[str] = None, timeout_s: float = 600.0):
+    """Initialise the default process group from the environment (idempotent)."""
+    if not dist.is_initialized():
+        if backend is None:
+            backend = "nccl" if torch.cuda.is_available() else "gloo"
+        import datetime
+        kwargs = {}
+        if backend == "nccl":
+            lr = int(os.environ.get("LOCAL_RANK", "0"))
+            torch.cuda.set_device(lr)
+            kwargs["device_id"] = torch.device("cuda", lr)
+        dist.init_process_group(backend, timeout=datetime.timedelta(seconds=timeout_s), **kwargs)
+    _STATE["local_rank"] = int(os.environ.get("LOCAL_RANK", "0"))
+    _STATE["local_size"] = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    return dist.group.WORLD
+
+
+def is_initialized() -> bool:
+    return dist.is_initialized()
+
+
+def rank() -> int:
+    return dist.get_rank() if dist.is_initialized() else 0
+
+
+def size() -> int:
+    return dist.get_world_size() if dist.is_initialized() else 1
+
+
+def local_rank() -> int:
+    return _STATE["local_rank"]
+
+
+def local_size() -> int:
+    return _STATE["local_size"]
+
+
+def shutdown() -> None:
+    if dist.is_initialized():
+        dist.destroy_process_group()
+
+
+def allreduce(tensor: torch.Tensor, average: bool = True, op=None) -> torch.Tensor:
+    """Out-of-place allreduce (Horovod semantics: returns a new tensor)."""
+    out = tensor.detach().clone()
+    allreduce_(out, average=average, op=op)
+    return out
+
+
+def allreduce_(tensor: torch.Tensor, average: bool = True, op=None) -> torch.Tensor:
+    if size() == 1:
+        return tensor
+    dist.all_reduce(tensor, op=op or dist.ReduceOp.SUM)
+    if average and (op is None or op == dist.ReduceOp.SUM):
+        tensor.div_(size())
+    return tensor
+
+
+def allgather(tensor: torch.Tensor) -> torch.Tensor:
+    """Concatenate along dim 0 across ranks (first dims may differ, like hvd.allgather)."""
+    if size() == 1:
+        return tensor.clone()
+    n = torch.tensor([tensor.shape[0]], device=tensor.device, dtype=torch.int64)
+    sizes = [torch.zeros_like(n) for _ in range(size())]
+    dist.all_gather(sizes, n)
+    mx = int(max(int(s.item()) for s in sizes))
+    pad = torch.zeros((mx,) + tuple(tensor.shape[1:]), device=tensor.device, dtype=tensor.dtype)
+    pad[: tensor.shape[0]] = tensor
+    outs = [torch.empty_like(pad) for _ in range(size())]
+    dist.all_gather(outs, pad)
+    return torch.cat([o[: int(s.item())] for o, s in zip(outs, sizes)], dim=0)
+
+
+def broadcast_(tensor: torch.Tensor, root_rank: int = 0) -> torch.Tensor:
+    if size() > 1:
+        dist.broadcast(tensor, root_rank)
+    return tensor
+
+
+def broadcast_parameters(params, root_rank: int = 0) -> None:
+    """Broadcast a state_dict / named_parameters / list of tensors from root (in place), packed
+    into one flat buffer per dtype so it is a handful of collectives, not one per tensor."""
+    if size() == 1:
+        return
+    if isinstance(params, dict):
+        tensors = list(params.values())
+    else:
+        tensors = [p[1] if isinstance(p, tuple) else p for p in params]
+    by_dtype: Dict[Tuple[torch.dtype, torch.device], List[torch.Tensor]] = {}
+    for t in tensors:
+        if torch.is_tensor(t):
+            by_dtype.setdefault((t.dtype, t.device), []).append(t)
+    for (dt, dev), ts in by_dtype.items():
+        flat = torch.cat([t.detach().reshape(-1) for t in ts])
+        dist.broadcast(flat, root_rank)
+        off = 0
+        with torch.no_grad():
+            for t in ts:
+                n = t.numel()
+                t.copy_(flat[off:off + n].view_as(t))
+                off += n
+
+
+def broadcast_optimizer_state(optimizer: torch.optim.Optimizer, root_rank: int = 0) -> None:
+    state = []
+    for group in optimizer.param_groups:
+        for p in group["params"]:
+            for v in optimizer.state.get(p, {}).values():
+                if torch.is_tensor(v):
+                    state.append(v)
+    broadcast_parameters(state, root_rank)
+
+
+class _Bucket:
+    def __init__(self, params: List[torch.nn.Parameter], device):
+        self.params = params
+        self.offsets = []
+        off = 0
+        for p in params:
+            self.offsets.append(off)
+            off += (p.numel() + 3) // 4 * 4
+        self.flat = torch.zeros(off, device=device, dtype=torch.float32)
+        self.pending = set(id(p) for p in params)
+        self.work = None
+
+
+class DistributedOptimizer:
+    """Wraps a torch optimizer: bucketed async gradient allreduce overlapped with backward."""
+
+    def __init__(self, optimizer: torch.optim.Optimizer, named_parameters=None,
+                 bucket_mb: float = 32.0, process_group=None):
+        self.opt = optimizer
+        self.pg = process_group
+        params = [p for _, p in named_parameters] if named_parameters is not None else \
+            [p for g in optimizer.param_groups for p in g["params"]]
+        params = [p for p in params if p.requires_grad]
+        if any(p.dtype != torch.float32 for p in params):
+            raise TypeError("DistributedOptimizer buckets are fp32 (master weights)")
+        # reverse registration order ~ the order gradients become ready in backward
+        cap = int(bucket_mb * 2**20 / 4)
+        self.buckets: List[_Bucket] = []
+        cur: List[torch.nn.Parameter] = []
+        n = 0
+        for p in reversed(params):
+            cur.append(p)
+            n += p.numel()
+            if n >= cap:
+                self.buckets.append(_Bucket(cur, p.device))
+                cur, n = [], 0
+        if cur:
+            self.buckets.append(_Bucket(cur, cur[0].device))
+        self._owner = {}
+        for b in self.buckets:
+            for p in b.params:
+                self._owner[id(p)] = b
+        self._hooks = []
+        if size() > 1:
+            for p in params:
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
+
+    @property
+    def param_groups(self):
+        return self.opt.param_groups
+
+    @property
+    def state(self):
+        return self.opt.state
+
+    def _launch(self, b: _Bucket) -> None:
+        grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in b.params]
+        ops.flatten_into([g.contiguous() for g in grads], b.offsets, b.flat, 1.0)
+        b.work = dist.all_reduce(b.flat, group=self.pg, async_op=True)
+
+    def _on_grad(self, p) -> None:
+        b = self._owner[id(p)]
+        b.pending.discard(id(p))
+        if not b.pending and b.work is None:
+            self._launch(b)
+
+    def synchronize(self) -> None:
+        if size() == 1:
+            return
+        inv = 1.0 / size()
+        for b in self.buckets:
+            if b.work is None:  # some grads never arrived (unused params): reduce anyway
+                self._launch(b)
+            b.work.wait()
+            grads = []
+            for p in b.params:
+                if p.grad is None:
+                    p.grad = torch.zeros_like(p)
+                grads.append(p.grad)
+            ops.unflatten_from(grads, b.offsets, b.flat, inv)
+            b.work = None
+            b.pending = set(id(p) for p in b.params)
+
+    def step(self, closure=None):
+        self.synchronize()
+        return self.opt.step(closure)
+
+    def zero_grad(self, set_to_none: bool = True):
+        self.opt.zero_grad(set_to_none=set_to_none)
+
+    def state_dict(self):
+        return self.opt.state_dict()
+
+    def load_state_dict(self, sd):
+        self.opt.load_state_dict(sd)
