@@ -1,4 +1,4 @@
-"""Build the native C++ runtime tools (no GPU needed): supervisor + GPU/topology probe.
+"""Build the native C++ runtime tools (no GPU needed): supervisor, GPU/topology probe, PS server.
 
 Outputs go to ``arena_amd/bin/`` (git-ignored, shipped to the GPU box with the tree).
 """
@@ -16,6 +16,7 @@ TOOLS = {
     # name: (sources, extra flags)
     "arena-supervisor": (["csrc/runtime/supervisor.cpp"], ["-Icsrc/runtime"]),
     "arena-probe": (["csrc/runtime/probe.cpp"], ["-Icsrc/runtime"]),
+    "arena-ps": (["csrc/runtime/ps_server.cpp"], ["-pthread", "-O3", "-march=x86-64-v3"]),
 }
 
 

@@ -122,8 +122,10 @@ def _command_args(ns) -> List[str]:
 
 def _submit(ctx: _Ctx, a: S.SubmitArgs, cmd: List[str]) -> int:
     a.namespace = ctx.namespace
-    a.prepare(cmd)
     b = ctx.backend
+    if not a.image and getattr(b, "name", "") == "local":
+        a.image = "local"   # processes on this host: there is no container image to pull
+    a.prepare(cmd)
     b.ensure_namespace(ctx.namespace)
     if b.release_exists(a.name):
         raise ArenaError(f"the job {a.name} is already exist, please delete it first. "

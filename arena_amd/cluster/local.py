@@ -191,8 +191,8 @@ class LocalBackend(Backend):
         os.makedirs(os.path.join(jd, "logs"), exist_ok=True)
         os.makedirs(os.path.join(jd, "control"), exist_ok=True)
         try:
-            plan, gpus, ports = self._plan(name, namespace, chart, values, state, jd)
             self._sync_code(values, jd)
+            plan, gpus, ports = self._plan(name, namespace, chart, values, state, jd)
         except Exception:
             shutil.rmtree(jd, ignore_errors=True)
             raise
@@ -483,6 +483,11 @@ class LocalBackend(Backend):
             for key in rel.get("deleted_services", []):
                 st.services.pop(tuple(key), None)
             st.reconcile()
+            # the view is rebuilt per call: the operator's StartTime = the first task start
+            starts = [ps.get("start") for ps in spods.values() if ps.get("start")]
+            for tf in st.tfjobs.values():
+                if tf.start_time is None and starts:
+                    tf.start_time = min(starts)
             # a Job whose pods were all deleted keeps its terminal counters
             for job in st.jobs.values():
                 if job.meta.labels.get("role") == "mpimaster" and state.get("phase") == "Failed":

@@ -76,8 +76,11 @@ class FusedMLPTrainer:
 
     def __init__(self, cfg: MLPConfig, train_x: torch.Tensor, train_y: torch.Tensor,
                  device: torch.device | str = "cuda", process_group=None,
-                 rank: int = 0, world: int = 1):
+                 rank: int = 0, world: int = 1, external_update: bool = False):
+        """``external_update``: steps only produce the flat gradient ``G`` (the optimizer runs
+        elsewhere -- the parameter server in PS mode); the step counter still advances."""
         self.cfg = cfg
+        self.external_update = external_update
         self.device = torch.device(device)
         self.pg = process_group
         self.rank, self.world = rank, world
@@ -91,7 +94,7 @@ class FusedMLPTrainer:
         self.P = torch.zeros(n, device=dev)
         self.M = torch.zeros(n, device=dev)
         self.V = torch.zeros(n, device=dev)
-        self.G = torch.zeros(n, device=dev) if self.distributed else None
+        self.G = torch.zeros(n, device=dev) if (self.distributed or external_update) else None
         self._init_params()
         if self.distributed:
             import torch.distributed as dist
@@ -176,6 +179,10 @@ class FusedMLPTrainer:
             for part in range(3):
                 self._launch_step_part(part)
             return
+        if self.external_update:
+            self._launch_fwd_head()
+            self._launch_wgrad(adam=False, commit=True)
+            return
         self._launch_fwd_head()
         self._launch_wgrad(adam=True)
 
@@ -189,7 +196,7 @@ class FusedMLPTrainer:
                            seed=cfg.seed * 2654435761 + self.rank, step=A, ctr_dst=Bc,
                            ctr_src=A, ctr_add=1)
 
-    def _launch_wgrad(self, adam: bool):
+    def _launch_wgrad(self, adam: bool, commit: bool = False):
         """Softmax-xent recomputed per workgroup from the logits; dW1 (dz via the W2 snapshot and
         the H mask) and dW2 in one launch. With ``adam`` the update is the epilogue (and A = B is
         committed), else the grads go to the flat all-reduce bucket."""
@@ -210,8 +217,9 @@ class FusedMLPTrainer:
                               t_step=Bc, tf_style=cfg.tf_adam, ctr_dst=A, ctr_src=Bc, ctr_add=0,
                               **common)
         else:
+            ctr = dict(ctr_dst=A, ctr_src=Bc, ctr_add=0) if commit else {}
             ops.wgrad_grouped(xs, dzs, [self.gW1, self.gW2], [self.gb1, self.gb2], mode=0,
-                              grad_scale=1.0, **common)
+                              grad_scale=1.0, **ctr, **common)
 
     def _capture(self, nsteps: int) -> torch.cuda.CUDAGraph:
         g = torch.cuda.CUDAGraph()

@@ -1,0 +1,249 @@
+"""LocalBackend end-to-end on CPU: real processes under the native supervisor.
+
+Covers SURVEY §7.3 step 4: job store, GPU allocator, rank launcher (standalone / allreduce /
+PS-worker), per-rank logs with timestamps and --follow, delete, retry (backoffLimit), jobmon
+reaping on success and failure, fault injection, and the native topology probe.
+"""
+from __future__ import annotations
+
+import io
+import json
+import os
+import sys
+import time
+
+import pytest
+
+from arena_amd import _build
+from arena_amd.cli.commands import run
+from arena_amd.cluster.local import LocalBackend, pick_gpus
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PY = sys.executable
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _tools():
+    _build.build_native_tools()
+
+
+@pytest.fixture
+def env(tmp_path, monkeypatch):
+    monkeypatch.setenv("ARENA_LOCAL_GPUS", "2")
+    monkeypatch.setenv("ARENA_NODE_IP", "10.0.0.7")
+    monkeypatch.setenv("ARENA_DATA_CACHE", str(tmp_path / "cache"))
+    b = LocalBackend(str(tmp_path / "home"), node_name="mi355x-0")
+    yield b
+    for name in b._release_names():
+        try:
+            b.delete_release(name)
+        except Exception:  # noqa: BLE001
+            pass
+
+
+def cli(backend, *argv) -> str:
+    out = io.StringIO()
+    rc = run(list(argv), backend=backend, out=out)
+    return out.getvalue() if rc == 0 else f"rc={rc}\n" + out.getvalue()
+
+
+def wait_phase(b: LocalBackend, name: str, phases=("Succeeded", "Failed"), timeout=60.0) -> dict:
+    deadline = time.time() + timeout
+    while time.time() < deadline:
+        st = b._state(name)
+        if st.get("phase") in phases and (st.get("finished") or st.get("phase") != "Running"):
+            return st
+        time.sleep(0.05)
+    raise AssertionError(f"{name} did not reach {phases}: {b._state(name)}")
+
+
+def test_standalone_job_lifecycle(env):
+    out = cli(env, "submit", "sj", "--name", "hello", "--gpus", "1",
+              "echo hello from $HOSTNAME gpus=$HIP_VISIBLE_DEVICES; echo second line")
+    assert "hello-training" in out
+    st = wait_phase(env, "hello")
+    assert st["phase"] == "Succeeded" and st["attempts"] == 1
+    lst = cli(env, "list")
+    assert lst.splitlines()[1].split()[:3] == ["hello", "SUCCEEDED", "STANDALONEJOB"]
+    logs = cli(env, "logs", "hello")
+    assert logs.startswith("hello from hello-training-") and "gpus=0" in logs
+    assert logs.splitlines()[1] == "second line"
+    ts = cli(env, "logs", "--timestamps", "--tail", "1", "hello")
+    assert ts.split(" ", 1)[0].endswith("Z") and ts.rstrip().endswith("second line")
+    got = cli(env, "get", "hello")
+    assert "standalonejob" in got and "hello-training-" in got
+    assert "deleted" in cli(env, "delete", "hello")
+    assert not os.path.exists(env.job_dir("hello"))
+    assert "doesn't exist" in cli(env, "get", "hello")
+
+
+def test_retry_is_backoff_limit(env):
+    cli(env, "submit", "sj", "--name", "flaky", "--retry", "2", "echo try; exit 3")
+    st = wait_phase(env, "flaky")
+    assert st["phase"] == "Failed" and st["attempts"] == 3
+    pod = next(iter(st["pods"].values()))
+    assert pod["exit_code"] == 3 and pod["restarts"] == 2
+    logs = cli(env, "logs", "flaky")
+    assert logs.count("try") == 3 and "restarting (attempt 3)" in logs
+    assert cli(env, "list").splitlines()[1].split()[1] == "FAILED"
+
+
+def test_gpu_allocation_and_exhaustion(env):
+    cli(env, "submit", "sj", "--name", "a", "--gpus", "1", "sleep 30")
+    cli(env, "submit", "sj", "--name", "b", "--gpus", "1", "sleep 30")
+    ra = json.load(open(os.path.join(env.job_dir("a"), "release.json")))
+    rb = json.load(open(os.path.join(env.job_dir("b"), "release.json")))
+    assert sorted(list(ra["gpus"].values())[0] + list(rb["gpus"].values())[0]) == [0, 1]
+    out = cli(env, "submit", "sj", "--name", "c", "--gpus", "1", "sleep 1")
+    assert "insufficient GPUs" in out
+    top = cli(env, "top", "node")
+    assert "2           2" in top.replace("\t", " ") or "2/2" in top
+    env.delete_release("a")
+    # a's GPU is free again
+    cli(env, "submit", "sj", "--name", "c", "--gpus", "1", "sleep 1")
+    rc = json.load(open(os.path.join(env.job_dir("c"), "release.json")))
+    assert list(rc["gpus"].values())[0] == list(ra["gpus"].values())[0]
+
+
+def test_pick_gpus_prefers_one_hive():
+    inv = {"count": 4, "gpus": [{"index": 0, "hive_id": "A"}, {"index": 1, "hive_id": "B"},
+                                {"index": 2, "hive_id": "B"}, {"index": 3, "hive_id": "A"}]}
+    assert pick_gpus(inv, set(), 2) == [0, 3] or pick_gpus(inv, set(), 2) == [1, 2]
+    assert pick_gpus(inv, {0}, 2) == [1, 2]
+    assert pick_gpus(inv, {0, 1}, 2) == [2, 3]   # no hive has 2 free: span hives
+
+
+def test_delete_kills_running_processes(env):
+    cli(env, "submit", "sj", "--name", "sleeper", "sleep 60")
+    deadline = time.time() + 10
+    pid = -1
+    while time.time() < deadline and pid <= 0:
+        st = env._state("sleeper")
+        pid = next(iter(st.get("pods", {}).values()), {}).get("pid", -1)
+        time.sleep(0.05)
+    assert pid > 0 and os.path.exists(f"/proc/{pid}")
+    assert cli(env, "list").splitlines()[1].split()[1] == "RUNNING"
+    env.delete_release("sleeper")
+    time.sleep(0.2)
+    gone = not os.path.exists(f"/proc/{pid}") or open(f"/proc/{pid}/stat").read().split()[2] == "Z"
+    assert gone
+
+
+ALLREDUCE = (
+    "import os, torch, torch.distributed as d; d.init_process_group('gloo'); "
+    "t = torch.tensor([float(d.get_rank() + 1)]); d.all_reduce(t); "
+    "print('rank', d.get_rank(), 'of', d.get_world_size(), 'sum', t.item(), "
+    "'addr', os.environ['MASTER_ADDR']); d.destroy_process_group()")
+
+
+def test_allreduce_job_ranks_rendezvous_and_reap(env):
+    cli(env, "submit", "mpi", "--name", "ar", "--workers", "3", f'{PY} -c "{ALLREDUCE}"')
+    st = wait_phase(env, "ar", timeout=120)
+    assert st["phase"] == "Succeeded", st
+    logs = "".join(open(os.path.join(env.job_dir("ar"), "logs", f)).read()
+                   for f in os.listdir(os.path.join(env.job_dir("ar"), "logs")))
+    for r in range(3):
+        assert f"rank {r} of 3 sum 6.0 addr 127.0.0.1" in logs
+    # jobmon semantics: worker StatefulSet pods are gone, the launcher Job shows SUCCEEDED
+    pods = env.list_pods("default", {"release": "ar"})
+    assert not [p for p in pods if p.meta.labels.get("role") == "mpiworker"]
+    assert cli(env, "list").splitlines()[1].split()[:3] == ["ar", "SUCCEEDED", "MPIJOB"]
+
+
+def test_allreduce_worker_fault_fails_job_and_reaps(env, monkeypatch):
+    monkeypatch.setenv("ARENA_FAULT_POD", "fi-tf-horovod-0")
+    monkeypatch.setenv("ARENA_FAULT_AFTER_MS", "300")
+    cli(env, "submit", "mpi", "--name", "fi", "--workers", "2", "sleep 30")
+    st = wait_phase(env, "fi", timeout=60)
+    assert st["phase"] == "Failed"
+    assert "fault injected" in st["message"] or st["pods"]["fi-tf-horovod-0"]["exit_code"] == 137
+    assert all(p["pid"] == -1 for p in st["pods"].values())  # everything reaped (Q11)
+    assert cli(env, "list").splitlines()[1].split()[1] == "FAILED"
+
+
+def test_allreduce_retry_restarts_gang(env, monkeypatch):
+    # the first attempt's worker dies; the retry runs the whole gang again and succeeds
+    cmd = ("if [ \"$RANK\" = 1 ] && [ ! -f $ARENA_JOB_DIR/once ]; then touch $ARENA_JOB_DIR/once;"
+           " exit 9; fi; sleep 0.5; echo ok $RANK")
+    cli(env, "submit", "mpi", "--name", "rt", "--workers", "2", "--retry", "1", cmd)
+    st = wait_phase(env, "rt", timeout=60)
+    assert st["phase"] == "Succeeded" and st["attempts"] == 2, st
+
+
+def test_tfjob_ps_workers_train_mnist(env):
+    cmd = (f"{PY} -m arena_amd.examples.mnist_ps --max_steps 40 --n_train 1000 --device cpu "
+           "--eval_every 20")
+    out = cli(env, "submit", "tf", "--name", "dist", "--ps", "1", "--workers", "2", cmd)
+    assert "dist-tfjob" in out or "TFJob" in out
+    plan = json.load(open(os.path.join(env.job_dir("dist"), "plan.json")))
+    tfc = [json.loads(p["env"]["TF_CONFIG"]) for p in plan["pods"] if "TF_CONFIG" in p["env"]]
+    assert {t["task"]["type"] for t in tfc} == {"ps", "worker"}
+    assert len(tfc[0]["cluster"]["worker"]) == 2 and len(tfc[0]["cluster"]["ps"]) == 1
+    st = wait_phase(env, "dist", timeout=180)
+    assert st["phase"] == "Succeeded", st
+    w0 = cli(env, "logs", "dist", "-i", "dist-tfjob-worker-0")
+    assert "Accuracy at step" in w0 and "test accuracy" in w0
+    assert "TFJOB" in cli(env, "list")
+    scal = os.path.join(env.job_dir("dist"), "tb", "test")
+    assert os.listdir(scal)
+
+
+def test_logs_follow_streams_until_exit(env):
+    cli(env, "submit", "sj", "--name", "fol", "for i in 1 2 3; do echo line $i; sleep 0.3; done")
+    time.sleep(0.2)
+    lines = list(env.pod_logs("default", env.list_pods("default", {"release": "fol"})[0].name,
+                              follow=True))
+    assert [x.strip() for x in lines] == ["line 1", "line 2", "line 3"]
+
+
+def test_data_mounts_and_env(env, tmp_path):
+    host = tmp_path / "hostdata"
+    host.mkdir()
+    (host / "f.txt").write_text("payload")
+    cli(env, "submit", "sj", "--name", "dm", "--dataDir", f"{host}:/data",
+        "cat $ARENA_MOUNT_ROOT/data/f.txt; echo; echo $ARENA_DATADIR_TRAINING_DATA_0")
+    wait_phase(env, "dm")
+    logs = cli(env, "logs", "dm")
+    assert "payload" in logs and str(host) in logs
+
+
+def test_code_sync_copy(env, tmp_path):
+    src = tmp_path / "proj"
+    src.mkdir()
+    (src / "train.py").write_text("print('synced code ran')\n")
+    cli(env, "submit", "sj", "--name", "cs", "--syncMode", "rsync", "--syncSource", str(src),
+        f"{PY} code/proj/train.py")
+    st = wait_phase(env, "cs")
+    assert st["phase"] == "Succeeded", cli(env, "logs", "cs")
+    assert "synced code ran" in cli(env, "logs", "cs")
+
+
+def test_probe_reads_fake_sysfs(tmp_path):
+    import subprocess
+    topo = tmp_path / "sys/class/kfd/kfd/topology/nodes"
+    (topo / "0").mkdir(parents=True)
+    (topo / "0/properties").write_text("simd_count 0\n")
+    for n, other in ((1, 2), (2, 1)):
+        d = topo / str(n)
+        (d / "io_links/0").mkdir(parents=True)
+        (d / "io_links/1").mkdir(parents=True)
+        (d / "properties").write_text(
+            f"simd_count 1024\ngfx_target_version 90500\nhive_id 77\nnum_xcc 8\n"
+            f"drm_render_minor {127 + n}\nunique_id {n}\nlocation_id {n * 256}\n")
+        (d / "io_links/0/properties").write_text("type 2\nnode_to 0\nweight 20\n")
+        (d / "io_links/1/properties").write_text(f"type 11\nnode_to {other}\nweight 15\n")
+        dev = tmp_path / f"sys/class/drm/renderD{127 + n}/device"
+        (dev / "hwmon/hwmon0").mkdir(parents=True)
+        (dev / "gpu_busy_percent").write_text("37\n")
+        (dev / "mem_info_vram_total").write_text(str(288 * 2**30) + "\n")
+        (dev / "mem_info_vram_used").write_text(str(2**30) + "\n")
+        (dev / "hwmon/hwmon0/power1_average").write_text("750000000\n")
+    out = subprocess.run([_build.ensure_tool("arena-probe"), "--root", str(tmp_path)],
+                         capture_output=True, text=True, check=True).stdout
+    inv = json.loads(out)
+    assert inv["count"] == 2
+    g0 = inv["gpus"][0]
+    assert g0["gfx"] == "gfx950" and g0["hive_id"] == "77" and g0["num_xcc"] == 8
+    assert g0["links"] == [{"to": 1, "type": "xgmi", "weight": 15}]
+    assert g0["busy_percent"] == 37 and g0["vram_total"] == 288 * 2**30
+    assert g0["power_uw"] == 750000000
