@@ -33,6 +33,14 @@ _STATE = {"pg": None, "local_rank": 0, "local_size": 1}
 def init(backend: Optional[str] = None, timeout_s: float = 600.0):
     """Initialise the default process group from the environment (idempotent)."""
     if not dist.is_initialized():
+        if "WORLD_SIZE" not in os.environ:  # plain `python script.py`: a world of one
+            import socket
+            with socket.socket() as s:
+                s.bind(("127.0.0.1", 0))
+                port = s.getsockname()[1]
+            os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                              MASTER_ADDR=os.environ.get("MASTER_ADDR", "127.0.0.1"),
+                              MASTER_PORT=os.environ.get("MASTER_PORT", str(port)))
         if backend is None:
             backend = "nccl" if torch.cuda.is_available() else "gloo"
         import datetime

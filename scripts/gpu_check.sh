@@ -42,4 +42,9 @@ if [[ $STEPS == all || $STEPS == *prof* ]]; then
   ok_or_stop $? "rocprofv3"
   find gpurun_out/prof -name '*kernel_stats.csv' -exec head -20 {} \;
 fi
+if [[ $STEPS == all || $STEPS == *e2e* ]]; then
+  timeout -k 10 900 bash scripts/e2e_mnist.sh > gpurun_out/e2e_driver.log 2>&1
+  ok_or_stop $? "e2e local backend"
+  tail -30 gpurun_out/e2e/e2e.log
+fi
 echo "[gpu_check] done"

@@ -1,0 +1,195 @@
+"""Parallel layer on CPU: Horovod-style API over gloo (world 2) and the native parameter server."""
+from __future__ import annotations
+
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from arena_amd import _build
+from arena_amd.parallel import ps as psmod
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _hvd_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from torch import nn
+    from arena_amd.parallel import hvd
+    hvd.init("gloo")
+    try:
+        assert hvd.rank() == rank and hvd.size() == world
+        # allreduce average / sum, allgather with ragged first dims, broadcast
+        t = torch.tensor([float(rank + 1)] * 3)
+        avg = hvd.allreduce(t)
+        tot = hvd.allreduce(t, average=False)
+        ag = hvd.allgather(torch.full((rank + 1, 2), float(rank)))
+        b = torch.tensor([float(rank * 10)])
+        hvd.broadcast_(b, root_rank=1)
+        # model: different init per rank -> broadcast_parameters makes them equal
+        torch.manual_seed(100 + rank)
+        model = nn.Sequential(nn.Linear(12, 16), nn.ReLU(), nn.Linear(16, 4))
+        hvd.broadcast_parameters(model.state_dict(), root_rank=0)
+        opt = hvd.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1),
+                                       named_parameters=model.named_parameters(), bucket_mb=0.0002)
+        g = torch.Generator().manual_seed(7)
+        data = [(torch.randn(8, 12, generator=g), torch.randint(0, 4, (8,), generator=g))
+                for _ in range(2 * world)]
+        # each rank takes its half of every global batch
+        for step in range(3):
+            x, y = data[step % len(data)]
+            xs, ys = x[rank::world], y[rank::world]
+            loss = nn.functional.cross_entropy(model(xs), ys, reduction="sum") / x.shape[0] * world
+            opt.zero_grad()
+            loss.backward()
+            opt.step()
+        flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+        q.put((rank, avg.tolist(), tot.tolist(), ag.tolist(), b.item(), flat.numpy(),
+               len(opt.buckets)))
+    finally:
+        hvd.shutdown()
+
+
+@pytest.mark.timeout(180)
+def test_hvd_api_world2_matches_single_process():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hvd_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=150) for _ in range(world))
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    (_, avg0, tot0, ag0, b0, flat0, nb0), (_, avg1, tot1, ag1, b1, flat1, nb1) = res
+    assert avg0 == avg1 == [1.5] * 3 and tot0 == [3.0] * 3
+    assert ag0 == [[0.0, 0.0], [1.0, 1.0], [1.0, 1.0]] == ag1
+    assert b0 == b1 == 10.0
+    assert nb0 > 1  # tiny bucket cap -> several buckets, reduced as grads become ready
+    np.testing.assert_array_equal(flat0, flat1)  # replicas stay identical
+    # == single-process SGD on the full batch from rank 0's initial weights
+    from torch import nn
+    torch.manual_seed(100)
+    model = nn.Sequential(nn.Linear(12, 16), nn.ReLU(), nn.Linear(16, 4))
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(7)
+    data = [(torch.randn(8, 12, generator=g), torch.randint(0, 4, (8,), generator=g))
+            for _ in range(2 * world)]
+    for step in range(3):
+        x, y = data[step % len(data)]
+        loss = nn.functional.cross_entropy(model(x), y)
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+    ref = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).numpy()
+    np.testing.assert_allclose(flat0, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_cluster_spec_parsing():
+    env = {"TF_CONFIG": '{"cluster":{"ps":["h:1"],"worker":["a:2","b:3"]},'
+                        '"task":{"type":"worker","index":1}}'}
+    s = psmod.ClusterSpec.from_env(env)
+    assert s.ps == ["h:1"] and s.worker == ["a:2", "b:3"] and s.task_index == 1 and not s.is_chief
+    env = {"MX_CLUSTER_SPEC": '{"cluster":{"ps":["h:1"],"chief":["c:9"],"worker":["a:2"]},'
+                              '"task":{"type":"worker","index":0}}'}
+    s = psmod.ClusterSpec.from_env(env)
+    assert s.worker == ["c:9", "a:2"] and s.task_index == 1
+    assert psmod.shard_ranges(10, 3) == [(0, 4), (4, 8), (8, 10)]
+    assert psmod.shard_ranges(5, 1) == [(0, 5)]
+
+
+@pytest.fixture(scope="module")
+def ps_tool():
+    _build.build_native_tools()
+
+
+def _torch_adam(p0, grads, lr):
+    p = torch.tensor(p0.copy(), requires_grad=True)
+    opt = torch.optim.Adam([p], lr=lr)
+    for g in grads:
+        p.grad = torch.tensor(g)
+        opt.step()
+    return p.detach().numpy()
+
+
+def test_native_ps_async_adam_matches_torch(ps_tool):
+    n, lr = 1003, 1e-2
+    ports = [_free_port(), _free_port()]
+    servers = [psmod.spawn_server(p, 1, lr=lr) for p in ports]
+    try:
+        cl = psmod.PSClient([f"127.0.0.1:{p}" for p in ports], n, timeout_s=10)
+        rng = np.random.default_rng(0)
+        p0 = rng.standard_normal(n).astype(np.float32)
+        cl.init(p0)
+        cl.init(p0 + 1)  # second INIT ignored (only the chief's takes effect)
+        out = np.empty(n, np.float32)
+        assert cl.pull(out) == 0
+        np.testing.assert_array_equal(out, p0)
+        grads = [rng.standard_normal(n).astype(np.float32) for _ in range(5)]
+        for i, g in enumerate(grads):
+            assert cl.push_pull(g, out) == i + 1
+        np.testing.assert_allclose(out, _torch_adam(p0, grads, lr), rtol=2e-5, atol=2e-6)
+        st = cl.stats()
+        assert [s[0] for s in st] == [5, 5] and sum(s[1] for s in st) == n
+        cl.done()
+        for s in servers:
+            assert s.wait(10) == 0  # all (1) workers done -> servers exit cleanly
+    finally:
+        for s in servers:
+            if s.poll() is None:
+                s.kill()
+
+
+def test_native_ps_sync_averages_one_grad_per_worker(ps_tool):
+    import threading
+    n, lr = 64, 0.5
+    port = _free_port()
+    srv = psmod.spawn_server(port, 2, lr=lr, optimizer="sgd", sync=True)
+    try:
+        p0 = np.zeros(n, np.float32)
+        clients = [psmod.PSClient([f"127.0.0.1:{port}"], n, timeout_s=10) for _ in range(2)]
+        clients[0].init(p0)
+        outs = [np.empty(n, np.float32) for _ in range(2)]
+        steps = [None, None]
+
+        def go(i):
+            g = np.full(n, float(i + 1), np.float32)     # 1 and 2 -> mean 1.5
+            steps[i] = clients[i].push_pull(g, outs[i])
+        ts = [threading.Thread(target=go, args=(i,)) for i in range(2)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(10)
+        assert steps == [1, 1]
+        np.testing.assert_allclose(outs[0], -lr * 1.5)
+        np.testing.assert_array_equal(outs[0], outs[1])
+        for c in clients:
+            c.done()
+        assert srv.wait(10) == 0
+    finally:
+        if srv.poll() is None:
+            srv.kill()
+
+
+def test_trainer_external_update_produces_grads_only():
+    from arena_amd.models.mlp import FusedMLPTrainer, MLPConfig
+    torch.manual_seed(0)
+    x = torch.randint(0, 256, (400, 784), dtype=torch.uint8)
+    y = torch.randint(0, 10, (400,), dtype=torch.uint8)
+    cfg = MLPConfig(batch=100)
+    tr = FusedMLPTrainer(cfg, x, y, device="cpu", external_update=True)
+    p_before = tr.P.clone()
+    tr.train_steps(2)
+    assert torch.equal(tr.P, p_before)              # no local optimizer
+    assert tr.G.abs().sum() > 0 and int(tr.ctrA.item()) == 2
