@@ -76,9 +76,13 @@ class FusedMLPTrainer:
 
     def __init__(self, cfg: MLPConfig, train_x: torch.Tensor, train_y: torch.Tensor,
                  device: torch.device | str = "cuda", process_group=None,
-                 rank: int = 0, world: int = 1, external_update: bool = False):
+                 rank: int = 0, world: int = 1, external_update: bool = False,
+                 comm: str = "auto"):
         """``external_update``: steps only produce the flat gradient ``G`` (the optimizer runs
-        elsewhere -- the parameter server in PS mode); the step counter still advances."""
+        elsewhere -- the parameter server in PS mode); the step counter still advances.
+        ``comm`` (data parallel on GPUs): "xgmi" = fused reduce-scatter/Adam/all-gather kernel over
+        xGMI peer memory, "rccl" = graph-captured RCCL all_reduce + flat Adam, "auto" = xgmi when
+        its self-test passes on every rank of a single-node job, else rccl."""
         self.cfg = cfg
         self.external_update = external_update
         self.device = torch.device(device)
@@ -96,9 +100,13 @@ class FusedMLPTrainer:
         self.V = torch.zeros(n, device=dev)
         self.G = torch.zeros(n, device=dev) if (self.distributed or external_update) else None
         self._init_params()
+        self.xgmi = None
         if self.distributed:
             import torch.distributed as dist
             dist.broadcast(self.P, src=0, group=self.pg)
+            if dev.type == "cuda" and comm in ("auto", "xgmi"):
+                self._setup_xgmi(n, required=(comm == "xgmi"))
+        self.comm = "xgmi" if self.xgmi is not None else ("rccl" if self.distributed else "none")
         L = self.layout
         self.W1, self.b1 = L.view(self.P, "W1"), L.view(self.P, "b1")
         self.W2, self.b2 = L.view(self.P, "W2"), L.view(self.P, "b2")
@@ -137,6 +145,28 @@ class FusedMLPTrainer:
         self.steps_done = 0
         self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_mode = None
+
+    def _setup_xgmi(self, n: int, required: bool) -> None:
+        """Move P and G into hipIpc-registered memory shared with the other ranks."""
+        from ..parallel import xgmi
+        if not xgmi.usable(self.pg):
+            if required:
+                raise xgmi.XgmiUnavailable("xGMI collective not usable for this process group")
+            return
+        try:
+            comm = xgmi.XgmiComm(self.pg, staging_elems=n, param_elems=n)
+        except xgmi.XgmiUnavailable as e:
+            if required:
+                raise
+            import logging
+            logging.getLogger("arena.mlp").warning("xGMI collective unavailable, using RCCL: %s", e)
+            return
+        P = comm.params()[:n]
+        P.copy_(self.P)
+        G = comm.buffer()[:n]
+        G.zero_()
+        self.P, self.G, self.xgmi = P, G, comm
+        self.shard_lo, self.shard_hi = comm.shard(n)
 
     # ------------------------------------------------------------------------------------------
     def _init_params(self):
@@ -287,8 +317,16 @@ class FusedMLPTrainer:
             self._launch_fwd_head()
             self._launch_wgrad(adam=False)
         elif part == 1:
+            if self.xgmi is not None:
+                return  # the reduction is fused into part 2
             import torch.distributed as dist
             dist.all_reduce(self.G, group=self.pg)
+        elif self.xgmi is not None:
+            # reduce-scatter G over xGMI + Adam on the owned shard + all-gather P, one kernel
+            self.xgmi.adam_(self.M, self.V, self.layout.total, lr=cfg.lr, lr_t=self.lr_t,
+                            betas=cfg.betas, eps=cfg.eps, t_step=Bc,
+                            grad_scale=1.0 / self.world, tf_style=cfg.tf_adam, ctr_dst=A,
+                            ctr_src=Bc, ctr_add=0)
         else:
             ops.adam_flat(self.P, self.M, self.V, self.G, grad_scale=1.0 / self.world,
                           ctr_dst=A, ctr_src=Bc, ctr_add=0, lr=cfg.lr, lr_t=self.lr_t,
@@ -352,13 +390,24 @@ class FusedMLPTrainer:
         return float(loss_acc.item()), float(corr.item()) / n
 
     def state_dict(self):
-        return {"P": self.P.detach().cpu(), "M": self.M.detach().cpu(), "V": self.V.detach().cpu(),
+        M, V = self.M, self.V
+        if self.xgmi is not None:
+            # optimizer state is sharded (each rank updates its chunk; the rest stays zero), so a
+            # sum over ranks reassembles it
+            M, V = M.clone(), V.clone()
+            self.xgmi.all_reduce_(M)
+            self.xgmi.all_reduce_(V)
+        return {"P": self.P.detach().cpu(), "M": M.detach().cpu(), "V": V.detach().cpu(),
                 "step": int(self.ctrA.item()), "layout": dict(self.layout.shapes)}
 
     def load_state_dict(self, sd):
         self.P.copy_(sd["P"])
         self.M.copy_(sd["M"])
         self.V.copy_(sd["V"])
+        if self.xgmi is not None:  # keep only this rank's optimizer shard
+            for t in (self.M, self.V):
+                t[:self.shard_lo].zero_()
+                t[self.shard_hi:].zero_()
         self.ctrA.fill_(int(sd["step"]))
         self.ctrB.fill_(int(sd["step"]))
         self.steps_done = int(sd["step"])

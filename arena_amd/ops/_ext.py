@@ -28,11 +28,11 @@ def load():
             f"`python -c 'import __graft_entry__ as g; g.build()'`): {_ERR}")
     try:
         mod = importlib.import_module("arena_amd._C")
-        src = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
-            os.path.abspath(__file__)))), "csrc", "ops")
-        if os.path.isdir(src):
+        csrc = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(
+            os.path.abspath(__file__)))), "csrc")
+        if os.path.isdir(os.path.join(csrc, "ops")):
             from ._srchash import source_hash
-            want = source_hash(src)
+            want = source_hash(os.path.join(csrc, "ops"), os.path.join(csrc, "ccl"))
             if getattr(mod, "src_hash", None) != want:
                 raise RuntimeError(f"stale build: extension built from sources {mod.src_hash}, "
                                    f"tree has {want}")

@@ -164,11 +164,22 @@ class _Bucket:
         self.work = None
 
 
+class _Done:
+    @staticmethod
+    def wait():
+        return None
+
+
+_DONE = _Done()
+
+
 class DistributedOptimizer:
     """Wraps a torch optimizer: bucketed async gradient allreduce overlapped with backward."""
 
     def __init__(self, optimizer: torch.optim.Optimizer, named_parameters=None,
-                 bucket_mb: float = 32.0, process_group=None):
+                 bucket_mb: float = 32.0, process_group=None, comm: str = "auto"):
+        """``comm``: "xgmi" (single-node fused xGMI kernel), "rccl" (torch.distributed),
+        "auto" (xgmi when its self-test passes on every rank, else rccl)."""
         self.opt = optimizer
         self.pg = process_group
         params = [p for _, p in named_parameters] if named_parameters is not None else \
@@ -194,6 +205,19 @@ class DistributedOptimizer:
             for p in b.params:
                 self._owner[id(p)] = b
         self._hooks = []
+        self.xgmi = None
+        if size() > 1 and comm in ("auto", "xgmi") and params and params[0].is_cuda:
+            from . import xgmi
+            if xgmi.usable(process_group):
+                try:
+                    self.xgmi = xgmi.XgmiComm(process_group,
+                                              staging_elems=max(b.flat.numel() for b in self.buckets))
+                except xgmi.XgmiUnavailable:
+                    if comm == "xgmi":
+                        raise
+            elif comm == "xgmi":
+                raise xgmi.XgmiUnavailable("xGMI collective not usable for this process group")
+        self.comm = "xgmi" if self.xgmi is not None else "rccl"
         if size() > 1:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -208,7 +232,16 @@ class DistributedOptimizer:
 
     def _launch(self, b: _Bucket) -> None:
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in b.params]
-        ops.flatten_into([g.contiguous() for g in grads], b.offsets, b.flat, 1.0)
+        grads = [g.contiguous() for g in grads]
+        if self.xgmi is not None:
+            # pack straight into the registered staging buffer (zero-copy input), average on the
+            # way out; stream-ordered, so it overlaps the host side of backward
+            stage = self.xgmi.buffer()[: b.flat.numel()]
+            ops.flatten_into(grads, b.offsets, stage, 1.0)
+            self.xgmi.all_reduce_(stage, scale=1.0 / size(), out=b.flat)
+            b.work = _DONE
+            return
+        ops.flatten_into(grads, b.offsets, b.flat, 1.0)
         b.work = dist.all_reduce(b.flat, group=self.pg, async_op=True)
 
     def _on_grad(self, p) -> None:
@@ -220,7 +253,7 @@ class DistributedOptimizer:
     def synchronize(self) -> None:
         if size() == 1:
             return
-        inv = 1.0 / size()
+        inv = 1.0 if self.xgmi is not None else 1.0 / size()
         for b in self.buckets:
             if b.work is None:  # some grads never arrived (unused params): reduce anyway
                 self._launch(b)

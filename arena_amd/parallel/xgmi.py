@@ -1,0 +1,230 @@
+"""Intra-node xGMI collectives (hipIpc peer memory) with an automatic RCCL fallback.
+
+The Horovod-equivalent gradient path of SURVEY §2.10/§2.12 ("xGMI one-/two-shot allreduce with
+RCCL fallback"). Kernels live in csrc/ccl/xgmi_ccl.hip; this module owns the registered memory:
+
+* every rank allocates a staging buffer (and optionally a parameter buffer) with hipMalloc and a
+  flag buffer in uncached memory, exports hipIpc handles, and exchanges them over the process
+  group (gloo or RCCL) with ``all_gather_object``;
+* ``all_reduce_`` = one kernel: copy-in, barrier, reduce own chunk from all W ranks (W-1 xGMI
+  links read in parallel), write it to all ranks, barrier, copy-out;
+* ``adam_`` = reduce-scatter of the gradient + Adam on the owned chunk + all-gather of the
+  updated parameters, in one kernel (ZeRO-1-style sharded optimizer state);
+* construction runs a self-test on every rank and agrees on the outcome over the process group,
+  so either ALL ranks use xGMI or all fall back to RCCL (never a split decision). Barrier waits are
+  bounded in-kernel; a timeout sets an error flag that ``check()`` raises on.
+
+Only meaningful on a single node (all ranks' GPUs in one xGMI hive); ``usable()`` checks that.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops import _ext
+from ..utils.logs import get_logger
+
+log = get_logger("xgmi")
+
+
+class XgmiUnavailable(RuntimeError):
+    pass
+
+
+def _sig_bytes(ext) -> int:
+    return 2 * ext.ccl_max_blocks * ext.ccl_max_ranks * 4
+
+
+def usable(group=None) -> bool:
+    """Same-node world of 2..8 GPU ranks with the native extension present."""
+    if os.environ.get("ARENA_XGMI", "1") == "0" or not torch.cuda.is_available():
+        return False
+    if not dist.is_initialized():
+        return False
+    w = dist.get_world_size(group)
+    if not 2 <= w <= 8:
+        return False
+    local = os.environ.get("LOCAL_WORLD_SIZE")
+    if local is not None and int(local) != int(os.environ.get("WORLD_SIZE", w)):
+        return False  # multi-node job: inter-node traffic belongs to RCCL
+    return _ext.available()
+
+
+def _round4(n: int) -> int:
+    return (n + 3) // 4 * 4
+
+
+class XgmiComm:
+    def __init__(self, group=None, staging_elems: int = 8 << 20, param_elems: int = 0,
+                 timeout_s: float = 20.0, selftest: bool = True):
+        if not dist.is_initialized():
+            raise XgmiUnavailable("torch.distributed is not initialised")
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if not 2 <= self.world <= 8:
+            raise XgmiUnavailable(f"world size {self.world} outside 2..8")
+        ext = _ext.load()
+        self.ext = ext
+        self.device = torch.cuda.current_device()
+        self.staging_elems = _round4(staging_elems)
+        self.param_elems = _round4(param_elems) if param_elems else 0
+        self._own, self._opened = [], []
+        ok = 1
+        err_msg = ""
+        handles = {}
+        try:
+            buf = ext.ccl_malloc(self.staging_elems * 4, False)
+            self._own.append(buf)
+            sig = ext.ccl_malloc(_sig_bytes(ext), True)
+            self._own.append(sig)
+            ext.ccl_memset(sig, 0, _sig_bytes(ext))
+            ext.ccl_memset(buf, 0, self.staging_elems * 4)
+            handles = {"buf": ext.ccl_ipc_get(buf), "sig": ext.ccl_ipc_get(sig)}
+            local = {"buf": buf, "sig": sig}
+            if self.param_elems:
+                b2 = ext.ccl_malloc(self.param_elems * 4, False)
+                self._own.append(b2)
+                ext.ccl_memset(b2, 0, self.param_elems * 4)
+                handles["buf2"] = ext.ccl_ipc_get(b2)
+                local["buf2"] = b2
+        except Exception as e:  # noqa: BLE001
+            ok, err_msg = 0, repr(e)
+        allh = [None] * self.world
+        dist.all_gather_object(allh, (ok, handles), group=group)
+        if not all(h[0] for h in allh):
+            self._free()
+            raise XgmiUnavailable(f"allocation failed on some rank ({err_msg})")
+        ptrs = {k: [0] * self.world for k in handles}
+        try:
+            for r in range(self.world):
+                for k in handles:
+                    if r == self.rank:
+                        ptrs[k][r] = local[k]
+                    else:
+                        p = ext.ccl_ipc_open(allh[r][1][k])
+                        self._opened.append(p)
+                        ptrs[k][r] = p
+        except Exception as e:  # noqa: BLE001
+            ok, err_msg = 0, repr(e)
+        self._epoch = torch.zeros(ext.ccl_max_blocks, dtype=torch.int32, device="cuda")
+        self._err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        if ok:
+            self.peers = ext.XgmiPeers(ptrs["buf"], ptrs.get("buf2", []), ptrs["sig"], self._epoch,
+                                       self._err, self.staging_elems, self.param_elems, self.rank,
+                                       float(timeout_s))
+            self._buf = ext.ccl_tensor(local["buf"], self.staging_elems, self.device)
+            self._buf2 = (ext.ccl_tensor(local["buf2"], self.param_elems, self.device)
+                          if self.param_elems else None)
+        torch.cuda.synchronize()
+        self._agree(ok, f"hipIpc mapping failed: {err_msg}")
+        if selftest:
+            self._selftest()
+
+    # --------------------------------------------------------------------------------- setup
+    def _agree(self, ok: int, why: str) -> None:
+        """All ranks learn whether every rank succeeded (so they fall back together)."""
+        flags = [None] * self.world
+        dist.all_gather_object(flags, int(ok), group=self.group)
+        if not all(flags):
+            self.close()
+            raise XgmiUnavailable(why if not ok else "a peer rank failed")
+
+    def _selftest(self) -> None:
+        ok, why = 1, ""
+        try:
+            tot = sum(range(1, self.world + 1))
+            for n in (4, 1000, min(self.staging_elems, 300004)):
+                base = (torch.arange(n, device="cuda", dtype=torch.float32) % 977)
+                x = base * (self.rank + 1)
+                out = torch.empty_like(x)
+                self.all_reduce_(x, out=out)
+                torch.cuda.synchronize()
+                if not torch.equal(out, base * tot):
+                    ok, why = 0, f"self-test mismatch at n={n}"
+                    break
+            if ok and int(self._err.item()):
+                ok, why = 0, "barrier timeout during self-test"
+        except Exception as e:  # noqa: BLE001
+            ok, why = 0, repr(e)
+        self._agree(ok, why)
+
+    def _free(self):
+        for p in self._own:
+            try:
+                self.ext.ccl_free(p)
+            except Exception:  # noqa: BLE001
+                pass
+        self._own = []
+
+    def close(self) -> None:
+        torch.cuda.synchronize()
+        for p in self._opened:
+            try:
+                self.ext.ccl_ipc_close(p)
+            except Exception:  # noqa: BLE001
+                pass
+        self._opened = []
+        self.peers = None
+        self._free()
+
+    # ------------------------------------------------------------------------------- buffers
+    def buffer(self) -> torch.Tensor:
+        """This rank's registered staging buffer (zero-copy input for ``all_reduce_``)."""
+        return self._buf
+
+    def params(self) -> torch.Tensor:
+        if self._buf2 is None:
+            raise XgmiUnavailable("communicator was created without a parameter buffer")
+        return self._buf2
+
+    def shard(self, n: int):
+        """[lo, hi) of the flat vector whose optimizer state this rank owns under ``adam_``."""
+        lo, hi = self.ext.ccl_shard(n, self.world, self.rank)
+        return lo, hi
+
+    # ----------------------------------------------------------------------------- collectives
+    def all_reduce_(self, t: torch.Tensor, scale: float = 1.0, out: Optional[torch.Tensor] = None):
+        """Sum (times ``scale``) of ``t`` over ranks into ``out`` (default: in place)."""
+        if t.dtype != torch.float32 or not t.is_cuda:
+            raise TypeError("xGMI allreduce takes float32 GPU tensors")
+        out = t if out is None else out
+        src, dst = t.reshape(-1), out.reshape(-1)
+        n = src.numel()
+        cap = self.staging_elems
+        buf = self._buf
+        if (n % 4 == 0 and n <= cap and src.is_contiguous() and dst.is_contiguous()):
+            self.peers.allreduce(src, dst, float(scale))
+            return out
+        # ragged or larger than the staging buffer: go through it in zero-padded pieces
+        for s in range(0, n, cap):
+            m = min(cap, n - s)
+            m4 = _round4(m)
+            view = buf[:m4]
+            view[:m].copy_(src[s:s + m])
+            if m4 != m:
+                view[m:].zero_()
+            self.peers.allreduce(view, view, float(scale))
+            dst[s:s + m].copy_(view[:m])
+        return out
+
+    def adam_(self, M: torch.Tensor, V: torch.Tensor, n: int, *, lr: float = 1e-3,
+              lr_t: Optional[torch.Tensor] = None, betas=(0.9, 0.999), eps: float = 1e-8,
+              weight_decay: float = 0.0, t_step: Optional[torch.Tensor] = None,
+              grad_scale: float = 1.0, tf_style: bool = False,
+              ctr_dst: Optional[torch.Tensor] = None, ctr_src: Optional[torch.Tensor] = None,
+              ctr_add: int = 0) -> None:
+        """Gradient in ``buffer()[:n]`` -> Adam on the owned shard -> parameters in every rank's
+        ``params()[:n]``."""
+        self.peers.adam(M, V, int(n), float(lr), lr_t, float(betas[0]), float(betas[1]),
+                        float(eps), float(weight_decay), t_step, float(grad_scale), bool(tf_style),
+                        ctr_dst, ctr_src, int(ctr_add))
+
+    def check(self) -> None:
+        """Raise if any barrier wait timed out since construction (host sync)."""
+        if int(self._err.item()):
+            raise RuntimeError("xGMI collective: a barrier wait timed out (a peer rank stalled "
+                               "or died); results since then are invalid")

@@ -1,0 +1,247 @@
+// Intra-node collectives over xGMI peer memory for MI355X (gfx950).
+//
+// The reference's allreduce jobs rely on Horovod + NCCL inside the user image (SURVEY §2.10,
+// §2.12: DistributedOptimizer gradient allreduce every step). On an 8x MI355X node every GPU has a
+// direct xGMI link to every other GPU, so instead of a ring (one link busy per hop) each rank
+// reads its 1/W chunk from ALL peers at once and writes the reduced chunk back to all of them:
+// a "two-shot" allreduce (reduce-scatter + all-gather) in ONE kernel, using all W-1 links in
+// both directions, with no host involvement (graph-capturable).
+//
+// Buffers are plain hipMalloc allocations shared through hipIpc handles; the barrier flags live
+// in uncached memory (hipDeviceMallocUncached). Block b of every rank owns sub-range b of every
+// chunk, and synchronises only with block b of the other ranks:
+//
+//   copy-in (own sub-range b of every chunk)    -> barrier 0 -> reduce chunk[rank] sub-range b
+//   from all ranks, write the sum to all ranks   -> barrier 1 -> copy-out sub-range b
+//
+// Why that is race-free: every remote access to a rank's buffer by block b of another rank
+// happens between that rank's block b arriving at barrier 0 and at barrier 1 of the same call,
+// and the accessed ranges (chunk[rank] sub-range b) are disjoint between ranks. Flag values are
+// per-block call counters (no reset between calls).
+//
+// xgmi_adam fuses the gradient reduce-scatter, a sharded Adam step and the parameter all-gather:
+// rank r sums chunk r of every rank's gradient, applies Adam to that chunk only (its optimizer
+// state shard), and pushes the updated parameters into every rank's parameter buffer. Bytes on
+// the wire equal one two-shot allreduce, but the optimizer pass runs on 1/W of the vector and
+// the separate all-reduce + Adam launches disappear.
+//
+// Barrier waits are bounded (timeout_cycles of the 100 MHz s_memrealtime clock): a peer that never
+// arrives sets *err and the kernel drains instead of hanging the GPU; the host checks err.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <algorithm>
+
+#include "abi.h"
+#include "adam.h"
+
+using namespace arena;
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxB = ARENA_CCL_MAX_BLOCKS;
+constexpr int kMaxR = ARENA_CCL_MAX_RANKS;
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+__device__ __forceinline__ float4 add4(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+
+template <int W>
+__device__ __forceinline__ void xbarrier(const ArenaXgmiPeers& P, int phase, int b, uint32_t e) {
+  // every wave's stores have completed (hipcc emits vmcnt(0) before s_barrier)
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < W) {
+    const int slot = (phase * kMaxB + b) * kMaxR;
+    // release at system scope: write back L2 so our (local and remote) stores are visible first
+    __hip_atomic_store(P.sig[t] + slot + P.rank, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint32_t* mine = P.sig[P.rank] + slot + t;
+    const long long t0 = wall_clock64();
+    while ((int)(__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (wall_clock64() - t0 > P.timeout_cycles) {
+        __hip_atomic_store(P.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+  }
+  __syncthreads();
+}
+
+template <int W>
+__global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(ArenaXgmiPeers P,
+                                                                   const float* __restrict__ in,
+                                                                   float* __restrict__ out,
+                                                                   long long n, long long L,
+                                                                   long long S, float scale) {
+  const int b = blockIdx.x;
+  const uint32_t e = P.epoch[b] + 1;
+  float* mine = P.buf[P.rank];
+  const long long lo = (long long)b * S;
+  const long long hi = std::min(lo + S, L);
+  if (in != mine) {
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+      for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
+        const long long i = (long long)c * L + o;
+        if (i < n) st4(mine + i, ld4(in + i));
+      }
+    }
+  }
+  xbarrier<W>(P, 0, b, e);
+  const long long base = (long long)P.rank * L;
+  for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
+    const long long i = base + o;
+    if (i >= n) break;
+    float4 v[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) v[q] = ld4(P.buf[q] + i);  // W loads in flight, one per link
+    float4 acc = v[0];
+#pragma unroll
+    for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);     // fixed order: identical on all ranks
+    acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
+#pragma unroll
+    for (int q = 0; q < W; ++q) st4(P.buf[q] + i, acc);
+  }
+  xbarrier<W>(P, 1, b, e);
+  if (out != mine) {
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+      for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
+        const long long i = (long long)c * L + o;
+        if (i < n) st4(out + i, ld4(mine + i));
+      }
+    }
+  }
+  if (threadIdx.x == 0) P.epoch[b] = e;
+}
+
+template <int W>
+__global__ __launch_bounds__(kThreads) void xgmi_adam_kernel(ArenaXgmiPeers P, float* __restrict__ M,
+                                                              float* __restrict__ V, long long n,
+                                                              long long L, long long S, ArenaAdam a,
+                                                              ArenaCounterOp ctr) {
+  const int b = blockIdx.x;
+  const uint32_t e = P.epoch[b] + 1;
+  const AdamCoef co = adam_coef(a);  // t / lr loads issued before the barrier wait
+  const long long lo = (long long)b * S;
+  const long long hi = std::min(lo + S, L);
+  xbarrier<W>(P, 0, b, e);
+  const long long base = (long long)P.rank * L;
+  float* Pm = P.buf2[P.rank];
+  for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
+    const long long i = base + o;
+    if (i >= n) break;
+    float4 v[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) v[q] = ld4(P.buf[q] + i);
+    float4 p = ld4(Pm + i);
+    float4 m = ld4(M + i);
+    float4 s = ld4(V + i);
+    float4 g = v[0];
+#pragma unroll
+    for (int q = 1; q < W; ++q) g = add4(g, v[q]);
+    adam_apply(co, g.x, p.x, m.x, s.x);
+    adam_apply(co, g.y, p.y, m.y, s.y);
+    adam_apply(co, g.z, p.z, m.z, s.z);
+    adam_apply(co, g.w, p.w, m.w, s.w);
+    st4(M + i, m);
+    st4(V + i, s);
+#pragma unroll
+    for (int q = 0; q < W; ++q) st4(P.buf2[q] + i, p);
+  }
+  xbarrier<W>(P, 1, b, e);
+  counter_op(ctr);
+  if (threadIdx.x == 0) P.epoch[b] = e;
+}
+
+void geometry(long long n, int W, long long* L, long long* S, int* nb) {
+  long long l = (n + W - 1) / W;
+  l = (l + 3) / 4 * 4;
+  int blocks = (int)std::min<long long>(kMaxB, std::max<long long>(1, (l + 1023) / 1024));
+  long long s = (l + blocks - 1) / blocks;
+  s = (s + 3) / 4 * 4;
+  *L = l;
+  *S = s;
+  *nb = blocks;
+}
+
+}  // namespace
+
+extern "C" {
+
+hipError_t arena_ccl_malloc(void** p, size_t bytes, int uncached) {
+  if (uncached) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+  return hipMalloc(p, bytes);
+}
+
+hipError_t arena_ccl_free(void* p) { return hipFree(p); }
+
+hipError_t arena_ccl_memset(void* p, int v, size_t bytes) {
+  hipError_t e = hipMemset(p, v, bytes);
+  if (e != hipSuccess) return e;
+  return hipDeviceSynchronize();
+}
+
+hipError_t arena_ccl_ipc_get(void* p, void* handle) {
+  return hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle), p);
+}
+
+hipError_t arena_ccl_ipc_open(const void* handle, void** p) {
+  hipIpcMemHandle_t h;
+  __builtin_memcpy(&h, handle, sizeof h);
+  return hipIpcOpenMemHandle(p, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+hipError_t arena_ccl_ipc_close(void* p) { return hipIpcCloseMemHandle(p); }
+
+#define ARENA_CCL_DISPATCH(W, KERNEL, ...)                                                   \
+  switch (W) {                                                                               \
+    case 2: hipLaunchKernelGGL(KERNEL<2>, __VA_ARGS__); break;                              \
+    case 3: hipLaunchKernelGGL(KERNEL<3>, __VA_ARGS__); break;                              \
+    case 4: hipLaunchKernelGGL(KERNEL<4>, __VA_ARGS__); break;                              \
+    case 5: hipLaunchKernelGGL(KERNEL<5>, __VA_ARGS__); break;                              \
+    case 6: hipLaunchKernelGGL(KERNEL<6>, __VA_ARGS__); break;                              \
+    case 7: hipLaunchKernelGGL(KERNEL<7>, __VA_ARGS__); break;                              \
+    case 8: hipLaunchKernelGGL(KERNEL<8>, __VA_ARGS__); break;                              \
+    default: return hipErrorInvalidValue;                                                    \
+  }
+
+hipError_t arena_ccl_allreduce(const ArenaXgmiPeers* P, const float* in, float* out, long long n,
+                               float scale, hipStream_t stream) {
+  const int W = P->world;
+  if (W < 2 || W > kMaxR || n <= 0 || n % 4 || n > P->buf_elems) return hipErrorInvalidValue;
+  long long L, S;
+  int nb;
+  geometry(n, W, &L, &S, &nb);
+  ARENA_CCL_DISPATCH(W, xgmi_allreduce_kernel, dim3(nb), dim3(kThreads), 0, stream, *P, in, out,
+                     n, L, S, scale);
+  return hipGetLastError();
+}
+
+hipError_t arena_ccl_adam(const ArenaXgmiPeers* P, float* M, float* V, long long n, ArenaAdam a,
+                          ArenaCounterOp ctr, hipStream_t stream) {
+  const int W = P->world;
+  if (W < 2 || W > kMaxR || n <= 0 || n % 4 || n > P->buf_elems || n > P->buf2_elems)
+    return hipErrorInvalidValue;
+  long long L, S;
+  int nb;
+  geometry(n, W, &L, &S, &nb);
+  ARENA_CCL_DISPATCH(W, xgmi_adam_kernel, dim3(nb), dim3(kThreads), 0, stream, *P, M, V, n, L, S,
+                     a, ctr);
+  return hipGetLastError();
+}
+
+// The slice of the flat vector whose optimizer state rank `r` owns under arena_ccl_adam.
+void arena_ccl_shard(long long n, int world, int r, long long* lo, long long* hi) {
+  long long L, S;
+  int nb;
+  geometry(n, world, &L, &S, &nb);
+  *lo = std::min(n, (long long)r * L);
+  *hi = std::min(n, (long long)(r + 1) * L);
+}
+
+}  // extern "C"

@@ -73,4 +73,20 @@ struct ArenaHead {
   float* loss_acc; int* correct_acc; int hist_len;  // metric ring (block 0), power of two
 };
 
+
+// Intra-node xGMI collective (csrc/ccl/xgmi_ccl.hip): every rank's registered buffers, mapped into
+// this process through hipIpc handles (buf[rank] / sig[rank] are the local allocations).
+#define ARENA_CCL_MAX_RANKS 8
+#define ARENA_CCL_MAX_BLOCKS 256
+struct ArenaXgmiPeers {
+  float* buf[ARENA_CCL_MAX_RANKS];    // staging / gradient buffer of each rank
+  float* buf2[ARENA_CCL_MAX_RANKS];   // second buffer (parameters for the fused Adam step)
+  uint32_t* sig[ARENA_CCL_MAX_RANKS]; // uncached flags: [2 phases][MAX_BLOCKS][MAX_RANKS]
+  uint32_t* epoch;                    // local, per block: calls completed
+  int* err;                           // local: set to 1 when a barrier wait timed out
+  long long buf_elems;                // capacity of buf[] (floats)
+  long long buf2_elems;
+  int rank, world;
+  long long timeout_cycles;           // barrier wait bound in s_memrealtime ticks (100 MHz)
+};
 }  // extern "C"

@@ -1,0 +1,49 @@
+// Device-side optimizer + step-counter helpers shared by the MLP kernels (mlp_kernels.hip) and
+// the fused xGMI reduce-scatter/Adam/all-gather collective (csrc/ccl/xgmi_ccl.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "abi.h"
+
+namespace arena {
+
+__device__ __forceinline__ void counter_op(const ArenaCounterOp& c) {
+  if (c.dst != nullptr && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    *c.dst = (c.src ? *c.src : 0) + c.add;
+  }
+}
+
+__device__ __forceinline__ float adam_lr(const ArenaAdam& a) { return a.lr_ptr ? *a.lr_ptr : a.lr; }
+
+struct AdamCoef {
+  float step_size, inv_sqrt_bc2, eps, b1, b2, wd, gscale;
+  int tf;
+};
+
+__device__ __forceinline__ AdamCoef adam_coef(const ArenaAdam& a) {
+  AdamCoef c;
+  const float t = a.t_ptr ? (float)(*a.t_ptr) : 1.0f;
+  const float bc1 = 1.0f - exp2f(t * log2f(a.beta1));
+  const float bc2 = 1.0f - exp2f(t * log2f(a.beta2));
+  const float lr = adam_lr(a);
+  c.tf = a.tf_style;
+  if (a.tf_style) {
+    c.step_size = lr * sqrtf(bc2) / bc1;
+    c.inv_sqrt_bc2 = 1.0f;
+  } else {
+    c.step_size = lr / bc1;
+    c.inv_sqrt_bc2 = 1.0f / sqrtf(bc2);
+  }
+  c.eps = a.eps; c.b1 = a.beta1; c.b2 = a.beta2; c.wd = a.weight_decay; c.gscale = a.grad_scale;
+  return c;
+}
+
+__device__ __forceinline__ void adam_apply(const AdamCoef& c, float g, float& p, float& m, float& v) {
+  g = g * c.gscale + c.wd * p;
+  m = c.b1 * m + (1.0f - c.b1) * g;
+  v = c.b2 * v + (1.0f - c.b2) * g * g;
+  // torch: p -= (lr/bc1) * m / (sqrt(v)/sqrt(bc2) + eps);  tf: p -= lr_t * m / (sqrt(v) + eps)
+  p -= c.step_size * m / (sqrtf(v) * c.inv_sqrt_bc2 + c.eps);
+}
+
+}  // namespace arena

@@ -5,6 +5,8 @@
 #include <c10/hip/HIPStream.h>
 #include <hip/hip_runtime_api.h>
 
+#include <cstring>
+#include <string>
 #include <vector>
 
 #include "abi.h"
@@ -28,6 +30,18 @@ hipError_t arena_softmax_xent(const float*, const long long*, int, int, float*, 
                               hipStream_t);
 hipError_t arena_mt_copy_scale(float* const*, const long long*, const long long*, int, float*, float,
                                int, hipStream_t);
+// csrc/ccl/xgmi_ccl.hip
+hipError_t arena_ccl_malloc(void**, size_t, int);
+hipError_t arena_ccl_free(void*);
+hipError_t arena_ccl_memset(void*, int, size_t);
+hipError_t arena_ccl_ipc_get(void*, void*);
+hipError_t arena_ccl_ipc_open(const void*, void**);
+hipError_t arena_ccl_ipc_close(void*);
+hipError_t arena_ccl_allreduce(const ArenaXgmiPeers*, const float*, float*, long long, float,
+                               hipStream_t);
+hipError_t arena_ccl_adam(const ArenaXgmiPeers*, float*, float*, long long, ArenaAdam,
+                          ArenaCounterOp, hipStream_t);
+void arena_ccl_shard(long long, int, int, long long*, long long*);
 }
 
 namespace {
@@ -487,6 +501,115 @@ void mt_copy_scale(std::vector<Tensor> tensors, std::vector<int64_t> offsets, Te
             "mt_copy_scale");
 }
 
+// ------------------------------------------------------------------------------ xGMI collective
+int64_t ccl_malloc(int64_t bytes, bool uncached) {
+  TORCH_CHECK(bytes > 0, "ccl_malloc: bytes must be positive");
+  void* p = nullptr;
+  check_hip(arena_ccl_malloc(&p, (size_t)bytes, uncached ? 1 : 0), "ccl_malloc");
+  return reinterpret_cast<int64_t>(p);
+}
+void ccl_free(int64_t p) { check_hip(arena_ccl_free(reinterpret_cast<void*>(p)), "ccl_free"); }
+void ccl_memset(int64_t p, int64_t v, int64_t bytes) {
+  check_hip(arena_ccl_memset(reinterpret_cast<void*>(p), (int)v, (size_t)bytes), "ccl_memset");
+}
+py::bytes ccl_ipc_get(int64_t p) {
+  char h[64];
+  check_hip(arena_ccl_ipc_get(reinterpret_cast<void*>(p), h), "hipIpcGetMemHandle");
+  return py::bytes(h, 64);
+}
+int64_t ccl_ipc_open(py::bytes handle) {
+  std::string h = handle;
+  TORCH_CHECK(h.size() == 64, "IPC handle must be 64 bytes");
+  void* p = nullptr;
+  check_hip(arena_ccl_ipc_open(h.data(), &p), "hipIpcOpenMemHandle");
+  return reinterpret_cast<int64_t>(p);
+}
+void ccl_ipc_close(int64_t p) {
+  check_hip(arena_ccl_ipc_close(reinterpret_cast<void*>(p)), "hipIpcCloseMemHandle");
+}
+// A float32 view of registered memory (no ownership: the communicator frees it).
+Tensor ccl_tensor(int64_t p, int64_t numel, int64_t device) {
+  auto opts = torch::TensorOptions().dtype(torch::kFloat32).device(torch::kCUDA, device);
+  return torch::from_blob(reinterpret_cast<void*>(p), {numel}, [](void*) {}, opts);
+}
+std::vector<int64_t> ccl_shard(int64_t n, int64_t world, int64_t rank) {
+  long long lo = 0, hi = 0;
+  arena_ccl_shard(n, (int)world, (int)rank, &lo, &hi);
+  return {lo, hi};
+}
+
+class XgmiPeers {
+ public:
+  XgmiPeers(std::vector<int64_t> bufs, std::vector<int64_t> bufs2, std::vector<int64_t> sigs,
+            Tensor epoch, Tensor err, int64_t buf_elems, int64_t buf2_elems, int64_t rank,
+            double timeout_s)
+      : epoch_(epoch), err_(err) {
+    const int64_t w = (int64_t)bufs.size();
+    TORCH_CHECK(w >= 2 && w <= ARENA_CCL_MAX_RANKS, "xGMI collective: world size must be 2..",
+                ARENA_CCL_MAX_RANKS);
+    TORCH_CHECK((int64_t)sigs.size() == w, "one signal buffer per rank");
+    TORCH_CHECK(bufs2.empty() || (int64_t)bufs2.size() == w, "one second buffer per rank");
+    TORCH_CHECK(rank >= 0 && rank < w, "rank out of range");
+    check_dev(epoch, "epoch");
+    check_dev(err, "err");
+    TORCH_CHECK(epoch.scalar_type() == torch::kInt32 && epoch.numel() >= ARENA_CCL_MAX_BLOCKS,
+                "epoch must be int32[", ARENA_CCL_MAX_BLOCKS, "]");
+    TORCH_CHECK(err.scalar_type() == torch::kInt32 && err.numel() >= 1, "err must be int32[1]");
+    std::memset(&p_, 0, sizeof p_);
+    for (int64_t i = 0; i < w; ++i) {
+      TORCH_CHECK(bufs[i] != 0 && sigs[i] != 0, "null peer pointer for rank ", i);
+      p_.buf[i] = reinterpret_cast<float*>(bufs[i]);
+      p_.sig[i] = reinterpret_cast<uint32_t*>(sigs[i]);
+      if (!bufs2.empty()) p_.buf2[i] = reinterpret_cast<float*>(bufs2[i]);
+    }
+    p_.epoch = reinterpret_cast<uint32_t*>(epoch.data_ptr<int32_t>());
+    p_.err = err.data_ptr<int32_t>();
+    p_.buf_elems = buf_elems;
+    p_.buf2_elems = bufs2.empty() ? 0 : buf2_elems;
+    p_.rank = (int)rank;
+    p_.world = (int)w;
+    p_.timeout_cycles = (long long)(timeout_s * 1e8);  // s_memrealtime runs at 100 MHz
+  }
+
+  void allreduce(Tensor in, Tensor out, double scale) {
+    check_f32(in, "in");
+    check_f32(out, "out");
+    const int64_t n = in.numel();
+    TORCH_CHECK(out.numel() == n, "allreduce: in/out size mismatch");
+    TORCH_CHECK(n % 4 == 0 && n <= p_.buf_elems, "allreduce: numel must be a multiple of 4 and <= ",
+                p_.buf_elems);
+    check_hip(arena_ccl_allreduce(&p_, in.data_ptr<float>(), out.data_ptr<float>(), n,
+                                  (float)scale, cur_stream()),
+              "xgmi_allreduce");
+  }
+
+  void adam(Tensor M, Tensor V, int64_t n, double lr, OptT lr_t, double b1, double b2, double eps,
+            double wd, OptT t_step, double grad_scale, bool tf_style, OptT ctr_dst, OptT ctr_src,
+            int64_t ctr_add) {
+    check_f32(M, "M");
+    check_f32(V, "V");
+    TORCH_CHECK(p_.buf2[0] != nullptr, "xgmi adam needs the parameter buffers (buf2)");
+    TORCH_CHECK(M.numel() >= n && V.numel() >= n && n % 4 == 0 && n <= p_.buf_elems &&
+                    n <= p_.buf2_elems,
+                "xgmi adam: bad sizes");
+    ArenaAdam a = make_adam(lr, lr_t, b1, b2, eps, wd, t_step, grad_scale, tf_style);
+    ArenaCounterOp ctr{};
+    if (ctr_dst.has_value()) {
+      ctr.dst = const_cast<long long*>(opt_i64_scalar(ctr_dst, "ctr_dst"));
+      ctr.src = opt_i64_scalar(ctr_src, "ctr_src");
+      ctr.add = (int)ctr_add;
+    }
+    check_hip(arena_ccl_adam(&p_, M.data_ptr<float>(), V.data_ptr<float>(), n, a, ctr, cur_stream()),
+              "xgmi_adam");
+  }
+
+  int64_t world() const { return p_.world; }
+
+ private:
+  ArenaXgmiPeers p_;
+  Tensor epoch_, err_;  // keep the device state alive
+};
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -499,6 +622,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_flat", &sgd_flat);
   m.def("softmax_xent", &softmax_xent);
   m.def("mt_copy_scale", &mt_copy_scale);
+  m.def("ccl_malloc", &ccl_malloc);
+  m.def("ccl_free", &ccl_free);
+  m.def("ccl_memset", &ccl_memset);
+  m.def("ccl_ipc_get", &ccl_ipc_get);
+  m.def("ccl_ipc_open", &ccl_ipc_open);
+  m.def("ccl_ipc_close", &ccl_ipc_close);
+  m.def("ccl_tensor", &ccl_tensor);
+  m.def("ccl_shard", &ccl_shard);
+  py::class_<XgmiPeers>(m, "XgmiPeers")
+      .def(py::init<std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, Tensor,
+                    Tensor, int64_t, int64_t, int64_t, double>())
+      .def("allreduce", &XgmiPeers::allreduce)
+      .def("adam", &XgmiPeers::adam)
+      .def_property_readonly("world", &XgmiPeers::world);
+  m.attr("ccl_max_blocks") = ARENA_CCL_MAX_BLOCKS;
+  m.attr("ccl_max_ranks") = ARENA_CCL_MAX_RANKS;
   m.attr("arch") = "gfx950";
 #ifndef ARENA_SRC_HASH
 #define ARENA_SRC_HASH "unknown"

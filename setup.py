@@ -19,7 +19,7 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 if ARCH != "gfx950":
     raise SystemExit(f"arena_amd targets MI355X only (gfx950); PYTORCH_ROCM_ARCH={ARCH}")
 
-HIP_SOURCES = ["csrc/ops/mlp_kernels.hip"]
+HIP_SOURCES = ["csrc/ops/mlp_kernels.hip", "csrc/ccl/xgmi_ccl.hip"]
 CPP_SOURCES = ["csrc/ops/bindings.cpp"]
 
 ext_modules = []
@@ -30,7 +30,7 @@ try:
     sys.path.insert(0, os.path.join(HERE, "arena_amd", "ops"))
     from _srchash import source_hash  # noqa: E402
 
-    src_hash = source_hash(os.path.join(HERE, "csrc", "ops"))
+    src_hash = source_hash(os.path.join(HERE, "csrc", "ops"), os.path.join(HERE, "csrc", "ccl"))
     obj_dir = os.path.join(HERE, "build", "hip_objs")
     hip_objs = [os.path.join(obj_dir, os.path.basename(s).replace(".hip", ".o"))
                 for s in HIP_SOURCES]
@@ -43,7 +43,8 @@ try:
             hipcc = os.path.join(ROCM, "bin", "hipcc")
             for src, obj in zip(HIP_SOURCES, hip_objs):
                 srcp = os.path.join(HERE, src)
-                deps = [srcp] + [os.path.join(HERE, "csrc", "ops", h) for h in ("abi.h", "common.h")]
+                deps = [srcp] + [os.path.join(HERE, "csrc", "ops", h)
+                                for h in ("abi.h", "common.h", "adam.h")]
                 if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d)
                                                for d in deps):
                     continue

@@ -1,0 +1,203 @@
+"""xGMI collective on a real MI355X: W processes share one GPU through hipIpc handles.
+
+(RCCL refuses two ranks on one device, but the hipIpc peer-memory protocol is the same whether the
+mapped buffers live on this GPU or on a peer over xGMI, so barrier/race logic and numerics are
+covered here; link bandwidth needs the multi-GPU node.) Reference = exact fp32 sums on the host
+and torch.optim.Adam / the flat Adam kernel.
+"""
+from __future__ import annotations
+
+import os
+import socket
+import traceback
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _init(rank, world, port):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(world))
+    torch.cuda.set_device(0)
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    return dist
+
+
+def _collectives(rank, world, port, q):
+    try:
+        dist = _init(rank, world, port)
+        from arena_amd.parallel.xgmi import XgmiComm
+        comm = XgmiComm(staging_elems=1 << 16, timeout_s=30.0)
+        res = {}
+        g = torch.Generator(device="cuda").manual_seed(1234)
+        for n in (4, 12, 4096, 65536, 1 << 16, 3 * (1 << 16) + 4, 1001, 70001):
+            xs = [torch.randint(-1000, 1000, (n,), device="cuda", generator=g).float()
+                  for _ in range(world)]
+            want = sum(xs) * 0.5
+            x = xs[rank].clone()
+            comm.all_reduce_(x, scale=0.5)
+            res[n] = bool(torch.equal(x, want))
+        # zero-copy from the staging buffer, out-of-place destination
+        stage = comm.buffer()[:256]
+        stage.copy_(torch.full((256,), float(rank + 1), device="cuda"))
+        out = torch.empty(256, device="cuda")
+        comm.all_reduce_(stage, out=out)
+        res["zc"] = bool(torch.all(out == sum(range(1, world + 1))))
+        # repeated calls (flag counters advance; no reset between calls), captured in a graph
+        y = torch.ones(4096, device="cuda") * (rank + 1)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            comm.all_reduce_(y, scale=1.0 / world)
+        torch.cuda.current_stream().wait_stream(s)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr):
+            for _ in range(3):
+                comm.all_reduce_(y, scale=1.0 / world)
+        for _ in range(5):
+            gr.replay()
+        torch.cuda.synchronize()
+        mean = sum(range(1, world + 1)) / world
+        res["graph"] = bool(torch.allclose(y, torch.full_like(y, mean)))
+        comm.check()
+        res["err"] = int(comm._err.item())
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
+def _adam(rank, world, port, q):
+    try:
+        dist = _init(rank, world, port)
+        from arena_amd import ops
+        from arena_amd.parallel.xgmi import XgmiComm
+        n = 50000
+        comm = XgmiComm(staging_elems=n, param_elems=n, timeout_s=30.0)
+        g = torch.Generator(device="cuda").manual_seed(7)
+        P0 = torch.randn(n, device="cuda", generator=g)
+        grads = [[torch.randn(n, device="cuda", generator=g) for _ in range(world)]
+                 for _ in range(3)]
+        P = comm.params()[:n]
+        P.copy_(P0)
+        M = torch.zeros(n, device="cuda")
+        V = torch.zeros(n, device="cuda")
+        t = torch.zeros(1, dtype=torch.int64, device="cuda")
+        Pr, Mr, Vr = P0.clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+        for step in range(3):
+            t.fill_(step + 1)
+            comm.buffer()[:n].copy_(grads[step][rank])
+            torch.cuda.synchronize()
+            dist.barrier()
+            comm.adam_(M, V, n, lr=1e-2, t_step=t, grad_scale=1.0 / world)
+            gsum = sum(grads[step])
+            ops.adam_flat(Pr, Mr, Vr, gsum, lr=1e-2, t_step=t, grad_scale=1.0 / world)
+        torch.cuda.synchronize()
+        dist.barrier()
+        lo, hi = comm.shard(n)
+        res = {"P": float((P - Pr).abs().max()),
+               "M_own": float((M[lo:hi] - Mr[lo:hi]).abs().max()),
+               "M_other_zero": bool(torch.all(M[:lo] == 0) and torch.all(M[hi:] == 0)),
+               "err": int(comm._err.item())}
+        comm.close()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
+def _trainer(rank, world, port, q):
+    try:
+        _init(rank, world, port)
+        import torch.distributed as dist
+        from arena_amd.models.mlp import FusedMLPTrainer, MLPConfig
+        g = torch.Generator().manual_seed(3)
+        x = torch.randint(0, 256, (2000, 784), dtype=torch.uint8, generator=g)
+        y = torch.randint(0, 10, (2000,), dtype=torch.uint8, generator=g)
+        cfg = MLPConfig(batch=100, seed=5)
+        class GlooRef(FusedMLPTrainer):
+            """Reference DP step: the flat gradient summed by gloo on the host."""
+
+            def _launch_step_part(self, part):
+                if part == 1:
+                    torch.cuda.synchronize()
+                    gh = self.G.cpu()
+                    dist.all_reduce(gh)
+                    self.G.copy_(gh)
+                    return
+                super()._launch_step_part(part)
+
+        tx = FusedMLPTrainer(cfg, x, y, device="cuda", process_group=dist.group.WORLD, rank=rank,
+                             world=world, comm="xgmi")
+        tr = GlooRef(cfg, x, y, device="cuda", process_group=dist.group.WORLD, rank=rank,
+                     world=world, comm="rccl")
+        assert tx.comm == "xgmi" and tr.comm == "rccl"
+        tx.train_steps(4)
+        tr.train_steps(4)
+        tx.enable_graphs(4)          # graph-captured xGMI step must continue identically
+        tx.train_steps(8)
+        tr.train_steps(8)
+        torch.cuda.synchronize()
+        sd = tx.state_dict()         # reassembles the sharded optimizer state
+        res = {"P": float((tx.P - tr.P).abs().max()), "M": float((sd["M"] - tr.M.cpu()).abs().max()),
+               "steps": int(tx.ctrA.item()), "mode": tx.graph_mode}
+        tx.xgmi.check()
+        q.put((rank, res, None))
+        dist.destroy_process_group()
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
+def _run(fn, world, timeout=240):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=fn, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = {}
+    try:
+        for _ in range(world):
+            r, res, err = q.get(timeout=timeout)
+            assert err is None, f"rank {r} failed:\n{err}"
+            out[r] = res
+    finally:
+        for p in procs:
+            p.join(30)
+            if p.is_alive():
+                p.kill()
+    return out
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_allreduce_exact(world):
+    out = _run(_collectives, world)
+    for r, res in out.items():
+        assert all(v is True for k, v in res.items() if k != "err"), (r, res)
+        assert res["err"] == 0
+
+
+def test_xgmi_fused_adam_matches_flat_adam():
+    out = _run(_adam, 2)
+    for r, res in out.items():
+        assert res["P"] < 1e-6 and res["M_own"] < 1e-6 and res["M_other_zero"], (r, res)
+        assert res["err"] == 0
+
+
+def test_trainer_dp_xgmi_matches_allreduce_path():
+    out = _run(_trainer, 2)
+    for r, res in out.items():
+        assert res["steps"] == 12 and res["mode"] == "full", res
+        # logits accumulate with f32 atomics (order varies run to run): equal to rounding
+        assert res["P"] < 5e-5 and res["M"] < 1e-6, (r, res)
