@@ -362,6 +362,7 @@ class LocalBackend(Backend):
             if kind == "allreduce" and role in ("mpimaster", "mpiworker"):
                 env["MASTER_ADDR"] = "127.0.0.1"
                 env["MASTER_PORT"] = str(ports["rdzv"])
+                env["LOCAL_WORLD_SIZE"] = str(len(ranks))   # every rank is on this node
                 if union:
                     env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, union))
                     env["LOCAL_RANK"] = str(union.index(own[0])) if own else "0"

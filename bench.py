@@ -33,6 +33,9 @@ def parse():
     ap.add_argument("--batch", type=int, default=100)
     ap.add_argument("--steps-per-graph", type=int, default=0, help="0 = auto")
     ap.add_argument("--eval", action="store_true", help="report test accuracy after timing")
+    ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
+                    help="DP gradient path: fused xGMI reduce-scatter/Adam/all-gather kernel or "
+                         "RCCL all_reduce + flat Adam (auto = xgmi when its self-test passes)")
     return ap.parse_args()
 
 
@@ -62,11 +65,13 @@ def main():
 
     if args.impl == "fused":
         tr = FusedMLPTrainer(cfg, data.train_images, data.train_labels, device=dev,
-                             process_group=pg, rank=rank, world=world)
+                             process_group=pg, rank=rank, world=world, comm=args.comm)
         spg = args.steps_per_graph or tr.pick_steps_per_graph()
         graphs = tr.enable_graphs(spg)
         run = tr.train_steps
         mode = f"hipgraph[{tr.graph_mode},{spg} steps/graph]" if graphs else "eager"
+        if world > 1:
+            mode += f",comm={tr.comm}"
     else:
         from arena_amd.models.torch_mlp import EagerMLPTrainer
         tr = EagerMLPTrainer(cfg, data.train_images, data.train_labels, device=dev,
@@ -93,6 +98,8 @@ def main():
         elapsed = float(e.item())
 
     extra = {}
+    if getattr(tr, "xgmi", None) is not None:
+        tr.xgmi.check()  # a timed-out barrier would mean invalid results: fail loudly
     loss, acc = tr.recent_metrics(100)
     extra["train_loss_last100"] = round(loss, 5)
     extra["train_acc_last100"] = round(acc, 5)

@@ -53,22 +53,47 @@ template <int W>
 __device__ __forceinline__ void xbarrier(const ArenaXgmiPeers& P, int phase, int b, uint32_t e) {
   // every wave's stores have completed (hipcc emits vmcnt(0) before s_barrier)
   __syncthreads();
-  const int t = threadIdx.x;
-  if (t < W) {
-    const int slot = (phase * kMaxB + b) * kMaxR;
-    // release at system scope: write back L2 so our (local and remote) stores are visible first
-    __hip_atomic_store(P.sig[t] + slot + P.rank, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    const uint32_t* mine = P.sig[P.rank] + slot + t;
-    const long long t0 = wall_clock64();
-    while ((int)(__hip_atomic_load(mine, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
-      if (wall_clock64() - t0 > P.timeout_cycles) {
-        __hip_atomic_store(P.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+  if (threadIdx.x < 64) {
+    // ONE system-scope release per block (buffer_wbl2: our stores reach memory before the flags),
+    // flags written and polled with relaxed system-scope accesses to uncached memory, then ONE
+    // acquire (buffer_inv). An acquire per poll would invalidate L2 on every spin iteration.
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    const int t = threadIdx.x;
+    if (t < W) {
+      const int slot = (phase * kMaxB + b) * kMaxR;
+      __hip_atomic_store(P.sig[t] + slot + P.rank, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t* mine = P.sig[P.rank] + slot + t;
+      const long long t0 = wall_clock64();
+      while ((int)(__hip_atomic_load(mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+        if (wall_clock64() - t0 > P.timeout_cycles) {
+          __hip_atomic_store(P.err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
       }
-      __builtin_amdgcn_s_sleep(1);
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
+}
+
+// dst[c*L + o] = src[c*L + o] for all chunks c, W loads in flight per thread.
+template <int W>
+__device__ __forceinline__ void copy_chunks(float* __restrict__ dst, const float* __restrict__ src,
+                                            long long n, long long L, long long lo, long long hi) {
+  for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
+    float4 v[W];
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+      const long long i = (long long)c * L + o;
+      if (i < n) v[c] = ld4(src + i);
+    }
+#pragma unroll
+    for (int c = 0; c < W; ++c) {
+      const long long i = (long long)c * L + o;
+      if (i < n) st4(dst + i, v[c]);
+    }
+  }
 }
 
 template <int W>
@@ -82,15 +107,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(ArenaXgmiPeers
   float* mine = P.buf[P.rank];
   const long long lo = (long long)b * S;
   const long long hi = std::min(lo + S, L);
-  if (in != mine) {
-#pragma unroll
-    for (int c = 0; c < W; ++c) {
-      for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
-        const long long i = (long long)c * L + o;
-        if (i < n) st4(mine + i, ld4(in + i));
-      }
-    }
-  }
+  if (in != mine) copy_chunks<W>(mine, in, n, L, lo, hi);
   xbarrier<W>(P, 0, b, e);
   const long long base = (long long)P.rank * L;
   for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
@@ -107,15 +124,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(ArenaXgmiPeers
     for (int q = 0; q < W; ++q) st4(P.buf[q] + i, acc);
   }
   xbarrier<W>(P, 1, b, e);
-  if (out != mine) {
-#pragma unroll
-    for (int c = 0; c < W; ++c) {
-      for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
-        const long long i = (long long)c * L + o;
-        if (i < n) st4(out + i, ld4(mine + i));
-      }
-    }
-  }
+  if (out != mine) copy_chunks<W>(out, mine, n, L, lo, hi);
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
@@ -158,10 +167,15 @@ __global__ __launch_bounds__(kThreads) void xgmi_adam_kernel(ArenaXgmiPeers P, f
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
+// Floats of a chunk per block. Every block pays two cross-rank barriers (one L2 writeback + one
+// invalidate each), so blocks are made fat rather than numerous; tunable for sweeps.
+long long g_block_elems = 4096;
+
 void geometry(long long n, int W, long long* L, long long* S, int* nb) {
   long long l = (n + W - 1) / W;
   l = (l + 3) / 4 * 4;
-  int blocks = (int)std::min<long long>(kMaxB, std::max<long long>(1, (l + 1023) / 1024));
+  int blocks = (int)std::min<long long>(
+      kMaxB, std::max<long long>(1, (l + g_block_elems - 1) / g_block_elems));
   long long s = (l + blocks - 1) / blocks;
   s = (s + 3) / 4 * 4;
   *L = l;
@@ -234,6 +248,8 @@ hipError_t arena_ccl_adam(const ArenaXgmiPeers* P, float* M, float* V, long long
                      a, ctr);
   return hipGetLastError();
 }
+
+void arena_ccl_set_block_elems(long long e) { g_block_elems = e < 256 ? 256 : e; }
 
 // The slice of the flat vector whose optimizer state rank `r` owns under arena_ccl_adam.
 void arena_ccl_shard(long long n, int world, int r, long long* lo, long long* hi) {

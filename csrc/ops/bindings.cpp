@@ -42,6 +42,7 @@ hipError_t arena_ccl_allreduce(const ArenaXgmiPeers*, const float*, float*, long
 hipError_t arena_ccl_adam(const ArenaXgmiPeers*, float*, float*, long long, ArenaAdam,
                           ArenaCounterOp, hipStream_t);
 void arena_ccl_shard(long long, int, int, long long*, long long*);
+void arena_ccl_set_block_elems(long long);
 }
 
 namespace {
@@ -630,6 +631,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ccl_ipc_close", &ccl_ipc_close);
   m.def("ccl_tensor", &ccl_tensor);
   m.def("ccl_shard", &ccl_shard);
+  m.def("ccl_set_block_elems", [](int64_t e) { arena_ccl_set_block_elems(e); });
   py::class_<XgmiPeers>(m, "XgmiPeers")
       .def(py::init<std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, Tensor,
                     Tensor, int64_t, int64_t, int64_t, double>())

@@ -1,0 +1,138 @@
+#!/usr/bin/env python3
+"""Collective microbenchmark: xGMI one-kernel allreduce / fused Adam vs RCCL.
+
+    # 8x MI355X node: one rank per GPU, RCCL process group
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 scripts/ccl_bench.py
+    # 1-GPU box: W ranks share GPU 0 (gloo process group, xGMI path only; "remote" reads are
+    # local HBM, so this measures the protocol's barrier + launch cost, not link bandwidth)
+    python scripts/ccl_bench.py --same-gpu 2
+
+Prints one JSON line per (op, size) from rank 0: time per call (graph-replayed, 50 calls per
+graph) and algorithm / bus bandwidth (busbw = 2 (W-1)/W * bytes / t, the ring-equivalent figure).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timed(fn, iters: int = 50, reps: int = 5) -> float:
+    """Seconds per call of fn, captured in a hipGraph of `iters` calls (launch cost excluded)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        fn()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(g):
+            for _ in range(iters):
+                fn()
+        run = g.replay
+    except Exception:  # noqa: BLE001 - e.g. a collective that refuses capture: time eagerly
+        torch.cuda.synchronize()
+
+        def run():
+            for _ in range(iters):
+                fn()
+    run()
+    torch.cuda.synchronize()
+    best = float("inf")
+    for _ in range(reps):
+        if dist.get_world_size() > 1:
+            dist.barrier()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        run()
+        b.record()
+        b.synchronize()
+        best = min(best, a.elapsed_time(b) / 1e3 / iters)
+    t = torch.tensor([best], dtype=torch.float64,
+                     device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def bench(rank: int, world: int, sizes, rccl: bool,
+          block_sweep=(1024, 2048, 4096, 8192, 16384)) -> None:
+    from arena_amd.parallel.xgmi import XgmiComm
+    maxn = max(sizes) // 4
+    comm = XgmiComm(staging_elems=maxn, param_elems=397520, timeout_s=30.0)
+    rows = []
+    for nbytes in sizes:
+        n = nbytes // 4
+        x = torch.randn(n, device="cuda")
+        stage = comm.buffer()[:n]
+        t = timed(lambda: comm.all_reduce_(stage, scale=1.0 / world))
+        rows.append(("xgmi_allreduce_zero_copy", nbytes, t))
+        y = torch.empty_like(x)
+        t = timed(lambda: comm.all_reduce_(x, out=y))
+        rows.append(("xgmi_allreduce", nbytes, t))
+        if rccl:
+            t = timed(lambda: dist.all_reduce(x))
+            rows.append(("rccl_allreduce", nbytes, t))
+    # the DP trainer's fused step collective on the MNIST MLP's flat parameter vector, swept over
+    # the per-block chunk size (fewer, fatter blocks = fewer barrier fences)
+    n = 397520
+    M = torch.zeros(n, device="cuda")
+    V = torch.zeros(n, device="cuda")
+    tt = torch.ones(1, dtype=torch.int64, device="cuda")
+    for be in block_sweep:
+        comm.ext.ccl_set_block_elems(be)
+        t = timed(lambda: comm.adam_(M, V, n, t_step=tt, grad_scale=1.0 / world))
+        rows.append((f"xgmi_rs_adam_ag(mnist_mlp,block_elems={be})", n * 4, t))
+        stage = comm.buffer()[:n]
+        t = timed(lambda: comm.all_reduce_(stage, scale=1.0 / world))
+        rows.append((f"xgmi_allreduce_zero_copy(block_elems={be})", n * 4, t))
+    comm.ext.ccl_set_block_elems(4096)
+    comm.check()
+    if rank == 0:
+        for op, nb, t in rows:
+            algbw = nb / t / 1e9
+            print(json.dumps({"op": op, "bytes": nb, "world": world, "us": round(t * 1e6, 2),
+                              "algbw_GBs": round(algbw, 2),
+                              "busbw_GBs": round(algbw * 2 * (world - 1) / world, 2)}), flush=True)
+    comm.close()
+
+
+def _same_gpu_rank(rank, world, port, sizes):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world), LOCAL_RANK="0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    bench(rank, world, sizes, rccl=False)
+    dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--same-gpu", type=int, default=0, help="W ranks sharing GPU 0 (gloo PG)")
+    ap.add_argument("--sizes", default="4096,65536,1048576,1590080,8388608,33554432")
+    args = ap.parse_args()
+    sizes = [int(s) for s in args.sizes.split(",")]
+    if args.same_gpu:
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            port = s.getsockname()[1]
+        mp.start_processes(_same_gpu_rank, args=(args.same_gpu, port, sizes), nprocs=args.same_gpu,
+                           start_method="spawn")
+        return
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    bench(dist.get_rank(), dist.get_world_size(), sizes, rccl=True)
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
