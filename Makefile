@@ -1,0 +1,35 @@
+# arena_amd build entry points (reference: Makefile:22-62 builds the static Go binaries).
+#   make            build the HIP extension (gfx950) + the native runtime tools
+#   make test       CPU test suite (no GPU needed)
+#   make test-gpu   GPU tests (MI355X)
+#   make bench      flagship benchmark, 1 GPU
+PYTHON ?= python3
+export PYTORCH_ROCM_ARCH ?= gfx950
+
+.PHONY: all ext native test test-gpu bench e2e clean version
+
+all: ext native
+
+ext:
+	$(PYTHON) setup.py build_ext --inplace
+
+native:
+	$(PYTHON) -c 'from arena_amd import _build; print("\n".join(_build.build_native_tools(force=True)))'
+
+test:
+	$(PYTHON) -m pytest tests -q -m "not gpu"
+
+test-gpu: all
+	$(PYTHON) -m pytest tests -q -m gpu
+
+bench: all
+	$(PYTHON) bench.py
+
+e2e: all
+	bash scripts/e2e_mnist.sh
+
+version:
+	$(PYTHON) -m arena_amd version
+
+clean:
+	rm -rf build arena_amd/_C*.so arena_amd/bin

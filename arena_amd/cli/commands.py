@@ -219,6 +219,8 @@ def cmd_logviewer(ctx, ns) -> int:
         ctx.out.write(f"The job {name} doesn't exist, please create it first. use 'arena submit'\n")
         return 1
     job = get_training_job(b, name, ctx.namespace)
+    if hasattr(b, "ensure_logviewer"):
+        b.ensure_logviewer()   # local backend: the built-in viewer stands in for the dashboards
     try:
         urls = job.get_job_dashboards(b, ctx.args.arenaNamespace)
     except LookupError as e:

@@ -30,8 +30,8 @@ from ..utils.timefmt import parse_rfc3339
 from . import charts
 from .backend import Backend, BackendError, Release
 from .controller import ClusterState
-from .objects import (AMD_GPU, GPU_RESOURCES, Meta, Node, POD_FAILED, POD_PENDING, POD_RUNNING,
-                      POD_SUCCEEDED, matches)
+from .objects import (AMD_GPU, GPU_RESOURCES, Endpoints, Meta, Node, POD_FAILED, POD_PENDING,
+                      POD_RUNNING, POD_SUCCEEDED, matches)
 
 log = get_logger("local")
 REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -523,8 +523,48 @@ class LocalBackend(Backend):
         return [s for s in self._cluster().services.values()
                 if s.meta.namespace == namespace and matches(s.meta.labels, selector)]
 
+    _DASHBOARDS = ("kubernetes-dashboard", "tf-job-dashboard")
+
     def get_endpoints(self, namespace, name):
+        if name in self._DASHBOARDS:
+            lv = self._logviewer()
+            if lv is None:
+                return None
+            return Endpoints(meta=Meta(name=name, namespace=namespace),
+                             addresses=[self.node_ip()], ports=[lv["port"]])
         return self._cluster().endpoints.get((namespace, name))
+
+    def _logviewer(self) -> Optional[dict]:
+        info = self._read_json(os.path.join(self.home, "logviewer.json"))
+        if info and _pid_alive(int(info.get("pid", 0))):
+            return info
+        return None
+
+    def ensure_logviewer(self, timeout_s: float = 10.0) -> Optional[dict]:
+        """Start the built-in log viewer (arena_amd.runtime.logviewer) once per job store."""
+        info = self._logviewer()
+        if info is not None:
+            return info
+        ready = os.path.join(self.home, "logviewer.json")
+        try:
+            os.unlink(ready)
+        except OSError:
+            pass
+        env = dict(os.environ)
+        env["PYTHONPATH"] = REPO_ROOT + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
+        with open(os.path.join(self.home, "logviewer.log"), "ab") as lf:
+            subprocess.Popen([sys.executable, "-m", "arena_amd.runtime.logviewer", "--home", self.home,
+                              "--port", os.environ.get("ARENA_LOGVIEWER_PORT", "0"),
+                              "--ready-file", ready],
+                             stdin=subprocess.DEVNULL, stdout=lf, stderr=lf, start_new_session=True,
+                             env=env, close_fds=True)
+        deadline = time.time() + timeout_s
+        while time.time() < deadline:
+            info = self._logviewer()
+            if info is not None:
+                return info
+            time.sleep(0.05)
+        return None
 
     def get_pod(self, namespace, name):
         return self._cluster().pods.get((namespace, name))

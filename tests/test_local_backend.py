@@ -247,3 +247,23 @@ def test_probe_reads_fake_sysfs(tmp_path):
     assert g0["links"] == [{"to": 1, "type": "xgmi", "weight": 15}]
     assert g0["busy_percent"] == 37 and g0["vram_total"] == 288 * 2**30
     assert g0["power_uw"] == 750000000
+
+
+def test_logviewer_serves_dashboard_urls(env):
+    import signal
+    import urllib.request
+    cli(env, "submit", "sj", "--name", "lvw", "echo viewer line")
+    wait_phase(env, "lvw")
+    out = cli(env, "logviewer", "lvw")
+    info = json.load(open(os.path.join(env.home, "logviewer.json")))
+    try:
+        assert f"10.0.0.7:{info['port']}/#!/log/default/lvw-training-" in out
+        base = f"http://127.0.0.1:{info['port']}"
+        jobs = json.load(urllib.request.urlopen(base + "/api/jobs", timeout=10))
+        pod = jobs[0]["pods"][0]["name"]
+        assert jobs[0]["name"] == "lvw" and jobs[0]["status"] == "Succeeded"
+        text = urllib.request.urlopen(f"{base}/api/log/default/{pod}", timeout=10).read().decode()
+        assert text == "viewer line\n"
+        assert b"arena log viewer" in urllib.request.urlopen(base + "/tfjobs/ui/", timeout=10).read()
+    finally:
+        os.kill(info["pid"], signal.SIGTERM)
