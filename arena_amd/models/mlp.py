@@ -100,6 +100,8 @@ class FusedMLPTrainer:
         self.V = torch.zeros(n, device=dev)
         self.G = torch.zeros(n, device=dev) if (self.distributed or external_update) else None
         self._init_params()
+        import os as _os
+        self._x_from_dataset = _os.environ.get("ARENA_WGRAD_X", "dataset") == "dataset"
         self.xgmi = None
         if self.distributed:
             import torch.distributed as dist
@@ -239,6 +241,13 @@ class FusedMLPTrainer:
                       head_loss_scale=1.0 / B, head_loss_acc=self.loss_hist,
                       head_correct_acc=self.corr_hist)
         xs, dzs = [self.xb, self.Hbuf], [None, None]
+        if self._x_from_dataset:
+            # gather the batch rows from the (never written) dataset instead of the forward's
+            # freshly published copy: the rows sit in this XCD's L2 from the forward's own reads
+            xs = [self.train_x, self.Hbuf]
+            # labels follow the layer-input gather: dataset labels, same rows
+            common.update(gather=[True, False], idx=self.perm, cursor=Bc, cursor_off=-1, batch=B,
+                          head_labels=self.train_y)
         if adam:
             ops.wgrad_grouped(xs, dzs, [self.W1, self.W2], [self.b1, self.b2], mode=1,
                               mW=[self.mW1, self.mW2], vW=[self.vW1, self.vW2],

@@ -20,12 +20,12 @@ struct AdamCoef {
   int tf;
 };
 
-__device__ __forceinline__ AdamCoef adam_coef(const ArenaAdam& a) {
+// coefficients from already-loaded step t and learning rate (lets a kernel issue those loads early
+// and do the math late)
+__device__ __forceinline__ AdamCoef adam_coef_tl(const ArenaAdam& a, float t, float lr) {
   AdamCoef c;
-  const float t = a.t_ptr ? (float)(*a.t_ptr) : 1.0f;
   const float bc1 = 1.0f - exp2f(t * log2f(a.beta1));
   const float bc2 = 1.0f - exp2f(t * log2f(a.beta2));
-  const float lr = adam_lr(a);
   c.tf = a.tf_style;
   if (a.tf_style) {
     c.step_size = lr * sqrtf(bc2) / bc1;
@@ -36,6 +36,10 @@ __device__ __forceinline__ AdamCoef adam_coef(const ArenaAdam& a) {
   }
   c.eps = a.eps; c.b1 = a.beta1; c.b2 = a.beta2; c.wd = a.weight_decay; c.gscale = a.grad_scale;
   return c;
+}
+
+__device__ __forceinline__ AdamCoef adam_coef(const ArenaAdam& a) {
+  return adam_coef_tl(a, a.t_ptr ? (float)(*a.t_ptr) : 1.0f, adam_lr(a));
 }
 
 __device__ __forceinline__ void adam_apply(const AdamCoef& c, float g, float& p, float& m, float& v) {

@@ -43,6 +43,9 @@ hipError_t arena_ccl_adam(const ArenaXgmiPeers*, float*, float*, long long, Aren
                           ArenaCounterOp, hipStream_t);
 void arena_ccl_shard(long long, int, int, long long*, long long*);
 void arena_ccl_set_block_elems(long long);
+#ifdef ARENA_TIMELINE
+hipError_t arena_timeline_read(long long*, int);
+#endif
 }
 
 namespace {
@@ -638,6 +641,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("allreduce", &XgmiPeers::allreduce)
       .def("adam", &XgmiPeers::adam)
       .def_property_readonly("world", &XgmiPeers::world);
+#ifdef ARENA_TIMELINE
+  m.def("timeline_read", [](bool clear) {
+    auto t = torch::empty({4, 1024, 16}, torch::TensorOptions().dtype(torch::kInt64));
+    check_hip(arena_timeline_read(reinterpret_cast<long long*>(t.data_ptr<int64_t>()), clear ? 1 : 0),
+              "timeline_read");
+    return t;
+  });
+#endif
   m.attr("ccl_max_blocks") = ARENA_CCL_MAX_BLOCKS;
   m.attr("ccl_max_ranks") = ARENA_CCL_MAX_RANKS;
   m.attr("arch") = "gfx950";

@@ -16,6 +16,36 @@
 
 namespace arena {
 
+// Optional in-kernel phase timeline (build with -DARENA_TIMELINE; scripts/timeline.py): thread 0
+// of every block stamps the 100 MHz s_memrealtime clock at phase points of a kernel, so phase
+// costs and launch skew can be read per block. Compiles to nothing in normal builds.
+#ifdef ARENA_TIMELINE
+#define ARENA_TL_SLOTS 16
+#define ARENA_TL_BLOCKS 1024
+extern __device__ long long arena_tl_buf[];
+#define ARENA_TL(kid, i)                                                                      \
+  do {                                                                                        \
+    if (threadIdx.x == 0) {                                                                   \
+      const int tl_b_ = (int)(blockIdx.x + gridDim.x * blockIdx.y);                           \
+      if (tl_b_ < ARENA_TL_BLOCKS)                                                            \
+        arena_tl_buf[((kid) * ARENA_TL_BLOCKS + tl_b_) * ARENA_TL_SLOTS + (i)] = wall_clock64(); \
+    }                                                                                         \
+  } while (0)
+#define ARENA_TL_DRAIN() __builtin_amdgcn_s_waitcnt(0)
+// make the next stamp wait until value x has arrived (loads) / been computed (MFMA)
+#define ARENA_TL_DEP(x) asm volatile("" ::"v"(x))
+#else
+#define ARENA_TL_DEP(x) \
+  do {                  \
+  } while (0)
+#define ARENA_TL(kid, i) \
+  do {                   \
+  } while (0)
+#define ARENA_TL_DRAIN() \
+  do {                   \
+  } while (0)
+#endif
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kWave = 64;

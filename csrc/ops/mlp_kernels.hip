@@ -22,6 +22,24 @@
 
 using namespace arena;
 
+#ifndef ARENA_EXP
+#define ARENA_EXP 0
+#endif
+#ifdef ARENA_TIMELINE
+__device__ long long arena::arena_tl_buf[4 * ARENA_TL_BLOCKS * ARENA_TL_SLOTS];
+extern "C" hipError_t arena_timeline_read(long long* host, int clear) {
+  const size_t bytes = sizeof(long long) * 4 * ARENA_TL_BLOCKS * ARENA_TL_SLOTS;
+  hipError_t e = hipDeviceSynchronize();
+  if (e == hipSuccess) e = hipMemcpyFromSymbol(host, HIP_SYMBOL(arena::arena_tl_buf), bytes);
+  if (e == hipSuccess && clear) {
+    void* p = nullptr;
+    e = hipGetSymbolAddress(&p, HIP_SYMBOL(arena::arena_tl_buf));
+    if (e == hipSuccess) e = hipMemset(p, 0, bytes);
+  }
+  return e;
+}
+#endif
+
 namespace {
 
 template <int XT>
@@ -361,51 +379,65 @@ __device__ __forceinline__ int load_label(const ArenaRowSource& lab, long long p
 //   D              : lane l, reg r -> dW[n0 + 4(l>>4) + r][k0 + 16w + (l&15)]   (coalesced rows)
 // >= 2 waves/SIMD so all 424 workgroups x 4 waves are co-resident in ONE round on 1024 SIMDs.
 // ---------------------------------------------------------------------------------------------
-template <int CB>  // compile-time bound on head classes (C <= CB): 10 (MNIST) or 16
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void wgrad_grouped_kernel(
-    WGradArgs args) {
-  __shared__ __attribute__((aligned(16))) float Xs[kMC * kXsStride];
-  __shared__ __attribute__((aligned(16))) float Zs[kMC * 16];
-  __shared__ __attribute__((aligned(16))) float Ds[kMC * 16];  // head: logits -> dlogits [m][c]
-  __shared__ __attribute__((aligned(16))) float W2s[16 * 16];  // head: W2 slice [c][n]
-  __shared__ int Ys[kMC];                                      // head: labels
-  __shared__ float B2s[16];
-  counter_op(args.ctr);
-  int pi = 0;
-#pragma unroll
-  for (int i = 1; i < kMaxProblems; ++i)
-    if (i < args.nprob && (int)blockIdx.x >= args.p[i].block_begin) pi = i;
+// Per-problem compile-time specialisation. SPEC == 0: every property of the problem is read at run
+// time (generic path). Otherwise SPEC - 1 = xt | hd_mode << 1 | gather << 3 | mode << 4, so hipcc
+// sees straight-line code: no branch around a load, and every independent global load of the
+// chunk is issued before the first wait (measured with scripts/timeline.py: the generic path
+// drained vmcnt between the label, index, row and step loads).
+template <int SPEC>
+struct WSpec {
+  static constexpr bool known = SPEC != 0;
+  static constexpr int s = SPEC - 1;
+  static constexpr int xt = s & 1, hm = (s >> 1) & 3, gather = (s >> 3) & 1, mode = (s >> 4) & 1;
+};
+
+constexpr int wgrad_spec(int xt, int hm, int gather, int mode) {
+  return 1 + xt + 2 * hm + 8 * gather + 16 * mode;
+}
+
+template <int CB, int SPEC, int LG>  // CB: bound on head classes (C <= CB); LG: labels gathered
+                                     // (-1: decided at run time from the label source)
+// (LDS images come in as plain pointers: __restrict__ here would let hipcc move LDS accesses
+// across the raw s_barrier in lds_barrier(), whose memory clobber noalias memory escapes)
+__device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float* Xs, float* Zs,
+                                           float* Ds, float* W2s, int* Ys, float* B2s) {
+  using WS = WSpec<SPEC>;
   const ArenaWGradProblem& P = args.p[pi];
   const ArenaHead& HD = args.head;
   const int local = blockIdx.x - P.block_begin;
-  const int tn = local / P.tiles_k, tk = local % P.tiles_k;
+  // XCD-aware tile order: workgroups are dealt to the 8 XCDs round-robin by linear block id, and
+  // the forward kernel's n-tile x runs on XCD x % 8. Giving this problem's n-tile tn to a block
+  // with blockIdx % 8 == tn % 8 keeps each 16-row slice of W (written here by Adam, read next by
+  // the forward) and of H / the W2 snapshot (written by the forward, read here) inside one XCD's L2.
+  int tn, tk;
+  if ((P.tiles_n & 7) == 0 && (P.block_begin & 7) == 0) {
+    const int xcd = local & 7, slot = local >> 3;
+    tn = xcd + 8 * (slot / P.tiles_k);
+    tk = slot % P.tiles_k;
+  } else {
+    tn = local / P.tiles_k;
+    tk = local % P.tiles_k;
+  }
   const int n0 = tn * 16, k0 = tk * 64;
   const int lane = lane_id(), w = wave_id();
   const int g = lane >> 4, c = lane & 15;
   const int kk = k0 + 16 * w + c;
   const int kkc = min(kk, P.K - 1);
   const bool bias_wave = (tk == 0) && (w == 0);
-  const bool has_bias = P.mode == 1 ? P.pB != nullptr : P.gB != nullptr;
-  const Gather gt = make_gather(P.x);
+  const int mode = WS::known ? WS::mode : P.mode;
+  const int xt = WS::known ? WS::xt : P.xt;
+  const int hmode = WS::known ? WS::hm : P.hd_mode;
+  const bool has_bias = mode == 1 ? P.pB != nullptr : P.gB != nullptr;
+  const Gather gt = (WS::known && !WS::gather) ? Gather{nullptr, 0, P.M} : make_gather(P.x);
   const bool zvec = (P.N & 3) == 0;
-  const int hmode = P.hd_mode;
-  AdamCoef co{};
-  if (P.mode == 1) co = adam_coef(args.adam);  // t / lr loads issued first, off the epilogue path
+  ARENA_TL(1, 0);
+  // step counter and Adam scalars: loads issued now, first used after the chunk's other loads
+  // are in flight (in-order vmcnt: waiting on these oldest loads leaves the younger ones going)
+  const long long hstep_raw = hmode ? *HD.step : 0;
+  const long long adam_t = (mode == 1 && args.adam.t_ptr) ? *args.adam.t_ptr : 1;
+  const float adam_lr = (mode == 1 && args.adam.lr_ptr) ? *args.adam.lr_ptr : args.adam.lr;
   const float* logits = nullptr;
   long long hstep = 0;
-  if (hmode) {
-    hstep = *HD.step + HD.step_off;
-    logits = HD.logits2 + (long long)(hstep & 1) * P.M * HD.C;
-    if ((int)blockIdx.x == args.head_block) {  // zero the other buffer + next metric slot
-      float* nxt = HD.logits2 + (long long)((hstep + 1) & 1) * P.M * HD.C;
-      for (int i = threadIdx.x; i < P.M * HD.C; i += 256) nxt[i] = 0.f;
-      if (threadIdx.x == 0 && HD.hist_len > 1) {
-        const int ns = (int)(hstep + 1) & (HD.hist_len - 1);
-        HD.loss_acc[ns] = 0.f;
-        HD.correct_acc[ns] = 0;
-      }
-    }
-  }
 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   f32x4 accb = {0.f, 0.f, 0.f, 0.f};
@@ -414,8 +446,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
     const int mcn = min(kMC, P.M - mc0);
     // (1) issue the chunk's loads
     float4 xv[kXItems];
-    if (P.xt == 1) load_x_items<1>(P, gt, mc0, mcn, k0, xv);
-    else load_x_items<0>(P, gt, mc0, mcn, k0, xv);
+    if (ARENA_EXP & 2) {
+#pragma unroll
+      for (int i = 0; i < kXItems; ++i) xv[i] = make_float4(0.5f, 0.25f, 0.f, 1.f);
+    } else if (xt == 1) {
+      load_x_items<1>(P, gt, mc0, mcn, k0, xv);
+    } else {
+      load_x_items<0>(P, gt, mc0, mcn, k0, xv);
+    }
     float4 zv[kZItems];
     float dv[kDItems];
     float wv = 0.f, bv = 0.f;
@@ -436,29 +474,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
       }
     } else {
       const int C = HD.C;
-#pragma unroll
-      for (int i = 0; i < kDItems; ++i) {  // raw logits rows: item t -> (m = t>>4, c = t&15)
-        const int t = threadIdx.x + 256 * i;
-        dv[i] = logits[(long long)(mc0 + min(t >> 4, mcn - 1)) * C + min(t & 15, C - 1)];
+      if ((int)threadIdx.x < kMC) {
+        // labels share the layer input's gather (same rows); no gather -> direct
+        const Gather lg = (LG == 0) ? Gather{nullptr, 0, P.M} : make_gather(HD.lab);
+        yv = load_label(HD.lab, gather_row(lg, mc0 + min((int)threadIdx.x, mcn - 1)));
       }
-      if ((int)threadIdx.x < kMC)
-        yv = load_label(HD.lab, gather_row(make_gather(HD.lab), mc0 + min((int)threadIdx.x, mcn - 1)));
       bv = HD.b2 ? HD.b2[min((int)threadIdx.x & 15, C - 1)] : 0.f;
       if (hmode == 2) {
 #pragma unroll
         for (int i = 0; i < kZItems; ++i) {  // mask source (post-dropout activation)
           const int t = threadIdx.x + 256 * i;
           const int rr = min(t >> 2, mcn - 1), q = t & 3;
-          zv[i] = *reinterpret_cast<const float4*>(P.hd_h + (long long)(mc0 + rr) * P.N +
-                                                   min(n0 + 4 * q, P.N - 4));
+          if (ARENA_EXP & 4) zv[i] = make_float4(1.f, 0.f, 1.f, 1.f);
+          else zv[i] = *reinterpret_cast<const float4*>(P.hd_h + (long long)(mc0 + rr) * P.N +
+                                                        min(n0 + 4 * q, P.N - 4));
         }
         wv = P.hd_w2[(long long)min((int)threadIdx.x >> 4, C - 1) * P.N +
                      min(n0 + ((int)threadIdx.x & 15), P.N - 1)];
       }
+      if (mc0 == 0) {  // first use of the step counter: every other load of the chunk is issued
+        hstep = hstep_raw + HD.step_off;
+        logits = HD.logits2 + (long long)(hstep & 1) * P.M * HD.C;
+        ARENA_TL_DEP((int)hstep);
+        ARENA_TL(1, 1);
+      }
+#pragma unroll
+      for (int i = 0; i < kDItems; ++i) {  // raw logits rows: item t -> (m = t>>4, c = t&15)
+        const int t = threadIdx.x + 256 * i;
+        if (ARENA_EXP & 1) dv[i] = 0.01f * (float)(t & 15);
+        else dv[i] = logits[(long long)(mc0 + min(t >> 4, mcn - 1)) * C + min(t & 15, C - 1)];
+      }
+      if (mc0 == 0 && (int)blockIdx.x == args.head_block) {  // zero the other buffer + next slot
+        float* nxt = HD.logits2 + (long long)((hstep + 1) & 1) * P.M * HD.C;
+        for (int i = threadIdx.x; i < P.M * HD.C; i += 256) nxt[i] = 0.f;
+        if (threadIdx.x == 0 && HD.hist_len > 1) {
+          const int ns = (int)(hstep + 1) & (HD.hist_len - 1);
+          HD.loss_acc[ns] = 0.f;
+          HD.correct_acc[ns] = 0;
+        }
+      }
     }
     // (2) on the first chunk, prefetch the tile's Adam state behind them (in-order vmcnt lets the
     //     staging waits below leave these in flight through the K-loop)
-    if (mc0 == 0 && P.mode == 1) {
+    if (mc0 == 0 && mode == 1) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const long long off = (long long)min(n0 + 4 * g + r, P.N - 1) * P.K + kkc;
@@ -502,6 +560,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
       if (threadIdx.x < 16) B2s[threadIdx.x] = bv;
       W2s[threadIdx.x] = (((int)threadIdx.x >> 4) < C) ? wv : 0.f;
       lds_barrier();
+      ARENA_TL(1, 2);
       // softmax-xent per row (thread = row): Ds row -> dlogits; block 0 also records metrics
       float loss = 0.f, corr = 0.f;
       if ((int)threadIdx.x < mcn) {
@@ -544,6 +603,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
         }
       }
       lds_barrier();
+      ARENA_TL(1, 3);
       // derive dZ for this tile into the Zs image
 #pragma unroll
       for (int i = 0; i < kZItems; ++i) {
@@ -576,6 +636,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
       }
     }
     lds_barrier();
+    ARENA_TL(1, 4);
     // (4) K-loop over all kMC rows of the image (rows >= mcn: Zs zero, Xs finite)
     if (mcn > kMC / 2) {
 #pragma unroll 8
@@ -598,8 +659,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
     }
     if (mc0 + kMC < P.M) lds_barrier();  // before the next chunk overwrites the images
   }
+  ARENA_TL_DEP(acc[0]);
+  ARENA_TL(1, 5);
+  AdamCoef co{};
+  if (mode == 1) co = adam_coef_tl(args.adam, (float)adam_t, adam_lr);
 
-  if (P.mode == 0) {
+  if (mode == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int n = n0 + 4 * g + r;
@@ -633,7 +698,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
       }
     }
   }
+  ARENA_TL(1, 6);
+  ARENA_TL_DRAIN();
+  ARENA_TL(1, 7);
 }
+
+// S0 / S1: specs of problems 0 / 1 (both nonzero = the fused MLP step's fixed pair; 0 = generic).
+template <int CB, int S0, int S1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) void wgrad_grouped_kernel(
+    WGradArgs args) {
+  __shared__ __attribute__((aligned(16))) float Xs[kMC * kXsStride];
+  __shared__ __attribute__((aligned(16))) float Zs[kMC * 16];
+  __shared__ __attribute__((aligned(16))) float Ds[kMC * 16];  // head: logits -> dlogits [m][c]
+  __shared__ __attribute__((aligned(16))) float W2s[16 * 16];  // head: W2 slice [c][n]
+  __shared__ int Ys[kMC];                                      // head: labels
+  __shared__ float B2s[16];
+  int pi = 0;
+#pragma unroll
+  for (int i = 1; i < kMaxProblems; ++i)
+    if (i < args.nprob && (int)blockIdx.x >= args.p[i].block_begin) pi = i;
+  if constexpr (S0 != 0 && S1 != 0) {
+    // the head's labels follow problem 0's gather (the binding shares it with the label source)
+    constexpr int LG = WSpec<S0>::gather;
+    if (pi == 0) wgrad_body<CB, S0, LG>(args, 0, Xs, Zs, Ds, W2s, Ys, B2s);
+    else wgrad_body<CB, S1, LG>(args, 1, Xs, Zs, Ds, W2s, Ys, B2s);
+  } else {
+    wgrad_body<CB, 0, -1>(args, pi, Xs, Zs, Ds, W2s, Ys, B2s);
+  }
+  counter_op(args.ctr);  // A = B last: nothing in this kernel reads A
+}
+
 
 // ---------------------------------------------------------------------------------------------
 // mlp_fwd_logits: linear_fwd of the hidden layer (bias, ReLU, dropout) that also emits the
@@ -654,11 +748,14 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
   const int lane = lane_id(), w = wave_id();
   const int g = lane >> 4, c = lane & 15;
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
+  ARENA_TL(0, 0);
   const int rowc = min(m0 + c, M - 1), colc = min(n0 + c, N - 1);
   const Gather gt = make_gather(src);
   const long long stepv = step_src ? *step_src : 0;
   const uint32_t step = (uint32_t)stepv;
   const long long prow = gather_row(gt, rowc);
+  ARENA_TL_DEP((int)prow);
+  ARENA_TL(0, 1);
   const float* wrow = W + (long long)colc * K;
   // n-tile-0 workgroups publish the step's gathered batch (u8 rows + labels) so the backward
   // kernel reads them directly instead of repeating the cursor -> index -> row chain
@@ -724,11 +821,14 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
       }
     }
   }
+  ARENA_TL_DEP(acc[0]);
+  ARENA_TL(0, 2);
 #pragma unroll
   for (int r = 0; r < 4; ++r) red[w][4 * g + r][c] = acc[r];
   if (threadIdx.x < 256)
     w2s[threadIdx.x >> 4][threadIdx.x & 15] = ((int)(threadIdx.x >> 4) < C) ? w2v : 0.f;
   __syncthreads();
+  ARENA_TL(0, 3);
   if (threadIdx.x < 256) {
     const int rr = threadIdx.x >> 4, cc = threadIdx.x & 15;
     const int gm = m0 + rr, gn = n0 + cc;
@@ -747,14 +847,22 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
       W2_copy[(long long)rr * N + gn] = w2v;  // thread (rr, cc) holds W2[rr][n0 + cc]
   }
   __syncthreads();
+  ARENA_TL(0, 4);
   float* lg = logits2 + (long long)(stepv & 1) * M * C;
   if ((int)threadIdx.x < 16 * C) {
     const int rr = threadIdx.x / C, cl = threadIdx.x % C;
     float p = 0.f;
 #pragma unroll
     for (int n = 0; n < 16; ++n) p += hs[rr][n] * w2s[cl][n];
-    if (m0 + rr < M) atomicAdd(&lg[(long long)(m0 + rr) * C + cl], p);
+    if (ARENA_EXP & 8) {
+      if (m0 + rr < M) lg[(long long)(m0 + rr) * C + cl] = p;
+    } else {
+      if (m0 + rr < M) atomicAdd(&lg[(long long)(m0 + rr) * C + cl], p);
+    }
   }
+  ARENA_TL(0, 5);
+  ARENA_TL_DRAIN();
+  ARENA_TL(0, 6);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -953,10 +1061,27 @@ hipError_t arena_wgrad_grouped(ArenaWGradProblem* probs, int nprob, ArenaAdam ad
   a.grad_scale = grad_scale;
   a.ctr = ctr;
   a.head = head;
-  if (head.C <= 10)
-    hipLaunchKernelGGL(wgrad_grouped_kernel<10>, dim3(blocks), dim3(256), 0, stream, a);
-  else
-    hipLaunchKernelGGL(wgrad_grouped_kernel<16>, dim3(blocks), dim3(256), 0, stream, a);
+  // the fused MLP step: problem 0 = u8 dataset rows + hidden head, problem 1 = f32 H + output head
+  const bool mlp_pair = nprob == 2 && head.C <= 10 && probs[0].xt == 1 && probs[0].hd_mode == 2 &&
+                        probs[1].xt == 0 && probs[1].hd_mode == 1 && probs[1].x.idx == nullptr &&
+                        probs[0].mode == probs[1].mode;
+  const dim3 grid(blocks), block(256);
+  if (mlp_pair) {
+    const int g0 = probs[0].x.idx != nullptr, m = probs[0].mode & 1;
+    constexpr int S1m0 = wgrad_spec(0, 1, 0, 0), S1m1 = wgrad_spec(0, 1, 0, 1);
+    if (g0 == 0 && m == 0)
+      hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, 0, 0), S1m0>), grid, block, 0, stream, a);
+    else if (g0 == 0 && m == 1)
+      hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, 0, 1), S1m1>), grid, block, 0, stream, a);
+    else if (g0 == 1 && m == 0)
+      hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, 1, 0), S1m0>), grid, block, 0, stream, a);
+    else
+      hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, 1, 1), S1m1>), grid, block, 0, stream, a);
+  } else if (head.C <= 10) {
+    hipLaunchKernelGGL((wgrad_grouped_kernel<10, 0, 0>), grid, block, 0, stream, a);
+  } else {
+    hipLaunchKernelGGL((wgrad_grouped_kernel<16, 0, 0>), grid, block, 0, stream, a);
+  }
   return hipGetLastError();
 }
 

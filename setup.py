@@ -20,6 +20,10 @@ if ARCH != "gfx950":
     raise SystemExit(f"arena_amd targets MI355X only (gfx950); PYTORCH_ROCM_ARCH={ARCH}")
 
 HIP_SOURCES = ["csrc/ops/mlp_kernels.hip", "csrc/ccl/xgmi_ccl.hip"]
+# ARENA_TIMELINE=1: instrumented build for scripts/timeline.py (never the default)
+TIMELINE = ["-DARENA_TIMELINE"] if os.environ.get("ARENA_TIMELINE") == "1" else []
+if TIMELINE:  # experiment switches for instrumented builds only (scripts/perf_exp.sh)
+    TIMELINE += os.environ.get("ARENA_EXP_FLAGS", "").split()
 CPP_SOURCES = ["csrc/ops/bindings.cpp"]
 
 ext_modules = []
@@ -50,7 +54,7 @@ try:
                     continue
                 cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
                        "-ffp-contract=fast", "-I", os.path.join(HERE, "csrc", "ops"), "-c", srcp,
-                       "-o", obj]
+                       "-o", obj] + TIMELINE
                 print(" ".join(cmd), flush=True)
                 subprocess.run(cmd, check=True)
             super().build_extensions()
@@ -65,7 +69,7 @@ try:
             libraries=["amdhip64", "c10_hip", "torch_hip"],
             define_macros=[("ARENA_SRC_HASH", f'"{src_hash}"'), ("__HIP_PLATFORM_AMD__", "1"),
                            ("USE_ROCM", "1")],
-            extra_compile_args=["-O3", "-std=c++17"],
+            extra_compile_args=["-O3", "-std=c++17"] + TIMELINE,
         )
     ]
     cmdclass = {"build_ext": HipBuildExt.with_options(use_ninja=True)}

@@ -36,8 +36,13 @@ def test_graph_replay_equals_eager(cuda, small_data):
     a.train_steps(20)
     b.train_steps(20)
     torch.cuda.synchronize()
-    # logits are accumulated with f32 atomics (order may differ run to run): equal to rounding
-    torch.testing.assert_close(a.P, b.P, rtol=1e-4, atol=1e-6)
+    # logits are accumulated with f32 atomics (order may differ run to run): equal to rounding,
+    # except where Adam amplifies it (a near-zero gradient whose sign flips moves a parameter by
+    # up to lr per step): allow a handful of such elements, bounded by the steps taken
+    diff = (a.P - b.P).abs()
+    off = diff > (1e-6 + 1e-4 * b.P.abs())
+    assert float(off.float().mean()) < 1e-4, int(off.sum())
+    assert float(diff.max()) < 20 * a.cfg.lr
     assert int(a.ctrA.item()) == 20
 
 
