@@ -101,7 +101,7 @@ class FusedMLPTrainer:
         self.G = torch.zeros(n, device=dev) if (self.distributed or external_update) else None
         self._init_params()
         import os as _os
-        self._x_from_dataset = _os.environ.get("ARENA_WGRAD_X", "dataset") == "dataset"
+        self._x_from_dataset = _os.environ.get("ARENA_WGRAD_X", "published") == "dataset"
         self.xgmi = None
         if self.distributed:
             import torch.distributed as dist

@@ -75,7 +75,7 @@ def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Optional[Tensor]], outW: S
                   grad_scale: float = 1.0, tf_style: bool = False,
                   ctr_dst: Optional[Tensor] = None, ctr_src: Optional[Tensor] = None,
                   ctr_add: int = 0) -> None:
-    """dW_i = dz_iᵀ·gather(x_i), db_i = Σ_rows dz_i for up to 4 layers in one launch.
+    """dW_i = dz_iᵀ·gather(x_i), db_i = Σ_rows dz_i for up to 2 layers in one launch.
 
     Head modes (fused MLP step): every workgroup recomputes softmax-xent from ``head_logits2``
     (+ ``head_b2``, ``head_labels``); ``head_modes[i]`` 1 -> dz = dlogits (output layer),

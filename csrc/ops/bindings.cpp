@@ -295,7 +295,7 @@ void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::ve
                    OptT lr_t, double b1, double b2, double eps, double wd, OptT t_step,
                    double grad_scale, bool tf_style, OptT ctr_dst, OptT ctr_src, int64_t ctr_add) {
   const size_t n = xs.size();
-  TORCH_CHECK(n >= 1 && n <= 4, "wgrad_grouped: 1..4 problems");
+  TORCH_CHECK(n >= 1 && n <= 2, "wgrad_grouped: 1..2 problems");
   TORCH_CHECK(x_scales.size() == n && gather.size() == n && dzs.size() == n && outW.size() == n &&
                   outB.size() == n && hd_modes.size() == n && hd_w2.size() == n &&
                   hd_h.size() == n,

@@ -315,7 +315,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
 //                    the two 16-lane groups of each half-wave hit disjoint banks)
 //   D              : lane l, reg r -> dW[n0 + 4(l>>4) + r][k0 + 16w + (l&15)]   (coalesced rows)
 // ---------------------------------------------------------------------------------------------
-constexpr int kMaxProblems = 4;
+constexpr int kMaxProblems = 2;  // kernarg stays small (launch latency)
 struct WGradArgs {
   ArenaWGradProblem p[kMaxProblems];
   int nprob;
