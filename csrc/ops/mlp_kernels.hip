@@ -391,12 +391,13 @@ struct WSpec {
   static constexpr int xt = s & 1, hm = (s >> 1) & 3, gather = (s >> 3) & 1, mode = (s >> 4) & 1;
 };
 
+
 constexpr int wgrad_spec(int xt, int hm, int gather, int mode) {
   return 1 + xt + 2 * hm + 8 * gather + 16 * mode;
 }
 
-template <int CB, int SPEC, int LG>  // CB: bound on head classes (C <= CB); LG: labels gathered
-                                     // (-1: decided at run time from the label source)
+template <int CB, int SPEC, int LG, int LDT>  // CB: bound on head classes (C <= CB); LG: labels
+                                              // gathered, LDT: label dtype (-1: run time)
 // (LDS images come in as plain pointers: __restrict__ here would let hipcc move LDS accesses
 // across the raw s_barrier in lds_barrier(), whose memory clobber noalias memory escapes)
 __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float* Xs, float* Zs,
@@ -433,16 +434,40 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
   ARENA_TL(1, 0);
   // step counter and Adam scalars: loads issued now, first used after the chunk's other loads
   // are in flight (in-order vmcnt: waiting on these oldest loads leaves the younger ones going)
-  const long long hstep_raw = hmode ? *HD.step : 0;
-  const long long adam_t = (mode == 1 && args.adam.t_ptr) ? *args.adam.t_ptr : 1;
-  const float adam_lr = (mode == 1 && args.adam.lr_ptr) ? *args.adam.lr_ptr : args.adam.lr;
+  // Loaded now, first used after every other load of the chunk is issued. Two hipcc habits are
+  // defeated here: (1) a load under a branch is drained at the branch, so the spec path loads
+  // unconditionally (the host guarantees the pointers); (2) a uniform loaded value is moved into an
+  // SGPR (v_readfirstlane) right after its load, draining vmcnt at once, so the values are made
+  // lane-varying by adding a lane-dependent zero the compiler cannot see through.
+  int lz;  // an opaque zero in a VGPR (hipcc cannot fold it or prove the sums below uniform)
+  asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+  long long hstep_raw = 0, adam_t = 1;
+  float adam_lr = args.adam.lr;
+  if constexpr (WS::known) {
+    // 32-bit loads of the counters' low words (< 2^31 steps): a 64-bit destination whose dead
+    // high half is reused would force an early wait (register write-after-read on the load)
+    if (WS::hm) hstep_raw = *reinterpret_cast<const int*>(HD.step) + lz;
+    if (WS::mode == 1) {
+      adam_t = *reinterpret_cast<const int*>(args.adam.t_ptr) + lz;
+      adam_lr = *args.adam.lr_ptr + __int_as_float(lz);
+    }
+  } else {
+    if (hmode) hstep_raw = *HD.step;
+    if (mode == 1) {
+      adam_t = args.adam.t_ptr ? *args.adam.t_ptr : 1;
+      adam_lr = args.adam.lr_ptr ? *args.adam.lr_ptr : args.adam.lr;
+    }
+  }
   const float* logits = nullptr;
   long long hstep = 0;
 
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   f32x4 accb = {0.f, 0.f, 0.f, 0.f};
   float pw[4], mw[4], vw[4], pb[4], mb[4], vb[4];
-  for (int mc0 = 0; mc0 < P.M; mc0 += kMC) {
+  // spec path: the host guarantees M <= kMC, so the chunk loop (and every mc0 == 0 test) folds away
+  const int nchunks = WS::known ? 1 : (P.M + kMC - 1) / kMC;
+  for (int ci = 0; ci < nchunks; ++ci) {
+    const int mc0 = ci * kMC;
     const int mcn = min(kMC, P.M - mc0);
     // (1) issue the chunk's loads
     float4 xv[kXItems];
@@ -454,6 +479,7 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
     } else {
       load_x_items<0>(P, gt, mc0, mcn, k0, xv);
     }
+    ARENA_TL(1, 8);
     float4 zv[kZItems];
     float dv[kDItems];
     float wv = 0.f, bv = 0.f;
@@ -477,9 +503,16 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
       if ((int)threadIdx.x < kMC) {
         // labels share the layer input's gather (same rows); no gather -> direct
         const Gather lg = (LG == 0) ? Gather{nullptr, 0, P.M} : make_gather(HD.lab);
-        yv = load_label(HD.lab, gather_row(lg, mc0 + min((int)threadIdx.x, mcn - 1)));
+        const long long pr = gather_row(lg, mc0 + min((int)threadIdx.x, mcn - 1));
+        if constexpr (LDT == 1) yv = static_cast<const uint8_t*>(HD.lab.ptr)[pr];
+        else if constexpr (LDT == 2) yv = static_cast<const int*>(HD.lab.ptr)[pr];
+        else yv = load_label(HD.lab, pr);
       }
-      bv = HD.b2 ? HD.b2[min((int)threadIdx.x & 15, C - 1)] : 0.f;
+      {
+        const float* b2p = HD.b2 ? HD.b2 : P.hd_w2 ? P.hd_w2 : HD.logits2;  // any valid address
+        const float b2v = b2p[min((int)threadIdx.x & 15, C - 1)];
+        bv = HD.b2 ? b2v : 0.f;
+      }
       if (hmode == 2) {
 #pragma unroll
         for (int i = 0; i < kZItems; ++i) {  // mask source (post-dropout activation)
@@ -492,7 +525,9 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
         wv = P.hd_w2[(long long)min((int)threadIdx.x >> 4, C - 1) * P.N +
                      min(n0 + ((int)threadIdx.x & 15), P.N - 1)];
       }
+      ARENA_TL(1, 9);
       if (mc0 == 0) {  // first use of the step counter: every other load of the chunk is issued
+        if (ARENA_EXP & 16) hstep_raw = 7;
         hstep = hstep_raw + HD.step_off;
         logits = HD.logits2 + (long long)(hstep & 1) * P.M * HD.C;
         ARENA_TL_DEP((int)hstep);
@@ -504,6 +539,7 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
         if (ARENA_EXP & 1) dv[i] = 0.01f * (float)(t & 15);
         else dv[i] = logits[(long long)(mc0 + min(t >> 4, mcn - 1)) * C + min(t & 15, C - 1)];
       }
+      ARENA_TL(1, 10);
       if (mc0 == 0 && (int)blockIdx.x == args.head_block) {  // zero the other buffer + next slot
         float* nxt = HD.logits2 + (long long)((hstep + 1) & 1) * P.M * HD.C;
         for (int i = threadIdx.x; i < P.M * HD.C; i += 256) nxt[i] = 0.f;
@@ -522,11 +558,14 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
         const long long off = (long long)min(n0 + 4 * g + r, P.N - 1) * P.K + kkc;
         pw[r] = P.pW[off]; mw[r] = P.mW[off]; vw[r] = P.vW[off];
       }
-      if (bias_wave && has_bias) {
+      {  // every wave loads (a branch around loads drains vmcnt); only the bias wave uses them
+        const float* pbp = has_bias ? P.pB : P.pW;
+        const float* mbp = has_bias ? P.mB : P.mW;
+        const float* vbp = has_bias ? P.vB : P.vW;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int n = min(n0 + 4 * g + r, P.N - 1);
-          pb[r] = P.pB[n]; mb[r] = P.mB[n]; vb[r] = P.vB[n];
+          pb[r] = pbp[n]; mb[r] = mbp[n]; vb[r] = vbp[n];
         }
       }
     }
@@ -657,7 +696,7 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
         if (bias_wave) accb = mfma_16x16x4(a, 1.f, accb);
       }
     }
-    if (mc0 + kMC < P.M) lds_barrier();  // before the next chunk overwrites the images
+    if (ci + 1 < nchunks) lds_barrier();  // before the next chunk overwrites the images
   }
   ARENA_TL_DEP(acc[0]);
   ARENA_TL(1, 5);
@@ -719,11 +758,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
     if (i < args.nprob && (int)blockIdx.x >= args.p[i].block_begin) pi = i;
   if constexpr (S0 != 0 && S1 != 0) {
     // the head's labels follow problem 0's gather (the binding shares it with the label source)
+    // (published batch: int32 labels; dataset gather: the dataset's uint8 labels)
     constexpr int LG = WSpec<S0>::gather;
-    if (pi == 0) wgrad_body<CB, S0, LG>(args, 0, Xs, Zs, Ds, W2s, Ys, B2s);
-    else wgrad_body<CB, S1, LG>(args, 1, Xs, Zs, Ds, W2s, Ys, B2s);
+    constexpr int LDT = LG ? 1 : 2;
+    if (pi == 0) wgrad_body<CB, S0, LG, LDT>(args, 0, Xs, Zs, Ds, W2s, Ys, B2s);
+    else wgrad_body<CB, S1, LG, LDT>(args, 1, Xs, Zs, Ds, W2s, Ys, B2s);
   } else {
-    wgrad_body<CB, 0, -1>(args, pi, Xs, Zs, Ds, W2s, Ys, B2s);
+    wgrad_body<CB, 0, -1, -1>(args, pi, Xs, Zs, Ds, W2s, Ys, B2s);
   }
   counter_op(args.ctr);  // A = B last: nothing in this kernel reads A
 }
@@ -1062,12 +1103,15 @@ hipError_t arena_wgrad_grouped(ArenaWGradProblem* probs, int nprob, ArenaAdam ad
   a.ctr = ctr;
   a.head = head;
   // the fused MLP step: problem 0 = u8 dataset rows + hidden head, problem 1 = f32 H + output head
+  const bool g0 = probs[0].x.idx != nullptr;
   const bool mlp_pair = nprob == 2 && head.C <= 10 && probs[0].xt == 1 && probs[0].hd_mode == 2 &&
                         probs[1].xt == 0 && probs[1].hd_mode == 1 && probs[1].x.idx == nullptr &&
-                        probs[0].mode == probs[1].mode;
+                        probs[0].mode == probs[1].mode && probs[0].M <= kMC &&
+                        (probs[0].mode == 0 || (adam.t_ptr && adam.lr_ptr)) && head.step &&
+                        probs[1].M <= kMC && head.lab.dtype == (g0 ? 1 : 2);
   const dim3 grid(blocks), block(256);
   if (mlp_pair) {
-    const int g0 = probs[0].x.idx != nullptr, m = probs[0].mode & 1;
+    const int m = probs[0].mode & 1;
     constexpr int S1m0 = wgrad_spec(0, 1, 0, 0), S1m1 = wgrad_spec(0, 1, 0, 1);
     if (g0 == 0 && m == 0)
       hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, 0, 0), S1m0>), grid, block, 0, stream, a);

@@ -27,6 +27,9 @@ PHASES = {
 }
 
 
+EXTRA = {1: {8: "x_issued", 9: "head_loads_issued", 10: "logits_issued"}}
+
+
 def analyse(tl, kid, nblocks):
     t = tl[kid, :nblocks].double() * 10.0 / 1000.0  # ticks (10 ns) -> us
     nph = len(PHASES[kid])
@@ -37,6 +40,11 @@ def analyse(tl, kid, nblocks):
     rel = t - t0
     out = {"blocks": int(valid.sum()), "entry_skew_us": round(float(rel[:, 0].max()), 3),
            "span_us": round(float(rel[:, nph - 1].max()), 3), "phases": {}}
+    extra = tl[kid, :nblocks].double()[valid] * 10.0 / 1000.0 - t0
+    for j, name in EXTRA.get(kid, {}).items():   # auxiliary stamps: median time since start
+        col = extra[:, j]
+        if bool((col > -t0 / 2).all()):
+            out[f"at_{name}_us"] = round(float(col.median()), 3)
     for i in range(1, nph):
         d = rel[:, i] - rel[:, i - 1]
         out["phases"][PHASES[kid][i]] = {"med_delta_us": round(float(d.median()), 3),
