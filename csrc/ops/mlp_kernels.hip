@@ -778,7 +778,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
 // m-tile-0 workgroups also snapshot W2 for the backward pass (which updates W2 in place). The
 // softmax itself is recomputed by every wgrad workgroup: no intra-kernel hand-off anywhere.
 // ---------------------------------------------------------------------------------------------
-template <int XT, int WAVES>
+template <int XT, int WAVES, bool FAST>
 __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
     ArenaRowSource src, const float* __restrict__ W, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int K, uint32_t keep_thr, float inv_keep, uint32_t seed,
@@ -791,35 +791,105 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
   const int n0 = blockIdx.x * 16, m0 = blockIdx.y * 16;
   ARENA_TL(0, 0);
   const int rowc = min(m0 + c, M - 1), colc = min(n0 + c, N - 1);
-  const Gather gt = make_gather(src);
-  const long long stepv = step_src ? *step_src : 0;
-  const uint32_t step = (uint32_t)stepv;
-  const long long prow = gather_row(gt, rowc);
-  ARENA_TL_DEP((int)prow);
-  ARENA_TL(0, 1);
   const float* wrow = W + (long long)colc * K;
+  const int nsteps = (K + 15) >> 4;
+  const int s0 = (nsteps * w) / WAVES, s1 = (nsteps * (w + 1)) / WAVES;
   // n-tile-0 workgroups publish the step's gathered batch (u8 rows + labels) so the backward
   // kernel reads them directly instead of repeating the cursor -> index -> row chain
   const bool publish = (xb != nullptr) && blockIdx.x == 0;
+  __shared__ float w2s[16][17];
+  __shared__ float hs[16][17];
+  __shared__ float red[WAVES][16][17];
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  long long stepv;
+  long long prow;
+  float w2v, bv;
+  if constexpr (FAST) {
+    // The fused training step (host-checked: cursor == step counter == counter-op source, one
+    // K chunk per wave, gather on, publishing on). One straight load stream: the step counter
+    // (oldest), then everything independent of it (this wave's W rows, the W2 slice, bias), then
+    // the cursor -> index -> row chain, whose waits leave the W loads in flight. The counter is
+    // kept lane-varying (opaque zero) so hipcc does not drain it into an SGPR at once, and the
+    // label publication and the counter update move to the end.
+    int lz;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+    const int A = *reinterpret_cast<const int*>(step_src) + lz;
+    __builtin_amdgcn_sched_barrier(0);
+    float b[CH][4];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int kc = min((s0 + i) * 16 + 4 * g, K - 4);
+      const float4 wv = *reinterpret_cast<const float4*>(wrow + kc);
+      b[i][0] = wv.x; b[i][1] = wv.y; b[i][2] = wv.z; b[i][3] = wv.w;
+    }
+    w2v = W2[(long long)min((int)(threadIdx.x >> 4) & 15, C - 1) * N +
+             min(n0 + ((int)threadIdx.x & 15), N - 1)];
+    bv = bias[min(n0 + ((int)threadIdx.x & 15), N - 1)];
+    __builtin_amdgcn_sched_barrier(0);  // keep the independent loads above the counter's first use
+    long long p = mod_fp64((double)A * (double)src.batch, src.idx_len) + rowc;
+    p = (p >= src.idx_len) ? p - src.idx_len : p;
+    prow = src.idx[p];
+    stepv = A;
+    ARENA_TL_DEP((int)prow);
+    ARENA_TL(0, 1);
+    float a[CH][4];
+    uint32_t raw[CH];
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const int kc = min((s0 + i) * 16 + 4 * g, K - 4);
+      if constexpr (XT == 1) {
+        raw[i] = *reinterpret_cast<const uint32_t*>(static_cast<const uint8_t*>(src.ptr) +
+                                                    prow * (long long)src.ld + kc);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) a[i][j] = (float)((raw[i] >> (8 * j)) & 0xffu) * src.scale;
+      } else {
+        load4<XT>(src, prow, kc, a[i]);
+        raw[i] = 0;
+      }
+    }
+    if constexpr (XT == 1) {
+      if (publish && m0 + c < M) {
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+          const int k = (s0 + i) * 16 + 4 * g;
+          if (s0 + i < s1 && k < K)  // stores only: the branch holds no load
+            *reinterpret_cast<uint32_t*>(xb + (long long)(m0 + c) * K + k) = raw[i];
+        }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      const bool kv = ((s0 + i) * 16 + 4 * g) < K;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) a[i][j] = kv ? a[i][j] : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < CH; ++i) {
+      if (s0 + i < s1) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc = mfma_16x16x4(a[i][j], b[i][j], acc);
+      }
+    }
+  } else {
+  const Gather gt = make_gather(src);
+  stepv = step_src ? *step_src : 0;
+  prow = gather_row(gt, rowc);
+  ARENA_TL_DEP((int)prow);
+  ARENA_TL(0, 1);
   if (publish && w == 0 && g == 0 && m0 + c < M) {
     const int y = (lab_dtype == 1) ? (int)static_cast<const uint8_t*>(lab_ptr)[prow]
                 : (lab_dtype == 2) ? static_cast<const int*>(lab_ptr)[prow]
                                    : (int)static_cast<const long long*>(lab_ptr)[prow];
     yb[m0 + c] = y;
   }
-  __shared__ float w2s[16][17];
-  __shared__ float hs[16][17];
-  __shared__ float red[WAVES][16][17];
-  float w2v = 0.f, bv = 0.f;
+  w2v = 0.f;
+  bv = 0.f;
   if (threadIdx.x < 256) {
     w2v = W2[(long long)min((int)threadIdx.x >> 4, C - 1) * N + min(n0 + ((int)threadIdx.x & 15), N - 1)];
     bv = bias[min(n0 + ((int)threadIdx.x & 15), N - 1)];
   }
   counter_op(ctr);
 
-  const int nsteps = (K + 15) >> 4;
-  const int s0 = (nsteps * w) / WAVES, s1 = (nsteps * (w + 1)) / WAVES;
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
   for (int sb = s0; sb < s1; sb += CH) {
     float a[CH][4], b[CH][4];
     uint32_t raw[CH];
@@ -862,6 +932,8 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
       }
     }
   }
+  }
+  const uint32_t step = (uint32_t)stepv;
   ARENA_TL_DEP(acc[0]);
   ARENA_TL(0, 2);
 #pragma unroll
@@ -900,6 +972,15 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
     } else {
       if (m0 + rr < M) atomicAdd(&lg[(long long)(m0 + rr) * C + cl], p);
     }
+  }
+  if constexpr (FAST) {
+    if (publish && w == 0 && g == 0 && m0 + c < M) {
+      const int y = (lab_dtype == 1) ? (int)static_cast<const uint8_t*>(lab_ptr)[prow]
+                  : (lab_dtype == 2) ? static_cast<const int*>(lab_ptr)[prow]
+                                     : (int)static_cast<const long long*>(lab_ptr)[prow];
+      yb[m0 + c] = y;
+    }
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) *ctr.dst = stepv + ctr.add;
   }
   ARENA_TL(0, 5);
   ARENA_TL_DRAIN();
@@ -1040,14 +1121,24 @@ hipError_t arena_mlp_fwd_logits(ArenaRowSource src, const float* W, const float*
     inv_keep = 1.f / keep_prob;
   }
   dim3 grid((N + 15) / 16, (M + 15) / 16);
-  if (src.dtype == 1)
-    hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8>), grid, dim3(512), 0, stream, src, W, bias, Y,
-                       M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2, xb,
-                       lab_ptr, lab_dtype, yb, ctr);
+  // the training step's configuration gets the straight-line variant (see the kernel)
+  const int nsteps = (K + 15) / 16;
+  const bool fast = src.dtype == 1 && src.idx != nullptr && src.cursor != nullptr &&
+                    src.cursor == step_src && src.cursor_off == 0 && ctr.dst != nullptr &&
+                    ctr.src == step_src && xb != nullptr && lab_ptr != nullptr &&
+                    (nsteps + 7) / 8 <= 8 && src.idx_len < (1LL << 31);
+  if (fast)
+    hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8, true>), grid, dim3(512), 0, stream, src, W,
+                       bias, Y, M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2,
+                       xb, lab_ptr, lab_dtype, yb, ctr);
+  else if (src.dtype == 1)
+    hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8, false>), grid, dim3(512), 0, stream, src, W,
+                       bias, Y, M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2,
+                       xb, lab_ptr, lab_dtype, yb, ctr);
   else
-    hipLaunchKernelGGL((mlp_fwd_logits_kernel<0, 8>), grid, dim3(512), 0, stream, src, W, bias, Y,
-                       M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2, nullptr,
-                       lab_ptr, lab_dtype, yb, ctr);
+    hipLaunchKernelGGL((mlp_fwd_logits_kernel<0, 8, false>), grid, dim3(512), 0, stream, src, W,
+                       bias, Y, M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2,
+                       nullptr, lab_ptr, lab_dtype, yb, ctr);
   return hipGetLastError();
 }
 
