@@ -676,16 +676,39 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
     }
     lds_barrier();
     ARENA_TL(1, 4);
-    // (4) K-loop over all kMC rows of the image (rows >= mcn: Zs zero, Xs finite)
+    // (4) K-loop over all kMC rows of the image (rows >= mcn: Zs zero, Xs finite). Four
+    //     independent accumulator chains (the f32 MFMA's dependent latency is 40 cycles, its
+    //     issue 8): a quarter of the serial depth. Bias columns (db = dZᵀ·1) run in the same
+    //     loop in the k-tile-0 blocks only (a block-uniform branch outside the loop).
     if (mcn > kMC / 2) {
-#pragma unroll 8
-      for (int s = 0; s < kMC / 4; ++s) {
-        const int m = 4 * s + g;
-        const float a = Zs[m * 16 + c];
-        const float b = Xs[m * kXsStride + 16 * w + c];
-        acc = mfma_16x16x4(a, b, acc);
-        if (bias_wave) accb = mfma_16x16x4(a, 1.f, accb);
+      f32x4 ch[4] = {acc, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+      if (tk == 0) {
+        f32x4 chb[4] = {accb, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+        for (int s = 0; s < kMC / 4; s += 4) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int m = 4 * (s + j) + g;
+            const float a = Zs[m * 16 + c];
+            const float b = Xs[m * kXsStride + 16 * w + c];
+            ch[j] = mfma_16x16x4(a, b, ch[j]);
+            chb[j] = mfma_16x16x4(a, 1.f, chb[j]);
+          }
+        }
+        accb = (chb[0] + chb[1]) + (chb[2] + chb[3]);
+      } else {
+#pragma unroll
+        for (int s = 0; s < kMC / 4; s += 4) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int m = 4 * (s + j) + g;
+            const float a = Zs[m * 16 + c];
+            const float b = Xs[m * kXsStride + 16 * w + c];
+            ch[j] = mfma_16x16x4(a, b, ch[j]);
+          }
+        }
       }
+      acc = (ch[0] + ch[1]) + (ch[2] + ch[3]);
     } else {
       const int nst = (mcn + 3) >> 2;
       for (int s = 0; s < nst; ++s) {
@@ -858,18 +881,19 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
       }
     }
 #pragma unroll
-    for (int i = 0; i < CH; ++i) {
-      const bool kv = ((s0 + i) * 16 + 4 * g) < K;
+    for (int i = 0; i < CH; ++i) {  // steps past this wave's range contribute zero (no branch)
+      const bool kv = ((s0 + i) * 16 + 4 * g) < K && (s0 + i) < s1;
 #pragma unroll
       for (int j = 0; j < 4; ++j) a[i][j] = kv ? a[i][j] : 0.f;
     }
+    // four independent accumulator chains (40-cycle dependent MFMA latency, 8-cycle issue)
+    f32x4 ch[4] = {acc, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
     for (int i = 0; i < CH; ++i) {
-      if (s0 + i < s1) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc = mfma_16x16x4(a[i][j], b[i][j], acc);
-      }
+      for (int j = 0; j < 4; ++j) ch[j] = mfma_16x16x4(a[i][j], b[i][j], ch[j]);
     }
+    acc = (ch[0] + ch[1]) + (ch[2] + ch[3]);
   } else {
   const Gather gt = make_gather(src);
   stepv = step_src ? *step_src : 0;
