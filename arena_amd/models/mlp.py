@@ -102,6 +102,9 @@ class FusedMLPTrainer:
         self._init_params()
         import os as _os
         self._x_from_dataset = _os.environ.get("ARENA_WGRAD_X", "published") == "dataset"
+        # forward row gather: "counter" (cursor -> permutation in the forward) or "rows" (the
+        # backward precomputes the next step's rows); measured equal-or-slower, so off by default
+        self._rows_ahead = _os.environ.get("ARENA_FWD_ROWS", "counter") == "rows"
         self.xgmi = None
         if self.distributed:
             import torch.distributed as dist
@@ -143,8 +146,11 @@ class FusedMLPTrainer:
         self.shard = self.shard.to(dev)
         self._gen = torch.Generator(device=dev).manual_seed(cfg.seed * 7919 + rank)
         self.perm = torch.empty(self.shard.numel(), dtype=torch.int32, device=dev)
-        self._reshuffle()
+        # this step's dataset rows: written one step ahead by the backward kernel, so the forward
+        # reads them directly (host refreshes them when the permutation changes)
+        self.rows = torch.empty(B, dtype=torch.int32, device=dev)
         self.steps_done = 0
+        self._reshuffle()
         self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_mode = None
 
@@ -194,6 +200,18 @@ class FusedMLPTrainer:
         this rank's shard, which was range-checked against the dataset at construction."""
         rp = torch.randperm(self.shard.numel(), generator=self._gen, device=self.device)
         self.perm.copy_(self.shard[rp].to(torch.int32))
+        self._sync_rows()
+
+    def set_permutation(self, perm: torch.Tensor) -> None:
+        """Replace this epoch's sample order (e.g. to replay another trainer's order)."""
+        self.perm.copy_(perm.to(self.perm.device, torch.int32))
+        self._sync_rows()
+
+    def _sync_rows(self):
+        """rows = perm[(step * B + r) % len] for the next step (host-known step count)."""
+        B, L = self.cfg.batch, self.perm.numel()
+        pos = (self.steps_done * B + torch.arange(B, device=self.device)) % L
+        self.rows.copy_(self.perm[pos])
 
     def pick_steps_per_graph(self, cap: int = 64) -> int:
         """Largest divisor of the epoch length <= cap, so graphs never straddle a reshuffle."""
@@ -226,7 +244,7 @@ class FusedMLPTrainer:
                            x_scale=1.0 / 255.0, idx=self.perm, cursor=A,
                            batch=B, keep_prob=cfg.keep_prob,
                            seed=cfg.seed * 2654435761 + self.rank, step=A, ctr_dst=Bc,
-                           ctr_src=A, ctr_add=1)
+                           ctr_src=A, ctr_add=1, rows=self.rows if self._rows_ahead else None)
 
     def _launch_wgrad(self, adam: bool, commit: bool = False):
         """Softmax-xent recomputed per workgroup from the logits; dW1 (dz via the W2 snapshot and
@@ -239,7 +257,9 @@ class FusedMLPTrainer:
                       head_keep_prob=cfg.keep_prob, head_logits2=self.logits2, head_step=Bc,
                       head_step_off=-1, head_b2=self.b2, head_labels=self.yb,
                       head_loss_scale=1.0 / B, head_loss_acc=self.loss_hist,
-                      head_correct_acc=self.corr_hist)
+                      head_correct_acc=self.corr_hist,
+                      next_rows=self.rows if self._rows_ahead else None,
+                      next_rows_perm=self.perm if self._rows_ahead else None)
         xs, dzs = [self.xb, self.Hbuf], [None, None]
         if self._x_from_dataset:
             # gather the batch rows from the (never written) dataset instead of the forward's
@@ -275,7 +295,8 @@ class FusedMLPTrainer:
         self.steps_per_graph = steps_per_graph
         # warm up on a side stream (allocator / collective communicators initialised outside
         # capture), then restore the state so warm-up steps do not count as training.
-        snap = [t.clone() for t in (self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2)]
+        snap = [t.clone() for t in (self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2,
+                                    self.rows)]
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -283,7 +304,8 @@ class FusedMLPTrainer:
                 self._launch_step()
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        for t, v in zip((self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2), snap):
+        for t, v in zip((self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2, self.rows),
+                        snap):
             t.copy_(v)
         try:
             self._graphs[steps_per_graph] = self._capture(steps_per_graph)
@@ -420,3 +442,4 @@ class FusedMLPTrainer:
         self.ctrA.fill_(int(sd["step"]))
         self.ctrB.fill_(int(sd["step"]))
         self.steps_done = int(sd["step"])
+        self._sync_rows()

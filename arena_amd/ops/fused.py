@@ -47,16 +47,18 @@ def mlp_fwd_logits(x: Tensor, W1: Tensor, b1: Tensor, H: Tensor, W2: Tensor, log
                    idx: Optional[Tensor] = None, cursor: Optional[Tensor] = None, batch: int = 0,
                    keep_prob: float = 1.0, seed: int = 0, step: Optional[Tensor] = None,
                    ctr_dst: Optional[Tensor] = None, ctr_src: Optional[Tensor] = None,
-                   ctr_add: int = 0) -> None:
+                   ctr_add: int = 0, rows: Optional[Tensor] = None) -> None:
     """H = dropout(relu(x·W1ᵀ+b1)) and logits2[step & 1] += H·W2ᵀ in ONE launch.
 
     ``logits2`` is [2, M, C]; the consuming wgrad (head mode) zeroes the other buffer each step.
     With ``xb``/``labels``/``yb`` the gathered u8 batch rows and their labels are published for the
     backward kernel (so it skips the cursor -> permutation -> row dependency chain).
+    ``rows`` (optional): this step's dataset rows, as the previous ``wgrad_grouped`` wrote them
+    with ``next_rows`` -- must equal ``idx[(cursor * batch + r) % len]``.
     """
     _impl(H).mlp_fwd_logits(x, float(x_scale), idx, cursor, int(batch), W1, b1, H,
                             float(keep_prob), int(seed), step, W2, W2_copy, logits2, xb, labels, yb,
-                            ctr_dst, ctr_src, int(ctr_add))
+                            ctr_dst, ctr_src, int(ctr_add), rows)
 
 
 def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Optional[Tensor]], outW: Sequence[Tensor],
@@ -74,7 +76,8 @@ def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Optional[Tensor]], outW: S
                   weight_decay: float = 0.0, t_step: Optional[Tensor] = None,
                   grad_scale: float = 1.0, tf_style: bool = False,
                   ctr_dst: Optional[Tensor] = None, ctr_src: Optional[Tensor] = None,
-                  ctr_add: int = 0) -> None:
+                  ctr_add: int = 0, next_rows: Optional[Tensor] = None,
+                  next_rows_perm: Optional[Tensor] = None) -> None:
     """dW_i = dz_iᵀ·gather(x_i), db_i = Σ_rows dz_i for up to 2 layers in one launch.
 
     Head modes (fused MLP step): every workgroup recomputes softmax-xent from ``head_logits2``
@@ -94,7 +97,7 @@ def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Optional[Tensor]], outW: S
         list(outW), list(outB), list(mW or none), list(vW or none), list(mB or none),
         list(vB or none), float(lr), lr_t, float(betas[0]), float(betas[1]), float(eps),
         float(weight_decay), t_step, float(grad_scale), bool(tf_style), ctr_dst, ctr_src,
-        int(ctr_add))
+        int(ctr_add), next_rows, next_rows_perm)
 
 
 def adam_flat(P: Tensor, M: Tensor, V: Tensor, G: Tensor, *, lr: float = 1e-3,

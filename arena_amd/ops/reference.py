@@ -137,8 +137,14 @@ def head_dz(dl, w2, h, keep_prob):
 
 
 def mlp_fwd_logits(x, x_scale, idx, cursor, batch, W1, b1, H, keep_prob, seed, step, W2, W2_copy,
-                   logits2, xb, labels, yb, ctr_dst, ctr_src, ctr_add):
-    """Reference for the logits-emitting forward: H and logits2[step & 1] += H·W2ᵀ."""
+                   logits2, xb, labels, yb, ctr_dst, ctr_src, ctr_add, rows=None):
+    """Reference for the logits-emitting forward: H and logits2[step & 1] += H·W2ᵀ.
+    ``rows`` (the kernel's precomputed gather) must equal the idx/cursor gather; checked here."""
+    if rows is not None:
+        want = gather_rows(torch.arange(x.shape[0], dtype=torch.int32), idx, cursor, batch,
+                           H.shape[0])
+        if not torch.equal(rows.to(torch.int32).cpu(), want.cpu()):
+            raise AssertionError("precomputed rows disagree with the cursor/permutation gather")
     if ctr_dst is not None:
         src = int(ctr_src.reshape(-1)[0].item()) if ctr_src is not None else 0
         ctr_new = src + ctr_add
@@ -179,10 +185,16 @@ def _head_dlogits(logits2, hd_step, hd_step_off, b2, labels, idx, cursor, cursor
 def wgrad_grouped(xs, x_scales, gather, idx, cursor, cursor_off, batch, dzs, hd_modes, hd_w2, hd_h,
                   hd_keep_prob, hd_logits2, hd_step, hd_step_off, hd_b2, hd_labels, hd_loss_scale,
                   hd_loss_acc, hd_correct_acc, mode, outW, outB, mW, vW, mB, vB, lr, lr_t, b1, b2,
-                  eps, wd, t_step, grad_scale, tf_style, ctr_dst, ctr_src, ctr_add):
+                  eps, wd, t_step, grad_scale, tf_style, ctr_dst, ctr_src, ctr_add,
+                  next_rows=None, next_rows_perm=None):
     t = int(t_step.reshape(-1)[0].item()) if t_step is not None else 1
     lr_v = float(lr_t.reshape(-1)[0].item()) if lr_t is not None else lr
     dl = None
+    if next_rows is not None:  # the next step's dataset rows (cursor = this step + 1)
+        st = int(hd_step.reshape(-1)[0].item()) + hd_step_off + 1
+        n, L = next_rows.numel(), next_rows_perm.numel()
+        pos = (st * n + torch.arange(n)) % L
+        next_rows.copy_(next_rows_perm.reshape(-1).cpu()[pos].to(next_rows.device))
     if any(m != 0 for m in hd_modes):
         dl = _head_dlogits(hd_logits2, hd_step, hd_step_off, hd_b2, hd_labels, idx, cursor,
                            cursor_off, batch, any(gather), hd_loss_scale, hd_loss_acc,

@@ -71,6 +71,9 @@ struct ArenaHead {
   ArenaRowSource lab;       // labels (same gather as the layer input)
   float loss_scale;         // 1/batch (mean loss)
   float* loss_acc; int* correct_acc; int hist_len;  // metric ring (block 0), power of two
+  // optional: the NEXT step's dataset rows, nr_out[r] = nr_perm[((step + 1) * nr_batch + r) %
+  // nr_len], written by the head block so the next forward skips the cursor -> permutation hop
+  const int* nr_perm; long long nr_len; int nr_batch; int* nr_out;
 };
 
 

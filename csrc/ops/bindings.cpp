@@ -17,7 +17,7 @@ hipError_t arena_linear_fwd(ArenaRowSource, const float*, const float*, float*, 
 hipError_t arena_mlp_fwd_logits(ArenaRowSource, const float*, const float*, float*, int, int, int,
                                 float, uint32_t, const long long*, const float*, float*, int,
                                 float*, uint8_t*, const void*, int, int*, ArenaCounterOp,
-                                hipStream_t);
+                                const int*, hipStream_t);
 hipError_t arena_xent_head(const float*, int, int, const float*, const float*, int, ArenaRowSource,
                            float*, float*, float, int, float, float*, int*, int, const long long*,
                            ArenaCounterOp, hipStream_t);
@@ -156,7 +156,7 @@ void linear_fwd(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch, 
 void mlp_fwd_logits(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t batch, Tensor W1,
                     Tensor b1, Tensor H, double keep_prob, int64_t seed, OptT step, Tensor W2,
                     OptT W2_copy, Tensor logits2, OptT xb, OptT labels, OptT yb, OptT ctr_dst,
-                    OptT ctr_src, int64_t ctr_add) {
+                    OptT ctr_src, int64_t ctr_add, OptT rows) {
   for (auto* t : {&W1, &b1, &H, &W2, &logits2}) check_f32(*t, "mlp_fwd_logits operand");
   const int64_t M = H.size(0), N = H.size(1), K = W1.size(1), C = W2.size(0);
   TORCH_CHECK(W1.dim() == 2 && W1.size(0) == N && x.dim() == 2 && x.size(1) == K,
@@ -202,11 +202,19 @@ void mlp_fwd_logits(Tensor x, double x_scale, OptT idx, OptT cursor, int64_t bat
     lab_dtype = dtype_code(*labels);
   }
   ArenaRowSource s = make_src(x, x_scale, idx, cursor, batch, M, "x");
+  const int* prows = nullptr;
+  if (rows.has_value()) {  // this step's dataset rows (each must index x)
+    check_dev(*rows, "rows");
+    TORCH_CHECK(rows->scalar_type() == torch::kInt32 && rows->numel() == M,
+                "rows must be int32 [M]");
+    TORCH_CHECK(idx.has_value(), "rows replaces the idx/cursor gather: pass idx too");
+    prows = rows->data_ptr<int>();
+  }
   check_hip(arena_mlp_fwd_logits(s, W1.data_ptr<float>(), b1.data_ptr<float>(),
                                  H.data_ptr<float>(), (int)M, (int)N, (int)K, (float)keep_prob,
                                  (uint32_t)seed, opt_i64_scalar(step, "step"), W2.data_ptr<float>(),
                                  w2c, (int)C, logits2.data_ptr<float>(), pxb, plab, lab_dtype, pyb,
-                                 ctr, cur_stream()),
+                                 ctr, prows, cur_stream()),
             "mlp_fwd_logits");
 }
 
@@ -293,7 +301,8 @@ void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::ve
                    std::vector<Tensor> outW, std::vector<OptT> outB, std::vector<OptT> mW,
                    std::vector<OptT> vW, std::vector<OptT> mB, std::vector<OptT> vB, double lr,
                    OptT lr_t, double b1, double b2, double eps, double wd, OptT t_step,
-                   double grad_scale, bool tf_style, OptT ctr_dst, OptT ctr_src, int64_t ctr_add) {
+                   double grad_scale, bool tf_style, OptT ctr_dst, OptT ctr_src, int64_t ctr_add,
+                   OptT next_rows, OptT next_rows_perm) {
   const size_t n = xs.size();
   TORCH_CHECK(n >= 1 && n <= 2, "wgrad_grouped: 1..2 problems");
   TORCH_CHECK(x_scales.size() == n && gather.size() == n && dzs.size() == n && outW.size() == n &&
@@ -424,6 +433,20 @@ void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::ve
     head.loss_acc = hd_loss_acc->data_ptr<float>();
     head.correct_acc = hd_correct_acc->data_ptr<int>();
     head.hist_len = (int)hd_loss_acc->numel();
+    if (next_rows.has_value()) {
+      TORCH_CHECK(next_rows_perm.has_value(), "next_rows needs next_rows_perm");
+      check_dev(*next_rows, "next_rows");
+      check_dev(*next_rows_perm, "next_rows_perm");
+      TORCH_CHECK(next_rows->scalar_type() == torch::kInt32 &&
+                      next_rows_perm->scalar_type() == torch::kInt32,
+                  "next_rows / next_rows_perm must be int32");
+      TORCH_CHECK(next_rows->numel() <= 256 && next_rows->numel() <= next_rows_perm->numel(),
+                  "next_rows: at most 256 rows, not more than the permutation");
+      head.nr_out = next_rows->data_ptr<int>();
+      head.nr_perm = next_rows_perm->data_ptr<int>();
+      head.nr_len = next_rows_perm->numel();
+      head.nr_batch = (int)next_rows->numel();
+    }
   }
   check_hip(arena_wgrad_grouped(probs.data(), (int)n, a, (float)grad_scale, ctr, head,
                                 cur_stream()),

@@ -543,6 +543,12 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
       if (mc0 == 0 && (int)blockIdx.x == args.head_block) {  // zero the other buffer + next slot
         float* nxt = HD.logits2 + (long long)((hstep + 1) & 1) * P.M * HD.C;
         for (int i = threadIdx.x; i < P.M * HD.C; i += 256) nxt[i] = 0.f;
+        if (HD.nr_out != nullptr && (int)threadIdx.x < HD.nr_batch) {
+          long long q = mod_fp64((double)(hstep + 1) * (double)HD.nr_batch, HD.nr_len) +
+                        (long long)threadIdx.x;
+          q = (q >= HD.nr_len) ? q - HD.nr_len : q;
+          HD.nr_out[threadIdx.x] = HD.nr_perm[q];
+        }
         if (threadIdx.x == 0 && HD.hist_len > 1) {
           const int ns = (int)(hstep + 1) & (HD.hist_len - 1);
           HD.loss_acc[ns] = 0.f;
@@ -801,13 +807,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 4))) voi
 // m-tile-0 workgroups also snapshot W2 for the backward pass (which updates W2 in place). The
 // softmax itself is recomputed by every wgrad workgroup: no intra-kernel hand-off anywhere.
 // ---------------------------------------------------------------------------------------------
-template <int XT, int WAVES, bool FAST>
+// FM: 0 = generic; 1 = training-step fast path gathering rows from the step counter; 2 = fast
+// path reading this step's rows precomputed by the previous backward kernel.
+template <int XT, int WAVES, int FM>
 __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
     ArenaRowSource src, const float* __restrict__ W, const float* __restrict__ bias,
     float* __restrict__ Y, int M, int N, int K, uint32_t keep_thr, float inv_keep, uint32_t seed,
     const long long* step_src, const float* __restrict__ W2, float* __restrict__ W2_copy, int C,
     float* __restrict__ logits2, uint8_t* __restrict__ xb, const void* __restrict__ lab_ptr,
-    int lab_dtype, int* __restrict__ yb, ArenaCounterOp ctr) {
+    int lab_dtype, int* __restrict__ yb, ArenaCounterOp ctr, const int* __restrict__ rows) {
   constexpr int CH = 8;
   const int lane = lane_id(), w = wave_id();
   const int g = lane >> 4, c = lane & 15;
@@ -827,6 +835,7 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
   long long stepv;
   long long prow;
   float w2v, bv;
+  constexpr bool FAST = FM != 0;
   if constexpr (FAST) {
     // The fused training step (host-checked: cursor == step counter == counter-op source, one
     // K chunk per wave, gather on, publishing on). One straight load stream: the step counter
@@ -836,6 +845,9 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
     // label publication and the counter update move to the end.
     int lz;
     asm volatile("v_mov_b32 %0, 0" : "=v"(lz));
+    // FM 2: the row index is the oldest load, so waiting for it leaves the W loads in flight
+    int prow2 = 0;
+    if constexpr (FM == 2) prow2 = rows[rowc] + lz;
     const int A = *reinterpret_cast<const int*>(step_src) + lz;
     __builtin_amdgcn_sched_barrier(0);
     float b[CH][4];
@@ -849,9 +861,13 @@ __global__ __launch_bounds__(WAVES * 64) void mlp_fwd_logits_kernel(
              min(n0 + ((int)threadIdx.x & 15), N - 1)];
     bv = bias[min(n0 + ((int)threadIdx.x & 15), N - 1)];
     __builtin_amdgcn_sched_barrier(0);  // keep the independent loads above the counter's first use
-    long long p = mod_fp64((double)A * (double)src.batch, src.idx_len) + rowc;
-    p = (p >= src.idx_len) ? p - src.idx_len : p;
-    prow = src.idx[p];
+    if constexpr (FM == 2) {  // this step's rows, precomputed by the previous backward kernel
+      prow = prow2;
+    } else {
+      long long p = mod_fp64((double)A * (double)src.batch, src.idx_len) + rowc;
+      p = (p >= src.idx_len) ? p - src.idx_len : p;
+      prow = src.idx[p];
+    }
     stepv = A;
     ARENA_TL_DEP((int)prow);
     ARENA_TL(0, 1);
@@ -1136,7 +1152,7 @@ hipError_t arena_mlp_fwd_logits(ArenaRowSource src, const float* W, const float*
                                 int M, int N, int K, float keep_prob, uint32_t seed,
                                 const long long* step_src, const float* W2, float* W2_copy, int C,
                                 float* logits2, uint8_t* xb, const void* lab_ptr, int lab_dtype,
-                                int* yb, ArenaCounterOp ctr, hipStream_t stream) {
+                                int* yb, ArenaCounterOp ctr, const int* rows, hipStream_t stream) {
   if (C < 1 || C > 16 || K % 4) return hipErrorInvalidValue;
   uint32_t thr = 0xFFFFFFFFu;
   float inv_keep = 1.f;
@@ -1151,18 +1167,22 @@ hipError_t arena_mlp_fwd_logits(ArenaRowSource src, const float* W, const float*
                     src.cursor == step_src && src.cursor_off == 0 && ctr.dst != nullptr &&
                     ctr.src == step_src && xb != nullptr && lab_ptr != nullptr &&
                     (nsteps + 7) / 8 <= 8 && src.idx_len < (1LL << 31);
-  if (fast)
-    hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8, true>), grid, dim3(512), 0, stream, src, W,
+  if (fast && rows != nullptr)
+    hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8, 2>), grid, dim3(512), 0, stream, src, W,
                        bias, Y, M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2,
-                       xb, lab_ptr, lab_dtype, yb, ctr);
+                       xb, lab_ptr, lab_dtype, yb, ctr, rows);
+  else if (fast)
+    hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8, 1>), grid, dim3(512), 0, stream, src, W,
+                       bias, Y, M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2,
+                       xb, lab_ptr, lab_dtype, yb, ctr, rows);
   else if (src.dtype == 1)
-    hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8, false>), grid, dim3(512), 0, stream, src, W,
+    hipLaunchKernelGGL((mlp_fwd_logits_kernel<1, 8, 0>), grid, dim3(512), 0, stream, src, W,
                        bias, Y, M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2,
-                       xb, lab_ptr, lab_dtype, yb, ctr);
+                       xb, lab_ptr, lab_dtype, yb, ctr, nullptr);
   else
-    hipLaunchKernelGGL((mlp_fwd_logits_kernel<0, 8, false>), grid, dim3(512), 0, stream, src, W,
+    hipLaunchKernelGGL((mlp_fwd_logits_kernel<0, 8, 0>), grid, dim3(512), 0, stream, src, W,
                        bias, Y, M, N, K, thr, inv_keep, seed, step_src, W2, W2_copy, C, logits2,
-                       nullptr, lab_ptr, lab_dtype, yb, ctr);
+                       nullptr, lab_ptr, lab_dtype, yb, ctr, nullptr);
   return hipGetLastError();
 }
 

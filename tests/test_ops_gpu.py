@@ -114,7 +114,7 @@ def test_wgrad_grouped(cuda, mode):
                 [st[6], st[7]], 1e-3, None, 0.9, 0.999, 1e-8, 0.0, t, 0.5, False, A, t, 0)
         if impl == "hip":
             from arena_amd.ops import _ext
-            _ext.load().wgrad_grouped(*args)
+            _ext.load().wgrad_grouped(*args, None, None)
         else:
             ref.wgrad_grouped(*args)
         torch.cuda.synchronize()
@@ -213,7 +213,7 @@ def test_mlp_fwd_logits_matches_reference(cuda, M, N, C):
                 Bc, A, 1)
         if impl == "hip":
             from arena_amd.ops import _ext
-            _ext.load().mlp_fwd_logits(*args)
+            _ext.load().mlp_fwd_logits(*args, None)
         else:
             ref.mlp_fwd_logits(*args)
         torch.cuda.synchronize()
@@ -263,7 +263,7 @@ def test_wgrad_head_modes(cuda, mode):
                 0)
         if impl == "hip":
             from arena_amd.ops import _ext
-            _ext.load().wgrad_grouped(*args)
+            _ext.load().wgrad_grouped(*args, None, None)
         else:
             ref.wgrad_grouped(*args)
         torch.cuda.synchronize()

@@ -18,7 +18,7 @@ def test_fused_gpu_matches_cpu_reference(cuda, small_data):
     cfg = MLPConfig(batch=100, seed=3)
     gpu = FusedMLPTrainer(cfg, x, y, device=cuda)
     cpu = FusedMLPTrainer(cfg, x, y, device="cpu")
-    cpu.perm.copy_(gpu.perm.cpu())  # same data order (device RNG streams differ by backend)
+    cpu.set_permutation(gpu.perm.cpu())  # same data order (device RNG streams differ by backend)
     for _ in range(10):
         gpu.train_steps(1)
         cpu.train_steps(1)
@@ -31,7 +31,7 @@ def test_graph_replay_equals_eager(cuda, small_data):
     cfg = MLPConfig(batch=100, seed=5)
     a = FusedMLPTrainer(cfg, x, y, device=cuda)
     b = FusedMLPTrainer(cfg, x, y, device=cuda)
-    b.perm.copy_(a.perm)
+    b.set_permutation(a.perm)
     assert a.enable_graphs(10)
     a.train_steps(20)
     b.train_steps(20)
