@@ -310,26 +310,47 @@ def cmd_completion(ctx, ns) -> int:
 
 
 # ------------------------------------------------------------------------------------ parser
+def _add_global_flags(p: argparse.ArgumentParser, defaults: bool) -> None:
+    def d(v):
+        return v if defaults else argparse.SUPPRESS
+    p.add_argument("--config", default=d(""), help="Path to a kube config. Only required if "
+                                                    "out-of-cluster (k8s backend)")
+    p.add_argument("--namespace", default=d("default"), help="the namespace of the job")
+    p.add_argument("--loglevel", default=d("info"), help="Set the logging level. One of: "
+                                                          "debug|info|warn|error")
+    p.add_argument("--pprof", action="store_true", default=d(False),
+                   help="enable cpu profile (/tmp/cpu_profile)")
+    p.add_argument("--arenaNamespace", default=d("arena-system"),
+                   help="The namespace of arena system service, like TFJob")
+    p.add_argument("--backend", default=d(None),
+                   help="local | k8s (default: $ARENA_BACKEND or local)")
+    p.add_argument("--home", default=d(None), help="job store directory (default: $ARENA_HOME "
+                                                   "or ~/.arena)")
+
+
 def build_parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(
         prog="arena",
         description="arena is the command line interface to Arena (MI355X-native): submit, "
                     "monitor and manage training jobs on AMD Instinct GPUs.")
-    p.add_argument("--config", default="", help="Path to a kube config. Only required if "
-                                                 "out-of-cluster (k8s backend)")
-    p.add_argument("--namespace", default="default", help="the namespace of the job")
-    p.add_argument("--loglevel", default="info", help="Set the logging level. One of: "
-                                                       "debug|info|warn|error")
-    p.add_argument("--pprof", action="store_true", help="enable cpu profile (/tmp/cpu_profile)")
-    p.add_argument("--arenaNamespace", default="arena-system",
-                   help="The namespace of arena system service, like TFJob")
-    p.add_argument("--backend", default=None, help="local | k8s (default: $ARENA_BACKEND or local)")
-    p.add_argument("--home", default=None, help="job store directory (default: $ARENA_HOME or "
-                                                "~/.arena)")
+    _add_global_flags(p, defaults=True)
+    # cobra persistent flags (root.go:39-44,60-70) are accepted after any subcommand too:
+    # every subparser inherits the global flags with SUPPRESS defaults, so a flag given after
+    # the subcommand overrides the root value and an absent one leaves it untouched.
+    glob = argparse.ArgumentParser(add_help=False)
+    _add_global_flags(glob, defaults=False)
+    _orig_sub = argparse._SubParsersAction.add_parser  # noqa: SLF001
+
+    def _add_parser(self, name, **kw):
+        kw.setdefault("parents", []).append(glob)
+        return _orig_sub(self, name, **kw)
+
     sub = p.add_subparsers(dest="cmd", metavar="COMMAND")
+    sub.add_parser = _add_parser.__get__(sub)
 
     sp = sub.add_parser("submit", help="Submit a job.")
     ssub = sp.add_subparsers(dest="kind", metavar="KIND")
+    ssub.add_parser = _add_parser.__get__(ssub)
     tf = ssub.add_parser("tfjob", aliases=["tf"], help="Submit a parameter-server/worker job.")
     _add_common_flags(tf)
     _add_sync_flags(tf)
@@ -400,6 +421,7 @@ def build_parser() -> argparse.ArgumentParser:
 
     tp = sub.add_parser("top", help="Display Resource (GPU) usage.")
     tsub = tp.add_subparsers(dest="topkind", metavar="KIND")
+    tsub.add_parser = _add_parser.__get__(tsub)
     tn = tsub.add_parser("node", help="Display Resource (GPU) usage of nodes")
     tn.add_argument("-d", "--details", action="store_true", help="Display details")
     tn.set_defaults(func=cmd_top_node)

@@ -231,3 +231,19 @@ def test_version_and_completion(env):
     assert "complete -F _arena arena" in out and "submit" in out
     rc, out = arena("completion", "zsh")
     assert "compdef _arena arena" in out
+
+
+def test_global_flags_after_subcommand(env):
+    """cobra persistent flags (root.go:39-44) work before or after the subcommand."""
+    fake, clock, arena = env
+    rc, out = arena("submit", "sj", "--name", "ns1", "--image", "i", "--namespace", "team-a",
+                    "python", "x.py")
+    assert rc == 0, out
+    fake.schedule()
+    rc, out = arena("list", "--namespace", "team-a")
+    assert rc == 0 and "ns1" in out
+    rc, out = arena("--namespace", "team-a", "get", "ns1")
+    assert rc == 0 and "ns1" in out
+    with pytest.raises(SystemExit) as ei:          # util/logs.go:20-21: fatal
+        arena("top", "job", "--loglevel", "bogus")
+    assert ei.value.code == 1
