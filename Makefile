@@ -3,10 +3,11 @@
 #   make test       CPU test suite (no GPU needed)
 #   make test-gpu   GPU tests (MI355X)
 #   make bench      flagship benchmark, 1 GPU
+#   make test-asan  CPU runtime tests with ASan+UBSan native tools (test-tsan: ThreadSanitizer)
 PYTHON ?= python3
 export PYTORCH_ROCM_ARCH ?= gfx950
 
-.PHONY: all ext native test test-gpu bench e2e clean version
+.PHONY: all ext native native-asan native-tsan test test-asan test-tsan test-gpu bench e2e clean version
 
 all: ext native
 
@@ -15,6 +16,19 @@ ext:
 
 native:
 	$(PYTHON) -c 'from arena_amd import _build; print("\n".join(_build.build_native_tools(force=True)))'
+
+# host-code sanitizers for the native runtime tools; GPU code is never sanitized
+native-asan:
+	$(PYTHON) -c 'from arena_amd import _build; print("\n".join(_build.build_native_tools(force=True, sanitize="asan")))'
+
+native-tsan:
+	$(PYTHON) -c 'from arena_amd import _build; print("\n".join(_build.build_native_tools(force=True, sanitize="tsan")))'
+
+test-asan: native-asan
+	ARENA_NATIVE_SANITIZE=asan $(PYTHON) -m pytest tests/test_local_backend.py tests/test_parallel.py tests/test_sanitizers.py -q -m "not gpu"
+
+test-tsan: native-tsan
+	ARENA_NATIVE_SANITIZE=tsan $(PYTHON) -m pytest tests/test_local_backend.py tests/test_parallel.py tests/test_sanitizers.py -q -m "not gpu"
 
 test:
 	$(PYTHON) -m pytest tests -q -m "not gpu"

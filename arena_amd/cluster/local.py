@@ -209,6 +209,8 @@ class LocalBackend(Backend):
     def _spawn_supervisor(self, jd: str) -> None:
         sup = _build.ensure_tool("arena-supervisor")
         env = dict(os.environ)
+        for k, v in _build.sanitizer_env().items():   # ARENA_NATIVE_SANITIZE=asan|tsan
+            env.setdefault(k, v)
         with open(os.path.join(jd, "supervisor.log"), "ab") as lf:
             p = subprocess.Popen([sup, jd], stdin=subprocess.DEVNULL, stdout=lf, stderr=lf,
                                  start_new_session=True, env=env, close_fds=True)

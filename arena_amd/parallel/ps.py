@@ -215,7 +215,11 @@ def spawn_server(port: int, workers: int, **kw) -> subprocess.Popen:
             "--lr", repr(kw.get("lr", 1e-3))]
     if kw.get("sync"):
         argv.append("--sync")
-    p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True)
+    env = dict(os.environ)
+    for k, v in _build.sanitizer_env().items():       # ARENA_NATIVE_SANITIZE=asan|tsan
+        env.setdefault(k, v)
+    p = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                         env=env)
     line = p.stdout.readline()          # "arena-ps: serving on ..."
     if "serving" not in line:
         p.kill()
