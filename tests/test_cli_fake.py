@@ -247,3 +247,17 @@ def test_global_flags_after_subcommand(env):
     with pytest.raises(SystemExit) as ei:          # util/logs.go:20-21: fatal
         arena("top", "job", "--loglevel", "bogus")
     assert ei.value.code == 1
+
+
+def test_pprof_writes_cpu_profile(tmp_path, monkeypatch, capsys):
+    """B1: --pprof anywhere on the command line dumps a CPU profile (cmd/arena/main.go:14-39)."""
+    import pstats
+    from arena_amd.cli.main import _pprof_enabled, main
+    prof = tmp_path / "cpu_profile"
+    monkeypatch.setenv("ARENA_PPROF_PATH", str(prof))
+    monkeypatch.setenv("ARENA_HOME", str(tmp_path / "home"))
+    assert main(["version", "--short", "--pprof"]) == 0
+    assert capsys.readouterr().out.startswith("v")
+    st = pstats.Stats(str(prof))
+    assert any("cmd_version" in fn for (_, _, fn) in st.stats)
+    assert not _pprof_enabled(["--pprof=false", "list"]) and _pprof_enabled(["list", "--pprof"])
