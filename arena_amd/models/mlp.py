@@ -428,8 +428,12 @@ class FusedMLPTrainer:
             M, V = M.clone(), V.clone()
             self.xgmi.all_reduce_(M)
             self.xgmi.all_reduce_(V)
+        # the epoch order and the shuffle generator too, so a resumed run replays exactly the
+        # batches (and dropout masks: keyed by the step counter) the uninterrupted run would see
         return {"P": self.P.detach().cpu(), "M": M.detach().cpu(), "V": V.detach().cpu(),
-                "step": int(self.ctrA.item()), "layout": dict(self.layout.shapes)}
+                "step": int(self.ctrA.item()), "layout": dict(self.layout.shapes),
+                "perm": self.perm.detach().cpu(), "rng": self._gen.get_state(),
+                "rank": self.rank, "world": self.world}
 
     def load_state_dict(self, sd):
         self.P.copy_(sd["P"])
@@ -442,4 +446,9 @@ class FusedMLPTrainer:
         self.ctrA.fill_(int(sd["step"]))
         self.ctrB.fill_(int(sd["step"]))
         self.steps_done = int(sd["step"])
+        if (sd.get("perm") is not None and sd.get("world", self.world) == self.world
+                and sd.get("rank", self.rank) == self.rank
+                and sd["perm"].numel() == self.perm.numel()):
+            self.perm.copy_(sd["perm"])
+            self._gen.set_state(sd["rng"])
         self._sync_rows()
