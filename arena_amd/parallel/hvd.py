@@ -218,6 +218,9 @@ class DistributedOptimizer:
             elif comm == "xgmi":
                 raise xgmi.XgmiUnavailable("xGMI collective not usable for this process group")
         self.comm = "xgmi" if self.xgmi is not None else "rccl"
+        # xGMI buckets run on their own stream (RCCL's async_op already has one), ordered after
+        # the gradients through an event, so the collective overlaps the rest of backward
+        self._stream = torch.cuda.Stream() if self.xgmi is not None else None
         if size() > 1:
             for p in params:
                 self._hooks.append(p.register_post_accumulate_grad_hook(self._on_grad))
@@ -235,10 +238,16 @@ class DistributedOptimizer:
         grads = [g.contiguous() for g in grads]
         if self.xgmi is not None:
             # pack straight into the registered staging buffer (zero-copy input), average on the
-            # way out; stream-ordered, so it overlaps the host side of backward
-            stage = self.xgmi.buffer()[: b.flat.numel()]
-            ops.flatten_into(grads, b.offsets, stage, 1.0)
-            self.xgmi.all_reduce_(stage, scale=1.0 / size(), out=b.flat)
+            # way out. Comm stream: waits for the grads (event), then buckets run in launch order,
+            # so the shared staging buffer is never overwritten while a reduction still reads it.
+            ready = torch.cuda.current_stream()
+            self._stream.wait_stream(ready)
+            with torch.cuda.stream(self._stream):
+                for g in grads:
+                    g.record_stream(self._stream)
+                stage = self.xgmi.buffer()[: b.flat.numel()]
+                ops.flatten_into(grads, b.offsets, stage, 1.0)
+                self.xgmi.all_reduce_(stage, scale=1.0 / size(), out=b.flat)
             b.work = _DONE
             return
         ops.flatten_into(grads, b.offsets, b.flat, 1.0)
@@ -257,6 +266,9 @@ class DistributedOptimizer:
         for b in self.buckets:
             if b.work is None:  # some grads never arrived (unused params): reduce anyway
                 self._launch(b)
+        if self._stream is not None:
+            torch.cuda.current_stream().wait_stream(self._stream)
+        for b in self.buckets:
             b.work.wait()
             grads = []
             for p in b.params:

@@ -159,6 +159,50 @@ def _trainer(rank, world, port, q):
         q.put((rank, None, traceback.format_exc()))
 
 
+def _hvd_optimizer(rank, world, port, q):
+    """hvd.DistributedOptimizer over the xGMI kernel (comm stream, small buckets so several are in
+    flight) vs the mean gradient of every rank's batch computed locally."""
+    try:
+        _init(rank, world, port)
+        from arena_amd.parallel import hvd
+        hvd.init()
+
+        def make():
+            torch.manual_seed(11)
+            return torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(),
+                                       torch.nn.Linear(256, 128), torch.nn.ReLU(),
+                                       torch.nn.Linear(128, 10)).cuda()
+
+        def batch(r, step):
+            g = torch.Generator(device="cuda").manual_seed(1000 * step + r)
+            return (torch.randn(32, 64, device="cuda", generator=g),
+                    torch.randint(0, 10, (32,), device="cuda", generator=g))
+
+        model, ref = make(), make()
+        opt = hvd.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1),
+                                       named_parameters=model.named_parameters(),
+                                       bucket_mb=0.05, comm="xgmi")
+        ropt = torch.optim.SGD(ref.parameters(), lr=0.1)
+        assert opt.comm == "xgmi" and len(opt.buckets) >= 2, (opt.comm, len(opt.buckets))
+        for step in range(3):
+            x, y = batch(rank, step)
+            opt.zero_grad()
+            torch.nn.functional.cross_entropy(model(x), y).backward()
+            opt.step()
+            ropt.zero_grad()
+            for r in range(world):      # reference: mean of every rank's gradient
+                xr, yr = batch(r, step)
+                (torch.nn.functional.cross_entropy(ref(xr), yr) / world).backward()
+            ropt.step()
+        torch.cuda.synchronize()
+        diff = max(float((a - b).abs().max()) for a, b in zip(model.parameters(), ref.parameters()))
+        opt.xgmi.check()
+        q.put((rank, {"diff": diff, "buckets": len(opt.buckets)}, None))
+        hvd.shutdown()
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
 def _run(fn, world, timeout=240):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -201,3 +245,9 @@ def test_trainer_dp_xgmi_matches_allreduce_path():
         assert res["steps"] == 12 and res["mode"] == "full", res
         # logits accumulate with f32 atomics (order varies run to run): equal to rounding
         assert res["P"] < 5e-5 and res["M"] < 1e-6, (r, res)
+
+
+def test_hvd_distributed_optimizer_xgmi_comm_stream():
+    out = _run(_hvd_optimizer, 2)
+    for r, res in out.items():
+        assert res["diff"] < 1e-5, (r, res)
