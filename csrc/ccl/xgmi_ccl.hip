@@ -77,6 +77,12 @@ __device__ __forceinline__ void xbarrier(const ArenaXgmiPeers& P, int phase, int
   __syncthreads();
 }
 
+// float4 slots per thread per reduce round: a block of kThreads covers kU * 4 * kThreads floats
+// with one xGMI round trip per thread (g_block_elems = 4096 -> one round). At W = 8 the fused
+// Adam kernel holds kU * (W + 3) float4 operands in flight: 256 VGPRs, no scratch (checked with
+// -Rpass-analysis=kernel-resource-usage).
+constexpr int kU = 4;
+
 // dst[c*L + o] = src[c*L + o] for all chunks c, W loads in flight per thread.
 template <int W>
 __device__ __forceinline__ void copy_chunks(float* __restrict__ dst, const float* __restrict__ src,
@@ -110,18 +116,33 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(ArenaXgmiPeers
   if (in != mine) copy_chunks<W>(mine, in, n, L, lo, hi);
   xbarrier<W>(P, 0, b, e);
   const long long base = (long long)P.rank * L;
-  for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
-    const long long i = base + o;
-    if (i >= n) break;
-    float4 v[W];
+  constexpr int U = kU;
+  for (long long o0 = lo + threadIdx.x * 4; o0 < hi; o0 += (long long)kThreads * 4 * U) {
+    // every remote load of this thread's U float4 slots is issued before the first store (the
+    // stores may alias the loads, so the compiler cannot hoist the next slot's loads above them):
+    // ONE xGMI round trip per thread instead of one per slot
+    float4 v[U][W];
+    bool ok[U];
+    long long idx[U];
 #pragma unroll
-    for (int q = 0; q < W; ++q) v[q] = ld4(P.buf[q] + i);  // W loads in flight, one per link
-    float4 acc = v[0];
+    for (int u = 0; u < U; ++u) {
+      const long long o = o0 + (long long)u * kThreads * 4;
+      ok[u] = o < hi && base + o < n;
+      idx[u] = ok[u] ? base + o : 0;  // clamped, branch-free loads
 #pragma unroll
-    for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);     // fixed order: identical on all ranks
-    acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
+      for (int q = 0; q < W; ++q) v[u][q] = ld4(P.buf[q] + idx[u]);  // one load per link
+    }
 #pragma unroll
-    for (int q = 0; q < W; ++q) st4(P.buf[q] + i, acc);
+    for (int u = 0; u < U; ++u) {
+      float4 acc = v[u][0];
+#pragma unroll
+      for (int q = 1; q < W; ++q) acc = add4(acc, v[u][q]);  // fixed order: same on all ranks
+      acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
+      if (ok[u]) {
+#pragma unroll
+        for (int q = 0; q < W; ++q) st4(P.buf[q] + idx[u], acc);
+      }
+    }
   }
   xbarrier<W>(P, 1, b, e);
   if (out != mine) copy_chunks<W>(out, mine, n, L, lo, hi);
@@ -141,26 +162,39 @@ __global__ __launch_bounds__(kThreads) void xgmi_adam_kernel(ArenaXgmiPeers P, f
   xbarrier<W>(P, 0, b, e);
   const long long base = (long long)P.rank * L;
   float* Pm = P.buf2[P.rank];
-  for (long long o = lo + threadIdx.x * 4; o < hi; o += kThreads * 4) {
-    const long long i = base + o;
-    if (i >= n) break;
-    float4 v[W];
+  constexpr int U = kU;
+  for (long long o0 = lo + threadIdx.x * 4; o0 < hi; o0 += (long long)kThreads * 4 * U) {
+    // all loads of the thread's U slots (W remote gradients + local P/M/V each) before any store
+    float4 v[U][W], p[U], m[U], s[U];
+    bool ok[U];
+    long long idx[U];
 #pragma unroll
-    for (int q = 0; q < W; ++q) v[q] = ld4(P.buf[q] + i);
-    float4 p = ld4(Pm + i);
-    float4 m = ld4(M + i);
-    float4 s = ld4(V + i);
-    float4 g = v[0];
+    for (int u = 0; u < U; ++u) {
+      const long long o = o0 + (long long)u * kThreads * 4;
+      ok[u] = o < hi && base + o < n;
+      idx[u] = ok[u] ? base + o : 0;
 #pragma unroll
-    for (int q = 1; q < W; ++q) g = add4(g, v[q]);
-    adam_apply(co, g.x, p.x, m.x, s.x);
-    adam_apply(co, g.y, p.y, m.y, s.y);
-    adam_apply(co, g.z, p.z, m.z, s.z);
-    adam_apply(co, g.w, p.w, m.w, s.w);
-    st4(M + i, m);
-    st4(V + i, s);
+      for (int q = 0; q < W; ++q) v[u][q] = ld4(P.buf[q] + idx[u]);
+      p[u] = ld4(Pm + idx[u]);
+      m[u] = ld4(M + idx[u]);
+      s[u] = ld4(V + idx[u]);
+    }
 #pragma unroll
-    for (int q = 0; q < W; ++q) st4(P.buf2[q] + i, p);
+    for (int u = 0; u < U; ++u) {
+      float4 g = v[u][0];
+#pragma unroll
+      for (int q = 1; q < W; ++q) g = add4(g, v[u][q]);
+      adam_apply(co, g.x, p[u].x, m[u].x, s[u].x);
+      adam_apply(co, g.y, p[u].y, m[u].y, s[u].y);
+      adam_apply(co, g.z, p[u].z, m[u].z, s[u].z);
+      adam_apply(co, g.w, p[u].w, m[u].w, s[u].w);
+      if (ok[u]) {
+        st4(M + idx[u], m[u]);
+        st4(V + idx[u], s[u]);
+#pragma unroll
+        for (int q = 0; q < W; ++q) st4(P.buf2[q] + idx[u], p[u]);
+      }
+    }
   }
   xbarrier<W>(P, 1, b, e);
   counter_op(ctr);
