@@ -362,6 +362,9 @@ class LocalBackend(Backend):
                 argv = self._argv(c.command, values, jd, p.name)
             own = gpus.get(p.name, [])
             if kind == "allreduce" and role in ("mpimaster", "mpiworker"):
+                # the chart's `export RANK=...` prefix, resolved here as well: a --profile-gpu
+                # rank runs without the shell (rocprofv3 execs the program directly)
+                env["RANK"] = "0" if role == "mpimaster" else str(int(p.name.rsplit("-", 1)[1]) + 1)
                 env["MASTER_ADDR"] = "127.0.0.1"
                 env["MASTER_PORT"] = str(ports["rdzv"])
                 env["LOCAL_WORLD_SIZE"] = str(len(ranks))   # every rank is on this node

@@ -267,3 +267,31 @@ def test_logviewer_serves_dashboard_urls(env):
         assert b"arena log viewer" in urllib.request.urlopen(base + "/tfjobs/ui/", timeout=10).read()
     finally:
         os.kill(info["pid"], signal.SIGTERM)
+
+
+def test_profile_gpu_runs_ranks_under_rocprofv3(env, tmp_path, monkeypatch):
+    """--profile-gpu: each rank is exec'd by rocprofv3 (no shell hop) with traces in the job dir,
+    and keeps its RANK although the chart's `export RANK=...` shell prefix is dropped."""
+    bindir = tmp_path / "fakebin"
+    bindir.mkdir()
+    fake = bindir / "rocprofv3"
+    fake.write_text("#!/bin/sh\n"
+                    "while [ \"$1\" != \"--\" ]; do\n"
+                    "  if [ \"$1\" = \"-d\" ]; then shift; mkdir -p \"$1\"; "
+                    "echo traced > \"$1/run_kernel_stats.csv\"; fi\n"
+                    "  shift\ndone\nshift\nexec \"$@\"\n")
+    fake.chmod(0o755)
+    monkeypatch.setenv("PATH", f"{bindir}{os.pathsep}{os.environ['PATH']}")
+    script = tmp_path / "ar.py"
+    script.write_text(ALLREDUCE.replace("; ", "\n"))
+    cli(env, "submit", "mpi", "--name", "pg", "--workers", "2", "--profile-gpu",
+        f"{PY} {script}")
+    st = wait_phase(env, "pg", timeout=120)
+    assert st["phase"] == "Succeeded", st
+    jd = env.job_dir("pg")
+    logs = "".join(open(os.path.join(jd, "logs", f)).read() for f in os.listdir(os.path.join(jd, "logs")))
+    for r in range(2):
+        assert f"rank {r} of 2 sum 3.0" in logs
+    traced = sorted(os.listdir(os.path.join(jd, "traces")))
+    assert len(traced) == 2 and all(
+        os.path.exists(os.path.join(jd, "traces", t, "run_kernel_stats.csv")) for t in traced)
