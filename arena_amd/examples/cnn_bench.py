@@ -1,0 +1,160 @@
+"""Synthetic-ImageNet CNN training benchmark with the Horovod-style API (tf_cnn_benchmarks shape).
+
+The reference's MPI demo runs the Horovod TF image's ``hvd-distribute.sh``
+(charts/tf-horovod/README.md:66-69). That image benchmarks the ResNet family on synthetic data
+with Horovod allreduce. The script is not in the reference repo, so exact flags are unpinned.
+This is the same workload, built for MI355X:
+
+* ResNet v1.5 (``arena_amd.models.resnet``), NHWC (``channels_last``), bf16 autocast on the MFMA
+  conv/GEMM paths, fp32 master weights;
+* momentum SGD with weight decay, as in tf_cnn_benchmarks;
+* one process per GPU: ``hvd.DistributedOptimizer`` buckets (RCCL or the xGMI kernel on a comm
+  stream) overlap the gradient allreduce with backward;
+* output lines shaped like tf_cnn_benchmarks' ``images/sec`` and ``total images/sec``.
+
+    arena submit mpijob --name r50 --workers 8 --gpus 1 \\
+        "python -m arena_amd.examples.cnn_bench --model resnet50 --batch_size 128"
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.nn.functional as F
+
+from .common import pick_device, share_cpu_threads
+
+
+def parse(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch_size", type=int, default=128, help="per-rank batch")
+    ap.add_argument("--image_size", type=int, default=224)
+    ap.add_argument("--num_classes", type=int, default=1000)
+    ap.add_argument("--width", type=int, default=64)
+    ap.add_argument("--num_batches", type=int, default=100)
+    ap.add_argument("--num_warmup_batches", type=int, default=10)
+    ap.add_argument("--display_every", type=int, default=10)
+    ap.add_argument("--learning_rate", type=float, default=0.1)
+    ap.add_argument("--momentum", type=float, default=0.9)
+    ap.add_argument("--weight_decay", type=float, default=4e-5)
+    ap.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    ap.add_argument("--data_format", choices=["NHWC", "NCHW"], default="NHWC")
+    ap.add_argument("--bucket_mb", type=float, default=64.0, help="Horovod fusion-buffer size")
+    ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto")
+    ap.add_argument("--device", default="auto")
+    ap.add_argument("--json", action="store_true", help="print one JSON summary line at the end")
+    return ap.parse_args(argv)
+
+
+def build(args, dev, world):
+    """Model, optimizer (wrapped for DP) and one synthetic batch, ready to step."""
+    from ..models.resnet import resnet
+    from ..parallel import hvd
+    torch.manual_seed(1234)
+    model = resnet(args.model, num_classes=args.num_classes, width=args.width).to(dev)
+    nhwc = dev.type == "cuda" and args.data_format == "NHWC"
+    if nhwc:
+        model = model.to(memory_format=torch.channels_last)
+    hvd.broadcast_parameters(model.state_dict(), root_rank=0)
+    decay, no_decay = [], []
+    for n, p in model.named_parameters():
+        (no_decay if p.ndim <= 1 else decay).append(p)   # no decay on BN / bias
+    opt = torch.optim.SGD([{"params": decay, "weight_decay": args.weight_decay},
+                           {"params": no_decay, "weight_decay": 0.0}],
+                          lr=args.learning_rate, momentum=args.momentum,
+                          foreach=dev.type == "cuda")
+    if world > 1:
+        opt = hvd.DistributedOptimizer(opt, named_parameters=model.named_parameters(),
+                                       bucket_mb=args.bucket_mb, comm=args.comm)
+    g = torch.Generator(device=dev).manual_seed(hvd.rank())
+    x = torch.randn(args.batch_size, 3, args.image_size, args.image_size, device=dev, generator=g)
+    if nhwc:
+        x = x.contiguous(memory_format=torch.channels_last)
+    y = torch.randint(0, args.num_classes, (args.batch_size,), device=dev, generator=g)
+    return model, opt, x, y
+
+
+def train_step(model, opt, x, y, amp_dtype):
+    with torch.autocast(device_type=x.device.type, dtype=amp_dtype, enabled=amp_dtype is not None):
+        loss = F.cross_entropy(model(x), y)
+    opt.zero_grad(set_to_none=True)
+    loss.backward()
+    opt.step()
+    return loss.detach()
+
+
+def main(argv=None) -> int:
+    args = parse(argv)
+    from ..parallel import hvd
+    dev = pick_device(args.device)
+    hvd.init("nccl" if dev.type == "cuda" else "gloo")
+    world, rank = hvd.size(), hvd.rank()
+    if dev.type == "cuda":
+        torch.cuda.set_device(dev)
+        torch.backends.cudnn.benchmark = True      # MIOpen: pick the fastest conv solvers once
+    else:
+        share_cpu_threads(int(os.environ.get("LOCAL_WORLD_SIZE", world)))
+    amp = torch.bfloat16 if args.dtype == "bf16" else None
+    model, opt, x, y = build(args, dev, world)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    if rank == 0:
+        print(f"Model: {args.model}  Batch size: {args.batch_size} per device, "
+              f"{args.batch_size * world} global  Devices: {world} x {dev.type}  "
+              f"Data: synthetic  dtype: {args.dtype}  comm: "
+              f"{getattr(opt, 'comm', 'none')}", flush=True)
+    for i in range(args.num_warmup_batches):
+        t = time.perf_counter()
+        train_step(model, opt, x, y, amp)
+        sync()
+        if rank == 0:   # the first steps include MIOpen's solver search: show progress
+            print(f"warmup {i + 1}/{args.num_warmup_batches}: {time.perf_counter() - t:.2f} s",
+                  flush=True)
+    sync()
+    if world > 1:
+        torch.distributed.barrier()
+    sync()
+    t0 = t_last = time.perf_counter()
+    loss = None
+    for i in range(1, args.num_batches + 1):
+        loss = train_step(model, opt, x, y, amp)
+        if i % args.display_every == 0 or i == args.num_batches:
+            sync()
+            now = time.perf_counter()
+            n = args.display_every if i % args.display_every == 0 else i % args.display_every
+            if rank == 0:
+                ips = n * args.batch_size / (now - t_last)
+                print(f"{i}\timages/sec: {ips:.1f} (per device)  loss {float(loss):.3f}",
+                      flush=True)
+            t_last = now
+    sync()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total = args.num_batches * args.batch_size * world / elapsed
+    if rank == 0:
+        print("-" * 64)
+        print(f"total images/sec: {total:.2f}", flush=True)
+        print("-" * 64)
+        if args.json:
+            print(json.dumps({"model": args.model, "images_per_s": round(total, 2),
+                              "ms_per_step": round(elapsed / args.num_batches * 1e3, 3),
+                              "batch_per_device": args.batch_size, "devices": world,
+                              "dtype": args.dtype, "comm": getattr(opt, "comm", "none"),
+                              "final_loss": round(float(loss), 4)}), flush=True)
+    hvd.shutdown()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
