@@ -8,8 +8,9 @@ one: a 7x7 stem, 4 stages of bottleneck blocks with the stride on the 3x3 conv (
 average pooling, and a 1000-way FC. ``width``/``depth`` knobs give tiny variants for CPU tests.
 
 MI355X layout: the model is meant to run with ``memory_format=torch.channels_last`` under bf16
-autocast, so the MIOpen convolutions take their NHWC MFMA paths. Parameters stay fp32 (master
-weights) for the data-parallel buckets and the optimizer.
+autocast, so the MIOpen convolutions take their NHWC MFMA paths. Each BatchNorm, with its ReLU
+and residual add, is one fused HIP kernel pair per direction (``arena_amd.ops.batchnorm``).
+Parameters stay fp32 (master weights) for the data-parallel buckets and the optimizer.
 """
 from __future__ import annotations
 
@@ -18,42 +19,45 @@ from typing import List
 import torch
 from torch import nn
 
+from ..ops.batchnorm import BatchNormAct2d
+
 DEPTHS = {"resnet50": [3, 4, 6, 3], "resnet101": [3, 4, 23, 3],
           "resnet152": [3, 8, 36, 3], "resnet_tiny": [1, 1, 1, 1]}
 
 
 class Bottleneck(nn.Module):
+    """conv1x1-BN-ReLU, conv3x3(stride)-BN-ReLU, conv1x1-BN, + shortcut, ReLU. Every BN is a
+    ``BatchNormAct2d``, so the last one also takes the residual add and the final ReLU
+    (one fused kernel pair instead of BN + add + ReLU)."""
     expansion = 4
 
     def __init__(self, cin: int, mid: int, stride: int):
         super().__init__()
         cout = mid * self.expansion
         self.conv1 = nn.Conv2d(cin, mid, 1, bias=False)
-        self.bn1 = nn.BatchNorm2d(mid)
+        self.bn1 = BatchNormAct2d(mid, act="relu")
         self.conv2 = nn.Conv2d(mid, mid, 3, stride=stride, padding=1, bias=False)
-        self.bn2 = nn.BatchNorm2d(mid)
+        self.bn2 = BatchNormAct2d(mid, act="relu")
         self.conv3 = nn.Conv2d(mid, cout, 1, bias=False)
-        self.bn3 = nn.BatchNorm2d(cout)
+        self.bn3 = BatchNormAct2d(cout, act="relu")
         nn.init.zeros_(self.bn3.weight)  # zero-init the residual branch's last BN (goyal et al.)
-        self.relu = nn.ReLU(inplace=True)
-        self.down = None
+        self.down_conv = self.down_bn = None
         if stride != 1 or cin != cout:
-            self.down = nn.Sequential(nn.Conv2d(cin, cout, 1, stride=stride, bias=False),
-                                      nn.BatchNorm2d(cout))
+            self.down_conv = nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+            self.down_bn = BatchNormAct2d(cout, act="none")
 
     def forward(self, x):
-        idt = x if self.down is None else self.down(x)
-        y = self.relu(self.bn1(self.conv1(x)))
-        y = self.relu(self.bn2(self.conv2(y)))
-        y = self.bn3(self.conv3(y))
-        return self.relu(y + idt)
+        idt = x if self.down_conv is None else self.down_bn(self.down_conv(x))
+        y = self.bn1(self.conv1(x))
+        y = self.bn2(self.conv2(y))
+        return self.bn3(self.conv3(y), residual=idt)
 
 
 class ResNet(nn.Module):
     def __init__(self, depths: List[int], num_classes: int = 1000, width: int = 64):
         super().__init__()
         self.stem = nn.Sequential(nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False),
-                                  nn.BatchNorm2d(width), nn.ReLU(inplace=True),
+                                  BatchNormAct2d(width, act="relu"),
                                   nn.MaxPool2d(3, stride=2, padding=1))
         layers = []
         cin = width

@@ -1,0 +1,111 @@
+"""Fused training BatchNorm (+ residual add) (+ ReLU) for NHWC activations.
+
+``BatchNormAct2d`` is a drop-in ``nn.BatchNorm2d`` whose forward can also add a residual tensor
+and apply ReLU: ``y = relu(bn(x) + residual)``. That is the whole tail of a ResNet bottleneck in
+one module. On an MI355X, with a channels_last bf16/fp32 input and a supported channel count,
+it runs the HIP kernels in ``csrc/ops/bn_kernels.hip``:
+
+* forward: 2 launches (statistics, then apply);
+* backward: 2 launches (reductions, then dx and the residual gradient).
+
+Otherwise it runs the same math as stock PyTorch ops. That includes CPU tensors, which serve as
+the reference.
+
+Semantics match ``nn.BatchNorm2d`` in training and eval mode:
+
+* batch statistics with the biased variance for normalisation;
+* running statistics updated with ``momentum`` and the unbiased variance;
+* the ReLU mask recovered from the saved output (y > 0).
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+from torch import nn
+
+from . import _ext
+
+SUPPORTED_C = {8, 16, 32, 64, 128, 256, 512, 1024, 2048}
+
+
+def kernel_ok(x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> bool:
+    """Shapes/layouts the HIP kernels take (everything else runs the PyTorch path)."""
+    ok = (x.is_cuda and x.dim() == 4 and x.shape[1] in SUPPORTED_C and x.numel() > 0
+          and x.dtype in (torch.bfloat16, torch.float32)
+          and x.is_contiguous(memory_format=torch.channels_last))
+    if ok and residual is not None:
+        ok = (residual.shape == x.shape and residual.dtype == x.dtype
+              and residual.is_contiguous(memory_format=torch.channels_last))
+    return ok
+
+
+def reference(x, residual, weight, bias, running_mean, running_var, training, momentum, eps,
+              relu):
+    """The PyTorch composition the kernels implement (CPU path and numerics reference)."""
+    y = F.batch_norm(x, running_mean, running_var, weight, bias, training, momentum, eps)
+    if residual is not None:
+        y = y + residual
+    return F.relu(y) if relu else y
+
+
+class _BNActFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum,
+                eps, relu):
+        ext = _ext.load()
+        y, mean, invstd = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
+                                     training, momentum, eps, relu)
+        ctx.save_for_backward(x, y, mean, invstd, weight)
+        ctx.relu, ctx.has_res, ctx.training = relu, residual is not None, training
+        ctx.affine = weight is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, y, mean, invstd, weight = ctx.saved_tensors
+        if not ctx.training:
+            raise RuntimeError("BatchNormAct2d backward in eval mode is not supported by the "
+                               "fused kernels; use train() or the PyTorch path")
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, y, x, mean, invstd, weight, ctx.relu,
+                                                     ctx.has_res, ctx.affine)
+        return (dx, dres if ctx.has_res else None, dgamma if ctx.affine else None,
+                dbeta if ctx.affine else None, None, None, None, None, None, None)
+
+
+def bn_act(x, residual=None, weight=None, bias=None, running_mean=None, running_var=None,
+           training=True, momentum=0.1, eps=1e-5, relu=True):
+    """Functional form of :class:`BatchNormAct2d`."""
+    if not kernel_ok(x, residual):
+        return reference(x, residual, weight, bias, running_mean, running_var, training,
+                         momentum, eps, relu)
+    return _BNActFn.apply(x, residual, weight, bias, running_mean, running_var, training,
+                          momentum, eps, relu)
+
+
+class BatchNormAct2d(nn.BatchNorm2d):
+    """``nn.BatchNorm2d`` + optional residual add + optional ReLU, fused on MI355X."""
+
+    def __init__(self, num_features: int, act: str = "relu", **kw):
+        super().__init__(num_features, **kw)
+        if act not in ("relu", "none"):
+            raise ValueError(f"act must be 'relu' or 'none', got {act!r}")
+        self.relu = act == "relu"
+
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+        training = self.training or not self.track_running_stats
+        if self.training and self.track_running_stats:
+            self.num_batches_tracked.add_(1)
+        mom = self.momentum if self.momentum is not None else \
+            1.0 / float(self.num_batches_tracked)
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        if not kernel_ok(x, residual) or (not training and torch.is_grad_enabled()
+                                           and x.requires_grad):
+            # layouts the kernels do not take, or eval with autograd on: the PyTorch path
+            return reference(x, residual, self.weight, self.bias, rm, rv, training, mom,
+                             self.eps, self.relu)
+        return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, training, mom,
+                              self.eps, self.relu)

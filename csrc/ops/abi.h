@@ -77,6 +77,28 @@ struct ArenaHead {
 };
 
 
+// Fused training BatchNorm (csrc/ops/bn_kernels.hip). Per-channel fp32 arrays of length C.
+struct ArenaBNStats {
+  float eps, momentum;
+  const float* gamma;     // optional (affine off -> 1)
+  const float* beta;      // optional (-> 0)
+  float* mean;            // out (training) / in (eval: running mean): batch mean
+  float* invstd;          // out: 1 / sqrt(biased var + eps)
+  float* scale;           // out (training) / in (eval): gamma * invstd
+  float* shift;           // out (training) / in (eval): beta;  y = (x - mean) * scale + shift
+  float* running_mean;    // optional, updated in place with momentum (unbiased variance)
+  float* running_var;
+};
+
+struct ArenaBNBwd {
+  const float* mean;      // saved batch statistics of the forward
+  const float* invstd;
+  const float* gamma;     // optional
+  float* dgamma;          // optional outputs
+  float* dbeta;
+  float* ca; float* cb; float* cc;  // workspace [C] each: dx = ca * (g - cb - (x - mean) * cc)
+};
+
 // Intra-node xGMI collective (csrc/ccl/xgmi_ccl.hip): every rank's registered buffers, mapped into
 // this process through hipIpc handles (buf[rank] / sig[rank] are the local allocations).
 #define ARENA_CCL_MAX_RANKS 8

@@ -43,6 +43,12 @@ hipError_t arena_ccl_adam(const ArenaXgmiPeers*, float*, float*, long long, Aren
                           ArenaCounterOp, hipStream_t);
 void arena_ccl_shard(long long, int, int, long long*, long long*);
 void arena_ccl_set_block_elems(long long);
+// csrc/ops/bn_kernels.hip
+long long arena_bn_workspace_floats(long long, int);
+hipError_t arena_bn_fwd(int, const void*, const void*, void*, long long, int, int, int, float*,
+                        ArenaBNStats, hipStream_t);
+hipError_t arena_bn_bwd(int, const void*, const void*, const void*, void*, void*, long long, int,
+                        int, float*, ArenaBNBwd, hipStream_t);
 #ifdef ARENA_TIMELINE
 hipError_t arena_timeline_read(long long*, int);
 #endif
@@ -565,6 +571,127 @@ std::vector<int64_t> ccl_shard(int64_t n, int64_t world, int64_t rank) {
   return {lo, hi};
 }
 
+// ---------------------------------------------------------------------- fused BatchNorm (NHWC)
+// Activations are [M][C] rows: a 4-D channels_last tensor (M = N*H*W) or a 2-D [M][C] tensor.
+struct BNGeom {
+  long long M;
+  int C;
+  int dtype;  // 0 f32, 1 bf16
+};
+
+BNGeom bn_geom(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 || t.scalar_type() == torch::kFloat32, name,
+              " must be bfloat16 or float32");
+  BNGeom g{};
+  if (t.dim() == 4) {
+    TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name,
+                " must be channels_last contiguous (NHWC)");
+    g.C = (int)t.size(1);
+  } else {
+    TORCH_CHECK(t.dim() == 2 && t.is_contiguous(), name, " must be 4-D NHWC or 2-D [M][C]");
+    g.C = (int)t.size(1);
+  }
+  g.M = g.C ? t.numel() / g.C : 0;
+  g.dtype = t.scalar_type() == torch::kBFloat16 ? 1 : 0;
+  TORCH_CHECK(arena_bn_workspace_floats(g.M, g.C) > 0, name, ": C=", g.C,
+              " unsupported (need C % 8 == 0, C <= 2048, C/8 dividing 256) or empty tensor");
+  return g;
+}
+
+void bn_same(const Tensor& a, const Tensor& b, const char* name) {
+  TORCH_CHECK(a.sizes() == b.sizes() && a.scalar_type() == b.scalar_type(), name,
+              " must match x in shape and dtype");
+  bn_geom(b, name);
+}
+
+const float* bn_vec(const OptT& t, int C, const char* name) {
+  if (!t.has_value()) return nullptr;
+  check_f32(*t, name);
+  TORCH_CHECK(t->numel() == C, name, " must have C=", C, " elements");
+  return t->data_ptr<float>();
+}
+
+// Returns (y, mean, invstd). Eval mode normalises with the running statistics.
+std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT running_mean,
+                           OptT running_var, bool training, double momentum, double eps,
+                           bool relu) {
+  const BNGeom g = bn_geom(x, "x");
+  if (res.has_value()) bn_same(x, *res, "residual");
+  auto f32 = x.options().dtype(torch::kFloat32);
+  Tensor mean = torch::empty({g.C}, f32), invstd = torch::empty({g.C}, f32);
+  Tensor scale = torch::empty({g.C}, f32), shift = torch::empty({g.C}, f32);
+  ArenaBNStats st{};
+  st.eps = (float)eps;
+  st.momentum = (float)momentum;
+  st.gamma = bn_vec(gamma, g.C, "weight");
+  st.beta = bn_vec(beta, g.C, "bias");
+  st.mean = mean.data_ptr<float>();
+  st.invstd = invstd.data_ptr<float>();
+  st.scale = scale.data_ptr<float>();
+  st.shift = shift.data_ptr<float>();
+  Tensor part;
+  if (training) {
+    if (running_mean.has_value() || running_var.has_value()) {
+      TORCH_CHECK(running_mean.has_value() && running_var.has_value(),
+                  "running_mean and running_var go together");
+      st.running_mean = const_cast<float*>(bn_vec(running_mean, g.C, "running_mean"));
+      st.running_var = const_cast<float*>(bn_vec(running_var, g.C, "running_var"));
+    }
+    part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
+  } else {
+    TORCH_CHECK(running_mean.has_value() && running_var.has_value(),
+                "eval-mode BatchNorm needs running statistics");
+    bn_vec(running_mean, g.C, "running_mean");
+    bn_vec(running_var, g.C, "running_var");
+    mean.copy_(*running_mean);
+    invstd.copy_(torch::rsqrt(*running_var + eps));
+    scale.copy_(gamma.has_value() ? *gamma * invstd : invstd);
+    if (beta.has_value()) shift.copy_(*beta); else shift.zero_();
+  }
+  Tensor y = torch::empty_like(x);
+  check_hip(arena_bn_fwd(g.dtype, x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr,
+                         y.data_ptr(), g.M, g.C, relu ? 1 : 0, training ? 1 : 0,
+                         training ? part.data_ptr<float>() : nullptr, st, cur_stream()),
+            "bn_fwd");
+  return {y, mean, invstd};
+}
+
+// Returns (dx, dres or empty, dgamma or empty, dbeta or empty).
+std::vector<Tensor> bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, OptT gamma,
+                           bool relu, bool with_res, bool affine_grads) {
+  const BNGeom g = bn_geom(x, "x");
+  bn_same(x, dy, "grad_output");
+  bn_same(x, y, "output");
+  check_f32(mean, "mean");
+  check_f32(invstd, "invstd");
+  TORCH_CHECK(mean.numel() == g.C && invstd.numel() == g.C, "saved statistics must have C elements");
+  auto f32 = x.options().dtype(torch::kFloat32);
+  Tensor co = torch::empty({3, g.C}, f32);
+  Tensor dgamma, dbeta;
+  ArenaBNBwd b{};
+  b.mean = mean.data_ptr<float>();
+  b.invstd = invstd.data_ptr<float>();
+  b.gamma = bn_vec(gamma, g.C, "weight");
+  if (affine_grads) {
+    dgamma = torch::empty({g.C}, f32);
+    dbeta = torch::empty({g.C}, f32);
+    b.dgamma = dgamma.data_ptr<float>();
+    b.dbeta = dbeta.data_ptr<float>();
+  }
+  b.ca = co.data_ptr<float>();
+  b.cb = b.ca + g.C;
+  b.cc = b.cb + g.C;
+  Tensor part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
+  Tensor dx = torch::empty_like(x);
+  Tensor dres = with_res ? torch::empty_like(x) : Tensor();
+  check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(), y.data_ptr(), x.data_ptr(), dx.data_ptr(),
+                         with_res ? dres.data_ptr() : nullptr, g.M, g.C, relu ? 1 : 0,
+                         part.data_ptr<float>(), b, cur_stream()),
+            "bn_bwd");
+  return {dx, dres, dgamma, dbeta};
+}
+
 class XgmiPeers {
  public:
   XgmiPeers(std::vector<int64_t> bufs, std::vector<int64_t> bufs2, std::vector<int64_t> sigs,
@@ -642,6 +769,8 @@ class XgmiPeers {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "arena_amd native HIP kernels (gfx950)";
   m.def("linear_fwd", &linear_fwd);
+  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_bwd", &bn_bwd);
   m.def("xent_head", &xent_head);
   m.def("mlp_fwd_logits", &mlp_fwd_logits);
   m.def("wgrad_grouped", &wgrad_grouped);

@@ -1,0 +1,537 @@
+// Fused training BatchNorm (+ residual add) (+ ReLU) for NHWC activations on gfx950 (MI355X).
+//
+// The ResNet workload of the Horovod demo family (arena_amd/examples/cnn_bench.py) spends more
+// than half of its GPU time outside the convolutions when BatchNorm, ReLU and the residual add
+// run as separate library/elementwise kernels (profiles/r1_resnet50_steady_kernels.csv: MIOpen
+// BN 34 %, elementwise 21 %). Every one of those ops is HBM-bound, so the win is in passes over
+// memory. Per BN layer these kernels make:
+//
+//   forward   stats      1 read of x            -> per-channel mean / invstd (+ running stats)
+//             apply      1 read of x (+ res), 1 write of y = act(x*scale + shift (+ res))
+//   backward  reduce     1 read of dy, y, x     -> dgamma, dbeta and the dx coefficients
+//             dx         1 read of dy, y, x, 1 write of dx (+ 1 write of dres = the masked dy)
+//
+// The ReLU mask comes from the saved output y (y > 0), so no mask tensor is stored. It is the
+// same y the next convolution keeps for its own backward.
+//
+// Layout: x is [M][C] with M = N*H*W (a channels_last tensor) and C % 8 == 0, C <= 2048.
+// A thread owns 8 consecutive channels: one 16-byte load for bf16, two for fp32.
+// A 256-thread block covers 256 / (C/8) rows per round.
+// Reductions:
+//   * per-thread Welford (stats) or plain fp32 sums (backward: x - mean uses the exact forward
+//     mean, so nothing cancels);
+//   * Chan merges across the block's row slots in LDS;
+//   * per-block partials in a workspace;
+//   * a finalize kernel with one block per 8 channels: 32 threads per channel merge strided
+//     subsets of the partials in fp64, then a 5-level LDS tree. A single "last block" doing
+//     the whole merge serially was latency-bound (hundreds of dependent L2 loads per channel)
+//     and cost more than the data passes themselves.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "abi.h"
+
+namespace {
+
+constexpr int kT = 256;      // threads per block
+constexpr int kVec = 8;      // channels per thread
+constexpr int kMaxC = 2048;  // C / kVec <= kT
+
+__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (NaN stays NaN)
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+// 8 channels of row `r`, group `g` (channels 8g..8g+7) as fp32.
+template <typename T>
+struct V8;
+template <>
+struct V8<uint16_t> {
+  static __device__ __forceinline__ void load(const uint16_t* p, float v[kVec]) {
+    const uint4 q = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {q.x, q.y, q.z, q.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(w[i] << 16);
+      v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  static __device__ __forceinline__ void store(uint16_t* p, const float v[kVec]) {
+    uint4 q;
+    q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    q.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    q.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = q;
+  }
+};
+template <>
+struct V8<float> {
+  static __device__ __forceinline__ void load(const float* p, float v[kVec]) {
+    const float4 a = *reinterpret_cast<const float4*>(p);
+    const float4 b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float v[kVec]) {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
+
+// 8 per-channel fp32 coefficients (two 16-byte loads; the arrays are tiny and stay in L1/L2)
+__device__ __forceinline__ void load8f(const float* p, float v[kVec]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+struct Geo {
+  int cg;    // channel groups (C / 8)
+  int rip;   // rows in parallel per block round
+  int g;     // this thread's channel group
+  int slot;  // this thread's row slot (active iff slot < rip)
+};
+__device__ __forceinline__ Geo geo(int C) {
+  Geo q;
+  q.cg = C / kVec;
+  q.rip = kT / q.cg;
+  q.g = threadIdx.x % q.cg;
+  q.slot = threadIdx.x / q.cg;
+  return q;
+}
+
+// Rows [r0, r1) of block b.
+__device__ __forceinline__ void block_rows(long long M, long long rpb, long long* r0,
+                                           long long* r1) {
+  *r0 = (long long)blockIdx.x * rpb;
+  *r1 = min(M, *r0 + rpb);
+}
+
+// ------------------------------------------------------------------------------------ stats
+// part: [nblk][2][C] (block mean, block M2)
+template <typename T>
+__global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, long long M, int C,
+                                                      long long rpb, float* __restrict__ part) {
+  const Geo q = geo(C);
+  long long r0, r1;
+  block_rows(M, rpb, &r0, &r1);
+  float mean[kVec], m2[kVec];
+#pragma unroll
+  for (int i = 0; i < kVec; ++i) mean[i] = m2[i] = 0.f;
+  float n = 0.f;
+  if (q.slot < q.rip) {
+    const T* base = x + (long long)q.g * kVec;
+    long long r = r0 + q.slot;
+    // 4 rows per step: all loads issued before the Welford updates
+    for (; r + 3LL * q.rip < r1; r += 4LL * q.rip) {
+      float v[4][kVec];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) V8<T>::load(base + (r + (long long)u * q.rip) * C, v[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        n += 1.f;
+        const float inv = 1.f / n;
+#pragma unroll
+        for (int i = 0; i < kVec; ++i) {
+          const float d = v[u][i] - mean[i];
+          mean[i] += d * inv;
+          m2[i] += d * (v[u][i] - mean[i]);
+        }
+      }
+    }
+    for (; r < r1; r += q.rip) {
+      float v[kVec];
+      V8<T>::load(base + r * C, v);
+      n += 1.f;
+      const float inv = 1.f / n;
+#pragma unroll
+      for (int i = 0; i < kVec; ++i) {
+        const float d = v[i] - mean[i];
+        mean[i] += d * inv;
+        m2[i] += d * (v[i] - mean[i]);
+      }
+    }
+  }
+  // Chan merge over the row slots of each channel group (LDS: [slot][C] mean, m2; [slot] n)
+  __shared__ float s_mean[kT * kVec], s_m2[kT * kVec], s_n[kT];
+  if (q.slot < q.rip) {
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      s_mean[q.slot * C + q.g * kVec + i] = mean[i];
+      s_m2[q.slot * C + q.g * kVec + i] = m2[i];
+    }
+    if (q.g == 0) s_n[q.slot] = n;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kT) {
+    float na = s_n[0], ma = s_mean[c], sa = s_m2[c];
+    for (int s = 1; s < q.rip; ++s) {
+      const float nb = s_n[s];
+      if (nb == 0.f) continue;
+      const float nab = na + nb;
+      const float d = s_mean[s * C + c] - ma;
+      ma += d * (nb / nab);
+      sa += s_m2[s * C + c] + d * d * (na * nb / nab);
+      na = nab;
+    }
+    part[(long long)blockIdx.x * 2 * C + c] = ma;
+    part[(long long)blockIdx.x * 2 * C + C + c] = sa;
+  }
+}
+
+// 8 channels per block; thread (j = t / 8, c = t % 8) merges partials j, j + 32, ... of channel
+// blockIdx.x * 8 + c in fp64, then the 32 per-thread results are merged by an LDS tree.
+constexpr int kFinCh = 8, kFinLanes = kT / kFinCh;
+
+__global__ __launch_bounds__(kT) void bn_stats_finalize_kernel(const float* __restrict__ part,
+                                                               int nblk, long long M, int C,
+                                                               long long rpb, ArenaBNStats out) {
+  const int cl = threadIdx.x % kFinCh, j = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  double na = 0.0, ma = 0.0, sa = 0.0;
+  if (c < C) {
+    for (int b = j; b < nblk; b += kFinLanes) {
+      const long long br0 = (long long)b * rpb;
+      const double nb = (double)(min(M, br0 + rpb) - br0);
+      if (nb <= 0.0) continue;
+      const double mb = part[(long long)b * 2 * C + c];
+      const double sb = part[(long long)b * 2 * C + C + c];
+      const double nab = na + nb;
+      const double d = mb - ma;
+      ma += d * (nb / nab);
+      sa += sb + d * d * (na * nb / nab);
+      na = nab;
+    }
+  }
+  __shared__ double s_n[kT], s_m[kT], s_s[kT];
+  s_n[threadIdx.x] = na; s_m[threadIdx.x] = ma; s_s[threadIdx.x] = sa;
+  __syncthreads();
+  for (int w = kFinLanes / 2; w > 0; w >>= 1) {
+    if (j < w) {
+      const int o = threadIdx.x + w * kFinCh;
+      const double nb = s_n[o];
+      if (nb > 0.0) {
+        const double n0 = s_n[threadIdx.x], m0 = s_m[threadIdx.x];
+        const double nab = n0 + nb, d = s_m[o] - m0;
+        s_m[threadIdx.x] = m0 + d * (nb / nab);
+        s_s[threadIdx.x] += s_s[o] + d * d * (n0 * nb / nab);
+        s_n[threadIdx.x] = nab;
+      }
+    }
+    __syncthreads();
+  }
+  if (j != 0 || c >= C) return;
+  na = s_n[cl]; ma = s_m[cl]; sa = s_s[cl];
+  const double var = sa / na;  // biased: what training normalises with
+  const float invstd = (float)(1.0 / sqrt(var + (double)out.eps));
+  out.mean[c] = (float)ma;
+  out.invstd[c] = invstd;
+  const float gam = out.gamma ? out.gamma[c] : 1.f;
+  const float bet = out.beta ? out.beta[c] : 0.f;
+  out.scale[c] = gam * invstd;
+  out.shift[c] = bet;  // y = (x - mean) * scale + shift: no cancellation when |mean| >> std
+  if (out.running_mean) {
+    const float mom = out.momentum;
+    out.running_mean[c] = (1.f - mom) * out.running_mean[c] + mom * (float)ma;
+    const double unbiased = na > 1.0 ? sa / (na - 1.0) : var;
+    out.running_var[c] = (1.f - mom) * out.running_var[c] + mom * (float)unbiased;
+  }
+}
+
+// ------------------------------------------------------------------------------------ apply
+// y = act((x - mean) * scale + shift (+ res)), 2 vectors per thread per round for load ILP.
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
+                                                      const T* __restrict__ res,
+                                                      T* __restrict__ y,
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
+                                                      long long nvec, int cg) {
+  const long long stride = (long long)gridDim.x * kT;
+  for (long long v0 = (long long)blockIdx.x * kT + threadIdx.x; v0 < nvec; v0 += 2 * stride) {
+    float a[2][kVec], b[2][kVec];
+    bool ok[2];
+    long long vv[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      vv[u] = v0 + u * stride;
+      ok[u] = vv[u] < nvec;
+      const long long vc = ok[u] ? vv[u] : v0;
+      V8<T>::load(x + vc * kVec, a[u]);
+      if (RES) V8<T>::load(res + vc * kVec, b[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int c0 = (int)(vv[u] & (cg - 1)) * kVec;  // cg is a power of two (host-checked)
+      float mu[kVec], sc[kVec], sh[kVec];
+      load8f(mean + c0, mu);
+      load8f(scale + c0, sc);
+      load8f(shift + c0, sh);
+      float o[kVec];
+#pragma unroll
+      for (int i = 0; i < kVec; ++i) {
+        float t = fmaf(a[u][i] - mu[i], sc[i], sh[i]);
+        if (RES) t += b[u][i];
+        o[i] = RELU ? fmaxf(t, 0.f) : t;
+      }
+      if (ok[u]) V8<T>::store(y + vv[u] * kVec, o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- backward sums
+// g = RELU ? dy * (y > 0) : dy;  per channel: sum g, sum g * (x - mean).  part: [nblk][2][C]
+template <typename T, bool RELU>
+__global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__ dy,
+                                                           const T* __restrict__ y,
+                                                           const T* __restrict__ x, long long M,
+                                                           int C, long long rpb,
+                                                           float* __restrict__ part,
+                                                           ArenaBNBwd out) {
+  const Geo q = geo(C);
+  long long r0, r1;
+  block_rows(M, rpb, &r0, &r1);
+  float sg[kVec], sgx[kVec], mu[kVec];
+#pragma unroll
+  for (int i = 0; i < kVec; ++i) sg[i] = sgx[i] = 0.f;
+  if (q.slot < q.rip) {
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) mu[i] = out.mean[q.g * kVec + i];
+    const long long off = (long long)q.g * kVec;
+    long long r = r0 + q.slot;
+    for (; r + q.rip < r1; r += 2LL * q.rip) {  // 2 rows per step: 6 loads in flight
+      float d[2][kVec], h[2][kVec], v[2][kVec];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const long long p = (r + (long long)u * q.rip) * C + off;
+        V8<T>::load(dy + p, d[u]);
+        if (RELU) V8<T>::load(y + p, h[u]);
+        V8<T>::load(x + p, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < kVec; ++i) {
+          const float g = RELU ? (h[u][i] > 0.f ? d[u][i] : 0.f) : d[u][i];
+          sg[i] += g;
+          sgx[i] = fmaf(g, v[u][i] - mu[i], sgx[i]);
+        }
+    }
+    for (; r < r1; r += q.rip) {
+      float d[kVec], h[kVec], v[kVec];
+      const long long p = r * C + off;
+      V8<T>::load(dy + p, d);
+      if (RELU) V8<T>::load(y + p, h);
+      V8<T>::load(x + p, v);
+#pragma unroll
+      for (int i = 0; i < kVec; ++i) {
+        const float g = RELU ? (h[i] > 0.f ? d[i] : 0.f) : d[i];
+        sg[i] += g;
+        sgx[i] = fmaf(g, v[i] - mu[i], sgx[i]);
+      }
+    }
+  }
+  __shared__ float s_g[kT * kVec], s_gx[kT * kVec];
+  if (q.slot < q.rip) {
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      s_g[q.slot * C + q.g * kVec + i] = sg[i];
+      s_gx[q.slot * C + q.g * kVec + i] = sgx[i];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += kT) {
+    float a = 0.f, b = 0.f;
+    for (int s = 0; s < q.rip; ++s) {
+      a += s_g[s * C + c];
+      b += s_gx[s * C + c];
+    }
+    part[(long long)blockIdx.x * 2 * C + c] = a;
+    part[(long long)blockIdx.x * 2 * C + C + c] = b;
+  }
+}
+
+__global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const float* __restrict__ part,
+                                                             int nblk, long long M, int C,
+                                                             ArenaBNBwd out) {
+  const int cl = threadIdx.x % kFinCh, j = threadIdx.x / kFinCh;
+  const int c = blockIdx.x * kFinCh + cl;
+  double a = 0.0, b = 0.0;
+  if (c < C) {
+    for (int blk = j; blk < nblk; blk += kFinLanes) {
+      a += part[(long long)blk * 2 * C + c];
+      b += part[(long long)blk * 2 * C + C + c];
+    }
+  }
+  __shared__ double s_a[kT], s_b[kT];
+  s_a[threadIdx.x] = a; s_b[threadIdx.x] = b;
+  __syncthreads();
+  for (int w = kFinLanes / 2; w > 0; w >>= 1) {
+    if (j < w) {
+      s_a[threadIdx.x] += s_a[threadIdx.x + w * kFinCh];
+      s_b[threadIdx.x] += s_b[threadIdx.x + w * kFinCh];
+    }
+    __syncthreads();
+  }
+  if (j != 0 || c >= C) return;
+  a = s_a[cl]; b = s_b[cl];
+  const float invstd = out.invstd[c];
+  const float gam = out.gamma ? out.gamma[c] : 1.f;
+  if (out.dgamma) out.dgamma[c] = (float)(b * invstd);
+  if (out.dbeta) out.dbeta[c] = (float)a;
+  // dx = gamma*invstd * (g - sum_g/M - (x - mean) * invstd^2 * sum_gx/M)
+  out.ca[c] = gam * invstd;
+  out.cb[c] = (float)(a / (double)M);
+  out.cc[c] = (float)(b / (double)M) * invstd * invstd;
+}
+
+// --------------------------------------------------------------------------------- backward dx
+template <typename T, bool RELU, bool RES>
+__global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
+                                                       const T* __restrict__ y,
+                                                       const T* __restrict__ x,
+                                                       T* __restrict__ dx, T* __restrict__ dres,
+                                                       long long nvec, int cg, ArenaBNBwd co) {
+  const long long stride = (long long)gridDim.x * kT;
+  for (long long v = (long long)blockIdx.x * kT + threadIdx.x; v < nvec; v += stride) {
+    float d[kVec], h[kVec], xv[kVec];
+    V8<T>::load(dy + v * kVec, d);
+    if (RELU) V8<T>::load(y + v * kVec, h);
+    V8<T>::load(x + v * kVec, xv);
+    const int c0 = (int)(v & (cg - 1)) * kVec;
+    float ca[kVec], cb[kVec], cc[kVec], mu[kVec];
+    load8f(co.ca + c0, ca);
+    load8f(co.cb + c0, cb);
+    load8f(co.cc + c0, cc);
+    load8f(co.mean + c0, mu);
+    float g[kVec], o[kVec];
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      g[i] = RELU ? (h[i] > 0.f ? d[i] : 0.f) : d[i];
+      o[i] = ca[i] * (g[i] - cb[i] - (xv[i] - mu[i]) * cc[i]);
+    }
+    V8<T>::store(dx + v * kVec, o);
+    if (RES) V8<T>::store(dres + v * kVec, g);
+  }
+}
+
+// Blocks for a reduction over M rows: ~32 row rounds per thread, at most 512 partials.
+long long reduce_blocks(long long M, int C, long long* rpb) {
+  const int rip = kT / (C / kVec);
+  long long rounds = (M + rip - 1) / rip;
+  long long nb = (rounds + 31) / 32;
+  nb = nb < 1 ? 1 : (nb > 512 ? 512 : nb);
+  long long r = (M + nb - 1) / nb;
+  r = (r + rip - 1) / rip * rip;  // whole rounds per block
+  *rpb = r;
+  return (M + r - 1) / r;
+}
+
+int elementwise_blocks(long long nvec) {
+  long long b = (nvec + 2LL * kT - 1) / (2LL * kT);
+  return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+}
+
+bool bad_shape(long long M, int C) {
+  return M <= 0 || C <= 0 || C % kVec != 0 || C > kMaxC || (kT % (C / kVec)) != 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+long long arena_bn_workspace_floats(long long M, int C) {
+  if (bad_shape(M, C)) return 0;
+  long long rpb;
+  return reduce_blocks(M, C, &rpb) * 2LL * C;
+}
+
+// dtype: 0 = f32, 1 = bf16 (all activation tensors share it)
+hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, long long M, int C,
+                        int relu, int training, float* part, ArenaBNStats st,
+                        hipStream_t stream) {
+  if (bad_shape(M, C)) return hipErrorInvalidValue;
+  if (training) {
+    long long rpb;
+    const long long nb = reduce_blocks(M, C, &rpb);
+    if (dtype == 1)
+      hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb), dim3(kT), 0, stream,
+                         static_cast<const uint16_t*>(x), M, C, rpb, part);
+    else
+      hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kT), 0, stream,
+                         static_cast<const float*>(x), M, C, rpb, part);
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kT), 0,
+                       stream, part, (int)nb, M, C, rpb, st);
+  }
+  const long long nvec = M * (C / kVec);
+  const int nb = elementwise_blocks(nvec);
+  const int cg = C / kVec;
+#define ARENA_BN_APPLY(TT, R, S)                                                             \
+  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S>), dim3(nb), dim3(kT), 0, stream,           \
+                     static_cast<const TT*>(x), static_cast<const TT*>(res), static_cast<TT*>(y), \
+                     st.mean, st.scale, st.shift, nvec, cg)
+  const bool r = relu != 0, s = res != nullptr;
+  if (dtype == 1) {
+    if (r && s) ARENA_BN_APPLY(uint16_t, true, true);
+    else if (r) ARENA_BN_APPLY(uint16_t, true, false);
+    else if (s) ARENA_BN_APPLY(uint16_t, false, true);
+    else ARENA_BN_APPLY(uint16_t, false, false);
+  } else {
+    if (r && s) ARENA_BN_APPLY(float, true, true);
+    else if (r) ARENA_BN_APPLY(float, true, false);
+    else if (s) ARENA_BN_APPLY(float, false, true);
+    else ARENA_BN_APPLY(float, false, false);
+  }
+#undef ARENA_BN_APPLY
+  return hipGetLastError();
+}
+
+hipError_t arena_bn_bwd(int dtype, const void* dy, const void* y, const void* x, void* dx,
+                        void* dres, long long M, int C, int relu, float* part,
+                        ArenaBNBwd co, hipStream_t stream) {
+  if (bad_shape(M, C)) return hipErrorInvalidValue;
+  long long rpb;
+  const long long nb = reduce_blocks(M, C, &rpb);
+#define ARENA_BN_RED(TT, R)                                                                  \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, R>), dim3(nb), dim3(kT), 0, stream,         \
+                     static_cast<const TT*>(dy), static_cast<const TT*>(y),                 \
+                     static_cast<const TT*>(x), M, C, rpb, part, co)
+  if (dtype == 1) {
+    if (relu) ARENA_BN_RED(uint16_t, true); else ARENA_BN_RED(uint16_t, false);
+  } else {
+    if (relu) ARENA_BN_RED(float, true); else ARENA_BN_RED(float, false);
+  }
+#undef ARENA_BN_RED
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kT), 0, stream,
+                     part, (int)nb, M, C, co);
+  const long long nvec = M * (C / kVec);
+  long long ne = (nvec + kT - 1) / kT;
+  ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);
+  const int cg = C / kVec;
+#define ARENA_BN_DX(TT, R, S)                                                                \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S>), dim3(ne), dim3(kT), 0, stream,          \
+                     static_cast<const TT*>(dy), static_cast<const TT*>(y),                 \
+                     static_cast<const TT*>(x), static_cast<TT*>(dx), static_cast<TT*>(dres), \
+                     nvec, cg, co)
+  const bool r = relu != 0, s = dres != nullptr;
+  if (dtype == 1) {
+    if (r && s) ARENA_BN_DX(uint16_t, true, true);
+    else if (r) ARENA_BN_DX(uint16_t, true, false);
+    else if (s) ARENA_BN_DX(uint16_t, false, true);
+    else ARENA_BN_DX(uint16_t, false, false);
+  } else {
+    if (r && s) ARENA_BN_DX(float, true, true);
+    else if (r) ARENA_BN_DX(float, true, false);
+    else if (s) ARENA_BN_DX(float, false, true);
+    else ARENA_BN_DX(float, false, false);
+  }
+#undef ARENA_BN_DX
+  return hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,124 @@
+"""Fused BatchNorm(+residual)(+ReLU) HIP kernels vs an fp32 PyTorch reference (F.batch_norm).
+
+Checks forward output, batch statistics / running-stat updates, eval mode, and the backward
+gradients (dx, residual grad, dgamma, dbeta) for fp32 and bf16 NHWC tensors. Reference = the same
+composition in fp32 on the (bf16-rounded) inputs, through autograd.
+"""
+from __future__ import annotations
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(4, 64, 14, 14), (2, 256, 7, 7), (8, 32, 9, 11), (3, 2048, 3, 3), (2, 8, 5, 5),
+          (16, 64, 56, 56)]
+
+
+def _ref(x, res, w, b, rm, rv, relu, training=True, mom=0.1, eps=1e-5):
+    y = F.batch_norm(x, rm, rv, w, b, training, mom, eps)
+    if res is not None:
+        y = y + res
+    return F.relu(y) if relu else y
+
+
+def _nhwc(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.parametrize("shape", SHAPES)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mode", ["relu", "relu_res", "plain"])
+def test_bn_act_fwd_bwd(shape, dtype, mode):
+    from arena_amd.ops.batchnorm import BatchNormAct2d
+    torch.manual_seed(0)
+    N, C, H, W = shape
+    relu, with_res = mode != "plain", mode == "relu_res"
+    x = _nhwc((torch.randn(shape, device="cuda") * 2 + 0.5).to(dtype))
+    res = _nhwc(torch.randn(shape, device="cuda").to(dtype)) if with_res else None
+    m = BatchNormAct2d(C, act="relu" if relu else "none").cuda()
+    with torch.no_grad():
+        m.weight.copy_(torch.rand(C, device="cuda") + 0.5)
+        m.bias.copy_(torch.randn(C, device="cuda") * 0.1)
+    rm0, rv0 = m.running_mean.clone(), m.running_var.clone()
+    xk = x.detach().clone().requires_grad_(True)
+    rk = res.detach().clone().requires_grad_(True) if with_res else None
+    y = m(xk, rk)
+    assert y.dtype == dtype and y.is_contiguous(memory_format=torch.channels_last)
+    # reference in fp32 from the same (rounded) inputs
+    xr = x.detach().float().requires_grad_(True)
+    rr = res.detach().float().requires_grad_(True) if with_res else None
+    wr = m.weight.detach().clone().requires_grad_(True)
+    br = m.bias.detach().clone().requires_grad_(True)
+    rmr, rvr = rm0.clone(), rv0.clone()
+    yr = _ref(xr, rr, wr, br, rmr, rvr, relu)
+    tol = dict(rtol=1e-4, atol=1e-4) if dtype == torch.float32 else dict(rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(y.float(), yr, **tol)
+    torch.testing.assert_close(m.running_mean, rmr, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(m.running_var, rvr, rtol=1e-4, atol=1e-5)
+    # backward
+    g = _nhwc(torch.randn(shape, device="cuda").to(dtype))
+    y.backward(g)
+    yr.backward(g.float())
+    gtol = dict(rtol=2e-3, atol=2e-3) if dtype == torch.float32 else dict(rtol=5e-2, atol=5e-2)
+    torch.testing.assert_close(xk.grad.float(), xr.grad, **gtol)
+    if with_res:
+        torch.testing.assert_close(rk.grad.float(), rr.grad, **gtol)
+    scale = max(1.0, float(wr.grad.abs().max()))
+    torch.testing.assert_close(m.weight.grad / scale, wr.grad / scale, **gtol)
+    scale = max(1.0, float(br.grad.abs().max()))
+    torch.testing.assert_close(m.bias.grad / scale, br.grad / scale, **gtol)
+
+
+def test_bn_statistics_robust_to_large_mean():
+    """Welford + Chan merges: a large common offset must not destroy the variance."""
+    from arena_amd.ops.batchnorm import BatchNormAct2d
+    torch.manual_seed(1)
+    # E[x^2] - E[x]^2 in fp32 would lose the unit variance under the 1e6 mean square
+    x = _nhwc(torch.randn(32, 64, 28, 28, device="cuda") + 1000.0)
+    m = BatchNormAct2d(64, act="none").cuda()
+    y = m(x)
+    yr = F.batch_norm(x.double(), None, None, m.weight.double(), m.bias.double(), True, 0.1, 1e-5)
+    torch.testing.assert_close(y.double(), yr, rtol=1e-3, atol=1e-3)
+
+
+def test_bn_eval_mode_uses_running_stats():
+    from arena_amd.ops.batchnorm import BatchNormAct2d
+    torch.manual_seed(2)
+    m = BatchNormAct2d(128, act="relu").cuda()
+    with torch.no_grad():
+        m.running_mean.copy_(torch.randn(128, device="cuda"))
+        m.running_var.copy_(torch.rand(128, device="cuda") + 0.5)
+    m.eval()
+    x = _nhwc(torch.randn(4, 128, 8, 8, device="cuda"))
+    with torch.no_grad():
+        y = m(x)
+    yr = _ref(x, None, m.weight, m.bias, m.running_mean, m.running_var, True, training=False)
+    torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-5)
+
+
+def test_resnet_tiny_bf16_step_uses_fused_bn():
+    """The model's BN layers take the kernel path under autocast + channels_last."""
+    from arena_amd.models.resnet import resnet
+    from arena_amd.ops import batchnorm
+    calls = {"n": 0}
+    orig = batchnorm._BNActFn.apply
+
+    def counting(*a):
+        calls["n"] += 1
+        return orig(*a)
+
+    batchnorm._BNActFn.apply = counting
+    try:
+        m = resnet("resnet_tiny", num_classes=10, width=16).cuda().to(
+            memory_format=torch.channels_last)
+        x = _nhwc(torch.randn(4, 3, 64, 64, device="cuda"))
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(m(x), torch.randint(0, 10, (4,), device="cuda"))
+        loss.backward()
+    finally:
+        batchnorm._BNActFn.apply = orig
+    n_bn = sum(1 for mod in m.modules() if isinstance(mod, batchnorm.BatchNormAct2d))
+    assert calls["n"] == n_bn and torch.isfinite(loss)
+    assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)

@@ -37,7 +37,7 @@ def _worker(rank, world, port, q):
         for _ in range(3):
             cnn_bench.train_step(model, opt, x, y, None)
         flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
-        q.put((rank, flat, len(opt.buckets)))
+        q.put((rank, flat.numpy(), len(opt.buckets)))   # by value: the child may exit first
     finally:
         hvd.shutdown()
 
@@ -73,6 +73,7 @@ def test_resnet_dp_world2_matches_mean_gradient():
         p.join(30)
         assert p.exitcode == 0
     (_, f0, nb), (_, f1, _) = res
+    f0, f1 = torch.from_numpy(f0), torch.from_numpy(f1)
     assert nb > 1                                   # several fusion buckets in flight
     assert torch.equal(f0, f1)                      # replicas identical
     torch.testing.assert_close(f0, _reference(world), rtol=2e-5, atol=2e-6)
