@@ -47,6 +47,9 @@ def parse(argv=None):
     ap.add_argument("--bucket_mb", type=float, default=64.0, help="Horovod fusion-buffer size")
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto")
     ap.add_argument("--device", default="auto")
+    ap.add_argument("--graph", type=int, default=1,
+                    help="1: capture the whole training step (fwd, bwd, optimizer) in one hipGraph "
+                         "and replay it (single rank; DP ranks run eagerly)")
     ap.add_argument("--json", action="store_true", help="print one JSON summary line at the end")
     return ap.parse_args(argv)
 
@@ -79,13 +82,26 @@ def build(args, dev, world):
     return model, opt, x, y
 
 
-def train_step(model, opt, x, y, amp_dtype):
-    with torch.autocast(device_type=x.device.type, dtype=amp_dtype, enabled=amp_dtype is not None):
+def train_step(model, opt, x, y, amp_dtype, zero_grad=True):
+    with torch.autocast(device_type=x.device.type, dtype=amp_dtype, enabled=amp_dtype is not None,
+                        cache_enabled=False):
         loss = F.cross_entropy(model(x), y)
-    opt.zero_grad(set_to_none=True)
+    if zero_grad:
+        opt.zero_grad(set_to_none=True)
     loss.backward()
     opt.step()
     return loss.detach()
+
+
+def capture_step(model, opt, x, y, amp_dtype):
+    """The whole step as one hipGraph: ~800 kernels per ResNet-50 step replay without host
+    launches or inter-kernel gaps. Gradients are None at capture, so the captured backward writes
+    (not accumulates) them, and every replay reuses the same memory (static x, y)."""
+    opt.zero_grad(set_to_none=True)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        loss = train_step(model, opt, x, y, amp_dtype, zero_grad=False)
+    return g, loss
 
 
 def main(argv=None) -> int:
@@ -109,7 +125,7 @@ def main(argv=None) -> int:
     if rank == 0:
         print(f"Model: {args.model}  Batch size: {args.batch_size} per device, "
               f"{args.batch_size * world} global  Devices: {world} x {dev.type}  "
-              f"Data: synthetic  dtype: {args.dtype}  comm: "
+              f"Data: synthetic  dtype: {args.dtype}  graph: {args.graph}  comm: "
               f"{getattr(opt, 'comm', 'none')}", flush=True)
     for i in range(args.num_warmup_batches):
         t = time.perf_counter()
@@ -119,13 +135,27 @@ def main(argv=None) -> int:
             print(f"warmup {i + 1}/{args.num_warmup_batches}: {time.perf_counter() - t:.2f} s",
                   flush=True)
     sync()
+    graph = None
+    if args.graph and world == 1 and dev.type == "cuda":
+        try:
+            graph, g_loss = capture_step(model, opt, x, y, amp)
+            graph.replay()  # one untimed replay: the step the capture recorded is now executed
+            sync()
+        except RuntimeError as e:  # capture refused by a library call: run eagerly
+            graph = None
+            if rank == 0:
+                print(f"hipGraph capture failed, running eagerly: {e}", flush=True)
     if world > 1:
         torch.distributed.barrier()
     sync()
     t0 = t_last = time.perf_counter()
     loss = None
     for i in range(1, args.num_batches + 1):
-        loss = train_step(model, opt, x, y, amp)
+        if graph is not None:
+            graph.replay()
+            loss = g_loss
+        else:
+            loss = train_step(model, opt, x, y, amp)
         if i % args.display_every == 0 or i == args.num_batches:
             sync()
             now = time.perf_counter()
@@ -151,6 +181,7 @@ def main(argv=None) -> int:
                               "ms_per_step": round(elapsed / args.num_batches * 1e3, 3),
                               "batch_per_device": args.batch_size, "devices": world,
                               "dtype": args.dtype, "comm": getattr(opt, "comm", "none"),
+                              "exec": "hipgraph" if graph is not None else "eager",
                               "final_loss": round(float(loss), 4)}), flush=True)
     hvd.shutdown()
     return 0

@@ -420,11 +420,14 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
   }
 }
 
-// Blocks for a reduction over M rows: ~32 row rounds per thread, at most 512 partials.
+// Blocks for a reduction over M rows: >= 8 row rounds per thread (the loops issue 4 or 2 rounds
+// of loads at once), as many blocks as that allows up to 512 partials. The 7x7 ResNet layers
+// (M = 6272) need the small per-thread share to fill the chip: at 32 rounds per thread they ran
+// 49 blocks and reached ~1 TB/s.
 long long reduce_blocks(long long M, int C, long long* rpb) {
   const int rip = kT / (C / kVec);
   long long rounds = (M + rip - 1) / rip;
-  long long nb = (rounds + 31) / 32;
+  long long nb = (rounds + 7) / 8;
   nb = nb < 1 ? 1 : (nb > 512 ? 512 : nb);
   long long r = (M + nb - 1) / nb;
   r = (r + rip - 1) / rip * rip;  // whole rounds per block
