@@ -73,6 +73,10 @@ def _add_common_flags(p: argparse.ArgumentParser) -> None:
     p.add_argument("--profile-gpu", dest="profile_gpu", action="store_true",
                    help="run the ranks under rocprofv3 --kernel-trace --stats; traces go to "
                         "<job dir>/traces/")
+    p.add_argument("--heartbeatTimeout", type=float, default=0.0,
+                   help="seconds without training progress (arena_amd.runtime.heartbeat beats) "
+                        "after which a rank counts as hung and is killed, so the retry policy "
+                        "applies; 0 disables")
     p.add_argument("command", nargs=argparse.REMAINDER, help="the training command")
 
 
@@ -102,6 +106,7 @@ def _fill_common(a: S.SubmitArgs, ns) -> S.SubmitArgs:
     a.data_dir_list = list(ns.dataDir)
     a.gpu_resource = ns.gpuResource
     a.profile_gpu = ns.profile_gpu
+    a.heartbeat_timeout = ns.heartbeatTimeout
     return a
 
 

@@ -15,6 +15,7 @@ from __future__ import annotations
 import copy
 from typing import Dict, List
 
+from ..runtime.heartbeat import liveness_probe
 from .objects import AMD_GPU
 
 ARENA_SYSTEM_NS = "arena-system"
@@ -91,6 +92,13 @@ def _container(name: str, values: dict, image: str, gpus: int, cpu="", memory=""
          "volumeMounts": list(mounts or [])}
     if ports:
         c["ports"] = ports
+    hb = float(values.get("heartbeatTimeout", 0) or 0)
+    if hb > 0 and name != "tensorboard":
+        # hang detection (arena_amd/runtime/heartbeat.py): the kubelet restarts a container
+        # whose training-progress file went stale
+        path = "/tmp/arena-heartbeat"
+        c["env"] = c["env"] + _env_list({"ARENA_HEARTBEAT_FILE": path})
+        c["livenessProbe"] = liveness_probe(path, hb)
     return c
 
 

@@ -386,13 +386,20 @@ class LocalBackend(Backend):
                         "environment": "cloud"}
                 env["TF_CONFIG"] = json.dumps(spec)
                 env["MX_CLUSTER_SPEC"] = env["TF_CONFIG"]
+            hb = ""
+            if float(values.get("heartbeatTimeout", 0) or 0) > 0 and not long_running:
+                os.makedirs(os.path.join(jd, "heartbeat"), exist_ok=True)
+                hb = os.path.join(jd, "heartbeat", p.name)
+                env["ARENA_HEARTBEAT_FILE"] = hb
             out_pods.append({"name": p.name, "role": role, "argv": argv, "env": env, "cwd": wd,
                              "log": os.path.join(jd, "logs", p.name + ".log"),
-                             "long_running": long_running})
+                             "long_running": long_running, "heartbeat": hb})
         plan = {"kind": kind, "retry": int(values.get("retry", 0)), "launcher": launcher,
                 "clean_pod_policy": values.get("cleanPodPolicy", "Running"),
                 "restart_policy": values.get("restartPolicy", "Never"),
-                "grace_s": float(values.get("gracePeriodSeconds", 5)), "pods": out_pods}
+                "grace_s": float(values.get("gracePeriodSeconds", 5)),
+                "heartbeat_timeout_s": float(values.get("heartbeatTimeout", 0) or 0),
+                "pods": out_pods}
         return plan, gpus, ports
 
     # ------------------------------------------------------------------------ release store

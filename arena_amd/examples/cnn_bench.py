@@ -26,6 +26,7 @@ import time
 import torch
 import torch.nn.functional as F
 
+from ..runtime import heartbeat
 from .common import pick_device, share_cpu_threads
 
 
@@ -156,6 +157,7 @@ def main(argv=None) -> int:
             loss = g_loss
         else:
             loss = train_step(model, opt, x, y, amp)
+        heartbeat.beat(i)
         if i % args.display_every == 0 or i == args.num_batches:
             sync()
             now = time.perf_counter()

@@ -101,6 +101,7 @@ class SubmitArgs:
     # MI355X-native placement/runtime knobs
     gpu_resource: str = AMD_GPU
     profile_gpu: bool = False
+    heartbeat_timeout: float = 0.0   # hang detection (0 = off), see arena_amd/runtime/heartbeat.py
 
     def check(self) -> None:
         if not self.name:
@@ -110,6 +111,8 @@ class SubmitArgs:
             raise ValidationError("--gpus must be >= 0")
         if self.retry < 0:
             raise ValidationError("--retry must be >= 0")
+        if self.heartbeat_timeout < 0:
+            raise ValidationError("--heartbeatTimeout must be >= 0")
 
     def transform(self) -> None:
         if self.data_dir_list:
@@ -131,11 +134,14 @@ class SubmitArgs:
         self.envs["gpus"] = str(self.gpu_count)
 
     def values(self) -> dict:
-        return {"image": self.image, "gpuCount": self.gpu_count, "envs": dict(self.envs),
-                "workingDir": self.working_dir, "command": self.command, "mode": self.mode,
-                "workers": self.workers, "retry": self.retry, "dataset": dict(self.dataset),
-                "dataDirs": copy.deepcopy(self.data_dirs), "gpuResource": self.gpu_resource,
-                "devices": ["/dev/kfd", "/dev/dri"], "profileGPU": self.profile_gpu}
+        v = {"image": self.image, "gpuCount": self.gpu_count, "envs": dict(self.envs),
+             "workingDir": self.working_dir, "command": self.command, "mode": self.mode,
+             "workers": self.workers, "retry": self.retry, "dataset": dict(self.dataset),
+             "dataDirs": copy.deepcopy(self.data_dirs), "gpuResource": self.gpu_resource,
+             "devices": ["/dev/kfd", "/dev/dri"], "profileGPU": self.profile_gpu}
+        if self.heartbeat_timeout > 0:
+            v["heartbeatTimeout"] = self.heartbeat_timeout
+        return v
 
 
 @dataclass

@@ -30,6 +30,7 @@ from typing import Optional
 import torch
 
 from .. import ops
+from ..runtime import heartbeat
 
 
 @dataclass
@@ -388,6 +389,7 @@ class FusedMLPTrainer:
                 self.steps_done += done
             if self.steps_done % spe == 0:
                 self._reshuffle()
+        heartbeat.beat(self.steps_done)  # progress for the runtime's hang detection
 
     # ------------------------------------------------------------------------------------------
     def recent_metrics(self, last: int = 100):

@@ -26,6 +26,7 @@ import torch
 import torch.distributed as dist
 
 from .. import ops
+from ..runtime import heartbeat
 
 _STATE = {"pg": None, "local_rank": 0, "local_size": 1}
 
@@ -281,7 +282,9 @@ class DistributedOptimizer:
 
     def step(self, closure=None):
         self.synchronize()
-        return self.opt.step(closure)
+        out = self.opt.step(closure)
+        heartbeat.beat()  # training progress: a rank hung in a collective stops beating
+        return out
 
     def zero_grad(self, set_to_none: bool = True):
         self.opt.zero_grad(set_to_none=set_to_none)

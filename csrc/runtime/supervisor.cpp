@@ -96,6 +96,7 @@ struct Pod {
   int restarts = 0;
   bool deleted = false;
   bool fault_done = false;
+  std::string heartbeat;  // progress file the pod touches (empty: no hang detection)
 };
 
 struct Plan {
@@ -105,6 +106,7 @@ struct Plan {
   std::string clean_pod_policy = "Running";
   std::string restart_policy = "Never";  // Never | OnFailure | ExitCode (tfjob)
   double grace_s = 5.0;
+  double heartbeat_timeout_s = 0;   // 0: off; else a pod silent this long after a beat is hung
   std::vector<Pod> pods;
 };
 
@@ -129,6 +131,7 @@ class Supervisor {
       reap();
       control();
       inject_fault();
+      watchdog();
       policy();
       if (g_stop) stop_all("Stopped");
       const double t = now_s();
@@ -165,6 +168,7 @@ class Supervisor {
     if (!j["clean_pod_policy"].as_str().empty()) plan_.clean_pod_policy = j["clean_pod_policy"].as_str();
     if (!j["restart_policy"].as_str().empty()) plan_.restart_policy = j["restart_policy"].as_str();
     plan_.grace_s = j["grace_s"].as_num(5.0);
+    plan_.heartbeat_timeout_s = j["heartbeat_timeout_s"].as_num(0.0);
     for (const auto& pj : j["pods"].elems()) {
       Pod p;
       p.name = pj["name"].as_str();
@@ -174,6 +178,7 @@ class Supervisor {
       p.cwd = pj["cwd"].as_str();
       p.log_path = pj["log"].as_str().empty() ? dir_ + "/logs/" + p.name + ".log" : pj["log"].as_str();
       p.long_running = pj["long_running"].as_bool(false);
+      p.heartbeat = pj["heartbeat"].as_str();
       plan_.pods.push_back(std::move(p));
     }
   }
@@ -198,6 +203,7 @@ class Supervisor {
       return;
     }
     if (!p.log) p.log = std::fopen(p.log_path.c_str(), "a");
+    if (!p.heartbeat.empty()) unlink(p.heartbeat.c_str());  // a restart starts unbeaten
     pid_t pid = fork();
     if (pid == 0) {
       // child: own process group (so the whole tree can be signalled), output into the pipe
@@ -376,6 +382,31 @@ class Supervisor {
       p->fault_done = true;
       kill(-p->pid, fault_sig_);
       message_ = "fault injected into " + p->name;
+    }
+  }
+
+  // Hang detection: a running pod that has beaten at least once (its heartbeat file exists) and
+  // has been silent for heartbeat_timeout_s is killed; the exit (137) then goes through the
+  // normal retry / gang-restart policy. Pods that never beat are not judged (no opt-in).
+  void watchdog() {
+    if (plan_.heartbeat_timeout_s <= 0) return;
+    const double t = now_s();
+    for (auto& p : plan_.pods) {
+      if (p.pid <= 0 || p.heartbeat.empty() || p.deleted) continue;
+      struct stat st;
+      if (stat(p.heartbeat.c_str(), &st) != 0) continue;
+      const double mt = st.st_mtim.tv_sec + st.st_mtim.tv_nsec * 1e-9;
+      const double silent = t - std::max(mt, p.start);
+      if (silent > plan_.heartbeat_timeout_s) {
+        char buf[160];
+        std::snprintf(buf, sizeof buf, "heartbeat timeout: %s made no progress for %.1f s",
+                      p.name.c_str(), silent);
+        message_ = buf;
+        log_line(p, std::string("arena-supervisor: ") + buf + "; killing it");
+        kill(-p.pid, SIGKILL);
+        unlink(p.heartbeat.c_str());
+        dirty_ = true;
+      }
     }
   }
 

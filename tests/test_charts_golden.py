@@ -120,3 +120,44 @@ def test_mpijob_properties():
         assert d["spec"]["template"]["spec"].get("hostIPC") is True
     assert "export RANK=0" in " ".join(_containers(job)[0]["command"])
     assert "HOSTNAME##*-" in " ".join(_containers(ss)[0]["command"])
+
+
+def test_heartbeat_timeout_renders_liveness_probe():
+    """--heartbeatTimeout: every training container gets the heartbeat file env and an exec
+    livenessProbe on its age; jobmon and TensorBoard stay unprobed (they never beat)."""
+    import subprocess
+    import tempfile
+    a = S.MPIJobArgs()
+    a.name, a.image, a.gpu_count, a.workers, a.heartbeat_timeout = "hb", "img", 1, 2, 30.0
+    a.prepare(["python", "train.py"])
+    docs = charts.render(a.chart, "hb", "default", a.values())
+    probed = 0
+    for d in docs:
+        if d["kind"] not in ("Job", "StatefulSet"):
+            continue
+        c = _containers(d)[0]
+        if d["metadata"]["name"].endswith("jobmon"):
+            assert "livenessProbe" not in c
+            continue
+        env = {e["name"]: e.get("value") for e in c["env"]}
+        assert env["ARENA_HEARTBEAT_FILE"] == "/tmp/arena-heartbeat"
+        probe = c["livenessProbe"]
+        assert probe["initialDelaySeconds"] == 30 and probe["failureThreshold"] == 1
+        probed += 1
+        # the probe script itself: passes with no file / a fresh file, fails on a stale one
+        script = probe["exec"]["command"][2]
+        with tempfile.TemporaryDirectory() as td:
+            f = os.path.join(td, "hb")
+            s = script.replace("/tmp/arena-heartbeat", f)
+            assert subprocess.run(["sh", "-c", s]).returncode == 0          # not started yet
+            open(f, "w").close()
+            assert subprocess.run(["sh", "-c", s]).returncode == 0          # fresh beat
+            os.utime(f, (0, 0))
+            assert subprocess.run(["sh", "-c", s]).returncode != 0          # stale: restart
+    assert probed == 2
+    # default: nothing rendered
+    b = S.MPIJobArgs()
+    b.name, b.image, b.workers = "nohb", "img", 2
+    b.prepare(["python", "train.py"])
+    assert all("livenessProbe" not in str(d) for d in charts.render(b.chart, "nohb", "default",
+                                                                     b.values()))

@@ -295,3 +295,42 @@ def test_profile_gpu_runs_ranks_under_rocprofv3(env, tmp_path, monkeypatch):
     traced = sorted(os.listdir(os.path.join(jd, "traces")))
     assert len(traced) == 2 and all(
         os.path.exists(os.path.join(jd, "traces", t, "run_kernel_stats.csv")) for t in traced)
+
+
+HANG_ONCE = """
+import os, sys, time
+from arena_amd.runtime import heartbeat
+heartbeat.configure(os.environ["ARENA_HEARTBEAT_FILE"], min_interval=0.05)
+marker = os.path.join(os.environ["ARENA_JOB_DIR"], "hung-once")
+first = not os.path.exists(marker)
+open(marker, "a").close()
+for step in range(10):
+    heartbeat.beat(step)
+    time.sleep(0.05)
+if first:
+    print("stuck in a collective", flush=True)
+    time.sleep(120)          # no more beats: the supervisor must kill this rank
+print("done", flush=True)
+"""
+
+
+def test_heartbeat_timeout_kills_hung_rank_and_retry_recovers(env, tmp_path):
+    script = tmp_path / "hang_once.py"
+    script.write_text(HANG_ONCE)
+    cli(env, "submit", "mpi", "--name", "hb", "--workers", "2", "--retry", "1",
+        "--heartbeatTimeout", "1.0", f"{PY} {script}")
+    st = wait_phase(env, "hb", timeout=90)
+    assert st["phase"] == "Succeeded" and st["attempts"] == 2, st
+    logs = "".join(open(os.path.join(env.job_dir("hb"), "logs", f)).read()
+                   for f in os.listdir(os.path.join(env.job_dir("hb"), "logs")))
+    assert "heartbeat timeout" in logs and logs.count("done") >= 2
+
+
+def test_heartbeat_timeout_without_retry_fails_job(env, tmp_path):
+    script = tmp_path / "hang.py"
+    script.write_text(HANG_ONCE)
+    cli(env, "submit", "sj", "--name", "hb2", "--heartbeatTimeout", "1.0", f"{PY} {script}")
+    st = wait_phase(env, "hb2", timeout=60)
+    assert st["phase"] == "Failed", st
+    pod = next(iter(st["pods"].values()))
+    assert pod["exit_code"] == 137
