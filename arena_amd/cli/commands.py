@@ -10,7 +10,7 @@ from __future__ import annotations
 import argparse
 import sys
 import time
-from typing import List, Optional
+from typing import List
 
 from .. import version as _version
 from ..cluster.backend import BackendError

@@ -19,7 +19,6 @@ import os
 import sys
 import time
 
-import numpy as np
 import torch
 
 from .common import default_log_dir, pick_device, share_cpu_threads

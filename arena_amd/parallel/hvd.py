@@ -20,7 +20,7 @@ to 32 MB: on a fully connected 8x MI355X node each ring hop is one ~153 GB/s xGM
 from __future__ import annotations
 
 import os
-from typing import Dict, Iterable, List, Optional, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
