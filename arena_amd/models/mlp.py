@@ -223,18 +223,20 @@ class FusedMLPTrainer:
         return self.perm.numel() // self.cfg.batch
 
     # ------------------------------------------------------------------------------------------
-    def _launch_step(self):
-        """Enqueue one training step (no host sync, graph-capturable)."""
+    def _launch_step(self, parity: int = -1):
+        """Enqueue one training step (no host sync, graph-capturable). ``parity`` = this step's
+        index & 1 when known at launch (lets the backward issue its logits loads without waiting
+        for the step counter); -1 = read it from the counter in-kernel."""
         if self.distributed:
             for part in range(3):
-                self._launch_step_part(part)
+                self._launch_step_part(part, parity)
             return
         if self.external_update:
             self._launch_fwd_head()
-            self._launch_wgrad(adam=False, commit=True)
+            self._launch_wgrad(adam=False, commit=True, parity=parity)
             return
         self._launch_fwd_head()
-        self._launch_wgrad(adam=True)
+        self._launch_wgrad(adam=True, parity=parity)
 
     def _launch_fwd_head(self):
         """Hidden layer + logits accumulation (one launch); writes B = A + 1."""
@@ -246,7 +248,7 @@ class FusedMLPTrainer:
                            seed=cfg.seed * 2654435761 + self.rank, step=A, ctr_dst=Bc,
                            ctr_src=A, ctr_add=1, rows=self.rows if self._rows_ahead else None)
 
-    def _launch_wgrad(self, adam: bool, commit: bool = False):
+    def _launch_wgrad(self, adam: bool, commit: bool = False, parity: int = -1):
         """Softmax-xent recomputed per workgroup from the logits; dW1 (dz via the W2 snapshot and
         the H mask) and dW2 in one launch. With ``adam`` the update is the epilogue (and A = B is
         committed), else the grads go to the flat all-reduce bucket."""
@@ -259,7 +261,8 @@ class FusedMLPTrainer:
                       head_loss_scale=1.0 / B, head_loss_acc=self.loss_hist,
                       head_correct_acc=self.corr_hist,
                       next_rows=self.rows if self._rows_ahead else None,
-                      next_rows_perm=self.perm if self._rows_ahead else None)
+                      next_rows_perm=self.perm if self._rows_ahead else None,
+                      head_parity=parity)
         xs, dzs = [self.xb, self.Hbuf], [None, None]
         if self._x_from_dataset:
             # gather the batch rows from the (never written) dataset instead of the forward's
@@ -281,10 +284,13 @@ class FusedMLPTrainer:
                               grad_scale=1.0, **ctr, **common)
 
     def _capture(self, nsteps: int) -> torch.cuda.CUDAGraph:
+        # an even-length graph replayed from an even step sees the same parity sequence every
+        # time, so the parity is baked into the launches (train_steps keeps replays even-aligned)
+        self._graph_static = nsteps % 2 == 0
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            for _ in range(nsteps):
-                self._launch_step()
+            for i in range(nsteps):
+                self._launch_step(parity=(i & 1) if self._graph_static else -1)
         return g
 
     def enable_graphs(self, steps_per_graph: int = 50) -> bool:
@@ -300,8 +306,8 @@ class FusedMLPTrainer:
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
-            for _ in range(2):
-                self._launch_step()
+            for k in range(2):
+                self._launch_step(parity=(self.steps_done + k) & 1)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
         for t, v in zip((self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2, self.rows),
@@ -341,12 +347,12 @@ class FusedMLPTrainer:
             torch.cuda.synchronize()
             return False
 
-    def _launch_step_part(self, part: int):
+    def _launch_step_part(self, part: int, parity: int = -1):
         """DP step in three parts: 0 = compute up to the grad bucket, 1 = all_reduce, 2 = Adam."""
         cfg, A, Bc = self.cfg, self.ctrA, self.ctrB
         if part == 0:
             self._launch_fwd_head()
-            self._launch_wgrad(adam=False)
+            self._launch_wgrad(adam=False, parity=parity)
         elif part == 1:
             if self.xgmi is not None:
                 return  # the reduction is fused into part 2
@@ -371,7 +377,8 @@ class FusedMLPTrainer:
             chunk = min(n, to_epoch_end)
             k = getattr(self, "steps_per_graph", 0)
             while chunk > 0:
-                if self._graphs and chunk >= k:
+                aligned = not getattr(self, "_graph_static", False) or self.steps_done % 2 == 0
+                if self._graphs and chunk >= k and aligned:
                     self._graphs[k].replay()
                     done = k
                 elif self.graph_mode == "split":
@@ -381,7 +388,7 @@ class FusedMLPTrainer:
                     post.replay()
                     done = 1
                 else:
-                    self._launch_step()
+                    self._launch_step(parity=self.steps_done & 1)
                     done = 1
                 chunk -= done
                 n -= done

@@ -77,12 +77,14 @@ def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Optional[Tensor]], outW: S
                   grad_scale: float = 1.0, tf_style: bool = False,
                   ctr_dst: Optional[Tensor] = None, ctr_src: Optional[Tensor] = None,
                   ctr_add: int = 0, next_rows: Optional[Tensor] = None,
-                  next_rows_perm: Optional[Tensor] = None) -> None:
+                  next_rows_perm: Optional[Tensor] = None, head_parity: int = -1) -> None:
     """dW_i = dz_iᵀ·gather(x_i), db_i = Σ_rows dz_i for up to 2 layers in one launch.
 
     Head modes (fused MLP step): every workgroup recomputes softmax-xent from ``head_logits2``
     (+ ``head_b2``, ``head_labels``); ``head_modes[i]`` 1 -> dz = dlogits (output layer),
     2 -> dz = (dlogits·head_w2[i]) ⊙ (head_h[i] > 0) / head_keep_prob (hidden layer).
+    ``head_parity`` 0/1 names this step's logits buffer at launch (it must equal the counter's
+    parity); -1 derives it from ``head_step`` in-kernel.
     mode 0 writes ``grad_scale * dW`` into ``outW`` (e.g. views of the flat all-reduce bucket);
     mode 1 applies Adam in place to parameters ``outW``/``outB`` with state ``mW,vW,mB,vB``.
     """
@@ -97,7 +99,7 @@ def wgrad_grouped(xs: Sequence[Tensor], dzs: Sequence[Optional[Tensor]], outW: S
         list(outW), list(outB), list(mW or none), list(vW or none), list(mB or none),
         list(vB or none), float(lr), lr_t, float(betas[0]), float(betas[1]), float(eps),
         float(weight_decay), t_step, float(grad_scale), bool(tf_style), ctr_dst, ctr_src,
-        int(ctr_add), next_rows, next_rows_perm)
+        int(ctr_add), next_rows, next_rows_perm, int(head_parity))
 
 
 def adam_flat(P: Tensor, M: Tensor, V: Tensor, G: Tensor, *, lr: float = 1e-3,

@@ -186,7 +186,11 @@ def wgrad_grouped(xs, x_scales, gather, idx, cursor, cursor_off, batch, dzs, hd_
                   hd_keep_prob, hd_logits2, hd_step, hd_step_off, hd_b2, hd_labels, hd_loss_scale,
                   hd_loss_acc, hd_correct_acc, mode, outW, outB, mW, vW, mB, vB, lr, lr_t, b1, b2,
                   eps, wd, t_step, grad_scale, tf_style, ctr_dst, ctr_src, ctr_add,
-                  next_rows=None, next_rows_perm=None):
+                  next_rows=None, next_rows_perm=None, hd_parity=-1):
+    if hd_parity >= 0:  # the launch-time parity must name the counter's buffer (kernel contract)
+        hs = int(hd_step.reshape(-1)[0].item()) + hd_step_off
+        if (hs & 1) != hd_parity:
+            raise AssertionError(f"head parity {hd_parity} does not match step {hs}")
     t = int(t_step.reshape(-1)[0].item()) if t_step is not None else 1
     lr_v = float(lr_t.reshape(-1)[0].item()) if lr_t is not None else lr
     dl = None

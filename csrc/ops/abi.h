@@ -66,6 +66,8 @@ struct ArenaHead {
   float* logits2;           // [2][M][C] Σ over hidden tiles of H·W2ᵀ (no bias)
   const long long* step;    // device step counter: (*step + step_off) = index of this step
   int step_off;
+  int parity;               // -1: buffer (*step + step_off) & 1; 0/1: known at launch, so the
+                            // logits loads need not wait for the step counter
   const float* b2;          // [C]
   int C;
   ArenaRowSource lab;       // labels (same gather as the layer input)

@@ -308,8 +308,9 @@ void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::ve
                    std::vector<OptT> vW, std::vector<OptT> mB, std::vector<OptT> vB, double lr,
                    OptT lr_t, double b1, double b2, double eps, double wd, OptT t_step,
                    double grad_scale, bool tf_style, OptT ctr_dst, OptT ctr_src, int64_t ctr_add,
-                   OptT next_rows, OptT next_rows_perm) {
+                   OptT next_rows, OptT next_rows_perm, int64_t hd_parity) {
   const size_t n = xs.size();
+  TORCH_CHECK(hd_parity >= -1 && hd_parity <= 1, "hd_parity must be -1 (from the counter), 0 or 1");
   TORCH_CHECK(n >= 1 && n <= 2, "wgrad_grouped: 1..2 problems");
   TORCH_CHECK(x_scales.size() == n && gather.size() == n && dzs.size() == n && outW.size() == n &&
                   outB.size() == n && hd_modes.size() == n && hd_w2.size() == n &&
@@ -413,6 +414,7 @@ void wgrad_grouped(std::vector<Tensor> xs, std::vector<double> x_scales, std::ve
     head.logits2 = hd_logits2->data_ptr<float>();
     head.step = opt_i64_scalar(hd_step, "hd_step");
     head.step_off = (int)hd_step_off;
+    head.parity = (int)hd_parity;
     head.C = (int)hd_logits2->size(-1);
     head.b2 = nullptr;
     if (hd_b2.has_value()) {

@@ -380,7 +380,8 @@ __device__ __forceinline__ int load_label(const ArenaRowSource& lab, long long p
 // >= 2 waves/SIMD so all 424 workgroups x 4 waves are co-resident in ONE round on 1024 SIMDs.
 // ---------------------------------------------------------------------------------------------
 // Per-problem compile-time specialisation. SPEC == 0: every property of the problem is read at run
-// time (generic path). Otherwise SPEC - 1 = xt | hd_mode << 1 | gather << 3 | mode << 4, so hipcc
+// time (generic path). Otherwise SPEC - 1 = xt | hd_mode << 1 | gather << 3 | mode << 4 |
+// static_parity << 5 (the head's logits buffer index comes from the launch, not the counter), so hipcc
 // sees straight-line code: no branch around a load, and every independent global load of the
 // chunk is issued before the first wait (measured with scripts/timeline.py: the generic path
 // drained vmcnt between the label, index, row and step loads).
@@ -389,11 +390,12 @@ struct WSpec {
   static constexpr bool known = SPEC != 0;
   static constexpr int s = SPEC - 1;
   static constexpr int xt = s & 1, hm = (s >> 1) & 3, gather = (s >> 3) & 1, mode = (s >> 4) & 1;
+  static constexpr bool sp = known && ((s >> 5) & 1);
 };
 
 
-constexpr int wgrad_spec(int xt, int hm, int gather, int mode) {
-  return 1 + xt + 2 * hm + 8 * gather + 16 * mode;
+constexpr int wgrad_spec(int xt, int hm, int gather, int mode, int sp = 0) {
+  return 1 + xt + 2 * hm + 8 * gather + 16 * mode + 32 * sp;
 }
 
 template <int CB, int SPEC, int LG, int LDT>  // CB: bound on head classes (C <= CB); LG: labels
@@ -526,12 +528,19 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
                      min(n0 + ((int)threadIdx.x & 15), P.N - 1)];
       }
       ARENA_TL(1, 9);
-      if (mc0 == 0) {  // first use of the step counter: every other load of the chunk is issued
-        if (ARENA_EXP & 16) hstep_raw = 7;
-        hstep = hstep_raw + HD.step_off;
-        logits = HD.logits2 + (long long)(hstep & 1) * P.M * HD.C;
-        ARENA_TL_DEP((int)hstep);
-        ARENA_TL(1, 1);
+      if (mc0 == 0) {
+        if constexpr (WS::sp) {
+          // buffer index known at launch: the logits loads go out now and the step counter is
+          // first waited for where the metric slot / next-step bookkeeping needs it
+          logits = HD.logits2 + (long long)HD.parity * P.M * HD.C;
+          ARENA_TL(1, 1);
+        } else {  // first use of the step counter: every other load of the chunk is issued
+          if (ARENA_EXP & 16) hstep_raw = 7;
+          hstep = hstep_raw + HD.step_off;
+          logits = HD.logits2 + (long long)(hstep & 1) * P.M * HD.C;
+          ARENA_TL_DEP((int)hstep);
+          ARENA_TL(1, 1);
+        }
       }
 #pragma unroll
       for (int i = 0; i < kDItems; ++i) {  // raw logits rows: item t -> (m = t>>4, c = t&15)
@@ -541,6 +550,7 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
       }
       ARENA_TL(1, 10);
       if (mc0 == 0 && (int)blockIdx.x == args.head_block) {  // zero the other buffer + next slot
+        if constexpr (WS::sp) hstep = hstep_raw + HD.step_off;  // this block only waits here
         float* nxt = HD.logits2 + (long long)((hstep + 1) & 1) * P.M * HD.C;
         for (int i = threadIdx.x; i < P.M * HD.C; i += 256) nxt[i] = 0.f;
         if (HD.nr_out != nullptr && (int)threadIdx.x < HD.nr_batch) {
@@ -1239,6 +1249,7 @@ hipError_t arena_wgrad_grouped(ArenaWGradProblem* probs, int nprob, ArenaAdam ad
   a.head = head;
   // the fused MLP step: problem 0 = u8 dataset rows + hidden head, problem 1 = f32 H + output head
   const bool g0 = probs[0].x.idx != nullptr;
+  const bool sp = head.parity == 0 || head.parity == 1;
   const bool mlp_pair = nprob == 2 && head.C <= 10 && probs[0].xt == 1 && probs[0].hd_mode == 2 &&
                         probs[1].xt == 0 && probs[1].hd_mode == 1 && probs[1].x.idx == nullptr &&
                         probs[0].mode == probs[1].mode && probs[0].M <= kMC &&
@@ -1247,15 +1258,21 @@ hipError_t arena_wgrad_grouped(ArenaWGradProblem* probs, int nprob, ArenaAdam ad
   const dim3 grid(blocks), block(256);
   if (mlp_pair) {
     const int m = probs[0].mode & 1;
-    constexpr int S1m0 = wgrad_spec(0, 1, 0, 0), S1m1 = wgrad_spec(0, 1, 0, 1);
-    if (g0 == 0 && m == 0)
-      hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, 0, 0), S1m0>), grid, block, 0, stream, a);
-    else if (g0 == 0 && m == 1)
-      hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, 0, 1), S1m1>), grid, block, 0, stream, a);
-    else if (g0 == 1 && m == 0)
-      hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, 1, 0), S1m0>), grid, block, 0, stream, a);
-    else
-      hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, 1, 1), S1m1>), grid, block, 0, stream, a);
+#define ARENA_WG_PAIR(G, M, SP)                                                                \
+  hipLaunchKernelGGL((wgrad_grouped_kernel<10, wgrad_spec(1, 2, G, M, SP),                     \
+                                           wgrad_spec(0, 1, 0, M, SP)>), grid, block, 0, stream, a)
+    if (sp) {
+      if (g0 == 0 && m == 0) ARENA_WG_PAIR(0, 0, 1);
+      else if (g0 == 0 && m == 1) ARENA_WG_PAIR(0, 1, 1);
+      else if (g0 == 1 && m == 0) ARENA_WG_PAIR(1, 0, 1);
+      else ARENA_WG_PAIR(1, 1, 1);
+    } else {
+      if (g0 == 0 && m == 0) ARENA_WG_PAIR(0, 0, 0);
+      else if (g0 == 0 && m == 1) ARENA_WG_PAIR(0, 1, 0);
+      else if (g0 == 1 && m == 0) ARENA_WG_PAIR(1, 0, 0);
+      else ARENA_WG_PAIR(1, 1, 0);
+    }
+#undef ARENA_WG_PAIR
   } else if (head.C <= 10) {
     hipLaunchKernelGGL((wgrad_grouped_kernel<10, 0, 0>), grid, block, 0, stream, a);
   } else {

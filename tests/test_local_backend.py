@@ -302,8 +302,11 @@ import os, sys, time
 from arena_amd.runtime import heartbeat
 heartbeat.configure(os.environ["ARENA_HEARTBEAT_FILE"], min_interval=0.05)
 marker = os.path.join(os.environ["ARENA_JOB_DIR"], "hung-once")
-first = not os.path.exists(marker)
-open(marker, "a").close()
+# the launcher (rank 0) hangs on the first attempt: a hung worker would just be reaped once the
+# launcher succeeds (jobmon semantics), which is not what this test is about
+first = os.environ.get("RANK", "0") == "0" and not os.path.exists(marker)
+if first:
+    open(marker, "a").close()
 for step in range(10):
     heartbeat.beat(step)
     time.sleep(0.05)

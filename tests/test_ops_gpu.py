@@ -114,7 +114,7 @@ def test_wgrad_grouped(cuda, mode):
                 [st[6], st[7]], 1e-3, None, 0.9, 0.999, 1e-8, 0.0, t, 0.5, False, A, t, 0)
         if impl == "hip":
             from arena_amd.ops import _ext
-            _ext.load().wgrad_grouped(*args, None, None)
+            _ext.load().wgrad_grouped(*args, None, None, -1)
         else:
             ref.wgrad_grouped(*args)
         torch.cuda.synchronize()
@@ -229,7 +229,8 @@ def test_mlp_fwd_logits_matches_reference(cuda, M, N, C):
 
 
 @pytest.mark.parametrize("mode", [0, 1])
-def test_wgrad_head_modes(cuda, mode):
+@pytest.mark.parametrize("parity", [-1, 1])  # from the counter / known at launch (step 5)
+def test_wgrad_head_modes(cuda, mode, parity):
     """Both layers' grads from raw logits (softmax recomputed per workgroup) vs the reference."""
     g = torch.Generator().manual_seed(10 + mode)
     M, N, K, C = 100, 500, 784, 10
@@ -263,9 +264,9 @@ def test_wgrad_head_modes(cuda, mode):
                 0)
         if impl == "hip":
             from arena_amd.ops import _ext
-            _ext.load().wgrad_grouped(*args, None, None)
+            _ext.load().wgrad_grouped(*args, None, None, parity)
         else:
-            ref.wgrad_grouped(*args)
+            ref.wgrad_grouped(*args, None, None, parity)
         torch.cuda.synchronize()
         res[impl] = (W1, W2, b1, b2, la, ca, lg2)
     h, r = res["hip"], res["ref"]

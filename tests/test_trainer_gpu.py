@@ -26,14 +26,16 @@ def test_fused_gpu_matches_cpu_reference(cuda, small_data):
     assert int(gpu.ctrA.item()) == 10 == int(cpu.ctrA.item())
 
 
-def test_graph_replay_equals_eager(cuda, small_data):
+@pytest.mark.parametrize("spg", [10, 5])  # even: launch-time logits parity; odd: from counter
+def test_graph_replay_equals_eager(cuda, small_data, spg):
     (x, y), _ = small_data
     cfg = MLPConfig(batch=100, seed=5)
     a = FusedMLPTrainer(cfg, x, y, device=cuda)
     b = FusedMLPTrainer(cfg, x, y, device=cuda)
     b.set_permutation(a.perm)
-    assert a.enable_graphs(10)
-    a.train_steps(20)
+    a.train_steps(1)              # odd start: the even-length graph must realign with one eager step
+    assert a.enable_graphs(spg)
+    a.train_steps(19)
     b.train_steps(20)
     torch.cuda.synchronize()
     # logits are accumulated with f32 atomics (order may differ run to run): equal to rounding,

@@ -129,14 +129,14 @@ def _trainer(rank, world, port, q):
         class GlooRef(FusedMLPTrainer):
             """Reference DP step: the flat gradient summed by gloo on the host."""
 
-            def _launch_step_part(self, part):
+            def _launch_step_part(self, part, parity=-1):
                 if part == 1:
                     torch.cuda.synchronize()
                     gh = self.G.cpu()
                     dist.all_reduce(gh)
                     self.G.copy_(gh)
                     return
-                super()._launch_step_part(part)
+                super()._launch_step_part(part, parity)
 
         tx = FusedMLPTrainer(cfg, x, y, device="cuda", process_group=dist.group.WORLD, rank=rank,
                              world=world, comm="xgmi")
