@@ -122,3 +122,24 @@ def test_resnet_tiny_bf16_step_uses_fused_bn():
     n_bn = sum(1 for mod in m.modules() if isinstance(mod, batchnorm.BatchNormAct2d))
     assert calls["n"] == n_bn and torch.isfinite(loss)
     assert all(torch.isfinite(p.grad).all() for p in m.parameters() if p.grad is not None)
+
+
+def test_cnn_bench_example_runs_with_graph_capture(tmp_path):
+    """The ResNet benchmark example end to end on the GPU (tiny ResNet): fused BN under bf16
+    autocast, whole-step hipGraph capture, tf_cnn_benchmarks-style output."""
+    import json
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, MIOPEN_FIND_MODE="FAST", ARENA_HEARTBEAT_FILE=str(tmp_path / "hb"))
+    r = subprocess.run([sys.executable, "-m", "arena_amd.examples.cnn_bench", "--model",
+                        "resnet_tiny", "--width", "16", "--image_size", "64", "--num_classes",
+                        "10", "--batch_size", "16", "--num_batches", "6",
+                        "--num_warmup_batches", "2", "--display_every", "3", "--json"],
+                       capture_output=True, text=True, timeout=240, env=env,
+                       cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "total images/sec:" in r.stdout
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["exec"] == "hipgraph" and res["images_per_s"] > 0
+    assert (tmp_path / "hb").exists()          # progress heartbeats were written
