@@ -507,10 +507,9 @@ class Supervisor {
     terminate_all(live);
   }
 
-  void publish(bool force) {
-    if (!dirty_ && !force) {
-      // heartbeat only
-    }
+  // Written on every change and, unchanged, at least once a second: the mtime/"heartbeat" field
+  // is how the CLI tells a live supervisor from a dead one.
+  void publish(bool /*force*/) {
     Json st = Json::object();
     st.set("supervisor_pid", (long long)getpid());
     st.set("heartbeat", now_s());
