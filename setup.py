@@ -22,7 +22,7 @@ if ARCH != "gfx950":
 HIP_SOURCES = ["csrc/ops/mlp_kernels.hip", "csrc/ops/bn_kernels.hip", "csrc/ccl/xgmi_ccl.hip"]
 # ARENA_TIMELINE=1: instrumented build for scripts/timeline.py (never the default)
 TIMELINE = ["-DARENA_TIMELINE"] if os.environ.get("ARENA_TIMELINE") == "1" else []
-if TIMELINE:  # experiment switches for instrumented builds only (scripts/perf_exp.sh)
+if TIMELINE:  # ARENA_EXP ablation switches, instrumented builds only (see scripts/timeline.py)
     TIMELINE += os.environ.get("ARENA_EXP_FLAGS", "").split()
 CPP_SOURCES = ["csrc/ops/bindings.cpp"]
 
