@@ -203,6 +203,36 @@ def _hvd_optimizer(rank, world, port, q):
         q.put((rank, None, traceback.format_exc()))
 
 
+def _rccl_capture(rank, world, port, q):
+    """The RCCL fallback of the DP step captures dist.all_reduce inside a hipGraph: check that
+    this torch/RCCL build supports it (a world-1 NCCL group: the collective still goes through
+    RCCL's enqueue/capture path)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",
+                          WORLD_SIZE="1", LOCAL_RANK="0")
+        torch.cuda.set_device(0)
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+        x = torch.arange(1024, device="cuda", dtype=torch.float32)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            dist.all_reduce(x)                         # communicator set up outside capture
+        torch.cuda.current_stream().wait_stream(s)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            x.mul_(2.0)
+            dist.all_reduce(x)
+        for _ in range(3):
+            g.replay()
+        torch.cuda.synchronize()
+        ok = bool(torch.equal(x, torch.arange(1024, device="cuda", dtype=torch.float32) * 8))
+        dist.destroy_process_group()
+        q.put((rank, {"ok": ok}, None))
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
 def _run(fn, world, timeout=240):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -251,3 +281,8 @@ def test_hvd_distributed_optimizer_xgmi_comm_stream():
     out = _run(_hvd_optimizer, 2)
     for r, res in out.items():
         assert res["diff"] < 1e-5, (r, res)
+
+
+def test_rccl_allreduce_is_graph_capturable():
+    out = _run(_rccl_capture, 1)
+    assert out[0]["ok"], out
