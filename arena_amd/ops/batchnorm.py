@@ -53,10 +53,10 @@ def reference(x, residual, weight, bias, running_mean, running_var, training, mo
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum,
-                eps, relu):
+                eps, relu, num_batches=None):
         ext = _ext.load()
         y, mean, invstd = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
-                                     training, momentum, eps, relu)
+                                     training, momentum, eps, relu, num_batches)
         ctx.save_for_backward(x, y, mean, invstd, weight)
         ctx.relu, ctx.has_res, ctx.training = relu, residual is not None, training
         ctx.affine = weight is not None
@@ -72,7 +72,7 @@ class _BNActFn(torch.autograd.Function):
         dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, y, x, mean, invstd, weight, ctx.relu,
                                                      ctx.has_res, ctx.affine)
         return (dx, dres if ctx.has_res else None, dgamma if ctx.affine else None,
-                dbeta if ctx.affine else None, None, None, None, None, None, None)
+                dbeta if ctx.affine else None, None, None, None, None, None, None, None)
 
 
 def bn_act(x, residual=None, weight=None, bias=None, running_mean=None, running_var=None,
@@ -96,14 +96,21 @@ class BatchNormAct2d(nn.BatchNorm2d):
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
         training = self.training or not self.track_running_stats
-        if self.training and self.track_running_stats:
+        tracking = self.training and self.track_running_stats
+        rm = self.running_mean if (not self.training or self.track_running_stats) else None
+        rv = self.running_var if (not self.training or self.track_running_stats) else None
+        fused = kernel_ok(x, residual) and not (not training and torch.is_grad_enabled()
+                                                and x.requires_grad)
+        if fused and training and self.momentum is not None:
+            # num_batches_tracked += 1 happens inside the statistics finalize kernel
+            return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, True,
+                                  self.momentum, self.eps, self.relu,
+                                  self.num_batches_tracked if tracking else None)
+        if tracking:
             self.num_batches_tracked.add_(1)
         mom = self.momentum if self.momentum is not None else \
             1.0 / float(self.num_batches_tracked)
-        rm = self.running_mean if (not self.training or self.track_running_stats) else None
-        rv = self.running_var if (not self.training or self.track_running_stats) else None
-        if not kernel_ok(x, residual) or (not training and torch.is_grad_enabled()
-                                           and x.requires_grad):
+        if not fused:
             # layouts the kernels do not take, or eval with autograd on: the PyTorch path
             return reference(x, residual, self.weight, self.bias, rm, rv, training, mom,
                              self.eps, self.relu)

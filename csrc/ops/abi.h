@@ -90,6 +90,7 @@ struct ArenaBNStats {
   float* shift;           // out (training) / in (eval): beta;  y = (x - mean) * scale + shift
   float* running_mean;    // optional, updated in place with momentum (unbiased variance)
   float* running_var;
+  long long* batches;     // optional nn.BatchNorm num_batches_tracked, += 1 by the finalize kernel
 };
 
 struct ArenaBNBwd {

@@ -617,7 +617,7 @@ const float* bn_vec(const OptT& t, int C, const char* name) {
 // Returns (y, mean, invstd). Eval mode normalises with the running statistics.
 std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT running_mean,
                            OptT running_var, bool training, double momentum, double eps,
-                           bool relu) {
+                           bool relu, OptT num_batches) {
   const BNGeom g = bn_geom(x, "x");
   if (res.has_value()) bn_same(x, *res, "residual");
   auto f32 = x.options().dtype(torch::kFloat32);
@@ -639,6 +639,12 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
                   "running_mean and running_var go together");
       st.running_mean = const_cast<float*>(bn_vec(running_mean, g.C, "running_mean"));
       st.running_var = const_cast<float*>(bn_vec(running_var, g.C, "running_var"));
+    }
+    if (num_batches.has_value()) {
+      check_dev(*num_batches, "num_batches_tracked");
+      TORCH_CHECK(num_batches->scalar_type() == torch::kInt64 && num_batches->numel() == 1,
+                  "num_batches_tracked must be an int64 scalar tensor");
+      st.batches = reinterpret_cast<long long*>(num_batches->data_ptr<int64_t>());
     }
     part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
   } else {

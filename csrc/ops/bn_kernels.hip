@@ -192,6 +192,8 @@ __global__ __launch_bounds__(kT) void bn_stats_finalize_kernel(const float* __re
                                                                long long rpb, ArenaBNStats out) {
   const int cl = threadIdx.x % kFinCh, j = threadIdx.x / kFinCh;
   const int c = blockIdx.x * kFinCh + cl;
+  // the module's batch counter rides along (one launch fewer per BN layer than a separate add)
+  if (out.batches != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *out.batches += 1;
   double na = 0.0, ma = 0.0, sa = 0.0;
   if (c < C) {
     for (int b = j; b < nblk; b += kFinLanes) {

@@ -57,6 +57,7 @@ def test_bn_act_fwd_bwd(shape, dtype, mode):
     torch.testing.assert_close(y.float(), yr, **tol)
     torch.testing.assert_close(m.running_mean, rmr, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(m.running_var, rvr, rtol=1e-4, atol=1e-5)
+    assert int(m.num_batches_tracked) == 1          # incremented by the finalize kernel
     # backward
     g = _nhwc(torch.randn(shape, device="cuda").to(dtype))
     y.backward(g)
