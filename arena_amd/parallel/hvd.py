@@ -152,6 +152,18 @@ def broadcast_optimizer_state(optimizer: torch.optim.Optimizer, root_rank: int =
     broadcast_parameters(state, root_rank)
 
 
+def _raw(t: torch.Tensor) -> Optional[torch.Tensor]:
+    """1-D view of a dense tensor's memory: contiguous, or channels_last (NHWC conv weights and
+    their gradients). Averaging is elementwise and every rank has the same layout for the same
+    parameter, so buckets can hold the memory order directly (no layout copies). None for any
+    other stride pattern."""
+    if t.is_contiguous():
+        return t.view(-1)
+    if t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last):
+        return t.permute(0, 2, 3, 1).reshape(-1)  # NHWC order == memory order: a view
+    return None
+
+
 class _Bucket:
     def __init__(self, params: List[torch.nn.Parameter], device):
         self.params = params
@@ -236,7 +248,7 @@ class DistributedOptimizer:
 
     def _launch(self, b: _Bucket) -> None:
         grads = [p.grad if p.grad is not None else torch.zeros_like(p) for p in b.params]
-        grads = [g.contiguous() for g in grads]
+        grads = [r if (r := _raw(g)) is not None else g.contiguous().view(-1) for g in grads]
         if self.xgmi is not None:
             # pack straight into the registered staging buffer (zero-copy input), average on the
             # way out. Comm stream: waits for the grads (event), then buckets run in launch order,
@@ -271,12 +283,18 @@ class DistributedOptimizer:
             torch.cuda.current_stream().wait_stream(self._stream)
         for b in self.buckets:
             b.work.wait()
-            grads = []
+            grads, strided = [], []
             for p in b.params:
                 if p.grad is None:
                     p.grad = torch.zeros_like(p)
-                grads.append(p.grad)
+                r = _raw(p.grad)
+                if r is None:  # exotic strides: unpack in logical order, then copy in
+                    r = torch.empty(p.numel(), device=p.device, dtype=p.grad.dtype)
+                    strided.append((p.grad, r))
+                grads.append(r)
             ops.unflatten_from(grads, b.offsets, b.flat, inv)
+            for g, r in strided:
+                g.copy_(r.view(g.shape))
             b.work = None
             b.pending = set(id(p) for p in b.params)
 

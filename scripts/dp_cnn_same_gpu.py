@@ -1,0 +1,101 @@
+#!/usr/bin/env python3
+"""Rehearse the data-parallel ResNet step (hvd.DistributedOptimizer over the xGMI kernel) on ONE
+GPU: W ranks share GPU 0, gloo process group for setup (RCCL refuses two ranks on one device).
+
+What it checks:
+
+* large fusion buckets (64 MB) through the xGMI allreduce staging buffer, issued on the comm
+  stream while backward is still running;
+* fused BN kernels under bf16 autocast in every rank;
+* that all replicas stay bit-identical after the steps (same averaged gradient everywhere).
+
+The ranks time-share the CUs, so images/s is a lower bound of what W GPUs do; the allreduce
+runs over same-device hipIpc mappings (protocol cost, not xGMI bandwidth).
+
+    python scripts/dp_cnn_same_gpu.py --world 2 --model resnet50 --batch_size 32 --steps 20
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import socket
+import sys
+import time
+import types
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def rank_main(rank, world, port, a, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(world))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    from arena_amd.examples import cnn_bench
+    from arena_amd.parallel import hvd
+    hvd.init()
+    torch.backends.cudnn.benchmark = True
+    args = types.SimpleNamespace(model=a.model, batch_size=a.batch_size, image_size=a.image_size,
+                                 num_classes=1000, width=64, learning_rate=0.1, momentum=0.9,
+                                 weight_decay=4e-5, bucket_mb=a.bucket_mb, comm="xgmi",
+                                 data_format="NHWC")
+    model, opt, x, y = cnn_bench.build(args, torch.device("cuda", 0), world)
+    assert opt.comm == "xgmi", opt.comm
+    for i in range(a.warmup):
+        cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
+        torch.cuda.synchronize()
+        if rank == 0:  # the first steps include the solver search: show progress
+            print(f"warmup {i + 1}/{a.warmup}", file=sys.stderr, flush=True)
+    dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        loss = cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    opt.xgmi.check()
+    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+    digest = float(flat.double().sum().item()), float(flat.double().abs().sum().item())
+    q.put((rank, dt, float(loss), digest, len(opt.buckets)))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--world", type=int, default=2)
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch_size", type=int, default=32)
+    ap.add_argument("--image_size", type=int, default=224)
+    ap.add_argument("--bucket_mb", type=float, default=64.0)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    a = ap.parse_args()
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=rank_main, args=(r, a.world, port, a, q)) for r in range(a.world)]
+    for p in ps:
+        p.start()
+    res = sorted(q.get(timeout=900) for _ in range(a.world))
+    for p in ps:
+        p.join(60)
+    dt = max(r[1] for r in res)
+    same = all(r[3] == res[0][3] for r in res)
+    print(json.dumps({"world": a.world, "same_gpu": True, "model": a.model,
+                      "batch_per_rank": a.batch_size, "steps": a.steps, "buckets": res[0][4],
+                      "images_per_s_all_ranks": round(a.world * a.batch_size * a.steps / dt, 1),
+                      "ms_per_step": round(dt / a.steps * 1e3, 3), "final_loss": round(res[0][2], 4),
+                      "replicas_identical": same}), flush=True)
+    if not same:
+        sys.exit(1)
+
+
+if __name__ == "__main__":
+    main()

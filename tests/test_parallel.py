@@ -193,3 +193,66 @@ def test_trainer_external_update_produces_grads_only():
     tr.train_steps(2)
     assert torch.equal(tr.P, p_before)              # no local optimizer
     assert tr.G.abs().sum() > 0 and int(tr.ctrA.item()) == 2
+
+
+def _hvd_nhwc_worker(rank, world, port, q):
+    """Channels_last conv weights: their gradients are NHWC-strided, not contiguous."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from torch import nn
+    from arena_amd.parallel import hvd
+    hvd.init("gloo")
+    try:
+        torch.manual_seed(3)
+        model = nn.Sequential(nn.Conv2d(3, 8, 3), nn.ReLU(), nn.Conv2d(8, 4, 1),
+                              nn.Flatten(), nn.LazyLinear(5))
+        model(torch.zeros(1, 3, 6, 6))
+        model = model.to(memory_format=torch.channels_last)
+        opt = hvd.DistributedOptimizer(torch.optim.SGD(model.parameters(), lr=0.1),
+                                       named_parameters=model.named_parameters(), bucket_mb=0.001)
+        g = torch.Generator().manual_seed(100 + rank)
+        x = torch.randn(4, 3, 6, 6, generator=g).contiguous(memory_format=torch.channels_last)
+        y = torch.randint(0, 5, (4,), generator=g)
+        loss = nn.functional.cross_entropy(model(x), y)
+        opt.zero_grad()
+        loss.backward()
+        strided = any(not p.grad.is_contiguous() for p in model.parameters())
+        opt.step()
+        flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
+        q.put((rank, flat.numpy(), strided))
+    finally:
+        hvd.shutdown()
+
+
+@pytest.mark.timeout(180)
+def test_hvd_channels_last_gradients_average_correctly():
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hvd_nhwc_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted((q.get(timeout=150) for _ in range(world)), key=lambda t: t[0])
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    (_, f0, strided), (_, f1, _) = res
+    assert strided                                   # the case under test actually occurred
+    np.testing.assert_array_equal(f0, f1)
+    # reference: mean of the two ranks' gradients, one SGD step, in one process
+    from torch import nn
+    torch.manual_seed(3)
+    model = nn.Sequential(nn.Conv2d(3, 8, 3), nn.ReLU(), nn.Conv2d(8, 4, 1), nn.Flatten(),
+                          nn.LazyLinear(5))
+    model(torch.zeros(1, 3, 6, 6))
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    opt.zero_grad()
+    for r in range(world):
+        g = torch.Generator().manual_seed(100 + r)
+        x = torch.randn(4, 3, 6, 6, generator=g)
+        y = torch.randint(0, 5, (4,), generator=g)
+        (nn.functional.cross_entropy(model(x), y) / world).backward()
+    opt.step()
+    ref = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).numpy()
+    np.testing.assert_allclose(f0, ref, rtol=1e-5, atol=1e-6)
