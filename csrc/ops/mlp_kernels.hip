@@ -42,6 +42,9 @@ extern "C" hipError_t arena_timeline_read(long long* host, int clear) {
 
 namespace {
 
+// softmax via the hardware exp2/log2 (v_exp_f32 / v_log_f32, see adam.h): exp(x) = 2^(x log2 e)
+constexpr float kLog2e = 1.4426950408889634f, kLn2 = 0.6931471805599453f;
+
 template <int XT>
 __device__ __forceinline__ void load4(const ArenaRowSource& s, long long prow, int k, float out[4]) {
   if constexpr (XT == 1) {
@@ -266,8 +269,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
   }
   float se = 0.f;
 #pragma unroll
-  for (int cc = 0; cc < CB; ++cc) se += (cc < C) ? expf(lg[cc] - mx) : 0.f;
-  const float lse = mx + logf(se);
+  for (int cc = 0; cc < CB; ++cc) se += (cc < C) ? hw_exp2((lg[cc] - mx) * kLog2e) : 0.f;
+  const float lse = mx + hw_log2(se) * kLn2;
   float ly = 0.f;
 #pragma unroll
   for (int cc = 0; cc < CB; ++cc) ly = (cc == y) ? lg[cc] : ly;
@@ -280,7 +283,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 4))) voi
   float gcl[CB];
 #pragma unroll
   for (int cc = 0; cc < CB; ++cc)
-    gcl[cc] = (cc < C) ? (expf(lg[cc] - lse) - (cc == y ? 1.f : 0.f)) * loss_scale : 0.f;
+    gcl[cc] = (cc < C) ? (hw_exp2((lg[cc] - lse) * kLog2e) - (cc == y ? 1.f : 0.f)) * loss_scale
+                       : 0.f;
   if (lane < C) {
     float v = 0.f;
 #pragma unroll
@@ -568,7 +572,12 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
     }
     // (2) on the first chunk, prefetch the tile's Adam state behind them (in-order vmcnt lets the
     //     staging waits below leave these in flight through the K-loop)
-    if (mc0 == 0 && mode == 1) {
+    if (mc0 == 0 && mode == 1 && (ARENA_EXP & 32)) {  // ablation: no Adam state loads
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { pw[r] = 0.1f; mw[r] = 0.01f; vw[r] = 0.001f; }
+#pragma unroll
+      for (int r = 0; r < 4; ++r) { pb[r] = 0.1f; mb[r] = 0.01f; vb[r] = 0.001f; }
+    } else if (mc0 == 0 && mode == 1) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const long long off = (long long)min(n0 + 4 * g + r, P.N - 1) * P.K + kkc;
@@ -635,11 +644,11 @@ __device__ __forceinline__ void wgrad_body(const WGradArgs& args, int pi, float*
         float se = 0.f;
 #pragma unroll
         for (int cc = 0; cc < CB; ++cc) {
-          pe[cc] = (cc < C) ? expf(lgv[cc] - mx) : 0.f;
+          pe[cc] = (cc < C) ? hw_exp2((lgv[cc] - mx) * kLog2e) : 0.f;  // x <= 0: no overflow
           se += pe[cc];
         }
-        const float inv = 1.f / se;
-        const float lse = mx + logf(se);
+        const float inv = hw_rcp(se);                  // se >= 1 (the max term is exp(0))
+        const float lse = mx + hw_log2(se) * kLn2;
         float ly = 0.f;
 #pragma unroll
         for (int cc = 0; cc < CB; ++cc) {
@@ -1089,15 +1098,15 @@ __global__ __launch_bounds__(256) void softmax_xent_kernel(const float* __restri
   for (int cc = lane; cc < C; cc += 64) mx = fmaxf(mx, x[cc]);
   mx = wave_max_fast(mx);
   float se = 0.f;
-  for (int cc = lane; cc < C; cc += 64) se += expf(x[cc] - mx);
+  for (int cc = lane; cc < C; cc += 64) se += hw_exp2((x[cc] - mx) * kLog2e);
   se = wave_sum_fast(se);
-  const float lse = mx + logf(se);
+  const float lse = mx + hw_log2(se) * kLn2;
   const long long y = labels[r];
   if (lane == 0) loss[r] = lse - x[y];
   if (dlogits) {
     float* d = dlogits + (long long)r * C;
     for (int cc = lane; cc < C; cc += 64)
-      d[cc] = (expf(x[cc] - lse) - (cc == y ? 1.f : 0.f)) * grad_scale;
+      d[cc] = (hw_exp2((x[cc] - lse) * kLog2e) - (cc == y ? 1.f : 0.f)) * grad_scale;
   }
 }
 
