@@ -58,6 +58,9 @@ __device__ __forceinline__ void xbarrier(const ArenaXgmiPeers& P, int phase, int
     // flags written and polled with relaxed system-scope accesses to uncached memory, then ONE
     // acquire (buffer_inv). An acquire per poll would invalidate L2 on every spin iteration.
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    // the write-back must complete before the flag goes out: hipcc drops the vmcnt(0) after
+    // buffer_wbl2 whenever the scoreboard is provably empty (MI355X_MICROARCH.md, compiler hazard)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int t = threadIdx.x;
     if (t < W) {
       const int slot = (phase * kMaxB + b) * kMaxR;
