@@ -76,6 +76,9 @@ __device__ __forceinline__ void xbarrier(const ArenaXgmiPeers& P, int phase, int
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    // buffer_inv completes asynchronously: hold the barrier until it has, or the block's other
+    // waves could load the peers' data through a not-yet-invalidated L1 (MI355X_MICROARCH.md)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __syncthreads();
 }
