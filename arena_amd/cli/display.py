@@ -55,7 +55,8 @@ def top_node_summary(out, infos: List[NodeInfo], telemetry=None) -> None:
     total = alloc = 0
     extra = telemetry is not None and any(telemetry.get(i.node.name) for i in infos)
     if extra:
-        w.write("NAME\tIPADDRESS\tROLE\tGPU(Total)\tGPU(Allocated)\tGPU(Busy%)\tVRAM(Used/Total GiB)\n")
+        w.write("NAME\tIPADDRESS\tROLE\tGPU(Total)\tGPU(Allocated)\tGPU(Busy%)\tVRAM(Used/Total GiB)"
+                "\tPower(W)\n")
     else:
         w.write("NAME\tIPADDRESS\tROLE\tGPU(Total)\tGPU(Allocated)\n")
     for i in infos:
@@ -65,7 +66,7 @@ def top_node_summary(out, infos: List[NodeInfo], telemetry=None) -> None:
         row = f"{i.node.name}\t{i.internal_ip()}\t{i.role()}\t{t}\t{a}"
         if extra:
             tel = telemetry.get(i.node.name) or {}
-            row += f"\t{tel.get('busy', 'N/A')}\t{tel.get('vram', 'N/A')}"
+            row += f"\t{tel.get('busy', 'N/A')}\t{tel.get('vram', 'N/A')}\t{tel.get('power', 'N/A')}"
         w.write(row + "\n")
     w.write(SEP + "\n")
     w.write("Allocated/Total GPUs In Cluster:\n")

@@ -683,5 +683,7 @@ class LocalBackend(Backend):
         busy = [g.get("busy_percent", -1) for g in inv["gpus"] if g.get("busy_percent", -1) >= 0]
         used = sum(max(g.get("vram_used", 0), 0) for g in inv["gpus"])
         total = sum(max(g.get("vram_total", 0), 0) for g in inv["gpus"])
+        power = [g.get("power_uw", -1) for g in inv["gpus"] if g.get("power_uw", -1) >= 0]
         return {"busy": f"{sum(busy) // len(busy)}%" if busy else "N/A",
-                "vram": f"{used / 2**30:.0f}/{total / 2**30:.0f}" if total else "N/A"}
+                "vram": f"{used / 2**30:.0f}/{total / 2**30:.0f}" if total else "N/A",
+                "power": f"{sum(power) / 1e6:.0f}" if power else "N/A"}   # node total

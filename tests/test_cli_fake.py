@@ -221,6 +221,22 @@ def test_top_node_details(env):
     assert out.rstrip().endswith("Allocated/Total GPUs In Cluster:  2/16 (12%)")
 
 
+def test_top_node_summary_with_live_telemetry():
+    """Local backend: `top node` adds the probe's live busy %, VRAM and power columns."""
+    from arena_amd.cli import display
+    from arena_amd.jobs.nodes import NodeInfo
+    node = make_node("mi355x-0", "10.0.0.7", 8)
+    out = io.StringIO()
+    display.top_node_summary(out, [NodeInfo(node, [])],
+                             telemetry={"mi355x-0": {"busy": "37%", "vram": "12/2304",
+                                                     "power": "5600"}})
+    lines = out.getvalue().splitlines()
+    assert lines[0].split() == ["NAME", "IPADDRESS", "ROLE", "GPU(Total)", "GPU(Allocated)",
+                                "GPU(Busy%)", "VRAM(Used/Total", "GiB)", "Power(W)"]
+    assert lines[1].split() == ["mi355x-0", "10.0.0.7", "worker", "8", "0", "37%", "12/2304",
+                                "5600"]
+
+
 def test_version_and_completion(env):
     fake, clock, arena = env
     rc, out = arena("version")
