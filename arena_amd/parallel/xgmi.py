@@ -6,8 +6,10 @@ RCCL fallback"). Kernels live in csrc/ccl/xgmi_ccl.hip; this module owns the reg
 * every rank allocates a staging buffer (and optionally a parameter buffer) with hipMalloc and a
   flag buffer in uncached memory, exports hipIpc handles, and exchanges them over the process
   group (gloo or RCCL) with ``all_gather_object``;
-* ``all_reduce_`` = one kernel: copy-in, barrier, reduce own chunk from all W ranks (W-1 xGMI
-  links read in parallel), write it to all ranks, barrier, copy-out;
+* ``all_reduce_`` = one kernel. Two-shot above 64 KB: copy-in, barrier, reduce own chunk from all
+  W ranks (W-1 xGMI links read in parallel), write it to all ranks, barrier, copy-out. One-shot up
+  to 64 KB: stage into a double-buffered tail, barrier, read the whole vector from all ranks and
+  reduce locally (one barrier instead of two: latency-bound sizes);
 * ``adam_`` = reduce-scatter of the gradient + Adam on the owned chunk + all-gather of the
   updated parameters, in one kernel (ZeRO-1-style sharded optimizer state);
 * construction runs a self-test on every rank and agrees on the outcome over the process group,
@@ -77,12 +79,14 @@ class XgmiComm:
         err_msg = ""
         handles = {}
         try:
-            buf = ext.ccl_malloc(self.staging_elems * 4, False)
+            # staging floats + the one-shot kernel's double-buffered tail right behind them
+            buf_bytes = (self.staging_elems + 2 * ext.ccl_oneshot_elems) * 4
+            buf = ext.ccl_malloc(buf_bytes, False)
             self._own.append(buf)
             sig = ext.ccl_malloc(_sig_bytes(ext), True)
             self._own.append(sig)
             ext.ccl_memset(sig, 0, _sig_bytes(ext))
-            ext.ccl_memset(buf, 0, self.staging_elems * 4)
+            ext.ccl_memset(buf, 0, buf_bytes)
             handles = {"buf": ext.ccl_ipc_get(buf), "sig": ext.ccl_ipc_get(sig)}
             local = {"buf": buf, "sig": sig}
             if self.param_elems:

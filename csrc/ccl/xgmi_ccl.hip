@@ -25,6 +25,11 @@
 // the wire equal one two-shot allreduce, but the optimizer pass runs on 1/W of the vector and
 // the separate all-reduce + Adam launches disappear.
 //
+// Small vectors (<= ARENA_CCL_ONESHOT_ELEMS floats: metrics, tail buckets) take a one-shot path
+// with ONE barrier instead of two: every rank stages its vector in a double-buffered tail region,
+// and after the barrier reads the whole vector from all peers and reduces it locally (see
+// xgmi_allreduce_oneshot_kernel for why the second barrier is not needed).
+//
 // Barrier waits are bounded (timeout_cycles of the 100 MHz s_memrealtime clock): a peer that never
 // arrives sets *err and the kernel drains instead of hanging the GPU; the host checks err.
 #include <hip/hip_runtime.h>
@@ -155,6 +160,42 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(ArenaXgmiPeers
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
+// One-shot: block b owns floats [b*kOneSub, (b+1)*kOneSub) of the vector, one float4 per thread.
+// Stage into tail half (e & 1), barrier, read that slot from all W ranks, reduce, store locally.
+//
+// Why one barrier is enough: block b of every rank reads my half-p slot b only between its
+// barrier of call e and its exit. I write that slot again at call e + 2 at the earliest (the half
+// flips every call of block b), and between the two I pass block b's barrier of call e + 1 (of
+// whatever kind), which needs block b of every peer to have arrived there, i.e. to have finished
+// call e. Only block b ever touches slot b of the tail; the two-shot and Adam kernels stay below
+// buf_elems. Per-block counters are equal on all ranks because every rank issues the same calls.
+constexpr int kOneSub = kThreads * 4;
+
+template <int W>
+__global__ __launch_bounds__(kThreads) void xgmi_allreduce_oneshot_kernel(ArenaXgmiPeers P,
+                                                                           const float* __restrict__ in,
+                                                                           float* __restrict__ out,
+                                                                           long long n, float scale) {
+  const int b = blockIdx.x;
+  const uint32_t e = P.epoch[b] + 1;
+  const long long tail = P.buf_elems + (long long)(e & 1) * ARENA_CCL_ONESHOT_ELEMS;
+  const long long o = (long long)b * kOneSub + threadIdx.x * 4;
+  const bool ok = o < n;
+  if (ok) st4(P.buf[P.rank] + tail + o, ld4(in + o));
+  xbarrier<W>(P, 0, b, e);
+  if (ok) {
+    float4 v[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) v[q] = ld4(P.buf[q] + tail + o);  // W loads in flight
+    float4 acc = v[0];
+#pragma unroll
+    for (int q = 1; q < W; ++q) acc = add4(acc, v[q]);  // same order as the two-shot kernel
+    acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
+    st4(out + o, acc);
+  }
+  if (threadIdx.x == 0) P.epoch[b] = e;
+}
+
 template <int W>
 __global__ __launch_bounds__(kThreads) void xgmi_adam_kernel(ArenaXgmiPeers P, float* __restrict__ M,
                                                               float* __restrict__ V, long long n,
@@ -210,6 +251,11 @@ __global__ __launch_bounds__(kThreads) void xgmi_adam_kernel(ArenaXgmiPeers P, f
 // Floats of a chunk per block. Every block pays two cross-rank barriers (one L2 writeback + one
 // invalidate each), so blocks are made fat rather than numerous; tunable for sweeps.
 long long g_block_elems = 4096;
+// Crossover measured on 1x MI355X, 2 ranks (profiles/r1_ccl_oneshot_ab.jsonl): one-shot 3.0 vs
+// 3.7 us at 4 KB, 3.56 vs 3.97 us at 16 KB, but 4.5 vs 4.26 us at 64 KB. One-shot also moves
+// (W-1) x n bytes per rank over the links instead of 2 (W-1)/W x n, so the default stays at 32 KB.
+long long g_oneshot_max = ARENA_CCL_ONESHOT_ELEMS / 2;
+static_assert(ARENA_CCL_ONESHOT_ELEMS / kOneSub <= kMaxB, "one-shot blocks exceed the flag slots");
 
 void geometry(long long n, int W, long long* L, long long* S, int* nb) {
   long long l = (n + W - 1) / W;
@@ -268,6 +314,12 @@ hipError_t arena_ccl_allreduce(const ArenaXgmiPeers* P, const float* in, float* 
                                float scale, hipStream_t stream) {
   const int W = P->world;
   if (W < 2 || W > kMaxR || n <= 0 || n % 4 || n > P->buf_elems) return hipErrorInvalidValue;
+  if (n <= g_oneshot_max) {
+    const int nb = (int)((n + kOneSub - 1) / kOneSub);
+    ARENA_CCL_DISPATCH(W, xgmi_allreduce_oneshot_kernel, dim3(nb), dim3(kThreads), 0, stream, *P,
+                       in, out, n, scale);
+    return hipGetLastError();
+  }
   long long L, S;
   int nb;
   geometry(n, W, &L, &S, &nb);
@@ -275,6 +327,12 @@ hipError_t arena_ccl_allreduce(const ArenaXgmiPeers* P, const float* in, float* 
                      n, L, S, scale);
   return hipGetLastError();
 }
+
+// Largest vector (floats) that takes the one-shot kernel; 0 forces two-shot (for A/B sweeps).
+void arena_ccl_set_oneshot_max(long long e) {
+  g_oneshot_max = e < 0 ? 0 : std::min<long long>(e, ARENA_CCL_ONESHOT_ELEMS);
+}
+long long arena_ccl_get_oneshot_max() { return g_oneshot_max; }
 
 hipError_t arena_ccl_adam(const ArenaXgmiPeers* P, float* M, float* V, long long n, ArenaAdam a,
                           ArenaCounterOp ctr, hipStream_t stream) {

@@ -43,6 +43,8 @@ hipError_t arena_ccl_adam(const ArenaXgmiPeers*, float*, float*, long long, Aren
                           ArenaCounterOp, hipStream_t);
 void arena_ccl_shard(long long, int, int, long long*, long long*);
 void arena_ccl_set_block_elems(long long);
+void arena_ccl_set_oneshot_max(long long);
+long long arena_ccl_get_oneshot_max();
 // csrc/ops/bn_kernels.hip
 long long arena_bn_workspace_floats(long long, int);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, long long, int, int, int, float*,
@@ -795,6 +797,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ccl_tensor", &ccl_tensor);
   m.def("ccl_shard", &ccl_shard);
   m.def("ccl_set_block_elems", [](int64_t e) { arena_ccl_set_block_elems(e); });
+  m.def("ccl_set_oneshot_max", [](int64_t e) { arena_ccl_set_oneshot_max(e); });
+  m.def("ccl_get_oneshot_max", []() { return (int64_t)arena_ccl_get_oneshot_max(); });
   py::class_<XgmiPeers>(m, "XgmiPeers")
       .def(py::init<std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, Tensor,
                     Tensor, int64_t, int64_t, int64_t, double>())
@@ -811,6 +815,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
 #endif
   m.attr("ccl_max_blocks") = ARENA_CCL_MAX_BLOCKS;
   m.attr("ccl_max_ranks") = ARENA_CCL_MAX_RANKS;
+  m.attr("ccl_oneshot_elems") = ARENA_CCL_ONESHOT_ELEMS;
   m.attr("arch") = "gfx950";
 #ifndef ARENA_SRC_HASH
 #define ARENA_SRC_HASH "unknown"

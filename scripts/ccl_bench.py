@@ -69,6 +69,8 @@ def bench(rank: int, world: int, sizes, rccl: bool,
     maxn = max(sizes) // 4
     comm = XgmiComm(staging_elems=maxn, param_elems=397520, timeout_s=30.0)
     rows = []
+    comm.all_reduce_(comm.buffer()[:1024])  # first-call warm-up (code object load), untimed
+    torch.cuda.synchronize()
     for nbytes in sizes:
         n = nbytes // 4
         x = torch.randn(n, device="cuda")
@@ -78,6 +80,13 @@ def bench(rank: int, world: int, sizes, rccl: bool,
         y = torch.empty_like(x)
         t = timed(lambda: comm.all_reduce_(x, out=y))
         rows.append(("xgmi_allreduce", nbytes, t))
+        if n <= comm.ext.ccl_oneshot_elems:  # A/B: one-shot vs two-shot kernel at this size
+            default = comm.ext.ccl_get_oneshot_max()
+            for kind, cap in (("one_shot", comm.ext.ccl_oneshot_elems), ("two_shot", 0)):
+                comm.ext.ccl_set_oneshot_max(cap)
+                t = timed(lambda: comm.all_reduce_(stage, scale=1.0 / world))
+                rows.append((f"xgmi_allreduce_zero_copy(forced_{kind})", nbytes, t))
+            comm.ext.ccl_set_oneshot_max(default)
         if rccl:
             t = timed(lambda: dist.all_reduce(x))
             rows.append(("rccl_allreduce", nbytes, t))

@@ -47,6 +47,26 @@ def _collectives(rank, world, port, q):
             x = xs[rank].clone()
             comm.all_reduce_(x, scale=0.5)
             res[n] = bool(torch.equal(x, want))
+        # one-shot (<= 16384 floats) and two-shot calls interleaved with different block counts:
+        # the one-shot tail is double-buffered by per-block call parity, no second barrier
+        default_cap = comm.ext.ccl_get_oneshot_max()
+        comm.ext.ccl_set_oneshot_max(comm.ext.ccl_oneshot_elems)  # the whole one-shot capacity
+        seq = [4096, 65536, 16, 16384, 70000, 8, 1024, 16388, 12, 16384] * 3
+        xs_all = [[torch.randint(-1000, 1000, (n,), device="cuda", generator=g).float()
+                   for _ in range(world)] for n in seq]
+        outs = []
+        for xs in xs_all:
+            x = xs[rank].clone()
+            comm.all_reduce_(x)  # back-to-back, no host sync in between
+            outs.append(x)
+        torch.cuda.synchronize()
+        res["interleaved"] = all(bool(torch.equal(o, sum(xs))) for o, xs in zip(outs, xs_all))
+        # forced two-shot on a one-shot size gives the identical result
+        comm.ext.ccl_set_oneshot_max(0)
+        x = xs_all[0][rank].clone()
+        comm.all_reduce_(x)
+        comm.ext.ccl_set_oneshot_max(default_cap)
+        res["forced_two_shot"] = bool(torch.equal(x, outs[0]))
         # zero-copy from the staging buffer, out-of-place destination
         stage = comm.buffer()[:256]
         stage.copy_(torch.full((256,), float(rank + 1), device="cuda"))
