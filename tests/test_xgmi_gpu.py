@@ -274,7 +274,9 @@ def _run(fn, world, timeout=240):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 4])
+# world 8 = the 8-GPU node's kernel instantiation (W = 8 register footprint, 7 peers), here as 8
+# ranks time-sharing one GPU
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_xgmi_allreduce_exact(world):
     out = _run(_collectives, world)
     for r, res in out.items():
@@ -282,8 +284,9 @@ def test_xgmi_allreduce_exact(world):
         assert res["err"] == 0
 
 
-def test_xgmi_fused_adam_matches_flat_adam():
-    out = _run(_adam, 2)
+@pytest.mark.parametrize("world", [2, 8])
+def test_xgmi_fused_adam_matches_flat_adam(world):
+    out = _run(_adam, world)
     for r, res in out.items():
         assert res["P"] < 1e-6 and res["M_own"] < 1e-6 and res["M_other_zero"], (r, res)
         assert res["err"] == 0
