@@ -137,15 +137,26 @@ def main(argv=None) -> int:
                   flush=True)
     sync()
     graph = None
-    if args.graph and world == 1 and dev.type == "cuda":
+    if args.graph and dev.type == "cuda":
+        # Data parallel too: the bucket hooks fire during the captured backward, so the graph
+        # holds the pack + collective (xGMI kernel on the comm stream, or RCCL) of every bucket
+        # exactly where eager mode issues them; all ranks replay the same collective sequence.
+        ok = True
         try:
             graph, g_loss = capture_step(model, opt, x, y, amp)
+        except RuntimeError as e:  # capture refused by a library call: run eagerly
+            graph, ok = None, False
+            print(f"[rank {rank}] hipGraph capture failed, running eagerly: {e}", flush=True)
+        if world > 1:  # every rank replays, or none does (a lone eager rank would still match
+            # the collective sequence, but the timing would not be one mode)
+            t = torch.tensor([1 if ok else 0], device=dev)
+            torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MIN)
+            if not int(t.item()):
+                graph = None
+            torch.distributed.barrier()
+        if graph is not None:
             graph.replay()  # one untimed replay: the step the capture recorded is now executed
             sync()
-        except RuntimeError as e:  # capture refused by a library call: run eagerly
-            graph = None
-            if rank == 0:
-                print(f"hipGraph capture failed, running eagerly: {e}", flush=True)
     if world > 1:
         torch.distributed.barrier()
     sync()

@@ -51,10 +51,20 @@ def rank_main(rank, world, port, a, q):
         torch.cuda.synchronize()
         if rank == 0:  # the first steps include the solver search: show progress
             print(f"warmup {i + 1}/{a.warmup}", file=sys.stderr, flush=True)
+    graph = None
+    if a.graph:  # the whole DP step (bucket hooks + xGMI kernels on the comm stream) as a hipGraph
+        graph, g_loss = cnn_bench.capture_step(model, opt, x, y, torch.bfloat16)
+        dist.barrier()
+        graph.replay()
+        torch.cuda.synchronize()
     dist.barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        loss = cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
+        if graph is not None:
+            graph.replay()
+            loss = g_loss
+        else:
+            loss = cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     opt.xgmi.check()
@@ -74,6 +84,7 @@ def main():
     ap.add_argument("--bucket_mb", type=float, default=64.0)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step as a hipGraph")
     a = ap.parse_args()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -89,7 +100,8 @@ def main():
     dt = max(r[1] for r in res)
     same = all(r[3] == res[0][3] for r in res)
     print(json.dumps({"world": a.world, "same_gpu": True, "model": a.model,
-                      "batch_per_rank": a.batch_size, "steps": a.steps, "buckets": res[0][4],
+                      "batch_per_rank": a.batch_size, "steps": a.steps,
+                      "exec": "hipgraph" if a.graph else "eager", "buckets": res[0][4],
                       "images_per_s_all_ranks": round(a.world * a.batch_size * a.steps / dt, 1),
                       "ms_per_step": round(dt / a.steps * 1e3, 3), "final_loss": round(res[0][2], 4),
                       "replicas_identical": same}), flush=True)

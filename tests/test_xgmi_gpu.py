@@ -253,6 +253,46 @@ def _rccl_capture(rank, world, port, q):
         q.put((rank, None, traceback.format_exc()))
 
 
+def _cnn_graph(rank, world, port, q):
+    """DP ResNet step replayed as one hipGraph (bucket hooks + xGMI kernels on the comm stream
+    captured) must equal the same steps run eagerly, and all replicas must stay identical."""
+    try:
+        dist = _init(rank, world, port)
+        import types
+        from arena_amd.examples import cnn_bench
+        from arena_amd.parallel import hvd
+        hvd.init()
+        args = types.SimpleNamespace(model="resnet_tiny", data_format="NHWC", batch_size=8,
+                                     image_size=32, num_classes=10, width=16, learning_rate=0.05,
+                                     momentum=0.9, weight_decay=1e-3, bucket_mb=0.05, comm="xgmi")
+        dev = torch.device("cuda", 0)
+        flats = []
+        for graph in (False, True):
+            model, opt, x, y = cnn_bench.build(args, dev, world)
+            assert opt.comm == "xgmi" and len(opt.buckets) > 1, (opt.comm, len(opt.buckets))
+            for _ in range(2):
+                cnn_bench.train_step(model, opt, x, y, None)
+            if graph:
+                g, _ = cnn_bench.capture_step(model, opt, x, y, None)
+                dist.barrier()
+                for _ in range(3):
+                    g.replay()
+            else:
+                for _ in range(3):
+                    cnn_bench.train_step(model, opt, x, y, None)
+            torch.cuda.synchronize()
+            opt.xgmi.check()
+            flats.append(torch.cat([p.detach().reshape(-1) for p in model.parameters()]).cpu())
+            dist.barrier()
+        res = {"graph_vs_eager": float((flats[0] - flats[1]).abs().max()),
+               "scale": float(flats[0].abs().max()), "digest": float(flats[1].double().sum())}
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
 def _run(fn, world, timeout=240):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -309,3 +349,10 @@ def test_hvd_distributed_optimizer_xgmi_comm_stream():
 def test_rccl_allreduce_is_graph_capturable():
     out = _run(_rccl_capture, 1)
     assert out[0]["ok"], out
+
+
+def test_dp_resnet_step_as_hipgraph_matches_eager():
+    out = _run(_cnn_graph, 2)
+    for r, res in out.items():
+        assert res["graph_vs_eager"] <= 1e-4 * max(1.0, res["scale"]), (r, res)
+    assert out[0]["digest"] == out[1]["digest"], out  # replicas bit-identical
