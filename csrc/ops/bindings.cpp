@@ -47,6 +47,7 @@ void arena_ccl_set_oneshot_max(long long);
 long long arena_ccl_get_oneshot_max();
 // csrc/ops/bn_kernels.hip
 long long arena_bn_workspace_floats(long long, int);
+void arena_bn_set_reduce_geometry(long long, long long);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, long long, int, int, int, float*,
                         ArenaBNStats, hipStream_t);
 hipError_t arena_bn_bwd(int, const void*, const void*, const void*, void*, void*, long long, int,
@@ -781,6 +782,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_fwd", &linear_fwd);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
+  m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
+    arena_bn_set_reduce_geometry(max_blocks, min_rounds);
+  });
   m.def("xent_head", &xent_head);
   m.def("mlp_fwd_logits", &mlp_fwd_logits);
   m.def("wgrad_grouped", &wgrad_grouped);

@@ -426,11 +426,15 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
 // of loads at once), as many blocks as that allows up to 512 partials. The 7x7 ResNet layers
 // (M = 6272) need the small per-thread share to fill the chip: at 32 rounds per thread they ran
 // 49 blocks and reached ~1 TB/s.
+// Both limits are runtime-tunable for sweeps (scripts/bn_bench.py); the workspace size follows.
+long long g_max_reduce_blocks = 512;
+long long g_min_rounds = 8;
+
 long long reduce_blocks(long long M, int C, long long* rpb) {
   const int rip = kT / (C / kVec);
   long long rounds = (M + rip - 1) / rip;
-  long long nb = (rounds + 7) / 8;
-  nb = nb < 1 ? 1 : (nb > 512 ? 512 : nb);
+  long long nb = (rounds + g_min_rounds - 1) / g_min_rounds;
+  nb = nb < 1 ? 1 : (nb > g_max_reduce_blocks ? g_max_reduce_blocks : nb);
   long long r = (M + nb - 1) / nb;
   r = (r + rip - 1) / rip * rip;  // whole rounds per block
   *rpb = r;
@@ -449,6 +453,11 @@ bool bad_shape(long long M, int C) {
 }  // namespace
 
 extern "C" {
+
+void arena_bn_set_reduce_geometry(long long max_blocks, long long min_rounds) {
+  g_max_reduce_blocks = max_blocks < 1 ? 1 : (max_blocks > 4096 ? 4096 : max_blocks);
+  g_min_rounds = min_rounds < 1 ? 1 : min_rounds;
+}
 
 long long arena_bn_workspace_floats(long long M, int C) {
   if (bad_shape(M, C)) return 0;
