@@ -20,6 +20,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.pool import MaxPool2dNHWC
 
 DEPTHS = {"resnet50": [3, 4, 6, 3], "resnet101": [3, 4, 23, 3],
           "resnet152": [3, 8, 36, 3], "resnet_tiny": [1, 1, 1, 1]}
@@ -58,7 +59,7 @@ class ResNet(nn.Module):
         super().__init__()
         self.stem = nn.Sequential(nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False),
                                   BatchNormAct2d(width, act="relu"),
-                                  nn.MaxPool2d(3, stride=2, padding=1))
+                                  MaxPool2dNHWC(3, stride=2, padding=1))
         layers = []
         cin = width
         for i, n in enumerate(depths):

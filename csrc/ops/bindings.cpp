@@ -48,6 +48,11 @@ long long arena_ccl_get_oneshot_max();
 // csrc/ops/bn_kernels.hip
 long long arena_bn_workspace_floats(long long, int);
 void arena_bn_set_reduce_geometry(long long, long long);
+// csrc/ops/pool_kernels.hip
+hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, int, int, int, int,
+                             hipStream_t);
+hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, int, int, int, int,
+                             int, hipStream_t);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, long long, int, int, int, float*,
                         ArenaBNStats, hipStream_t);
 hipError_t arena_bn_bwd(int, const void*, const void*, const void*, void*, void*, long long, int,
@@ -703,6 +708,50 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor in
   return {dx, dres, dgamma, dbeta};
 }
 
+// ------------------------------------------------------------------- NHWC max pooling
+void pool_check(const Tensor& t, const char* name) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 4, name, " must be a 4-D GPU tensor");
+  TORCH_CHECK(t.scalar_type() == torch::kBFloat16 || t.scalar_type() == torch::kFloat32, name,
+              " must be bfloat16 or float32");
+  TORCH_CHECK(t.is_contiguous(at::MemoryFormat::ChannelsLast), name,
+              " must be channels_last contiguous (NHWC)");
+  TORCH_CHECK(t.size(1) % 8 == 0, name, ": C must be a multiple of 8");
+}
+
+// Returns (y, pos): pos = uint8 in-window argmax, same NHWC layout as y.
+std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
+  pool_check(x, "x");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(k >= 1 && k <= 15 && s >= 1 && p >= 0 && 2 * p <= k && H + 2 * p >= k &&
+                  W + 2 * p >= k,
+              "maxpool: unsupported kernel/stride/padding");
+  const int OH = (int)((H + 2 * p - k) / s + 1), OW = (int)((W + 2 * p - k) / s + 1);
+  Tensor y = torch::empty({N, C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor pos = torch::empty({N, C, OH, OW},
+                            x.options().dtype(torch::kUInt8).memory_format(at::MemoryFormat::ChannelsLast));
+  check_hip(arena_maxpool_fwd(x.scalar_type() == torch::kBFloat16 ? 1 : 0, x.data_ptr(),
+                              y.data_ptr(), pos.data_ptr<uint8_t>(), N, H, W, C, (int)k, (int)s,
+                              (int)p, cur_stream()),
+            "maxpool_fwd");
+  return {y, pos};
+}
+
+Tensor maxpool_bwd(Tensor dy, Tensor pos, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p) {
+  pool_check(dy, "grad_output");
+  TORCH_CHECK(pos.scalar_type() == torch::kUInt8 && pos.sizes() == dy.sizes() &&
+                  pos.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool_bwd: positions must be uint8 NHWC shaped like grad_output");
+  const int N = (int)dy.size(0), C = (int)dy.size(1);
+  TORCH_CHECK(dy.size(2) == (H + 2 * p - k) / s + 1 && dy.size(3) == (W + 2 * p - k) / s + 1,
+              "maxpool_bwd: grad_output shape does not match the input geometry");
+  Tensor dx = torch::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_hip(arena_maxpool_bwd(dy.scalar_type() == torch::kBFloat16 ? 1 : 0, dy.data_ptr(),
+                              pos.data_ptr<uint8_t>(), dx.data_ptr(), N, (int)H, (int)W, C, (int)k,
+                              (int)s, (int)p, cur_stream()),
+            "maxpool_bwd");
+  return dx;
+}
+
 class XgmiPeers {
  public:
   XgmiPeers(std::vector<int64_t> bufs, std::vector<int64_t> bufs2, std::vector<int64_t> sigs,
@@ -782,6 +831,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_fwd", &linear_fwd);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
+  m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
     arena_bn_set_reduce_geometry(max_blocks, min_rounds);
   });

@@ -1,0 +1,60 @@
+"""NHWC max-pool HIP kernels vs PyTorch's max_pool2d on fp32 copies of the same data (MI355X).
+
+Forward values are exact (max is exact in any precision) and the window scan order (kh-major,
+first strict maximum) matches PyTorch's, so even ties pick the same input; the backward sums the
+same <= ceil(k/s)^2 gradients in fp32 (bf16 rounded once at the end).
+"""
+from __future__ import annotations
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+CASES = [  # (N, C, H, W, k, s, p)
+    (2, 64, 112, 112, 3, 2, 1),   # ResNet stem
+    (3, 16, 15, 17, 3, 2, 1),     # odd sizes: partial windows at the far edge
+    (2, 8, 8, 8, 2, 2, 0),
+    (2, 24, 9, 10, 3, 1, 1),      # stride 1: every input sits in up to 9 windows
+    (1, 32, 13, 13, 5, 3, 2),
+    (2, 8, 10, 10, 1, 2, 0),      # k < s: the last row/column lies in no window (dx = 0)
+]
+
+
+def _ref(x, dy, k, s, p):
+    xr = x.detach().float().requires_grad_(True)
+    y = F.max_pool2d(xr, k, s, p)
+    y.backward(dy.float())
+    return y.detach(), xr.grad
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", CASES)
+@pytest.mark.parametrize("ties", [False, True])
+def test_maxpool_matches_pytorch(case, dtype, ties):
+    from arena_amd.ops import pool
+    N, C, H, W, k, s, p = case
+    g = torch.Generator(device="cuda").manual_seed(hash((case, ties)) % 2**31)
+    x = torch.randn(N, C, H, W, device="cuda", generator=g)
+    if ties:  # few distinct values: most windows hold several equal maxima
+        x = torch.randint(-2, 3, (N, C, H, W), device="cuda", generator=g).float()
+    x = x.to(dtype).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    assert pool.kernel_ok(x, k, s, p)
+    y = pool.max_pool2d(x, k, s, p)
+    assert y.is_contiguous(memory_format=torch.channels_last)
+    dy = torch.randn(y.shape, device="cuda", generator=g).to(dtype)
+    y.backward(dy)
+    y_ref, dx_ref = _ref(x, dy, k, s, p)
+    assert torch.equal(y.float(), y_ref)
+    if dtype == torch.float32:
+        torch.testing.assert_close(x.grad, dx_ref, rtol=1e-6, atol=1e-6)
+    else:
+        torch.testing.assert_close(x.grad.float(), dx_ref.to(dtype).float(), rtol=8e-3, atol=1e-2)
+
+
+def test_resnet_stem_uses_the_kernel():
+    from arena_amd.models.resnet import resnet
+    from arena_amd.ops.pool import MaxPool2dNHWC
+    m = resnet("resnet_tiny", num_classes=10, width=8)
+    assert isinstance(m.stem[2], MaxPool2dNHWC)
