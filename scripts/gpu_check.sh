@@ -17,7 +17,7 @@ ok_or_stop() {  # rc 0 = pass, 1 = test failures (GPU healthy) -> continue; anyt
 STEPS=${STEPS:-all}
 
 if [[ $STEPS == all || $STEPS == *tests* ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
   ok_or_stop $? "pytest -m gpu"
   tail -5 gpurun_out/pytest_gpu.log
 fi
