@@ -51,6 +51,9 @@ def parse(argv=None):
     ap.add_argument("--graph", type=int, default=1,
                     help="1: capture the whole training step (fwd, bwd, optimizer) in one hipGraph "
                          "and replay it (single rank; DP ranks run eagerly)")
+    ap.add_argument("--master_weights", choices=["auto", "on", "off"], default="auto",
+                    help="bf16 conv/linear weights with fp32 master copies updated by one "
+                         "multi-tensor HIP kernel (auto: on for single-rank bf16 GPU runs)")
     ap.add_argument("--json", action="store_true", help="print one JSON summary line at the end")
     return ap.parse_args(argv)
 
@@ -68,10 +71,25 @@ def build(args, dev, world):
     decay, no_decay = [], []
     for n, p in model.named_parameters():
         (no_decay if p.ndim <= 1 else decay).append(p)   # no decay on BN / bias
-    opt = torch.optim.SGD([{"params": decay, "weight_decay": args.weight_decay},
-                           {"params": no_decay, "weight_decay": 0.0}],
-                          lr=args.learning_rate, momentum=args.momentum,
-                          foreach=dev.type == "cuda")
+    mw = getattr(args, "master_weights", "auto")
+    master = mw == "on" or (
+        mw == "auto" and world == 1 and dev.type == "cuda"
+        and getattr(args, "dtype", "bf16") == "bf16" and all(p.numel() % 4 == 0 for p in decay))
+    if master and world > 1:
+        raise SystemExit("--master_weights on is single-rank only (DP buckets carry fp32 grads)")
+    if master:
+        # conv/fc weights live in bf16 (fp32 masters inside MasterSGD): no per-step casts
+        from ..ops.optim import MasterSGD, OptimizerGroup
+        opt = OptimizerGroup(
+            MasterSGD(decay, lr=args.learning_rate, momentum=args.momentum,
+                      weight_decay=args.weight_decay),
+            torch.optim.SGD(no_decay, lr=args.learning_rate, momentum=args.momentum,
+                            foreach=True))
+    else:
+        opt = torch.optim.SGD([{"params": decay, "weight_decay": args.weight_decay},
+                               {"params": no_decay, "weight_decay": 0.0}],
+                              lr=args.learning_rate, momentum=args.momentum,
+                              foreach=dev.type == "cuda")
     if world > 1:
         opt = hvd.DistributedOptimizer(opt, named_parameters=model.named_parameters(),
                                        bucket_mb=args.bucket_mb, comm=args.comm)

@@ -135,3 +135,11 @@ def unflatten_from(tensors: Sequence[Tensor], offsets: Sequence[int], flat: Tens
                    scale: float = 1.0) -> None:
     """t_i = flat[off_i : off_i+n_i] * scale."""
     _impl(flat).mt_copy_scale(list(tensors), [int(o) for o in offsets], flat, float(scale), 1)
+
+
+def mt_sgd_master(grads: Sequence[Tensor], offsets: Sequence[int], master: Tensor, mom: Tensor,
+                  wbf: Tensor, *, lr: float, momentum: float, weight_decay: float) -> None:
+    """One launch (per 48 tensors) of momentum SGD over bf16 grads with fp32 master weights;
+    also writes the rounded bf16 weights into ``wbf`` (see ``mt_sgd_master_kernel``)."""
+    _impl(master).mt_sgd_master(list(grads), [int(o) for o in offsets], master, mom, wbf,
+                                float(lr), float(momentum), float(weight_decay))

@@ -268,3 +268,17 @@ def mt_copy_scale(tensors, offsets, flat, scale, direction):
             flat[off:off + n].copy_(t.reshape(-1) * scale)
         else:
             t.view(-1).copy_(flat[off:off + n] * scale)
+
+
+def _storage_flat(t):
+    """A dense tensor's elements in memory order (channels_last weights included)."""
+    return t.as_strided((t.numel(),), (1,), t.storage_offset())
+
+
+def mt_sgd_master(grads, offsets, master, mom, wbf, lr, momentum, weight_decay):
+    for g, off in zip(grads, offsets):
+        n = g.numel()
+        w, m = master[off:off + n], mom[off:off + n]
+        m.mul_(momentum).add_(_storage_flat(g).float() + weight_decay * w)
+        w.sub_(lr * m)
+        wbf[off:off + n].copy_(w)

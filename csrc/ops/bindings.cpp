@@ -30,6 +30,8 @@ hipError_t arena_softmax_xent(const float*, const long long*, int, int, float*, 
                               hipStream_t);
 hipError_t arena_mt_copy_scale(float* const*, const long long*, const long long*, int, float*, float,
                                int, hipStream_t);
+hipError_t arena_mt_sgd_master(const void* const*, const long long*, const long long*, int,
+                               float*, float*, void*, float, float, float, hipStream_t);
 // csrc/ccl/xgmi_ccl.hip
 hipError_t arena_ccl_malloc(void**, size_t, int);
 hipError_t arena_ccl_free(void*);
@@ -544,6 +546,37 @@ void mt_copy_scale(std::vector<Tensor> tensors, std::vector<int64_t> offsets, Te
             "mt_copy_scale");
 }
 
+void mt_sgd_master(std::vector<Tensor> grads, std::vector<int64_t> offsets, Tensor master,
+                   Tensor mom, Tensor wbf, double lr, double momentum, double weight_decay) {
+  check_f32(master, "master");
+  check_f32(mom, "mom");
+  check_dev(wbf, "wbf");
+  TORCH_CHECK(wbf.scalar_type() == torch::kBFloat16 && wbf.is_contiguous() &&
+                  mom.numel() == master.numel() && wbf.numel() == master.numel(),
+              "mt_sgd_master: flat buffers must be fp32/fp32/bf16 of equal size");
+  TORCH_CHECK(grads.size() == offsets.size(), "offsets length");
+  std::vector<const void*> ptrs;
+  std::vector<long long> offs, ns;
+  for (size_t i = 0; i < grads.size(); ++i) {
+    const Tensor& g = grads[i];
+    TORCH_CHECK(g.is_cuda() && g.device() == master.device(), "grad ", i,
+                " must be on the master buffer's GPU");
+    TORCH_CHECK(g.scalar_type() == torch::kBFloat16 && g.is_non_overlapping_and_dense(),
+                "mt_sgd_master: grad ", i, " must be dense bf16");
+    TORCH_CHECK(g.numel() % 4 == 0 && offsets[i] % 4 == 0 && offsets[i] >= 0 &&
+                    offsets[i] + g.numel() <= master.numel(),
+                "mt_sgd_master: segment ", i, " misaligned or out of bounds");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(g.data_ptr()) % 8 == 0, "grad ", i, " not 8B aligned");
+    ptrs.push_back(g.data_ptr());
+    offs.push_back(offsets[i]);
+    ns.push_back(g.numel());
+  }
+  check_hip(arena_mt_sgd_master(ptrs.data(), offs.data(), ns.data(), (int)ptrs.size(),
+                                master.data_ptr<float>(), mom.data_ptr<float>(), wbf.data_ptr(),
+                                (float)lr, (float)momentum, (float)weight_decay, cur_stream()),
+            "mt_sgd_master");
+}
+
 // ------------------------------------------------------------------------------ xGMI collective
 int64_t ccl_malloc(int64_t bytes, bool uncached) {
   TORCH_CHECK(bytes > 0, "ccl_malloc: bytes must be positive");
@@ -843,6 +876,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_flat", &sgd_flat);
   m.def("softmax_xent", &softmax_xent);
   m.def("mt_copy_scale", &mt_copy_scale);
+  m.def("mt_sgd_master", &mt_sgd_master);
   m.def("ccl_malloc", &ccl_malloc);
   m.def("ccl_free", &ccl_free);
   m.def("ccl_memset", &ccl_memset);

@@ -1141,6 +1141,50 @@ __global__ __launch_bounds__(256) void mt_copy_scale_kernel(MtArgs a, float* __r
   }
 }
 
+
+// Momentum SGD over bf16 weights with fp32 master copies (mixed-precision CNN training).
+// Tensor i: bf16 gradient at a.ptr[i] (autograd-owned, same storage order as the parameter),
+// master/momentum/bf16-param segments at a.off[i] of the flat buffers. One pass reads the bf16
+// grad + fp32 master + fp32 momentum and writes master, momentum and the rounded bf16 weight
+// the next forward consumes, so autocast needs no per-step weight/grad casts.
+// Matches torch.optim.SGD (dampening 0, no nesterov): d = g + wd*w; m = mu*m + d; w -= lr*m.
+__device__ inline float bf16_to_f32(uint32_t v) { return __uint_as_float(v << 16); }
+__device__ inline uint32_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);                                  // round to nearest even
+  return u >> 16;
+}
+
+__global__ __launch_bounds__(256) void mt_sgd_master_kernel(MtArgs a, float* __restrict__ master,
+                                                            float* __restrict__ mom,
+                                                            uint16_t* __restrict__ wbf, float lr,
+                                                            float mu, float wd) {
+  int ti = 0;
+  for (int i = 1; i < a.count; ++i)
+    if ((int)blockIdx.x >= a.blk_begin[i]) ti = i;
+  const long long j = (long long)(blockIdx.x - a.blk_begin[ti]) * 1024 + threadIdx.x * 4;
+  if (j >= a.n[ti]) return;  // n % 4 == 0 (host-checked): a live thread owns 4 whole elements
+  const long long o = a.off[ti] + j;
+  const uint2 g2 = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(a.ptr[ti]) + j);
+  float4 w4 = *reinterpret_cast<const float4*>(master + o);
+  float4 m4 = *reinterpret_cast<const float4*>(mom + o);
+  const float g[4] = {bf16_to_f32(g2.x & 0xffffu), bf16_to_f32(g2.x >> 16),
+                      bf16_to_f32(g2.y & 0xffffu), bf16_to_f32(g2.y >> 16)};
+  float* w = &w4.x;
+  float* m = &m4.x;
+  uint32_t r[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    m[k] = mu * m[k] + (g[k] + wd * w[k]);
+    w[k] = w[k] - lr * m[k];
+    r[k] = f32_to_bf16(w[k]);
+  }
+  *reinterpret_cast<float4*>(master + o) = w4;
+  *reinterpret_cast<float4*>(mom + o) = m4;
+  *reinterpret_cast<uint2*>(wbf + o) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -1336,6 +1380,33 @@ hipError_t arena_mt_copy_scale(float* const* ptrs, const long long* offs, const 
     if (blocks == 0) continue;
     hipLaunchKernelGGL(mt_copy_scale_kernel, dim3(blocks), dim3(256), 0, stream, a, flat, scale,
                        dir);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+// grads[i]: bf16 gradient pointers; offs/ns: segment offsets (multiples of 4) and sizes (n % 4 == 0).
+hipError_t arena_mt_sgd_master(const void* const* grads, const long long* offs, const long long* ns,
+                               int count, float* master, float* mom, void* wbf, float lr, float mu,
+                               float wd, hipStream_t stream) {
+  for (int base = 0; base < count; base += kMtMax) {
+    MtArgs a;
+    const int cnt = std::min(kMtMax, count - base);
+    int blocks = 0;
+    for (int i = 0; i < cnt; ++i) {
+      if (ns[base + i] % 4 || offs[base + i] % 4) return hipErrorInvalidValue;
+      a.ptr[i] = const_cast<float*>(reinterpret_cast<const float*>(grads[base + i]));
+      a.off[i] = offs[base + i];
+      a.n[i] = ns[base + i];
+      a.blk_begin[i] = blocks;
+      blocks += (int)((ns[base + i] + 1023) / 1024);
+    }
+    a.blk_begin[cnt] = blocks;
+    a.count = cnt;
+    if (blocks == 0) continue;
+    hipLaunchKernelGGL(mt_sgd_master_kernel, dim3(blocks), dim3(256), 0, stream, a, master, mom,
+                       reinterpret_cast<uint16_t*>(wbf), lr, mu, wd);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
