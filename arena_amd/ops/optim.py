@@ -76,7 +76,20 @@ class MasterSGD:
                                 momentum=self.momentum, weight_decay=self.weight_decay)
 
     def state_dict(self) -> dict:
-        return {"master": self.master, "momentum_buffer": self.mom, "lr": self.lr}
+        """fp32 masters + momentum (the bf16 parameters are derived from the masters)."""
+        return {"master": self.master.clone(), "momentum_buffer": self.mom.clone(),
+                "lr": self.lr, "momentum": self.momentum, "weight_decay": self.weight_decay}
+
+    @torch.no_grad()
+    def load_state_dict(self, state: dict) -> None:
+        if state["master"].numel() != self.master.numel():
+            raise ValueError("MasterSGD state does not match this parameter set")
+        self.master.copy_(state["master"])
+        self.mom.copy_(state["momentum_buffer"])
+        self.lr = float(state["lr"])
+        self.momentum = float(state.get("momentum", self.momentum))
+        self.weight_decay = float(state.get("weight_decay", self.weight_decay))
+        self.wbf.copy_(self.master)   # bf16 weights are views into wbf
 
 
 class OptimizerGroup:
@@ -92,3 +105,10 @@ class OptimizerGroup:
     def step(self) -> None:
         for o in self.opts:
             o.step()
+
+    def state_dict(self) -> dict:
+        return {"opts": [o.state_dict() for o in self.opts]}
+
+    def load_state_dict(self, state: dict) -> None:
+        for o, st in zip(self.opts, state["opts"]):
+            o.load_state_dict(st)

@@ -60,6 +60,24 @@ def test_optimizer_group_and_checks():
         MasterSGD([torch.nn.Parameter(torch.zeros(3))], lr=0.1)
 
 
+def test_master_sgd_state_roundtrip():
+    ps = _params("cpu")
+    opt = MasterSGD(ps, lr=0.1, momentum=0.9)
+    for p in ps:
+        p.grad = torch.ones(p.shape, dtype=torch.bfloat16).contiguous(
+            memory_format=torch.channels_last if p.dim() == 4 and p.is_contiguous(
+                memory_format=torch.channels_last) else torch.contiguous_format)
+    opt.step()
+    st = opt.state_dict()
+    ps2 = _params("cpu")
+    opt2 = MasterSGD(ps2, lr=0.5)
+    opt2.load_state_dict(st)
+    assert opt2.lr == 0.1 and opt2.momentum == 0.9
+    for a, b in zip(ps, ps2):
+        assert torch.equal(a, b)
+    assert torch.equal(opt2.mom, opt.mom)
+
+
 @pytest.mark.gpu
 def test_master_sgd_kernel_matches_torch_sgd_gpu():
     from arena_amd.ops import _ext
