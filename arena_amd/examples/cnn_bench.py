@@ -77,6 +77,9 @@ def build(args, dev, world):
         and getattr(args, "dtype", "bf16") == "bf16" and all(p.numel() % 4 == 0 for p in decay))
     if master and world > 1:
         raise SystemExit("--master_weights on is single-rank only (DP buckets carry fp32 grads)")
+    if master and (getattr(args, "dtype", "bf16") != "bf16" or dev.type != "cuda"):
+        raise SystemExit("--master_weights on needs --dtype bf16 on a GPU (the weights become "
+                         "bf16 and the update runs in the HIP multi-tensor kernel)")
     if master:
         # conv/fc weights live in bf16 (fp32 masters inside MasterSGD): no per-step casts
         from ..ops.optim import MasterSGD, OptimizerGroup

@@ -67,29 +67,83 @@ class MasterSGD:
             g = p.grad
             if g is None:
                 continue
-            if g.dtype != torch.bfloat16 or g.stride() != p.stride():
-                raise RuntimeError("MasterSGD: gradient must be bf16 with the parameter's strides")
+            if g.dtype != torch.bfloat16 or not _same_memory_order(g, p):
+                raise RuntimeError("MasterSGD: gradient must be bf16 with the parameter's strides "
+                                   f"(param {tuple(p.shape)} strides {p.stride()}, grad "
+                                   f"{g.dtype} strides {g.stride()})")
             grads.append(g)
             offs.append(off)
         if grads:
             fused.mt_sgd_master(grads, offs, self.master, self.mom, self.wbf, lr=self.lr,
                                 momentum=self.momentum, weight_decay=self.weight_decay)
 
+    def _views(self, flat: Tensor):
+        return [flat.as_strided(p.shape, p.stride(), off) for p, off in zip(self.params,
+                                                                            self.offsets)]
+
+    @torch.no_grad()
+    def sync_from_params(self) -> None:
+        """Re-derive the fp32 masters from the current (bf16) parameter values.
+
+        Call this after ``model.load_state_dict(...)`` on a model whose optimizer already exists:
+        otherwise the next :meth:`step` overwrites the loaded weights with the stale masters.
+        (Momentum is left as is; load the optimizer state too to restore it.)"""
+        for p, m, w in zip(self.params, self._views(self.master), self._views(self.wbf)):
+            if p.data_ptr() != w.data_ptr():
+                # the parameter's data was re-bound (``p.data = t``): adopt its values and
+                # make it a view into the flat bf16 buffer again. (``load_state_dict(...,
+                # assign=True)`` replaces the Parameter objects themselves; like any torch
+                # optimizer, MasterSGD must then be rebuilt.)
+                w.copy_(p)
+                p.data = w
+            m.copy_(p)
+
+    def master_params(self) -> List[Tensor]:
+        """fp32 master weights, one tensor per parameter in logical (contiguous) layout."""
+        return [m.contiguous() for m in self._views(self.master)]
+
     def state_dict(self) -> dict:
-        """fp32 masters + momentum (the bf16 parameters are derived from the masters)."""
-        return {"master": self.master.clone(), "momentum_buffer": self.mom.clone(),
+        """fp32 masters + momentum, one tensor per parameter in LOGICAL layout (independent of
+        channels_last strides), so a checkpoint moves between NHWC and NCHW runs and CPU/GPU."""
+        return {"master": self.master_params(),
+                "momentum_buffer": [m.contiguous() for m in self._views(self.mom)],
+                "shapes": [tuple(p.shape) for p in self.params],
                 "lr": self.lr, "momentum": self.momentum, "weight_decay": self.weight_decay}
 
     @torch.no_grad()
     def load_state_dict(self, state: dict) -> None:
-        if state["master"].numel() != self.master.numel():
-            raise ValueError("MasterSGD state does not match this parameter set")
-        self.master.copy_(state["master"])
-        self.mom.copy_(state["momentum_buffer"])
+        masters, moms = state["master"], state["momentum_buffer"]
+        if isinstance(masters, Tensor) or isinstance(moms, Tensor):
+            raise ValueError("MasterSGD state is in the old flat format (memory-order dependent); "
+                             "re-save it with this version")
+        n = len(self.params)
+        if len(masters) != n or len(moms) != n:
+            raise ValueError(f"MasterSGD state holds {len(masters)} masters / {len(moms)} momentum "
+                             f"buffers for {n} parameters")
+        for i, (p, a, b) in enumerate(zip(self.params, masters, moms)):
+            if tuple(a.shape) != tuple(p.shape) or tuple(b.shape) != tuple(p.shape):
+                raise ValueError(f"MasterSGD state: parameter {i} has shape {tuple(p.shape)}, "
+                                 f"state has {tuple(a.shape)} / {tuple(b.shape)}")
+        for m, a in zip(self._views(self.master), masters):
+            m.copy_(a)
+        for m, b in zip(self._views(self.mom), moms):
+            m.copy_(b)
         self.lr = float(state["lr"])
         self.momentum = float(state.get("momentum", self.momentum))
         self.weight_decay = float(state.get("weight_decay", self.weight_decay))
         self.wbf.copy_(self.master)   # bf16 weights are views into wbf
+
+
+def _same_memory_order(g: Tensor, p: Tensor) -> bool:
+    """True if ``g`` is dense and walks memory in the same element order as ``p``.
+
+    Strides of size-1 dims are irrelevant (autograd's AccumulateGrad keeps such gradients as they
+    come: a channels_last gradient of a [Cout, Cin, 1, 1] weight is contiguous in both senses)."""
+    if g.shape != p.shape:
+        return False
+    if not (g.is_contiguous() or g.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    return all(gs == ps for gs, ps, n in zip(g.stride(), p.stride(), p.shape) if n > 1)
 
 
 class OptimizerGroup:
@@ -110,5 +164,8 @@ class OptimizerGroup:
         return {"opts": [o.state_dict() for o in self.opts]}
 
     def load_state_dict(self, state: dict) -> None:
+        if len(state["opts"]) != len(self.opts):
+            raise ValueError(f"OptimizerGroup state holds {len(state['opts'])} optimizers, "
+                             f"this group has {len(self.opts)}")
         for o, st in zip(self.opts, state["opts"]):
             o.load_state_dict(st)

@@ -78,6 +78,84 @@ def test_master_sgd_state_roundtrip():
     assert torch.equal(opt2.mom, opt.mom)
 
 
+def test_master_sgd_state_is_layout_independent():
+    """A checkpoint saved from a channels_last (NHWC) run loads into a contiguous (NCHW) model
+    with the same logical weights and momentum (advisor r1: flat memory-order state)."""
+    ps = _params("cpu")                       # mixes channels_last and contiguous 4-D weights
+    opt = MasterSGD(ps, lr=0.1, momentum=0.9)
+    g = torch.Generator().manual_seed(5)
+    for p in ps:
+        p.grad = torch.randn(p.shape, generator=g).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last if p.dim() == 4 and p.is_contiguous(
+                memory_format=torch.channels_last) else torch.contiguous_format)
+    opt.step()
+    st = opt.state_dict()
+    assert all(t.is_contiguous() for t in st["master"] + st["momentum_buffer"])
+    ps2 = [torch.nn.Parameter(p.detach().float().contiguous()) for p in _params("cpu")]
+    opt2 = MasterSGD(ps2, lr=0.5)
+    opt2.load_state_dict(st)
+    for a, b, ma, mb in zip(ps, ps2, opt.master_params(), opt2.master_params()):
+        assert b.is_contiguous()
+        assert torch.equal(a, b) and torch.equal(ma, mb)
+    for (pa, oa), (pb, ob) in zip(zip(ps, opt.offsets), zip(ps2, opt2.offsets)):
+        ma = opt.mom.as_strided(pa.shape, pa.stride(), oa)
+        mb = opt2.mom.as_strided(pb.shape, pb.stride(), ob)
+        assert torch.equal(ma, mb)
+    # a state for a different parameter set is refused (same total numel is not enough)
+    ps3 = [torch.nn.Parameter(torch.zeros(8, 4)), torch.nn.Parameter(torch.zeros(4, 8))]
+    st3 = MasterSGD(ps3, lr=0.1).state_dict()
+    ps4 = [torch.nn.Parameter(torch.zeros(4, 8)), torch.nn.Parameter(torch.zeros(8, 4))]
+    with pytest.raises(ValueError, match="shape"):
+        MasterSGD(ps4, lr=0.1).load_state_dict(st3)
+    with pytest.raises(ValueError, match="2 masters"):
+        MasterSGD(ps4[:1], lr=0.1).load_state_dict(st3)
+
+
+def test_master_sgd_accepts_1x1_channels_last_grad():
+    """AccumulateGrad keeps a gradient whose strides differ only on size-1 dims: for a 1x1 conv
+    weight a channels_last gradient has the same memory order as a contiguous parameter."""
+    p = torch.nn.Parameter(torch.randn(16, 8, 1, 1))
+    ref = torch.nn.Parameter(p.detach().clone())
+    opt = MasterSGD([p], lr=0.1, momentum=0.9)
+    g = torch.empty_strided((16, 8, 1, 1), (8, 1, 8, 8), dtype=torch.bfloat16)  # channels_last
+    g.copy_(torch.randn(16, 8, 1, 1))
+    assert g.stride() != p.stride()
+    p.grad = g
+    opt.step()
+    ref.grad = g.float()
+    torch.optim.SGD([ref], lr=0.1, momentum=0.9).step()
+    torch.testing.assert_close(opt.master_params()[0], ref.detach())
+
+
+def test_master_sgd_sync_from_params_after_model_load():
+    """model.load_state_dict after the optimizer exists: sync_from_params makes the next step
+    start from the loaded weights instead of the stale masters."""
+    model = torch.nn.Linear(8, 4, bias=False)
+    opt = MasterSGD(model.parameters(), lr=0.1)
+    new = {"weight": torch.full((4, 8), 0.5)}
+    model.load_state_dict(new)
+    opt.sync_from_params()
+    model.weight.grad = torch.ones(4, 8, dtype=torch.bfloat16)
+    opt.step()
+    torch.testing.assert_close(model.weight.float(), torch.full((4, 8), 0.4), rtol=0, atol=2e-3)
+    # re-binding the parameter's data: sync adopts it as a view of the flat buffer again
+    model.weight.data = torch.full((4, 8), 0.25, dtype=torch.bfloat16)
+    opt.sync_from_params()
+    assert model.weight.data_ptr() == opt.wbf.data_ptr()
+    model.weight.grad = torch.zeros(4, 8, dtype=torch.bfloat16)
+    opt.step()
+    torch.testing.assert_close(model.weight.float(), torch.full((4, 8), 0.25))
+
+
+def test_optimizer_group_state_count_checked():
+    ps = _params("cpu")
+    grp = OptimizerGroup(MasterSGD(ps[:2], lr=0.1), torch.optim.SGD(ps[2:], lr=0.1))
+    st = grp.state_dict()
+    st["opts"] = st["opts"][:1]
+    with pytest.raises(ValueError, match="1 optimizers"):
+        grp.load_state_dict(st)
+
+
 @pytest.mark.gpu
 def test_master_sgd_kernel_matches_torch_sgd_gpu():
     from arena_amd.ops import _ext
