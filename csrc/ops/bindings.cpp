@@ -47,6 +47,9 @@ void arena_ccl_shard(long long, int, int, long long*, long long*);
 void arena_ccl_set_block_elems(long long);
 void arena_ccl_set_oneshot_max(long long);
 long long arena_ccl_get_oneshot_max();
+// csrc/ops/conv_kernels.hip
+hipError_t arena_conv_fwd(const void*, const void*, void*, int, int, int, int, int, int, int, int,
+                          int, int, hipStream_t);
 // csrc/ops/bn_kernels.hip
 long long arena_bn_workspace_floats(long long, int);
 void arena_bn_set_reduce_geometry(long long, long long);
@@ -752,6 +755,36 @@ void pool_check(const Tensor& t, const char* name) {
 }
 
 // Returns (y, pos): pos = uint8 in-window argmax, same NHWC layout as y.
+// NHWC bf16 implicit-GEMM convolution (csrc/ops/conv_kernels.hip). x: [N,C,H,W] channels_last,
+// w: [Cout,C,R,S] channels_last (memory order [Cout][R][S][C]).
+Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4,
+              "conv_fwd: x and w must be 4-D GPU tensors");
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16,
+              "conv_fwd: bfloat16 only");
+  TORCH_CHECK(x.device() == w.device(), "conv_fwd: x and w on different devices");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_fwd: x and w must be channels_last contiguous");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = w.size(0), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(w.size(1) == C, "conv_fwd: weight has ", w.size(1), " input channels, x has ", C);
+  TORCH_CHECK(C % 64 == 0 && Cout % 64 == 0, "conv_fwd: C and Cout must be multiples of 64");
+  TORCH_CHECK(stride >= 1 && pad >= 0 && H + 2 * pad >= R && W + 2 * pad >= S,
+              "conv_fwd: bad stride/padding");
+  TORCH_CHECK(variant >= 0 && variant <= 3 && ((variant & 1) || Cout % 128 == 0),
+              "conv_fwd: variant ", variant, " needs Cout % 128 == 0");
+  const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_fwd: too many output pixels");
+  Tensor y = torch::empty({N, Cout, Ho, Wo},
+                          x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_hip(arena_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W,
+                           (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad, (int)variant,
+                           cur_stream()),
+            "conv_fwd");
+  return y;
+}
+
 std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
   pool_check(x, "x");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
@@ -864,6 +897,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_fwd", &linear_fwd);
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
+  m.def("conv_fwd", &conv_fwd);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {

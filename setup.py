@@ -20,6 +20,7 @@ if ARCH != "gfx950":
     raise SystemExit(f"arena_amd targets MI355X only (gfx950); PYTORCH_ROCM_ARCH={ARCH}")
 
 HIP_SOURCES = ["csrc/ops/mlp_kernels.hip", "csrc/ops/bn_kernels.hip", "csrc/ops/pool_kernels.hip",
+               "csrc/ops/conv_kernels.hip",
                "csrc/ccl/xgmi_ccl.hip"]
 # ARENA_TIMELINE=1: instrumented build for scripts/timeline.py (never the default)
 TIMELINE = ["-DARENA_TIMELINE"] if os.environ.get("ARENA_TIMELINE") == "1" else []
