@@ -217,6 +217,11 @@ def main(argv=None) -> int:
                               "dtype": args.dtype, "comm": getattr(opt, "comm", "none"),
                               "exec": "hipgraph" if graph is not None else "eager",
                               "final_loss": round(float(loss), 4)}), flush=True)
+    if rank == 0 and os.environ.get("ARENA_CONV_LOG"):
+        from ..ops import conv
+        for key, plan in conv.plans().items():
+            print(f"conv {key[0]} w{key[1]} s{key[2]} p{key[3]}: fwd={plan.fwd} bwd={plan.bwd} "
+                  f"wgrad={plan.wgrad} {plan.times}", file=sys.stderr)
     hvd.shutdown()
     return 0
 

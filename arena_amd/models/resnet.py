@@ -8,7 +8,8 @@ one: a 7x7 stem, 4 stages of bottleneck blocks with the stride on the 3x3 conv (
 average pooling, and a 1000-way FC. ``width``/``depth`` knobs give tiny variants for CPU tests.
 
 MI355X layout: the model is meant to run with ``memory_format=torch.channels_last`` under bf16
-autocast, so the MIOpen convolutions take their NHWC MFMA paths. Each BatchNorm, with its ReLU
+autocast. Every convolution is a ``Conv2dNHWC``: per shape and direction it runs the faster of
+the hand-written MFMA implicit-GEMM kernels (``csrc/ops/conv_kernels.hip``) and MIOpen. Each BatchNorm, with its ReLU
 and residual add, is one fused HIP kernel pair per direction (``arena_amd.ops.batchnorm``).
 Parameters stay fp32 (master weights) for the data-parallel buckets and the optimizer.
 """
@@ -20,6 +21,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
+from ..ops.conv import Conv2dNHWC
 from ..ops.pool import MaxPool2dNHWC
 
 DEPTHS = {"resnet50": [3, 4, 6, 3], "resnet101": [3, 4, 23, 3],
@@ -35,29 +37,35 @@ class Bottleneck(nn.Module):
     def __init__(self, cin: int, mid: int, stride: int):
         super().__init__()
         cout = mid * self.expansion
-        self.conv1 = nn.Conv2d(cin, mid, 1, bias=False)
+        self.conv1 = Conv2dNHWC(cin, mid, 1, bias=False)
         self.bn1 = BatchNormAct2d(mid, act="relu")
-        self.conv2 = nn.Conv2d(mid, mid, 3, stride=stride, padding=1, bias=False)
+        self.conv2 = Conv2dNHWC(mid, mid, 3, stride=stride, padding=1, bias=False)
         self.bn2 = BatchNormAct2d(mid, act="relu")
-        self.conv3 = nn.Conv2d(mid, cout, 1, bias=False)
+        self.conv3 = Conv2dNHWC(mid, cout, 1, bias=False)
         self.bn3 = BatchNormAct2d(cout, act="relu")
         nn.init.zeros_(self.bn3.weight)  # zero-init the residual branch's last BN (goyal et al.)
         self.down_conv = self.down_bn = None
         if stride != 1 or cin != cout:
-            self.down_conv = nn.Conv2d(cin, cout, 1, stride=stride, bias=False)
+            self.down_conv = Conv2dNHWC(cin, cout, 1, stride=stride, bias=False)
             self.down_bn = BatchNormAct2d(cout, act="none")
 
     def forward(self, x):
-        idt = x if self.down_conv is None else self.down_bn(self.down_conv(x))
-        y = self.bn1(self.conv1(x))
-        y = self.bn2(self.conv2(y))
-        return self.bn3(self.conv3(y), residual=idt)
+        # forward_stats: when a conv runs on the MFMA kernel, its epilogue also produces the
+        # BatchNorm statistics partials of its output, and the BN skips its statistics pass
+        idt = x
+        if self.down_conv is not None:
+            y, st = self.down_conv.forward_stats(x)
+            idt = self.down_bn(y, stats=st)
+        y, st = self.conv1.forward_stats(x)
+        y, st = self.conv2.forward_stats(self.bn1(y, stats=st))
+        y, st = self.conv3.forward_stats(self.bn2(y, stats=st))
+        return self.bn3(y, residual=idt, stats=st)
 
 
 class ResNet(nn.Module):
     def __init__(self, depths: List[int], num_classes: int = 1000, width: int = 64):
         super().__init__()
-        self.stem = nn.Sequential(nn.Conv2d(3, width, 7, stride=2, padding=3, bias=False),
+        self.stem = nn.Sequential(Conv2dNHWC(3, width, 7, stride=2, padding=3, bias=False),
                                   BatchNormAct2d(width, act="relu"),
                                   MaxPool2dNHWC(3, stride=2, padding=1))
         layers = []

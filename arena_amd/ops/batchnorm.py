@@ -53,10 +53,11 @@ def reference(x, residual, weight, bias, running_mean, running_var, training, mo
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum,
-                eps, relu, num_batches=None):
+                eps, relu, num_batches=None, stats=None):
         ext = _ext.load()
+        part, rpb = stats if (stats is not None and training) else (None, 0)
         y, mean, invstd = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
-                                     training, momentum, eps, relu, num_batches)
+                                     training, momentum, eps, relu, num_batches, part, rpb)
         ctx.save_for_backward(x, y, mean, invstd, weight)
         ctx.relu, ctx.has_res, ctx.training = relu, residual is not None, training
         ctx.affine = weight is not None
@@ -72,7 +73,7 @@ class _BNActFn(torch.autograd.Function):
         dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, y, x, mean, invstd, weight, ctx.relu,
                                                      ctx.has_res, ctx.affine)
         return (dx, dres if ctx.has_res else None, dgamma if ctx.affine else None,
-                dbeta if ctx.affine else None, None, None, None, None, None, None, None)
+                dbeta if ctx.affine else None, None, None, None, None, None, None, None, None)
 
 
 def bn_act(x, residual=None, weight=None, bias=None, running_mean=None, running_var=None,
@@ -94,7 +95,10 @@ class BatchNormAct2d(nn.BatchNorm2d):
             raise ValueError(f"act must be 'relu' or 'none', got {act!r}")
         self.relu = act == "relu"
 
-    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None) -> torch.Tensor:
+    def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
+                stats=None) -> torch.Tensor:
+        """``stats``: BatchNorm partials of ``x`` from the producing ``Conv2dNHWC.forward_stats``
+        (skips the statistics pass over x; training mode on the fused kernels only)."""
         training = self.training or not self.track_running_stats
         tracking = self.training and self.track_running_stats
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
@@ -105,7 +109,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
             # num_batches_tracked += 1 happens inside the statistics finalize kernel
             return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, True,
                                   self.momentum, self.eps, self.relu,
-                                  self.num_batches_tracked if tracking else None)
+                                  self.num_batches_tracked if tracking else None, stats)
         if tracking:
             self.num_batches_tracked.add_(1)
         mom = self.momentum if self.momentum is not None else \

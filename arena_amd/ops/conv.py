@@ -54,14 +54,22 @@ def pick_variant(m: int, cout: int) -> int:
     return best
 
 
-def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int = -1) -> Tensor:
-    """y = conv2d(x, w) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S]."""
+def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int = -1,
+               with_stats: bool = False):
+    """y = conv2d(x, w) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S].
+
+    with_stats: returns (y, (part, rpb)) where part holds per-tile BatchNorm partials of y
+    (tile mean and sum of squared deviations per channel, ``rpb`` output pixels per tile), which
+    ``BatchNormAct2d(..., stats=...)`` finalizes instead of re-reading y."""
     x = x.contiguous(memory_format=torch.channels_last)
     w = w.contiguous(memory_format=torch.channels_last)
     if variant < 0:
         ho, wo = out_hw(x.shape[2], x.shape[3], w.shape[2], w.shape[3], stride, pad)
         variant = pick_variant(x.shape[0] * ho * wo, w.shape[0])
-    return _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant))
+    out = _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant), bool(with_stats))
+    if with_stats:
+        return out[0], (out[1], TILES[variant][0])
+    return out[0]
 
 
 def flip_weight(w: Tensor) -> Tensor:
@@ -73,3 +81,223 @@ def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1) -> Tenso
     """dX of a stride-1 convolution (same spatial size when pad = (R-1)/2)."""
     r = w.shape[2]
     return conv2d_fwd(dy, flip_weight(w), 1, r - 1 - pad, variant)
+
+
+WGRAD_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}   # Cout x R*S*C
+
+
+def wgrad_variants_for(cin: int, cout: int):
+    return [v for v, (bm, bn) in WGRAD_TILES.items() if cout % bm == 0 and cin % bn == 0]
+
+
+def conv2d_wgrad(x: Tensor, dy: Tensor, kernel: Tuple[int, int], stride: int = 1, pad: int = 0,
+                 variant: int = -1, splits: int = 0, out_dtype=torch.bfloat16,
+                 scale: float = 1.0) -> Tensor:
+    """dW [Cout, C, R, S] (channels_last) of y = conv2d(x, w): split-K MFMA kernel + a
+    fixed-order slab reduction (bit-reproducible)."""
+    x = x.contiguous(memory_format=torch.channels_last)
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    if variant < 0:
+        variant = wgrad_variants_for(x.shape[1], dy.shape[1])[0]
+    return _ext.load().conv_wgrad(x, dy, int(kernel[0]), int(kernel[1]), int(stride), int(pad),
+                                  int(variant), int(splits), out_dtype == torch.float32,
+                                  float(scale))
+
+
+# ------------------------------------------------------------------------------------------------
+# Per-shape plan: for each of forward / backward-data / backward-weight, the fastest of MIOpen and
+# the kernel's tile variants (and split counts), timed once on the live device (like
+# cudnn.benchmark, which this complements). ARENA_CONV=miopen forces the library everywhere,
+# ARENA_CONV=ours forces the kernel wherever it applies (heuristic tiles, no timing).
+# ------------------------------------------------------------------------------------------------
+import os  # noqa: E402
+from dataclasses import dataclass, field  # noqa: E402
+from typing import Dict, Optional  # noqa: E402
+
+import torch.nn.functional as F  # noqa: E402
+from torch import nn  # noqa: E402
+
+MIOPEN = "miopen"
+
+
+_MODE_OVERRIDE: Optional[str] = None
+
+
+def set_mode(mode: Optional[str]) -> None:
+    """Process-wide override of ARENA_CONV (auto | ours | miopen | off; None = use the env)."""
+    global _MODE_OVERRIDE
+    if mode not in (None, "auto", "ours", MIOPEN, "off"):
+        raise ValueError(f"unknown conv mode {mode!r}")
+    _MODE_OVERRIDE = mode
+
+
+def _mode() -> str:
+    return _MODE_OVERRIDE or os.environ.get("ARENA_CONV", "auto")
+
+
+@dataclass
+class ConvPlan:
+    fwd: object = MIOPEN            # MIOPEN or a tile variant
+    bwd: object = MIOPEN
+    wgrad: object = MIOPEN          # MIOPEN or (variant, splits)
+    tuned: bool = False
+    times: Dict[str, float] = field(default_factory=dict)
+
+
+_PLANS: Dict[tuple, ConvPlan] = {}
+
+
+def _time(fn, reps: int = 5) -> float:
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    fn()
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) * 1e3 / reps
+
+
+def _miopen_bwd(dy, x, w, stride, pad, mask):
+    return torch.ops.aten.convolution_backward(dy, x, w, None, [stride, stride], [pad, pad],
+                                               [1, 1], False, [0, 0], 1, mask)
+
+
+def _wgrad_candidates(cin, cout, k):
+    """(tile variant, split count) pairs: splits that give ~1, 2 or 4 blocks per CU."""
+    out = []
+    for v in wgrad_variants_for(cin, cout):
+        bm, bn = WGRAD_TILES[v]
+        tiles = (cout // bm) * (k[0] * k[1] * cin // bn)
+        for blocks in (_CUS, 2 * _CUS, 4 * _CUS):
+            out.append((v, max(1, -(-blocks // tiles))))
+    return sorted(set(out))
+
+
+def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode())
+    plan = _PLANS.get(key)
+    if plan is not None and (plan.tuned or torch.cuda.is_current_stream_capturing()):
+        return plan
+    mode = _mode()
+    plan = plan or ConvPlan()
+    cin, cout, k = w.shape[1], w.shape[0], (w.shape[2], w.shape[3])
+    ok = kernel_ok(x, w, stride, pad)
+    ho, wo = out_hw(x.shape[2], x.shape[3], k[0], k[1], stride, pad)
+    wg = _wgrad_candidates(cin, cout, k) if ok else []
+    if mode == MIOPEN or not ok:
+        plan.tuned = True
+    elif mode == "ours" or torch.cuda.is_current_stream_capturing():
+        plan.fwd = pick_variant(x.shape[0] * ho * wo, cout)
+        plan.bwd = pick_variant(x.shape[0] * x.shape[2] * x.shape[3], cin) if stride == 1 else MIOPEN
+        plan.wgrad = wg[len(wg) // 2] if wg else MIOPEN
+        plan.tuned = mode == "ours"
+    else:
+        y = F.conv2d(x, w, stride=stride, padding=pad)
+        dy = torch.randn_like(y)
+        t = {}
+        # the kernel's forward also produces the BatchNorm statistics of y (every conv of the
+        # model family feeds a BN), which saves the BN's statistics pass over y: charge MIOpen
+        # for that pass (one HBM read of y at ~4.5 TB/s plus a launch)
+        stats_pass = y.numel() * y.element_size() / 4.5e6 + 3.0
+        t[("fwd", MIOPEN)] = _time(lambda: F.conv2d(x, w, stride=stride, padding=pad)) + \
+            stats_pass
+        for v in variants_for(cout):
+            t[("fwd", v)] = _time(lambda: conv2d_fwd(x, w, stride, pad, v, with_stats=True))
+        t[("bwd", MIOPEN)] = _time(lambda: _miopen_bwd(dy, x, w, stride, pad, [True, False, False]))
+        if stride == 1:
+            for v in variants_for(cin):
+                t[("bwd", v)] = _time(lambda: conv2d_bwd_data(dy, w, pad, v))
+        t[("wgrad", MIOPEN)] = _time(lambda: _miopen_bwd(dy, x, w, stride, pad,
+                                                         [False, True, False]))
+        for c in wg:
+            t[("wgrad", c)] = _time(lambda: conv2d_wgrad(x, dy, k, stride, pad, c[0], c[1]))
+        for kind in ("fwd", "bwd", "wgrad"):
+            best = min((v for (kd, _), v in t.items() if kd == kind))
+            choice = next(c for (kd, c), v in t.items() if kd == kind and v == best)
+            setattr(plan, kind, choice)
+        plan.times = {f"{kd}:{c}": round(v, 1) for (kd, c), v in t.items()}
+        plan.tuned = True
+    _PLANS[key] = plan
+    return plan
+
+
+def plans() -> Dict[tuple, ConvPlan]:
+    """The per-shape choices made so far (for logs and profiles)."""
+    return dict(_PLANS)
+
+
+class _ConvFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, w, stride, pad, plan, want_stats):
+        part = x.new_empty(0, dtype=torch.float32)
+        if plan.fwd == MIOPEN:
+            y = F.conv2d(x, w, stride=stride, padding=pad)
+        elif want_stats:
+            y, (part, _) = conv2d_fwd(x, w, stride, pad, plan.fwd, with_stats=True)
+        else:
+            y = conv2d_fwd(x, w, stride, pad, plan.fwd)
+        ctx.save_for_backward(x, w)
+        ctx.conf = (stride, pad, plan)
+        ctx.mark_non_differentiable(part)
+        return y, part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        x, w = ctx.saved_tensors
+        stride, pad, plan = ctx.conf
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = dw = None
+        if ctx.needs_input_grad[0]:
+            if plan.bwd == MIOPEN:
+                dx = _miopen_bwd(dy, x, w, stride, pad, [True, False, False])[0]
+            else:
+                dx = conv2d_bwd_data(dy, w, pad, plan.bwd)
+        if ctx.needs_input_grad[1]:
+            if plan.wgrad == MIOPEN:
+                dw = _miopen_bwd(dy, x, w, stride, pad, [False, True, False])[1]
+            else:
+                v, sp = plan.wgrad
+                dw = conv2d_wgrad(x, dy, (w.shape[2], w.shape[3]), stride, pad, v, sp,
+                                  out_dtype=w.dtype)
+        return dx, dw, None, None, None, None
+
+
+class Conv2dNHWC(nn.Conv2d):
+    """``nn.Conv2d`` (no bias, no groups/dilation) that runs channels_last bf16 convolutions on
+    the MFMA implicit-GEMM kernels when they are faster than MIOpen for the shape (timed once
+    per shape). Under bf16 autocast the weight/input casts happen here, as autocast would do
+    them. Everything else (CPU, fp32, unsupported shapes) is plain ``nn.Conv2d``."""
+
+    def __init__(self, *args, **kw):
+        super().__init__(*args, **kw)
+        if isinstance(self.padding, str) or self.bias is not None or self.groups != 1 or \
+                self.dilation != (1, 1) or self.stride[0] != self.stride[1] or \
+                self.padding[0] != self.padding[1]:
+            raise ValueError("Conv2dNHWC: square stride/padding, no bias, groups or dilation")
+
+    def forward(self, x: Tensor) -> Tensor:
+        return self.forward_stats(x, want_stats=False)[0]
+
+    def forward_stats(self, x: Tensor, want_stats: bool = True):
+        """(y, stats): ``stats`` are the BatchNorm partials of y for ``BatchNormAct2d(y,
+        stats=stats)`` when the kernel produced y (else None: the BN computes them itself)."""
+        if not x.is_cuda or _mode() == "off":
+            return super().forward(x), None
+        amp = torch.is_autocast_enabled("cuda") and \
+            torch.get_autocast_dtype("cuda") == torch.bfloat16
+        w = self.weight
+        if amp:
+            x = x.to(torch.bfloat16)
+            w = w.to(torch.bfloat16)
+        if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+            return super().forward(x), None
+        x = x.contiguous(memory_format=torch.channels_last)
+        w = w.contiguous(memory_format=torch.channels_last)
+        s, p = self.stride[0], self.padding[0]
+        plan = plan_for(x, w, s, p)
+        want = want_stats and plan.fwd != MIOPEN and torch.is_grad_enabled() and self.training
+        with torch.autocast("cuda", enabled=False):
+            y, part = _ConvFn.apply(x, w, s, p, plan, want)
+        return y, ((part, TILES[plan.fwd][0]) if want else None)

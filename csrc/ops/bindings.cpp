@@ -48,8 +48,11 @@ void arena_ccl_set_block_elems(long long);
 void arena_ccl_set_oneshot_max(long long);
 long long arena_ccl_get_oneshot_max();
 // csrc/ops/conv_kernels.hip
-hipError_t arena_conv_fwd(const void*, const void*, void*, int, int, int, int, int, int, int, int,
-                          int, int, hipStream_t);
+hipError_t arena_conv_fwd(const void*, const void*, void*, float*, int, int, int, int, int, int,
+                          int, int, int, int, hipStream_t);
+int arena_conv_wgrad_splits(int, int, int, int, int, int, int);
+hipError_t arena_conv_wgrad(const void*, const void*, float*, void*, float*, int, int, int, int,
+                            int, int, int, int, int, int, int, float, hipStream_t);
 // csrc/ops/bn_kernels.hip
 long long arena_bn_workspace_floats(long long, int);
 void arena_bn_set_reduce_geometry(long long, long long);
@@ -59,7 +62,7 @@ hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, i
 hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, int, int, int, int,
                              int, hipStream_t);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, long long, int, int, int, float*,
-                        ArenaBNStats, hipStream_t);
+                        int, long long, ArenaBNStats, hipStream_t);
 hipError_t arena_bn_bwd(int, const void*, const void*, const void*, void*, void*, long long, int,
                         int, float*, ArenaBNBwd, hipStream_t);
 #ifdef ARENA_TIMELINE
@@ -659,9 +662,10 @@ const float* bn_vec(const OptT& t, int C, const char* name) {
 }
 
 // Returns (y, mean, invstd). Eval mode normalises with the running statistics.
+// stats_part/stats_rpb: BatchNorm partials of x from conv_fwd(with_stats=True) (training only).
 std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT running_mean,
                            OptT running_var, bool training, double momentum, double eps,
-                           bool relu, OptT num_batches) {
+                           bool relu, OptT num_batches, OptT stats_part, int64_t stats_rpb) {
   const BNGeom g = bn_geom(x, "x");
   if (res.has_value()) bn_same(x, *res, "residual");
   auto f32 = x.options().dtype(torch::kFloat32);
@@ -690,7 +694,16 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
                   "num_batches_tracked must be an int64 scalar tensor");
       st.batches = reinterpret_cast<long long*>(num_batches->data_ptr<int64_t>());
     }
-    part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
+    if (stats_part.has_value()) {
+      check_f32(*stats_part, "stats_part");
+      TORCH_CHECK(stats_rpb > 0 && stats_part->is_contiguous(), "stats_part: bad layout");
+      const int64_t nblk = (g.M + stats_rpb - 1) / stats_rpb;
+      TORCH_CHECK(stats_part->numel() == nblk * 2 * g.C, "stats_part has ", stats_part->numel(),
+                  " floats, expected ", nblk * 2 * g.C);
+      part = *stats_part;
+    } else {
+      part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
+    }
   } else {
     TORCH_CHECK(running_mean.has_value() && running_var.has_value(),
                 "eval-mode BatchNorm needs running statistics");
@@ -704,7 +717,10 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
   Tensor y = torch::empty_like(x);
   check_hip(arena_bn_fwd(g.dtype, x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr,
                          y.data_ptr(), g.M, g.C, relu ? 1 : 0, training ? 1 : 0,
-                         training ? part.data_ptr<float>() : nullptr, st, cur_stream()),
+                         training ? part.data_ptr<float>() : nullptr,
+                         training && stats_part.has_value()
+                             ? (int)((g.M + stats_rpb - 1) / stats_rpb) : 0,
+                         (long long)stats_rpb, st, cur_stream()),
             "bn_fwd");
   return {y, mean, invstd};
 }
@@ -757,7 +773,10 @@ void pool_check(const Tensor& t, const char* name) {
 // Returns (y, pos): pos = uint8 in-window argmax, same NHWC layout as y.
 // NHWC bf16 implicit-GEMM convolution (csrc/ops/conv_kernels.hip). x: [N,C,H,W] channels_last,
 // w: [Cout,C,R,S] channels_last (memory order [Cout][R][S][C]).
-Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant) {
+// with_stats: also returns the BatchNorm partials of y ([ceil(M/BM)][2][Cout] fp32, BM rows per
+// partial) for bn_fwd(..., stats_part, BM): the BN layer after the conv skips its stats pass.
+std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant,
+                             bool with_stats) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4,
               "conv_fwd: x and w must be 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16,
@@ -778,11 +797,57 @@ Tensor conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_fwd: too many output pixels");
   Tensor y = torch::empty({N, Cout, Ho, Wo},
                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  check_hip(arena_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(), (int)N, (int)H, (int)W,
+  static const int bm[4] = {128, 128, 64, 64};
+  const int64_t m_tiles = (N * Ho * Wo + bm[variant] - 1) / bm[variant];
+  Tensor part = with_stats ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
+                           : Tensor();
+  check_hip(arena_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                           with_stats ? part.data_ptr<float>() : nullptr, (int)N, (int)H, (int)W,
                            (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad, (int)variant,
                            cur_stream()),
             "conv_fwd");
-  return y;
+  if (with_stats) return {y, part};
+  return {y};
+}
+
+// dW of an NHWC convolution: [Cout, C, R, S] channels_last, bf16 (for MasterSGD) or fp32.
+Tensor conv_wgrad(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int64_t pad,
+                  int64_t variant, int64_t splits_hint, bool out_fp32, double scale) {
+  TORCH_CHECK(x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4,
+              "conv_wgrad: x and dy must be 4-D GPU tensors");
+  TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && dy.scalar_type() == torch::kBFloat16,
+              "conv_wgrad: bfloat16 only");
+  TORCH_CHECK(x.device() == dy.device(), "conv_wgrad: x and dy on different devices");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_wgrad: x and dy must be channels_last contiguous");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = dy.size(1);
+  TORCH_CHECK(stride >= 1 && pad >= 0 && R >= 1 && S >= 1 && H + 2 * pad >= R && W + 2 * pad >= S,
+              "conv_wgrad: bad geometry");
+  const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
+  TORCH_CHECK(dy.size(0) == N && dy.size(2) == Ho && dy.size(3) == Wo,
+              "conv_wgrad: dy shape does not match the convolution geometry");
+  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
+  TORCH_CHECK(variant >= 0 && variant <= 3, "conv_wgrad: variant must be 0..3");
+  TORCH_CHECK(C % bn[variant] == 0 && Cout % bm[variant] == 0, "conv_wgrad: variant ", variant,
+              " needs C % ", bn[variant], " == 0 and Cout % ", bm[variant], " == 0");
+  TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad: too many output pixels");
+  const int64_t Ktot = R * S * C;
+  const int splits = arena_conv_wgrad_splits((int)N, (int)Ho, (int)Wo, (int)Cout, (int)Ktot,
+                                             (int)variant, (int)splits_hint);
+  TORCH_CHECK(splits >= 1, "conv_wgrad: bad split count");
+  Tensor ws = torch::empty({(int64_t)splits * Cout * Ktot}, x.options().dtype(torch::kFloat32));
+  Tensor dw = torch::empty({Cout, C, R, S}, x.options()
+                                                .dtype(out_fp32 ? torch::kFloat32 : torch::kBFloat16)
+                                                .memory_format(at::MemoryFormat::ChannelsLast));
+  check_hip(arena_conv_wgrad(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(),
+                             out_fp32 ? nullptr : dw.data_ptr(),
+                             out_fp32 ? dw.data_ptr<float>() : nullptr, (int)N, (int)H, (int)W,
+                             (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad,
+                             (int)variant, (int)splits_hint, (float)scale, cur_stream()),
+            "conv_wgrad");
+  return dw;
 }
 
 std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
@@ -898,6 +963,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd", &bn_fwd);
   m.def("bn_bwd", &bn_bwd);
   m.def("conv_fwd", &conv_fwd);
+  m.def("conv_wgrad", &conv_wgrad);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {

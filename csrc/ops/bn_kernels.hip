@@ -466,11 +466,17 @@ long long arena_bn_workspace_floats(long long M, int C) {
 }
 
 // dtype: 0 = f32, 1 = bf16 (all activation tensors share it)
+// ext_nblk > 0: `part` already holds the statistics partials of x ([ext_nblk][2][C], ext_rpb rows
+// each), written by the producing convolution's epilogue (conv_kernels.hip): no statistics pass.
 hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, long long M, int C,
-                        int relu, int training, float* part, ArenaBNStats st,
-                        hipStream_t stream) {
+                        int relu, int training, float* part, int ext_nblk, long long ext_rpb,
+                        ArenaBNStats st, hipStream_t stream) {
   if (bad_shape(M, C)) return hipErrorInvalidValue;
-  if (training) {
+  if (training && ext_nblk > 0) {
+    if (ext_rpb <= 0 || (long long)ext_nblk * ext_rpb < M) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kT), 0,
+                       stream, part, ext_nblk, M, C, ext_rpb, st);
+  } else if (training) {
     long long rpb;
     const long long nb = reduce_blocks(M, C, &rpb);
     if (dtype == 1)

@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
@@ -48,6 +50,7 @@ struct ConvArgs {
   const uint16_t* x;   // [N][H][W][C] bf16
   const uint16_t* w;   // [Cout][R][S][C] bf16
   uint16_t* y;         // [N][Ho][Wo][Cout] bf16
+  float* part;         // optional BatchNorm partials [m_tiles][2][Cout] (tile mean, tile M2)
   int N, H, W, C, Cout, R, S, stride, pad, Ho, Wo;
   int M;               // N * Ho * Wo
   int Ktot;            // R * S * C
@@ -68,7 +71,22 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
   return ua | ub;
 }
 
-template <int BM, int BN>
+__device__ __forceinline__ float bf16_round(float f) {
+  uint32_t u = __float_as_uint(f);
+  u = (u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u;
+  return __uint_as_float(u);
+}
+
+// sum over the 16 lanes of a DPP row (lane bits 0..3); every lane of the row gets the sum
+__device__ __forceinline__ float row16_sum(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x124, 0xF, 0xF, false));
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));
+  return v;
+}
+
+template <int BM, int BN, bool STATS>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;        // per-wave output tile (2 x 2 waves)
   constexpr int MI = WM / 16, NI = WN / 16;      // 16x16 MFMA tiles per wave
@@ -193,6 +211,53 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
       *reinterpret_cast<uint2*>(yrow + j * 16) = v;
     }
   }
+  if constexpr (STATS) {
+    // BatchNorm statistics of this tile's bf16 outputs, two-pass (mean, then sum of squared
+    // deviations) over the valid rows: the partial format of bn_stats_kernel with rpb = BM, so
+    // the BN layer that consumes this output skips its own statistics pass over HBM.
+    const int nrows = min(BM, a.M - m0);
+    const float inv_n = 1.f / (float)nrows;
+    float* red = reinterpret_cast<float*>(lds);   // [2 (wm)][BN]; staging buffers are free now
+    float mean[NI][4];
+#pragma unroll
+    for (int pass = 0; pass < 2; ++pass) {
+      float s[NI][4];
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float t = 0.f;
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const bool valid = m0 + wm * WM + i * 16 + fr < a.M;
+            const float v = bf16_round(acc[i][j][r]);
+            const float d = pass == 0 ? v : v - mean[j][r];
+            t += valid ? (pass == 0 ? d : d * d) : 0.f;
+          }
+          s[j][r] = row16_sum(t);
+        }
+      __syncthreads();   // previous readers of red (or of the staging buffers) are done
+      if (fr == 0) {
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) red[wm * BN + wn * WN + j * 16 + 4 * fq + r] = s[j][r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wn * WN + j * 16 + 4 * fq + r;
+          const float tot = red[c] + red[BN + c];
+          if (pass == 0) mean[j][r] = tot * inv_n;
+          else if (wm == 0 && fr == 0) {
+            a.part[(size_t)mt * 2 * a.Cout + n0 + c] = mean[j][r];
+            a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = tot;
+          }
+        }
+    }
+  }
 }
 
 template <int BM, int BN>
@@ -201,7 +266,10 @@ hipError_t launch(const ConvArgs& a0, hipStream_t st) {
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
-  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN>), dim3(nwg), dim3(kThreads), 0, st, a);
+  if (a.part)
+    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, true>), dim3(nwg), dim3(kThreads), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, false>), dim3(nwg), dim3(kThreads), 0, st, a);
   return hipGetLastError();
 }
 
@@ -212,8 +280,9 @@ extern "C" {
 // Returns hipErrorInvalidValue for shapes the kernel does not cover (the caller falls back to
 // MIOpen): C % 64 != 0, Cout % 64 != 0, or an unknown tile variant.
 // variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (BM x BN output tile per block).
-hipError_t arena_conv_fwd(const void* x, const void* w, void* y, int N, int H, int W, int C,
-                          int Cout, int R, int S, int stride, int pad, int variant,
+// part (optional): BatchNorm partials of y, [ceil(M / BM)][2][Cout] (see the STATS epilogue).
+hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W,
+                          int C, int Cout, int R, int S, int stride, int pad, int variant,
                           hipStream_t st) {
   if (C % kBK || Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
     return hipErrorInvalidValue;
@@ -221,6 +290,7 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, int N, int H, i
   a.x = (const uint16_t*)x;
   a.w = (const uint16_t*)w;
   a.y = (uint16_t*)y;
+  a.part = part;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
   a.stride = stride; a.pad = pad;
   a.Ho = (H + 2 * pad - R) / stride + 1;
@@ -237,6 +307,289 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, int N, int H, i
     case 3: return launch<64, 64>(a, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+}  // extern "C"
+
+// ================================================================================================
+// Backward-weight: dW[co][r][s][ci] = sum_m dY[m][co] * X[pix(m, r, s)][ci]
+//
+// A GEMM of Cout rows, R*S*C columns and N*Ho*Wo (up to 400k) reduction steps, so the reduction
+// is split over blocks: block (split, co-tile, k-tile) sums 64-pixel steps [split*SPS, ...) into
+// an fp32 slab ws[split][Cout][R*S*C] with plain stores, and conv_wgrad_reduce sums the slabs in
+// a fixed order (bit-reproducible, no float atomics: those run at ~1.3 TB/s, MI355X_MICROARCH.md).
+//
+// Both operands are reduction-strided (a pixel row holds 64..2048 consecutive channels), so the
+// tiles are staged pixel-major ([64 pixels][BM or BN channels], glds, 16-byte chunks permuted per
+// row) and the MFMA fragments are read with ds_read_b64_tr_b16, which hands each lane one channel
+// of 4 consecutive pixels. The permutation moves 32-byte chunk pairs so that the 8 rows one
+// 32-lane half of a transposed read touches sit in 8 distinct 32-byte bank slots.
+// ================================================================================================
+namespace {
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4* lds_s4_t;
+
+struct FastDiv {  // n / d for 0 <= n < 2^31 (Granlund-Montgomery, 32-bit)
+  uint32_t mul, shift, d;
+};
+
+__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) {
+  return (__umulhi(n, f.mul) + n) >> f.shift;
+}
+
+struct WgradArgs {
+  const uint16_t* x;   // [N][H][W][C]
+  const uint16_t* dy;  // [N][Ho][Wo][Cout]
+  float* ws;           // [splits][Cout][Ktot]
+  int N, H, W, C, Cout, R, S, stride, pad, Ho, Wo;
+  int M, Ktot;
+  int m_tiles, n_tiles, splits, sps;  // sps = 64-pixel steps per split
+  FastDiv div_hw, div_w;
+};
+
+// chunk permutation of a pixel row of RB bytes (bit 0 of the chunk index is kept: 32-B pairs)
+template <int RB>
+__device__ __forceinline__ int wswz(int row) {
+  if constexpr (RB == 256) return 2 * ((row & 3) | (((row >> 3) & 1) << 2));
+  else return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
+  constexpr int RA = BM * 2, RBB = BN * 2;        // row bytes of the A (dY) and B (X) images
+  constexpr int CA = RA / 16, CB = RBB / 16;       // 16-byte chunks per row
+  constexpr int kPix = 64;                         // pixels per step
+  constexpr int AI = kPix * CA / kThreads, BI = kPix * CB / kThreads;
+  constexpr int kBuf = kPix * (RA + RBB);
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kBuf];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles = a.m_tiles * a.n_tiles;
+  const int nwg = tiles * a.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  // split-major order: the blocks of one XCD share a pixel range (dY and X rows hit its L2)
+  const int split = lin / tiles, t2 = lin - split * tiles;
+  const int mt = t2 / a.n_tiles, nt = t2 - mt * a.n_tiles;
+  const int co0 = mt * BM, kk0 = nt * BN;
+  const int tap = kk0 / a.C, ci0 = kk0 - tap * a.C;
+  const int rr = tap / a.S, ss = tap - rr * a.S;
+  const int step0 = split * a.sps;
+  const int nsteps = min(a.sps, (a.M + kPix - 1) / kPix - step0);
+
+  // staging: wave-instruction i of this wave fills rows [(wave*I + i) * RPI, +RPI) of the image
+  constexpr int RPI_A = 64 / CA, RPI_B = 64 / CB;  // rows per wave-instruction
+  const int a_row_l = lane / CA, a_pos = lane % CA;
+  const int b_row_l = lane / CB, b_pos = lane % CB;
+
+  auto stage = [&](int step, int buf) {
+    uint8_t* base = lds + buf * kBuf;
+    const int p0 = (step0 + step) * kPix;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int row = (wave * AI + i) * RPI_A + a_row_l;
+      const int m = p0 + row;
+      const void* src = m < a.M ? (const void*)(a.dy + (size_t)m * a.Cout + co0 +
+                                                (a_pos ^ wswz<RA>(row)) * 8)
+                                : (const void*)g_zero_page;
+      glds16(src, base + (wave * AI + i) * 1024);
+    }
+    uint8_t* bb = base + kPix * RA;
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = (wave * BI + i) * RPI_B + b_row_l;
+      const int m = p0 + row;
+      const void* src = (const void*)g_zero_page;
+      if (m < a.M) {
+        const int n = (int)fdiv((uint32_t)m, a.div_hw);
+        const int rem = m - n * a.Ho * a.Wo;
+        const int ho = (int)fdiv((uint32_t)rem, a.div_w);
+        const int wo = rem - ho * a.Wo;
+        const int hi = ho * a.stride - a.pad + rr, wi = wo * a.stride - a.pad + ss;
+        if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
+          src = (const void*)(a.x + ((size_t)(n * a.H + hi) * a.W + wi) * a.C + ci0 +
+                              (b_pos ^ wswz<RBB>(row)) * 8);
+      }
+      glds16(src, bb + (wave * BI + i) * 1024);
+    }
+  };
+
+  f32x4v acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+
+  if (nsteps > 0) {
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  for (int t = 0; t < nsteps; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nsteps) stage(t + 1, cur ^ 1);
+    const uint8_t* abuf = lds + cur * kBuf;
+    const uint8_t* bbuf = abuf + kPix * RA;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = kk * 32 + 8 * g + 4 * h + qq;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int byte = 2 * (wm * WM + i * 16 + 4 * pp);
+          const int off = row * RA + (((byte >> 4) ^ wswz<RA>(row)) << 4) + (byte & 15);
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(abuf + off));
+          af[i][4 * h + 0] = v[0]; af[i][4 * h + 1] = v[1];
+          af[i][4 * h + 2] = v[2]; af[i][4 * h + 3] = v[3];
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int byte = 2 * (wn * WN + j * 16 + 4 * pp);
+          const int off = row * RBB + (((byte >> 4) ^ wswz<RBB>(row)) << 4) + (byte & 15);
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(bbuf + off));
+          bfr[j][4 * h + 0] = v[0]; bfr[j][4 * h + 1] = v[1];
+          bfr[j][4 * h + 2] = v[2]; bfr[j][4 * h + 3] = v[3];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // lane holds D[co = .. + 4*g + reg][kk = .. + (lane & 15)]
+  float* slab = a.ws + (size_t)split * a.Cout * a.Ktot;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = kk0 + wn * WN + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int co = co0 + wm * WM + i * 16 + 4 * g + r;
+        slab[(size_t)co * a.Ktot + col] = acc[i][j][r];
+      }
+    }
+}
+
+// out = sum over splits of ws (fixed order: 8 interleaved partial sums, then combined), bf16
+// and/or fp32 output. One float per thread, so a small dW (4096 floats for a 64x64 1x1 conv,
+// summed over hundreds of slabs) still spreads over enough waves; 8 loads in flight per thread.
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ ws,
+                                                                int splits, long long n,
+                                                                uint16_t* __restrict__ out_bf,
+                                                                float* __restrict__ out_f,
+                                                                float scale) {
+  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    int k = 0;
+    for (; k + 8 <= splits; k += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = ws[i + (long long)(k + u) * n];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) p[u] += v[u];
+    }
+    for (int u = 0; k < splits; ++k, ++u) p[u] += ws[i + (long long)k * n];
+    const float s = (((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]))) * scale;
+    if (out_f) out_f[i] = s;
+    if (out_bf) out_bf[i] = (uint16_t)(__float_as_uint(bf16_round(s)) >> 16);
+  }
+}
+
+FastDiv make_fastdiv(uint32_t d) {
+  FastDiv f{};
+  f.d = d;
+  uint32_t l = 0;
+  while ((1ull << l) < d) ++l;
+  f.shift = l;
+  f.mul = (uint32_t)(((1ull << 32) * ((1ull << l) - d)) / d + 1);
+  return f;
+}
+
+template <int BM, int BN>
+hipError_t launch_wgrad(WgradArgs a, int splits_hint, hipStream_t st) {
+  a.m_tiles = a.Cout / BM;
+  a.n_tiles = a.Ktot / BN;
+  const int tiles = a.m_tiles * a.n_tiles;
+  const int total = (a.M + 63) / 64;
+  int splits = splits_hint > 0 ? splits_hint : std::max(1, (1024 + tiles / 2) / tiles);
+  splits = std::min(splits, total);
+  a.sps = (total + splits - 1) / splits;
+  a.splits = (total + a.sps - 1) / a.sps;
+  hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN>), dim3(tiles * a.splits), dim3(kThreads), 0, st,
+                     a);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+// Number of split slabs the wgrad launch will use (the caller sizes the workspace with it).
+int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int variant,
+                            int splits_hint) {
+  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
+  if (variant < 0 || variant > 3) return -1;
+  const int tiles = (Cout / bm[variant]) * (Ktot / bn[variant]);
+  const long long M = (long long)N * Ho * Wo;
+  const int total = (int)((M + 63) / 64);
+  int splits = splits_hint > 0 ? splits_hint : std::max(1, (1024 + tiles / 2) / tiles);
+  splits = std::min(splits, total);
+  const int sps = (total + splits - 1) / splits;
+  return (total + sps - 1) / sps;
+}
+
+// variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (Cout x R*S*C tile). Needs C % BN == 0
+// (a tile never straddles two filter taps) and Cout % BM == 0.
+hipError_t arena_conv_wgrad(const void* x, const void* dy, float* ws, void* dw_bf16, float* dw_f32,
+                            int N, int H, int W, int C, int Cout, int R, int S, int stride,
+                            int pad, int variant, int splits_hint, float scale, hipStream_t st) {
+  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
+  if (variant < 0 || variant > 3) return hipErrorInvalidValue;
+  if (C % bn[variant] || Cout % bm[variant] || N <= 0 || stride <= 0 || pad < 0)
+    return hipErrorInvalidValue;
+  WgradArgs a{};
+  a.x = (const uint16_t*)x;
+  a.dy = (const uint16_t*)dy;
+  a.ws = ws;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
+  a.stride = stride; a.pad = pad;
+  a.Ho = (H + 2 * pad - R) / stride + 1;
+  a.Wo = (W + 2 * pad - S) / stride + 1;
+  if (a.Ho <= 0 || a.Wo <= 0) return hipErrorInvalidValue;
+  const long long M = (long long)N * a.Ho * a.Wo;
+  if (M >= (1LL << 31)) return hipErrorInvalidValue;
+  a.M = (int)M;
+  a.Ktot = R * S * C;
+  a.div_hw = make_fastdiv((uint32_t)(a.Ho * a.Wo));
+  a.div_w = make_fastdiv((uint32_t)a.Wo);
+  hipError_t e;
+  switch (variant) {
+    case 0: e = launch_wgrad<128, 128>(a, splits_hint, st); break;
+    case 1: e = launch_wgrad<128, 64>(a, splits_hint, st); break;
+    case 2: e = launch_wgrad<64, 128>(a, splits_hint, st); break;
+    default: e = launch_wgrad<64, 64>(a, splits_hint, st); break;
+  }
+  if (e != hipSuccess) return e;
+  const int splits = arena_conv_wgrad_splits(N, a.Ho, a.Wo, Cout, a.Ktot, variant, splits_hint);
+  const long long n = (long long)Cout * a.Ktot;
+  const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, n,
+                     (uint16_t*)dw_bf16, dw_f32, scale);
+  return hipGetLastError();
 }
 
 }  // extern "C"

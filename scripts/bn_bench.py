@@ -76,8 +76,8 @@ def main():
         ext.bn_set_reduce_geometry(mb, mr)
         rows, tot_us, tot_bytes = [], 0.0, 0.0
         for M, C, uses, relu, res, x, dy, r, w, bias, rm, rv in data:
-            y, mean, invstd = ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None)
-            f = timed(lambda: ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None))
+            y, mean, invstd = ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None, None, 0)
+            f = timed(lambda: ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None, None, 0))
             bk = timed(lambda: ext.bn_bwd(dy, y, x, mean, invstd, w, relu, res, True))
             e = M * C * 2
             # fwd: read x twice (+ res), write y; bwd: read dy, x (+ y) twice, write dx (+ dres)

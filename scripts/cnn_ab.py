@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""In-process A/B of ResNet training-step variants on one GPU (interleaved graph replays).
+
+Builds one model + optimizer + synthetic batch per variant (same seed), warms each up eagerly
+(conv autotuning happens there), captures each whole step as a hipGraph, then alternates
+``--chunk`` timed replays of each variant for ``--rounds`` rounds, so clock/thermal drift hits
+every variant alike (cdna_hip_programming.md §5.4 rule 24). Variants are conv modes
+(ARENA_CONV values). Prints one JSON line per variant: median / min ms per step, images/s.
+
+    python scripts/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+from arena_amd.examples import cnn_bench  # noqa: E402
+from arena_amd.ops import conv  # noqa: E402
+from arena_amd.parallel import hvd  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--modes", default="miopen,auto")
+    ap.add_argument("--model", default="resnet50")
+    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--chunk", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=4)
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    torch.cuda.set_device(dev)
+    torch.backends.cudnn.benchmark = True
+    hvd.init("gloo")
+    args = cnn_bench.parse(["--model", a.model, "--batch_size", str(a.batch)])
+    variants = {}
+    for mode in a.modes.split(","):
+        conv.set_mode(mode)
+        model, opt, x, y = cnn_bench.build(args, dev, 1)
+        for _ in range(a.warmup):
+            cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
+        torch.cuda.synchronize()
+        g, loss = cnn_bench.capture_step(model, opt, x, y, torch.bfloat16)
+        g.replay()
+        torch.cuda.synchronize()
+        variants[mode] = (g, loss)
+        print(f"[ab] {mode}: captured, loss {float(loss):.4f}", file=sys.stderr, flush=True)
+    conv.set_mode(None)
+    times = {m: [] for m in variants}
+    for r in range(a.rounds):
+        for m, (g, _) in variants.items():
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(a.chunk):
+                g.replay()
+            torch.cuda.synchronize()
+            times[m].append((time.perf_counter() - t0) / a.chunk * 1e3)
+        print(f"[ab] round {r}: " + " ".join(f"{m}={times[m][-1]:.3f}ms" for m in times),
+              file=sys.stderr, flush=True)
+    for m, ts in times.items():
+        med = statistics.median(ts)
+        print(json.dumps({"variant": m, "model": a.model, "batch": a.batch,
+                          "ms_per_step_median": round(med, 3), "ms_per_step_min": round(min(ts), 3),
+                          "images_per_s": round(a.batch / med * 1e3, 1),
+                          "loss": round(float(variants[m][1]), 4), "rounds": a.rounds,
+                          "chunk": a.chunk}), flush=True)
+    hvd.shutdown()
+
+
+if __name__ == "__main__":
+    main()

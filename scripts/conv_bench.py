@@ -62,6 +62,14 @@ def main():
             for v in conv.variants_for(cin):
                 dx = conv.conv2d_bwd_data(dys, wt, pad, v)
                 errs[f"bwd_v{v}"] = rel_err(dx, dref)
+        dys = torch.randn_like(ref).to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        wref = torch.ops.aten.convolution_backward(
+            dys.float(), xs.float(), wt.float(), None, [st, st], [pad, pad], [1, 1], False,
+            [0, 0], 1, [False, True, False])[1]
+        for v in conv.wgrad_variants_for(cin, cout):
+            dw = conv.conv2d_wgrad(xs, dys, (k, k), st, pad, v, out_dtype=torch.float32)
+            errs[f"wgrad_v{v}"] = rel_err(dw, wref)
         worst = max(errs.values())
         ok = worst < 2e-2
         bad += not ok
@@ -100,6 +108,24 @@ def main():
             res["bwd_data_speedup"] = round(t_mi / best, 3)
             tot["miopen_bwd_data"] += t_mi * cnt
             tot["ours_bwd_data"] += min(best, t_mi) * cnt
+        dy = torch.randn_like(y)
+        t_mi = timeit(lambda: torch.ops.aten.convolution_backward(
+            dy, x, wb, None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+            [False, True, False]), args.reps)
+        res["miopen_wgrad_us"] = round(t_mi, 1)
+        best = None
+        for v in conv.wgrad_variants_for(cin, cout):
+            bm, bn = conv.WGRAD_TILES[v]
+            tiles = (cout // bm) * (k * k * cin // bn)
+            auto = max(1, (1024 + tiles // 2) // tiles)
+            for sp in sorted({max(1, auto // 2), auto, auto * 2}):
+                t = timeit(lambda: conv.conv2d_wgrad(x, dy, (k, k), st, pad, v, splits=sp),
+                           args.reps)
+                res[f"ours_wgrad_v{v}_s{sp}_us"] = round(t, 1)
+                best = t if best is None else min(best, t)
+        res["wgrad_speedup"] = round(t_mi / best, 3)
+        tot["miopen_wgrad"] += t_mi * cnt
+        tot["ours_wgrad"] += min(best, t_mi) * cnt
         print(json.dumps(res), flush=True)
     print(json.dumps({"total_us_per_step": {k: round(v, 1) for k, v in tot.items()},
                       "numerics_failures": bad}), flush=True)

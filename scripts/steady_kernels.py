@@ -14,7 +14,7 @@ def category(n: str) -> str:
         return "arena fused BN (HIP)"
     if "BatchNorm" in n:
         return "batchnorm (MIOpen)"
-    if "wrw" in n or "bwd_weight" in n:
+    if "wrw" in n or "bwd_weight" in n or "conv_wgrad" in n:
         return "conv wgrad"
     if "igemm_bwd" in n or "bwd_data" in n:
         return "conv dgrad"
@@ -36,11 +36,17 @@ def main():
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=25)
     ap.add_argument("--csv", default="")
+    ap.add_argument("--last-ms", type=float, default=0.0,
+                    help="keep only kernels that start in the last N ms of the trace (graph "
+                         "replays at the end of a run) instead of cutting at MIOpen's find")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
     naive = [int(r["End_Timestamp"]) for r in rows if "naive" in r["Kernel_Name"]]
     t_cut = max(naive) if naive else 0
+    if a.last_ms > 0:
+        t_end = max(int(r["End_Timestamp"]) for r in rows)
+        t_cut = t_end - int(a.last_ms * 1e6)
     ss = [r for r in rows if int(r["Start_Timestamp"]) > t_cut]
     dur = lambda r: int(r["End_Timestamp"]) - int(r["Start_Timestamp"])  # noqa: E731
     busy = sum(dur(r) for r in ss)

@@ -1,0 +1,182 @@
+"""NHWC bf16 implicit-GEMM convolution kernels (csrc/ops/conv_kernels.hip) vs fp32 PyTorch.
+
+GPU: forward, backward-data (flipped weight) and backward-weight (split-K slabs) of every tile
+variant on shapes with padding, stride 2, 1x1/3x3 taps and output-pixel counts that are not a
+multiple of the tile (tail rows); the autotuned ``Conv2dNHWC`` module under bf16 autocast; a
+ResNet training step with the kernels equal to the MIOpen one. CPU: the module is nn.Conv2d.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from arena_amd.ops import conv
+
+SHAPES = [  # n, cin, h, w, cout, k, stride
+    (2, 64, 9, 11, 64, 3, 1),
+    (3, 128, 7, 7, 128, 1, 1),
+    (2, 64, 10, 10, 128, 3, 2),
+    (1, 128, 15, 13, 64, 1, 2),
+    (2, 192, 6, 5, 256, 3, 1),
+]
+
+
+def _rel(a, b):
+    return float((a.float() - b.float()).abs().max() / b.float().abs().max().clamp_min(1e-6))
+
+
+def _data(n, cin, h, w, cout, k, dev, seed=0):
+    g = torch.Generator(device=dev).manual_seed(seed)
+    x = torch.randn(n, cin, h, w, device=dev, generator=g).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    wt = (torch.randn(cout, cin, k, k, device=dev, generator=g) * 0.1).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    return x, wt
+
+
+def test_conv2d_nhwc_module_is_nn_conv2d_on_cpu():
+    torch.manual_seed(0)
+    m = conv.Conv2dNHWC(8, 16, 3, stride=2, padding=1, bias=False)
+    ref = torch.nn.Conv2d(8, 16, 3, stride=2, padding=1, bias=False)
+    ref.weight.data.copy_(m.weight.data)
+    x = torch.randn(2, 8, 9, 9, requires_grad=True)
+    x2 = x.detach().clone().requires_grad_()
+    y, y2 = m(x), ref(x2)
+    torch.testing.assert_close(y, y2)
+    y.sum().backward()
+    y2.sum().backward()
+    torch.testing.assert_close(x.grad, x2.grad)
+    torch.testing.assert_close(m.weight.grad, ref.weight.grad)
+    with pytest.raises(ValueError):
+        conv.Conv2dNHWC(8, 16, 3, bias=True)
+
+
+def test_pick_variant_fills_the_chip():
+    assert conv.pick_variant(128 * 56 * 56, 256) == 0
+    assert conv.pick_variant(128 * 7 * 7, 512) in (2, 3)   # 49 m-tiles: smaller tiles
+    assert conv.pick_variant(1000, 64) in (1, 3)           # Cout 64 needs a 64-wide tile
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", SHAPES)
+def test_conv_fwd_bwd_wgrad_match_fp32(shape):
+    from arena_amd.ops import _ext
+    _ext.load()
+    n, cin, h, w, cout, k, st = shape
+    pad = k // 2
+    x, wt = _data(n, cin, h, w, cout, k, "cuda")
+    ref = F.conv2d(x.float(), wt.float(), stride=st, padding=pad)
+    for v in conv.variants_for(cout):
+        y = conv.conv2d_fwd(x, wt, st, pad, v)
+        assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+        assert _rel(y, ref) < 1e-2, (v, _rel(y, ref))
+    dy = torch.randn(ref.shape, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dx_ref, dw_ref, _ = torch.ops.aten.convolution_backward(
+        dy.float(), x.float(), wt.float(), None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+        [True, True, False])
+    if st == 1:
+        for v in conv.variants_for(cin):
+            dx = conv.conv2d_bwd_data(dy, wt, pad, v)
+            assert dx.shape == x.shape
+            assert _rel(dx, dx_ref) < 1e-2, (v, _rel(dx, dx_ref))
+    for v in conv.wgrad_variants_for(cin, cout):
+        for sp in (1, 3, 0):
+            dw = conv.conv2d_wgrad(x, dy, (k, k), st, pad, v, sp, out_dtype=torch.float32)
+            assert dw.shape == wt.shape
+            assert _rel(dw, dw_ref) < 5e-3, (v, sp, _rel(dw, dw_ref))
+            # fixed-order slab reduction: bit-reproducible
+            dw2 = conv.conv2d_wgrad(x, dy, (k, k), st, pad, v, sp, out_dtype=torch.float32)
+            assert torch.equal(dw, dw2)
+        dwb = conv.conv2d_wgrad(x, dy, (k, k), st, pad, v, 0)
+        assert dwb.dtype == torch.bfloat16 and dwb.is_contiguous(memory_format=torch.channels_last)
+
+
+@pytest.mark.gpu
+def test_conv_kernel_rejects_bad_shapes():
+    from arena_amd.ops import _ext
+    x, wt = _data(1, 32, 8, 8, 64, 3, "cuda")
+    with pytest.raises(RuntimeError, match="multiples of 64"):
+        _ext.load().conv_fwd(x, wt, 1, 1, 1, False)
+    x, wt = _data(1, 64, 8, 8, 64, 3, "cuda")
+    with pytest.raises(RuntimeError, match="Cout % 128"):
+        _ext.load().conv_fwd(x, wt, 1, 1, 0, False)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", ["auto", "ours"])
+def test_conv2d_nhwc_module_autocast(mode, monkeypatch):
+    monkeypatch.setenv("ARENA_CONV", mode)
+    torch.manual_seed(0)
+    m = conv.Conv2dNHWC(64, 128, 3, stride=1, padding=1, bias=False).cuda().to(
+        memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(64, 128, 3, stride=1, padding=1, bias=False).cuda()
+    ref.weight.data.copy_(m.weight.data)
+    x = torch.randn(4, 64, 14, 14, device="cuda").contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    xr = x.detach().clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+    assert y.dtype == torch.bfloat16
+    yr = ref(xr)
+    assert _rel(y, yr) < 1e-2
+    gy = torch.randn_like(yr)
+    y.backward(gy.to(torch.bfloat16))
+    yr.backward(gy)
+    assert m.weight.grad.dtype == torch.float32
+    assert _rel(m.weight.grad, ref.weight.grad) < 2e-2
+    assert _rel(x.grad, xr.grad) < 2e-2
+    if mode == "ours":
+        plan = conv.plan_for(x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last),
+                             m.weight.to(torch.bfloat16).contiguous(
+                                 memory_format=torch.channels_last), 1, 1)
+        assert plan.fwd != conv.MIOPEN and plan.bwd != conv.MIOPEN and plan.wgrad != conv.MIOPEN
+
+
+@pytest.mark.gpu
+def test_resnet_step_kernels_match_miopen(monkeypatch):
+    """One bf16 training step of a small ResNet: MFMA conv kernels vs ARENA_CONV=miopen."""
+    from arena_amd.models.resnet import ResNet
+    outs = {}
+    for mode in ("miopen", "ours"):
+        monkeypatch.setenv("ARENA_CONV", mode)
+        torch.manual_seed(0)
+        model = ResNet([1, 1], num_classes=10, width=64).cuda().to(
+            memory_format=torch.channels_last)
+        x = torch.randn(4, 3, 32, 32, device="cuda").contiguous(memory_format=torch.channels_last)
+        y = torch.arange(4, device="cuda")
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            loss = F.cross_entropy(model(x), y)
+        loss.backward()
+        outs[mode] = (loss.item(), {n: p.grad.float().clone() for n, p in model.named_parameters()})
+    assert abs(outs["miopen"][0] - outs["ours"][0]) < 2e-2
+    for n, g in outs["miopen"][1].items():
+        assert _rel(outs["ours"][1][n], g) < 0.1, n
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", SHAPES[:4])
+def test_conv_fused_bn_statistics(shape):
+    """The conv epilogue's BatchNorm partials give the same BN output, batch statistics and
+    running statistics as the BN's own statistics pass (tail tiles included)."""
+    from arena_amd.ops.batchnorm import BatchNormAct2d
+    n, cin, h, w, cout, k, st = shape
+    pad = k // 2
+    x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=3)
+    for v in conv.variants_for(cout):
+        y0 = conv.conv2d_fwd(x, wt, st, pad, v)
+        y, stats = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True)
+        assert torch.equal(y, y0)
+        part, rpb = stats
+        m = y.shape[0] * y.shape[2] * y.shape[3]
+        assert rpb == conv.TILES[v][0] and part.numel() == -(-m // rpb) * 2 * cout
+        bns = [BatchNormAct2d(cout).cuda() for _ in range(2)]
+        for b in bns:
+            b.weight.data.uniform_(0.5, 1.5)
+            b.bias.data.uniform_(-0.5, 0.5)
+        bns[1].load_state_dict(bns[0].state_dict())
+        ref = bns[0](y)
+        out = bns[1](y, stats=stats)
+        assert _rel(out, ref) < 1e-2
+        torch.testing.assert_close(bns[1].running_mean, bns[0].running_mean, rtol=1e-4, atol=1e-5)
+        torch.testing.assert_close(bns[1].running_var, bns[0].running_var, rtol=1e-3, atol=1e-5)
+        assert int(bns[1].num_batches_tracked) == 1
