@@ -147,16 +147,26 @@ class ConvPlan:
 _PLANS: Dict[tuple, ConvPlan] = {}
 
 
-def _time(fn, reps: int = 5) -> float:
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+def _time(fn, reps: int = 4, iters: int = 3) -> float:
+    """GPU time of fn() in us: ``reps`` calls captured in a hipGraph, replayed ``iters`` times.
+    (Eager timing would charge a library's host-side launch cost, which the training step's
+    graph replay never pays: MIOpen's convolution_backward costs ~50 us of host time per call.)"""
     fn()
     torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(reps):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
-    for _ in range(reps):
-        fn()
+    for _ in range(iters):
+        g.replay()
     e.record()
     e.synchronize()
-    return s.elapsed_time(e) * 1e3 / reps
+    del g
+    return s.elapsed_time(e) * 1e3 / (reps * iters)
 
 
 def _miopen_bwd(dy, x, w, stride, pad, mask):

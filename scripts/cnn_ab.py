@@ -35,13 +35,13 @@ def main():
     ap.add_argument("--chunk", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=4)
     a = ap.parse_args()
-    dev = torch.device("cuda")
+    dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
     torch.backends.cudnn.benchmark = True
     hvd.init("gloo")
     args = cnn_bench.parse(["--model", a.model, "--batch_size", str(a.batch)])
     variants = {}
-    for mode in a.modes.split(","):
+    for i, mode in enumerate(a.modes.split(",")):
         conv.set_mode(mode)
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
@@ -50,20 +50,24 @@ def main():
         g, loss = cnn_bench.capture_step(model, opt, x, y, torch.bfloat16)
         g.replay()
         torch.cuda.synchronize()
-        variants[mode] = (g, loss)
+        # the graph holds raw pointers into this model's parameters, optimizer state and batch:
+        # keep them alive (rebinding the names would free them into the next variant's use)
+        variants[f"{mode}" if mode not in variants else f"{mode}#{i}"] = (g, loss,
+                                                                          (model, opt, x, y))
         print(f"[ab] {mode}: captured, loss {float(loss):.4f}", file=sys.stderr, flush=True)
     conv.set_mode(None)
     times = {m: [] for m in variants}
     for r in range(a.rounds):
-        for m, (g, _) in variants.items():
+        for m, (g, _, _) in variants.items():
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(a.chunk):
                 g.replay()
             torch.cuda.synchronize()
             times[m].append((time.perf_counter() - t0) / a.chunk * 1e3)
-        print(f"[ab] round {r}: " + " ".join(f"{m}={times[m][-1]:.3f}ms" for m in times),
-              file=sys.stderr, flush=True)
+        print(f"[ab] round {r}: " + " ".join(
+            f"{m}={times[m][-1]:.3f}ms/loss {float(variants[m][1]):.4f}" for m in times),
+            file=sys.stderr, flush=True)
     for m, ts in times.items():
         med = statistics.median(ts)
         print(json.dumps({"variant": m, "model": a.model, "batch": a.batch,

@@ -50,18 +50,26 @@ def resnet50_convs(batch: int):
 
 
 def timeit(fn, reps):
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for _ in range(3):
-        fn()
+    """Median GPU time (us) of fn(): ``reps`` graph replays of 4 captured calls each (no host
+    launch cost, which a library like MIOpen would otherwise add to every eager call)."""
+    fn()
     torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        for _ in range(4):
+            fn()
+    g.replay()
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ts = []
     for _ in range(reps):
         s.record()
-        fn()
+        g.replay()
         e.record()
         e.synchronize()
-        ts.append(s.elapsed_time(e) * 1e3)
+        ts.append(s.elapsed_time(e) * 1e3 / 4)
     ts.sort()
+    del g
     return ts[len(ts) // 2]
 
 
