@@ -21,7 +21,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import Conv2dNHWC
+from ..ops.conv import Conv2dNHWC, GradJoin
 from ..ops.pool import MaxPool2dNHWC
 
 DEPTHS = {"resnet50": [3, 4, 6, 3], "resnet101": [3, 4, 23, 3],
@@ -52,14 +52,17 @@ class Bottleneck(nn.Module):
     def forward(self, x):
         # forward_stats: when a conv runs on the MFMA kernel, its epilogue also produces the
         # BatchNorm statistics partials of its output, and the BN skips its statistics pass
+        # join: x feeds conv1 and the shortcut; its two gradients are summed inside the second
+        # backward (conv1's backward-data epilogue) instead of by a separate add pass
+        join = GradJoin() if (torch.is_grad_enabled() and x.requires_grad) else None
         idt = x
         if self.down_conv is not None:
-            y, st = self.down_conv.forward_stats(x)
+            y, st = self.down_conv.forward_stats(x, join=join)
             idt = self.down_bn(y, stats=st)
-        y, st = self.conv1.forward_stats(x)
+        y, st = self.conv1.forward_stats(x, join=join)
         y, st = self.conv2.forward_stats(self.bn1(y, stats=st))
         y, st = self.conv3.forward_stats(self.bn2(y, stats=st))
-        return self.bn3(y, residual=idt, stats=st)
+        return self.bn3(y, residual=idt, stats=st, join=join if self.down_conv is None else None)
 
 
 class ResNet(nn.Module):

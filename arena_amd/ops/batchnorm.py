@@ -53,7 +53,7 @@ def reference(x, residual, weight, bias, running_mean, running_var, training, mo
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum,
-                eps, relu, num_batches=None, stats=None):
+                eps, relu, num_batches=None, stats=None, join=None):
         ext = _ext.load()
         part, rpb = stats if (stats is not None and training) else (None, 0)
         y, mean, invstd = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
@@ -61,6 +61,8 @@ class _BNActFn(torch.autograd.Function):
         ctx.save_for_backward(x, y, mean, invstd, weight)
         ctx.relu, ctx.has_res, ctx.training = relu, residual is not None, training
         ctx.affine = weight is not None
+        # the residual is also another op's input: gradients meet in a GradJoin (ops/conv.py)
+        ctx.join = join.register() if (join is not None and residual is not None) else None
         return y
 
     @staticmethod
@@ -72,8 +74,17 @@ class _BNActFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, y, x, mean, invstd, weight, ctx.relu,
                                                      ctx.has_res, ctx.affine)
-        return (dx, dres if ctx.has_res else None, dgamma if ctx.affine else None,
-                dbeta if ctx.affine else None, None, None, None, None, None, None, None, None)
+        if not ctx.has_res:
+            dres = None
+        elif ctx.join is not None and ctx.join.active() and ctx.needs_input_grad[1]:
+            other = ctx.join.other()
+            if other is not None:   # second consumer (the conv usually comes second and fuses)
+                dres = dres + other
+            if ctx.join.park_or_take(dres):
+                dres = None
+        return (dx, dres, dgamma if ctx.affine else None,
+                dbeta if ctx.affine else None, None, None, None, None, None, None, None, None,
+                None)
 
 
 def bn_act(x, residual=None, weight=None, bias=None, running_mean=None, running_var=None,
@@ -96,9 +107,10 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.relu = act == "relu"
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                stats=None) -> torch.Tensor:
+                stats=None, join=None) -> torch.Tensor:
         """``stats``: BatchNorm partials of ``x`` from the producing ``Conv2dNHWC.forward_stats``
-        (skips the statistics pass over x; training mode on the fused kernels only)."""
+        (skips the statistics pass over x; training mode on the fused kernels only).
+        ``join``: a ``GradJoin`` the residual's other consumer is registered on."""
         training = self.training or not self.track_running_stats
         tracking = self.training and self.track_running_stats
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
@@ -109,7 +121,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
             # num_batches_tracked += 1 happens inside the statistics finalize kernel
             return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, True,
                                   self.momentum, self.eps, self.relu,
-                                  self.num_batches_tracked if tracking else None, stats)
+                                  self.num_batches_tracked if tracking else None, stats, join)
         if tracking:
             self.num_batches_tracked.add_(1)
         mom = self.momentum if self.momentum is not None else \
@@ -119,4 +131,4 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return reference(x, residual, self.weight, self.bias, rm, rv, training, mom,
                              self.eps, self.relu)
         return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, training, mom,
-                              self.eps, self.relu)
+                              self.eps, self.relu, None, None, join)

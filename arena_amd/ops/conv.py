@@ -55,32 +55,77 @@ def pick_variant(m: int, cout: int) -> int:
 
 
 def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int = -1,
-               with_stats: bool = False):
-    """y = conv2d(x, w) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S].
+               with_stats: bool = False, addend: Tensor | None = None):
+    """y = conv2d(x, w) (+ addend) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S].
 
     with_stats: returns (y, (part, rpb)) where part holds per-tile BatchNorm partials of y
     (tile mean and sum of squared deviations per channel, ``rpb`` output pixels per tile), which
-    ``BatchNormAct2d(..., stats=...)`` finalizes instead of re-reading y."""
+    ``BatchNormAct2d(..., stats=...)`` finalizes instead of re-reading y.
+    addend: a bf16 tensor shaped like y, added to the fp32 sums before rounding (epilogue)."""
     x = x.contiguous(memory_format=torch.channels_last)
     w = w.contiguous(memory_format=torch.channels_last)
     if variant < 0:
         ho, wo = out_hw(x.shape[2], x.shape[3], w.shape[2], w.shape[3], stride, pad)
         variant = pick_variant(x.shape[0] * ho * wo, w.shape[0])
-    out = _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant), bool(with_stats))
+    if addend is not None:
+        addend = addend.contiguous(memory_format=torch.channels_last)
+    out = _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant), bool(with_stats),
+                               addend)
     if with_stats:
         return out[0], (out[1], TILES[variant][0])
     return out[0]
 
 
 def flip_weight(w: Tensor) -> Tensor:
-    """W' [Cin, Cout, R, S] (channels_last) with W'[ci, co, r, s] = W[co, ci, R-1-r, S-1-s]."""
+    """W' [Cin, Cout, R, S] (channels_last) with W'[ci, co, r, s] = W[co, ci, R-1-r, S-1-s]
+    (one transpose kernel on the GPU; torch ops elsewhere)."""
+    if (w.is_cuda and w.dtype == torch.bfloat16 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0):
+        return _ext.load().conv_flip_weight(w.contiguous(memory_format=torch.channels_last))
     return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
 
 
-def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1) -> Tensor:
-    """dX of a stride-1 convolution (same spatial size when pad = (R-1)/2)."""
+def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1,
+                    addend: Tensor | None = None) -> Tensor:
+    """dX (+ addend) of a stride-1 convolution (same spatial size when pad = (R-1)/2)."""
     r = w.shape[2]
-    return conv2d_fwd(dy, flip_weight(w), 1, r - 1 - pad, variant)
+    return conv2d_fwd(dy, flip_weight(w), 1, r - 1 - pad, variant, addend=addend)
+
+
+class GradJoin:
+    """One tensor, two consumers (a ResNet block input feeds conv1 and the shortcut): instead of
+    letting autograd add the two gradients in a separate elementwise pass, the consumer whose
+    backward runs first parks its gradient here and returns None for the input, and the second
+    returns the sum -- fused into the backward-data kernel's epilogue when it runs on ours.
+    Consumers ``register()`` in their forward; with fewer than two registered, both behave
+    normally. The two backwards must both run (true inside one block), exactly once."""
+    __slots__ = ("n", "arrived", "pending")
+
+    def __init__(self):
+        self.n = 0
+        self.arrived = 0
+        self.pending: Tensor | None = None
+
+    def register(self) -> "GradJoin":
+        self.n += 1
+        return self
+
+    def active(self) -> bool:
+        return self.n == 2
+
+    def other(self) -> Tensor | None:
+        """The first consumer's gradient when called from the second (else None)."""
+        return self.pending if self.arrived == 1 else None
+
+    def park_or_take(self, g: Tensor | None) -> bool:
+        """Record this consumer's arrival with its gradient g. Returns True for the first one
+        (g is parked: return None for the input), False for the second (g must already include
+        ``other()``)."""
+        self.arrived += 1
+        if self.arrived == 1:
+            self.pending = g
+            return True
+        self.arrived, self.pending = 0, None
+        return False
 
 
 WGRAD_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}   # Cout x R*S*C
@@ -240,7 +285,7 @@ def plans() -> Dict[tuple, ConvPlan]:
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, plan, want_stats):
+    def forward(ctx, x, w, stride, pad, plan, want_stats, join=None):
         part = x.new_empty(0, dtype=torch.float32)
         if plan.fwd == MIOPEN:
             y = F.conv2d(x, w, stride=stride, padding=pad)
@@ -250,20 +295,32 @@ class _ConvFn(torch.autograd.Function):
             y = conv2d_fwd(x, w, stride, pad, plan.fwd)
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pad, plan)
+        ctx.join = join.register() if join is not None else None
         ctx.mark_non_differentiable(part)
+        # no zero-filled gradient for the statistics output (one fill kernel per conv per step)
+        ctx.set_materialize_grads(False)
         return y, part
 
     @staticmethod
     def backward(ctx, dy, _dpart):
+        if dy is None:
+            return None, None, None, None, None, None, None
         x, w = ctx.saved_tensors
         stride, pad, plan = ctx.conf
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
         if ctx.needs_input_grad[0]:
+            join = ctx.join if (ctx.join is not None and ctx.join.active()) else None
+            # the second consumer of a joined input folds the first one's gradient in
+            other = join.other() if join is not None else None
             if plan.bwd == MIOPEN:
                 dx = _miopen_bwd(dy, x, w, stride, pad, [True, False, False])[0]
+                if other is not None:
+                    dx.add_(other)
             else:
-                dx = conv2d_bwd_data(dy, w, pad, plan.bwd)
+                dx = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other)
+            if join is not None and join.park_or_take(dx):
+                dx = None
         if ctx.needs_input_grad[1]:
             if plan.wgrad == MIOPEN:
                 dw = _miopen_bwd(dy, x, w, stride, pad, [False, True, False])[1]
@@ -271,7 +328,7 @@ class _ConvFn(torch.autograd.Function):
                 v, sp = plan.wgrad
                 dw = conv2d_wgrad(x, dy, (w.shape[2], w.shape[3]), stride, pad, v, sp,
                                   out_dtype=w.dtype)
-        return dx, dw, None, None, None, None
+        return dx, dw, None, None, None, None, None
 
 
 class Conv2dNHWC(nn.Conv2d):
@@ -290,9 +347,10 @@ class Conv2dNHWC(nn.Conv2d):
     def forward(self, x: Tensor) -> Tensor:
         return self.forward_stats(x, want_stats=False)[0]
 
-    def forward_stats(self, x: Tensor, want_stats: bool = True):
+    def forward_stats(self, x: Tensor, want_stats: bool = True, join: GradJoin | None = None):
         """(y, stats): ``stats`` are the BatchNorm partials of y for ``BatchNormAct2d(y,
-        stats=stats)`` when the kernel produced y (else None: the BN computes them itself)."""
+        stats=stats)`` when the kernel produced y (else None: the BN computes them itself).
+        ``join``: x has a second consumer registered on the same GradJoin (see there)."""
         if not x.is_cuda or _mode() == "off":
             return super().forward(x), None
         amp = torch.is_autocast_enabled("cuda") and \
@@ -309,5 +367,5 @@ class Conv2dNHWC(nn.Conv2d):
         plan = plan_for(x, w, s, p)
         want = want_stats and plan.fwd != MIOPEN and torch.is_grad_enabled() and self.training
         with torch.autocast("cuda", enabled=False):
-            y, part = _ConvFn.apply(x, w, s, p, plan, want)
+            y, part = _ConvFn.apply(x, w, s, p, plan, want, join)
         return y, ((part, TILES[plan.fwd][0]) if want else None)

@@ -48,13 +48,15 @@ void arena_ccl_set_block_elems(long long);
 void arena_ccl_set_oneshot_max(long long);
 long long arena_ccl_get_oneshot_max();
 // csrc/ops/conv_kernels.hip
-hipError_t arena_conv_fwd(const void*, const void*, void*, float*, int, int, int, int, int, int,
-                          int, int, int, int, hipStream_t);
+hipError_t arena_conv_fwd(const void*, const void*, void*, float*, const void*, int, int, int, int,
+                          int, int, int, int, int, int, hipStream_t);
+hipError_t arena_conv_flip_weight(const void*, void*, int, int, int, int, hipStream_t);
 int arena_conv_wgrad_splits(int, int, int, int, int, int, int);
 hipError_t arena_conv_wgrad(const void*, const void*, float*, void*, float*, int, int, int, int,
                             int, int, int, int, int, int, int, float, hipStream_t);
 // csrc/ops/bn_kernels.hip
 long long arena_bn_workspace_floats(long long, int);
+long long arena_bn_lvl2_doubles(long long, int);
 void arena_bn_set_reduce_geometry(long long, long long);
 // csrc/ops/pool_kernels.hip
 hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, int, int, int, int,
@@ -62,9 +64,9 @@ hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, i
 hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, int, int, int, int,
                              int, hipStream_t);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, long long, int, int, int, float*,
-                        int, long long, ArenaBNStats, hipStream_t);
+                        int, long long, double*, unsigned*, ArenaBNStats, hipStream_t);
 hipError_t arena_bn_bwd(int, const void*, const void*, const void*, void*, void*, long long, int,
-                        int, float*, ArenaBNBwd, hipStream_t);
+                        int, float*, double*, unsigned*, ArenaBNBwd, hipStream_t);
 #ifdef ARENA_TIMELINE
 hipError_t arena_timeline_read(long long*, int);
 #endif
@@ -661,6 +663,36 @@ const float* bn_vec(const OptT& t, int C, const char* name) {
   return t->data_ptr<float>();
 }
 
+// Ticket counters of the BN finalize kernels (bn_kernels.hip, fin_level2): zero-initialised once
+// per device and left zero by every launch. Consecutive launches take different sets, so two
+// finalizes that overlap on different streams never share a counter.
+constexpr int kTicketSets = 64, kTicketsPerSet = 32;  // 32 groups of 64 channels = C <= 2048
+
+unsigned* bn_tickets(const Tensor& like) {
+  static std::vector<Tensor> pools;
+  static std::vector<unsigned> next;
+  const int dev = like.get_device();
+  if ((int)pools.size() <= dev) {
+    pools.resize(dev + 1);
+    next.resize(dev + 1, 0);
+  }
+  if (!pools[dev].defined()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    check_hip(hipStreamIsCapturing(cur_stream(), &cs), "bn_tickets");
+    TORCH_CHECK(cs == hipStreamCaptureStatusNone,
+                "arena BatchNorm: run one eager step before capturing a graph (its ticket "
+                "counters are allocated and zeroed on first use)");
+    pools[dev] = torch::zeros({kTicketSets * kTicketsPerSet}, like.options().dtype(torch::kInt32));
+    check_hip(hipStreamSynchronize(cur_stream()), "bn_tickets zero");
+  }
+  const unsigned set = next[dev]++ % kTicketSets;
+  return reinterpret_cast<unsigned*>(pools[dev].data_ptr<int32_t>()) + set * kTicketsPerSet;
+}
+
+Tensor bn_lvl2(int64_t nblk, int64_t C, const Tensor& like) {
+  return torch::empty({arena_bn_lvl2_doubles(nblk, (int)C)}, like.options().dtype(torch::kFloat64));
+}
+
 // Returns (y, mean, invstd). Eval mode normalises with the running statistics.
 // stats_part/stats_rpb: BatchNorm partials of x from conv_fwd(with_stats=True) (training only).
 std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT running_mean,
@@ -715,12 +747,20 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
     if (beta.has_value()) shift.copy_(*beta); else shift.zero_();
   }
   Tensor y = torch::empty_like(x);
+  const int ext_nblk = training && stats_part.has_value()
+                           ? (int)((g.M + stats_rpb - 1) / stats_rpb) : 0;
+  Tensor lvl2;
+  unsigned* tickets = nullptr;
+  if (training) {
+    const int64_t nblk = ext_nblk > 0 ? ext_nblk : part.numel() / (2 * g.C);
+    lvl2 = bn_lvl2(nblk, g.C, x);
+    tickets = bn_tickets(x);
+  }
   check_hip(arena_bn_fwd(g.dtype, x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr,
                          y.data_ptr(), g.M, g.C, relu ? 1 : 0, training ? 1 : 0,
-                         training ? part.data_ptr<float>() : nullptr,
-                         training && stats_part.has_value()
-                             ? (int)((g.M + stats_rpb - 1) / stats_rpb) : 0,
-                         (long long)stats_rpb, st, cur_stream()),
+                         training ? part.data_ptr<float>() : nullptr, ext_nblk,
+                         (long long)stats_rpb, training ? lvl2.data_ptr<double>() : nullptr,
+                         tickets, st, cur_stream()),
             "bn_fwd");
   return {y, mean, invstd};
 }
@@ -751,11 +791,13 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor in
   b.cb = b.ca + g.C;
   b.cc = b.cb + g.C;
   Tensor part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
+  Tensor lvl2 = bn_lvl2(part.numel() / (2 * g.C), g.C, x);
   Tensor dx = torch::empty_like(x);
   Tensor dres = with_res ? torch::empty_like(x) : Tensor();
   check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(), y.data_ptr(), x.data_ptr(), dx.data_ptr(),
                          with_res ? dres.data_ptr() : nullptr, g.M, g.C, relu ? 1 : 0,
-                         part.data_ptr<float>(), b, cur_stream()),
+                         part.data_ptr<float>(), lvl2.data_ptr<double>(), bn_tickets(x), b,
+                         cur_stream()),
             "bn_bwd");
   return {dx, dres, dgamma, dbeta};
 }
@@ -775,8 +817,10 @@ void pool_check(const Tensor& t, const char* name) {
 // w: [Cout,C,R,S] channels_last (memory order [Cout][R][S][C]).
 // with_stats: also returns the BatchNorm partials of y ([ceil(M/BM)][2][Cout] fp32, BM rows per
 // partial) for bn_fwd(..., stats_part, BM): the BN layer after the conv skips its stats pass.
+// addend (optional): bf16 tensor shaped like y (channels_last) added to the fp32 sums before the
+// bf16 rounding: the second gradient of a tensor with two consumers (arena_amd.ops.conv.GradJoin).
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant,
-                             bool with_stats) {
+                             bool with_stats, OptT addend) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4,
               "conv_fwd: x and w must be 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16,
@@ -801,13 +845,35 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
   const int64_t m_tiles = (N * Ho * Wo + bm[variant] - 1) / bm[variant];
   Tensor part = with_stats ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
                            : Tensor();
+  if (addend.has_value()) {
+    TORCH_CHECK(addend->sizes() == y.sizes() && addend->scalar_type() == torch::kBFloat16 &&
+                    addend->device() == y.device() &&
+                    addend->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_fwd: addend must be a channels_last bf16 tensor shaped like the output");
+  }
   check_hip(arena_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(),
-                           with_stats ? part.data_ptr<float>() : nullptr, (int)N, (int)H, (int)W,
+                           with_stats ? part.data_ptr<float>() : nullptr,
+                           addend.has_value() ? addend->data_ptr() : nullptr, (int)N, (int)H, (int)W,
                            (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad, (int)variant,
                            cur_stream()),
             "conv_fwd");
   if (with_stats) return {y, part};
   return {y};
+}
+
+// W'[ci][co][r][s] = W[co][ci][R-1-r][S-1-s] as a channels_last [C, Cout, R, S] bf16 tensor: the
+// weight of the backward-data pass run through conv_fwd.
+Tensor conv_flip_weight(Tensor w) {
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == torch::kBFloat16 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_flip_weight: w must be a channels_last bf16 GPU tensor [Cout, C, R, S]");
+  const int64_t Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(Cout % 64 == 0 && C % 64 == 0, "conv_flip_weight: C and Cout must be multiples of 64");
+  Tensor wt = torch::empty({C, Cout, R, S}, w.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_hip(arena_conv_flip_weight(w.data_ptr(), wt.data_ptr(), (int)Cout, (int)C, (int)R, (int)S,
+                                   cur_stream()),
+            "conv_flip_weight");
+  return wt;
 }
 
 // dW of an NHWC convolution: [Cout, C, R, S] channels_last, bf16 (for MasterSGD) or fp32.
@@ -961,8 +1027,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "arena_amd native HIP kernels (gfx950)";
   m.def("linear_fwd", &linear_fwd);
   m.def("bn_fwd", &bn_fwd);
+  m.def("conv_flip_weight", &conv_flip_weight);
   m.def("bn_bwd", &bn_bwd);
-  m.def("conv_fwd", &conv_fwd);
+  m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
+        py::arg("variant"), py::arg("with_stats"), py::arg("addend") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

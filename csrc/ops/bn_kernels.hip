@@ -183,54 +183,124 @@ __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, l
   }
 }
 
-// 8 channels per block; thread (j = t / 8, c = t % 8) merges partials j, j + 32, ... of channel
-// blockIdx.x * 8 + c in fp64, then the 32 per-thread results are merged by an LDS tree.
-constexpr int kFinCh = 8, kFinLanes = kT / kFinCh;
+// Finalize = merge of the per-block (or per-conv-tile) partials, [nblk][2][C] floats, into the
+// per-channel outputs. Up to 3136 partials per channel arrive from a conv epilogue, so the merge is
+// a two-level parallel reduction: block (g, p) of a (C/64) x P grid gives each of its 4 waves one
+// channel per lane (coalesced 256-byte reads of a partial row) and a strided share of the
+// partials, with 8 loads in flight per lane and no division in the loop; the block's sums go to
+// `lvl2` and the last of the P blocks of channel group g (ticket counter) merges them in a fixed
+// order and writes the outputs. Statistics use shifted fp64 sums: with K = the first partial's
+// mean, S1 = sum n_b (m_b - K), S2 = sum (M2_b + n_b (m_b - K)^2), so mean = K + S1/N and
+// M2 = S2 - S1^2/N without cancellation. (The previous form, a serial fp64 Chan merge per thread,
+// was latency-bound: 13.5 us per layer on average, 43 us behind a 56x56 conv.)
+constexpr int kFinWaves = kT / 64;
+constexpr int kFinU = 8;        // partials per lane per load batch
+constexpr int kFinMaxP = 64;    // level-1 blocks per channel group
+
+int fin_blocks_per_group(int nblk) {
+  int p = (nblk + kFinWaves * kFinU - 1) / (kFinWaves * kFinU);
+  return p < 1 ? 1 : (p > kFinMaxP ? kFinMaxP : p);
+}
+
+// Sum of the 4 waves' (a, b, c) in LDS, fixed order, into wave 0's lanes. Returns false on the
+// other waves (they are done).
+__device__ __forceinline__ bool fin_block_sum(double& a, double& b, double& c) {
+  __shared__ double sh[3][kFinWaves][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  sh[0][wv][lane] = a; sh[1][wv][lane] = b; sh[2][wv][lane] = c;
+  __syncthreads();
+  if (wv != 0) return false;
+  a = ((sh[0][0][lane] + sh[0][1][lane]) + (sh[0][2][lane] + sh[0][3][lane]));
+  b = ((sh[1][0][lane] + sh[1][1][lane]) + (sh[1][2][lane] + sh[1][3][lane]));
+  c = ((sh[2][0][lane] + sh[2][1][lane]) + (sh[2][2][lane] + sh[2][3][lane]));
+  return true;
+}
+
+// Wave 0 of a level-1 block: publish (a, b, c) and take a ticket. Returns true on the last block
+// of the group, with (a, b, c) replaced by the merge over all P blocks (fixed order).
+__device__ __forceinline__ bool fin_level2(double& a, double& b, double& c, double* __restrict__ lvl2,
+                                           unsigned* __restrict__ tickets) {
+  const int lane = threadIdx.x & 63, g = blockIdx.x, p = blockIdx.y, P = gridDim.y;
+  double* mine = lvl2 + ((long long)g * P + p) * 3 * 64;
+  mine[lane] = a; mine[64 + lane] = b; mine[128 + lane] = c;
+  // release: this wave's stores reach device scope before the ticket (the explicit vmcnt(0):
+  // hipcc may drop the wait after the L2 write-back when its scoreboard looks empty)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned old = 0;
+  if (lane == 0) old = __hip_atomic_fetch_add(tickets + g, 1u, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
+  old = __shfl(old, 0);
+  if (old != (unsigned)(P - 1)) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidate has landed before the reads
+  const double* base = lvl2 + (long long)g * P * 3 * 64;
+  double sa = 0.0, sb = 0.0, sc = 0.0;
+  int q = 0;
+  for (; q + 4 <= P; q += 4) {
+    double va[4], vb[4], vc[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double* r = base + (long long)(q + u) * 3 * 64;
+      va[u] = r[lane]; vb[u] = r[64 + lane]; vc[u] = r[128 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) { sa += va[u]; sb += vb[u]; sc += vc[u]; }
+  }
+  for (; q < P; ++q) {
+    const double* r = base + (long long)q * 3 * 64;
+    sa += r[lane]; sb += r[64 + lane]; sc += r[128 + lane];
+  }
+  if (lane == 0) __hip_atomic_store(tickets + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  a = sa; b = sb; c = sc;
+  return true;
+}
 
 __global__ __launch_bounds__(kT) void bn_stats_finalize_kernel(const float* __restrict__ part,
                                                                int nblk, long long M, int C,
-                                                               long long rpb, ArenaBNStats out) {
-  const int cl = threadIdx.x % kFinCh, j = threadIdx.x / kFinCh;
-  const int c = blockIdx.x * kFinCh + cl;
+                                                               long long rpb,
+                                                               double* __restrict__ lvl2,
+                                                               unsigned* __restrict__ tickets,
+                                                               ArenaBNStats out) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int ci = c < C ? c : C - 1;
+  const float* pc = part + ci;
+  const double K = (double)pc[0];
+  double n = 0.0, s1 = 0.0, s2 = 0.0;
+  const int stride = kFinWaves * (int)gridDim.y;
+  for (int b = (int)blockIdx.y * kFinWaves + wv; b < nblk; b += kFinU * stride) {
+    float mb[kFinU], sb[kFinU];
+    double nb[kFinU];
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u) {
+      const int bb = b + u * stride;
+      const bool ok = bb < nblk;
+      const long long o = (long long)(ok ? bb : 0) * 2 * C;
+      mb[u] = pc[o];
+      sb[u] = pc[o + C];
+      const long long r0 = (long long)bb * rpb;
+      nb[u] = ok ? (double)(min(M, r0 + rpb) - r0) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u) {
+      const double d = (double)mb[u] - K;
+      n += nb[u];
+      s1 += nb[u] * d;
+      s2 += (nb[u] > 0.0 ? (double)sb[u] : 0.0) + nb[u] * d * d;
+    }
+  }
+  if (!fin_block_sum(n, s1, s2)) return;
+  if (gridDim.y > 1 && !fin_level2(n, s1, s2, lvl2, tickets)) return;
   // the module's batch counter rides along (one launch fewer per BN layer than a separate add)
-  if (out.batches != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *out.batches += 1;
-  double na = 0.0, ma = 0.0, sa = 0.0;
-  if (c < C) {
-    for (int b = j; b < nblk; b += kFinLanes) {
-      const long long br0 = (long long)b * rpb;
-      const double nb = (double)(min(M, br0 + rpb) - br0);
-      if (nb <= 0.0) continue;
-      const double mb = part[(long long)b * 2 * C + c];
-      const double sb = part[(long long)b * 2 * C + C + c];
-      const double nab = na + nb;
-      const double d = mb - ma;
-      ma += d * (nb / nab);
-      sa += sb + d * d * (na * nb / nab);
-      na = nab;
-    }
-  }
-  __shared__ double s_n[kT], s_m[kT], s_s[kT];
-  s_n[threadIdx.x] = na; s_m[threadIdx.x] = ma; s_s[threadIdx.x] = sa;
-  __syncthreads();
-  for (int w = kFinLanes / 2; w > 0; w >>= 1) {
-    if (j < w) {
-      const int o = threadIdx.x + w * kFinCh;
-      const double nb = s_n[o];
-      if (nb > 0.0) {
-        const double n0 = s_n[threadIdx.x], m0 = s_m[threadIdx.x];
-        const double nab = n0 + nb, d = s_m[o] - m0;
-        s_m[threadIdx.x] = m0 + d * (nb / nab);
-        s_s[threadIdx.x] += s_s[o] + d * d * (n0 * nb / nab);
-        s_n[threadIdx.x] = nab;
-      }
-    }
-    __syncthreads();
-  }
-  if (j != 0 || c >= C) return;
-  na = s_n[cl]; ma = s_m[cl]; sa = s_s[cl];
-  const double var = sa / na;  // biased: what training normalises with
+  if (out.batches != nullptr && blockIdx.x == 0 && lane == 0) *out.batches += 1;
+  if (c >= C) return;
+  const double mean = K + s1 / n;
+  double m2 = s2 - s1 * s1 / n;
+  m2 = m2 > 0.0 ? m2 : 0.0;
+  const double var = m2 / n;  // biased: what training normalises with
   const float invstd = (float)(1.0 / sqrt(var + (double)out.eps));
-  out.mean[c] = (float)ma;
+  out.mean[c] = (float)mean;
   out.invstd[c] = invstd;
   const float gam = out.gamma ? out.gamma[c] : 1.f;
   const float bet = out.beta ? out.beta[c] : 0.f;
@@ -238,8 +308,8 @@ __global__ __launch_bounds__(kT) void bn_stats_finalize_kernel(const float* __re
   out.shift[c] = bet;  // y = (x - mean) * scale + shift: no cancellation when |mean| >> std
   if (out.running_mean) {
     const float mom = out.momentum;
-    out.running_mean[c] = (1.f - mom) * out.running_mean[c] + mom * (float)ma;
-    const double unbiased = na > 1.0 ? sa / (na - 1.0) : var;
+    out.running_mean[c] = (1.f - mom) * out.running_mean[c] + mom * (float)mean;
+    const double unbiased = n > 1.0 ? m2 / (n - 1.0) : var;
     out.running_var[c] = (1.f - mom) * out.running_var[c] + mom * (float)unbiased;
   }
 }
@@ -360,28 +430,31 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
 
 __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const float* __restrict__ part,
                                                              int nblk, long long M, int C,
+                                                             double* __restrict__ lvl2,
+                                                             unsigned* __restrict__ tickets,
                                                              ArenaBNBwd out) {
-  const int cl = threadIdx.x % kFinCh, j = threadIdx.x / kFinCh;
-  const int c = blockIdx.x * kFinCh + cl;
-  double a = 0.0, b = 0.0;
-  if (c < C) {
-    for (int blk = j; blk < nblk; blk += kFinLanes) {
-      a += part[(long long)blk * 2 * C + c];
-      b += part[(long long)blk * 2 * C + C + c];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const float* pc = part + (c < C ? c : C - 1);
+  double a = 0.0, b = 0.0, unused = 0.0;
+  const int stride = kFinWaves * (int)gridDim.y;
+  for (int blk = (int)blockIdx.y * kFinWaves + wv; blk < nblk; blk += kFinU * stride) {
+    float va[kFinU], vb[kFinU];
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u) {
+      const int bb = blk + u * stride;
+      const bool ok = bb < nblk;
+      const long long o = (long long)(ok ? bb : 0) * 2 * C;
+      const float x0 = pc[o], x1 = pc[o + C];  // clamped address: unconditional loads
+      va[u] = ok ? x0 : 0.f;
+      vb[u] = ok ? x1 : 0.f;
     }
+#pragma unroll
+    for (int u = 0; u < kFinU; ++u) { a += (double)va[u]; b += (double)vb[u]; }
   }
-  __shared__ double s_a[kT], s_b[kT];
-  s_a[threadIdx.x] = a; s_b[threadIdx.x] = b;
-  __syncthreads();
-  for (int w = kFinLanes / 2; w > 0; w >>= 1) {
-    if (j < w) {
-      s_a[threadIdx.x] += s_a[threadIdx.x + w * kFinCh];
-      s_b[threadIdx.x] += s_b[threadIdx.x + w * kFinCh];
-    }
-    __syncthreads();
-  }
-  if (j != 0 || c >= C) return;
-  a = s_a[cl]; b = s_b[cl];
+  if (!fin_block_sum(a, b, unused)) return;
+  if (gridDim.y > 1 && !fin_level2(a, b, unused, lvl2, tickets)) return;
+  if (c >= C) return;
   const float invstd = out.invstd[c];
   const float gam = out.gamma ? out.gamma[c] : 1.f;
   if (out.dgamma) out.dgamma[c] = (float)(b * invstd);
@@ -459,6 +532,12 @@ void arena_bn_set_reduce_geometry(long long max_blocks, long long min_rounds) {
   g_min_rounds = min_rounds < 1 ? 1 : min_rounds;
 }
 
+// Level-2 workspace of the finalize kernels for `nblk` partials of C channels (doubles), and the
+// ticket counters they need: ARENA_BN_TICKETS_PER_SET per launch, zero on entry and left zero.
+long long arena_bn_lvl2_doubles(long long nblk, int C) {
+  return (long long)((C + 63) / 64) * fin_blocks_per_group((int)nblk) * 3 * 64;
+}
+
 long long arena_bn_workspace_floats(long long M, int C) {
   if (bad_shape(M, C)) return 0;
   long long rpb;
@@ -470,12 +549,13 @@ long long arena_bn_workspace_floats(long long M, int C) {
 // each), written by the producing convolution's epilogue (conv_kernels.hip): no statistics pass.
 hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, long long M, int C,
                         int relu, int training, float* part, int ext_nblk, long long ext_rpb,
-                        ArenaBNStats st, hipStream_t stream) {
+                        double* lvl2, unsigned* tickets, ArenaBNStats st, hipStream_t stream) {
   if (bad_shape(M, C)) return hipErrorInvalidValue;
+  const int groups = (C + 63) / 64;
   if (training && ext_nblk > 0) {
     if (ext_rpb <= 0 || (long long)ext_nblk * ext_rpb < M) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kT), 0,
-                       stream, part, ext_nblk, M, C, ext_rpb, st);
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups, fin_blocks_per_group(ext_nblk)),
+                       dim3(kT), 0, stream, part, ext_nblk, M, C, ext_rpb, lvl2, tickets, st);
   } else if (training) {
     long long rpb;
     const long long nb = reduce_blocks(M, C, &rpb);
@@ -485,8 +565,8 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, long
     else
       hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kT), 0, stream,
                          static_cast<const float*>(x), M, C, rpb, part);
-    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kT), 0,
-                       stream, part, (int)nb, M, C, rpb, st);
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups, fin_blocks_per_group((int)nb)),
+                       dim3(kT), 0, stream, part, (int)nb, M, C, rpb, lvl2, tickets, st);
   }
   const long long nvec = M * (C / kVec);
   const int nb = elementwise_blocks(nvec);
@@ -512,8 +592,8 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, long
 }
 
 hipError_t arena_bn_bwd(int dtype, const void* dy, const void* y, const void* x, void* dx,
-                        void* dres, long long M, int C, int relu, float* part,
-                        ArenaBNBwd co, hipStream_t stream) {
+                        void* dres, long long M, int C, int relu, float* part, double* lvl2,
+                        unsigned* tickets, ArenaBNBwd co, hipStream_t stream) {
   if (bad_shape(M, C)) return hipErrorInvalidValue;
   long long rpb;
   const long long nb = reduce_blocks(M, C, &rpb);
@@ -527,8 +607,8 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const void* y, const void* x,
     if (relu) ARENA_BN_RED(float, true); else ARENA_BN_RED(float, false);
   }
 #undef ARENA_BN_RED
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + kFinCh - 1) / kFinCh), dim3(kT), 0, stream,
-                     part, (int)nb, M, C, co);
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64, fin_blocks_per_group((int)nb)),
+                     dim3(kT), 0, stream, part, (int)nb, M, C, lvl2, tickets, co);
   const long long nvec = M * (C / kVec);
   long long ne = (nvec + kT - 1) / kT;
   ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);

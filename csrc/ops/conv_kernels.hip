@@ -51,6 +51,8 @@ struct ConvArgs {
   const uint16_t* w;   // [Cout][R][S][C] bf16
   uint16_t* y;         // [N][Ho][Wo][Cout] bf16
   float* part;         // optional BatchNorm partials [m_tiles][2][Cout] (tile mean, tile M2)
+  const uint16_t* add; // optional [M][Cout] bf16 added to the fp32 sums before rounding (the
+                       // other gradient of a tensor with two consumers: the residual join)
   int N, H, W, C, Cout, R, S, stride, pad, Ho, Wo;
   int M;               // N * Ho * Wo
   int Ktot;            // R * S * C
@@ -203,6 +205,19 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
     const int m = m0 + wm * WM + i * 16 + fr;
     if (m >= a.M) continue;
     uint16_t* yrow = a.y + (size_t)m * a.Cout + n0 + wn * WN + 4 * fq;
+    if (a.add != nullptr) {
+      const uint16_t* arow = a.add + (yrow - a.y);
+      uint2 q[NI];
+#pragma unroll
+      for (int j = 0; j < NI; ++j) q[j] = *reinterpret_cast<const uint2*>(arow + j * 16);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        acc[i][j][0] += __uint_as_float(q[j].x << 16);
+        acc[i][j][1] += __uint_as_float(q[j].x & 0xffff0000u);
+        acc[i][j][2] += __uint_as_float(q[j].y << 16);
+        acc[i][j][3] += __uint_as_float(q[j].y & 0xffff0000u);
+      }
+    }
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
       uint2 v;
@@ -281,9 +296,9 @@ extern "C" {
 // MIOpen): C % 64 != 0, Cout % 64 != 0, or an unknown tile variant.
 // variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (BM x BN output tile per block).
 // part (optional): BatchNorm partials of y, [ceil(M / BM)][2][Cout] (see the STATS epilogue).
-hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, int N, int H, int W,
-                          int C, int Cout, int R, int S, int stride, int pad, int variant,
-                          hipStream_t st) {
+hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, const void* add,
+                          int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad,
+                          int variant, hipStream_t st) {
   if (C % kBK || Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
     return hipErrorInvalidValue;
   ConvArgs a{};
@@ -291,6 +306,7 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, in
   a.w = (const uint16_t*)w;
   a.y = (uint16_t*)y;
   a.part = part;
+  a.add = (const uint16_t*)add;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
   a.stride = stride; a.pad = pad;
   a.Ho = (H + 2 * pad - R) / stride + 1;
@@ -310,6 +326,58 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, in
 }
 
 }  // extern "C"
+
+// ================================================================================================
+// The backward-data pass runs the forward kernel on W'[ci][r][s][co] = W[co][R-1-r][S-1-s][ci]
+// (arena_amd/ops/conv.py). Per tap that is a transpose of the [Cout][C] slice: one 64x64 bf16 tile
+// per block through LDS (a 2-byte pad per row keeps the column reads on distinct banks), 16-byte
+// loads and stores. One launch instead of torch's flip + strided copy (two kernels per dgrad, and
+// a memcpy for 1x1 weights).
+// ================================================================================================
+namespace {
+
+__global__ __launch_bounds__(256) void conv_flip_weight_kernel(const uint16_t* __restrict__ w,
+                                                               uint16_t* __restrict__ wt, int Cout,
+                                                               int C, int R, int S) {
+  __shared__ uint16_t tile[64][64 + 2];
+  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64, tap = blockIdx.z;
+  const int r = tap / S, s = tap - r * S;
+  const int src_tap = (R - 1 - r) * S + (S - 1 - s);
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {   // 64 rows (co) x 8 chunks of 8 ci
+    const int q = t + k * 256, row = q >> 3, ch = q & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(
+        w + ((size_t)(co0 + row) * R * S + src_tap) * C + ci0 + ch * 8);
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      tile[row][ch * 8 + 2 * e] = (uint16_t)(u[e] & 0xffffu);
+      tile[row][ch * 8 + 2 * e + 1] = (uint16_t)(u[e] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {   // 64 rows (ci) x 8 chunks of 8 co
+    const int q = t + k * 256, row = q >> 3, ch = q & 7;
+    uint32_t u[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      u[e] = (uint32_t)tile[ch * 8 + 2 * e][row] | ((uint32_t)tile[ch * 8 + 2 * e + 1][row] << 16);
+    *reinterpret_cast<uint4*>(wt + ((size_t)(ci0 + row) * R * S + tap) * Cout + co0 + ch * 8) =
+        make_uint4(u[0], u[1], u[2], u[3]);
+  }
+}
+
+}  // namespace
+
+extern "C" hipError_t arena_conv_flip_weight(const void* w, void* wt, int Cout, int C, int R, int S,
+                                             hipStream_t st) {
+  if (Cout % 64 || C % 64 || R <= 0 || S <= 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(conv_flip_weight_kernel, dim3(C / 64, Cout / 64, R * S), dim3(256), 0, st,
+                     (const uint16_t*)w, (uint16_t*)wt, Cout, C, R, S);
+  return hipGetLastError();
+}
 
 // ================================================================================================
 // Backward-weight: dW[co][r][s][ci] = sum_m dY[m][co] * X[pix(m, r, s)][ci]
@@ -484,28 +552,53 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
     }
 }
 
-// out = sum over splits of ws (fixed order: 8 interleaved partial sums, then combined), bf16
-// and/or fp32 output. One float per thread, so a small dW (4096 floats for a 64x64 1x1 conv,
-// summed over hundreds of slabs) still spreads over enough waves; 8 loads in flight per thread.
-__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float* __restrict__ ws,
-                                                                int splits, long long n,
-                                                                uint16_t* __restrict__ out_bf,
-                                                                float* __restrict__ out_f,
+// out = sum over splits of ws, bf16 and/or fp32. Thread (col, grp) of a block sums float4 column
+// blockIdx.x * 32 + col over splits grp, grp + 8, ... (8 float4 loads in flight), and the 8 groups
+// are combined in LDS in a fixed order (bit-reproducible). Splitting the split dimension over the
+// block's waves keeps a small dW (4096 floats for a 64x64 1x1 conv, summed over hundreds of slabs)
+// from being a serial chain of dependent load batches (16 us per layer on average before).
+constexpr int kRedCols = 32, kRedGroups = 8, kRedU = 8;
+
+__global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float4* __restrict__ ws,
+                                                                int splits, long long n4,
+                                                                uint2* __restrict__ out_bf,
+                                                                float4* __restrict__ out_f,
                                                                 float scale) {
-  for (long long i = blockIdx.x * 256LL + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
-    float p[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    int k = 0;
-    for (; k + 8 <= splits; k += 8) {
-      float v[8];
+  const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
+  const long long i = (long long)blockIdx.x * kRedCols + col;
+  const float4* src = ws + (i < n4 ? i : 0);
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  int k = grp;
+  for (; k + (kRedU - 1) * kRedGroups < splits; k += kRedU * kRedGroups) {
+    float4 v[kRedU];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = ws[i + (long long)(k + u) * n];
+    for (int u = 0; u < kRedU; ++u) v[u] = src[(long long)(k + u * kRedGroups) * n4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) p[u] += v[u];
+    for (int u = 0; u < kRedU; ++u) {
+      acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
     }
-    for (int u = 0; k < splits; ++k, ++u) p[u] += ws[i + (long long)k * n];
-    const float s = (((p[0] + p[1]) + (p[2] + p[3])) + ((p[4] + p[5]) + (p[6] + p[7]))) * scale;
-    if (out_f) out_f[i] = s;
-    if (out_bf) out_bf[i] = (uint16_t)(__float_as_uint(bf16_round(s)) >> 16);
+  }
+  for (; k < splits; k += kRedGroups) {
+    const float4 v = src[(long long)k * n4];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  __shared__ float4 red[kRedGroups][kRedCols];
+  red[grp][col] = acc;
+  __syncthreads();
+  if (grp != 0 || i >= n4) return;
+  float4 s = red[0][col];
+#pragma unroll
+  for (int g = 1; g < kRedGroups; ++g) {
+    const float4 v = red[g][col];
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  s.x *= scale; s.y *= scale; s.z *= scale; s.w *= scale;
+  if (out_f) out_f[i] = s;
+  if (out_bf) {
+    uint2 b;
+    b.x = pack_bf16x2(s.x, s.y);
+    b.y = pack_bf16x2(s.z, s.w);
+    out_bf[i] = b;
   }
 }
 
@@ -585,10 +678,11 @@ hipError_t arena_conv_wgrad(const void* x, const void* dy, float* ws, void* dw_b
   }
   if (e != hipSuccess) return e;
   const int splits = arena_conv_wgrad_splits(N, a.Ho, a.Wo, Cout, a.Ktot, variant, splits_hint);
-  const long long n = (long long)Cout * a.Ktot;
-  const int blocks = (int)std::min<long long>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, splits, n,
-                     (uint16_t*)dw_bf16, dw_f32, scale);
+  const long long n4 = (long long)Cout * a.Ktot / 4;  // Cout % 64 == 0
+  const int blocks = (int)((n4 + kRedCols - 1) / kRedCols);
+  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st,
+                     reinterpret_cast<const float4*>(ws), splits, n4,
+                     reinterpret_cast<uint2*>(dw_bf16), reinterpret_cast<float4*>(dw_f32), scale);
   return hipGetLastError();
 }
 

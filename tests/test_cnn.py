@@ -87,3 +87,48 @@ def test_resnet50_shape_and_size():
     assert out.shape == (2, 10)
     with pytest.raises(ValueError):
         resnet("vgg16")
+
+
+def test_grad_join_protocol_either_order():
+    """GradJoin: whichever consumer's backward runs first parks its gradient and returns None;
+    the second returns the sum. The input's gradient equals autograd's own sum in both orders,
+    and a join with a single registered consumer is inert."""
+    import torch
+    from arena_amd.ops.conv import GradJoin
+
+    class Consumer(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, k, join, log, name):
+            ctx.k, ctx.join, ctx.log, ctx.name = k, join.register() if join else None, log, name
+            return x * k
+
+        @staticmethod
+        def backward(ctx, g):
+            ctx.log.append(ctx.name)
+            dx = g * ctx.k
+            j = ctx.join
+            if j is not None and j.active():
+                other = j.other()
+                if other is not None:
+                    dx = dx + other
+                if j.park_or_take(dx):
+                    dx = None
+            return dx, None, None, None, None
+
+    for order in ("ab", "ba"):
+        x = torch.randn(5, requires_grad=True)
+        log = []
+        join = GradJoin()
+        a = Consumer.apply(x, 2.0, join, log, "a")
+        b = Consumer.apply(x, 3.0, join, log, "b")
+        # make one branch longer so the engine reaches the consumers in the wanted order
+        loss = (a * 1.0).sum() + b.sum() if order == "ab" else a.sum() + (b * 1.0).sum()
+        loss.backward()
+        torch.testing.assert_close(x.grad, torch.full_like(x, 5.0))
+        assert join.arrived == 0 and join.pending is None
+        assert sorted(log) == ["a", "b"]
+    x = torch.randn(3, requires_grad=True)
+    lone = GradJoin()
+    y = Consumer.apply(x, 4.0, lone, [], "a") + x   # second consumer is plain autograd
+    y.sum().backward()
+    torch.testing.assert_close(x.grad, torch.full_like(x, 5.0))
