@@ -5,8 +5,9 @@ and apply ReLU: ``y = relu(bn(x) + residual)``. That is the whole tail of a ResN
 one module. On an MI355X, with a channels_last bf16/fp32 input and a supported channel count,
 it runs the HIP kernels in ``csrc/ops/bn_kernels.hip``:
 
-* forward: 2 launches (statistics, then apply);
-* backward: 2 launches (reductions, then dx and the residual gradient).
+* forward: 2 launches (statistics, then apply + ReLU mask bits); the statistics come from the
+  producing convolution's epilogue when it ran on the MFMA kernel (then only a finalize);
+* backward: 2 launches (reductions, then dx and the residual gradient) plus a finalize.
 
 Otherwise it runs the same math as stock PyTorch ops. That includes CPU tensors, which serve as
 the reference.
@@ -15,7 +16,7 @@ Semantics match ``nn.BatchNorm2d`` in training and eval mode:
 
 * batch statistics with the biased variance for normalisation;
 * running statistics updated with ``momentum`` and the unbiased variance;
-* the ReLU mask recovered from the saved output (y > 0).
+* the ReLU mask is the saved output's sign (y > 0), stored as one bit per element.
 """
 from __future__ import annotations
 
@@ -56,9 +57,10 @@ class _BNActFn(torch.autograd.Function):
                 eps, relu, num_batches=None, stats=None, join=None):
         ext = _ext.load()
         part, rpb = stats if (stats is not None and training) else (None, 0)
-        y, mean, invstd = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
-                                     training, momentum, eps, relu, num_batches, part, rpb)
-        ctx.save_for_backward(x, y, mean, invstd, weight)
+        y, mean, invstd, mask = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
+                                           training, momentum, eps, relu, num_batches, part, rpb)
+        # the ReLU mask is kept as bits (M*C/8 bytes), not as a reference to y
+        ctx.save_for_backward(x, mask if relu and training else None, mean, invstd, weight)
         ctx.relu, ctx.has_res, ctx.training = relu, residual is not None, training
         ctx.affine = weight is not None
         # the residual is also another op's input: gradients meet in a GradJoin (ops/conv.py)
@@ -67,12 +69,12 @@ class _BNActFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, y, mean, invstd, weight = ctx.saved_tensors
+        x, mask, mean, invstd, weight = ctx.saved_tensors
         if not ctx.training:
             raise RuntimeError("BatchNormAct2d backward in eval mode is not supported by the "
                                "fused kernels; use train() or the PyTorch path")
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, y, x, mean, invstd, weight, ctx.relu,
+        dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, mask, x, mean, invstd, weight, ctx.relu,
                                                      ctx.has_res, ctx.affine)
         if not ctx.has_res:
             dres = None

@@ -63,9 +63,9 @@ hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, i
                              hipStream_t);
 hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, int, int, int, int,
                              int, hipStream_t);
-hipError_t arena_bn_fwd(int, const void*, const void*, void*, long long, int, int, int, float*,
-                        int, long long, double*, unsigned*, ArenaBNStats, hipStream_t);
-hipError_t arena_bn_bwd(int, const void*, const void*, const void*, void*, void*, long long, int,
+hipError_t arena_bn_fwd(int, const void*, const void*, void*, uint8_t*, long long, int, int, int,
+                        float*, int, long long, double*, unsigned*, ArenaBNStats, hipStream_t);
+hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, void*, long long, int,
                         int, float*, double*, unsigned*, ArenaBNBwd, hipStream_t);
 #ifdef ARENA_TIMELINE
 hipError_t arena_timeline_read(long long*, int);
@@ -693,7 +693,8 @@ Tensor bn_lvl2(int64_t nblk, int64_t C, const Tensor& like) {
   return torch::empty({arena_bn_lvl2_doubles(nblk, (int)C)}, like.options().dtype(torch::kFloat64));
 }
 
-// Returns (y, mean, invstd). Eval mode normalises with the running statistics.
+// Returns (y, mean, invstd, mask). Eval mode normalises with the running statistics. mask (relu
+// in training, else empty): uint8 [M * C / 8], bit i of byte v = (y.flat[8 v + i] > 0).
 // stats_part/stats_rpb: BatchNorm partials of x from conv_fwd(with_stats=True) (training only).
 std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT running_mean,
                            OptT running_var, bool training, double momentum, double eps,
@@ -747,6 +748,8 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
     if (beta.has_value()) shift.copy_(*beta); else shift.zero_();
   }
   Tensor y = torch::empty_like(x);
+  Tensor mask = (training && relu) ? torch::empty({g.M * g.C / 8}, x.options().dtype(torch::kUInt8))
+                                   : Tensor();
   const int ext_nblk = training && stats_part.has_value()
                            ? (int)((g.M + stats_rpb - 1) / stats_rpb) : 0;
   Tensor lvl2;
@@ -757,20 +760,26 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
     tickets = bn_tickets(x);
   }
   check_hip(arena_bn_fwd(g.dtype, x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr,
-                         y.data_ptr(), g.M, g.C, relu ? 1 : 0, training ? 1 : 0,
+                         y.data_ptr(), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, g.M,
+                         g.C, relu ? 1 : 0, training ? 1 : 0,
                          training ? part.data_ptr<float>() : nullptr, ext_nblk,
                          (long long)stats_rpb, training ? lvl2.data_ptr<double>() : nullptr,
                          tickets, st, cur_stream()),
             "bn_fwd");
-  return {y, mean, invstd};
+  return {y, mean, invstd, mask};
 }
 
-// Returns (dx, dres or empty, dgamma or empty, dbeta or empty).
-std::vector<Tensor> bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor invstd, OptT gamma,
+// Returns (dx, dres or empty, dgamma or empty, dbeta or empty). mask: bn_fwd's ReLU bits (relu).
+std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor invstd, OptT gamma,
                            bool relu, bool with_res, bool affine_grads) {
   const BNGeom g = bn_geom(x, "x");
   bn_same(x, dy, "grad_output");
-  bn_same(x, y, "output");
+  if (relu) {
+    TORCH_CHECK(mask.has_value() && mask->is_cuda() && mask->scalar_type() == torch::kUInt8 &&
+                    mask->is_contiguous() && mask->numel() == g.M * g.C / 8 &&
+                    mask->device() == x.device(),
+                "bn_bwd: relu needs the forward's uint8 mask of M*C/8 bytes");
+  }
   check_f32(mean, "mean");
   check_f32(invstd, "invstd");
   TORCH_CHECK(mean.numel() == g.C && invstd.numel() == g.C, "saved statistics must have C elements");
@@ -794,7 +803,8 @@ std::vector<Tensor> bn_bwd(Tensor dy, Tensor y, Tensor x, Tensor mean, Tensor in
   Tensor lvl2 = bn_lvl2(part.numel() / (2 * g.C), g.C, x);
   Tensor dx = torch::empty_like(x);
   Tensor dres = with_res ? torch::empty_like(x) : Tensor();
-  check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(), y.data_ptr(), x.data_ptr(), dx.data_ptr(),
+  check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(),
+                         relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(), dx.data_ptr(),
                          with_res ? dres.data_ptr() : nullptr, g.M, g.C, relu ? 1 : 0,
                          part.data_ptr<float>(), lvl2.data_ptr<double>(), bn_tickets(x), b,
                          cur_stream()),

@@ -8,11 +8,13 @@
 //
 //   forward   stats      1 read of x            -> per-channel mean / invstd (+ running stats)
 //             apply      1 read of x (+ res), 1 write of y = act(x*scale + shift (+ res))
-//   backward  reduce     1 read of dy, y, x     -> dgamma, dbeta and the dx coefficients
-//             dx         1 read of dy, y, x, 1 write of dx (+ 1 write of dres = the masked dy)
+//   backward  reduce     1 read of dy, x (+ mask bits) -> dgamma, dbeta and the dx coefficients
+//             dx         1 read of dy, x (+ mask bits), 1 write of dx (+ 1 write of dres = the
+//                        masked dy)
 //
-// The ReLU mask comes from the saved output y (y > 0), so no mask tensor is stored. It is the
-// same y the next convolution keeps for its own backward.
+// The ReLU mask (y > 0) is written by the apply pass as one bit per element (a byte per 8-channel
+// vector): the backward passes read M*C/8 bytes instead of re-reading the bf16 output y, which
+// removes one of the three input streams of the reduction and one of the four of the dx pass.
 //
 // Layout: x is [M][C] with M = N*H*W (a channels_last tensor) and C % 8 == 0, C <= 2048.
 // A thread owns 8 consecutive channels: one 16-byte load for bf16, two for fp32.
@@ -316,10 +318,30 @@ __global__ __launch_bounds__(kT) void bn_stats_finalize_kernel(const float* __re
 
 // ------------------------------------------------------------------------------------ apply
 // y = act((x - mean) * scale + shift (+ res)), 2 vectors per thread per round for load ILP.
+// Bits of the 8 stored outputs that are > 0 (after the rounding the store applies, so the mask is
+// exactly "saved y > 0").
+template <typename T>
+__device__ __forceinline__ uint32_t pos_bits(const float o[kVec]) {
+  uint32_t b = 0;
+#pragma unroll
+  for (int i = 0; i < kVec; ++i) {
+    bool p;
+    if constexpr (sizeof(T) == 2) {
+      const uint16_t h = f2bf(o[i]);
+      p = (h & 0x8000u) == 0 && (h & 0x7fffu) != 0 && (h & 0x7fffu) <= 0x7f80u;
+    } else {
+      p = o[i] > 0.f;
+    }
+    b |= (p ? 1u : 0u) << i;
+  }
+  return b;
+}
+
 template <typename T, bool RELU, bool RES>
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
                                                       const T* __restrict__ res,
                                                       T* __restrict__ y,
+                                                      uint8_t* __restrict__ mask,
                                                       const float* __restrict__ mean,
                                                       const float* __restrict__ scale,
                                                       const float* __restrict__ shift,
@@ -351,16 +373,19 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
         if (RES) t += b[u][i];
         o[i] = RELU ? fmaxf(t, 0.f) : t;
       }
-      if (ok[u]) V8<T>::store(y + vv[u] * kVec, o);
+      if (ok[u]) {
+        V8<T>::store(y + vv[u] * kVec, o);
+        if (RELU && mask != nullptr) mask[vv[u]] = (uint8_t)pos_bits<T>(o);
+      }
     }
   }
 }
 
 // ---------------------------------------------------------------------------- backward sums
-// g = RELU ? dy * (y > 0) : dy;  per channel: sum g, sum g * (x - mean).  part: [nblk][2][C]
+// g = RELU ? dy * mask : dy;  per channel: sum g, sum g * (x - mean).  part: [nblk][2][C]
 template <typename T, bool RELU>
 __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__ dy,
-                                                           const T* __restrict__ y,
+                                                           const uint8_t* __restrict__ mask,
                                                            const T* __restrict__ x, long long M,
                                                            int C, long long rpb,
                                                            float* __restrict__ part,
@@ -376,33 +401,35 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
     for (int i = 0; i < kVec; ++i) mu[i] = out.mean[q.g * kVec + i];
     const long long off = (long long)q.g * kVec;
     long long r = r0 + q.slot;
-    for (; r + q.rip < r1; r += 2LL * q.rip) {  // 2 rows per step: 6 loads in flight
-      float d[2][kVec], h[2][kVec], v[2][kVec];
+    for (; r + q.rip < r1; r += 2LL * q.rip) {  // 2 rows per step: all loads in flight
+      float d[2][kVec], v[2][kVec];
+      uint32_t mb[2] = {0xffu, 0xffu};
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
-        const long long p = (r + (long long)u * q.rip) * C + off;
+        const long long rr = r + (long long)u * q.rip;
+        const long long p = rr * C + off;
         V8<T>::load(dy + p, d[u]);
-        if (RELU) V8<T>::load(y + p, h[u]);
+        if (RELU) mb[u] = mask[rr * q.cg + q.g];
         V8<T>::load(x + p, v[u]);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int i = 0; i < kVec; ++i) {
-          const float g = RELU ? (h[u][i] > 0.f ? d[u][i] : 0.f) : d[u][i];
+          const float g = ((mb[u] >> i) & 1u) ? d[u][i] : 0.f;
           sg[i] += g;
           sgx[i] = fmaf(g, v[u][i] - mu[i], sgx[i]);
         }
     }
     for (; r < r1; r += q.rip) {
-      float d[kVec], h[kVec], v[kVec];
+      float d[kVec], v[kVec];
       const long long p = r * C + off;
       V8<T>::load(dy + p, d);
-      if (RELU) V8<T>::load(y + p, h);
+      const uint32_t mb = RELU ? (uint32_t)mask[r * q.cg + q.g] : 0xffu;
       V8<T>::load(x + p, v);
 #pragma unroll
       for (int i = 0; i < kVec; ++i) {
-        const float g = RELU ? (h[i] > 0.f ? d[i] : 0.f) : d[i];
+        const float g = ((mb >> i) & 1u) ? d[i] : 0.f;
         sg[i] += g;
         sgx[i] = fmaf(g, v[i] - mu[i], sgx[i]);
       }
@@ -468,15 +495,15 @@ __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const float* __rest
 // --------------------------------------------------------------------------------- backward dx
 template <typename T, bool RELU, bool RES>
 __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
-                                                       const T* __restrict__ y,
+                                                       const uint8_t* __restrict__ mask,
                                                        const T* __restrict__ x,
                                                        T* __restrict__ dx, T* __restrict__ dres,
                                                        long long nvec, int cg, ArenaBNBwd co) {
   const long long stride = (long long)gridDim.x * kT;
   for (long long v = (long long)blockIdx.x * kT + threadIdx.x; v < nvec; v += stride) {
-    float d[kVec], h[kVec], xv[kVec];
+    float d[kVec], xv[kVec];
     V8<T>::load(dy + v * kVec, d);
-    if (RELU) V8<T>::load(y + v * kVec, h);
+    const uint32_t mb = RELU ? (uint32_t)mask[v] : 0xffu;
     V8<T>::load(x + v * kVec, xv);
     const int c0 = (int)(v & (cg - 1)) * kVec;
     float ca[kVec], cb[kVec], cc[kVec], mu[kVec];
@@ -487,7 +514,7 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
     float g[kVec], o[kVec];
 #pragma unroll
     for (int i = 0; i < kVec; ++i) {
-      g[i] = RELU ? (h[i] > 0.f ? d[i] : 0.f) : d[i];
+      g[i] = ((mb >> i) & 1u) ? d[i] : 0.f;
       o[i] = ca[i] * (g[i] - cb[i] - (xv[i] - mu[i]) * cc[i]);
     }
     V8<T>::store(dx + v * kVec, o);
@@ -547,8 +574,10 @@ long long arena_bn_workspace_floats(long long M, int C) {
 // dtype: 0 = f32, 1 = bf16 (all activation tensors share it)
 // ext_nblk > 0: `part` already holds the statistics partials of x ([ext_nblk][2][C], ext_rpb rows
 // each), written by the producing convolution's epilogue (conv_kernels.hip): no statistics pass.
-hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, long long M, int C,
-                        int relu, int training, float* part, int ext_nblk, long long ext_rpb,
+// mask (optional, relu only): [M * C / 8] bytes, bit i of byte v = (y[v * 8 + i] > 0)
+hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint8_t* mask,
+                        long long M, int C, int relu, int training, float* part, int ext_nblk,
+                        long long ext_rpb,
                         double* lvl2, unsigned* tickets, ArenaBNStats st, hipStream_t stream) {
   if (bad_shape(M, C)) return hipErrorInvalidValue;
   const int groups = (C + 63) / 64;
@@ -574,7 +603,7 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, long
 #define ARENA_BN_APPLY(TT, R, S)                                                             \
   hipLaunchKernelGGL((bn_apply_kernel<TT, R, S>), dim3(nb), dim3(kT), 0, stream,           \
                      static_cast<const TT*>(x), static_cast<const TT*>(res), static_cast<TT*>(y), \
-                     st.mean, st.scale, st.shift, nvec, cg)
+                     mask, st.mean, st.scale, st.shift, nvec, cg)
   const bool r = relu != 0, s = res != nullptr;
   if (dtype == 1) {
     if (r && s) ARENA_BN_APPLY(uint16_t, true, true);
@@ -591,16 +620,16 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, long
   return hipGetLastError();
 }
 
-hipError_t arena_bn_bwd(int dtype, const void* dy, const void* y, const void* x, void* dx,
+hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const void* x, void* dx,
                         void* dres, long long M, int C, int relu, float* part, double* lvl2,
                         unsigned* tickets, ArenaBNBwd co, hipStream_t stream) {
-  if (bad_shape(M, C)) return hipErrorInvalidValue;
+  if (bad_shape(M, C) || (relu && mask == nullptr)) return hipErrorInvalidValue;
   long long rpb;
   const long long nb = reduce_blocks(M, C, &rpb);
 #define ARENA_BN_RED(TT, R)                                                                  \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, R>), dim3(nb), dim3(kT), 0, stream,         \
-                     static_cast<const TT*>(dy), static_cast<const TT*>(y),                 \
-                     static_cast<const TT*>(x), M, C, rpb, part, co)
+                     static_cast<const TT*>(dy), mask, static_cast<const TT*>(x), M, C, rpb, \
+                     part, co)
   if (dtype == 1) {
     if (relu) ARENA_BN_RED(uint16_t, true); else ARENA_BN_RED(uint16_t, false);
   } else {
@@ -615,9 +644,8 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const void* y, const void* x,
   const int cg = C / kVec;
 #define ARENA_BN_DX(TT, R, S)                                                                \
   hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S>), dim3(ne), dim3(kT), 0, stream,          \
-                     static_cast<const TT*>(dy), static_cast<const TT*>(y),                 \
-                     static_cast<const TT*>(x), static_cast<TT*>(dx), static_cast<TT*>(dres), \
-                     nvec, cg, co)
+                     static_cast<const TT*>(dy), mask, static_cast<const TT*>(x),            \
+                     static_cast<TT*>(dx), static_cast<TT*>(dres), nvec, cg, co)
   const bool r = relu != 0, s = dres != nullptr;
   if (dtype == 1) {
     if (r && s) ARENA_BN_DX(uint16_t, true, true);

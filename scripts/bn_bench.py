@@ -76,9 +76,10 @@ def main():
         ext.bn_set_reduce_geometry(mb, mr)
         rows, tot_us, tot_bytes = [], 0.0, 0.0
         for M, C, uses, relu, res, x, dy, r, w, bias, rm, rv in data:
-            y, mean, invstd = ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None, None, 0)
+            y, mean, invstd, mask = ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None,
+                                               None, 0)
             f = timed(lambda: ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None, None, 0))
-            bk = timed(lambda: ext.bn_bwd(dy, y, x, mean, invstd, w, relu, res, True))
+            bk = timed(lambda: ext.bn_bwd(dy, mask if relu else None, x, mean, invstd, w, relu, res, True))
             e = M * C * 2
             # fwd: read x twice (+ res), write y; bwd: read dy, x (+ y) twice, write dx (+ dres)
             nbytes = e * ((3 + res) + (2 * (2 + relu) + 1 + res))
