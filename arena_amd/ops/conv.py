@@ -278,9 +278,56 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
     return plan
 
 
+# ------------------------------------------------------------------------------------------------
+# Weight gradients on a side stream. In a conv's backward, dX (-> the BatchNorm backward chain:
+# reduce, finalize, dx) and dW are independent; most BN-backward and finalize launches are latency-
+# or tail-bound and leave CUs idle, so running dW concurrently on a second HIP stream fills them
+# (in a captured step the two streams become parallel graph branches). The caller must join the
+# side stream before anything reads the weight gradients: ``sync_wgrad()`` (cnn_bench does it
+# between backward and the optimizer step). Off by default; single-process use only (DP bucket
+# hooks read gradients as soon as autograd hands them over).
+# ------------------------------------------------------------------------------------------------
+_ASYNC_WGRAD = False
+_SIDE: Dict[int, "torch.cuda.Stream"] = {}
+
+
+def set_async_wgrad(on: bool) -> None:
+    global _ASYNC_WGRAD
+    _ASYNC_WGRAD = bool(on)
+
+
+def async_wgrad() -> bool:
+    return _ASYNC_WGRAD
+
+
+def _side_stream(dev: torch.device) -> "torch.cuda.Stream":
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    s = _SIDE.get(idx)
+    if s is None:
+        s = _SIDE[idx] = torch.cuda.Stream(device=idx)
+    return s
+
+
+def sync_wgrad() -> None:
+    """Make the current stream wait for every weight gradient queued on the side stream."""
+    if not _SIDE or not torch.cuda.is_available():
+        return
+    s = _SIDE.get(torch.cuda.current_device())
+    if s is not None:
+        torch.cuda.current_stream().wait_stream(s)
+
+
 def plans() -> Dict[tuple, ConvPlan]:
     """The per-shape choices made so far (for logs and profiles)."""
     return dict(_PLANS)
+
+
+class _nullctx:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
 
 
 class _ConvFn(torch.autograd.Function):
@@ -322,12 +369,23 @@ class _ConvFn(torch.autograd.Function):
             if join is not None and join.park_or_take(dx):
                 dx = None
         if ctx.needs_input_grad[1]:
-            if plan.wgrad == MIOPEN:
-                dw = _miopen_bwd(dy, x, w, stride, pad, [False, True, False])[1]
-            else:
-                v, sp = plan.wgrad
-                dw = conv2d_wgrad(x, dy, (w.shape[2], w.shape[3]), stride, pad, v, sp,
-                                  out_dtype=w.dtype)
+            side = None
+            if _ASYNC_WGRAD and dy.is_cuda:
+                main = torch.cuda.current_stream()
+                side = _side_stream(dy.device)
+                side.wait_stream(main)   # dy, x (and w) are complete on the main stream
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                if plan.wgrad == MIOPEN:
+                    dw = _miopen_bwd(dy, x, w, stride, pad, [False, True, False])[1]
+                else:
+                    v, sp = plan.wgrad
+                    dw = conv2d_wgrad(x, dy, (w.shape[2], w.shape[3]), stride, pad, v, sp,
+                                      out_dtype=w.dtype)
+            if side is not None:
+                # allocator bookkeeping across the two streams
+                x.record_stream(side)
+                dy.record_stream(side)
+                dw.record_stream(main)
         return dx, dw, None, None, None, None, None
 
 

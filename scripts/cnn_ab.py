@@ -5,7 +5,8 @@ Builds one model + optimizer + synthetic batch per variant (same seed), warms ea
 (conv autotuning happens there), captures each whole step as a hipGraph, then alternates
 ``--chunk`` timed replays of each variant for ``--rounds`` rounds, so clock/thermal drift hits
 every variant alike (cdna_hip_programming.md §5.4 rule 24). Variants are conv modes
-(ARENA_CONV values). Prints one JSON line per variant: median / min ms per step, images/s.
+(ARENA_CONV values), optionally suffixed ``:async`` (weight gradients on a side stream).
+Prints one JSON line per variant: median / min ms per step, images/s.
 
     python scripts/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
 """
@@ -41,8 +42,10 @@ def main():
     hvd.init("gloo")
     args = cnn_bench.parse(["--model", a.model, "--batch_size", str(a.batch)])
     variants = {}
-    for i, mode in enumerate(a.modes.split(",")):
+    for i, name in enumerate(a.modes.split(",")):
+        mode, _, opt_s = name.partition(":")
         conv.set_mode(mode)
+        conv.set_async_wgrad(opt_s == "async")
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
             cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
@@ -52,9 +55,9 @@ def main():
         torch.cuda.synchronize()
         # the graph holds raw pointers into this model's parameters, optimizer state and batch:
         # keep them alive (rebinding the names would free them into the next variant's use)
-        variants[f"{mode}" if mode not in variants else f"{mode}#{i}"] = (g, loss,
+        variants[f"{name}" if name not in variants else f"{name}#{i}"] = (g, loss,
                                                                           (model, opt, x, y))
-        print(f"[ab] {mode}: captured, loss {float(loss):.4f}", file=sys.stderr, flush=True)
+        print(f"[ab] {name}: captured, loss {float(loss):.4f}", file=sys.stderr, flush=True)
     conv.set_mode(None)
     times = {m: [] for m in variants}
     for r in range(a.rounds):

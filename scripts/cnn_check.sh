@@ -35,4 +35,5 @@ if has prof; then
   python3 scripts/steady_kernels.py "$TRACE" --last-ms 400 --top 45 --csv "$OUT/steady_top.csv" \
       > "$OUT/steady.txt" 2>&1 || true
   head -12 "$OUT/steady.txt"
+  rm -f "$TRACE"   # ~100 MB: keep the summaries only (gpurun copies back at most 64 MiB)
 fi

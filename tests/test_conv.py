@@ -200,6 +200,10 @@ def test_grad_join_matches_autograd_sum(mode, monkeypatch):
     autograd's own summation, for an identity block and a downsample block."""
     from arena_amd.models import resnet as R
     conv.set_mode(mode)
+    # MIOpen's default solvers for some of these shapes accumulate split results in a run-order
+    # dependent way (run-to-run spread up to ~10 % max-relative on the block-input gradient):
+    # ask for its deterministic solvers so the comparison is about the join
+    monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
 
     class NoJoin(conv.GradJoin):
         def register(self):
