@@ -21,7 +21,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import Conv2dNHWC, GradJoin
+from ..ops.conv import BNGradLink, Conv2dNHWC, GradJoin
 from ..ops.pool import MaxPool2dNHWC
 
 DEPTHS = {"resnet50": [3, 4, 6, 3], "resnet101": [3, 4, 23, 3],
@@ -49,20 +49,28 @@ class Bottleneck(nn.Module):
             self.down_conv = Conv2dNHWC(cin, cout, 1, stride=stride, bias=False)
             self.down_bn = BatchNormAct2d(cout, act="none")
 
-    def forward(self, x):
+    def forward(self, x, link: BNGradLink | None = None, link_out: BNGradLink | None = None):
+        """``link``: x is the output of the previous block's last BN, which filled this link;
+        ``link_out``: handed to this block's last BN for the next block."""
         # forward_stats: when a conv runs on the MFMA kernel, its epilogue also produces the
-        # BatchNorm statistics partials of its output, and the BN skips its statistics pass
+        # BatchNorm statistics partials of its output, and the BN skips its statistics pass.
         # join: x feeds conv1 and the shortcut; its two gradients are summed inside the second
-        # backward (conv1's backward-data epilogue) instead of by a separate add pass
-        join = GradJoin() if (torch.is_grad_enabled() and x.requires_grad) else None
+        # backward (conv1's backward-data epilogue) instead of by a separate add pass.
+        # links: each BN's output feeds a conv whose backward-data epilogue computes that BN's
+        # backward partial sums (the BN skips its reduction pass); for the block input, the conv
+        # that completes the join does it.
+        train = torch.is_grad_enabled() and x.requires_grad
+        join = GradJoin() if train else None
+        lk1, lk2 = (BNGradLink(), BNGradLink()) if train else (None, None)
         idt = x
         if self.down_conv is not None:
-            y, st = self.down_conv.forward_stats(x, join=join)
+            y, st = self.down_conv.forward_stats(x, join=join, bn_link=link)
             idt = self.down_bn(y, stats=st)
-        y, st = self.conv1.forward_stats(x, join=join)
-        y, st = self.conv2.forward_stats(self.bn1(y, stats=st))
-        y, st = self.conv3.forward_stats(self.bn2(y, stats=st))
-        return self.bn3(y, residual=idt, stats=st, join=join if self.down_conv is None else None)
+        y, st = self.conv1.forward_stats(x, join=join, bn_link=link)
+        y, st = self.conv2.forward_stats(self.bn1(y, stats=st, link=lk1), bn_link=lk1)
+        y, st = self.conv3.forward_stats(self.bn2(y, stats=st, link=lk2), bn_link=lk2)
+        return self.bn3(y, residual=idt, stats=st, join=join if self.down_conv is None else None,
+                        link=link_out)
 
 
 class ResNet(nn.Module):
@@ -85,7 +93,12 @@ class ResNet(nn.Module):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
 
     def forward(self, x):
-        x = self.layers(self.stem(x))
+        x = self.stem(x)
+        link = None
+        for blk in self.layers:
+            out_link = BNGradLink() if torch.is_grad_enabled() else None
+            x = blk(x, link=link, link_out=out_link)
+            link = out_link
         return self.fc(torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1))
 
 

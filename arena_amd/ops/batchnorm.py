@@ -54,7 +54,7 @@ def reference(x, residual, weight, bias, running_mean, running_var, training, mo
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum,
-                eps, relu, num_batches=None, stats=None, join=None):
+                eps, relu, num_batches=None, stats=None, join=None, link=None):
         ext = _ext.load()
         part, rpb = stats if (stats is not None and training) else (None, 0)
         y, mean, invstd, mask = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
@@ -65,6 +65,11 @@ class _BNActFn(torch.autograd.Function):
         ctx.affine = weight is not None
         # the residual is also another op's input: gradients meet in a GradJoin (ops/conv.py)
         ctx.join = join.register() if (join is not None and residual is not None) else None
+        # the conv consuming y computes this layer's backward partials (ops/conv.py BNGradLink)
+        ctx.link = None
+        if link is not None and training and x.dtype == torch.bfloat16:
+            link.set_bn(x, mask if relu else None, mean)
+            ctx.link = link
         return y
 
     @staticmethod
@@ -74,8 +79,10 @@ class _BNActFn(torch.autograd.Function):
             raise RuntimeError("BatchNormAct2d backward in eval mode is not supported by the "
                                "fused kernels; use train() or the PyTorch path")
         dy = dy.contiguous(memory_format=torch.channels_last)
+        ext = ctx.link.take(dy) if ctx.link is not None else None
         dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, mask, x, mean, invstd, weight, ctx.relu,
-                                                     ctx.has_res, ctx.affine)
+                                                     ctx.has_res, ctx.affine,
+                                                     ext[0] if ext else None, ext[1] if ext else 0)
         if not ctx.has_res:
             dres = None
         elif ctx.join is not None and ctx.join.active() and ctx.needs_input_grad[1]:
@@ -86,7 +93,7 @@ class _BNActFn(torch.autograd.Function):
                 dres = None
         return (dx, dres, dgamma if ctx.affine else None,
                 dbeta if ctx.affine else None, None, None, None, None, None, None, None, None,
-                None)
+                None, None)
 
 
 def bn_act(x, residual=None, weight=None, bias=None, running_mean=None, running_var=None,
@@ -109,10 +116,11 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.relu = act == "relu"
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                stats=None, join=None) -> torch.Tensor:
+                stats=None, join=None, link=None) -> torch.Tensor:
         """``stats``: BatchNorm partials of ``x`` from the producing ``Conv2dNHWC.forward_stats``
         (skips the statistics pass over x; training mode on the fused kernels only).
-        ``join``: a ``GradJoin`` the residual's other consumer is registered on."""
+        ``join``: a ``GradJoin`` the residual's other consumer is registered on.
+        ``link``: a ``BNGradLink`` handed to the conv that consumes the output."""
         training = self.training or not self.track_running_stats
         tracking = self.training and self.track_running_stats
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
@@ -123,7 +131,8 @@ class BatchNormAct2d(nn.BatchNorm2d):
             # num_batches_tracked += 1 happens inside the statistics finalize kernel
             return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, True,
                                   self.momentum, self.eps, self.relu,
-                                  self.num_batches_tracked if tracking else None, stats, join)
+                                  self.num_batches_tracked if tracking else None, stats, join,
+                                  link)
         if tracking:
             self.num_batches_tracked.add_(1)
         mom = self.momentum if self.momentum is not None else \
@@ -133,4 +142,4 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return reference(x, residual, self.weight, self.bias, rm, rv, training, mom,
                              self.eps, self.relu)
         return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, training, mom,
-                              self.eps, self.relu, None, None, join)
+                              self.eps, self.relu, None, None, join, link)

@@ -13,6 +13,7 @@ which. The variant picks the block's output tile (0: 128x128, 1: 128x64, 2: 64x1
 """
 from __future__ import annotations
 
+import os
 from typing import Tuple
 
 import torch
@@ -55,13 +56,16 @@ def pick_variant(m: int, cout: int) -> int:
 
 
 def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int = -1,
-               with_stats: bool = False, addend: Tensor | None = None):
+               with_stats: bool = False, addend: Tensor | None = None, bn=None):
     """y = conv2d(x, w) (+ addend) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S].
 
     with_stats: returns (y, (part, rpb)) where part holds per-tile BatchNorm partials of y
     (tile mean and sum of squared deviations per channel, ``rpb`` output pixels per tile), which
     ``BatchNormAct2d(..., stats=...)`` finalizes instead of re-reading y.
-    addend: a bf16 tensor shaped like y, added to the fp32 sums before rounding (epilogue)."""
+    addend: a bf16 tensor shaped like y, added to the fp32 sums before rounding (epilogue).
+    bn: (bn_x, bn_mask or None, bn_mean) when y is the gradient of a BatchNorm layer's output:
+    returns (y, (part, rpb)) with that BN's backward partials (sum g, sum g (bn_x - mean) per
+    tile, g = y * mask) for its backward, which then skips its reduction pass."""
     x = x.contiguous(memory_format=torch.channels_last)
     w = w.contiguous(memory_format=torch.channels_last)
     if variant < 0:
@@ -69,8 +73,12 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
         variant = pick_variant(x.shape[0] * ho * wo, w.shape[0])
     if addend is not None:
         addend = addend.contiguous(memory_format=torch.channels_last)
+    bx = bm = bmu = None
+    if bn is not None:
+        bx, bm, bmu = bn
+        with_stats = True
     out = _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant), bool(with_stats),
-                               addend)
+                               addend, bx, bm, bmu)
     if with_stats:
         return out[0], (out[1], TILES[variant][0])
     return out[0]
@@ -85,10 +93,58 @@ def flip_weight(w: Tensor) -> Tensor:
 
 
 def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1,
-                    addend: Tensor | None = None) -> Tensor:
-    """dX (+ addend) of a stride-1 convolution (same spatial size when pad = (R-1)/2)."""
+                    addend: Tensor | None = None, bn=None):
+    """dX (+ addend) of a stride-1 convolution (same spatial size when pad = (R-1)/2).
+    With ``bn`` (see conv2d_fwd) returns (dX, (part, rpb)): the backward partials of the
+    BatchNorm layer whose output is this convolution's input."""
     r = w.shape[2]
-    return conv2d_fwd(dy, flip_weight(w), 1, r - 1 - pad, variant, addend=addend)
+    return conv2d_fwd(dy, flip_weight(w), 1, r - 1 - pad, variant, addend=addend, bn=bn)
+
+
+# Off by default: on ResNet-50 bs128 the heavier dgrad epilogue cost more than the reduction pass
+# it saves (15.69 / 15.74 vs 15.37 / 15.53 ms per step, same-process A/B, docs/perf.md).
+_BN_LINKS = os.environ.get("ARENA_BN_LINKS", "0") == "1"
+
+
+def set_bn_links(on: bool) -> None:
+    """Enable/disable BNGradLink fusion (off by default; ARENA_BN_LINKS=1)."""
+    global _BN_LINKS
+    _BN_LINKS = bool(on)
+
+
+class BNGradLink:
+    """A BatchNorm layer whose output is the input of a convolution: the conv's backward-data
+    pass produces exactly the gradient the BN's backward starts from, so its epilogue also
+    computes the BN backward's per-channel partial sums (sum g, sum g * (x - mean), g = dY *
+    ReLU mask) and the BN skips its reduction pass over dY and x. The BN's forward fills
+    ``set_bn``; the conv's backward ``publish``es; the BN's backward ``take``s, which checks that
+    it received the very tensor the partials describe (else it runs its own reduction)."""
+    __slots__ = ("x", "mask", "mean", "part", "rpb", "dy_ptr")
+
+    def __init__(self):
+        self.x = self.mask = self.mean = self.part = None
+        self.rpb = 0
+        self.dy_ptr = 0
+
+    def set_bn(self, x: Tensor, mask: Tensor | None, mean: Tensor) -> None:
+        if _BN_LINKS:
+            self.x, self.mask, self.mean = x, mask, mean
+
+    def ready(self) -> bool:
+        return self.x is not None
+
+    def publish(self, part: Tensor, rpb: int, dy: Tensor) -> None:
+        self.part, self.rpb, self.dy_ptr = part, int(rpb), dy.data_ptr()
+
+    def take(self, dy: Tensor):
+        """(part, rpb) if the partials describe ``dy``, else None. Releases the references."""
+        out = None
+        if self.part is not None and dy.data_ptr() == self.dy_ptr and self.x is not None \
+                and dy.shape == self.x.shape:
+            out = (self.part, self.rpb)
+        self.x = self.mask = self.mean = self.part = None
+        self.dy_ptr = 0
+        return out
 
 
 class GradJoin:
@@ -155,7 +211,6 @@ def conv2d_wgrad(x: Tensor, dy: Tensor, kernel: Tuple[int, int], stride: int = 1
 # cudnn.benchmark, which this complements). ARENA_CONV=miopen forces the library everywhere,
 # ARENA_CONV=ours forces the kernel wherever it applies (heuristic tiles, no timing).
 # ------------------------------------------------------------------------------------------------
-import os  # noqa: E402
 from dataclasses import dataclass, field  # noqa: E402
 from typing import Dict, Optional  # noqa: E402
 
@@ -332,7 +387,7 @@ class _nullctx:
 
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, plan, want_stats, join=None):
+    def forward(ctx, x, w, stride, pad, plan, want_stats, join=None, bn_link=None):
         part = x.new_empty(0, dtype=torch.float32)
         if plan.fwd == MIOPEN:
             y = F.conv2d(x, w, stride=stride, padding=pad)
@@ -343,6 +398,7 @@ class _ConvFn(torch.autograd.Function):
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pad, plan)
         ctx.join = join.register() if join is not None else None
+        ctx.bn_link = bn_link if (bn_link is not None and bn_link.ready()) else None
         ctx.mark_non_differentiable(part)
         # no zero-filled gradient for the statistics output (one fill kernel per conv per step)
         ctx.set_materialize_grads(False)
@@ -351,7 +407,7 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dpart):
         if dy is None:
-            return None, None, None, None, None, None, None
+            return None, None, None, None, None, None, None, None
         x, w = ctx.saved_tensors
         stride, pad, plan = ctx.conf
         dy = dy.contiguous(memory_format=torch.channels_last)
@@ -360,10 +416,18 @@ class _ConvFn(torch.autograd.Function):
             join = ctx.join if (ctx.join is not None and ctx.join.active()) else None
             # the second consumer of a joined input folds the first one's gradient in
             other = join.other() if join is not None else None
+            lk = ctx.bn_link
+            # the BN partials need the COMPLETE gradient of x: not from a join's first arriver
+            use_bn = (lk is not None and plan.bwd != MIOPEN and lk.x.shape == x.shape
+                      and (join is None or other is not None))
             if plan.bwd == MIOPEN:
                 dx = _miopen_bwd(dy, x, w, stride, pad, [True, False, False])[0]
                 if other is not None:
                     dx.add_(other)
+            elif use_bn:
+                dx, (part, rpb) = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other,
+                                                  bn=(lk.x, lk.mask, lk.mean))
+                lk.publish(part, rpb, dx)
             else:
                 dx = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other)
             if join is not None and join.park_or_take(dx):
@@ -386,7 +450,7 @@ class _ConvFn(torch.autograd.Function):
                 x.record_stream(side)
                 dy.record_stream(side)
                 dw.record_stream(main)
-        return dx, dw, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 class Conv2dNHWC(nn.Conv2d):
@@ -405,10 +469,12 @@ class Conv2dNHWC(nn.Conv2d):
     def forward(self, x: Tensor) -> Tensor:
         return self.forward_stats(x, want_stats=False)[0]
 
-    def forward_stats(self, x: Tensor, want_stats: bool = True, join: GradJoin | None = None):
+    def forward_stats(self, x: Tensor, want_stats: bool = True, join: GradJoin | None = None,
+                      bn_link: BNGradLink | None = None):
         """(y, stats): ``stats`` are the BatchNorm partials of y for ``BatchNormAct2d(y,
         stats=stats)`` when the kernel produced y (else None: the BN computes them itself).
-        ``join``: x has a second consumer registered on the same GradJoin (see there)."""
+        ``join``: x has a second consumer registered on the same GradJoin (see there).
+        ``bn_link``: x is the output of the BatchNorm layer that filled this link."""
         if not x.is_cuda or _mode() == "off":
             return super().forward(x), None
         amp = torch.is_autocast_enabled("cuda") and \
@@ -425,5 +491,5 @@ class Conv2dNHWC(nn.Conv2d):
         plan = plan_for(x, w, s, p)
         want = want_stats and plan.fwd != MIOPEN and torch.is_grad_enabled() and self.training
         with torch.autocast("cuda", enabled=False):
-            y, part = _ConvFn.apply(x, w, s, p, plan, want, join)
+            y, part = _ConvFn.apply(x, w, s, p, plan, want, join, bn_link)
         return y, ((part, TILES[plan.fwd][0]) if want else None)

@@ -48,8 +48,9 @@ void arena_ccl_set_block_elems(long long);
 void arena_ccl_set_oneshot_max(long long);
 long long arena_ccl_get_oneshot_max();
 // csrc/ops/conv_kernels.hip
-hipError_t arena_conv_fwd(const void*, const void*, void*, float*, const void*, int, int, int, int,
-                          int, int, int, int, int, int, hipStream_t);
+hipError_t arena_conv_fwd(const void*, const void*, void*, float*, const void*, const void*,
+                          const uint8_t*, const float*, int, int, int, int, int, int, int, int,
+                          int, int, hipStream_t);
 hipError_t arena_conv_flip_weight(const void*, void*, int, int, int, int, hipStream_t);
 int arena_conv_wgrad_splits(int, int, int, int, int, int, int);
 hipError_t arena_conv_wgrad(const void*, const void*, float*, void*, float*, int, int, int, int,
@@ -66,7 +67,7 @@ hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, 
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, uint8_t*, long long, int, int, int,
                         float*, int, long long, double*, unsigned*, ArenaBNStats, hipStream_t);
 hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, void*, long long, int,
-                        int, float*, double*, unsigned*, ArenaBNBwd, hipStream_t);
+                        int, float*, int, double*, unsigned*, ArenaBNBwd, hipStream_t);
 #ifdef ARENA_TIMELINE
 hipError_t arena_timeline_read(long long*, int);
 #endif
@@ -770,8 +771,10 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
 }
 
 // Returns (dx, dres or empty, dgamma or empty, dbeta or empty). mask: bn_fwd's ReLU bits (relu).
+// ext_part/ext_rpb: the (dy, x) partials from conv_fwd(..., bn_x=x, ...) that produced dy.
 std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor invstd, OptT gamma,
-                           bool relu, bool with_res, bool affine_grads) {
+                           bool relu, bool with_res, bool affine_grads, OptT ext_part,
+                           int64_t ext_rpb) {
   const BNGeom g = bn_geom(x, "x");
   bn_same(x, dy, "grad_output");
   if (relu) {
@@ -799,14 +802,26 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
   b.ca = co.data_ptr<float>();
   b.cb = b.ca + g.C;
   b.cc = b.cb + g.C;
-  Tensor part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
+  Tensor part;
+  int ext_nblk = 0;
+  if (ext_part.has_value()) {
+    check_f32(*ext_part, "ext_part");
+    TORCH_CHECK(ext_rpb > 0, "bn_bwd: ext_rpb must be positive");
+    const int64_t nblk = (g.M + ext_rpb - 1) / ext_rpb;
+    TORCH_CHECK(ext_part->numel() == nblk * 2 * g.C, "bn_bwd: ext_part has ", ext_part->numel(),
+                " floats, expected ", nblk * 2 * g.C);
+    part = *ext_part;
+    ext_nblk = (int)nblk;
+  } else {
+    part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
+  }
   Tensor lvl2 = bn_lvl2(part.numel() / (2 * g.C), g.C, x);
   Tensor dx = torch::empty_like(x);
   Tensor dres = with_res ? torch::empty_like(x) : Tensor();
   check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(),
                          relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(), dx.data_ptr(),
                          with_res ? dres.data_ptr() : nullptr, g.M, g.C, relu ? 1 : 0,
-                         part.data_ptr<float>(), lvl2.data_ptr<double>(), bn_tickets(x), b,
+                         part.data_ptr<float>(), ext_nblk, lvl2.data_ptr<double>(), bn_tickets(x), b,
                          cur_stream()),
             "bn_bwd");
   return {dx, dres, dgamma, dbeta};
@@ -829,8 +844,12 @@ void pool_check(const Tensor& t, const char* name) {
 // partial) for bn_fwd(..., stats_part, BM): the BN layer after the conv skips its stats pass.
 // addend (optional): bf16 tensor shaped like y (channels_last) added to the fp32 sums before the
 // bf16 rounding: the second gradient of a tensor with two consumers (arena_amd.ops.conv.GradJoin).
+// bn_x/bn_mask/bn_mean (optional, backward-data use): y is the gradient of a BatchNorm layer's
+// output; with with_stats the returned partials are that BN's backward partials (g = y * mask,
+// sum g, sum g * (bn_x - bn_mean)) for bn_bwd(..., ext_part, BM) instead of forward statistics.
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant,
-                             bool with_stats, OptT addend) {
+                             bool with_stats, OptT addend, OptT bn_x, OptT bn_mask,
+                             OptT bn_mean) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4,
               "conv_fwd: x and w must be 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16,
@@ -861,9 +880,28 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                     addend->is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_fwd: addend must be a channels_last bf16 tensor shaped like the output");
   }
+  if (bn_x.has_value()) {
+    TORCH_CHECK(with_stats && bn_mean.has_value(), "conv_fwd: bn_x needs with_stats and bn_mean");
+    TORCH_CHECK(bn_x->sizes() == y.sizes() && bn_x->scalar_type() == torch::kBFloat16 &&
+                    bn_x->device() == y.device() &&
+                    bn_x->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_fwd: bn_x must be a channels_last bf16 tensor shaped like the output");
+    check_f32(*bn_mean, "bn_mean");
+    TORCH_CHECK(bn_mean->numel() == Cout, "conv_fwd: bn_mean must have Cout elements");
+    if (bn_mask.has_value()) {
+      TORCH_CHECK(bn_mask->scalar_type() == torch::kUInt8 && bn_mask->is_contiguous() &&
+                      bn_mask->device() == y.device() && bn_mask->numel() == y.numel() / 8,
+                  "conv_fwd: bn_mask must be uint8 with numel(y) / 8 bytes");
+    }
+  }
   check_hip(arena_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(),
                            with_stats ? part.data_ptr<float>() : nullptr,
-                           addend.has_value() ? addend->data_ptr() : nullptr, (int)N, (int)H, (int)W,
+                           addend.has_value() ? addend->data_ptr() : nullptr,
+                           bn_x.has_value() ? bn_x->data_ptr() : nullptr,
+                           bn_x.has_value() && bn_mask.has_value() ? bn_mask->data_ptr<uint8_t>()
+                                                                   : nullptr,
+                           bn_x.has_value() ? bn_mean->data_ptr<float>() : nullptr,
+                           (int)N, (int)H, (int)W,
                            (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad, (int)variant,
                            cur_stream()),
             "conv_fwd");
@@ -1038,9 +1076,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_fwd", &linear_fwd);
   m.def("bn_fwd", &bn_fwd);
   m.def("conv_flip_weight", &conv_flip_weight);
-  m.def("bn_bwd", &bn_bwd);
+  m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("mean"),
+        py::arg("invstd"), py::arg("gamma"), py::arg("relu"), py::arg("with_res"),
+        py::arg("affine_grads"), py::arg("ext_part") = py::none(), py::arg("ext_rpb") = 0);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
-        py::arg("variant"), py::arg("with_stats"), py::arg("addend") = py::none());
+        py::arg("variant"), py::arg("with_stats"), py::arg("addend") = py::none(),
+        py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
+        py::arg("bn_mean") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

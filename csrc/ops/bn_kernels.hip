@@ -620,22 +620,29 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
   return hipGetLastError();
 }
 
+// ext_nblk > 0: `part` already holds the backward partials of (dy, x) ([ext_nblk][2][C]), written
+// by the epilogue of the backward-data convolution that produced dy (conv_kernels.hip, EPI 2):
+// no reduction pass.
 hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const void* x, void* dx,
-                        void* dres, long long M, int C, int relu, float* part, double* lvl2,
-                        unsigned* tickets, ArenaBNBwd co, hipStream_t stream) {
+                        void* dres, long long M, int C, int relu, float* part, int ext_nblk,
+                        double* lvl2, unsigned* tickets, ArenaBNBwd co, hipStream_t stream) {
   if (bad_shape(M, C) || (relu && mask == nullptr)) return hipErrorInvalidValue;
   long long rpb;
-  const long long nb = reduce_blocks(M, C, &rpb);
+  long long nb = reduce_blocks(M, C, &rpb);
+  if (ext_nblk > 0) {
+    nb = ext_nblk;
+  } else {
 #define ARENA_BN_RED(TT, R)                                                                  \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, R>), dim3(nb), dim3(kT), 0, stream,         \
                      static_cast<const TT*>(dy), mask, static_cast<const TT*>(x), M, C, rpb, \
                      part, co)
-  if (dtype == 1) {
-    if (relu) ARENA_BN_RED(uint16_t, true); else ARENA_BN_RED(uint16_t, false);
-  } else {
-    if (relu) ARENA_BN_RED(float, true); else ARENA_BN_RED(float, false);
-  }
+    if (dtype == 1) {
+      if (relu) ARENA_BN_RED(uint16_t, true); else ARENA_BN_RED(uint16_t, false);
+    } else {
+      if (relu) ARENA_BN_RED(float, true); else ARENA_BN_RED(float, false);
+    }
 #undef ARENA_BN_RED
+  }
   hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64, fin_blocks_per_group((int)nb)),
                      dim3(kT), 0, stream, part, (int)nb, M, C, lvl2, tickets, co);
   const long long nvec = M * (C / kVec);

@@ -53,6 +53,12 @@ struct ConvArgs {
   float* part;         // optional BatchNorm partials [m_tiles][2][Cout] (tile mean, tile M2)
   const uint16_t* add; // optional [M][Cout] bf16 added to the fp32 sums before rounding (the
                        // other gradient of a tensor with two consumers: the residual join)
+  // BatchNorm-backward partials of the output (EPI 2, a backward-data pass whose output dY is the
+  // gradient of a BN layer's output): g = dY (* ReLU mask bit); part[tile][0][c] = sum g,
+  // part[tile][1][c] = sum g * (bnx - bnmean[c]) -- the bn_bwd_reduce partial format.
+  const uint16_t* bnx;     // [M][Cout] the BN layer's input
+  const uint8_t* bnmask;   // [M][Cout / 8] ReLU bits of the BN output, or null (no ReLU)
+  const float* bnmean;     // [Cout] the BN layer's batch mean
   int N, H, W, C, Cout, R, S, stride, pad, Ho, Wo;
   int M;               // N * Ho * Wo
   int Ktot;            // R * S * C
@@ -88,14 +94,19 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
-template <int BM, int BN, bool STATS>
+// NBUF = LDS stage buffers: 2 (double-buffered K loop) or 1 for a single 64-deep K step (1x1
+// convolutions over 64 channels): half the LDS, so twice the blocks per CU overlap their loads
+// with other blocks' epilogues -- those shapes are bound by the output write.
+// EPI: 0 = plain, 1 = BatchNorm statistics of Y (forward), 2 = BatchNorm-backward partials of Y
+// (see ConvArgs::bnx).
+template <int BM, int BN, int EPI, int NBUF = 2>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
   constexpr int WM = BM / 2, WN = BN / 2;        // per-wave output tile (2 x 2 waves)
   constexpr int MI = WM / 16, NI = WN / 16;      // 16x16 MFMA tiles per wave
   constexpr int AI = BM * 8 / kThreads;          // A staging instructions per thread
   constexpr int BI = BN * 8 / kThreads;
   constexpr int kBufBytes = (BM + BN) * kRowBytes;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kBufBytes];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBufBytes];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
@@ -171,8 +182,8 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
   __syncthreads();
 
   for (int t = 0; t < T; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < T) stage(t + 1, cur ^ 1);
+    const int cur = NBUF == 1 ? 0 : (t & 1);
+    if (NBUF == 2 && t + 1 < T) stage(t + 1, cur ^ 1);
     const uint8_t* abuf = lds + cur * kBufBytes;
     const uint8_t* bbuf = abuf + BM * kRowBytes;
 #pragma unroll
@@ -200,6 +211,26 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
   }
 
   // ---- epilogue: lane holds channels n0+wn*WN+j*16+4*fq .. +3 of pixel m0+wm*WM+i*16+fr ----
+  // EPI 2 operands, issued before the stores so their latency overlaps them (clamped addresses)
+  uint2 bx[EPI == 2 ? MI : 1][EPI == 2 ? NI : 1];
+  uint32_t bm[EPI == 2 ? MI : 1][EPI == 2 ? NI : 1];
+  float4 bmu[EPI == 2 ? NI : 1];
+  if constexpr (EPI == 2) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = min(m0 + wm * WM + i * 16 + fr, a.M - 1);
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int c0 = n0 + wn * WN + j * 16 + 4 * fq;
+        bx[i][j] = *reinterpret_cast<const uint2*>(a.bnx + (size_t)m * a.Cout + c0);
+        bm[i][j] = a.bnmask ? ((uint32_t)a.bnmask[(size_t)m * (a.Cout >> 3) + (c0 >> 3)] >>
+                               (c0 & 7)) : 0xfu;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+      bmu[j] = *reinterpret_cast<const float4*>(a.bnmean + n0 + wn * WN + j * 16 + 4 * fq);
+  }
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * WM + i * 16 + fr;
@@ -226,7 +257,53 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
       *reinterpret_cast<uint2*>(yrow + j * 16) = v;
     }
   }
-  if constexpr (STATS) {
+  if constexpr (EPI == 2) {
+    // per channel over the tile's valid rows: sum g, sum g * (x - mean), g = stored dY * mask
+    float* red = reinterpret_cast<float*>(lds);   // [2 (wm)][2][BN]
+    float s1[NI][4], s2[NI][4];
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const float mu[4] = {bmu[j].x, bmu[j].y, bmu[j].z, bmu[j].w};
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const bool valid = m0 + wm * WM + i * 16 + fr < a.M && ((bm[i][j] >> r) & 1u);
+          const uint32_t w2 = r < 2 ? bx[i][j].x : bx[i][j].y;
+          const float xv = __uint_as_float((r & 1) ? (w2 & 0xffff0000u) : (w2 << 16));
+          const float g = valid ? bf16_round(acc[i][j][r]) : 0.f;
+          t1 += g;
+          t2 = fmaf(g, xv - mu[r], t2);
+        }
+        s1[j][r] = row16_sum(t1);
+        s2[j][r] = row16_sum(t2);
+      }
+    }
+    __syncthreads();   // every wave is past its last read of the staging buffers
+    if (fr == 0) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wn * WN + j * 16 + 4 * fq + r;
+          red[wm * 2 * BN + c] = s1[j][r];
+          red[wm * 2 * BN + BN + c] = s2[j][r];
+        }
+    }
+    __syncthreads();
+    if (wm == 0 && fr == 0) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wn * WN + j * 16 + 4 * fq + r;
+          a.part[(size_t)mt * 2 * a.Cout + n0 + c] = red[c] + red[2 * BN + c];
+          a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = red[BN + c] + red[3 * BN + c];
+        }
+    }
+  }
+  if constexpr (EPI == 1) {
     // BatchNorm statistics of this tile's bf16 outputs, two-pass (mean, then sum of squared
     // deviations) over the valid rows: the partial format of bn_stats_kernel with rpb = BM, so
     // the BN layer that consumes this output skips its own statistics pass over HBM.
@@ -281,10 +358,14 @@ hipError_t launch(const ConvArgs& a0, hipStream_t st) {
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
-  if (a.part)
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, true>), dim3(nwg), dim3(kThreads), 0, st, a);
-  else
-    hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, false>), dim3(nwg), dim3(kThreads), 0, st, a);
+  const bool one = a.Ktot == kBK;  // a single K step: no second stage buffer
+  const int epi = a.part == nullptr ? 0 : (a.bnx != nullptr ? 2 : 1);
+#define ARENA_CONV_LAUNCH(E, NB) \
+  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, E, NB>), dim3(nwg), dim3(kThreads), 0, st, a)
+  if (epi == 0) { if (one) ARENA_CONV_LAUNCH(0, 1); else ARENA_CONV_LAUNCH(0, 2); }
+  else if (epi == 1) { if (one) ARENA_CONV_LAUNCH(1, 1); else ARENA_CONV_LAUNCH(1, 2); }
+  else { if (one) ARENA_CONV_LAUNCH(2, 1); else ARENA_CONV_LAUNCH(2, 2); }
+#undef ARENA_CONV_LAUNCH
   return hipGetLastError();
 }
 
@@ -295,8 +376,11 @@ extern "C" {
 // Returns hipErrorInvalidValue for shapes the kernel does not cover (the caller falls back to
 // MIOpen): C % 64 != 0, Cout % 64 != 0, or an unknown tile variant.
 // variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (BM x BN output tile per block).
-// part (optional): BatchNorm partials of y, [ceil(M / BM)][2][Cout] (see the STATS epilogue).
+// part (optional): BatchNorm partials of y, [ceil(M / BM)][2][Cout] (EPI 1 / EPI 2 epilogues).
+// bnx/bnmask/bnmean (optional, with part): the backward-data form, part = BatchNorm-backward
+// partials of y instead of forward statistics (see ConvArgs).
 hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, const void* add,
+                          const void* bnx, const uint8_t* bnmask, const float* bnmean,
                           int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad,
                           int variant, hipStream_t st) {
   if (C % kBK || Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
@@ -307,6 +391,10 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
   a.y = (uint16_t*)y;
   a.part = part;
   a.add = (const uint16_t*)add;
+  a.bnx = (const uint16_t*)bnx;
+  a.bnmask = bnmask;
+  a.bnmean = bnmean;
+  if (bnx != nullptr && (part == nullptr || bnmean == nullptr)) return hipErrorInvalidValue;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
   a.stride = stride; a.pad = pad;
   a.Ho = (H + 2 * pad - R) / stride + 1;

@@ -5,7 +5,8 @@ Builds one model + optimizer + synthetic batch per variant (same seed), warms ea
 (conv autotuning happens there), captures each whole step as a hipGraph, then alternates
 ``--chunk`` timed replays of each variant for ``--rounds`` rounds, so clock/thermal drift hits
 every variant alike (cdna_hip_programming.md §5.4 rule 24). Variants are conv modes
-(ARENA_CONV values), optionally suffixed ``:async`` (weight gradients on a side stream).
+(ARENA_CONV values), optionally suffixed ``:async`` (weight gradients on a side stream) and/or
+``:link`` (BN-backward partials in the dgrad epilogues), joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
     python scripts/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
@@ -45,7 +46,8 @@ def main():
     for i, name in enumerate(a.modes.split(",")):
         mode, _, opt_s = name.partition(":")
         conv.set_mode(mode)
-        conv.set_async_wgrad(opt_s == "async")
+        conv.set_async_wgrad("async" in opt_s.split("+"))
+        conv.set_bn_links("link" in opt_s.split("+"))
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
             cnn_bench.train_step(model, opt, x, y, torch.bfloat16)

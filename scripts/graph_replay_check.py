@@ -26,6 +26,8 @@ def main():
                     help="cnn_ab's exact sequence: both captured first, then interleaved chunks "
                          "of back-to-back replays")
     ap.add_argument("--sync_each", action="store_true", help="(--ab) sync after every replay")
+    ap.add_argument("--reset_mode", action="store_true",
+                    help="(--ab) conv.set_mode(None) after the captures, as cnn_ab does")
     a = ap.parse_args()
     from arena_amd.ops import conv
     from arena_amd.examples import cnn_bench
@@ -66,6 +68,8 @@ def main():
             v["g"].replay()
             torch.cuda.synchronize()
             vs.append(v)
+        if a.reset_mode:
+            conv.set_mode(None)
         for r in range(4):
             line = []
             for i, v in enumerate(vs):

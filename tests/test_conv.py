@@ -241,3 +241,92 @@ def test_grad_join_matches_autograd_sum(mode, monkeypatch):
                 assert _rel(out["join"][1][n], gp) < ptol, n
     finally:
         conv.set_mode(None)
+
+
+@pytest.mark.gpu
+def test_dgrad_epilogue_bn_backward_partials():
+    """conv2d_bwd_data(..., bn=(x, mask, mean)): per-tile sum g and sum g (x - mean) of the
+    stored dX (g = dX * mask bit), the bn_bwd_reduce partial format, tail tile included."""
+    n, cin, h, w, cout, k = 3, 128, 9, 11, 64, 3
+    x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=5)
+    dy = torch.randn(n, cout, h, w, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    bnx = torch.randn(n, cin, h, w, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    m = n * h * w
+    mask = torch.randint(0, 256, (m * cin // 8,), device="cuda", dtype=torch.uint8)
+    mean = torch.randn(cin, device="cuda") * 0.3
+    bits = ((mask.view(m, cin // 8, 1).int() >> torch.arange(8, device="cuda").view(1, 1, 8)) & 1)
+    bits = bits.view(m, cin).float()
+    for v in conv.variants_for(cin):
+        dx0 = conv.conv2d_bwd_data(dy, wt, 1, v)
+        dx, (part, rpb) = conv.conv2d_bwd_data(dy, wt, 1, v, bn=(bnx, mask, mean))
+        assert torch.equal(dx, dx0)
+        g = dx.permute(0, 2, 3, 1).reshape(m, cin).float() * bits
+        xc = bnx.permute(0, 2, 3, 1).reshape(m, cin).float() - mean
+        nt = -(-m // rpb)
+        assert part.numel() == nt * 2 * cin
+        p = part.view(nt, 2, cin)
+        for t in range(nt):
+            sl = slice(t * rpb, min(m, (t + 1) * rpb))
+            torch.testing.assert_close(p[t, 0], g[sl].sum(0), rtol=1e-4, atol=1e-3)
+            torch.testing.assert_close(p[t, 1], (g[sl] * xc[sl]).sum(0), rtol=1e-4, atol=1e-3)
+        # no ReLU: every bit set
+        _, (part1, _) = conv.conv2d_bwd_data(dy, wt, 1, v, bn=(bnx, None, mean))
+        torch.testing.assert_close(part1.view(nt, 2, cin)[:, 0].sum(0),
+                                   dx.permute(0, 2, 3, 1).reshape(m, cin).float().sum(0),
+                                   rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.gpu
+def test_bn_grad_links_match_plain_backward(monkeypatch):
+    """Two ResNet blocks with the BN backward partials computed in the convs' backward-data
+    epilogues (BNGradLink) give the gradients of the plain BN reduction path."""
+    from arena_amd.models import resnet as R
+    conv.set_mode("ours")
+    conv.set_bn_links(True)
+
+    class NoLink(conv.BNGradLink):
+        def set_bn(self, x, mask, mean):
+            pass   # never ready: every BN runs its own reduction
+
+    class Counting(conv.BNGradLink):
+        hits = 0
+
+        def take(self, dy):
+            r = super().take(dy)
+            Counting.hits += r is not None
+            return r
+
+    try:
+        torch.manual_seed(0)
+        # channel counts the kernels take (multiples of 64)
+        net = torch.nn.ModuleList([R.Bottleneck(256, 64, 1), R.Bottleneck(256, 64, 1)]).cuda()
+        net = net.to(memory_format=torch.channels_last)
+        with torch.no_grad():
+            for b in net:
+                b.bn3.weight.uniform_(0.5, 1.5)
+        x0 = torch.randn(4, 256, 12, 12, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        g = torch.randn(4, 256, 12, 12, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        out = {}
+        for name, cls in (("link", Counting), ("plain", NoLink)):
+            monkeypatch.setattr(R, "BNGradLink", cls)
+            net.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                link = cls()
+                y = net[0](x, link_out=link)
+                y = net[1](y, link=link)
+            y.backward(g)
+            out[name] = (x.grad.float(), {n: p.grad.float().clone()
+                                          for n, p in net.named_parameters()})
+        # bn1, bn2 of both blocks and block 0's bn3 (joined through block 1's conv1)
+        assert Counting.hits == 5, Counting.hits
+        assert _rel(out["link"][0], out["plain"][0]) < 2e-2
+        for n, gp in out["plain"][1].items():
+            assert _rel(out["link"][1][n], gp) < 2e-2, n
+    finally:
+        conv.set_mode(None)
+        conv.set_bn_links(False)
