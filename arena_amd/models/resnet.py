@@ -21,7 +21,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import BNGradLink, Conv2dNHWC, GradJoin
+from ..ops.conv import BNGradLink, Conv2dNHWC, GradJoin, StemConv2d
 from ..ops.pool import MaxPool2dNHWC
 
 DEPTHS = {"resnet50": [3, 4, 6, 3], "resnet101": [3, 4, 23, 3],
@@ -76,7 +76,7 @@ class Bottleneck(nn.Module):
 class ResNet(nn.Module):
     def __init__(self, depths: List[int], num_classes: int = 1000, width: int = 64):
         super().__init__()
-        self.stem = nn.Sequential(Conv2dNHWC(3, width, 7, stride=2, padding=3, bias=False),
+        self.stem = nn.Sequential(StemConv2d(3, width, 7, stride=2, padding=3, bias=False),
                                   BatchNormAct2d(width, act="relu"),
                                   MaxPool2dNHWC(3, stride=2, padding=1))
         layers = []
@@ -93,7 +93,8 @@ class ResNet(nn.Module):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
 
     def forward(self, x):
-        x = self.stem(x)
+        y, st = self.stem[0].forward_stats(x)        # epilogue BN statistics, as in the blocks
+        x = self.stem[2](self.stem[1](y, stats=st))
         link = None
         for blk in self.layers:
             out_link = BNGradLink() if torch.is_grad_enabled() else None

@@ -112,6 +112,103 @@ def set_bn_links(on: bool) -> None:
     _BN_LINKS = bool(on)
 
 
+def conv2d_bwd_data_strided(dy: Tensor, w: Tensor, x_hw: Tuple[int, int], stride: int, pad: int,
+                            variant: int = -1, addend: Tensor | None = None) -> Tensor:
+    """dX of a stride-``stride`` convolution as ``stride**2`` phase convolutions on the kernel.
+
+    Input pixel (i*s + a, j*s + b) only receives the filter taps r with (a + pad - r) % s == 0;
+    over the phase grid (i, j) that is a stride-1 convolution of dY with the flipped sub-filter
+    W[:, :, r0::s, c0::s], written straight into the (a, b) parity class of dX (the kernel's
+    mapped output). Phases without taps (1x1, stride 2: three of four) keep ``addend`` (or 0)."""
+    N, Cout, Ho, Wo = dy.shape
+    Cin, R, S = w.shape[1], w.shape[2], w.shape[3]
+    H, W = x_hw
+    dy = dy.contiguous(memory_format=torch.channels_last)
+    ext = _ext.load()
+    full = all((a + pad) % stride < R for a in range(stride)) and \
+        all((b + pad) % stride < S for b in range(stride))
+    if addend is not None:
+        dx = addend.contiguous(memory_format=torch.channels_last).clone()
+    elif full:
+        dx = torch.empty(N, Cin, H, W, device=dy.device, dtype=dy.dtype,
+                         memory_format=torch.channels_last)
+    else:
+        dx = torch.zeros(N, Cin, H, W, device=dy.device, dtype=dy.dtype).contiguous(
+            memory_format=torch.channels_last)
+    for a in range(stride):
+        r0 = (a + pad) % stride
+        if r0 >= R:
+            continue
+        Rp = len(range(r0, R, stride))
+        ca = (a + pad - r0) // stride
+        Hp = (H - a + stride - 1) // stride
+        for b in range(stride):
+            c0 = (b + pad) % stride
+            if c0 >= S or Hp <= 0:
+                continue
+            Sp = len(range(c0, S, stride))
+            cb = (b + pad - c0) // stride
+            Wp = (W - b + stride - 1) // stride
+            if Wp <= 0:
+                continue
+            wp = w[:, :, r0::stride, c0::stride].flip(2, 3).transpose(0, 1).contiguous(
+                memory_format=torch.channels_last)
+            v = variant if variant >= 0 else pick_variant(N * Hp * Wp, Cin)
+            ext.conv_fwd_ex(dy, wp, 1, Rp - 1 - ca, Sp - 1 - cb, Hp, Wp, int(v), False,
+                            dx if addend is not None else None, dx, [stride, stride, a, b],
+                            False)
+    return dx
+
+
+# ------------------------------------------------------------------------------------------------
+# The 7x7/2 ResNet stem (3 input channels) as a space-to-depth 4x4/1 convolution over 16 channels
+# (12 used), which the MFMA kernel runs in its c16 mode: K = 4*4*16 = 256 (147 useful), against
+# 7*7*64 = 3136 if the 3 channels were padded to one 64-channel K step.
+#   z[n][i][j][(dy*2+dx)*3 + c] = x[n][2i+dy][2j+dx][c]
+#   W16[co][u][v][(dy*2+dx)*3 + c] = W[co][c][2u+dy-1][2v+dx-1]  (0 outside the 7x7 filter)
+#   y[ho][wo] = sum_{u,v} z[ho-2+u][wo-2+v] . W16[u][v]
+# ------------------------------------------------------------------------------------------------
+def stem_weight(w: Tensor) -> Tensor:
+    """W16 [Cout, 16, 4, 4] (channels_last) from a [Cout, C, 7, 7] stem weight, C <= 4 (torch
+    ops, differentiable: dW comes back through them)."""
+    co, c = w.shape[0], w.shape[1]
+    wp = F.pad(w, (1, 0, 1, 0))                                   # [co, c, 8, 8]
+    wp = wp.view(co, c, 4, 2, 4, 2).permute(0, 2, 4, 3, 5, 1)     # co, u, v, dy, dx, c
+    wp = wp.reshape(co, 4, 4, 4 * c)
+    wp = F.pad(wp, (0, 16 - 4 * c))                                # [co, 4, 4, 16]
+    return wp.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
+
+
+class _StemFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, w16, want_stats, fwd_variant, wgrad_cfg):
+        Ho, Wo = z.shape[2], z.shape[3]
+        out = _ext.load().conv_fwd_ex(z, w16, 1, 2, 2, Ho, Wo, int(fwd_variant), bool(want_stats),
+                                      None, None, [], True)
+        ctx.save_for_backward(z)
+        ctx.wgrad_cfg = wgrad_cfg
+        ctx.set_materialize_grads(False)
+        part = out[1] if want_stats else z.new_empty(0, dtype=torch.float32)
+        ctx.mark_non_differentiable(part)
+        return out[0], part
+
+    @staticmethod
+    def backward(ctx, dy, _dpart):
+        if dy is None or not ctx.needs_input_grad[1]:
+            return None, None, None, None, None
+        (z,) = ctx.saved_tensors
+        v, sp = ctx.wgrad_cfg
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dw = _ext.load().conv_wgrad_ex(z, dy, 4, 4, 1, 2, 2, int(v), int(sp), False, 1.0, True)
+        return None, dw, None, None, None
+
+
+def stem_ok(x: Tensor, w: Tensor, stride: int, pad: int) -> bool:
+    return (x.is_cuda and x.dim() == 4 and tuple(w.shape[2:]) == (7, 7) and stride == 2
+            and pad == 3 and x.shape[1] <= 4 and w.shape[0] % 64 == 0 and x.shape[2] % 2 == 0
+            and x.shape[3] % 2 == 0 and not x.requires_grad)
+
+
 class BNGradLink:
     """A BatchNorm layer whose output is the input of a convolution: the conv's backward-data
     pass produces exactly the gradient the BN's backward starts from, so its epilogue also
@@ -253,13 +350,20 @@ def _time(fn, reps: int = 4, iters: int = 3) -> float:
     graph replay never pays: MIOpen's convolution_backward costs ~50 us of host time per call.)"""
     fn()
     torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if os.environ.get("ARENA_CONV_TIME_EAGER") == "1":
+        s.record()
+        for _ in range(reps * iters):
+            fn()
+        e.record()
+        e.synchronize()
+        return s.elapsed_time(e) * 1e3 / (reps * iters)
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         for _ in range(reps):
             fn()
     g.replay()
     torch.cuda.synchronize()
-    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     s.record()
     for _ in range(iters):
         g.replay()
@@ -299,28 +403,29 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
     if mode == MIOPEN or not ok:
         plan.tuned = True
     elif mode == "ours" or torch.cuda.is_current_stream_capturing():
-        plan.fwd = pick_variant(x.shape[0] * ho * wo, cout)
-        plan.bwd = pick_variant(x.shape[0] * x.shape[2] * x.shape[3], cin) if stride == 1 else MIOPEN
-        plan.wgrad = wg[len(wg) // 2] if wg else MIOPEN
+        # ARENA_CONV_DIRS (debugging): the directions "ours" puts on the kernels
+        dirs = os.environ.get("ARENA_CONV_DIRS", "fwd,bwd,wgrad").split(",")
+        plan.fwd = pick_variant(x.shape[0] * ho * wo, cout) if "fwd" in dirs else MIOPEN
+        plan.bwd = ((pick_variant(x.shape[0] * x.shape[2] * x.shape[3], cin) if stride == 1
+                     else -1) if "bwd" in dirs else MIOPEN)
+        plan.wgrad = wg[len(wg) // 2] if (wg and "wgrad" in dirs) else MIOPEN
         plan.tuned = mode == "ours"
     else:
+        # Only the MFMA kernels are candidates: a captured step with MIOpen convolutions in it
+        # returned wrong gradients on replays that followed other GPU/host work, while the same
+        # step on these kernels alone stayed bit-identical run to run (scripts/graph_mem_*.py,
+        # docs/perf.md "MIOpen inside a captured step"). ARENA_CONV=miopen keeps the library
+        # path for comparisons.
         y = F.conv2d(x, w, stride=stride, padding=pad)
         dy = torch.randn_like(y)
         t = {}
-        # the kernel's forward also produces the BatchNorm statistics of y (every conv of the
-        # model family feeds a BN), which saves the BN's statistics pass over y: charge MIOpen
-        # for that pass (one HBM read of y at ~4.5 TB/s plus a launch)
-        stats_pass = y.numel() * y.element_size() / 4.5e6 + 3.0
-        t[("fwd", MIOPEN)] = _time(lambda: F.conv2d(x, w, stride=stride, padding=pad)) + \
-            stats_pass
         for v in variants_for(cout):
             t[("fwd", v)] = _time(lambda: conv2d_fwd(x, w, stride, pad, v, with_stats=True))
-        t[("bwd", MIOPEN)] = _time(lambda: _miopen_bwd(dy, x, w, stride, pad, [True, False, False]))
         if stride == 1:
             for v in variants_for(cin):
                 t[("bwd", v)] = _time(lambda: conv2d_bwd_data(dy, w, pad, v))
-        t[("wgrad", MIOPEN)] = _time(lambda: _miopen_bwd(dy, x, w, stride, pad,
-                                                         [False, True, False]))
+        else:   # phase decomposition, per-phase tile heuristic
+            t[("bwd", -1)] = 0.0
         for c in wg:
             t[("wgrad", c)] = _time(lambda: conv2d_wgrad(x, dy, k, stride, pad, c[0], c[1]))
         for kind in ("fwd", "bwd", "wgrad"):
@@ -418,12 +523,16 @@ class _ConvFn(torch.autograd.Function):
             other = join.other() if join is not None else None
             lk = ctx.bn_link
             # the BN partials need the COMPLETE gradient of x: not from a join's first arriver
-            use_bn = (lk is not None and plan.bwd != MIOPEN and lk.x.shape == x.shape
+            use_bn = (lk is not None and plan.bwd != MIOPEN and stride == 1
+                      and lk.x.shape == x.shape
                       and (join is None or other is not None))
             if plan.bwd == MIOPEN:
                 dx = _miopen_bwd(dy, x, w, stride, pad, [True, False, False])[0]
                 if other is not None:
                     dx.add_(other)
+            elif stride != 1:
+                dx = conv2d_bwd_data_strided(dy, w, (x.shape[2], x.shape[3]), stride, pad,
+                                             plan.bwd, addend=other)
             elif use_bn:
                 dx, (part, rpb) = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other,
                                                   bn=(lk.x, lk.mask, lk.mean))
@@ -493,3 +602,35 @@ class Conv2dNHWC(nn.Conv2d):
         with torch.autocast("cuda", enabled=False):
             y, part = _ConvFn.apply(x, w, s, p, plan, want, join, bn_link)
         return y, ((part, TILES[plan.fwd][0]) if want else None)
+
+
+class StemConv2d(Conv2dNHWC):
+    """The 7x7/2 stem convolution (3 input channels) on the MFMA kernel through its space-to-depth
+    form (see ``stem_weight``): one s2d kernel + one c16 convolution forward (with the BN
+    statistics epilogue), one c16 split-K wgrad backward. Same parameters and state_dict as
+    ``nn.Conv2d(C, Cout, 7, stride=2, padding=3, bias=False)``; anything else (CPU, fp32, an input
+    that needs a gradient, ARENA_CONV=miopen/off) runs ``Conv2dNHWC``."""
+
+    def forward_stats(self, x: Tensor, want_stats: bool = True, join: GradJoin | None = None,
+                      bn_link: BNGradLink | None = None):
+        s, p = self.stride[0], self.padding[0]
+        if not x.is_cuda or _mode() in ("off", MIOPEN) or join is not None:
+            return super().forward_stats(x, want_stats, join, bn_link)
+        amp = torch.is_autocast_enabled("cuda") and \
+            torch.get_autocast_dtype("cuda") == torch.bfloat16
+        w = self.weight
+        if amp:
+            x = x.to(torch.bfloat16)
+            w = w.to(torch.bfloat16)
+        if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or not stem_ok(x, w, s, p):
+            return super().forward_stats(x, want_stats, join, bn_link)
+        x = x.contiguous(memory_format=torch.channels_last)
+        ho, wo = x.shape[2] // 2, x.shape[3] // 2
+        fv = pick_variant(x.shape[0] * ho * wo, w.shape[0])
+        fv = fv if TILES[fv][1] == 64 else 1          # c16 needs a 64-wide output tile
+        want = want_stats and torch.is_grad_enabled() and self.training
+        with torch.autocast("cuda", enabled=False):
+            z = _ext.load().s2d_stem(x)
+            w16 = stem_weight(w)
+            y, part = _StemFn.apply(z, w16, want, fv, (3, 0))
+        return y, ((part, TILES[fv][0]) if want else None)

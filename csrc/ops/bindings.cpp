@@ -52,6 +52,13 @@ hipError_t arena_conv_fwd(const void*, const void*, void*, float*, const void*, 
                           const uint8_t*, const float*, int, int, int, int, int, int, int, int,
                           int, int, hipStream_t);
 hipError_t arena_conv_flip_weight(const void*, void*, int, int, int, int, hipStream_t);
+hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void*, const void*,
+                             const uint8_t*, const float*, int, int, int, int, int, int, int, int,
+                             int, int, int, int, const int*, int, int, hipStream_t);
+hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
+                               int, int, int, int, int, int, int, int, int, int, int, float,
+                               hipStream_t);
+hipError_t arena_s2d_stem(const void*, void*, int, int, int, int, hipStream_t);
 int arena_conv_wgrad_splits(int, int, int, int, int, int, int);
 hipError_t arena_conv_wgrad(const void*, const void*, float*, void*, float*, int, int, int, int,
                             int, int, int, int, int, int, int, float, hipStream_t);
@@ -59,6 +66,7 @@ hipError_t arena_conv_wgrad(const void*, const void*, float*, void*, float*, int
 long long arena_bn_workspace_floats(long long, int);
 long long arena_bn_lvl2_doubles(long long, int);
 void arena_bn_set_reduce_geometry(long long, long long);
+void arena_bn_set_fin_max_blocks(int);
 // csrc/ops/pool_kernels.hip
 hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, int, int, int, int,
                              hipStream_t);
@@ -924,6 +932,123 @@ Tensor conv_flip_weight(Tensor w) {
   return wt;
 }
 
+// General NHWC convolution on the MFMA kernel (csrc/ops/conv_kernels.hip arena_conv_fwd_ex):
+// top/left padding, explicit output size, optional placement of the output pixels into a larger
+// preallocated tensor (y_out with y_map = [osh, osw, ooh, oow]: output (ho, wo) -> (ho*osh+ooh,
+// wo*osw+oow) of y_out), c16 mode (C == 16, S % 4 == 0). addend may alias y_out (in-place
+// accumulate: each element is read and written by the same lane).
+std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_h, int64_t pad_w,
+                                int64_t Ho, int64_t Wo, int64_t variant, bool with_stats,
+                                OptT addend, OptT y_out, std::vector<int64_t> y_map, bool c16) {
+  TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4 &&
+                  x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16 &&
+                  x.device() == w.device(),
+              "conv_fwd_ex: x and w must be 4-D bf16 tensors on one GPU");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_fwd_ex: x and w must be channels_last contiguous");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = w.size(0), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(w.size(1) == C, "conv_fwd_ex: weight/input channel mismatch");
+  TORCH_CHECK(Cout % 64 == 0 && (c16 ? (C == 16 && S % 4 == 0) : C % 64 == 0),
+              "conv_fwd_ex: Cout % 64, and C % 64 (or C == 16, S % 4 == 0 in c16 mode)");
+  TORCH_CHECK(variant >= 0 && variant <= 3 && ((variant & 1) || Cout % 128 == 0),
+              "conv_fwd_ex: bad variant");
+  TORCH_CHECK(stride >= 1 && Ho >= 1 && Wo >= 1, "conv_fwd_ex: bad geometry");
+  TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_fwd_ex: too many output pixels");
+  Tensor y;
+  std::vector<int> map6;
+  if (y_out.has_value()) {
+    y = *y_out;
+    TORCH_CHECK(y.is_cuda() && y.device() == x.device() && y.dim() == 4 &&
+                    y.scalar_type() == torch::kBFloat16 && y.size(0) == N && y.size(1) == Cout &&
+                    y.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_fwd_ex: y_out must be a channels_last bf16 [N, Cout, Hy, Wy] tensor");
+    TORCH_CHECK(y_map.size() == 4 && y_map[0] >= 1 && y_map[1] >= 1 && y_map[2] >= 0 &&
+                    y_map[3] >= 0 && (Ho - 1) * y_map[0] + y_map[2] < y.size(2) &&
+                    (Wo - 1) * y_map[1] + y_map[3] < y.size(3),
+                "conv_fwd_ex: y_map must place every output pixel inside y_out");
+    map6 = {(int)y.size(2), (int)y.size(3), (int)y_map[0], (int)y_map[1], (int)y_map[2],
+            (int)y_map[3]};
+  } else {
+    y = torch::empty({N, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
+  if (addend.has_value()) {
+    TORCH_CHECK(addend->sizes() == y.sizes() && addend->scalar_type() == torch::kBFloat16 &&
+                    addend->device() == y.device() &&
+                    addend->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_fwd_ex: addend must be shaped like the output tensor");
+  }
+  static const int bm[4] = {128, 128, 64, 64};
+  const int64_t m_tiles = (N * Ho * Wo + bm[variant] - 1) / bm[variant];
+  TORCH_CHECK(!(with_stats && y_out.has_value()), "conv_fwd_ex: statistics need a dense output");
+  Tensor part = with_stats ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
+                           : Tensor();
+  check_hip(arena_conv_fwd_ex(x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                              with_stats ? part.data_ptr<float>() : nullptr,
+                              addend.has_value() ? addend->data_ptr() : nullptr, nullptr, nullptr,
+                              nullptr, (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R, (int)S,
+                              (int)stride, (int)pad_h, (int)pad_w, (int)Ho, (int)Wo,
+                              y_out.has_value() ? map6.data() : nullptr, c16 ? 1 : 0,
+                              (int)variant, cur_stream()),
+            "conv_fwd_ex");
+  if (with_stats) return {y, part};
+  return {y};
+}
+
+// dW [Cout, C, R, S] (channels_last) of a convolution with top/left padding and an explicit
+// output size (dy's), c16 mode as conv_fwd_ex.
+Tensor conv_wgrad_ex(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int64_t pad_h,
+                     int64_t pad_w, int64_t variant, int64_t splits_hint, bool out_fp32,
+                     double scale, bool c16) {
+  TORCH_CHECK(x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4 &&
+                  x.scalar_type() == torch::kBFloat16 && dy.scalar_type() == torch::kBFloat16 &&
+                  x.device() == dy.device(),
+              "conv_wgrad_ex: x and dy must be 4-D bf16 tensors on one GPU");
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_wgrad_ex: x and dy must be channels_last contiguous");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  const int64_t Cout = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
+  TORCH_CHECK(dy.size(0) == N && R >= 1 && S >= 1 && stride >= 1, "conv_wgrad_ex: bad geometry");
+  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
+  TORCH_CHECK(variant >= 0 && variant <= 3 && Cout % bm[variant] == 0 &&
+                  (c16 ? (C == 16 && S % 4 == 0 && bn[variant] == 64) : C % bn[variant] == 0),
+              "conv_wgrad_ex: variant ", variant, " does not fit C=", C, " Cout=", Cout);
+  TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad_ex: too many output pixels");
+  const int64_t Ktot = R * S * C;
+  const int splits = arena_conv_wgrad_splits((int)N, (int)Ho, (int)Wo, (int)Cout, (int)Ktot,
+                                             (int)variant, (int)splits_hint);
+  TORCH_CHECK(splits >= 1, "conv_wgrad_ex: bad split count");
+  Tensor ws = torch::empty({(int64_t)splits * Cout * Ktot}, x.options().dtype(torch::kFloat32));
+  Tensor dw = torch::empty({Cout, C, R, S}, x.options()
+                                                .dtype(out_fp32 ? torch::kFloat32 : torch::kBFloat16)
+                                                .memory_format(at::MemoryFormat::ChannelsLast));
+  check_hip(arena_conv_wgrad_ex(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(),
+                                out_fp32 ? nullptr : dw.data_ptr(),
+                                out_fp32 ? dw.data_ptr<float>() : nullptr, (int)N, (int)H, (int)W,
+                                (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad_h,
+                                (int)pad_w, (int)Ho, (int)Wo, c16 ? 1 : 0, (int)variant,
+                                (int)splits_hint, (float)scale, cur_stream()),
+            "conv_wgrad_ex");
+  return dw;
+}
+
+// Space-to-depth of a channels_last [N, C<=4, H, W] bf16 image: [N, 16, H/2, W/2] (see kernel).
+Tensor s2d_stem(Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == torch::kBFloat16 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) <= 4 &&
+                  x.size(2) % 2 == 0 && x.size(3) % 2 == 0,
+              "s2d_stem: channels_last bf16 [N, C<=4, H, W] with even H, W");
+  const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
+  Tensor z = torch::empty({N, 16, H / 2, W / 2},
+                          x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_hip(arena_s2d_stem(x.data_ptr(), z.data_ptr(), (int)N, (int)H, (int)W, (int)C,
+                           cur_stream()),
+            "s2d_stem");
+  return z;
+}
+
 // dW of an NHWC convolution: [Cout, C, R, S] channels_last, bf16 (for MasterSGD) or fp32.
 Tensor conv_wgrad(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int64_t pad,
                   int64_t variant, int64_t splits_hint, bool out_fp32, double scale) {
@@ -1076,6 +1201,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_fwd", &linear_fwd);
   m.def("bn_fwd", &bn_fwd);
   m.def("conv_flip_weight", &conv_flip_weight);
+  m.def("conv_fwd_ex", &conv_fwd_ex);
+  m.def("conv_wgrad_ex", &conv_wgrad_ex);
+  m.def("s2d_stem", &s2d_stem);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("mean"),
         py::arg("invstd"), py::arg("gamma"), py::arg("relu"), py::arg("with_res"),
         py::arg("affine_grads"), py::arg("ext_part") = py::none(), py::arg("ext_rpb") = 0);
@@ -1086,6 +1214,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_wgrad", &conv_wgrad);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
+  m.def("bn_set_fin_max_blocks", [](int64_t p) { arena_bn_set_fin_max_blocks((int)p); });
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
     arena_bn_set_reduce_geometry(max_blocks, min_rounds);
   });

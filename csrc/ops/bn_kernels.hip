@@ -197,11 +197,11 @@ __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, l
 // was latency-bound: 13.5 us per layer on average, 43 us behind a 56x56 conv.)
 constexpr int kFinWaves = kT / 64;
 constexpr int kFinU = 8;        // partials per lane per load batch
-constexpr int kFinMaxP = 64;    // level-1 blocks per channel group
+int g_fin_max_p = 64;           // level-1 blocks per channel group (runtime-tunable; 1 = no tickets)
 
 int fin_blocks_per_group(int nblk) {
   int p = (nblk + kFinWaves * kFinU - 1) / (kFinWaves * kFinU);
-  return p < 1 ? 1 : (p > kFinMaxP ? kFinMaxP : p);
+  return p < 1 ? 1 : (p > g_fin_max_p ? g_fin_max_p : p);
 }
 
 // Sum of the 4 waves' (a, b, c) in LDS, fixed order, into wave 0's lanes. Returns false on the
@@ -553,6 +553,8 @@ bool bad_shape(long long M, int C) {
 }  // namespace
 
 extern "C" {
+
+void arena_bn_set_fin_max_blocks(int p) { g_fin_max_p = p < 1 ? 1 : (p > 64 ? 64 : p); }
 
 void arena_bn_set_reduce_geometry(long long max_blocks, long long min_rounds) {
   g_max_reduce_blocks = max_blocks < 1 ? 1 : (max_blocks > 4096 ? 4096 : max_blocks);

@@ -63,6 +63,15 @@ struct ConvArgs {
   int M;               // N * Ho * Wo
   int Ktot;            // R * S * C
   int m_tiles, n_tiles;
+  int pad_w;           // left padding (pad is the top one)
+  // Output placement: output pixel (n, ho, wo) is stored at (n, ho*osh + ooh, wo*osw + oow) of a
+  // [N][Hy][Wy][Cout] tensor (mapped != 0; else dense [N][Ho][Wo][Cout]). The phases of a
+  // stride-2 backward-data pass each write one parity class of dX this way.
+  int mapped, Hy, Wy, osh, osw, ooh, oow;
+  // c16: C == 16 and a 64-deep K step is one filter row and FOUR consecutive filter columns
+  // (4 pixels x 16 channels = 128 contiguous bytes of an NHWC row). S is a multiple of 4. The
+  // space-to-depth form of the 7x7/2 stem runs on it.
+  int c16;
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -133,7 +142,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
       const int n = m / hw, rem = m - n * hw;
       const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
       a_hb[i] = ho * a.stride - a.pad;
-      a_wb[i] = wo * a.stride - a.pad;
+      a_wb[i] = wo * a.stride - a.pad_w;
       a_nb[i] = n * a.H;
     } else {
       a_hb[i] = -(1 << 28);  // every tap invalid -> zero page
@@ -147,20 +156,36 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
     const int row = (wave * BI + i) * 8 + (lane >> 3);
     b_src[i] = a.w + (size_t)(n0 + row) * a.Ktot + (pos ^ swz(row)) * 8;
   }
-  const int CB = a.C / kBK;  // 64-channel blocks per tap
+  const int CB = a.c16 ? 1 : a.C / kBK;  // 64-channel blocks per tap
 
   auto stage = [&](int t, int buf) {
-    const int tap = t / CB, cb = t - tap * CB;
-    const int r = tap / a.S, s = tap - r * a.S;
     uint8_t* base = lds + buf * kBufBytes;
+    if (a.c16) {
+      // K step t = filter row r, columns 4*sb .. 4*sb+3; 16-byte chunk c = pixel c/2, half c%2
+      const int SB = a.S >> 2;
+      const int r = t / SB, sb = t - r * SB;
 #pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const int hi = a_hb[i] + r, wi = a_wb[i] + s;
-      const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-      const void* src = ok ? (const void*)(a.x + ((size_t)(a_nb[i] + hi) * a.W + wi) * a.C +
-                                           cb * kBK + a_chunk[i] * 8)
-                           : (const void*)g_zero_page;
-      glds16(src, base + (wave * AI + i) * 64 * 16);
+      for (int i = 0; i < AI; ++i) {
+        const int c = a_chunk[i];
+        const int hi = a_hb[i] + r, wi = a_wb[i] + sb * 4 + (c >> 1);
+        const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        const void* src = ok ? (const void*)(a.x + ((size_t)(a_nb[i] + hi) * a.W + wi) * 16 +
+                                             (c & 1) * 8)
+                             : (const void*)g_zero_page;
+        glds16(src, base + (wave * AI + i) * 64 * 16);
+      }
+    } else {
+      const int tap = t / CB, cb = t - tap * CB;
+      const int r = tap / a.S, s = tap - r * a.S;
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int hi = a_hb[i] + r, wi = a_wb[i] + s;
+        const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+        const void* src = ok ? (const void*)(a.x + ((size_t)(a_nb[i] + hi) * a.W + wi) * a.C +
+                                             cb * kBK + a_chunk[i] * 8)
+                             : (const void*)g_zero_page;
+        glds16(src, base + (wave * AI + i) * 64 * 16);
+      }
     }
     uint8_t* bbase = base + BM * kRowBytes;
 #pragma unroll
@@ -235,7 +260,14 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * WM + i * 16 + fr;
     if (m >= a.M) continue;
-    uint16_t* yrow = a.y + (size_t)m * a.Cout + n0 + wn * WN + 4 * fq;
+    size_t pix = (size_t)m;
+    if (a.mapped) {
+      const int hw = a.Ho * a.Wo;
+      const int n = m / hw, rem = m - n * hw;
+      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+      pix = ((size_t)n * a.Hy + ho * a.osh + a.ooh) * a.Wy + wo * a.osw + a.oow;
+    }
+    uint16_t* yrow = a.y + pix * a.Cout + n0 + wn * WN + 4 * fq;
     if (a.add != nullptr) {
       const uint16_t* arow = a.add + (yrow - a.y);
       uint2 q[NI];
@@ -377,14 +409,17 @@ extern "C" {
 // MIOpen): C % 64 != 0, Cout % 64 != 0, or an unknown tile variant.
 // variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (BM x BN output tile per block).
 // part (optional): BatchNorm partials of y, [ceil(M / BM)][2][Cout] (EPI 1 / EPI 2 epilogues).
+// General form. pad_h/pad_w: top/left padding; Ho/Wo: output size (<= 0: derived from a symmetric
+// padding); y_map {Hy, Wy, osh, osw, ooh, oow} (null: dense output); c16: see ConvArgs.
 // bnx/bnmask/bnmean (optional, with part): the backward-data form, part = BatchNorm-backward
 // partials of y instead of forward statistics (see ConvArgs).
-hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, const void* add,
-                          const void* bnx, const uint8_t* bnmask, const float* bnmean,
-                          int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad,
-                          int variant, hipStream_t st) {
-  if (C % kBK || Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
-    return hipErrorInvalidValue;
+hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part, const void* add,
+                             const void* bnx, const uint8_t* bnmask, const float* bnmean, int N,
+                             int H, int W, int C, int Cout, int R, int S, int stride, int pad_h,
+                             int pad_w, int Ho, int Wo, const int* y_map, int c16, int variant,
+                             hipStream_t st) {
+  if (Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0) return hipErrorInvalidValue;
+  if (c16 ? (C != 16 || S % 4) : (C % kBK)) return hipErrorInvalidValue;
   ConvArgs a{};
   a.x = (const uint16_t*)x;
   a.w = (const uint16_t*)w;
@@ -394,12 +429,23 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
   a.bnx = (const uint16_t*)bnx;
   a.bnmask = bnmask;
   a.bnmean = bnmean;
-  if (bnx != nullptr && (part == nullptr || bnmean == nullptr)) return hipErrorInvalidValue;
+  if (bnx != nullptr && (part == nullptr || bnmean == nullptr || y_map != nullptr))
+    return hipErrorInvalidValue;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
-  a.stride = stride; a.pad = pad;
-  a.Ho = (H + 2 * pad - R) / stride + 1;
-  a.Wo = (W + 2 * pad - S) / stride + 1;
+  a.stride = stride; a.pad = pad_h; a.pad_w = pad_w;
+  a.Ho = Ho > 0 ? Ho : (H + 2 * pad_h - R) / stride + 1;
+  a.Wo = Wo > 0 ? Wo : (W + 2 * pad_w - S) / stride + 1;
   if (a.Ho <= 0 || a.Wo <= 0) return hipErrorInvalidValue;
+  a.c16 = c16;
+  if (y_map != nullptr) {
+    a.mapped = 1;
+    a.Hy = y_map[0]; a.Wy = y_map[1]; a.osh = y_map[2]; a.osw = y_map[3];
+    a.ooh = y_map[4]; a.oow = y_map[5];
+    // every mapped output pixel inside the [Hy][Wy] image (the caller checked the sizes too)
+    if ((a.Ho - 1) * a.osh + a.ooh >= a.Hy || (a.Wo - 1) * a.osw + a.oow >= a.Wy || a.ooh < 0 ||
+        a.oow < 0 || a.osh <= 0 || a.osw <= 0)
+      return hipErrorInvalidValue;
+  }
   const long long M = (long long)N * a.Ho * a.Wo;
   if (M >= (1LL << 31) || (long long)N * H * W * C >= (1LL << 40)) return hipErrorInvalidValue;
   a.M = (int)M;
@@ -411,6 +457,14 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
     case 3: return launch<64, 64>(a, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, const void* add,
+                          const void* bnx, const uint8_t* bnmask, const float* bnmean,
+                          int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad,
+                          int variant, hipStream_t st) {
+  return arena_conv_fwd_ex(x, w, y, part, add, bnx, bnmask, bnmean, N, H, W, C, Cout, R, S,
+                           stride, pad, pad, 0, 0, nullptr, 0, variant, st);
 }
 
 }  // extern "C"
@@ -468,6 +522,54 @@ extern "C" hipError_t arena_conv_flip_weight(const void* w, void* wt, int Cout, 
 }
 
 // ================================================================================================
+// Space-to-depth for the 7x7/2 stem: x [N][H][W][C] (C <= 4) -> z [N][H/2][W/2][16] with
+// z[n][i][j][(dy*2 + dx)*C + c] = x[n][2i+dy][2j+dx][c] and channels 4C..15 zero. The stride-2
+// 7x7 convolution over x is then a stride-1 4x4 convolution over z (arena_amd/ops/conv.py
+// StemConv2d), which the MFMA kernel runs in its c16 mode.
+// ================================================================================================
+namespace {
+
+__global__ __launch_bounds__(256) void s2d_stem_kernel(const uint16_t* __restrict__ x,
+                                                       uint16_t* __restrict__ z, int N, int H,
+                                                       int W, int C) {
+  const int Hz = H >> 1, Wz = W >> 1;
+  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (p >= (long long)N * Hz * Wz) return;
+  const int j = (int)(p % Wz);
+  const long long t = p / Wz;
+  const int i = (int)(t % Hz), n = (int)(t / Hz);
+  uint16_t v[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) v[k] = 0;
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint16_t* src = x + (((size_t)n * H + 2 * i + (d >> 1)) * W + 2 * j + (d & 1)) * C;
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+      if (c < C) v[d * C + c] = src[c];
+  }
+  uint4 o0, o1;
+  o0.x = v[0] | ((uint32_t)v[1] << 16); o0.y = v[2] | ((uint32_t)v[3] << 16);
+  o0.z = v[4] | ((uint32_t)v[5] << 16); o0.w = v[6] | ((uint32_t)v[7] << 16);
+  o1.x = v[8] | ((uint32_t)v[9] << 16); o1.y = v[10] | ((uint32_t)v[11] << 16);
+  o1.z = v[12] | ((uint32_t)v[13] << 16); o1.w = v[14] | ((uint32_t)v[15] << 16);
+  uint4* dst = reinterpret_cast<uint4*>(z + p * 16);
+  dst[0] = o0;
+  dst[1] = o1;
+}
+
+}  // namespace
+
+extern "C" hipError_t arena_s2d_stem(const void* x, void* z, int N, int H, int W, int C,
+                                     hipStream_t st) {
+  if (N <= 0 || H % 2 || W % 2 || C < 1 || C > 4) return hipErrorInvalidValue;
+  const long long P = (long long)N * (H / 2) * (W / 2);
+  hipLaunchKernelGGL(s2d_stem_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st,
+                     (const uint16_t*)x, (uint16_t*)z, N, H, W, C);
+  return hipGetLastError();
+}
+
+// ================================================================================================
 // Backward-weight: dW[co][r][s][ci] = sum_m dY[m][co] * X[pix(m, r, s)][ci]
 //
 // A GEMM of Cout rows, R*S*C columns and N*Ho*Wo (up to 400k) reduction steps, so the reduction
@@ -502,6 +604,8 @@ struct WgradArgs {
   int M, Ktot;
   int m_tiles, n_tiles, splits, sps;  // sps = 64-pixel steps per split
   FastDiv div_hw, div_w;
+  int pad_w;           // left padding (pad is the top one)
+  int c16;             // C == 16, a BN = 64 column tile = one filter row x 4 columns x 16 channels
 };
 
 // chunk permutation of a pixel row of RB bytes (bit 0 of the chunk index is kept: 32-B pairs)
@@ -531,8 +635,19 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
   const int split = lin / tiles, t2 = lin - split * tiles;
   const int mt = t2 / a.n_tiles, nt = t2 - mt * a.n_tiles;
   const int co0 = mt * BM, kk0 = nt * BN;
-  const int tap = kk0 / a.C, ci0 = kk0 - tap * a.C;
-  const int rr = tap / a.S, ss = tap - rr * a.S;
+  int tap, ci0, rr, ss;
+  if (a.c16) {   // column tile nt = filter row rr, columns 4*sb .. 4*sb+3 (BN == 64, host-checked)
+    const int SB = a.S >> 2;
+    rr = nt / SB;
+    ss = (nt - rr * SB) * 4;
+    tap = 0;
+    ci0 = 0;
+  } else {
+    tap = kk0 / a.C;
+    ci0 = kk0 - tap * a.C;
+    rr = tap / a.S;
+    ss = tap - rr * a.S;
+  }
   const int step0 = split * a.sps;
   const int nsteps = min(a.sps, (a.M + kPix - 1) / kPix - step0);
 
@@ -564,10 +679,14 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
         const int rem = m - n * a.Ho * a.Wo;
         const int ho = (int)fdiv((uint32_t)rem, a.div_w);
         const int wo = rem - ho * a.Wo;
-        const int hi = ho * a.stride - a.pad + rr, wi = wo * a.stride - a.pad + ss;
+        const int cch = b_pos ^ wswz<RBB>(row);   // this slot's global 16-byte chunk
+        const int hi = ho * a.stride - a.pad + rr;
+        const int wi = wo * a.stride - a.pad_w + ss + (a.c16 ? (cch >> 1) : 0);
         if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
-          src = (const void*)(a.x + ((size_t)(n * a.H + hi) * a.W + wi) * a.C + ci0 +
-                              (b_pos ^ wswz<RBB>(row)) * 8);
+          src = a.c16 ? (const void*)(a.x + ((size_t)(n * a.H + hi) * a.W + wi) * 16 +
+                                      (cch & 1) * 8)
+                      : (const void*)(a.x + ((size_t)(n * a.H + hi) * a.W + wi) * a.C + ci0 +
+                                      cch * 8);
       }
       glds16(src, bb + (wave * BI + i) * 1024);
     }
@@ -734,22 +853,25 @@ int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int varia
 }
 
 // variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (Cout x R*S*C tile). Needs C % BN == 0
-// (a tile never straddles two filter taps) and Cout % BM == 0.
-hipError_t arena_conv_wgrad(const void* x, const void* dy, float* ws, void* dw_bf16, float* dw_f32,
-                            int N, int H, int W, int C, int Cout, int R, int S, int stride,
-                            int pad, int variant, int splits_hint, float scale, hipStream_t st) {
+// (a tile never straddles two filter taps) and Cout % BM == 0; c16 mode: C == 16, S % 4 == 0 and
+// BN == 64 (variants 1 and 3). Ho/Wo <= 0: derived from a symmetric padding.
+hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* dw_bf16,
+                               float* dw_f32, int N, int H, int W, int C, int Cout, int R, int S,
+                               int stride, int pad_h, int pad_w, int Ho, int Wo, int c16,
+                               int variant, int splits_hint, float scale, hipStream_t st) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
   if (variant < 0 || variant > 3) return hipErrorInvalidValue;
-  if (C % bn[variant] || Cout % bm[variant] || N <= 0 || stride <= 0 || pad < 0)
+  if (c16 ? (C != 16 || S % 4 || bn[variant] != 64) : (C % bn[variant] != 0))
     return hipErrorInvalidValue;
+  if (Cout % bm[variant] || N <= 0 || stride <= 0) return hipErrorInvalidValue;
   WgradArgs a{};
   a.x = (const uint16_t*)x;
   a.dy = (const uint16_t*)dy;
   a.ws = ws;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
-  a.stride = stride; a.pad = pad;
-  a.Ho = (H + 2 * pad - R) / stride + 1;
-  a.Wo = (W + 2 * pad - S) / stride + 1;
+  a.stride = stride; a.pad = pad_h; a.pad_w = pad_w; a.c16 = c16;
+  a.Ho = Ho > 0 ? Ho : (H + 2 * pad_h - R) / stride + 1;
+  a.Wo = Wo > 0 ? Wo : (W + 2 * pad_w - S) / stride + 1;
   if (a.Ho <= 0 || a.Wo <= 0) return hipErrorInvalidValue;
   const long long M = (long long)N * a.Ho * a.Wo;
   if (M >= (1LL << 31)) return hipErrorInvalidValue;
@@ -772,6 +894,13 @@ hipError_t arena_conv_wgrad(const void* x, const void* dy, float* ws, void* dw_b
                      reinterpret_cast<const float4*>(ws), splits, n4,
                      reinterpret_cast<uint2*>(dw_bf16), reinterpret_cast<float4*>(dw_f32), scale);
   return hipGetLastError();
+}
+
+hipError_t arena_conv_wgrad(const void* x, const void* dy, float* ws, void* dw_bf16, float* dw_f32,
+                            int N, int H, int W, int C, int Cout, int R, int S, int stride,
+                            int pad, int variant, int splits_hint, float scale, hipStream_t st) {
+  return arena_conv_wgrad_ex(x, dy, ws, dw_bf16, dw_f32, N, H, W, C, Cout, R, S, stride, pad, pad,
+                             0, 0, 0, variant, splits_hint, scale, st);
 }
 
 }  // extern "C"
