@@ -119,44 +119,47 @@ def conv2d_bwd_data_strided(dy: Tensor, w: Tensor, x_hw: Tuple[int, int], stride
     Input pixel (i*s + a, j*s + b) only receives the filter taps r with (a + pad - r) % s == 0;
     over the phase grid (i, j) that is a stride-1 convolution of dY with the flipped sub-filter
     W[:, :, r0::s, c0::s], written straight into the (a, b) parity class of dX (the kernel's
-    mapped output). Phases without taps (1x1, stride 2: three of four) keep ``addend`` (or 0)."""
+    mapped output). All phase weights come from one ``conv_phase_weights`` launch. ``addend`` (the
+    residual join's other gradient) is added in the epilogue. Phases without taps (1x1 stride 2:
+    three of four) are the addend or zero: when phase (0, 0) is the only one with taps its
+    epilogue writes them too (fill_sib), so dX is written in one pass."""
     N, Cout, Ho, Wo = dy.shape
     Cin, R, S = w.shape[1], w.shape[2], w.shape[3]
     H, W = x_hw
     dy = dy.contiguous(memory_format=torch.channels_last)
-    ext = _ext.load()
-    full = all((a + pad) % stride < R for a in range(stride)) and \
-        all((b + pad) % stride < S for b in range(stride))
     if addend is not None:
-        dx = addend.contiguous(memory_format=torch.channels_last).clone()
-    elif full:
-        dx = torch.empty(N, Cin, H, W, device=dy.device, dtype=dy.dtype,
-                         memory_format=torch.channels_last)
-    else:
-        dx = torch.zeros(N, Cin, H, W, device=dy.device, dtype=dy.dtype).contiguous(
-            memory_format=torch.channels_last)
+        addend = addend.contiguous(memory_format=torch.channels_last)
+    ext = _ext.load()
+    phases = []
     for a in range(stride):
         r0 = (a + pad) % stride
         if r0 >= R:
             continue
-        Rp = len(range(r0, R, stride))
-        ca = (a + pad - r0) // stride
-        Hp = (H - a + stride - 1) // stride
         for b in range(stride):
             c0 = (b + pad) % stride
-            if c0 >= S or Hp <= 0:
+            if c0 >= S:
                 continue
-            Sp = len(range(c0, S, stride))
-            cb = (b + pad - c0) // stride
-            Wp = (W - b + stride - 1) // stride
-            if Wp <= 0:
-                continue
-            wp = w[:, :, r0::stride, c0::stride].flip(2, 3).transpose(0, 1).contiguous(
-                memory_format=torch.channels_last)
-            v = variant if variant >= 0 else pick_variant(N * Hp * Wp, Cin)
-            ext.conv_fwd_ex(dy, wp, 1, Rp - 1 - ca, Sp - 1 - cb, Hp, Wp, int(v), False,
-                            dx if addend is not None else None, dx, [stride, stride, a, b],
-                            False)
+            phases.append((a, b, r0, c0))
+    wps = ext.conv_phase_weights(w.contiguous(memory_format=torch.channels_last), stride, pad)
+    full = len(phases) == stride * stride
+    sib = len(phases) == 1 and phases[0][:2] == (0, 0)
+    dx = torch.empty(N, Cin, H, W, device=dy.device, dtype=dy.dtype,
+                     memory_format=torch.channels_last)
+    if not (full or sib):          # uncovered pixels: addend or zero, then accumulate in place
+        if addend is not None:
+            dx.copy_(addend)
+        else:
+            dx.zero_()
+        addend = dx
+    for (a, b, r0, c0), wp in zip(phases, wps):
+        Rp, Sp = wp.shape[2], wp.shape[3]
+        ca, cb = (a + pad - r0) // stride, (b + pad - c0) // stride
+        Hp, Wp = (H - a + stride - 1) // stride, (W - b + stride - 1) // stride
+        if Hp <= 0 or Wp <= 0:
+            continue
+        v = variant if variant >= 0 else pick_variant(N * Hp * Wp, Cin)
+        ext.conv_fwd_ex(dy, wp, 1, Rp - 1 - ca, Sp - 1 - cb, Hp, Wp, int(v), False, addend, dx,
+                        [stride, stride, a, b] + ([1] if sib else []), False)
     return dx
 
 

@@ -59,6 +59,8 @@ hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, 
                                int, int, int, int, int, int, int, int, int, int, int, float,
                                hipStream_t);
 hipError_t arena_s2d_stem(const void*, void*, int, int, int, int, hipStream_t);
+hipError_t arena_conv_phase_weights(const void*, void*, int, int, int, int, int, int, long long*,
+                                    hipStream_t);
 int arena_conv_wgrad_splits(int, int, int, int, int, int, int);
 hipError_t arena_conv_wgrad(const void*, const void*, float*, void*, float*, int, int, int, int,
                             int, int, int, int, int, int, int, float, hipStream_t);
@@ -932,11 +934,47 @@ Tensor conv_flip_weight(Tensor w) {
   return wt;
 }
 
+// Phase weights of a stride-`stride` backward-data pass (arena_conv_phase_weights): one launch,
+// one buffer; returns one channels_last [C, Cout, Rp, Sp] view per phase with taps, in phase
+// order (a, b) row-major (phases without taps are absent).
+std::vector<Tensor> conv_phase_weights(Tensor w, int64_t stride, int64_t pad) {
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == torch::kBFloat16 &&
+                  w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_phase_weights: w must be a channels_last bf16 GPU tensor [Cout, C, R, S]");
+  const int64_t Cout = w.size(0), C = w.size(1), R = w.size(2), S = w.size(3);
+  TORCH_CHECK(Cout % 64 == 0 && C % 64 == 0 && stride >= 1 && pad >= 0,
+              "conv_phase_weights: C and Cout must be multiples of 64");
+  long long total = 0;
+  check_hip(arena_conv_phase_weights(w.data_ptr(), nullptr, (int)Cout, (int)C, (int)R, (int)S,
+                                     (int)stride, (int)pad, &total, cur_stream()),
+            "conv_phase_weights (geometry)");
+  Tensor flat = torch::empty({std::max<long long>(total, 1)}, w.options());
+  check_hip(arena_conv_phase_weights(w.data_ptr(), flat.data_ptr(), (int)Cout, (int)C, (int)R,
+                                     (int)S, (int)stride, (int)pad, nullptr, cur_stream()),
+            "conv_phase_weights");
+  std::vector<Tensor> out;
+  int64_t off = 0;
+  for (int64_t a = 0; a < stride; ++a) {
+    const int64_t r0 = (a + pad) % stride;
+    if (r0 >= R) continue;
+    const int64_t Rp = (R - r0 + stride - 1) / stride;
+    for (int64_t b = 0; b < stride; ++b) {
+      const int64_t c0 = (b + pad) % stride;
+      if (c0 >= S) continue;
+      const int64_t Sp = (S - c0 + stride - 1) / stride;
+      out.push_back(flat.as_strided({C, Cout, Rp, Sp}, {Rp * Sp * Cout, 1, Sp * Cout, Cout}, off));
+      off += C * Rp * Sp * Cout;
+    }
+  }
+  return out;
+}
+
 // General NHWC convolution on the MFMA kernel (csrc/ops/conv_kernels.hip arena_conv_fwd_ex):
 // top/left padding, explicit output size, optional placement of the output pixels into a larger
 // preallocated tensor (y_out with y_map = [osh, osw, ooh, oow]: output (ho, wo) -> (ho*osh+ooh,
-// wo*osw+oow) of y_out), c16 mode (C == 16, S % 4 == 0). addend may alias y_out (in-place
-// accumulate: each element is read and written by the same lane).
+// wo*osw+oow) of y_out; an optional 5th entry fill_sib = 1 also writes the untapped sibling pixels
+// of phase (0, 0) with the addend or zero), c16 mode (C == 16, S % 4 == 0). addend may alias y_out
+// (in-place accumulate: each element is read and written by the same lane).
 std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_h, int64_t pad_w,
                                 int64_t Ho, int64_t Wo, int64_t variant, bool with_stats,
                                 OptT addend, OptT y_out, std::vector<int64_t> y_map, bool c16) {
@@ -964,12 +1002,18 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
                     y.scalar_type() == torch::kBFloat16 && y.size(0) == N && y.size(1) == Cout &&
                     y.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_fwd_ex: y_out must be a channels_last bf16 [N, Cout, Hy, Wy] tensor");
-    TORCH_CHECK(y_map.size() == 4 && y_map[0] >= 1 && y_map[1] >= 1 && y_map[2] >= 0 &&
-                    y_map[3] >= 0 && (Ho - 1) * y_map[0] + y_map[2] < y.size(2) &&
+    TORCH_CHECK((y_map.size() == 4 || y_map.size() == 5) && y_map[0] >= 1 && y_map[1] >= 1 &&
+                    y_map[2] >= 0 && y_map[3] >= 0 && (Ho - 1) * y_map[0] + y_map[2] < y.size(2) &&
                     (Wo - 1) * y_map[1] + y_map[3] < y.size(3),
                 "conv_fwd_ex: y_map must place every output pixel inside y_out");
+    const bool fill = y_map.size() == 5 && y_map[4] != 0;
+    // sibling fill: phase (0, 0) whose pixels' siblings tile all of y_out
+    TORCH_CHECK(!fill || (y_map[2] == 0 && y_map[3] == 0 &&
+                          Ho == (y.size(2) + y_map[0] - 1) / y_map[0] &&
+                          Wo == (y.size(3) + y_map[1] - 1) / y_map[1]),
+                "conv_fwd_ex: fill_sib needs phase (0, 0) covering y_out");
     map6 = {(int)y.size(2), (int)y.size(3), (int)y_map[0], (int)y_map[1], (int)y_map[2],
-            (int)y_map[3]};
+            (int)y_map[3], fill ? 1 : 0};
   } else {
     y = torch::empty({N, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   }
@@ -1201,6 +1245,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_fwd", &linear_fwd);
   m.def("bn_fwd", &bn_fwd);
   m.def("conv_flip_weight", &conv_flip_weight);
+  m.def("conv_phase_weights", &conv_phase_weights);
   m.def("conv_fwd_ex", &conv_fwd_ex);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);
   m.def("s2d_stem", &s2d_stem);

@@ -68,6 +68,10 @@ struct ConvArgs {
   // [N][Hy][Wy][Cout] tensor (mapped != 0; else dense [N][Ho][Wo][Cout]). The phases of a
   // stride-2 backward-data pass each write one parity class of dX this way.
   int mapped, Hy, Wy, osh, osw, ooh, oow;
+  // fill_sib (mapped, ooh == oow == 0, the only phase with filter taps: 1x1 stride-2 backward
+  // data): each output pixel also stores its osh*osw - 1 sibling pixels of the [Hy][Wy] image,
+  // which receive no taps -- the addend there (add != null) or zero. One pass writes all of dX.
+  int fill_sib;
   // c16: C == 16 and a 64-deep K step is one filter row and FOUR consecutive filter columns
   // (4 pixels x 16 channels = 128 contiguous bytes of an NHWC row). S is a multiple of 4. The
   // space-to-depth form of the 7x7/2 stem runs on it.
@@ -261,13 +265,33 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
     const int m = m0 + wm * WM + i * 16 + fr;
     if (m >= a.M) continue;
     size_t pix = (size_t)m;
+    int n = 0, ho = 0, wo = 0;
     if (a.mapped) {
       const int hw = a.Ho * a.Wo;
-      const int n = m / hw, rem = m - n * hw;
-      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+      n = m / hw;
+      const int rem = m - n * hw;
+      ho = rem / a.Wo;
+      wo = rem - ho * a.Wo;
       pix = ((size_t)n * a.Hy + ho * a.osh + a.ooh) * a.Wy + wo * a.osw + a.oow;
     }
     uint16_t* yrow = a.y + pix * a.Cout + n0 + wn * WN + 4 * fq;
+    if (a.fill_sib) {
+      for (int da = 0; da < a.osh; ++da) {
+        const int hy = ho * a.osh + da;
+        if (hy >= a.Hy) break;
+        for (int db = 0; db < a.osw; ++db) {
+          const int wy = wo * a.osw + db;
+          if ((da == 0 && db == 0) || wy >= a.Wy) continue;
+          const size_t off = (((size_t)n * a.Hy + hy) * a.Wy + wy) * a.Cout + n0 + wn * WN + 4 * fq;
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const uint2 v = a.add ? *reinterpret_cast<const uint2*>(a.add + off + j * 16)
+                                  : make_uint2(0u, 0u);
+            *reinterpret_cast<uint2*>(a.y + off + j * 16) = v;
+          }
+        }
+      }
+    }
     if (a.add != nullptr) {
       const uint16_t* arow = a.add + (yrow - a.y);
       uint2 q[NI];
@@ -410,7 +434,8 @@ extern "C" {
 // variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (BM x BN output tile per block).
 // part (optional): BatchNorm partials of y, [ceil(M / BM)][2][Cout] (EPI 1 / EPI 2 epilogues).
 // General form. pad_h/pad_w: top/left padding; Ho/Wo: output size (<= 0: derived from a symmetric
-// padding); y_map {Hy, Wy, osh, osw, ooh, oow} (null: dense output); c16: see ConvArgs.
+// padding); y_map {Hy, Wy, osh, osw, ooh, oow, fill_sib} (null: dense output); c16, fill_sib:
+// see ConvArgs.
 // bnx/bnmask/bnmean (optional, with part): the backward-data form, part = BatchNorm-backward
 // partials of y instead of forward statistics (see ConvArgs).
 hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part, const void* add,
@@ -440,7 +465,10 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   if (y_map != nullptr) {
     a.mapped = 1;
     a.Hy = y_map[0]; a.Wy = y_map[1]; a.osh = y_map[2]; a.osw = y_map[3];
-    a.ooh = y_map[4]; a.oow = y_map[5];
+    a.ooh = y_map[4]; a.oow = y_map[5]; a.fill_sib = y_map[6];
+    if (a.fill_sib && (a.ooh || a.oow || a.Ho != (a.Hy + a.osh - 1) / a.osh ||
+                       a.Wo != (a.Wy + a.osw - 1) / a.osw))
+      return hipErrorInvalidValue;
     // every mapped output pixel inside the [Hy][Wy] image (the caller checked the sizes too)
     if ((a.Ho - 1) * a.osh + a.ooh >= a.Hy || (a.Wo - 1) * a.osw + a.oow >= a.Wy || a.ooh < 0 ||
         a.oow < 0 || a.osh <= 0 || a.osw <= 0)
@@ -475,22 +503,34 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
 // per block through LDS (a 2-byte pad per row keeps the column reads on distinct banks), 16-byte
 // loads and stores. One launch instead of torch's flip + strided copy (two kernels per dgrad, and
 // a memcpy for 1x1 weights).
+// A stride-s backward-data pass splits into s*s phase convolutions (conv2d_bwd_data_strided), each
+// with the flipped sub-filter of the taps r = r0 (mod s): one launch writes every phase's weights,
+// packed phase after phase, from a per-tap table (blockIdx.z = destination tap).
 // ================================================================================================
 namespace {
 
+constexpr int kMaxFlipTaps = 64;
+
+struct FlipTaps {
+  int src[kMaxFlipTaps];    // source tap r * S + s of W
+  int dtap[kMaxFlipTaps];   // destination tap u * Sp + v within its phase
+  int ntap[kMaxFlipTaps];   // Rp * Sp of that phase
+  int off[kMaxFlipTaps];    // element offset of that phase's [C][Rp][Sp][Cout] block
+};
+
 __global__ __launch_bounds__(256) void conv_flip_weight_kernel(const uint16_t* __restrict__ w,
                                                                uint16_t* __restrict__ wt, int Cout,
-                                                               int C, int R, int S) {
+                                                               int C, int RS, FlipTaps tp) {
   __shared__ uint16_t tile[64][64 + 2];
-  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64, tap = blockIdx.z;
-  const int r = tap / S, s = tap - r * S;
-  const int src_tap = (R - 1 - r) * S + (S - 1 - s);
+  const int ci0 = blockIdx.x * 64, co0 = blockIdx.y * 64, z = blockIdx.z;
+  const int src_tap = tp.src[z], dtap = tp.dtap[z], ntap = tp.ntap[z];
+  uint16_t* dst = wt + tp.off[z];
   const int t = threadIdx.x;
 #pragma unroll
   for (int k = 0; k < 2; ++k) {   // 64 rows (co) x 8 chunks of 8 ci
     const int q = t + k * 256, row = q >> 3, ch = q & 7;
     const uint4 v = *reinterpret_cast<const uint4*>(
-        w + ((size_t)(co0 + row) * R * S + src_tap) * C + ci0 + ch * 8);
+        w + ((size_t)(co0 + row) * RS + src_tap) * C + ci0 + ch * 8);
     const uint32_t u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
@@ -506,20 +546,62 @@ __global__ __launch_bounds__(256) void conv_flip_weight_kernel(const uint16_t* _
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       u[e] = (uint32_t)tile[ch * 8 + 2 * e][row] | ((uint32_t)tile[ch * 8 + 2 * e + 1][row] << 16);
-    *reinterpret_cast<uint4*>(wt + ((size_t)(ci0 + row) * R * S + tap) * Cout + co0 + ch * 8) =
+    *reinterpret_cast<uint4*>(dst + ((size_t)(ci0 + row) * ntap + dtap) * Cout + co0 + ch * 8) =
         make_uint4(u[0], u[1], u[2], u[3]);
   }
 }
 
 }  // namespace
 
-extern "C" hipError_t arena_conv_flip_weight(const void* w, void* wt, int Cout, int C, int R, int S,
-                                             hipStream_t st) {
-  if (Cout % 64 || C % 64 || R <= 0 || S <= 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(conv_flip_weight_kernel, dim3(C / 64, Cout / 64, R * S), dim3(256), 0, st,
-                     (const uint16_t*)w, (uint16_t*)wt, Cout, C, R, S);
+extern "C" {
+
+// Phase weights of a stride-`stride`, top/left-`pad` convolution's backward-data pass, packed in
+// phase order (a, b) = (0, 0), (0, 1), ... skipping phases without taps:
+//   Wp[ci][u][v][co] = W[co][r0 + s*(Rp-1-u)][c0 + s*(Sp-1-v)][ci],  r0 = (a + pad) % s, ...
+// stride 1 is the plain flip. Returns the number of elements written via *total (may be null).
+hipError_t arena_conv_phase_weights(const void* w, void* wt, int Cout, int C, int R, int S,
+                                    int stride, int pad, long long* total, hipStream_t st) {
+  if (Cout % 64 || C % 64 || R <= 0 || S <= 0 || stride <= 0 || pad < 0)
+    return hipErrorInvalidValue;
+  FlipTaps tp{};
+  int nz = 0;
+  long long off = 0;
+  for (int a = 0; a < stride; ++a) {
+    const int r0 = (a + pad) % stride;
+    if (r0 >= R) continue;
+    const int Rp = (R - r0 + stride - 1) / stride;
+    for (int b = 0; b < stride; ++b) {
+      const int c0 = (b + pad) % stride;
+      if (c0 >= S) continue;
+      const int Sp = (S - c0 + stride - 1) / stride;
+      if (nz + Rp * Sp > kMaxFlipTaps || off + (long long)C * Rp * Sp * Cout >= (1LL << 31))
+        return hipErrorInvalidValue;
+      for (int u = 0; u < Rp; ++u)
+        for (int v = 0; v < Sp; ++v) {
+          tp.src[nz] = (r0 + stride * (Rp - 1 - u)) * S + c0 + stride * (Sp - 1 - v);
+          tp.dtap[nz] = u * Sp + v;
+          tp.ntap[nz] = Rp * Sp;
+          tp.off[nz] = (int)off;
+          ++nz;
+        }
+      off += (long long)C * Rp * Sp * Cout;
+    }
+  }
+  if (total != nullptr) *total = off;
+  if (wt == nullptr) return hipSuccess;   // size query
+  if (nz == 0) return hipSuccess;
+  hipLaunchKernelGGL(conv_flip_weight_kernel, dim3(C / 64, Cout / 64, nz), dim3(256), 0, st,
+                     (const uint16_t*)w, (uint16_t*)wt, Cout, C, R * S, tp);
   return hipGetLastError();
 }
+
+hipError_t arena_conv_flip_weight(const void* w, void* wt, int Cout, int C, int R, int S,
+                                  hipStream_t st) {
+  if (R * S > kMaxFlipTaps) return hipErrorInvalidValue;
+  return arena_conv_phase_weights(w, wt, Cout, C, R, S, 1, 0, nullptr, st);
+}
+
+}  // extern "C"
 
 // ================================================================================================
 // Space-to-depth for the 7x7/2 stem: x [N][H][W][C] (C <= 4) -> z [N][H/2][W/2][16] with

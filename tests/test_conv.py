@@ -342,27 +342,50 @@ def test_bn_grad_links_match_plain_backward(monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("k,pad,h", [(3, 1, 10), (1, 0, 10), (3, 1, 11), (1, 0, 7)])
-def test_strided_dgrad_phases_match_fp32(k, pad, h):
-    """Backward-data of a stride-2 convolution as parity-class phase convolutions (mapped kernel
-    output), with and without the in-place addend, odd sizes included."""
+@pytest.mark.parametrize("k,pad,h,st", [(3, 1, 10, 2), (1, 0, 10, 2), (3, 1, 11, 2), (1, 0, 7, 2),
+                                        (1, 0, 10, 3), (2, 0, 11, 3)])
+def test_strided_dgrad_phases_match_fp32(k, pad, h, st):
+    """Backward-data of a strided convolution as parity-class phase convolutions (mapped kernel
+    output), with and without the addend, odd sizes included; covers the three ways dX gets
+    written: every phase tapped, phase (0, 0) alone (sibling fill), and a zero/addend pre-pass
+    (k=2, stride 3: a phase row without taps)."""
     n, cin, cout = 2, 64, 128
     x, wt = _data(n, cin, h, h, cout, k, "cuda", seed=7)
-    ref = F.conv2d(x.float(), wt.float(), stride=2, padding=pad)
+    ref = F.conv2d(x.float(), wt.float(), stride=st, padding=pad)
     dy = torch.randn(ref.shape, device="cuda").to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
     dx_ref = torch.ops.aten.convolution_backward(
-        dy.float(), x.float(), wt.float(), None, [2, 2], [pad, pad], [1, 1], False, [0, 0], 1,
+        dy.float(), x.float(), wt.float(), None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
         [True, False, False])[0]
-    dx = conv.conv2d_bwd_data_strided(dy, wt, (h, h), 2, pad)
+    dx = conv.conv2d_bwd_data_strided(dy, wt, (h, h), st, pad)
     assert dx.shape == x.shape and dx.is_contiguous(memory_format=torch.channels_last)
     assert _rel(dx, dx_ref) < 1e-2, _rel(dx, dx_ref)
     addend = torch.randn(x.shape, device="cuda").to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
-    dxa = conv.conv2d_bwd_data_strided(dy, wt, (h, h), 2, pad, addend=addend)
+    dxa = conv.conv2d_bwd_data_strided(dy, wt, (h, h), st, pad, addend=addend)
     assert _rel(dxa, dx_ref + addend.float()) < 1e-2
     for v in conv.variants_for(cin):   # every tile variant of the phases
-        assert _rel(conv.conv2d_bwd_data_strided(dy, wt, (h, h), 2, pad, v), dx_ref) < 1e-2
+        assert _rel(conv.conv2d_bwd_data_strided(dy, wt, (h, h), st, pad, v), dx_ref) < 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,st,pad", [(3, 2, 1), (1, 2, 0), (3, 1, 1), (5, 3, 2)])
+def test_phase_weights_match_torch_slicing(k, st, pad):
+    """conv_phase_weights (one launch) == W[:, :, r0::s, c0::s].flip(2, 3).transpose(0, 1) per
+    phase, bit for bit."""
+    _, wt = _data(1, 64, 4, 4, 128, k, "cuda", seed=3)
+    got = conv._ext.load().conv_phase_weights(wt, st, pad)
+    want = []
+    for a in range(st):
+        r0 = (a + pad) % st
+        for b in range(st):
+            c0 = (b + pad) % st
+            if r0 < k and c0 < k:
+                want.append(wt[:, :, r0::st, c0::st].flip(2, 3).transpose(0, 1))
+    assert len(got) == len(want)
+    for g, w in zip(got, want):
+        assert g.shape == w.shape and g.is_contiguous(memory_format=torch.channels_last)
+        assert torch.equal(g, w)
 
 
 @pytest.mark.gpu
