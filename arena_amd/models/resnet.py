@@ -8,9 +8,12 @@ one: a 7x7 stem, 4 stages of bottleneck blocks with the stride on the 3x3 conv (
 average pooling, and a 1000-way FC. ``width``/``depth`` knobs give tiny variants for CPU tests.
 
 MI355X layout: the model is meant to run with ``memory_format=torch.channels_last`` under bf16
-autocast. Every convolution is a ``Conv2dNHWC``: per shape and direction it runs the faster of
-the hand-written MFMA implicit-GEMM kernels (``csrc/ops/conv_kernels.hip``) and MIOpen. Each BatchNorm, with its ReLU
-and residual add, is one fused HIP kernel pair per direction (``arena_amd.ops.batchnorm``).
+autocast. Every convolution runs on the hand-written MFMA implicit-GEMM kernels
+(``csrc/ops/conv_kernels.hip``, tile autotuned per shape and direction): ``Conv2dNHWC`` for the
+bottleneck convs (stride-2 backward-data as phase convolutions), ``StemConv2d`` for the 7x7/2 stem
+in space-to-depth form. Each BatchNorm, with its ReLU and residual add, is one fused HIP kernel
+pair per direction (``arena_amd.ops.batchnorm``); its forward statistics come from the producing
+conv's epilogue.
 Parameters stay fp32 (master weights) for the data-parallel buckets and the optimizer.
 """
 from __future__ import annotations

@@ -7,9 +7,13 @@ spends half its step in convolutions. ``conv2d_fwd`` runs one on the gfx950 kern
     dX = conv(dY, W'),  W'[ci][r][s][co] = W[co][R-1-r][S-1-s][ci],  padding R-1-pad
 
 (``flip_weight``), so one tuned GEMM serves both directions. Shapes the kernel does not cover
-(C or Cout not a multiple of 64, e.g. the 3-channel stem) belong to MIOpen: ``kernel_ok`` says
-which. The variant picks the block's output tile (0: 128x128, 1: 128x64, 2: 64x128, 3: 64x64);
-``pick_variant`` is the fill-the-chip heuristic, ``Conv2dNHWC`` autotunes per shape.
+(C or Cout not a multiple of 64) fall back to MIOpen: ``kernel_ok`` says which. Strided
+backward-data runs as parity-class phase convolutions (``conv2d_bwd_data_strided``) and the
+3-channel 7x7/2 stem as a space-to-depth 4x4 convolution (``StemConv2d``), so a ResNet step needs
+no MIOpen convolution at all -- which matters for hipGraph capture (docs/perf.md "MIOpen inside a
+captured step"). The variant picks the block's output tile (0: 128x128, 1: 128x64, 2: 64x128,
+3: 64x64); ``pick_variant`` is the fill-the-chip heuristic, ``Conv2dNHWC`` autotunes per shape
+among the kernel variants (ARENA_CONV=miopen selects the library instead, for comparisons).
 """
 from __future__ import annotations
 
@@ -427,8 +431,10 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
         if stride == 1:
             for v in variants_for(cin):
                 t[("bwd", v)] = _time(lambda: conv2d_bwd_data(dy, w, pad, v))
-        else:   # phase decomposition, per-phase tile heuristic
-            t[("bwd", -1)] = 0.0
+        else:   # phase decomposition: per-phase heuristic (-1) or one tile for every phase
+            hw = (x.shape[2], x.shape[3])
+            for v in [-1] + variants_for(cin):
+                t[("bwd", v)] = _time(lambda: conv2d_bwd_data_strided(dy, w, hw, stride, pad, v))
         for c in wg:
             t[("wgrad", c)] = _time(lambda: conv2d_wgrad(x, dy, k, stride, pad, c[0], c[1]))
         for kind in ("fwd", "bwd", "wgrad"):
