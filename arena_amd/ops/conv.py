@@ -26,6 +26,8 @@ from . import _ext
 
 Tensor = torch.Tensor
 TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
+# + 4: three-stage K pipeline; + 8: single stage buffer, serial K loop, high occupancy
+TILES.update({v + d: t for v, t in list(TILES.items()) for d in (4, 8)})
 _CUS = 256
 
 

@@ -874,14 +874,14 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
   TORCH_CHECK(C % 64 == 0 && Cout % 64 == 0, "conv_fwd: C and Cout must be multiples of 64");
   TORCH_CHECK(stride >= 1 && pad >= 0 && H + 2 * pad >= R && W + 2 * pad >= S,
               "conv_fwd: bad stride/padding");
-  TORCH_CHECK(variant >= 0 && variant <= 3 && ((variant & 1) || Cout % 128 == 0),
+  TORCH_CHECK(variant >= 0 && variant <= 11 && ((variant & 1) || Cout % 128 == 0),
               "conv_fwd: variant ", variant, " needs Cout % 128 == 0");
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_fwd: too many output pixels");
   Tensor y = torch::empty({N, Cout, Ho, Wo},
                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
   static const int bm[4] = {128, 128, 64, 64};
-  const int64_t m_tiles = (N * Ho * Wo + bm[variant] - 1) / bm[variant];
+  const int64_t m_tiles = (N * Ho * Wo + bm[variant & 3] - 1) / bm[variant & 3];
   Tensor part = with_stats ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
                            : Tensor();
   if (addend.has_value()) {
@@ -990,7 +990,7 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
   TORCH_CHECK(w.size(1) == C, "conv_fwd_ex: weight/input channel mismatch");
   TORCH_CHECK(Cout % 64 == 0 && (c16 ? (C == 16 && S % 4 == 0) : C % 64 == 0),
               "conv_fwd_ex: Cout % 64, and C % 64 (or C == 16, S % 4 == 0 in c16 mode)");
-  TORCH_CHECK(variant >= 0 && variant <= 3 && ((variant & 1) || Cout % 128 == 0),
+  TORCH_CHECK(variant >= 0 && variant <= 11 && ((variant & 1) || Cout % 128 == 0),
               "conv_fwd_ex: bad variant");
   TORCH_CHECK(stride >= 1 && Ho >= 1 && Wo >= 1, "conv_fwd_ex: bad geometry");
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_fwd_ex: too many output pixels");
@@ -1024,7 +1024,7 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
                 "conv_fwd_ex: addend must be shaped like the output tensor");
   }
   static const int bm[4] = {128, 128, 64, 64};
-  const int64_t m_tiles = (N * Ho * Wo + bm[variant] - 1) / bm[variant];
+  const int64_t m_tiles = (N * Ho * Wo + bm[variant & 3] - 1) / bm[variant & 3];
   TORCH_CHECK(!(with_stats && y_out.has_value()), "conv_fwd_ex: statistics need a dense output");
   Tensor part = with_stats ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
                            : Tensor();

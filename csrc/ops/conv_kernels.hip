@@ -31,6 +31,7 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -72,6 +73,10 @@ struct ConvArgs {
   // data): each output pixel also stores its osh*osw - 1 sibling pixels of the [Hy][Wy] image,
   // which receive no taps -- the addend there (add != null) or zero. One pass writes all of dX.
   int fill_sib;
+  // coal: stage the output tile through LDS (fp32, half a tile at a time) and store whole 16-byte
+  // chunks with consecutive lanes on consecutive chunks of a pixel row (the MFMA layout alone
+  // stores 8 bytes per lane, 16 rows per instruction). Needed off only for EPI != 0 with an addend.
+  int coal;
   // c16: C == 16 and a 64-deep K step is one filter row and FOUR consecutive filter columns
   // (4 pixels x 16 channels = 128 contiguous bytes of an NHWC row). S is a multiple of 4. The
   // space-to-depth form of the 7x7/2 stem runs on it.
@@ -113,7 +118,7 @@ __device__ __forceinline__ float row16_sum(float v) {
 // EPI: 0 = plain, 1 = BatchNorm statistics of Y (forward), 2 = BatchNorm-backward partials of Y
 // (see ConvArgs::bnx).
 template <int BM, int BN, int EPI, int NBUF = 2>
-__global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
+__device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
   constexpr int WM = BM / 2, WN = BN / 2;        // per-wave output tile (2 x 2 waves)
   constexpr int MI = WM / 16, NI = WN / 16;      // 16x16 MFMA tiles per wave
   constexpr int AI = BM * 8 / kThreads;          // A staging instructions per thread
@@ -206,14 +211,8 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
   const int fr = lane & 15, fq = lane >> 4;
   const int T = a.Ktot / kBK;
 
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int t = 0; t < T; ++t) {
-    const int cur = NBUF == 1 ? 0 : (t & 1);
-    if (NBUF == 2 && t + 1 < T) stage(t + 1, cur ^ 1);
-    const uint8_t* abuf = lds + cur * kBufBytes;
+  auto compute = [&](int buf) {
+    const uint8_t* abuf = lds + buf * kBufBytes;
     const uint8_t* bbuf = abuf + BM * kRowBytes;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -235,8 +234,52 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
+  };
+
+  if constexpr (NBUF == 3) {
+    // Three stage buffers, two K steps in flight: the glds of step t+2 stay outstanding across
+    // the barrier that publishes step t+1 (counted vmcnt = this thread's glds of ONE stage, raw
+    // s_barrier: __syncthreads() would drain every outstanding LDS-DMA with a vmcnt(0)).
+    // RAW: stage t+1 is read in iteration t+1, after the vmcnt that retired it and a barrier.
+    // WAR: stage t+2 overwrites buffer (t-1)%3, whose reads finished before iteration t-1's barrier.
+    constexpr int kLps = AI + BI;   // glds per thread per stage
+    stage(0, 0);
+    if (T > 1) {
+      stage(1, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLps) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    int cur = 0;
+    for (int t = 0; t < T; ++t) {
+      if (t + 2 < T) stage(t + 2, cur == 0 ? 2 : cur - 1);
+      compute(cur);
+      if (t + 2 < T)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kLps) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      cur = cur == 2 ? 0 : cur + 1;
+    }
+  } else {
+    stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+
+    for (int t = 0; t < T; ++t) {
+      const int cur = NBUF == 1 ? 0 : (t & 1);
+      if (NBUF == 2 && t + 1 < T) stage(t + 1, cur ^ 1);
+      compute(cur);
+      if (NBUF == 1 && t + 1 < T) {   // serial: every wave is done with the buffer, restage it
+        __syncthreads();
+        stage(t + 1, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: lane holds channels n0+wn*WN+j*16+4*fq .. +3 of pixel m0+wm*WM+i*16+fr ----
@@ -260,6 +303,73 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
     for (int j = 0; j < NI; ++j)
       bmu[j] = *reinterpret_cast<const float4*>(a.bnmean + n0 + wn * WN + j * 16 + 4 * fq);
   }
+  if (a.coal && !(EPI != 0 && a.add != nullptr)) {
+    // ---- coalesced store through LDS (stage buffers are free: the K loop ended on a barrier) ----
+    float* stg = reinterpret_cast<float*>(lds);
+    constexpr int F4R = BN / 4;   // float4 slots per staged row (>= 16: the XOR below stays inside)
+    constexpr int CPR = BN / 8;   // 16-byte bf16 output chunks per row
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (h) __syncthreads();     // every reader of the first half is done
+      if (wm == h) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int row = i * 16 + fr;
+#pragma unroll
+          for (int j = 0; j < NI; ++j) {
+            const int slot = (wn * WN + j * 16) / 4 + fq;
+            *reinterpret_cast<f32x4v*>(stg + (row * F4R + (slot ^ (row & 7))) * 4) = acc[i][j];
+          }
+        }
+      }
+      __syncthreads();
+      for (int q = tid; q < WM * CPR; q += kThreads) {
+        const int row = q / CPR, cc = q - row * CPR;
+        const int m = m0 + h * WM + row;
+        if (m >= a.M) continue;
+        const f32x4v lo = *reinterpret_cast<const f32x4v*>(stg + (row * F4R + ((2 * cc) ^ (row & 7))) * 4);
+        const f32x4v hi =
+            *reinterpret_cast<const f32x4v*>(stg + (row * F4R + ((2 * cc + 1) ^ (row & 7))) * 4);
+        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+        size_t pix = (size_t)m;
+        int n = 0, ho = 0, wo = 0;
+        if (a.mapped) {
+          const int hw = a.Ho * a.Wo;
+          n = m / hw;
+          const int rem = m - n * hw;
+          ho = rem / a.Wo;
+          wo = rem - ho * a.Wo;
+          pix = ((size_t)n * a.Hy + ho * a.osh + a.ooh) * a.Wy + wo * a.osw + a.oow;
+        }
+        const size_t off = pix * a.Cout + n0 + cc * 8;
+        if (a.add != nullptr) {
+          const uint4 qa = *reinterpret_cast<const uint4*>(a.add + off);
+          const uint32_t u[4] = {qa.x, qa.y, qa.z, qa.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            v[2 * e] += __uint_as_float(u[e] << 16);
+            v[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
+          }
+        }
+        *reinterpret_cast<uint4*>(a.y + off) =
+            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                       pack_bf16x2(v[6], v[7]));
+        if (a.fill_sib) {
+          for (int da = 0; da < a.osh; ++da) {
+            const int hy = ho * a.osh + da;
+            if (hy >= a.Hy) break;
+            for (int db = 0; db < a.osw; ++db) {
+              const int wy = wo * a.osw + db;
+              if ((da == 0 && db == 0) || wy >= a.Wy) continue;
+              const size_t so = (((size_t)n * a.Hy + hy) * a.Wy + wy) * a.Cout + n0 + cc * 8;
+              *reinterpret_cast<uint4*>(a.y + so) =
+                  a.add ? *reinterpret_cast<const uint4*>(a.add + so) : make_uint4(0u, 0u, 0u, 0u);
+            }
+          }
+        }
+      }
+    }
+  } else {
 #pragma unroll
   for (int i = 0; i < MI; ++i) {
     const int m = m0 + wm * WM + i * 16 + fr;
@@ -312,6 +422,7 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
       v.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
       *reinterpret_cast<uint2*>(yrow + j * 16) = v;
     }
+  }
   }
   if constexpr (EPI == 2) {
     // per channel over the tile's valid rows: sum g, sum g * (x - mean), g = stored dY * mask
@@ -408,19 +519,42 @@ __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
   }
 }
 
+template <int BM, int BN, int EPI, int NBUF>
+__global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
+  conv_fwd_body<BM, BN, EPI, NBUF>(a);
+}
+
+// Single stage buffer (one K step -- 1x1 over 64 channels -- or the serial variants 8..11): the
+// shapes that want it are bound by streaming the output, so it trades registers for occupancy --
+// four waves per SIMD (<= 128 VGPRs) instead of two, up to five blocks per CU by LDS.
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+void conv_fwd_kernel_occ4(ConvArgs a) {
+  conv_fwd_body<BM, BN, EPI, 1>(a);
+}
+
 template <int BM, int BN>
-hipError_t launch(const ConvArgs& a0, hipStream_t st) {
+hipError_t launch(const ConvArgs& a0, int pipe, hipStream_t st) {
   ConvArgs a = a0;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
-  const bool one = a.Ktot == kBK;  // a single K step: no second stage buffer
+  // stage buffers: pipe 0 (variants 0..3) two, pipe 1 (4..7) three, pipe 2 (8..11) one (serial,
+  // high occupancy); a single K step always one
+  const int nb = a.Ktot == kBK || pipe == 2 ? 1 : (pipe == 1 ? 3 : 2);
   const int epi = a.part == nullptr ? 0 : (a.bnx != nullptr ? 2 : 1);
 #define ARENA_CONV_LAUNCH(E, NB) \
   hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, E, NB>), dim3(nwg), dim3(kThreads), 0, st, a)
-  if (epi == 0) { if (one) ARENA_CONV_LAUNCH(0, 1); else ARENA_CONV_LAUNCH(0, 2); }
-  else if (epi == 1) { if (one) ARENA_CONV_LAUNCH(1, 1); else ARENA_CONV_LAUNCH(1, 2); }
-  else { if (one) ARENA_CONV_LAUNCH(2, 1); else ARENA_CONV_LAUNCH(2, 2); }
+#define ARENA_CONV_NB(E) \
+  do { if (nb == 1 && (E == 0 || BM * BN < 128 * 128)) /* fits 128 VGPRs without spills */ \
+         hipLaunchKernelGGL((conv_fwd_kernel_occ4<BM, BN, E>), dim3(nwg), dim3(kThreads), 0, st, a); \
+       else if (nb == 1) ARENA_CONV_LAUNCH(E, 1); \
+       else if (nb == 2) ARENA_CONV_LAUNCH(E, 2); \
+       else ARENA_CONV_LAUNCH(E, 3); } while (0)
+  if (epi == 0) ARENA_CONV_NB(0);
+  else if (epi == 1) ARENA_CONV_NB(1);
+  else ARENA_CONV_NB(2);
+#undef ARENA_CONV_NB
 #undef ARENA_CONV_LAUNCH
   return hipGetLastError();
 }
@@ -431,7 +565,9 @@ extern "C" {
 
 // Returns hipErrorInvalidValue for shapes the kernel does not cover (the caller falls back to
 // MIOpen): C % 64 != 0, Cout % 64 != 0, or an unknown tile variant.
-// variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (BM x BN output tile per block).
+// variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (BM x BN output tile per block);
+// variant + 4: the same tile with a three-stage K pipeline (two glds steps in flight);
+// variant + 8: one stage buffer, serial K loop, high occupancy (streaming-bound 1x1 shapes).
 // part (optional): BatchNorm partials of y, [ceil(M / BM)][2][Cout] (EPI 1 / EPI 2 epilogues).
 // General form. pad_h/pad_w: top/left padding; Ho/Wo: output size (<= 0: derived from a symmetric
 // padding); y_map {Hy, Wy, osh, osw, ooh, oow, fill_sib} (null: dense output); c16, fill_sib:
@@ -462,6 +598,11 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.Wo = Wo > 0 ? Wo : (W + 2 * pad_w - S) / stride + 1;
   if (a.Ho <= 0 || a.Wo <= 0) return hipErrorInvalidValue;
   a.c16 = c16;
+  static const int coal = [] {
+    const char* e = getenv("ARENA_CONV_COAL");
+    return e == nullptr || e[0] != '0' ? 1 : 0;
+  }();
+  a.coal = coal;
   if (y_map != nullptr) {
     a.mapped = 1;
     a.Hy = y_map[0]; a.Wy = y_map[1]; a.osh = y_map[2]; a.osw = y_map[3];
@@ -478,11 +619,13 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   if (M >= (1LL << 31) || (long long)N * H * W * C >= (1LL << 40)) return hipErrorInvalidValue;
   a.M = (int)M;
   a.Ktot = R * S * C;
-  switch (variant) {
-    case 0: return Cout % 128 ? hipErrorInvalidValue : launch<128, 128>(a, st);
-    case 1: return launch<128, 64>(a, st);
-    case 2: return Cout % 128 ? hipErrorInvalidValue : launch<64, 128>(a, st);
-    case 3: return launch<64, 64>(a, st);
+  if (variant < 0 || variant > 11) return hipErrorInvalidValue;
+  const int pipe = variant >> 2;
+  switch (variant & 3) {
+    case 0: return Cout % 128 ? hipErrorInvalidValue : launch<128, 128>(a, pipe, st);
+    case 1: return launch<128, 64>(a, pipe, st);
+    case 2: return Cout % 128 ? hipErrorInvalidValue : launch<64, 128>(a, pipe, st);
+    case 3: return launch<64, 64>(a, pipe, st);
     default: return hipErrorInvalidValue;
   }
 }
