@@ -291,6 +291,7 @@ class GradJoin:
 
 
 WGRAD_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}   # Cout x R*S*C
+WGRAD_TILES.update({v + 4: t for v, t in list(WGRAD_TILES.items())})   # + 4: serial
 
 
 def wgrad_variants_for(cin: int, cout: int):
@@ -636,12 +637,44 @@ class StemConv2d(Conv2dNHWC):
         if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or not stem_ok(x, w, s, p):
             return super().forward_stats(x, want_stats, join, bn_link)
         x = x.contiguous(memory_format=torch.channels_last)
-        ho, wo = x.shape[2] // 2, x.shape[3] // 2
-        fv = pick_variant(x.shape[0] * ho * wo, w.shape[0])
-        fv = fv if TILES[fv][1] == 64 else 1          # c16 needs a 64-wide output tile
         want = want_stats and torch.is_grad_enabled() and self.training
         with torch.autocast("cuda", enabled=False):
             z = _ext.load().s2d_stem(x)
             w16 = stem_weight(w)
-            y, part = _StemFn.apply(z, w16, want, fv, (3, 0))
+            fv, wcfg = _stem_plan(z, w16)
+            y, part = _StemFn.apply(z, w16, want, fv, wcfg)
         return y, ((part, TILES[fv][0]) if want else None)
+
+
+_STEM_PLANS: Dict[tuple, Tuple[int, Tuple[int, int]]] = {}
+
+
+def _stem_plan(z: Tensor, w16: Tensor) -> Tuple[int, Tuple[int, int]]:
+    """(forward tile variant, (wgrad variant, splits)) of the c16 stem convolution: the fastest
+    of the 64-wide tiles (c16 needs BN = 64) and wgrad forms, timed once per shape like
+    ``plan_for`` (heuristic under ARENA_CONV=ours or while a graph is being captured)."""
+    key = (tuple(z.shape), tuple(w16.shape), z.device.index, _mode())
+    plan = _STEM_PLANS.get(key)
+    if plan is not None:
+        return plan
+    ext = _ext.load()
+    ho, wo = z.shape[2], z.shape[3]
+    fvs = [v for v in variants_for(w16.shape[0]) if TILES[v][1] == 64]
+    wcs = [(3, 0), (7, 0)]
+    if _mode() == "ours" or torch.cuda.is_current_stream_capturing():
+        fv = pick_variant(z.shape[0] * ho * wo, w16.shape[0])
+        plan = (fv if TILES[fv][1] == 64 else 1, wcs[0])
+        if _mode() == "ours":
+            _STEM_PLANS[key] = plan
+        return plan
+    tf = {v: _time(lambda: ext.conv_fwd_ex(z, w16, 1, 2, 2, ho, wo, v, True, None, None, [],
+                                            True)) for v in fvs}
+    dy = torch.randn(z.shape[0], w16.shape[0], ho, wo, device=z.device, dtype=z.dtype).contiguous(
+        memory_format=torch.channels_last)
+    tw = {c: _time(lambda: ext.conv_wgrad_ex(z, dy, 4, 4, 1, 2, 2, c[0], c[1], False, 1.0, True))
+          for c in wcs}
+    plan = (min(tf, key=tf.get), min(tw, key=tw.get))
+    _STEM_PLANS[key] = plan
+    if os.environ.get("ARENA_CONV_LOG") == "1":
+        print(f"stem {tuple(z.shape)}: fwd={plan[0]} wgrad={plan[1]} {tf} {tw}", flush=True)
+    return plan

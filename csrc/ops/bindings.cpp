@@ -1056,8 +1056,9 @@ Tensor conv_wgrad_ex(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, 
   const int64_t Cout = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
   TORCH_CHECK(dy.size(0) == N && R >= 1 && S >= 1 && stride >= 1, "conv_wgrad_ex: bad geometry");
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  TORCH_CHECK(variant >= 0 && variant <= 3 && Cout % bm[variant] == 0 &&
-                  (c16 ? (C == 16 && S % 4 == 0 && bn[variant] == 64) : C % bn[variant] == 0),
+  TORCH_CHECK(variant >= 0 && variant <= 7 && Cout % bm[variant & 3] == 0 &&
+                  (c16 ? (C == 16 && S % 4 == 0 && bn[variant & 3] == 64)
+                       : C % bn[variant & 3] == 0),
               "conv_wgrad_ex: variant ", variant, " does not fit C=", C, " Cout=", Cout);
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad_ex: too many output pixels");
   const int64_t Ktot = R * S * C;
@@ -1112,9 +1113,10 @@ Tensor conv_wgrad(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int
   TORCH_CHECK(dy.size(0) == N && dy.size(2) == Ho && dy.size(3) == Wo,
               "conv_wgrad: dy shape does not match the convolution geometry");
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  TORCH_CHECK(variant >= 0 && variant <= 3, "conv_wgrad: variant must be 0..3");
-  TORCH_CHECK(C % bn[variant] == 0 && Cout % bm[variant] == 0, "conv_wgrad: variant ", variant,
-              " needs C % ", bn[variant], " == 0 and Cout % ", bm[variant], " == 0");
+  TORCH_CHECK(variant >= 0 && variant <= 7, "conv_wgrad: variant must be 0..7");
+  TORCH_CHECK(C % bn[variant & 3] == 0 && Cout % bm[variant & 3] == 0, "conv_wgrad: variant ",
+              variant, " needs C % ", bn[variant & 3], " == 0 and Cout % ", bm[variant & 3],
+              " == 0");
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad: too many output pixels");
   const int64_t Ktot = R * S * C;
   const int splits = arena_conv_wgrad_splits((int)N, (int)Ho, (int)Wo, (int)Cout, (int)Ktot,

@@ -840,15 +840,17 @@ __device__ __forceinline__ int wswz(int row) {
   else return 2 * (((row >> 1) & 1) | (((row >> 3) & 1) << 1));
 }
 
-template <int BM, int BN>
-__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
+// NBUF 2: double-buffered pixel steps; NBUF 1 (variants 4..7): one buffer, serial steps, four
+// waves per SIMD -- more blocks per CU hide the staging latency instead (see conv_fwd_kernel_occ4).
+template <int BM, int BN, int NBUF>
+__device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
   constexpr int RA = BM * 2, RBB = BN * 2;        // row bytes of the A (dY) and B (X) images
   constexpr int CA = RA / 16, CB = RBB / 16;       // 16-byte chunks per row
   constexpr int kPix = 64;                         // pixels per step
   constexpr int AI = kPix * CA / kThreads, BI = kPix * CB / kThreads;
   constexpr int kBuf = kPix * (RA + RBB);
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[2 * kBuf];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = a.m_tiles * a.n_tiles;
@@ -932,8 +934,8 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
     __syncthreads();
   }
   for (int t = 0; t < nsteps; ++t) {
-    const int cur = t & 1;
-    if (t + 1 < nsteps) stage(t + 1, cur ^ 1);
+    const int cur = NBUF == 1 ? 0 : (t & 1);
+    if (NBUF == 2 && t + 1 < nsteps) stage(t + 1, cur ^ 1);
     const uint8_t* abuf = lds + cur * kBuf;
     const uint8_t* bbuf = abuf + kPix * RA;
 #pragma unroll
@@ -965,6 +967,10 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
         for (int j = 0; j < NI; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+    if (NBUF == 1 && t + 1 < nsteps) {   // serial: every wave is done with the buffer
+      __syncthreads();
+      stage(t + 1, 0);
+    }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
@@ -982,6 +988,17 @@ __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
         slab[(size_t)co * a.Ktot + col] = acc[i][j][r];
       }
     }
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
+  conv_wgrad_body<BM, BN, 2>(a);
+}
+
+template <int BM, int BN>
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
+void conv_wgrad_kernel_occ4(WgradArgs a) {
+  conv_wgrad_body<BM, BN, 1>(a);
 }
 
 // out = sum over splits of ws, bf16 and/or fp32. Thread (col, grp) of a block sums float4 column
@@ -1045,7 +1062,7 @@ FastDiv make_fastdiv(uint32_t d) {
 }
 
 template <int BM, int BN>
-hipError_t launch_wgrad(WgradArgs a, int splits_hint, hipStream_t st) {
+hipError_t launch_wgrad(WgradArgs a, int splits_hint, bool serial, hipStream_t st) {
   a.m_tiles = a.Cout / BM;
   a.n_tiles = a.Ktot / BN;
   const int tiles = a.m_tiles * a.n_tiles;
@@ -1054,8 +1071,12 @@ hipError_t launch_wgrad(WgradArgs a, int splits_hint, hipStream_t st) {
   splits = std::min(splits, total);
   a.sps = (total + splits - 1) / splits;
   a.splits = (total + a.sps - 1) / a.sps;
-  hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN>), dim3(tiles * a.splits), dim3(kThreads), 0, st,
-                     a);
+  if (serial)
+    hipLaunchKernelGGL((conv_wgrad_kernel_occ4<BM, BN>), dim3(tiles * a.splits), dim3(kThreads), 0,
+                       st, a);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN>), dim3(tiles * a.splits), dim3(kThreads), 0, st,
+                       a);
   return hipGetLastError();
 }
 
@@ -1067,8 +1088,8 @@ extern "C" {
 int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int variant,
                             int splits_hint) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (variant < 0 || variant > 3) return -1;
-  const int tiles = (Cout / bm[variant]) * (Ktot / bn[variant]);
+  if (variant < 0 || variant > 7) return -1;
+  const int tiles = (Cout / bm[variant & 3]) * (Ktot / bn[variant & 3]);
   const long long M = (long long)N * Ho * Wo;
   const int total = (int)((M + 63) / 64);
   int splits = splits_hint > 0 ? splits_hint : std::max(1, (1024 + tiles / 2) / tiles);
@@ -1077,7 +1098,8 @@ int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int varia
   return (total + sps - 1) / sps;
 }
 
-// variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (Cout x R*S*C tile). Needs C % BN == 0
+// variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (Cout x R*S*C tile); + 4: serial
+// single-buffer high-occupancy form of the same tile. Needs C % BN == 0
 // (a tile never straddles two filter taps) and Cout % BM == 0; c16 mode: C == 16, S % 4 == 0 and
 // BN == 64 (variants 1 and 3). Ho/Wo <= 0: derived from a symmetric padding.
 hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* dw_bf16,
@@ -1085,10 +1107,11 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
                                int stride, int pad_h, int pad_w, int Ho, int Wo, int c16,
                                int variant, int splits_hint, float scale, hipStream_t st) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (variant < 0 || variant > 3) return hipErrorInvalidValue;
-  if (c16 ? (C != 16 || S % 4 || bn[variant] != 64) : (C % bn[variant] != 0))
-    return hipErrorInvalidValue;
-  if (Cout % bm[variant] || N <= 0 || stride <= 0) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 7) return hipErrorInvalidValue;
+  const int tv = variant & 3;
+  const bool serial = variant >= 4;
+  if (c16 ? (C != 16 || S % 4 || bn[tv] != 64) : (C % bn[tv] != 0)) return hipErrorInvalidValue;
+  if (Cout % bm[tv] || N <= 0 || stride <= 0) return hipErrorInvalidValue;
   WgradArgs a{};
   a.x = (const uint16_t*)x;
   a.dy = (const uint16_t*)dy;
@@ -1105,11 +1128,11 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
   a.div_hw = make_fastdiv((uint32_t)(a.Ho * a.Wo));
   a.div_w = make_fastdiv((uint32_t)a.Wo);
   hipError_t e;
-  switch (variant) {
-    case 0: e = launch_wgrad<128, 128>(a, splits_hint, st); break;
-    case 1: e = launch_wgrad<128, 64>(a, splits_hint, st); break;
-    case 2: e = launch_wgrad<64, 128>(a, splits_hint, st); break;
-    default: e = launch_wgrad<64, 64>(a, splits_hint, st); break;
+  switch (tv) {
+    case 0: e = launch_wgrad<128, 128>(a, splits_hint, serial, st); break;
+    case 1: e = launch_wgrad<128, 64>(a, splits_hint, serial, st); break;
+    case 2: e = launch_wgrad<64, 128>(a, splits_hint, serial, st); break;
+    default: e = launch_wgrad<64, 64>(a, splits_hint, serial, st); break;
   }
   if (e != hipSuccess) return e;
   const int splits = arena_conv_wgrad_splits(N, a.Ho, a.Wo, Cout, a.Ktot, variant, splits_hint);

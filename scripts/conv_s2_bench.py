@@ -75,7 +75,7 @@ def main():
     res["miopen_wgrad_us"] = round(timeit(lambda: torch.ops.aten.convolution_backward(
         dy, x, wb, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1, [False, True, False]),
         args.reps), 1)
-    for v in (3,):
+    for v in (3, 7):
         for sp in (0, 64, 128, 256):
             res[f"ours_wgrad_v{v}_s{sp}_us"] = round(timeit(lambda: ext.conv_wgrad_ex(
                 z, dy, 4, 4, 1, 2, 2, v, sp, False, 1.0, True), args.reps), 1)
