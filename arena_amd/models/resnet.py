@@ -24,7 +24,7 @@ import torch
 from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d
-from ..ops.conv import BNGradLink, Conv2dNHWC, GradJoin, StemConv2d
+from ..ops.conv import BNGradLink, Conv2dNHWC, GradJoin, StemConv2d, WeightFlipper
 from ..ops.pool import MaxPool2dNHWC
 
 DEPTHS = {"resnet50": [3, 4, 6, 3], "resnet101": [3, 4, 23, 3],
@@ -94,15 +94,18 @@ class ResNet(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        # every stride-1 conv weight flipped for its backward-data pass in one launch per step
+        self._flipper = WeightFlipper(list(self.layers.modules()))
 
     def forward(self, x):
-        y, st = self.stem[0].forward_stats(x)        # epilogue BN statistics, as in the blocks
-        x = self.stem[2](self.stem[1](y, stats=st))
-        link = None
-        for blk in self.layers:
-            out_link = BNGradLink() if torch.is_grad_enabled() else None
-            x = blk(x, link=link, link_out=out_link)
-            link = out_link
+        with self._flipper.scope():
+            y, st = self.stem[0].forward_stats(x)    # epilogue BN statistics, as in the blocks
+            x = self.stem[2](self.stem[1](y, stats=st))
+            link = None
+            for blk in self.layers:
+                out_link = BNGradLink() if torch.is_grad_enabled() else None
+                x = blk(x, link=link, link_out=out_link)
+                link = out_link
         return self.fc(torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1))
 
 

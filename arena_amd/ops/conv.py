@@ -99,12 +99,14 @@ def flip_weight(w: Tensor) -> Tensor:
 
 
 def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1,
-                    addend: Tensor | None = None, bn=None):
+                    addend: Tensor | None = None, bn=None, wflip: Tensor | None = None):
     """dX (+ addend) of a stride-1 convolution (same spatial size when pad = (R-1)/2).
     With ``bn`` (see conv2d_fwd) returns (dX, (part, rpb)): the backward partials of the
-    BatchNorm layer whose output is this convolution's input."""
+    BatchNorm layer whose output is this convolution's input. ``wflip``: ``flip_weight(w)``
+    computed ahead of time (``WeightFlipper``)."""
     r = w.shape[2]
-    return conv2d_fwd(dy, flip_weight(w), 1, r - 1 - pad, variant, addend=addend, bn=bn)
+    wf = wflip if wflip is not None else flip_weight(w)
+    return conv2d_fwd(dy, wf, 1, r - 1 - pad, variant, addend=addend, bn=bn)
 
 
 # Off by default: on ResNet-50 bs128 the heavier dgrad epilogue cost more than the reduction pass
@@ -494,6 +496,84 @@ def plans() -> Dict[tuple, ConvPlan]:
     return dict(_PLANS)
 
 
+# ------------------------------------------------------------------------------------------------
+# Flipped weights for a whole model in one launch. Every stride-1 backward-data pass on the kernel
+# runs on W' = flip_weight(W): one transpose launch per conv per step (49 in a ResNet-50 step,
+# ~5 us each). ``WeightFlipper.scope()`` wraps a model's training forward: it flips every eligible
+# weight in ONE conv_flip_multi launch into persistent buffers, and the convolutions that run
+# inside the scope hand their flipped copy to their backward (ctx). The weights cannot change
+# between that forward and its backward, and nothing outside the scope ever reads the buffers, so
+# a copy is never stale. Under hipGraph capture the launch is part of the captured forward.
+# ------------------------------------------------------------------------------------------------
+_ACTIVE_FLIPS: Optional[Dict[int, Tensor]] = None
+
+
+def _flip_eligible(w: Tensor) -> bool:
+    return (w.is_cuda and w.dim() == 4 and w.dtype == torch.bfloat16
+            and w.is_contiguous(memory_format=torch.channels_last) and w.shape[0] % 64 == 0
+            and w.shape[1] % 64 == 0 and w.shape[2] * w.shape[3] <= 64)
+
+
+class WeightFlipper:
+    """Pre-flips the weights of a model's stride-1 ``Conv2dNHWC`` layers for their backward-data
+    passes (see above). bf16 channels_last weights only (master-weight training); with fp32
+    weights under autocast each conv casts and flips its own weight as before."""
+
+    def __init__(self, modules):
+        self.convs = [m for m in modules if type(m) is Conv2dNHWC and m.stride[0] == 1]
+        self._key = None
+        self._src: list = []
+        self._dst: list = []
+
+    def scope(self):
+        return _FlipScope(self)
+
+    def _prepare(self):
+        if _mode() in ("off", MIOPEN) or not torch.is_grad_enabled():
+            return None
+        ws = [m.weight for m in self.convs if m.training and _flip_eligible(m.weight)]
+        if not ws:
+            return None
+        key = tuple((w.data_ptr(), tuple(w.shape)) for w in ws)
+        if key != self._key:
+            self._src = ws
+            self._dst = [torch.empty(w.shape[1], w.shape[0], w.shape[2], w.shape[3],
+                                     device=w.device, dtype=w.dtype,
+                                     memory_format=torch.channels_last) for w in ws]
+            self._key = key
+        _ext.load().conv_flip_multi(self._src, self._dst)
+        return {w.data_ptr(): d for w, d in zip(self._src, self._dst)}
+
+
+class _FlipScope:
+    def __init__(self, flipper: WeightFlipper):
+        self.flipper = flipper
+        self.prev = None
+
+    def __enter__(self):
+        global _ACTIVE_FLIPS
+        self.prev = _ACTIVE_FLIPS
+        flips = self.flipper._prepare()
+        if flips is not None:
+            _ACTIVE_FLIPS = flips
+        return self
+
+    def __exit__(self, *exc):
+        global _ACTIVE_FLIPS
+        _ACTIVE_FLIPS = self.prev
+        return False
+
+
+def _active_flip(w: Tensor) -> Optional[Tensor]:
+    if _ACTIVE_FLIPS is None:
+        return None
+    wf = _ACTIVE_FLIPS.get(w.data_ptr())
+    if wf is None or wf.shape[0] != w.shape[1] or wf.shape[1] != w.shape[0] \
+            or wf.shape[2:] != w.shape[2:]:
+        return None
+    return wf
+
+
 class _nullctx:
     def __enter__(self):
         return None
@@ -514,6 +594,8 @@ class _ConvFn(torch.autograd.Function):
             y = conv2d_fwd(x, w, stride, pad, plan.fwd)
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pad, plan)
+        # W' of a WeightFlipper scope (flipped this step, before this forward)
+        ctx.wflip = _active_flip(w) if (stride == 1 and plan.bwd != MIOPEN) else None
         ctx.join = join.register() if join is not None else None
         ctx.bn_link = bn_link if (bn_link is not None and bn_link.ready()) else None
         ctx.mark_non_differentiable(part)
@@ -547,10 +629,10 @@ class _ConvFn(torch.autograd.Function):
                                              plan.bwd, addend=other)
             elif use_bn:
                 dx, (part, rpb) = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other,
-                                                  bn=(lk.x, lk.mask, lk.mean))
+                                                  bn=(lk.x, lk.mask, lk.mean), wflip=ctx.wflip)
                 lk.publish(part, rpb, dx)
             else:
-                dx = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other)
+                dx = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other, wflip=ctx.wflip)
             if join is not None and join.park_or_take(dx):
                 dx = None
         if ctx.needs_input_grad[1]:

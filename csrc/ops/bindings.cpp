@@ -52,6 +52,8 @@ hipError_t arena_conv_fwd(const void*, const void*, void*, float*, const void*, 
                           const uint8_t*, const float*, int, int, int, int, int, int, int, int,
                           int, int, hipStream_t);
 hipError_t arena_conv_flip_weight(const void*, void*, int, int, int, int, hipStream_t);
+hipError_t arena_conv_flip_multi(int, const void* const*, void* const*, const int*, const int*,
+                                 const int*, hipStream_t);
 hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void*, const void*,
                              const uint8_t*, const float*, int, int, int, int, int, int, int, int,
                              int, int, int, int, const int*, int, int, hipStream_t);
@@ -934,6 +936,40 @@ Tensor conv_flip_weight(Tensor w) {
   return wt;
 }
 
+// conv_flip_weight for many weights in one launch per 64 tensors, into caller-owned outputs
+// (dst[i]: channels_last [C, Cout, R, S] of src[i]'s shape).
+void conv_flip_multi(std::vector<Tensor> src, std::vector<Tensor> dst) {
+  TORCH_CHECK(src.size() == dst.size(), "conv_flip_multi: src and dst lengths differ");
+  std::vector<const void*> sp;
+  std::vector<void*> dp;
+  std::vector<int> co, ci, rs;
+  for (size_t i = 0; i < src.size(); ++i) {
+    const Tensor& w = src[i];
+    const Tensor& d = dst[i];
+    TORCH_CHECK(w.is_cuda() && w.dim() == 4 && w.scalar_type() == torch::kBFloat16 &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_flip_multi: src must be channels_last bf16 GPU tensors [Cout, C, R, S]");
+    TORCH_CHECK(d.is_cuda() && d.scalar_type() == torch::kBFloat16 && d.dim() == 4 &&
+                    d.size(0) == w.size(1) && d.size(1) == w.size(0) && d.size(2) == w.size(2) &&
+                    d.size(3) == w.size(3) && d.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    d.get_device() == w.get_device(),
+                "conv_flip_multi: dst must be a channels_last bf16 [C, Cout, R, S] tensor");
+    TORCH_CHECK(w.size(0) % 64 == 0 && w.size(1) % 64 == 0 && w.size(2) * w.size(3) <= 64,
+                "conv_flip_multi: C and Cout must be multiples of 64, R*S <= 64");
+    sp.push_back(w.data_ptr());
+    dp.push_back(d.data_ptr());
+    co.push_back((int)w.size(0));
+    ci.push_back((int)w.size(1));
+    rs.push_back((int)(w.size(2) * w.size(3)));
+  }
+  for (size_t b = 0; b < sp.size(); b += 64) {
+    const int n = (int)std::min<size_t>(64, sp.size() - b);
+    check_hip(arena_conv_flip_multi(n, sp.data() + b, dp.data() + b, co.data() + b, ci.data() + b,
+                                    rs.data() + b, cur_stream()),
+              "conv_flip_multi");
+  }
+}
+
 // Phase weights of a stride-`stride` backward-data pass (arena_conv_phase_weights): one launch,
 // one buffer; returns one channels_last [C, Cout, Rp, Sp] view per phase with taps, in phase
 // order (a, b) row-major (phases without taps are absent).
@@ -1247,6 +1283,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("linear_fwd", &linear_fwd);
   m.def("bn_fwd", &bn_fwd);
   m.def("conv_flip_weight", &conv_flip_weight);
+  m.def("conv_flip_multi", &conv_flip_multi);
   m.def("conv_phase_weights", &conv_phase_weights);
   m.def("conv_fwd_ex", &conv_fwd_ex);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);

@@ -85,22 +85,32 @@ struct ConvArgs {
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS accesses (lgkmcnt) but not
+// for its outstanding global stores. __syncthreads() also waits vmcnt(0), which in an epilogue
+// that stores in two halves exposes the first half's store latency on every block.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
 __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
 }
 
-// bf16 round-to-nearest-even of two floats, packed (lo = a)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// bf16 round-to-nearest-even of two floats, packed (lo = a): ONE v_cvt_pk_bf16_f32 on gfx950.
+// The integer form (add 0x7fff + lsb, shift) took ~9 VALU ops per pair, which on the streaming-
+// bound 1x1 convolutions was a visible share of the epilogue (and turned some NaNs into Inf).
 __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
-  uint32_t ua = __float_as_uint(a), ub = __float_as_uint(b);
-  ua = (ua + 0x7FFFu + ((ua >> 16) & 1u)) >> 16;
-  ub = (ub + 0x7FFFu + ((ub >> 16) & 1u)) & 0xFFFF0000u;
-  return ua | ub;
+  const f32x2 v = {a, b};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
 }
 
 __device__ __forceinline__ float bf16_round(float f) {
-  uint32_t u = __float_as_uint(f);
-  u = (u + 0x7FFFu + ((u >> 16) & 1u)) & 0xFFFF0000u;
-  return __uint_as_float(u);
+  return __uint_as_float(pack_bf16x2(f, 0.f) << 16);
 }
 
 // sum over the 16 lanes of a DPP row (lane bits 0..3); every lane of the row gets the sum
@@ -303,6 +313,20 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     for (int j = 0; j < NI; ++j)
       bmu[j] = *reinterpret_cast<const float4*>(a.bnmean + n0 + wn * WN + j * 16 + 4 * fq);
   }
+  // EPI 1: round the accumulators to their stored bf16 values once; the stores (whose own
+  // rounding is then exact) and the statistics below both read them.
+  if constexpr (EPI == 1) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; r += 2) {
+          const uint32_t u = pack_bf16x2(acc[i][j][r], acc[i][j][r + 1]);
+          acc[i][j][r] = __uint_as_float(u << 16);
+          acc[i][j][r + 1] = __uint_as_float(u & 0xffff0000u);
+        }
+  }
   if (a.coal && !(EPI != 0 && a.add != nullptr)) {
     // ---- coalesced store through LDS (stage buffers are free: the K loop ended on a barrier) ----
     float* stg = reinterpret_cast<float*>(lds);
@@ -310,7 +334,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     constexpr int CPR = BN / 8;   // 16-byte bf16 output chunks per row
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      if (h) __syncthreads();     // every reader of the first half is done
+      if (h) lds_barrier();       // every reader of the first half is done
       if (wm == h) {
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
@@ -322,7 +346,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
           }
         }
       }
-      __syncthreads();
+      lds_barrier();              // the staged half is complete (global stores may be in flight)
       for (int q = tid; q < WM * CPR; q += kThreads) {
         const int row = q / CPR, cc = q - row * CPR;
         const int m = m0 + h * WM + row;
@@ -471,49 +495,79 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     }
   }
   if constexpr (EPI == 1) {
-    // BatchNorm statistics of this tile's bf16 outputs, two-pass (mean, then sum of squared
-    // deviations) over the valid rows: the partial format of bn_stats_kernel with rpb = BM, so
-    // the BN layer that consumes this output skips its own statistics pass over HBM.
+    // BatchNorm statistics of this tile's (rounded) outputs, two-pass -- mean, then sum of
+    // squared deviations -- over the valid rows: the partial format of bn_stats_kernel with
+    // rpb = BM, so the BN layer that consumes this output skips its statistics pass over HBM.
+    // Every output element passes through it, which on the streaming-bound 1x1 shapes made its
+    // scalar per-element math (a rounding sequence per pass, selects) a measurable cost: the
+    // values are rounded once before the stores, the sums are packed fp32 (two channels per op)
+    // and the row-validity selects only run on the last, partial tile (1x1 64->256 @56x56,
+    // batch 128: 94 -> 85 us; profiles/r2_conv_epi_{before,after}.jsonl).
     const int nrows = min(BM, a.M - m0);
-    const float inv_n = 1.f / (float)nrows;
-    float* red = reinterpret_cast<float*>(lds);   // [2 (wm)][BN]; staging buffers are free now
-    float mean[NI][4];
-#pragma unroll
-    for (int pass = 0; pass < 2; ++pass) {
-      float s[NI][4];
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float t = 0.f;
-#pragma unroll
-          for (int i = 0; i < MI; ++i) {
-            const bool valid = m0 + wm * WM + i * 16 + fr < a.M;
-            const float v = bf16_round(acc[i][j][r]);
-            const float d = pass == 0 ? v : v - mean[j][r];
-            t += valid ? (pass == 0 ? d : d * d) : 0.f;
-          }
-          s[j][r] = row16_sum(t);
-        }
-      __syncthreads();   // previous readers of red (or of the staging buffers) are done
+    const bool full = nrows == BM;
+    float* red = reinterpret_cast<float*>(lds);   // [2 (wm)][BN]
+    float mean[NI][4], s[NI][4];
+    auto exchange = [&](bool first) {   // s (row-16 sums of this wave) -> per-block channel sums
+      if (!first) lds_barrier();        // every wave has read the previous sums
       if (fr == 0) {
 #pragma unroll
         for (int j = 0; j < NI; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) red[wm * BN + wn * WN + j * 16 + 4 * fq + r] = s[j][r];
       }
-      __syncthreads();
+      lds_barrier();
 #pragma unroll
       for (int j = 0; j < NI; ++j)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = wn * WN + j * 16 + 4 * fq + r;
-          const float tot = red[c] + red[BN + c];
-          if (pass == 0) mean[j][r] = tot * inv_n;
-          else if (wm == 0 && fr == 0) {
-            a.part[(size_t)mt * 2 * a.Cout + n0 + c] = mean[j][r];
-            a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = tot;
-          }
+          s[j][r] = red[c] + red[BN + c];
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      f32x2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        f32x2 v0 = {acc[i][j][0], acc[i][j][1]}, v1 = {acc[i][j][2], acc[i][j][3]};
+        if (!full && m0 + wm * WM + i * 16 + fr >= a.M) v0 = v1 = f32x2{0.f, 0.f};
+        t0 += v0;
+        t1 += v1;
+      }
+      s[j][0] = row16_sum(t0.x); s[j][1] = row16_sum(t0.y);
+      s[j][2] = row16_sum(t1.x); s[j][3] = row16_sum(t1.y);
+    }
+    lds_barrier();   // the coalesced store path's last reads of the staging LDS are done
+    exchange(true);
+    const float inv_n = 1.f / (float)nrows;
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) mean[j][r] = s[j][r] * inv_n;
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const f32x2 mu0 = {mean[j][0], mean[j][1]}, mu1 = {mean[j][2], mean[j][3]};
+      f32x2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f};
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        f32x2 d0 = f32x2{acc[i][j][0], acc[i][j][1]} - mu0;
+        f32x2 d1 = f32x2{acc[i][j][2], acc[i][j][3]} - mu1;
+        if (!full && m0 + wm * WM + i * 16 + fr >= a.M) d0 = d1 = f32x2{0.f, 0.f};
+        t0 = __builtin_elementwise_fma(d0, d0, t0);
+        t1 = __builtin_elementwise_fma(d1, d1, t1);
+      }
+      s[j][0] = row16_sum(t0.x); s[j][1] = row16_sum(t0.y);
+      s[j][2] = row16_sum(t1.x); s[j][3] = row16_sum(t1.y);
+    }
+    exchange(false);
+    if (wm == 0 && fr == 0) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int c = wn * WN + j * 16 + 4 * fq + r;
+          a.part[(size_t)mt * 2 * a.Cout + n0 + c] = mean[j][r];
+          a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = s[j][r];
         }
     }
   }
@@ -592,6 +646,8 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.bnmean = bnmean;
   if (bnx != nullptr && (part == nullptr || bnmean == nullptr || y_map != nullptr))
     return hipErrorInvalidValue;
+  // forward statistics are taken from the accumulators before the epilogue adds an addend
+  if (part != nullptr && bnx == nullptr && add != nullptr) return hipErrorInvalidValue;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
   a.stride = stride; a.pad = pad_h; a.pad_w = pad_w;
   a.Ho = Ho > 0 ? Ho : (H + 2 * pad_h - R) / stride + 1;
@@ -694,9 +750,87 @@ __global__ __launch_bounds__(256) void conv_flip_weight_kernel(const uint16_t* _
   }
 }
 
+// Many stride-1 flips in one launch (a ResNet step flips every stride-1 conv weight once, at the
+// start of its forward: one launch instead of one per backward-data pass). Block b belongs to the
+// tensor whose [start, next start) range holds b; within it, b -> (ci tile, co tile, tap).
+constexpr int kMaxFlipTensors = 64;
+struct FlipMulti {
+  const uint16_t* src[kMaxFlipTensors];
+  uint16_t* dst[kMaxFlipTensors];
+  int cout[kMaxFlipTensors], cin[kMaxFlipTensors], rs[kMaxFlipTensors];
+  int start[kMaxFlipTensors + 1];
+  int n;
+};
+
+__global__ __launch_bounds__(256) void conv_flip_multi_kernel(FlipMulti fm) {
+  __shared__ uint16_t tile[64][64 + 2];
+  const int b = blockIdx.x;
+  int k = 0;
+  while (k + 1 < fm.n && b >= fm.start[k + 1]) ++k;   // <= 64 uniform scalar steps
+  const int Cout = fm.cout[k], C = fm.cin[k], RS = fm.rs[k];
+  int rem = b - fm.start[k];
+  const int cit = C >> 6, cot = Cout >> 6;
+  const int ci0 = (rem % cit) * 64;
+  rem /= cit;
+  const int co0 = (rem % cot) * 64, dtap = rem / cot, src_tap = RS - 1 - dtap;
+  const uint16_t* w = fm.src[k];
+  uint16_t* dst = fm.dst[k];
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {   // 64 rows (co) x 8 chunks of 8 ci
+    const int q = t + s * 256, row = q >> 3, ch = q & 7;
+    const uint4 v = *reinterpret_cast<const uint4*>(
+        w + ((size_t)(co0 + row) * RS + src_tap) * C + ci0 + ch * 8);
+    const uint32_t u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      tile[row][ch * 8 + 2 * e] = (uint16_t)(u[e] & 0xffffu);
+      tile[row][ch * 8 + 2 * e + 1] = (uint16_t)(u[e] >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {   // 64 rows (ci) x 8 chunks of 8 co
+    const int q = t + s * 256, row = q >> 3, ch = q & 7;
+    uint32_t u[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      u[e] = (uint32_t)tile[ch * 8 + 2 * e][row] | ((uint32_t)tile[ch * 8 + 2 * e + 1][row] << 16);
+    *reinterpret_cast<uint4*>(dst + ((size_t)(ci0 + row) * RS + dtap) * Cout + co0 + ch * 8) =
+        make_uint4(u[0], u[1], u[2], u[3]);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// W'[ci][r][s][co] = W[co][R-1-r][S-1-s][ci] for n weights in one launch (see conv_flip_multi_kernel).
+// Every Cout and C a multiple of 64, R*S <= 64, n <= 64.
+hipError_t arena_conv_flip_multi(int n, const void* const* src, void* const* dst, const int* cout,
+                                 const int* cin, const int* rs, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  if (n > kMaxFlipTensors) return hipErrorInvalidValue;
+  FlipMulti fm{};
+  long long blocks = 0;
+  for (int i = 0; i < n; ++i) {
+    if (cout[i] % 64 || cin[i] % 64 || cout[i] <= 0 || cin[i] <= 0 || rs[i] <= 0 ||
+        rs[i] > kMaxFlipTaps)
+      return hipErrorInvalidValue;
+    fm.src[i] = (const uint16_t*)src[i];
+    fm.dst[i] = (uint16_t*)dst[i];
+    fm.cout[i] = cout[i];
+    fm.cin[i] = cin[i];
+    fm.rs[i] = rs[i];
+    fm.start[i] = (int)blocks;
+    blocks += (long long)(cin[i] / 64) * (cout[i] / 64) * rs[i];
+    if (blocks >= (1LL << 31)) return hipErrorInvalidValue;
+  }
+  fm.start[n] = (int)blocks;
+  fm.n = n;
+  hipLaunchKernelGGL(conv_flip_multi_kernel, dim3((unsigned)blocks), dim3(256), 0, st, fm);
+  return hipGetLastError();
+}
 
 // Phase weights of a stride-`stride`, top/left-`pad` convolution's backward-data pass, packed in
 // phase order (a, b) = (0, 0), (0, 1), ... skipping phases without taps:

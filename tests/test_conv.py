@@ -415,3 +415,68 @@ def test_stem_conv_space_to_depth_matches_fp32():
         g.float(), x.float(), wb, None, [2, 2], [3, 3], [1, 1], False, [0, 0], 1,
         [False, True, False])[1]
     assert _rel(m.weight.grad, dw_ref) < 1e-2, _rel(m.weight.grad, dw_ref)
+
+
+@pytest.mark.gpu
+def test_conv_flip_multi_matches_flip_weight():
+    """One conv_flip_multi launch over mixed shapes (1x1, 3x3, Cout != C) writes exactly what
+    flip_weight writes per tensor."""
+    from arena_amd.ops import _ext
+    shapes = [(64, 64, 1, 1), (128, 64, 3, 3), (64, 256, 1, 1), (256, 128, 3, 3), (512, 2048, 1, 1)]
+    ws = [(torch.randn(*s, device="cuda") * 0.1).to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last) for s in shapes]
+    dst = [torch.full((w.shape[1], w.shape[0], w.shape[2], w.shape[3]), float("nan"),
+                      device="cuda", dtype=torch.bfloat16).contiguous(
+        memory_format=torch.channels_last) for w in ws]
+    _ext.load().conv_flip_multi(ws, dst)
+    for w, d in zip(ws, dst):
+        ref = w.flip(2, 3).transpose(0, 1)
+        assert torch.equal(d, ref)
+        assert torch.equal(d, conv.flip_weight(w))
+
+
+@pytest.mark.gpu
+def test_weight_flipper_scope_matches_per_conv_flips():
+    """A bf16 channels_last ResNet trained through the WeightFlipper scope (one flip launch per
+    step) gives bit-identical gradients to per-conv flips, and the scope's flipped copies are the
+    ones the backward-data passes use."""
+    from arena_amd.models import resnet as R
+    conv.set_mode("ours")
+    try:
+        torch.manual_seed(0)
+        net = R.resnet("resnet_tiny", num_classes=10).cuda().to(memory_format=torch.channels_last)
+        for m in net.modules():   # bf16 conv weights, as under MasterSGD
+            if isinstance(m, torch.nn.Conv2d):
+                m.weight.data = m.weight.data.to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last)
+        x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+        used = []
+        orig = conv.conv2d_bwd_data
+
+        def spy(*a, **k):
+            used.append(k.get("wflip") is not None)
+            return orig(*a, **k)
+
+        grads = {}
+        for name in ("flipper", "per_conv"):
+            if name == "per_conv":
+                net._flipper.convs = []
+            net.zero_grad(set_to_none=True)
+            conv.conv2d_bwd_data = spy
+            try:
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    out = net(x)
+                out.float().square().mean().backward()
+            finally:
+                conv.conv2d_bwd_data = orig
+            grads[name] = {n: p.grad.clone() for n, p in net.named_parameters()}
+            if name == "flipper":
+                assert used and all(used), used
+            else:
+                assert used and not any(used)
+            used.clear()
+        for n, g in grads["per_conv"].items():
+            assert torch.equal(grads["flipper"][n], g), n
+        assert conv._ACTIVE_FLIPS is None   # the scope does not leak past forward
+    finally:
+        conv.set_mode(None)
