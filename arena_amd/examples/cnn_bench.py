@@ -128,7 +128,7 @@ def capture_step(model, opt, x, y, amp_dtype):
     (not accumulates) them, and every replay reuses the same memory (static x, y)."""
     opt.zero_grad(set_to_none=True)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         loss = train_step(model, opt, x, y, amp_dtype, zero_grad=False)
     return g, loss
 

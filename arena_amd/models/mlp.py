@@ -287,8 +287,12 @@ class FusedMLPTrainer:
         # an even-length graph replayed from an even step sees the same parity sequence every
         # time, so the parity is baked into the launches (train_steps keeps replays even-aligned)
         self._graph_static = nsteps % 2 == 0
+        # thread_local: the RCCL process group's watchdog thread polls the events of earlier
+        # collectives (the xGMI handle exchange, barriers); under the default global capture mode
+        # such a poll landing inside the capture is an error that aborts the rank
+        # (tests/test_xgmi_gpu.py::test_rccl_allreduce_is_graph_capturable hit it on a GPU run)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for i in range(nsteps):
                 self._launch_step(parity=(i & 1) if self._graph_static else -1)
         return g
@@ -332,9 +336,9 @@ class FusedMLPTrainer:
         try:
             pre, post = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
             self._split = True
-            with torch.cuda.graph(pre):
+            with torch.cuda.graph(pre, capture_error_mode="thread_local"):
                 self._launch_step_part(0)
-            with torch.cuda.graph(post):
+            with torch.cuda.graph(post, capture_error_mode="thread_local"):
                 self._launch_step_part(2)
             self._split_graphs = (pre, post)
             self.graph_mode = "split"

@@ -371,7 +371,7 @@ def _time(fn, reps: int = 4, iters: int = 3) -> float:
         e.synchronize()
         return s.elapsed_time(e) * 1e3 / (reps * iters)
     g = torch.cuda.CUDAGraph()
-    with torch.cuda.graph(g):
+    with torch.cuda.graph(g, capture_error_mode="thread_local"):
         for _ in range(reps):
             fn()
     g.replay()

@@ -35,7 +35,7 @@ def timed(fn, iters: int = 50, reps: int = 5) -> float:
     torch.cuda.synchronize()
     g = torch.cuda.CUDAGraph()
     try:
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for _ in range(iters):
                 fn()
         run = g.replay

@@ -81,7 +81,7 @@ def _collectives(rank, world, port, q):
             comm.all_reduce_(y, scale=1.0 / world)
         torch.cuda.current_stream().wait_stream(s)
         gr = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(gr):
+        with torch.cuda.graph(gr, capture_error_mode="thread_local"):
             for _ in range(3):
                 comm.all_reduce_(y, scale=1.0 / world)
         for _ in range(5):
@@ -240,7 +240,7 @@ def _rccl_capture(rank, world, port, q):
             dist.all_reduce(x)                         # communicator set up outside capture
         torch.cuda.current_stream().wait_stream(s)
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, capture_error_mode="thread_local"):
             x.mul_(2.0)
             dist.all_reduce(x)
         for _ in range(3):
