@@ -190,6 +190,30 @@ def stem_weight(w: Tensor) -> Tensor:
     return wp.permute(0, 3, 1, 2).contiguous(memory_format=torch.channels_last)
 
 
+_STEM_FUSED = True
+
+
+def set_stem_fused(on: bool) -> None:
+    """Fused stem casts + one-kernel weight transform (default) or the torch-op form (A/Bs)."""
+    global _STEM_FUSED
+    _STEM_FUSED = bool(on)
+
+
+class _StemWeightFn(torch.autograd.Function):
+    """``stem_weight`` as one HIP kernel each way (instead of ~5 pad/permute/copy kernels per
+    direction per step); the gradient comes back in the weight's dtype and memory layout."""
+
+    @staticmethod
+    def forward(ctx, w):
+        ctx.save_for_backward(w)
+        return _ext.load().stem_weight(w)
+
+    @staticmethod
+    def backward(ctx, dw16):
+        (w,) = ctx.saved_tensors
+        return _ext.load().stem_weight_grad(dw16.contiguous(memory_format=torch.channels_last), w)
+
+
 class _StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, w16, want_stats, fwd_variant, wgrad_cfg):
@@ -713,16 +737,21 @@ class StemConv2d(Conv2dNHWC):
         amp = torch.is_autocast_enabled("cuda") and \
             torch.get_autocast_dtype("cuda") == torch.bfloat16
         w = self.weight
-        if amp:
-            x = x.to(torch.bfloat16)
-            w = w.to(torch.bfloat16)
-        if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16 or not stem_ok(x, w, s, p):
+        # under autocast both casts are fused: s2d_stem rounds an fp32 batch to bf16 as it
+        # rearranges it, and the stem-weight kernel rounds an fp32 weight (its backward writes
+        # the gradient in the parameter's own dtype and layout)
+        fuse = _STEM_FUSED
+        xin = x if (not amp or (fuse and x.dtype == torch.float32)) else x.to(torch.bfloat16)
+        ok = (xin.dtype in (torch.bfloat16, torch.float32) and w.dtype in (torch.bfloat16,
+                                                                          torch.float32)
+              if amp else (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16))
+        if not ok or not stem_ok(xin, w, s, p):
             return super().forward_stats(x, want_stats, join, bn_link)
-        x = x.contiguous(memory_format=torch.channels_last)
+        xin = xin.contiguous(memory_format=torch.channels_last)
         want = want_stats and torch.is_grad_enabled() and self.training
         with torch.autocast("cuda", enabled=False):
-            z = _ext.load().s2d_stem(x)
-            w16 = stem_weight(w)
+            z = _ext.load().s2d_stem(xin)
+            w16 = _StemWeightFn.apply(w) if fuse else stem_weight(w.to(torch.bfloat16))
             fv, wcfg = _stem_plan(z, w16)
             y, part = _StemFn.apply(z, w16, want, fv, wcfg)
         return y, ((part, TILES[fv][0]) if want else None)

@@ -60,7 +60,11 @@ hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void
 hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
                                int, int, int, int, int, int, int, int, int, int, int, float,
                                hipStream_t);
-hipError_t arena_s2d_stem(const void*, void*, int, int, int, int, hipStream_t);
+hipError_t arena_s2d_stem(const void*, void*, int, int, int, int, int, hipStream_t);
+hipError_t arena_stem_weight(const void*, void*, int, int, long long, long long, long long,
+                             long long, int, hipStream_t);
+hipError_t arena_stem_weight_grad(const void*, void*, int, int, long long, long long, long long,
+                                  long long, int, hipStream_t);
 hipError_t arena_conv_phase_weights(const void*, void*, int, int, int, int, int, int, long long*,
                                     hipStream_t);
 int arena_conv_wgrad_splits(int, int, int, int, int, int, int);
@@ -1116,18 +1120,59 @@ Tensor conv_wgrad_ex(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, 
 }
 
 // Space-to-depth of a channels_last [N, C<=4, H, W] bf16 image: [N, 16, H/2, W/2] (see kernel).
+// x: channels_last [N, C<=4, H, W], bf16 or fp32 (rounded to bf16: the autocast cast, fused)
 Tensor s2d_stem(Tensor x) {
-  TORCH_CHECK(x.is_cuda() && x.dim() == 4 && x.scalar_type() == torch::kBFloat16 &&
+  const bool f32 = x.scalar_type() == torch::kFloat32;
+  TORCH_CHECK(x.is_cuda() && x.dim() == 4 &&
+                  (f32 || x.scalar_type() == torch::kBFloat16) &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) <= 4 &&
                   x.size(2) % 2 == 0 && x.size(3) % 2 == 0,
-              "s2d_stem: channels_last bf16 [N, C<=4, H, W] with even H, W");
+              "s2d_stem: channels_last bf16/fp32 [N, C<=4, H, W] with even H, W");
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
-  Tensor z = torch::empty({N, 16, H / 2, W / 2},
-                          x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  check_hip(arena_s2d_stem(x.data_ptr(), z.data_ptr(), (int)N, (int)H, (int)W, (int)C,
+  Tensor z = torch::empty({N, 16, H / 2, W / 2}, x.options().dtype(torch::kBFloat16).memory_format(
+                                                     at::MemoryFormat::ChannelsLast));
+  check_hip(arena_s2d_stem(x.data_ptr(), z.data_ptr(), (int)N, (int)H, (int)W, (int)C, f32 ? 1 : 0,
                            cur_stream()),
             "s2d_stem");
   return z;
+}
+
+// The 7x7 stem weight [Cout, C<=4, 7, 7] (fp32 or bf16, any strides) -> its space-to-depth form,
+// channels_last bf16 [Cout, 16, 4, 4] (ops/conv.py stem_weight).
+Tensor stem_weight(Tensor w) {
+  const bool f32 = w.scalar_type() == torch::kFloat32;
+  TORCH_CHECK(w.is_cuda() && w.dim() == 4 && (f32 || w.scalar_type() == torch::kBFloat16) &&
+                  w.size(1) >= 1 && w.size(1) <= 4 && w.size(2) == 7 && w.size(3) == 7,
+              "stem_weight: [Cout, C<=4, 7, 7] fp32/bf16 GPU tensor");
+  const int64_t Cout = w.size(0);
+  Tensor w16 = torch::empty({Cout, 16, 4, 4}, w.options().dtype(torch::kBFloat16).memory_format(
+                                                  at::MemoryFormat::ChannelsLast));
+  check_hip(arena_stem_weight(w.data_ptr(), w16.data_ptr(), (int)Cout, (int)w.size(1),
+                              w.stride(0), w.stride(1), w.stride(2), w.stride(3), f32 ? 1 : 0,
+                              cur_stream()),
+            "stem_weight");
+  return w16;
+}
+
+// dW of the stem weight from dW16 (channels_last bf16 [Cout, 16, 4, 4]), allocated like `w`
+// (its dtype and strides, so autograd accumulates it without a layout copy)
+Tensor stem_weight_grad(Tensor dw16, Tensor w) {
+  TORCH_CHECK(dw16.is_cuda() && dw16.dim() == 4 && dw16.scalar_type() == torch::kBFloat16 &&
+                  dw16.size(1) == 16 && dw16.size(2) == 4 && dw16.size(3) == 4 &&
+                  dw16.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_weight_grad: dw16 must be channels_last bf16 [Cout, 16, 4, 4]");
+  const bool f32 = w.scalar_type() == torch::kFloat32;
+  TORCH_CHECK(w.dim() == 4 && w.size(0) == dw16.size(0) && w.size(1) >= 1 && w.size(1) <= 4 &&
+                  w.size(2) == 7 && w.size(3) == 7 &&
+                  (f32 || w.scalar_type() == torch::kBFloat16),
+              "stem_weight_grad: w must be [Cout, C<=4, 7, 7] fp32/bf16");
+  Tensor dw = torch::empty_like(w);
+  TORCH_CHECK(dw.is_non_overlapping_and_dense(), "stem_weight_grad: dense weight layout needed");
+  check_hip(arena_stem_weight_grad(dw16.data_ptr(), dw.data_ptr(), (int)w.size(0),
+                                   (int)w.size(1), dw.stride(0), dw.stride(1), dw.stride(2),
+                                   dw.stride(3), f32 ? 1 : 0, cur_stream()),
+            "stem_weight_grad");
+  return dw;
 }
 
 // dW of an NHWC convolution: [Cout, C, R, S] channels_last, bf16 (for MasterSGD) or fp32.
@@ -1288,6 +1333,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd_ex", &conv_fwd_ex);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);
   m.def("s2d_stem", &s2d_stem);
+  m.def("stem_weight", &stem_weight);
+  m.def("stem_weight_grad", &stem_weight_grad);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("mean"),
         py::arg("invstd"), py::arg("gamma"), py::arg("relu"), py::arg("with_res"),
         py::arg("affine_grads"), py::arg("ext_part") = py::none(), py::arg("ext_rpb") = 0);

@@ -888,7 +888,17 @@ hipError_t arena_conv_flip_weight(const void* w, void* wt, int Cout, int C, int 
 // ================================================================================================
 namespace {
 
-__global__ __launch_bounds__(256) void s2d_stem_kernel(const uint16_t* __restrict__ x,
+// TIn = uint16_t (bf16) or float: an fp32 input batch is rounded to bf16 here, which under
+// autocast replaces the separate cast pass over the whole batch (a 77 MB read + 38 MB write at
+// ResNet-50 batch 128).
+__device__ __forceinline__ uint16_t s2d_in(uint16_t v) { return v; }
+__device__ __forceinline__ uint16_t s2d_in(float v) {
+  const f32x2 p = {v, 0.f};
+  return (uint16_t)(__builtin_bit_cast(uint32_t, __builtin_convertvector(p, bf16x2_t)) & 0xffffu);
+}
+
+template <typename TIn>
+__global__ __launch_bounds__(256) void s2d_stem_kernel(const TIn* __restrict__ x,
                                                        uint16_t* __restrict__ z, int N, int H,
                                                        int W, int C) {
   const int Hz = H >> 1, Wz = W >> 1;
@@ -902,10 +912,10 @@ __global__ __launch_bounds__(256) void s2d_stem_kernel(const uint16_t* __restric
   for (int k = 0; k < 16; ++k) v[k] = 0;
 #pragma unroll
   for (int d = 0; d < 4; ++d) {
-    const uint16_t* src = x + (((size_t)n * H + 2 * i + (d >> 1)) * W + 2 * j + (d & 1)) * C;
+    const TIn* src = x + (((size_t)n * H + 2 * i + (d >> 1)) * W + 2 * j + (d & 1)) * C;
 #pragma unroll
     for (int c = 0; c < 4; ++c)
-      if (c < C) v[d * C + c] = src[c];
+      if (c < C) v[d * C + c] = s2d_in(src[c]);
   }
   uint4 o0, o1;
   o0.x = v[0] | ((uint32_t)v[1] << 16); o0.y = v[2] | ((uint32_t)v[3] << 16);
@@ -917,14 +927,94 @@ __global__ __launch_bounds__(256) void s2d_stem_kernel(const uint16_t* __restric
   dst[1] = o1;
 }
 
+// The stem weight in its space-to-depth form, one thread per W16 element (and its backward, one
+// thread per W element: every W tap has exactly one W16 slot):
+//   W16[co][u][v][(dy*2+dx)*C + c] = W[co][c][2u+dy-1][2v+dx-1]  (0 outside the 7x7 filter)
+// W is [Cout][C][7][7] in any memory layout (element strides given), fp32 or bf16; W16 is the
+// channels_last bf16 [Cout][16][4][4] the c16 conv reads, i.e. memory [co][u][v][16].
+template <typename TW>
+__global__ __launch_bounds__(256) void stem_weight_kernel(const TW* __restrict__ w,
+                                                          uint16_t* __restrict__ w16, int Cout,
+                                                          int C, long long sco, long long sc,
+                                                          long long sr, long long ss) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= Cout * 256) return;
+  const int ch = e & 15, v = (e >> 4) & 3, u = (e >> 6) & 3, co = e >> 8;
+  float val = 0.f;
+  if (ch < 4 * C) {
+    const int d = ch / C, c = ch - d * C;
+    const int r = 2 * u + (d >> 1) - 1, s = 2 * v + (d & 1) - 1;
+    if (r >= 0 && r < 7 && s >= 0 && s < 7) {
+      const TW q = w[co * sco + c * sc + r * sr + s * ss];
+      if constexpr (sizeof(TW) == 2) val = __uint_as_float((uint32_t)q << 16);
+      else val = q;
+    }
+  }
+  const f32x2 pr = {val, 0.f};
+  w16[e] = (uint16_t)(__builtin_bit_cast(uint32_t, __builtin_convertvector(pr, bf16x2_t)) & 0xffffu);
+}
+
+// dW[co][c][r][s] = dW16 at W's slot; dW [Cout][C][7][7] with element strides (dco, dc, dr, ds),
+// fp32 or bf16 (the parameter's own dtype and layout: no copy in autograd's accumulation)
+template <typename TW>
+__global__ __launch_bounds__(256) void stem_weight_grad_kernel(const uint16_t* __restrict__ dw16,
+                                                               TW* __restrict__ dw, int Cout,
+                                                               int C, long long dco, long long dc,
+                                                               long long dr, long long ds) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= Cout * C * 49) return;
+  const int s = e % 7, r = (e / 7) % 7, c = (e / 49) % C, co = e / (49 * C);
+  const int u = (r + 1) >> 1, dy = (r + 1) & 1, v = (s + 1) >> 1, dx = (s + 1) & 1;
+  const int ch = (dy * 2 + dx) * C + c;
+  const uint16_t g = dw16[((co * 4 + u) * 4 + v) * 16 + ch];
+  TW* o = dw + co * dco + c * dc + r * dr + s * ds;
+  if constexpr (sizeof(TW) == 2) *o = g;
+  else *o = __uint_as_float((uint32_t)g << 16);
+}
+
 }  // namespace
 
+// in_f32: x is fp32 (rounded to bf16 on the way), else bf16
 extern "C" hipError_t arena_s2d_stem(const void* x, void* z, int N, int H, int W, int C,
-                                     hipStream_t st) {
+                                     int in_f32, hipStream_t st) {
   if (N <= 0 || H % 2 || W % 2 || C < 1 || C > 4) return hipErrorInvalidValue;
   const long long P = (long long)N * (H / 2) * (W / 2);
-  hipLaunchKernelGGL(s2d_stem_kernel, dim3((unsigned)((P + 255) / 256)), dim3(256), 0, st,
-                     (const uint16_t*)x, (uint16_t*)z, N, H, W, C);
+  const dim3 g((unsigned)((P + 255) / 256));
+  if (in_f32)
+    hipLaunchKernelGGL(s2d_stem_kernel<float>, g, dim3(256), 0, st, (const float*)x,
+                       (uint16_t*)z, N, H, W, C);
+  else
+    hipLaunchKernelGGL(s2d_stem_kernel<uint16_t>, g, dim3(256), 0, st, (const uint16_t*)x,
+                       (uint16_t*)z, N, H, W, C);
+  return hipGetLastError();
+}
+
+// W [Cout][C][7][7] (element strides sco, sc, sr, ss; fp32 if w_f32 else bf16) -> W16
+extern "C" hipError_t arena_stem_weight(const void* w, void* w16, int Cout, int C, long long sco,
+                                        long long sc, long long sr, long long ss, int w_f32,
+                                        hipStream_t st) {
+  if (Cout <= 0 || C < 1 || C > 4) return hipErrorInvalidValue;
+  const dim3 g((unsigned)((Cout * 256 + 255) / 256));
+  if (w_f32)
+    hipLaunchKernelGGL(stem_weight_kernel<float>, g, dim3(256), 0, st, (const float*)w,
+                       (uint16_t*)w16, Cout, C, sco, sc, sr, ss);
+  else
+    hipLaunchKernelGGL(stem_weight_kernel<uint16_t>, g, dim3(256), 0, st, (const uint16_t*)w,
+                       (uint16_t*)w16, Cout, C, sco, sc, sr, ss);
+  return hipGetLastError();
+}
+
+extern "C" hipError_t arena_stem_weight_grad(const void* dw16, void* dw, int Cout, int C,
+                                             long long dco, long long dc, long long dr,
+                                             long long ds, int dw_f32, hipStream_t st) {
+  if (Cout <= 0 || C < 1 || C > 4) return hipErrorInvalidValue;
+  const dim3 g((unsigned)((Cout * C * 49 + 255) / 256));
+  if (dw_f32)
+    hipLaunchKernelGGL(stem_weight_grad_kernel<float>, g, dim3(256), 0, st,
+                       (const uint16_t*)dw16, (float*)dw, Cout, C, dco, dc, dr, ds);
+  else
+    hipLaunchKernelGGL(stem_weight_grad_kernel<uint16_t>, g, dim3(256), 0, st,
+                       (const uint16_t*)dw16, (uint16_t*)dw, Cout, C, dco, dc, dr, ds);
   return hipGetLastError();
 }
 

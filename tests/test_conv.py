@@ -480,3 +480,38 @@ def test_weight_flipper_scope_matches_per_conv_flips():
         assert conv._ACTIVE_FLIPS is None   # the scope does not leak past forward
     finally:
         conv.set_mode(None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("wdtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("cl", [True, False])
+def test_stem_weight_kernels_match_torch(wdtype, cl):
+    """The one-kernel stem weight transform equals the torch-op form (stem_weight) on the
+    bf16-rounded weight, and its backward equals autograd through that form, written in the
+    weight's own dtype and memory layout."""
+    from arena_amd.ops import _ext
+    torch.manual_seed(0)
+    w = torch.randn(64, 3, 7, 7, device="cuda").to(wdtype)
+    if cl:
+        w = w.contiguous(memory_format=torch.channels_last)
+    w16 = _ext.load().stem_weight(w)
+    ref = conv.stem_weight(w.to(torch.bfloat16))
+    assert w16.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(w16, ref)
+    g16 = torch.randn(64, 16, 4, 4, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    wr = w.detach().to(torch.bfloat16).requires_grad_(True)
+    conv.stem_weight(wr).backward(g16)
+    dw = _ext.load().stem_weight_grad(g16, w)
+    assert dw.dtype == w.dtype and dw.stride() == w.stride()
+    assert torch.equal(dw.float(), wr.grad.float())
+
+
+@pytest.mark.gpu
+def test_s2d_stem_fp32_input_rounds_like_the_cast():
+    """s2d_stem on an fp32 batch equals s2d_stem on the same batch cast to bf16 first."""
+    from arena_amd.ops import _ext
+    x = torch.randn(3, 3, 22, 18, device="cuda").contiguous(memory_format=torch.channels_last)
+    a = _ext.load().s2d_stem(x)
+    b = _ext.load().s2d_stem(x.to(torch.bfloat16))
+    assert a.dtype == torch.bfloat16 and torch.equal(a, b)
