@@ -307,6 +307,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         bx[i][j] = *reinterpret_cast<const uint2*>(a.bnx + (size_t)m * a.Cout + c0);
         bm[i][j] = a.bnmask ? ((uint32_t)a.bnmask[(size_t)m * (a.Cout >> 3) + (c0 >> 3)] >>
                                (c0 & 7)) : 0xfu;
+        if (m0 + wm * WM + i * 16 + fr >= a.M) bm[i][j] = 0u;   // rows past M: no contribution
       }
     }
 #pragma unroll
@@ -449,29 +450,39 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
   }
   }
   if constexpr (EPI == 2) {
-    // per channel over the tile's valid rows: sum g, sum g * (x - mean), g = stored dY * mask
+    // per channel over the tile's valid rows: sum g, sum g * (x - mean), g = stored dY * mask.
+    // Per element: the stored (bf16-rounded) value via one v_cvt_pk_bf16_f32 per pair, the mask
+    // select (rows past M were cleared from the mask bits at load), packed fp32 sums.
     float* red = reinterpret_cast<float*>(lds);   // [2 (wm)][2][BN]
     float s1[NI][4], s2[NI][4];
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
-      const float mu[4] = {bmu[j].x, bmu[j].y, bmu[j].z, bmu[j].w};
+      const f32x2 mu01 = {bmu[j].x, bmu[j].y}, mu23 = {bmu[j].z, bmu[j].w};
+      f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f}, b01 = {0.f, 0.f}, b23 = {0.f, 0.f};
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const bool valid = m0 + wm * WM + i * 16 + fr < a.M && ((bm[i][j] >> r) & 1u);
-          const uint32_t w2 = r < 2 ? bx[i][j].x : bx[i][j].y;
-          const float xv = __uint_as_float((r & 1) ? (w2 & 0xffff0000u) : (w2 << 16));
-          const float g = valid ? bf16_round(acc[i][j][r]) : 0.f;
-          t1 += g;
-          t2 = fmaf(g, xv - mu[r], t2);
-        }
-        s1[j][r] = row16_sum(t1);
-        s2[j][r] = row16_sum(t2);
+      for (int i = 0; i < MI; ++i) {
+        const uint32_t u01 = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+        const uint32_t u23 = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+        const uint32_t mk = bm[i][j];
+        const f32x2 g01 = {(mk & 1u) ? __uint_as_float(u01 << 16) : 0.f,
+                           (mk & 2u) ? __uint_as_float(u01 & 0xffff0000u) : 0.f};
+        const f32x2 g23 = {(mk & 4u) ? __uint_as_float(u23 << 16) : 0.f,
+                           (mk & 8u) ? __uint_as_float(u23 & 0xffff0000u) : 0.f};
+        const f32x2 x01 = {__uint_as_float(bx[i][j].x << 16),
+                           __uint_as_float(bx[i][j].x & 0xffff0000u)};
+        const f32x2 x23 = {__uint_as_float(bx[i][j].y << 16),
+                           __uint_as_float(bx[i][j].y & 0xffff0000u)};
+        a01 += g01;
+        a23 += g23;
+        b01 = __builtin_elementwise_fma(g01, x01 - mu01, b01);
+        b23 = __builtin_elementwise_fma(g23, x23 - mu23, b23);
       }
+      s1[j][0] = row16_sum(a01.x); s1[j][1] = row16_sum(a01.y);
+      s1[j][2] = row16_sum(a23.x); s1[j][3] = row16_sum(a23.y);
+      s2[j][0] = row16_sum(b01.x); s2[j][1] = row16_sum(b01.y);
+      s2[j][2] = row16_sum(b23.x); s2[j][3] = row16_sum(b23.y);
     }
-    __syncthreads();   // every wave is past its last read of the staging buffers
+    lds_barrier();   // every wave is past its last read of the staging LDS (stores may be in flight)
     if (fr == 0) {
 #pragma unroll
       for (int j = 0; j < NI; ++j)
@@ -482,7 +493,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
           red[wm * 2 * BN + BN + c] = s2[j][r];
         }
     }
-    __syncthreads();
+    lds_barrier();
     if (wm == 0 && fr == 0) {
 #pragma unroll
       for (int j = 0; j < NI; ++j)
