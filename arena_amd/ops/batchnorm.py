@@ -26,7 +26,7 @@ import torch
 import torch.nn.functional as F
 from torch import nn
 
-from . import _ext
+from . import _ext, conv
 
 SUPPORTED_C = {8, 16, 32, 64, 128, 256, 512, 1024, 2048}
 
@@ -80,10 +80,20 @@ class _BNActFn(torch.autograd.Function):
                                "fused kernels; use train() or the PyTorch path")
         dy = dy.contiguous(memory_format=torch.channels_last)
         ext = ctx.link.take(dy) if ctx.link is not None else None
+        # the residual gradient is dy * ReLU mask; when this BN reaches the residual join first
+        # and the other consumer's dgrad epilogue takes a masked addend, park (dy, mask) instead
+        # of writing that product (one full write of the block input's size saved)
+        masked = (ctx.has_res and ctx.relu and mask is not None and conv.masked_join()
+                  and ctx.join is not None and ctx.join.active() and ctx.needs_input_grad[1]
+                  and ctx.join.other() is None and ctx.join.peer_takes_masked())
         dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, mask, x, mean, invstd, weight, ctx.relu,
-                                                     ctx.has_res, ctx.affine,
+                                                     ctx.has_res and not masked, ctx.affine,
                                                      ext[0] if ext else None, ext[1] if ext else 0)
-        if not ctx.has_res:
+        if masked:
+            parked = ctx.join.park_or_take(conv.MaskedGrad(dy, mask))
+            assert parked, "masked residual gradient must be the join's first arrival"
+            dres = None
+        elif not ctx.has_res:
             dres = None
         elif ctx.join is not None and ctx.join.active() and ctx.needs_input_grad[1]:
             other = ctx.join.other()

@@ -62,13 +62,16 @@ def pick_variant(m: int, cout: int) -> int:
 
 
 def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int = -1,
-               with_stats: bool = False, addend: Tensor | None = None, bn=None):
+               with_stats: bool = False, addend: Tensor | None = None, bn=None,
+               addmask: Tensor | None = None):
     """y = conv2d(x, w) (+ addend) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S].
 
     with_stats: returns (y, (part, rpb)) where part holds per-tile BatchNorm partials of y
     (tile mean and sum of squared deviations per channel, ``rpb`` output pixels per tile), which
     ``BatchNormAct2d(..., stats=...)`` finalizes instead of re-reading y.
     addend: a bf16 tensor shaped like y, added to the fp32 sums before rounding (epilogue).
+    addmask: uint8 bits (numel(y) / 8 bytes, bit i of byte v for element 8v + i, NHWC order):
+    only the addend elements whose bit is set are added (a ReLU'd gradient, see GradJoin).
     bn: (bn_x, bn_mask or None, bn_mean) when y is the gradient of a BatchNorm layer's output:
     returns (y, (part, rpb)) with that BN's backward partials (sum g, sum g (bn_x - mean) per
     tile, g = y * mask) for its backward, which then skips its reduction pass."""
@@ -84,7 +87,7 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
         bx, bm, bmu = bn
         with_stats = True
     out = _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant), bool(with_stats),
-                               addend, bx, bm, bmu)
+                               addend, bx, bm, bmu, addmask if addend is not None else None)
     if with_stats:
         return out[0], (out[1], TILES[variant][0])
     return out[0]
@@ -99,14 +102,15 @@ def flip_weight(w: Tensor) -> Tensor:
 
 
 def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1,
-                    addend: Tensor | None = None, bn=None, wflip: Tensor | None = None):
+                    addend: Tensor | None = None, bn=None, wflip: Tensor | None = None,
+                    addmask: Tensor | None = None):
     """dX (+ addend) of a stride-1 convolution (same spatial size when pad = (R-1)/2).
     With ``bn`` (see conv2d_fwd) returns (dX, (part, rpb)): the backward partials of the
     BatchNorm layer whose output is this convolution's input. ``wflip``: ``flip_weight(w)``
     computed ahead of time (``WeightFlipper``)."""
     r = w.shape[2]
     wf = wflip if wflip is not None else flip_weight(w)
-    return conv2d_fwd(dy, wf, 1, r - 1 - pad, variant, addend=addend, bn=bn)
+    return conv2d_fwd(dy, wf, 1, r - 1 - pad, variant, addend=addend, bn=bn, addmask=addmask)
 
 
 # Off by default: on ResNet-50 bs128 the heavier dgrad epilogue cost more than the reduction pass
@@ -279,6 +283,42 @@ class BNGradLink:
         return out
 
 
+_MASKED_JOIN = True
+
+
+def set_masked_join(on: bool) -> None:
+    """A block's last BN parks (dy, ReLU bits) in the residual join instead of writing dy * mask
+    (default on; off for A/Bs)."""
+    global _MASKED_JOIN
+    _MASKED_JOIN = bool(on)
+
+
+def masked_join() -> bool:
+    return _MASKED_JOIN
+
+
+class MaskedGrad:
+    """A gradient given as (g, bits): the value is g where the bit is set, 0 elsewhere (a
+    ReLU'd BatchNorm output's gradient, parked in a GradJoin without materializing g * mask)."""
+    __slots__ = ("g", "bits")
+
+    def __init__(self, g: Tensor, bits: Tensor):
+        self.g, self.bits = g, bits
+
+    def materialize(self) -> Tensor:
+        """g * mask as a dense tensor (for consumers without a masked epilogue)."""
+        return (self.g * _unpack_bits(self.bits, self.g)).contiguous(
+            memory_format=torch.channels_last)
+
+
+def _unpack_bits(bits: Tensor, like: Tensor) -> Tensor:
+    """The 0/1 mask (dtype of ``like``, its NHWC layout) of a bit-packed mask."""
+    shifts = torch.arange(8, device=bits.device, dtype=torch.uint8)
+    m = ((bits.view(-1, 1) >> shifts) & 1).reshape(-1)
+    n, c, h, w = like.shape
+    return m.view(n, h, w, c).permute(0, 3, 1, 2).to(like.dtype)
+
+
 class GradJoin:
     """One tensor, two consumers (a ResNet block input feeds conv1 and the shortcut): instead of
     letting autograd add the two gradients in a separate elementwise pass, the consumer whose
@@ -286,16 +326,27 @@ class GradJoin:
     returns the sum -- fused into the backward-data kernel's epilogue when it runs on ours.
     Consumers ``register()`` in their forward; with fewer than two registered, both behave
     normally. The two backwards must both run (true inside one block), exactly once."""
-    __slots__ = ("n", "arrived", "pending")
+    __slots__ = ("n", "arrived", "pending", "first_takes_masked")
 
     def __init__(self):
         self.n = 0
         self.arrived = 0
-        self.pending: Tensor | None = None
+        self.pending = None
+        self.first_takes_masked = False
 
-    def register(self) -> "GradJoin":
+    def register(self, takes_masked: bool = False) -> "GradJoin":
+        """``takes_masked``: this consumer can fold a ``MaskedGrad`` into its own gradient (its
+        backward-data kernel takes the addend's bit mask)."""
         self.n += 1
+        if self.n == 1:
+            self.first_takes_masked = bool(takes_masked)
         return self
+
+    def peer_takes_masked(self) -> bool:
+        """For the second registrant (a block's last BatchNorm; the conv consuming the block input
+        registers first in forward order): the other consumer folds a MaskedGrad in, so this one
+        may park (dy, ReLU bits) instead of writing dy * mask."""
+        return self.n == 2 and self.first_takes_masked
 
     def active(self) -> bool:
         return self.n == 2
@@ -620,7 +671,9 @@ class _ConvFn(torch.autograd.Function):
         ctx.conf = (stride, pad, plan)
         # W' of a WeightFlipper scope (flipped this step, before this forward)
         ctx.wflip = _active_flip(w) if (stride == 1 and plan.bwd != MIOPEN) else None
-        ctx.join = join.register() if join is not None else None
+        # the backward-data kernel can take a masked addend (a BN's (dy, ReLU bits), see GradJoin)
+        ctx.join = join.register(takes_masked=(stride == 1 and plan.bwd != MIOPEN)) \
+            if join is not None else None
         ctx.bn_link = bn_link if (bn_link is not None and bn_link.ready()) else None
         ctx.mark_non_differentiable(part)
         # no zero-filled gradient for the statistics output (one fill kernel per conv per step)
@@ -639,6 +692,13 @@ class _ConvFn(torch.autograd.Function):
             join = ctx.join if (ctx.join is not None and ctx.join.active()) else None
             # the second consumer of a joined input folds the first one's gradient in
             other = join.other() if join is not None else None
+            omask = None
+            if isinstance(other, MaskedGrad):
+                if stride == 1 and plan.bwd != MIOPEN:
+                    other, omask = other.g.contiguous(memory_format=torch.channels_last), \
+                        other.bits
+                else:
+                    other = other.materialize()
             lk = ctx.bn_link
             # the BN partials need the COMPLETE gradient of x: not from a join's first arriver
             use_bn = (lk is not None and plan.bwd != MIOPEN and stride == 1
@@ -653,10 +713,12 @@ class _ConvFn(torch.autograd.Function):
                                              plan.bwd, addend=other)
             elif use_bn:
                 dx, (part, rpb) = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other,
-                                                  bn=(lk.x, lk.mask, lk.mean), wflip=ctx.wflip)
+                                                  bn=(lk.x, lk.mask, lk.mean), wflip=ctx.wflip,
+                                                  addmask=omask)
                 lk.publish(part, rpb, dx)
             else:
-                dx = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other, wflip=ctx.wflip)
+                dx = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other, wflip=ctx.wflip,
+                                     addmask=omask)
             if join is not None and join.park_or_take(dx):
                 dx = None
         if ctx.needs_input_grad[1]:

@@ -54,9 +54,9 @@ hipError_t arena_conv_fwd(const void*, const void*, void*, float*, const void*, 
 hipError_t arena_conv_flip_weight(const void*, void*, int, int, int, int, hipStream_t);
 hipError_t arena_conv_flip_multi(int, const void* const*, void* const*, const int*, const int*,
                                  const int*, hipStream_t);
-hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void*, const void*,
-                             const uint8_t*, const float*, int, int, int, int, int, int, int, int,
-                             int, int, int, int, const int*, int, int, hipStream_t);
+hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void*, const uint8_t*,
+                             const void*, const uint8_t*, const float*, int, int, int, int, int,
+                             int, int, int, int, int, int, int, const int*, int, int, hipStream_t);
 hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
                                int, int, int, int, int, int, int, int, int, int, int, float,
                                hipStream_t);
@@ -865,7 +865,7 @@ void pool_check(const Tensor& t, const char* name) {
 // sum g, sum g * (bn_x - bn_mean)) for bn_bwd(..., ext_part, BM) instead of forward statistics.
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant,
                              bool with_stats, OptT addend, OptT bn_x, OptT bn_mask,
-                             OptT bn_mean) {
+                             OptT bn_mean, OptT addmask) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4,
               "conv_fwd: x and w must be 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16,
@@ -910,16 +910,24 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                   "conv_fwd: bn_mask must be uint8 with numel(y) / 8 bytes");
     }
   }
-  check_hip(arena_conv_fwd(x.data_ptr(), w.data_ptr(), y.data_ptr(),
-                           with_stats ? part.data_ptr<float>() : nullptr,
-                           addend.has_value() ? addend->data_ptr() : nullptr,
-                           bn_x.has_value() ? bn_x->data_ptr() : nullptr,
-                           bn_x.has_value() && bn_mask.has_value() ? bn_mask->data_ptr<uint8_t>()
-                                                                   : nullptr,
-                           bn_x.has_value() ? bn_mean->data_ptr<float>() : nullptr,
-                           (int)N, (int)H, (int)W,
-                           (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad, (int)variant,
-                           cur_stream()),
+  if (addmask.has_value()) {
+    TORCH_CHECK(addend.has_value() && addmask->scalar_type() == torch::kUInt8 &&
+                    addmask->is_contiguous() && addmask->device() == y.device() &&
+                    addmask->numel() == y.numel() / 8,
+                "conv_fwd: addmask needs an addend and numel(y) / 8 uint8 bytes");
+  }
+  check_hip(arena_conv_fwd_ex(x.data_ptr(), w.data_ptr(), y.data_ptr(),
+                              with_stats ? part.data_ptr<float>() : nullptr,
+                              addend.has_value() ? addend->data_ptr() : nullptr,
+                              addmask.has_value() ? addmask->data_ptr<uint8_t>() : nullptr,
+                              bn_x.has_value() ? bn_x->data_ptr() : nullptr,
+                              bn_x.has_value() && bn_mask.has_value()
+                                  ? bn_mask->data_ptr<uint8_t>()
+                                  : nullptr,
+                              bn_x.has_value() ? bn_mean->data_ptr<float>() : nullptr,
+                              (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R, (int)S,
+                              (int)stride, (int)pad, (int)pad, 0, 0, nullptr, 0, (int)variant,
+                              cur_stream()),
             "conv_fwd");
   if (with_stats) return {y, part};
   return {y};
@@ -1071,7 +1079,8 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
   check_hip(arena_conv_fwd_ex(x.data_ptr(), w.data_ptr(), y.data_ptr(),
                               with_stats ? part.data_ptr<float>() : nullptr,
                               addend.has_value() ? addend->data_ptr() : nullptr, nullptr, nullptr,
-                              nullptr, (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R, (int)S,
+                              nullptr, nullptr, (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R,
+                              (int)S,
                               (int)stride, (int)pad_h, (int)pad_w, (int)Ho, (int)Wo,
                               y_out.has_value() ? map6.data() : nullptr, c16 ? 1 : 0,
                               (int)variant, cur_stream()),
@@ -1341,7 +1350,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("variant"), py::arg("with_stats"), py::arg("addend") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
-        py::arg("bn_mean") = py::none());
+        py::arg("bn_mean") = py::none(), py::arg("addmask") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

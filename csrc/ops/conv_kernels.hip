@@ -54,6 +54,10 @@ struct ConvArgs {
   float* part;         // optional BatchNorm partials [m_tiles][2][Cout] (tile mean, tile M2)
   const uint16_t* add; // optional [M][Cout] bf16 added to the fp32 sums before rounding (the
                        // other gradient of a tensor with two consumers: the residual join)
+  // optional bit mask of the addend, [M][Cout / 8] bytes, bit i of byte v <-> element 8v + i:
+  // only set elements are added. The residual join's other gradient is dY of a ReLU'd BatchNorm
+  // times its ReLU mask; taking (dY, mask) spares the BN backward writing that product.
+  const uint8_t* addmask;
   // BatchNorm-backward partials of the output (EPI 2, a backward-data pass whose output dY is the
   // gradient of a BN layer's output): g = dY (* ReLU mask bit); part[tile][0][c] = sum g,
   // part[tile][1][c] = sum g * (bnx - bnmean[c]) -- the bn_bwd_reduce partial format.
@@ -100,6 +104,32 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+
+// 8 bf16 addend elements at element offset `off` (a multiple of 8), zeroed where the mask bit is 0
+__device__ __forceinline__ uint4 masked_add8(const uint16_t* add, const uint8_t* mask,
+                                             size_t off) {
+  uint4 q = *reinterpret_cast<const uint4*>(add + off);
+  if (mask != nullptr) {
+    const uint32_t mk = mask[off >> 3];
+    uint32_t* w = reinterpret_cast<uint32_t*>(&q);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      w[e] &= ((mk >> (2 * e)) & 1u ? 0x0000ffffu : 0u) | ((mk >> (2 * e + 1)) & 1u ? 0xffff0000u : 0u);
+  }
+  return q;
+}
+
+// 4 bf16 addend elements at element offset `off` (a multiple of 4), masked likewise
+__device__ __forceinline__ uint2 masked_add4(const uint16_t* add, const uint8_t* mask,
+                                             size_t off) {
+  uint2 q = *reinterpret_cast<const uint2*>(add + off);
+  if (mask != nullptr) {
+    const uint32_t mk = (uint32_t)mask[off >> 3] >> (off & 7);
+    q.x &= ((mk & 1u) ? 0x0000ffffu : 0u) | ((mk & 2u) ? 0xffff0000u : 0u);
+    q.y &= ((mk & 4u) ? 0x0000ffffu : 0u) | ((mk & 8u) ? 0xffff0000u : 0u);
+  }
+  return q;
+}
 
 // bf16 round-to-nearest-even of two floats, packed (lo = a): ONE v_cvt_pk_bf16_f32 on gfx950.
 // The integer form (add 0x7fff + lsb, shift) took ~9 VALU ops per pair, which on the streaming-
@@ -368,7 +398,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         }
         const size_t off = pix * a.Cout + n0 + cc * 8;
         if (a.add != nullptr) {
-          const uint4 qa = *reinterpret_cast<const uint4*>(a.add + off);
+          const uint4 qa = masked_add8(a.add, a.addmask, off);
           const uint32_t u[4] = {qa.x, qa.y, qa.z, qa.w};
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -388,7 +418,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
               if ((da == 0 && db == 0) || wy >= a.Wy) continue;
               const size_t so = (((size_t)n * a.Hy + hy) * a.Wy + wy) * a.Cout + n0 + cc * 8;
               *reinterpret_cast<uint4*>(a.y + so) =
-                  a.add ? *reinterpret_cast<const uint4*>(a.add + so) : make_uint4(0u, 0u, 0u, 0u);
+                  a.add ? masked_add8(a.add, a.addmask, so) : make_uint4(0u, 0u, 0u, 0u);
             }
           }
         }
@@ -420,7 +450,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
           const size_t off = (((size_t)n * a.Hy + hy) * a.Wy + wy) * a.Cout + n0 + wn * WN + 4 * fq;
 #pragma unroll
           for (int j = 0; j < NI; ++j) {
-            const uint2 v = a.add ? *reinterpret_cast<const uint2*>(a.add + off + j * 16)
+            const uint2 v = a.add ? masked_add4(a.add, a.addmask, off + j * 16)
                                   : make_uint2(0u, 0u);
             *reinterpret_cast<uint2*>(a.y + off + j * 16) = v;
           }
@@ -428,10 +458,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
       }
     }
     if (a.add != nullptr) {
-      const uint16_t* arow = a.add + (yrow - a.y);
+      const size_t aoff = (size_t)(yrow - a.y);
       uint2 q[NI];
 #pragma unroll
-      for (int j = 0; j < NI; ++j) q[j] = *reinterpret_cast<const uint2*>(arow + j * 16);
+      for (int j = 0; j < NI; ++j) q[j] = masked_add4(a.add, a.addmask, aoff + j * 16);
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         acc[i][j][0] += __uint_as_float(q[j].x << 16);
@@ -640,6 +670,7 @@ extern "C" {
 // bnx/bnmask/bnmean (optional, with part): the backward-data form, part = BatchNorm-backward
 // partials of y instead of forward statistics (see ConvArgs).
 hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part, const void* add,
+                             const uint8_t* addmask,
                              const void* bnx, const uint8_t* bnmask, const float* bnmean, int N,
                              int H, int W, int C, int Cout, int R, int S, int stride, int pad_h,
                              int pad_w, int Ho, int Wo, const int* y_map, int c16, int variant,
@@ -652,6 +683,8 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.y = (uint16_t*)y;
   a.part = part;
   a.add = (const uint16_t*)add;
+  a.addmask = add != nullptr ? addmask : nullptr;
+  if (addmask != nullptr && Cout % 8) return hipErrorInvalidValue;
   a.bnx = (const uint16_t*)bnx;
   a.bnmask = bnmask;
   a.bnmean = bnmean;
@@ -701,7 +734,7 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
                           const void* bnx, const uint8_t* bnmask, const float* bnmean,
                           int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad,
                           int variant, hipStream_t st) {
-  return arena_conv_fwd_ex(x, w, y, part, add, bnx, bnmask, bnmean, N, H, W, C, Cout, R, S,
+  return arena_conv_fwd_ex(x, w, y, part, add, nullptr, bnx, bnmask, bnmean, N, H, W, C, Cout, R, S,
                            stride, pad, pad, 0, 0, nullptr, 0, variant, st);
 }
 

@@ -6,8 +6,9 @@ Builds one model + optimizer + synthetic batch per variant (same seed), warms ea
 ``--chunk`` timed replays of each variant for ``--rounds`` rounds, so clock/thermal drift hits
 every variant alike (cdna_hip_programming.md §5.4 rule 24). Variants are conv modes
 (ARENA_CONV values), optionally suffixed ``:async`` (weight gradients on a side stream) and/or
-``:link`` (BN-backward partials in the dgrad epilogues) and/or ``:torchstem`` (the stem's
-input/weight casts and weight transform as torch ops), joined with ``+``.
+``:link`` (BN-backward partials in the dgrad epilogues), ``:torchstem`` (the stem's
+input/weight casts and weight transform as torch ops) and/or ``:nomask`` (the last BN writes
+dy * mask for the residual join instead of parking (dy, bits)), joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
     python scripts/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
@@ -50,6 +51,7 @@ def main():
         conv.set_async_wgrad("async" in opt_s.split("+"))
         conv.set_bn_links("link" in opt_s.split("+"))
         conv.set_stem_fused("torchstem" not in opt_s.split("+"))
+        conv.set_masked_join("nomask" not in opt_s.split("+"))
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
             cnn_bench.train_step(model, opt, x, y, torch.bfloat16)

@@ -215,7 +215,7 @@ def test_grad_join_matches_autograd_sum(mode, monkeypatch):
     monkeypatch.setattr(torch.backends.cudnn, "deterministic", True)
 
     class NoJoin(conv.GradJoin):
-        def register(self):
+        def register(self, takes_masked=False):
             return self   # never reaches two consumers: both behave as plain autograd
 
     try:
@@ -515,3 +515,67 @@ def test_s2d_stem_fp32_input_rounds_like_the_cast():
     a = _ext.load().s2d_stem(x)
     b = _ext.load().s2d_stem(x.to(torch.bfloat16))
     assert a.dtype == torch.bfloat16 and torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_masked_residual_join_matches_materialized():
+    """Identity blocks whose last BN parks (dy, ReLU bits) in the residual join (the conv's
+    backward-data epilogue adds dy where the bit is set) give the same gradients, bit for bit,
+    as the BN writing dy * mask; and the masked path is the one taken."""
+    from arena_amd.models import resnet as R
+    conv.set_mode("ours")
+    made = []
+    orig = conv.MaskedGrad.__init__
+
+    def spy(self, g, bits):
+        made.append(1)
+        orig(self, g, bits)
+
+    try:
+        torch.manual_seed(0)
+        net = torch.nn.ModuleList([R.Bottleneck(256, 64, 1), R.Bottleneck(256, 64, 1)]).cuda()
+        net = net.to(memory_format=torch.channels_last)
+        with torch.no_grad():
+            for b in net:
+                b.bn3.weight.uniform_(0.5, 1.5)
+        x0 = torch.randn(4, 256, 12, 12, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        g = torch.randn(4, 256, 12, 12, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        out = {}
+        conv.MaskedGrad.__init__ = spy
+        for on in (True, False):
+            conv.set_masked_join(on)
+            made.clear()
+            net.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = net[1](net[0](x))
+            y.backward(g)
+            out[on] = (x.grad.clone(), {n: p.grad.clone() for n, p in net.named_parameters()},
+                       len(made))
+        assert out[True][2] == 2 and out[False][2] == 0, (out[True][2], out[False][2])
+        assert torch.equal(out[True][0], out[False][0])
+        for n, gp in out[False][1].items():
+            assert torch.equal(out[True][1][n], gp), n
+    finally:
+        conv.MaskedGrad.__init__ = orig
+        conv.set_masked_join(True)
+        conv.set_mode(None)
+
+
+@pytest.mark.gpu
+def test_conv_masked_addend_matches_torch():
+    """conv2d_bwd_data with a bit-masked addend equals adding addend * mask."""
+    torch.manual_seed(0)
+    x, w = _data(2, 64, 9, 11, 128, 3, "cuda")
+    dy = torch.randn(2, 128, 9, 11, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    add = torch.randn(2, 64, 9, 11, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    bits = torch.randint(0, 256, (add.numel() // 8,), device="cuda", dtype=torch.uint8)
+    dense = conv.MaskedGrad(add, bits).materialize()
+    for v in conv.variants_for(64):
+        a = conv.conv2d_bwd_data(dy, w, 1, v, addend=add, addmask=bits)
+        b = conv.conv2d_bwd_data(dy, w, 1, v, addend=dense)
+        assert torch.equal(a, b), v
