@@ -23,7 +23,7 @@ from typing import List
 import torch
 from torch import nn
 
-from ..ops.batchnorm import BatchNormAct2d
+from ..ops.batchnorm import BatchNormAct2d, ResidualMask
 from ..ops.conv import BNGradLink, Conv2dNHWC, GradJoin, StemConv2d, WeightFlipper
 from ..ops.pool import MaxPool2dNHWC
 
@@ -66,14 +66,16 @@ class Bottleneck(nn.Module):
         join = GradJoin() if train else None
         lk1, lk2 = (BNGradLink(), BNGradLink()) if train else (None, None)
         idt = x
+        # downsample block: bn3's residual gradient reaches down_bn as (dy, bn3's ReLU mask)
+        rmask = ResidualMask() if (train and self.down_conv is not None) else None
         if self.down_conv is not None:
             y, st = self.down_conv.forward_stats(x, join=join, bn_link=link)
-            idt = self.down_bn(y, stats=st)
+            idt = self.down_bn(y, stats=st, res_in=rmask)
         y, st = self.conv1.forward_stats(x, join=join, bn_link=link)
         y, st = self.conv2.forward_stats(self.bn1(y, stats=st, link=lk1), bn_link=lk1)
         y, st = self.conv3.forward_stats(self.bn2(y, stats=st, link=lk2), bn_link=lk2)
         return self.bn3(y, residual=idt, stats=st, join=join if self.down_conv is None else None,
-                        link=link_out)
+                        link=link_out, res_out=rmask)
 
 
 class ResNet(nn.Module):

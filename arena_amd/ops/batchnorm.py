@@ -51,10 +51,32 @@ def reference(x, residual, weight, bias, running_mean, running_var, training, mo
     return F.relu(y) if relu else y
 
 
+class ResidualMask:
+    """The residual gradient of ``relu(bn3(x) + r)`` is dy * ReLU mask. When r is the output of
+    another fused BN (a downsample block's ``down_bn``), bn3's backward returns dy itself for r and
+    hands over the mask here, and down_bn's backward applies it as if it had a ReLU: its reduction
+    and dx passes already read a mask, so dy * mask is never written. The gradient down_bn
+    receives is the unmasked dy whenever bn3 published, so ``take`` always returns the mask then.
+    bn3 only publishes when down_bn ran on the fused kernels (``armed`` by its forward), the only
+    path whose backward takes the mask."""
+    __slots__ = ("armed", "mask")
+
+    def __init__(self):
+        self.armed, self.mask = False, None
+
+    def publish(self, mask: torch.Tensor) -> None:
+        self.mask = mask
+
+    def take(self):
+        m, self.mask = self.mask, None
+        return m
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum,
-                eps, relu, num_batches=None, stats=None, join=None, link=None):
+                eps, relu, num_batches=None, stats=None, join=None, link=None, res_out=None,
+                res_in=None):
         ext = _ext.load()
         part, rpb = stats if (stats is not None and training) else (None, 0)
         y, mean, invstd, mask = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
@@ -70,6 +92,13 @@ class _BNActFn(torch.autograd.Function):
         if link is not None and training and x.dtype == torch.bfloat16:
             link.set_bn(x, mask if relu else None, mean)
             ctx.link = link
+        # res_out: this BN's residual is another fused BN's output (see ResidualMask);
+        # res_in: this BN's output is that residual
+        ctx.res_out = res_out if (res_out is not None and res_out.armed and residual is not None
+                                  and relu and training and conv.masked_join()) else None
+        ctx.res_in = res_in if training else None
+        if res_in is not None:
+            res_in.armed = training
         return y
 
     @staticmethod
@@ -80,16 +109,27 @@ class _BNActFn(torch.autograd.Function):
                                "fused kernels; use train() or the PyTorch path")
         dy = dy.contiguous(memory_format=torch.channels_last)
         ext = ctx.link.take(dy) if ctx.link is not None else None
+        relu = ctx.relu
+        if ctx.res_in is not None:   # the consumer BN handed over its ReLU mask for this dy
+            m = ctx.res_in.take()
+            if m is not None:
+                relu, mask = True, m
         # the residual gradient is dy * ReLU mask; when this BN reaches the residual join first
         # and the other consumer's dgrad epilogue takes a masked addend, park (dy, mask) instead
         # of writing that product (one full write of the block input's size saved)
         masked = (ctx.has_res and ctx.relu and mask is not None and conv.masked_join()
                   and ctx.join is not None and ctx.join.active() and ctx.needs_input_grad[1]
                   and ctx.join.other() is None and ctx.join.peer_takes_masked())
-        dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, mask, x, mean, invstd, weight, ctx.relu,
-                                                     ctx.has_res and not masked, ctx.affine,
-                                                     ext[0] if ext else None, ext[1] if ext else 0)
-        if masked:
+        to_res = (not masked and ctx.res_out is not None and ctx.has_res and mask is not None
+                  and ctx.needs_input_grad[1] and ctx.join is None)
+        dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, mask, x, mean, invstd, weight, relu,
+                                                     ctx.has_res and not masked and not to_res,
+                                                     ctx.affine, ext[0] if ext else None,
+                                                     ext[1] if ext else 0)
+        if to_res:
+            ctx.res_out.publish(mask)
+            dres = dy
+        elif masked:
             parked = ctx.join.park_or_take(conv.MaskedGrad(dy, mask))
             assert parked, "masked residual gradient must be the join's first arrival"
             dres = None
@@ -103,7 +143,7 @@ class _BNActFn(torch.autograd.Function):
                 dres = None
         return (dx, dres, dgamma if ctx.affine else None,
                 dbeta if ctx.affine else None, None, None, None, None, None, None, None, None,
-                None, None)
+                None, None, None, None)
 
 
 def bn_act(x, residual=None, weight=None, bias=None, running_mean=None, running_var=None,
@@ -126,11 +166,13 @@ class BatchNormAct2d(nn.BatchNorm2d):
         self.relu = act == "relu"
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
-                stats=None, join=None, link=None) -> torch.Tensor:
+                stats=None, join=None, link=None, res_out=None, res_in=None) -> torch.Tensor:
         """``stats``: BatchNorm partials of ``x`` from the producing ``Conv2dNHWC.forward_stats``
         (skips the statistics pass over x; training mode on the fused kernels only).
         ``join``: a ``GradJoin`` the residual's other consumer is registered on.
-        ``link``: a ``BNGradLink`` handed to the conv that consumes the output."""
+        ``link``: a ``BNGradLink`` handed to the conv that consumes the output.
+        ``res_out`` / ``res_in``: a ``ResidualMask`` shared by the BN whose residual is this
+        other BN's output (res_out) and that other BN (res_in)."""
         training = self.training or not self.track_running_stats
         tracking = self.training and self.track_running_stats
         rm = self.running_mean if (not self.training or self.track_running_stats) else None
@@ -142,7 +184,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, True,
                                   self.momentum, self.eps, self.relu,
                                   self.num_batches_tracked if tracking else None, stats, join,
-                                  link)
+                                  link, res_out, res_in)
         if tracking:
             self.num_batches_tracked.add_(1)
         mom = self.momentum if self.momentum is not None else \
@@ -152,4 +194,4 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return reference(x, residual, self.weight, self.bias, rm, rv, training, mom,
                              self.eps, self.relu)
         return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, training, mom,
-                              self.eps, self.relu, None, None, join, link)
+                              self.eps, self.relu, None, None, join, link, res_out, res_in)

@@ -579,3 +579,50 @@ def test_conv_masked_addend_matches_torch():
         a = conv.conv2d_bwd_data(dy, w, 1, v, addend=add, addmask=bits)
         b = conv.conv2d_bwd_data(dy, w, 1, v, addend=dense)
         assert torch.equal(a, b), v
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,stride", [(128, 2), (64, 1)])
+def test_residual_mask_handoff_matches_materialized(cin, stride):
+    """A downsample block whose bn3 hands (dy, ReLU bits) to down_bn (ResidualMask) gives the same
+    gradients, bit for bit, as bn3 writing dy * mask for down_bn; the handoff is taken."""
+    from arena_amd.models import resnet as R
+    from arena_amd.ops import batchnorm as B
+    conv.set_mode("ours")
+    taken = []
+    orig = B.ResidualMask.take
+
+    def spy(self):
+        m = orig(self)
+        taken.append(m is not None)
+        return m
+
+    try:
+        torch.manual_seed(0)
+        blk = R.Bottleneck(cin, 64, stride).cuda().to(memory_format=torch.channels_last)
+        with torch.no_grad():
+            blk.bn3.weight.uniform_(0.5, 1.5)
+        x0 = torch.randn(4, cin, 14, 14, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        g = torch.randn(4, 256, 14 // stride, 14 // stride, device="cuda").to(
+            torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        B.ResidualMask.take = spy
+        out = {}
+        for on in (True, False):
+            conv.set_masked_join(on)
+            taken.clear()
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = blk(x)
+            y.backward(g)
+            out[on] = (x.grad.clone(), {n: p.grad.clone() for n, p in blk.named_parameters()},
+                       list(taken))
+        assert out[True][2] == [True] and out[False][2] == [False], (out[True][2], out[False][2])
+        assert torch.equal(out[True][0], out[False][0])
+        for n, gp in out[False][1].items():
+            assert torch.equal(out[True][1][n], gp), n
+    finally:
+        B.ResidualMask.take = orig
+        conv.set_masked_join(True)
+        conv.set_mode(None)
