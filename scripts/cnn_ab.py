@@ -8,7 +8,8 @@ every variant alike (cdna_hip_programming.md §5.4 rule 24). Variants are conv m
 (ARENA_CONV values), optionally suffixed ``:async`` (weight gradients on a side stream) and/or
 ``:link`` (BN-backward partials in the dgrad epilogues), ``:torchstem`` (the stem's
 input/weight casts and weight transform as torch ops) and/or ``:nomask`` (the last BN writes
-dy * mask for the residual join instead of parking (dy, bits)), joined with ``+``.
+dy * mask for the residual join instead of parking (dy, bits)) and/or ``:finP<n>`` (at most n
+level-1 blocks per channel group in the BN finalize kernels), joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
     python scripts/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
@@ -52,6 +53,11 @@ def main():
         conv.set_bn_links("link" in opt_s.split("+"))
         conv.set_stem_fused("torchstem" not in opt_s.split("+"))
         conv.set_masked_join("nomask" not in opt_s.split("+"))
+        # finP<n>: at most n level-1 blocks per channel group in the BN finalize kernels (the
+        # grid is baked into this variant's captured graph)
+        finp = [int(o[4:]) for o in opt_s.split("+") if o.startswith("finP")]
+        from arena_amd.ops import _ext as _e
+        _e.load().bn_set_fin_max_blocks(finp[0] if finp else 64)
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
             cnn_bench.train_step(model, opt, x, y, torch.bfloat16)

@@ -626,3 +626,22 @@ def test_residual_mask_handoff_matches_materialized(cin, stride):
         B.ResidualMask.take = orig
         conv.set_masked_join(True)
         conv.set_mode(None)
+
+
+def test_masked_grad_materialize_and_join_registration_cpu():
+    """MaskedGrad.materialize (the fallback for consumers without a masked epilogue) applies the
+    NHWC bit order of the BN kernels' ReLU mask; a join offers the masked form only when its first
+    registrant takes it."""
+    torch.manual_seed(0)
+    g = torch.randn(2, 16, 3, 5).contiguous(memory_format=torch.channels_last)
+    keep = torch.rand(2, 16, 3, 5) > 0.5
+    flat = keep.permute(0, 2, 3, 1).reshape(-1, 8).to(torch.uint8)   # NHWC order, 8 per byte
+    bits = (flat << torch.arange(8, dtype=torch.uint8)).sum(1).to(torch.uint8)
+    dense = conv.MaskedGrad(g, bits).materialize()
+    assert torch.equal(dense, torch.where(keep, g, torch.zeros_like(g)))
+    assert dense.is_contiguous(memory_format=torch.channels_last)
+    j = conv.GradJoin().register(takes_masked=True).register()
+    assert j.active() and j.peer_takes_masked()
+    j2 = conv.GradJoin().register(takes_masked=False).register()
+    assert j2.active() and not j2.peer_takes_masked()
+    assert not conv.GradJoin().register(takes_masked=True).peer_takes_masked()
