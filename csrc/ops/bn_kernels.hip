@@ -49,8 +49,20 @@ __device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (N
 // 8 channels of row `r`, group `g` (channels 8g..8g+7) as fp32.
 template <typename T>
 struct V8;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
 template <>
 struct V8<uint16_t> {
+  // non-temporal (last read of a streamed tensor in this pass sequence)
+  static __device__ __forceinline__ void loadnt(const uint16_t* p, float v[kVec]) {
+    const u32x4_t q = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      v[2 * i] = __uint_as_float(q[i] << 16);
+      v[2 * i + 1] = __uint_as_float(q[i] & 0xffff0000u);
+    }
+  }
   static __device__ __forceinline__ void load(const uint16_t* p, float v[kVec]) {
     const uint4 q = *reinterpret_cast<const uint4*>(p);
     const uint32_t w[4] = {q.x, q.y, q.z, q.w};
@@ -71,6 +83,12 @@ struct V8<uint16_t> {
 };
 template <>
 struct V8<float> {
+  static __device__ __forceinline__ void loadnt(const float* p, float v[kVec]) {
+    const f32x4_t a = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p));
+    const f32x4_t b = __builtin_nontemporal_load(reinterpret_cast<const f32x4_t*>(p + 4));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) { v[i] = a[i]; v[4 + i] = b[i]; }
+  }
   static __device__ __forceinline__ void load(const float* p, float v[kVec]) {
     const float4 a = *reinterpret_cast<const float4*>(p);
     const float4 b = *reinterpret_cast<const float4*>(p + 4);
@@ -337,7 +355,8 @@ __device__ __forceinline__ uint32_t pos_bits(const float o[kVec]) {
   return b;
 }
 
-template <typename T, bool RELU, bool RES>
+// NT: non-temporal loads of x (and res) -- their last read before the backward pass
+template <typename T, bool RELU, bool RES, bool NT>
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
                                                       const T* __restrict__ res,
                                                       T* __restrict__ y,
@@ -356,8 +375,13 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
       vv[u] = v0 + u * stride;
       ok[u] = vv[u] < nvec;
       const long long vc = ok[u] ? vv[u] : v0;
-      V8<T>::load(x + vc * kVec, a[u]);
-      if (RES) V8<T>::load(res + vc * kVec, b[u]);
+      if (NT) {
+        V8<T>::loadnt(x + vc * kVec, a[u]);
+        if (RES) V8<T>::loadnt(res + vc * kVec, b[u]);
+      } else {
+        V8<T>::load(x + vc * kVec, a[u]);
+        if (RES) V8<T>::load(res + vc * kVec, b[u]);
+      }
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -493,7 +517,8 @@ __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const float* __rest
 }
 
 // --------------------------------------------------------------------------------- backward dx
-template <typename T, bool RELU, bool RES>
+// NT: non-temporal loads of dy and x (their last read in the step)
+template <typename T, bool RELU, bool RES, bool NT>
 __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
                                                        const uint8_t* __restrict__ mask,
                                                        const T* __restrict__ x,
@@ -502,9 +527,9 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
   const long long stride = (long long)gridDim.x * kT;
   for (long long v = (long long)blockIdx.x * kT + threadIdx.x; v < nvec; v += stride) {
     float d[kVec], xv[kVec];
-    V8<T>::load(dy + v * kVec, d);
+    if (NT) V8<T>::loadnt(dy + v * kVec, d); else V8<T>::load(dy + v * kVec, d);
     const uint32_t mb = RELU ? (uint32_t)mask[v] : 0xffu;
-    V8<T>::load(x + v * kVec, xv);
+    if (NT) V8<T>::loadnt(x + v * kVec, xv); else V8<T>::load(x + v * kVec, xv);
     const int c0 = (int)(v & (cg - 1)) * kVec;
     float ca[kVec], cb[kVec], cc[kVec], mu[kVec];
     load8f(co.ca + c0, ca);
@@ -528,6 +553,7 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
 // 49 blocks and reached ~1 TB/s.
 // Both limits are runtime-tunable for sweeps (scripts/bn_bench.py); the workspace size follows.
 long long g_max_reduce_blocks = 512;
+int g_bn_nt = 1;           // non-temporal loads in the apply / dx passes (runtime switch for A/Bs)
 long long g_min_rounds = 8;
 
 long long reduce_blocks(long long M, int C, long long* rpb) {
@@ -555,6 +581,8 @@ bool bad_shape(long long M, int C) {
 extern "C" {
 
 void arena_bn_set_fin_max_blocks(int p) { g_fin_max_p = p < 1 ? 1 : (p > 64 ? 64 : p); }
+
+void arena_bn_set_nt(int on) { g_bn_nt = on ? 1 : 0; }
 
 void arena_bn_set_reduce_geometry(long long max_blocks, long long min_rounds) {
   g_max_reduce_blocks = max_blocks < 1 ? 1 : (max_blocks > 4096 ? 4096 : max_blocks);
@@ -602,10 +630,13 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
   const long long nvec = M * (C / kVec);
   const int nb = elementwise_blocks(nvec);
   const int cg = C / kVec;
-#define ARENA_BN_APPLY(TT, R, S)                                                             \
-  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S>), dim3(nb), dim3(kT), 0, stream,           \
+#define ARENA_BN_APPLY_NT(TT, R, S, NT)                                                      \
+  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S, NT>), dim3(nb), dim3(kT), 0, stream,       \
                      static_cast<const TT*>(x), static_cast<const TT*>(res), static_cast<TT*>(y), \
                      mask, st.mean, st.scale, st.shift, nvec, cg)
+#define ARENA_BN_APPLY(TT, R, S) \
+  do { if (g_bn_nt) ARENA_BN_APPLY_NT(TT, R, S, true); else ARENA_BN_APPLY_NT(TT, R, S, false); } \
+  while (0)
   const bool r = relu != 0, s = res != nullptr;
   if (dtype == 1) {
     if (r && s) ARENA_BN_APPLY(uint16_t, true, true);
@@ -619,6 +650,7 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
     else ARENA_BN_APPLY(float, false, false);
   }
 #undef ARENA_BN_APPLY
+#undef ARENA_BN_APPLY_NT
   return hipGetLastError();
 }
 
@@ -651,10 +683,13 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
   long long ne = (nvec + kT - 1) / kT;
   ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);
   const int cg = C / kVec;
-#define ARENA_BN_DX(TT, R, S)                                                                \
-  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S>), dim3(ne), dim3(kT), 0, stream,          \
+#define ARENA_BN_DX_NT(TT, R, S, NT)                                                         \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S, NT>), dim3(ne), dim3(kT), 0, stream,      \
                      static_cast<const TT*>(dy), mask, static_cast<const TT*>(x),            \
                      static_cast<TT*>(dx), static_cast<TT*>(dres), nvec, cg, co)
+#define ARENA_BN_DX(TT, R, S) \
+  do { if (g_bn_nt) ARENA_BN_DX_NT(TT, R, S, true); else ARENA_BN_DX_NT(TT, R, S, false); } \
+  while (0)
   const bool r = relu != 0, s = dres != nullptr;
   if (dtype == 1) {
     if (r && s) ARENA_BN_DX(uint16_t, true, true);
@@ -668,6 +703,7 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
     else ARENA_BN_DX(float, false, false);
   }
 #undef ARENA_BN_DX
+#undef ARENA_BN_DX_NT
   return hipGetLastError();
 }
 

@@ -58,6 +58,7 @@ def main():
         finp = [int(o[4:]) for o in opt_s.split("+") if o.startswith("finP")]
         from arena_amd.ops import _ext as _e
         _e.load().bn_set_fin_max_blocks(finp[0] if finp else 64)
+        _e.load().bn_set_nt(0 if "bnnt0" in opt_s.split("+") else 1)   # BN non-temporal loads
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
             cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
