@@ -76,6 +76,7 @@ long long arena_bn_lvl2_doubles(long long, int);
 void arena_bn_set_reduce_geometry(long long, long long);
 void arena_bn_set_fin_max_blocks(int);
 void arena_bn_set_nt(int);
+void arena_conv_set_wgrad_nt(int);
 // csrc/ops/pool_kernels.hip
 hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, int, int, int, int,
                              hipStream_t);
@@ -1357,6 +1358,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_set_fin_max_blocks", [](int64_t p) { arena_bn_set_fin_max_blocks((int)p); });
   m.def("bn_set_nt", [](int64_t on) { arena_bn_set_nt((int)on); });
+  m.def("conv_set_wgrad_nt", [](int64_t on) { arena_conv_set_wgrad_nt((int)on); });
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
     arena_bn_set_reduce_geometry(max_blocks, min_rounds);
   });

@@ -102,6 +102,11 @@ __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
 }
 
+// the same with the non-temporal cache policy (aux bit 1: nt)
+__device__ __forceinline__ void glds16nt(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 16, 0, 2);
+}
+
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
@@ -1099,6 +1104,7 @@ struct WgradArgs {
   FastDiv div_hw, div_w;
   int pad_w;           // left padding (pad is the top one)
   int c16;             // C == 16, a BN = 64 column tile = one filter row x 4 columns x 16 channels
+  int nt;              // stage dY and X with the non-temporal policy (this pass is their last read)
 };
 
 // chunk permutation of a pixel row of RB bytes (bit 0 of the chunk index is kept: 32-B pairs)
@@ -1161,7 +1167,8 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
       const void* src = m < a.M ? (const void*)(a.dy + (size_t)m * a.Cout + co0 +
                                                 (a_pos ^ wswz<RA>(row)) * 8)
                                 : (const void*)g_zero_page;
-      glds16(src, base + (wave * AI + i) * 1024);
+      if (a.nt) glds16nt(src, base + (wave * AI + i) * 1024);
+      else glds16(src, base + (wave * AI + i) * 1024);
     }
     uint8_t* bb = base + kPix * RA;
 #pragma unroll
@@ -1183,7 +1190,8 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
                       : (const void*)(a.x + ((size_t)(n * a.H + hi) * a.W + wi) * a.C + ci0 +
                                       cch * 8);
       }
-      glds16(src, bb + (wave * BI + i) * 1024);
+      if (a.nt) glds16nt(src, bb + (wave * BI + i) * 1024);
+      else glds16(src, bb + (wave * BI + i) * 1024);
     }
   };
 
@@ -1350,7 +1358,11 @@ hipError_t launch_wgrad(WgradArgs a, int splits_hint, bool serial, hipStream_t s
 
 }  // namespace
 
+int g_wgrad_nt = 0;   // non-temporal staging in the wgrad kernel (runtime switch for A/Bs)
+
 extern "C" {
+
+void arena_conv_set_wgrad_nt(int on) { g_wgrad_nt = on ? 1 : 0; }
 
 // Number of split slabs the wgrad launch will use (the caller sizes the workspace with it).
 int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int variant,
@@ -1386,6 +1398,7 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
   a.ws = ws;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
   a.stride = stride; a.pad = pad_h; a.pad_w = pad_w; a.c16 = c16;
+  a.nt = g_wgrad_nt;
   a.Ho = Ho > 0 ? Ho : (H + 2 * pad_h - R) / stride + 1;
   a.Wo = Wo > 0 ? Wo : (W + 2 * pad_w - S) / stride + 1;
   if (a.Ho <= 0 || a.Wo <= 0) return hipErrorInvalidValue;
