@@ -366,6 +366,13 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
                                                       const float* __restrict__ shift,
                                                       long long nvec, int cg) {
   const long long stride = (long long)gridDim.x * kT;
+  // every vector this thread touches has the same channel group: the grid stride is a multiple
+  // of kT, and cg divides kT (host-checked), so the per-channel coefficients load once
+  const int c0 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1)) * kVec;
+  float mu[kVec], sc[kVec], sh[kVec];
+  load8f(mean + c0, mu);
+  load8f(scale + c0, sc);
+  load8f(shift + c0, sh);
   for (long long v0 = (long long)blockIdx.x * kT + threadIdx.x; v0 < nvec; v0 += 2 * stride) {
     float a[2][kVec], b[2][kVec];
     bool ok[2];
@@ -385,11 +392,6 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int c0 = (int)(vv[u] & (cg - 1)) * kVec;  // cg is a power of two (host-checked)
-      float mu[kVec], sc[kVec], sh[kVec];
-      load8f(mean + c0, mu);
-      load8f(scale + c0, sc);
-      load8f(shift + c0, sh);
       float o[kVec];
 #pragma unroll
       for (int i = 0; i < kVec; ++i) {
@@ -525,17 +527,18 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
                                                        T* __restrict__ dx, T* __restrict__ dres,
                                                        long long nvec, int cg, ArenaBNBwd co) {
   const long long stride = (long long)gridDim.x * kT;
+  // fixed channel group per thread (grid stride = multiple of kT, cg | kT): coefficients once
+  const int c0 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1)) * kVec;
+  float ca[kVec], cb[kVec], cc[kVec], mu[kVec];
+  load8f(co.ca + c0, ca);
+  load8f(co.cb + c0, cb);
+  load8f(co.cc + c0, cc);
+  load8f(co.mean + c0, mu);
   for (long long v = (long long)blockIdx.x * kT + threadIdx.x; v < nvec; v += stride) {
     float d[kVec], xv[kVec];
     if (NT) V8<T>::loadnt(dy + v * kVec, d); else V8<T>::load(dy + v * kVec, d);
     const uint32_t mb = RELU ? (uint32_t)mask[v] : 0xffu;
     if (NT) V8<T>::loadnt(x + v * kVec, xv); else V8<T>::load(x + v * kVec, xv);
-    const int c0 = (int)(v & (cg - 1)) * kVec;
-    float ca[kVec], cb[kVec], cc[kVec], mu[kVec];
-    load8f(co.ca + c0, ca);
-    load8f(co.cb + c0, cb);
-    load8f(co.cc + c0, cc);
-    load8f(co.mean + c0, mu);
     float g[kVec], o[kVec];
 #pragma unroll
     for (int i = 0; i < kVec; ++i) {
