@@ -39,18 +39,14 @@ constexpr int kT = 256;      // threads per block
 constexpr int kVec = 8;      // channels per thread
 constexpr int kMaxC = 2048;  // C / kVec <= kT
 
-__device__ __forceinline__ uint16_t f2bf(float f) {  // round to nearest even (NaN stays NaN)
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
 
 // 8 channels of row `r`, group `g` (channels 8g..8g+7) as fp32.
 template <typename T>
 struct V8;
 typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
 
 template <>
 struct V8<uint16_t> {
@@ -72,13 +68,28 @@ struct V8<uint16_t> {
       v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
     }
   }
+  // round to nearest even, two per v_cvt_pk_bf16_f32 (NaN stays NaN, quieted)
+  static __device__ __forceinline__ uint32_t pack2(float a, float b) {
+    const f32x2_t v = {a, b};
+    return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+  }
   static __device__ __forceinline__ void store(uint16_t* p, const float v[kVec]) {
-    uint4 q;
-    q.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    q.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    q.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-    q.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-    *reinterpret_cast<uint4*>(p) = q;
+    *reinterpret_cast<uint4*>(p) = make_uint4(pack2(v[0], v[1]), pack2(v[2], v[3]),
+                                              pack2(v[4], v[5]), pack2(v[6], v[7]));
+  }
+  // store, and return the bits of the stored (rounded) values that are > 0 (not NaN)
+  static __device__ __forceinline__ uint32_t store_pos(uint16_t* p, const float v[kVec]) {
+    const uint32_t w[4] = {pack2(v[0], v[1]), pack2(v[2], v[3]), pack2(v[4], v[5]),
+                           pack2(v[6], v[7])};
+    *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+    uint32_t b = 0;
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      const uint32_t h = (i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xffffu);
+      const bool pos = (h & 0x8000u) == 0 && (h & 0x7fffu) != 0 && (h & 0x7fffu) <= 0x7f80u;
+      b |= (pos ? 1u : 0u) << i;
+    }
+    return b;
   }
 };
 template <>
@@ -98,6 +109,13 @@ struct V8<float> {
   static __device__ __forceinline__ void store(float* p, const float v[kVec]) {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+  static __device__ __forceinline__ uint32_t store_pos(float* p, const float v[kVec]) {
+    store(p, v);
+    uint32_t b = 0;
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) b |= (v[i] > 0.f ? 1u : 0u) << i;
+    return b;
   }
 };
 
@@ -336,24 +354,8 @@ __global__ __launch_bounds__(kT) void bn_stats_finalize_kernel(const float* __re
 
 // ------------------------------------------------------------------------------------ apply
 // y = act((x - mean) * scale + shift (+ res)), 2 vectors per thread per round for load ILP.
-// Bits of the 8 stored outputs that are > 0 (after the rounding the store applies, so the mask is
-// exactly "saved y > 0").
-template <typename T>
-__device__ __forceinline__ uint32_t pos_bits(const float o[kVec]) {
-  uint32_t b = 0;
-#pragma unroll
-  for (int i = 0; i < kVec; ++i) {
-    bool p;
-    if constexpr (sizeof(T) == 2) {
-      const uint16_t h = f2bf(o[i]);
-      p = (h & 0x8000u) == 0 && (h & 0x7fffu) != 0 && (h & 0x7fffu) <= 0x7f80u;
-    } else {
-      p = o[i] > 0.f;
-    }
-    b |= (p ? 1u : 0u) << i;
-  }
-  return b;
-}
+// The mask bits are those of the stored (rounded) outputs that are > 0: exactly "saved y > 0"
+// (V8::store_pos).
 
 // NT: non-temporal loads of x (and res) -- their last read before the backward pass
 template <typename T, bool RELU, bool RES, bool NT>
@@ -400,8 +402,10 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
         o[i] = RELU ? fmaxf(t, 0.f) : t;
       }
       if (ok[u]) {
-        V8<T>::store(y + vv[u] * kVec, o);
-        if (RELU && mask != nullptr) mask[vv[u]] = (uint8_t)pos_bits<T>(o);
+        if (RELU && mask != nullptr)
+          mask[vv[u]] = (uint8_t)V8<T>::store_pos(y + vv[u] * kVec, o);
+        else
+          V8<T>::store(y + vv[u] * kVec, o);
       }
     }
   }
