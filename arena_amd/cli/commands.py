@@ -151,6 +151,7 @@ def cmd_submit_tf(ctx, ns) -> int:
     a.worker_cpu, a.worker_memory = ns.workerCpu, ns.workerMemory
     a.ps_cpu, a.ps_memory = ns.psCpu, ns.psMemory
     a.clean_pod_policy = ns.cleanTaskPolicy
+    a.tf_operator = ns.tfOperator
     _fill_sync_tb(a, ns)
     return _submit(ctx, a, _command_args(ns))
 
@@ -372,6 +373,9 @@ def build_parser() -> argparse.ArgumentParser:
     tf.add_argument("--psMemory", default="", help="the memory resource for the PS")
     tf.add_argument("--cleanTaskPolicy", default="Running",
                     help="How to clean tasks after Training is done, only support Running, None.")
+    tf.add_argument("--tfOperator", action="store_true",
+                    help="render a kubeflow.org TFJob for a cluster running tf-operator, instead "
+                         "of the built-in per-task Jobs + headless Services")
     tf.set_defaults(func=cmd_submit_tf)
 
     mpi = ssub.add_parser("mpijob", aliases=["mpi"], help="Submit an allreduce (MPI) job.")

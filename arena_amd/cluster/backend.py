@@ -89,6 +89,10 @@ class Backend(abc.ABC):
     def delete_service(self, namespace: str, name: str) -> None: ...
 
     @abc.abstractmethod
+    def delete_job(self, namespace: str, name: str) -> None:
+        """Delete a batch Job and its pods (jobmon's cleanPodPolicy for PS/worker jobs)."""
+
+    @abc.abstractmethod
     def ensure_namespace(self, namespace: str) -> None: ...
 
     @abc.abstractmethod

@@ -13,6 +13,7 @@ SURVEY §2.7) with plain functions. The object names, labels and env contract ar
 from __future__ import annotations
 
 import copy
+import json
 from typing import Dict, List
 
 from ..runtime.heartbeat import liveness_probe
@@ -20,6 +21,9 @@ from .objects import AMD_GPU
 
 ARENA_SYSTEM_NS = "arena-system"
 JOBMON_IMAGE = "arena-amd/jobmon:latest"
+# what the jobmon Job runs; deploy/jobmon.Dockerfile installs the package so this module (and the
+# `arena-jobmon` console script) exists in the image -- tests/test_charts_golden.py checks both
+JOBMON_COMMAND = ("python", "-m", "arena_amd.runtime.jobmon")
 
 
 def fullname(release: str, chart: str) -> str:
@@ -81,14 +85,21 @@ def _sync_init_containers(values: dict) -> List[dict]:
              "volumeMounts": [{"name": "code-sync", "mountPath": "/code"}]}]
 
 
+def _field_env_list(fields: Dict[str, str]) -> List[dict]:
+    """Downward-API env (``valueFrom.fieldRef``): the kubelet resolves these per pod."""
+    return [{"name": k, "valueFrom": {"fieldRef": {"fieldPath": v}}}
+            for k, v in sorted(fields.items())]
+
+
 def _container(name: str, values: dict, image: str, gpus: int, cpu="", memory="",
-               extra_env=None, mounts=None, ports=None, command=None) -> dict:
+               extra_env=None, mounts=None, ports=None, command=None, field_env=None) -> dict:
     env = dict(values.get("envs") or {})
     env.update(extra_env or {})
     c = {"name": name, "image": image,
          "command": command or ["sh", "-c", values.get("command", "")],
          "workingDir": values.get("workingDir", "/root"),
-         "env": _env_list(env), "resources": _resources(values, gpus, cpu, memory),
+         "env": _env_list(env) + _field_env_list(field_env or {}),
+         "resources": _resources(values, gpus, cpu, memory),
          "volumeMounts": list(mounts or [])}
     if ports:
         c["ports"] = ports
@@ -131,6 +142,17 @@ def _tensorboard(release: str, ns: str, values: dict, app: str, affinity_labels=
     ]
 
 
+def _net_spec(values: dict, **extra) -> dict:
+    """hostNetwork (the charts' default) + the DNS policy that keeps cluster DNS working under it:
+    with plain ``ClusterFirst`` a hostNetwork pod resolves names like the node does, so the
+    headless-Service names used for rendezvous (``<fullname>-master``, ``<tfjob>-ps-0``) would
+    not resolve."""
+    host = bool(values.get("useHostNetwork", True))
+    spec = {"hostNetwork": host, "dnsPolicy": "ClusterFirstWithHostNet" if host else "ClusterFirst"}
+    spec.update(extra)
+    return spec
+
+
 def _log_mount(values: dict):
     if not values.get("useTensorboard"):
         return [], []
@@ -148,21 +170,109 @@ def render_training(release: str, ns: str, values: dict) -> List[dict]:
     vols += lv
     mounts += lm
     pod = {"metadata": {"labels": dict(labels)},
-           "spec": {"restartPolicy": "Never", "hostNetwork": values.get("useHostNetwork", True),
-                    "initContainers": _sync_init_containers(values),
-                    "containers": [_container("job", values, values.get("image", ""),
-                                              int(values.get("gpuCount", 0)),
-                                              values.get("cpu", ""), values.get("memory", ""),
-                                              mounts=mounts)],
-                    "volumes": vols}}
+           "spec": _net_spec(values, restartPolicy="Never",
+                             initContainers=_sync_init_containers(values),
+                             containers=[_container("job", values, values.get("image", ""),
+                                                    int(values.get("gpuCount", 0)),
+                                                    values.get("cpu", ""),
+                                                    values.get("memory", ""), mounts=mounts)],
+                             volumes=vols)}
     out = [{"apiVersion": "batch/v1", "kind": "Job",
             "metadata": {"name": name, "namespace": ns, "labels": {**labels, "role": "job"}},
             "spec": {"backoffLimit": int(values.get("retry", 0)), "template": pod}}]
     return out + _tensorboard(release, ns, values, "training")
 
 
+def tf_cluster_spec(release: str, ns: str, values: dict) -> Dict[str, List[str]]:
+    """The TF_CONFIG ``cluster`` of a PS/worker job: one stable DNS name per task, the headless
+    Service ``<release>-tfjob-<type>-<i>`` rendered next to each task's Job (what tf-operator
+    generates; trainer_tensorflow.go:357-418 relies on the same per-replica identity)."""
+    name = f"{release}-tfjob"
+    out: Dict[str, List[str]] = {}
+    for t, n, port in (("ps", int(values.get("ps", 0)), int(values.get("psPort", 22223))),
+                       ("worker", int(values.get("workers", 1)),
+                        int(values.get("workerPort", 22222)))):
+        if n > 0:
+            out[t] = [f"{name}-{t}-{i}.{ns}.svc:{port}" for i in range(n)]
+    return out
+
+
+def _tf_task_pod(release: str, ns: str, values: dict, rtype: str, index: int,
+                 cluster: Dict[str, List[str]], vols, mounts) -> dict:
+    name = f"{release}-tfjob"
+    is_ps = rtype == "ps"
+    labels = {"app": "tfjob", "release": release, "group_name": "kubeflow.org",
+              "tf-replica-type": rtype, "tf-replica-index": str(index), "tf_job_name": name}
+    tf_config = json.dumps({"cluster": cluster, "task": {"type": rtype, "index": index},
+                            "environment": "cloud"}, sort_keys=True)
+    port = int(values.get("psPort" if is_ps else "workerPort", 22223 if is_ps else 22222))
+    lv, lm = ([], []) if is_ps else _log_mount(values)
+    ctr = _container("tensorflow", values,
+                     values.get("psImage" if is_ps else "workerImage", ""),
+                     0 if is_ps else int(values.get("gpuCount", 0)),
+                     values.get("psCPU" if is_ps else "workerCPU", ""),
+                     values.get("psMemory" if is_ps else "workerMemory", ""),
+                     extra_env={"TF_CONFIG": tf_config, "MX_CLUSTER_SPEC": tf_config},
+                     mounts=mounts + lm,
+                     ports=[{"name": "tfjob-port", "containerPort": port}])
+    return {"metadata": {"labels": labels},
+            "spec": _net_spec(values, restartPolicy="Never",
+                              hostPID=values.get("useHostPID", True),
+                              hostIPC=values.get("useHostIPC", True),
+                              initContainers=_sync_init_containers(values),
+                              containers=[ctr], volumes=list(vols) + lv)}
+
+
 def render_tfjob(release: str, ns: str, values: dict) -> List[dict]:
-    """PS/worker job: kubeflow.org/v1alpha2 TFJob `<release>-tfjob` (charts/tfjob/templates)."""
+    """PS/worker job (charts/tfjob/templates/tfjob.yaml:25-340) WITHOUT an external operator.
+
+    Every task is a ``batch/v1`` Job ``<release>-tfjob-<type>-<i>`` plus a headless Service of
+    the same name; arena computes ``TF_CONFIG`` (and the identical ``MX_CLUSTER_SPEC`` read by
+    ``arena_amd.parallel.ps``) from those stable DNS names, which is what tf-operator would
+    inject. The pods keep tf-operator's labels (``group_name``, ``tf-replica-type``,
+    ``tf-replica-index``), so discovery and chief selection are unchanged, and the status is
+    derived from the Jobs (``arena_amd.jobs.tensorflow``). ``cleanPodPolicy`` is enforced by a
+    jobmon Job that removes the still-running tasks (the PS) once every worker has finished.
+
+    ``values["tfOperator"]`` renders the reference's ``kubeflow.org`` TFJob instead, for clusters
+    that run tf-operator."""
+    if values.get("tfOperator"):
+        return _render_tfjob_crd(release, ns, values)
+    name = f"{release}-tfjob"
+    vols, mounts = _volumes_and_mounts(values)
+    cluster = tf_cluster_spec(release, ns, values)
+    out: List[dict] = []
+    for rtype, addrs in cluster.items():
+        for i, addr in enumerate(addrs):
+            task = f"{name}-{rtype}-{i}"
+            pod = _tf_task_pod(release, ns, values, rtype, i, cluster, vols, mounts)
+            sel = {k: pod["metadata"]["labels"][k]
+                   for k in ("app", "release", "tf-replica-type", "tf-replica-index")}
+            out.append({"apiVersion": "v1", "kind": "Service",
+                        "metadata": {"name": task, "namespace": ns,
+                                     "labels": {"app": "tfjob", "release": release}},
+                        "spec": {"clusterIP": "None", "selector": sel,
+                                 "ports": [{"name": "tfjob-port",
+                                            "port": int(addr.rsplit(":", 1)[1])}]}})
+            out.append({"apiVersion": "batch/v1", "kind": "Job",
+                        "metadata": {"name": task, "namespace": ns,
+                                     "labels": {"app": "tfjob", "release": release,
+                                                "tf-replica-type": rtype,
+                                                "tf-replica-index": str(i)}},
+                        "spec": {"backoffLimit": 0, "template": pod}})
+    policy = values.get("cleanPodPolicy", "Running")
+    if policy != "None" and "ps" in cluster:
+        out.append(_jobmon(release, ns, values, "tfjob",
+                           {"NAMESPACE": ns, "TFJOBNAME": name, "RELEASE": release,
+                            "CLEANPODPOLICY": policy}))
+    return out + _tensorboard(release, ns, values, "tfjob",
+                              affinity_labels={"app": "tfjob", "release": release,
+                                               "tf-replica-type": "worker",
+                                               "tf-replica-index": "0"})
+
+
+def _render_tfjob_crd(release: str, ns: str, values: dict) -> List[dict]:
+    """kubeflow.org/v1alpha2 TFJob `<release>-tfjob` for an operator-managed cluster."""
     name = f"{release}-tfjob"
     labels = {"app": "tfjob", "release": release}
     vols, mounts = _volumes_and_mounts(values)
@@ -171,32 +281,31 @@ def render_tfjob(release: str, ns: str, values: dict) -> List[dict]:
     if ps > 0:
         replicas["PS"] = {"replicas": ps, "restartPolicy": "Never", "template": {
             "metadata": {"labels": dict(labels)},
-            "spec": {"hostNetwork": values.get("useHostNetwork", True),
-                     "hostPID": values.get("useHostPID", True),
-                     "hostIPC": values.get("useHostIPC", True),
-                     "initContainers": _sync_init_containers(values),
-                     "containers": [_container(
-                         "tensorflow", values, values.get("psImage", ""), 0,
-                         values.get("psCPU", ""), values.get("psMemory", ""), mounts=mounts,
-                         ports=[{"name": "tfjob-port",
-                                 "containerPort": int(values.get("psPort", 22223))}])],
-                     "volumes": list(vols)}}}
+            "spec": _net_spec(values, hostPID=values.get("useHostPID", True),
+                              hostIPC=values.get("useHostIPC", True),
+                              initContainers=_sync_init_containers(values),
+                              containers=[_container(
+                                  "tensorflow", values, values.get("psImage", ""), 0,
+                                  values.get("psCPU", ""), values.get("psMemory", ""),
+                                  mounts=mounts,
+                                  ports=[{"name": "tfjob-port",
+                                          "containerPort": int(values.get("psPort", 22223))}])],
+                              volumes=list(vols))}}
     workers = int(values.get("workers", 1))
     if workers > 0:
         lv, lm = _log_mount(values)
         replicas["Worker"] = {"replicas": workers, "restartPolicy": "Never", "template": {
             "metadata": {"labels": dict(labels)},
-            "spec": {"hostNetwork": values.get("useHostNetwork", True),
-                     "hostPID": values.get("useHostPID", True),
-                     "hostIPC": values.get("useHostIPC", True),
-                     "initContainers": _sync_init_containers(values),
-                     "containers": [_container(
-                         "tensorflow", values, values.get("workerImage", ""),
-                         int(values.get("gpuCount", 0)), values.get("workerCPU", ""),
-                         values.get("workerMemory", ""), mounts=mounts + lm,
-                         ports=[{"name": "tfjob-port",
-                                 "containerPort": int(values.get("workerPort", 22222))}])],
-                     "volumes": list(vols) + lv}}}
+            "spec": _net_spec(values, hostPID=values.get("useHostPID", True),
+                              hostIPC=values.get("useHostIPC", True),
+                              initContainers=_sync_init_containers(values),
+                              containers=[_container(
+                                  "tensorflow", values, values.get("workerImage", ""),
+                                  int(values.get("gpuCount", 0)), values.get("workerCPU", ""),
+                                  values.get("workerMemory", ""), mounts=mounts + lm,
+                                  ports=[{"name": "tfjob-port",
+                                          "containerPort": int(values.get("workerPort", 22222))}])],
+                              volumes=list(vols) + lv)}}
     out = [{"apiVersion": "kubeflow.org/v1alpha2", "kind": "TFJob",
             "metadata": {"name": name, "namespace": ns, "labels": labels},
             "spec": {"cleanPodPolicy": values.get("cleanPodPolicy", "Running"),
@@ -207,10 +316,39 @@ def render_tfjob(release: str, ns: str, values: dict) -> List[dict]:
                                                "tf-replica-index": "0"})
 
 
+def _jobmon(release: str, ns: str, values: dict, app: str, env: Dict[str, str]) -> dict:
+    """The job monitor as a batch Job in arena-system (charts/tf-horovod/templates/jobmon.yaml).
+    The command is the module itself, which the jobmon image (deploy/jobmon.Dockerfile) ships;
+    ``ARENA_BACKEND=k8s`` makes it talk to the API server with the pod's service account, and
+    ``ARENA_JOBMON_TIMEOUT`` bounds the wait for a launcher that never finishes (quirk Q11)."""
+    fn = fullname(release, "tf-horovod") if app == "tf-horovod" else f"{release}-{app}"
+    labels = {"app": app, "release": release, "role": "jobmon"}
+    full_env = {"ARENA_BACKEND": "k8s", "ARENA_JOBMON_TIMEOUT":
+                str(values.get("jobmonTimeout", "168h")), **env}
+    return {"apiVersion": "batch/v1", "kind": "Job",
+            "metadata": {"name": f"{fn}-jobmon", "namespace": ARENA_SYSTEM_NS, "labels": labels},
+            "spec": {"backoffLimit": 3,
+                     "template": {"metadata": {"labels": dict(labels)},
+                                  "spec": {"serviceAccountName": "jobmon",
+                                           "restartPolicy": "Never",
+                                           "containers": [{
+                                               "name": "jobmon", "image": JOBMON_IMAGE,
+                                               "imagePullPolicy": values.get("jobmonPullPolicy",
+                                                                             "IfNotPresent"),
+                                               "command": list(JOBMON_COMMAND),
+                                               "env": _env_list(full_env)}]}}}}
+
+
 def render_tf_horovod(release: str, ns: str, values: dict) -> List[dict]:
     """Allreduce job (charts/tf-horovod/templates): launcher Job + worker StatefulSet + headless
     Services + jobmon. Ranks rendezvous on a TCPStore served by the launcher (rank 0) at
-    `<fullname>-master:rdzvPort`; the StatefulSet ordinal i is rank i+1."""
+    `<fullname>-master:rdzvPort`; the StatefulSet ordinal i is rank i+1.
+
+    The ordinal comes from the pod's own name through the downward API (``POD_NAME`` =
+    ``metadata.name`` = ``<fullname>-<i>``), never from ``$HOSTNAME``: under ``hostNetwork`` (the
+    default, as in the reference chart) the hostname is the NODE's name, identical for every
+    worker on a node. The reference's hostfile used per-pod DNS names for the same reason
+    (charts/tf-horovod/templates/config.yaml:13-17)."""
     fn = fullname(release, "tf-horovod")
     labels = {"app": "tf-horovod", "release": release}
     world = int(values.get("workers", 0)) + 1
@@ -223,10 +361,9 @@ def render_tf_horovod(release: str, ns: str, values: dict) -> List[dict]:
     rdzv = {"MASTER_ADDR": f"{fn}-master", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
             "HSA_ENABLE_IPC_MODE_LEGACY": "0", "NCCL_SOCKET_IFNAME": "^lo,docker"}
     gpus = int(values.get("gpuCount", 0))
-    common_spec = {"hostNetwork": values.get("useHostNetwork", True),
-                   "hostIPC": True, "volumes": vols + lv + shm}
+    common_spec = _net_spec(values, hostIPC=True, volumes=vols + lv + shm)
     master_cmd = ["sh", "-c", "export RANK=0; " + values.get("command", "")]
-    worker_cmd = ["sh", "-c", "export RANK=$(( ${HOSTNAME##*-} + 1 )); " + values.get("command", "")]
+    worker_cmd = ["sh", "-c", "export RANK=$(( ${POD_NAME##*-} + 1 )); " + values.get("command", "")]
     out = [
         {"apiVersion": "v1", "kind": "Service",
          "metadata": {"name": fn, "namespace": ns, "labels": labels},
@@ -250,7 +387,8 @@ def render_tf_horovod(release: str, ns: str, values: dict) -> List[dict]:
                                                "tf-horovod", values, values.get("image", ""), gpus,
                                                values.get("cpu", ""), values.get("memory", ""),
                                                extra_env=rdzv, mounts=mounts + lm + shm_m,
-                                               command=worker_cmd)]}}}})
+                                               command=worker_cmd,
+                                               field_env={"POD_NAME": "metadata.name"})]}}}})
     out.append({
         "apiVersion": "batch/v1", "kind": "Job",
         "metadata": {"name": f"{fn}-job", "namespace": ns, "labels": {**labels, "role": "mpimaster"}},
@@ -263,20 +401,8 @@ def render_tf_horovod(release: str, ns: str, values: dict) -> List[dict]:
                                            values.get("cpu", ""), values.get("memory", ""),
                                            extra_env=rdzv, mounts=mounts + lm + shm_m,
                                            command=master_cmd)]}}}})
-    out.append({
-        "apiVersion": "batch/v1", "kind": "Job",
-        "metadata": {"name": f"{fn}-jobmon", "namespace": ARENA_SYSTEM_NS,
-                     "labels": {**labels, "role": "jobmon"}},
-        "spec": {"template": {"metadata": {"labels": {**labels, "role": "jobmon"}},
-                              "spec": {"serviceAccountName": "jobmon", "restartPolicy": "Never",
-                                       "containers": [{
-                                           "name": "jobmon", "image": JOBMON_IMAGE,
-                                           "imagePullPolicy": values.get("jobmonPullPolicy",
-                                                                         "IfNotPresent"),
-                                           "command": ["arena-jobmon"],
-                                           "env": _env_list({"NAMESPACE": ns,
-                                                             "JOBNAME": f"{fn}-job",
-                                                             "STATEFULSETNAME": fn})}]}}}})
+    out.append(_jobmon(release, ns, values, "tf-horovod",
+                       {"NAMESPACE": ns, "JOBNAME": f"{fn}-job", "STATEFULSETNAME": fn}))
     return out + _tensorboard(release, ns, values, "tf-horovod",
                               affinity_labels={**labels, "role": "mpimaster"})
 

@@ -28,11 +28,20 @@ def _suffix(seed: str, n: int = 5) -> str:
     return "".join(out)
 
 
-def containers_from_template(tpl: dict) -> List[Container]:
+def _env_value(e: dict, pod_fields: dict) -> str:
+    """A literal env value, or a downward-API ``fieldRef`` resolved for this pod (as the kubelet
+    does at container start)."""
+    ref = ((e.get("valueFrom") or {}).get("fieldRef") or {}).get("fieldPath")
+    if ref:
+        return str(pod_fields.get(ref, ""))
+    return e.get("value", "")
+
+
+def containers_from_template(tpl: dict, pod_fields: Optional[dict] = None) -> List[Container]:
     out = []
     for c in (tpl.get("spec") or {}).get("containers", []):
         res = c.get("resources") or {}
-        env = {e["name"]: e.get("value", "") for e in c.get("env", [])}
+        env = {e["name"]: _env_value(e, pod_fields or {}) for e in c.get("env", [])}
         out.append(Container(name=c.get("name", ""), image=c.get("image", ""),
                              command=list(c.get("command", [])), env=env,
                              limits={k: v for k, v in (res.get("limits") or {}).items()
@@ -69,8 +78,10 @@ class ClusterState:
     def _new_pod(self, name: str, ns: str, tpl: dict, owner: str, extra_labels=None) -> Pod:
         tmeta = dict(tpl.get("metadata") or {})
         tmeta["namespace"] = ns
+        fields = {"metadata.name": name, "metadata.namespace": ns}
         pod = Pod(meta=self._meta(tmeta, extra_labels, owner, name=name),
-                  containers=containers_from_template(tpl))
+                  containers=containers_from_template(tpl, fields),
+                  host_network=bool((tpl.get("spec") or {}).get("hostNetwork", False)))
         self.pods[(ns, name)] = pod
         return pod
 

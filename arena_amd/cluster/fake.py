@@ -119,6 +119,14 @@ class FakeBackend(Backend):
         if self.state.services.pop((namespace, name), None) is None:
             raise BackendError(f"services \"{name}\" not found")
 
+    def delete_job(self, namespace, name):
+        if self.state.jobs.pop((namespace, name), None) is None:
+            raise BackendError(f"jobs.batch \"{name}\" not found")
+        for key in [k for k, p in self.state.pods.items()
+                    if k[0] == namespace and "Job" in p.meta.owner_kinds
+                    and k[1].rsplit("-", 1)[0] == name]:
+            del self.state.pods[key]
+
     def ensure_namespace(self, namespace):
         self.state.namespaces.add(namespace)
 

@@ -188,6 +188,11 @@ class K8sBackend(Backend):
     def delete_service(self, namespace, name):
         self._run("delete", "services", name, "-n", namespace, "--wait=false")
 
+    def delete_job(self, namespace, name):
+        # background propagation: the Job's pods are garbage-collected with it
+        self._run("delete", "jobs.batch", name, "-n", namespace, "--cascade=background",
+                  "--wait=false")
+
     def ensure_namespace(self, namespace):
         if self._run("get", "namespace", namespace, check=False).strip():
             return

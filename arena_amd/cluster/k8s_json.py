@@ -85,7 +85,8 @@ def pod_from(o: dict) -> Pod:
                node_name=spec.get("nodeName", ""), phase=st.get("phase", "Pending"),
                host_ip=st.get("hostIP", ""), pod_ip=st.get("podIP", ""),
                start_time=_t(st.get("startTime")),
-               exit_code=term.get("exitCode"), restart_count=int(cs.get("restartCount", 0) or 0))
+               exit_code=term.get("exitCode"), restart_count=int(cs.get("restartCount", 0) or 0),
+               host_network=bool(spec.get("hostNetwork", False)))
 
 
 def pod_to(p: Pod) -> dict:
@@ -102,6 +103,8 @@ def pod_to(p: Pod) -> dict:
         cs["state"] = {"terminated": {"exitCode": p.exit_code}}
     st["containerStatuses"] = [cs]
     spec = {"containers": [container_to(c) for c in p.containers]}
+    if p.host_network:
+        spec["hostNetwork"] = True
     if p.node_name:
         spec["nodeName"] = p.node_name
     return {"apiVersion": "v1", "kind": "Pod", "metadata": meta_to(p.meta), "spec": spec,

@@ -508,9 +508,11 @@ class LocalBackend(Backend):
                         job.failed = 1
             for store in ("pods", "jobs", "statefulsets", "services", "tfjobs", "endpoints"):
                 getattr(full, store).update(getattr(st, store))
-            # StatefulSets deleted by jobmon disappear
+            # StatefulSets / Jobs deleted by jobmon disappear (their pods were killed)
             for key in rel.get("deleted_statefulsets", []):
                 full.statefulsets.pop(tuple(key), None)
+            for key in rel.get("deleted_jobs", []):
+                full.jobs.pop(tuple(key), None)
         return full
 
     def list_pods(self, namespace=None, selector=None, active_only=False):
@@ -599,6 +601,16 @@ class LocalBackend(Backend):
         for p in self.list_pods(namespace, {"release": rel_name, "role": "mpiworker"}):
             open(os.path.join(jd, "control", f"kill-{p.name}"), "w").close()
         self._append_rel_list(rel_name, "deleted_statefulsets", [namespace, name])
+
+    def delete_job(self, namespace, name):
+        rel_name = self._release_of(namespace, name, "jobs")
+        if rel_name is None:
+            raise BackendError(f"jobs.batch \"{name}\" not found")
+        jd = self.job_dir(rel_name)
+        for p in self.list_pods(namespace, {"release": rel_name}):
+            if "Job" in p.meta.owner_kinds and p.name.rsplit("-", 1)[0] == name:
+                open(os.path.join(jd, "control", f"kill-{p.name}"), "w").close()
+        self._append_rel_list(rel_name, "deleted_jobs", [namespace, name])
 
     def delete_service(self, namespace, name):
         rel_name = self._release_of(namespace, name, "services")

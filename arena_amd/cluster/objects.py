@@ -56,10 +56,17 @@ class Pod:
     start_time: Optional[float] = None
     exit_code: Optional[int] = None
     restart_count: int = 0
+    host_network: bool = False
 
     @property
     def name(self) -> str:
         return self.meta.name
+
+    @property
+    def hostname(self) -> str:
+        """What ``$HOSTNAME`` is inside the pod: the node's name under hostNetwork (the charts'
+        default), else the pod's own name."""
+        return (self.node_name or "") if self.host_network else self.meta.name
 
     @property
     def namespace(self) -> str:

@@ -158,6 +158,7 @@ class TFJobArgs(SubmitArgs):
     ps_cpu: str = ""
     ps_memory: str = ""
     clean_pod_policy: str = "Running"
+    tf_operator: bool = False   # render a kubeflow.org TFJob for tf-operator instead of Jobs
     tensorboard: TensorboardArgs = field(default_factory=TensorboardArgs)
     sync: SyncCodeArgs = field(default_factory=SyncCodeArgs)
     chart: str = TF_CHART
@@ -203,6 +204,8 @@ class TFJobArgs(SubmitArgs):
                   "psImage": self.ps_image, "workerCPU": self.worker_cpu,
                   "workerMemory": self.worker_memory, "psCPU": self.ps_cpu,
                   "psMemory": self.ps_memory, "cleanPodPolicy": self.clean_pod_policy})
+        if self.tf_operator:
+            v["tfOperator"] = True
         v.update(self.tensorboard.values())
         v.update(self.sync.values())
         return v

@@ -153,6 +153,8 @@ class FusedMLPTrainer:
         self._reshuffle()
         self._graphs: dict[int, torch.cuda.CUDAGraph] = {}
         self.graph_mode = None
+        self.graph_steps = self.eager_steps = 0   # how train_steps executed (bench reports it)
+        self._graph_parity0 = 0
 
     def _setup_xgmi(self, n: int, required: bool) -> None:
         """Move P and G into hipIpc-registered memory shared with the other ranks."""
@@ -213,10 +215,16 @@ class FusedMLPTrainer:
         pos = (self.steps_done * B + torch.arange(B, device=self.device)) % L
         self.rows.copy_(self.perm[pos])
 
-    def pick_steps_per_graph(self, cap: int = 64) -> int:
-        """Largest divisor of the epoch length <= cap, so graphs never straddle a reshuffle."""
-        spe = self.steps_per_epoch
-        return max(d for d in range(1, min(cap, spe) + 1) if spe % d == 0)
+    def pick_steps_per_graph(self, cap: int = 64, runs=()) -> int:
+        """Largest divisor of the epoch length <= cap, so graphs never straddle a reshuffle.
+        ``runs``: step counts that will be requested from ``train_steps`` in sequence (e.g. the
+        bench's warmup and timed steps); the graph length then divides each of them too, so every
+        one of those steps is a graph replay (no eager remainder, no misaligned start)."""
+        g = self.steps_per_epoch
+        for r in runs:
+            if r > 0:
+                g = math.gcd(g, int(r))
+        return max(d for d in range(1, min(cap, g) + 1) if g % d == 0)
 
     @property
     def steps_per_epoch(self) -> int:
@@ -284,9 +292,11 @@ class FusedMLPTrainer:
                               grad_scale=1.0, **ctr, **common)
 
     def _capture(self, nsteps: int) -> torch.cuda.CUDAGraph:
-        # an even-length graph replayed from an even step sees the same parity sequence every
-        # time, so the parity is baked into the launches (train_steps keeps replays even-aligned)
+        # an even-length graph replayed from steps of one parity sees the same parity sequence
+        # every time, so the parity is baked into the launches (train_steps only replays it from
+        # steps whose parity is ``_graph_parity0``)
         self._graph_static = nsteps % 2 == 0
+        p0 = self._graph_parity0
         # thread_local: the RCCL process group's watchdog thread polls the events of earlier
         # collectives (the xGMI handle exchange, barriers); under the default global capture mode
         # such a poll landing inside the capture is an error that aborts the rank
@@ -294,15 +304,18 @@ class FusedMLPTrainer:
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g, capture_error_mode="thread_local"):
             for i in range(nsteps):
-                self._launch_step(parity=(i & 1) if self._graph_static else -1)
+                self._launch_step(parity=((p0 + i) & 1) if self._graph_static else -1)
         return g
 
-    def enable_graphs(self, steps_per_graph: int = 50) -> bool:
+    def enable_graphs(self, steps_per_graph: int = 50, start_parity: int = 0) -> bool:
         """Capture ``steps_per_graph`` steps per hipGraph. Returns False if capture failed
-        (e.g. a collective backend that refuses capture) -- steps then run eagerly."""
+        (e.g. a collective backend that refuses capture) -- steps then run eagerly.
+        ``start_parity``: parity (step & 1) of the steps the replays will start from, e.g. 1 when
+        an odd number of warmup steps precedes the timed ones."""
         if self.device.type != "cuda":
             return False
         self.steps_per_graph = steps_per_graph
+        self._graph_parity0 = start_parity & 1
         # warm up on a side stream (allocator / collective communicators initialised outside
         # capture), then restore the state so warm-up steps do not count as training.
         snap = [t.clone() for t in (self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2,
@@ -381,19 +394,23 @@ class FusedMLPTrainer:
             chunk = min(n, to_epoch_end)
             k = getattr(self, "steps_per_graph", 0)
             while chunk > 0:
-                aligned = not getattr(self, "_graph_static", False) or self.steps_done % 2 == 0
+                aligned = (not getattr(self, "_graph_static", False)
+                           or self.steps_done % 2 == self._graph_parity0)
                 if self._graphs and chunk >= k and aligned:
                     self._graphs[k].replay()
                     done = k
+                    self.graph_steps += k
                 elif self.graph_mode == "split":
                     pre, post = self._split_graphs
                     pre.replay()
                     self._launch_step_part(1)
                     post.replay()
                     done = 1
+                    self.graph_steps += 1
                 else:
                     self._launch_step(parity=self.steps_done & 1)
                     done = 1
+                    self.eager_steps += 1
                 chunk -= done
                 n -= done
                 self.steps_done += done

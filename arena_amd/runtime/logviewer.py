@@ -1,6 +1,11 @@
-"""Built-in log viewer for the local backend (the role of the kubernetes-dashboard / tf-job-dashboard
-URLs that ``arena logviewer`` prints in the reference: dashboard_helper.go:12-47,
-trainer_mpi.go:34-63, trainer_tensorflow.go:106-133).
+"""Built-in log viewer (the role of the kubernetes-dashboard / tf-job-dashboard URLs that
+``arena logviewer`` prints in the reference: dashboard_helper.go:12-47, trainer_mpi.go:34-63,
+trainer_tensorflow.go:106-133; the reference deploys kubernetes/dashboard/dashboard.yaml:1-104).
+
+Runs against either backend: the local job store (started on demand by ``arena logviewer``), or a
+cluster -- ``deploy/logviewer.yaml`` runs it as the ``kubernetes-dashboard`` Deployment + Service in
+``arena-system`` with ``--backend k8s``, reading pod logs through the API server with its service
+account, so ``arena logviewer <job>`` on the K8s backend resolves that Service's Endpoints.
 
 Serves the same URL shapes the CLI prints, so they work unchanged:
   http://<node>:<port>/#!/log/<ns>/<pod>/<container>?namespace=<ns>   (MPI / standalone)
@@ -46,6 +51,8 @@ window.onhashchange=route; route();
 
 
 def make_handler(backend):
+    from ..jobs.trainer import get_training_job
+
     class H(BaseHTTPRequestHandler):
         def log_message(self, *a):  # quiet
             pass
@@ -66,8 +73,10 @@ def make_handler(backend):
                 out = []
                 for name, ns in sorted(backend.list_releases().items()):
                     pods = backend.list_pods(ns, {"release": name})
-                    st = backend._state(name).get("phase", "Unknown") if hasattr(backend, "_state") \
-                        else "Unknown"
+                    try:
+                        st = get_training_job(backend, name, ns).get_status() or "Unknown"
+                    except Exception:  # noqa: BLE001 - a job being deleted: still list it
+                        st = "Unknown"
                     out.append({"name": name, "namespace": ns, "status": st,
                                 "pods": [{"name": p.name, "phase": p.phase,
                                           "container": p.containers[0].name if p.containers else ""}
@@ -99,15 +108,24 @@ def serve(backend, host: str = "0.0.0.0", port: int = 0, ready_file: str = "") -
 
 
 def main(argv=None) -> int:
-    ap = argparse.ArgumentParser(description="arena local log viewer")
+    ap = argparse.ArgumentParser(description="arena log viewer")
     ap.add_argument("--home", default=os.environ.get("ARENA_HOME",
                                                      os.path.join(os.path.expanduser("~"), ".arena")))
+    ap.add_argument("--backend", choices=["local", "k8s"],
+                    default=os.environ.get("ARENA_BACKEND", "local"))
+    ap.add_argument("--config", default=os.environ.get("KUBECONFIG", ""),
+                    help="kubeconfig (k8s backend; in a pod the service account is used)")
     ap.add_argument("--host", default="0.0.0.0")
     ap.add_argument("--port", type=int, default=0)
     ap.add_argument("--ready-file", default="")
     a = ap.parse_args(argv)
-    from ..cluster.local import LocalBackend
-    serve(LocalBackend(a.home), a.host, a.port, a.ready_file)
+    if a.backend == "k8s":
+        from ..cluster.k8s import K8sBackend
+        backend = K8sBackend(kubeconfig=a.config, home=a.home)
+    else:
+        from ..cluster.local import LocalBackend
+        backend = LocalBackend(a.home)
+    serve(backend, a.host, a.port, a.ready_file)
     return 0
 
 

@@ -11,6 +11,11 @@ gradient all-reduce when N>1, Adam update, device-side data gather + epoch reshu
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+The MNIST steps run as replays of one hipGraph whose length divides the warmup, the timed step
+count and the epoch; ``config.exec`` reports how many timed steps were replayed vs run eagerly.
+On one GPU the same line also carries ``resnet50_images_per_s`` / ``resnet50_ms_per_step``
+(ResNet-50 bs128 bf16, whole training step in one hipGraph; ``--resnet 0`` skips it).
+
 Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
@@ -36,7 +41,45 @@ def parse():
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
                     help="DP gradient path: fused xGMI reduce-scatter/Adam/all-gather kernel or "
                          "RCCL all_reduce + flat Adam (auto = xgmi when its self-test passes)")
+    ap.add_argument("--resnet", type=int, default=1,
+                    help="1: also time ResNet-50 training (bs128/GPU, bf16, hipGraph) and report "
+                         "it as extra resnet50_* keys of the same JSON line (single GPU only)")
+    ap.add_argument("--resnet-steps", type=int, default=20)
+    ap.add_argument("--resnet-batch", type=int, default=128)
     return ap.parse_args()
+
+
+def bench_resnet50(dev, steps: int, batch: int) -> dict:
+    """ResNet-50 v1.5 training step (fwd + bwd + momentum-SGD on fp32 masters, bf16 MFMA convs,
+    synthetic 224x224 ImageNet batch) as ONE hipGraph: 8 eager warmup steps (conv autotuning,
+    MIOpen solver search), capture, one untimed replay, then ``steps`` timed replays bracketed by
+    device synchronisation. Same code path as ``arena_amd.examples.cnn_bench``."""
+    import torch
+    from arena_amd.examples import cnn_bench
+    args = cnn_bench.parse(["--model", "resnet50", "--batch_size", str(batch), "--dtype", "bf16"])
+    torch.backends.cudnn.benchmark = True
+    model, opt, x, y = cnn_bench.build(args, dev, 1)
+    amp = torch.bfloat16
+    for _ in range(8):
+        cnn_bench.train_step(model, opt, x, y, amp)
+    torch.cuda.synchronize()
+    graph, g_loss = cnn_bench.capture_step(model, opt, x, y, amp)
+    graph.replay()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        graph.replay()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    loss = float(g_loss)
+    if not loss == loss:
+        raise RuntimeError("ResNet-50 bench: non-finite loss")
+    return {"resnet50_images_per_s": round(steps * batch / dt, 1),
+            "resnet50_ms_per_step": round(dt / steps * 1e3, 3),
+            "resnet50_config": {"batch_per_gpu": batch, "image": 224, "dtype": "bf16",
+                                "optimizer": "momentum-sgd fp32 masters", "timed_steps": steps,
+                                "exec": f"hipgraph[whole step] {steps}/{steps} replays",
+                                "final_loss": round(loss, 4)}}
 
 
 def main():
@@ -66,8 +109,11 @@ def main():
     if args.impl == "fused":
         tr = FusedMLPTrainer(cfg, data.train_images, data.train_labels, device=dev,
                              process_group=pg, rank=rank, world=world, comm=args.comm)
-        spg = args.steps_per_graph or tr.pick_steps_per_graph()
-        graphs = tr.enable_graphs(spg)
+        # the graph length divides the timed steps and the epoch, and its baked-in step parity is
+        # the parity of the first timed step, so every timed step is a replay of the graph
+        # captured here, before the warmup (warmup steps that do not fit replays run eagerly)
+        spg = args.steps_per_graph or tr.pick_steps_per_graph(runs=(args.steps,))
+        graphs = tr.enable_graphs(spg, start_parity=args.warmup & 1)
         run = tr.train_steps
         mode = f"hipgraph[{tr.graph_mode},{spg} steps/graph]" if graphs else "eager"
         if world > 1:
@@ -84,10 +130,15 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    g0, e0 = getattr(tr, "graph_steps", 0), getattr(tr, "eager_steps", 0)
     t0 = time.perf_counter()
     run(args.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if args.impl == "fused":
+        # what the timed region actually executed (not what was configured)
+        mode += f"; timed: {tr.graph_steps - g0}/{args.steps} graph-replayed, " \
+                f"{tr.eager_steps - e0} eager"
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
@@ -107,6 +158,11 @@ def main():
         tl, ta = tr.evaluate(data.test_images, data.test_labels)
         extra["test_loss"] = round(tl, 5)
         extra["test_acc"] = round(ta, 5)
+
+    if args.resnet and world == 1 and args.impl == "fused":
+        del tr
+        torch.cuda.empty_cache()
+        extra.update(bench_resnet50(dev, args.resnet_steps, args.resnet_batch))
 
     samples = world * cfg.batch * args.steps
     value = samples / elapsed

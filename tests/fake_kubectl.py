@@ -5,11 +5,16 @@ controller as the Fake/Local backends (Job/StatefulSet/TFJob/Deployment -> pods)
 Kubernetes JSON, and are served back by ``get -o json``.
 
 Supported: get (list/one, -n/-A/-l, -o json), apply -f -, delete, create namespace, logs.
+The endpoints controller is modelled too: a selector Service's Endpoints are the IPs of its
+Running pods (the node's IP under hostNetwork) and its target port.
 Test hooks (not kubectl): fake-node NAME IP GPUS, fake-phase NS POD PHASE [NODE] [EXIT],
-fake-log NS POD TEXT..., fake-endpoints NS NAME IP PORT.
+fake-log NS POD TEXT..., fake-endpoints NS NAME IP PORT, fake-exec NS POD -- runs the pod's
+container command the way the kubelet would start it: its env (downward-API fields resolved) plus
+HOSTNAME = the node's name under hostNetwork, else the pod's name.
 """
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -74,6 +79,25 @@ def reconcile(s):
         s["jobs"][key(ns, name)] = kj.job_to(j)
     for (ns, name), t in st.tfjobs.items():
         s["tfjobs"][key(ns, name)] = kj.tfjob_to(t)
+    # endpoints controller (manual fake-endpoints entries are left alone)
+    for k, svc in s["services"].items():
+        sel = (svc.get("spec") or {}).get("selector")
+        if not sel or s["endpoints"].get(k, {}).get("manual"):
+            continue
+        ns = k.split("/", 1)[0]
+        ips = []
+        for pk, p in sorted(s["pods"].items()):
+            st_ = p.get("status") or {}
+            if (pk.startswith(ns + "/") and st_.get("phase") == "Running"
+                    and matches((p.get("metadata") or {}).get("labels") or {}, sel)):
+                ip = st_.get("podIP") or st_.get("hostIP")
+                if ip:
+                    ips.append(ip)
+        ports = [int(p.get("targetPort") or p["port"]) for p in svc["spec"].get("ports") or []]
+        s["endpoints"][k] = {"apiVersion": "v1", "kind": "Endpoints",
+                             "metadata": {"name": k.split("/", 1)[1], "namespace": ns},
+                             "subsets": [{"addresses": [{"ip": i} for i in ips],
+                                          "ports": [{"port": p} for p in ports]}] if ips else []}
 
 
 def apply(s, docs):
@@ -83,6 +107,12 @@ def apply(s, docs):
         st.nodes[node.name] = node
     for d in docs:
         if not d:
+            continue
+        if d["kind"] in ("ServiceAccount", "ClusterRole", "ClusterRoleBinding", "Role",
+                         "RoleBinding", "CustomResourceDefinition"):
+            continue   # RBAC / API objects: accepted, nothing to reconcile
+        if d["kind"] == "Namespace":
+            s["namespaces"].setdefault(d["metadata"]["name"], {"metadata": d["metadata"]})
             continue
         ns = d["metadata"].setdefault("namespace", "default")
         s["namespaces"].setdefault(ns, {"metadata": {"name": ns}})
@@ -144,6 +174,9 @@ def main(argv):
     ns = flags.get("-n", flags.get("--namespace", "default"))
     if cmd == "get":
         store = KINDS[pos[1]]
+        if store == "tfjobs" and os.environ.get("FAKE_KUBE_NO_TFJOB_CRD"):
+            print(f'error: the server doesn\'t have a resource type "{pos[1]}"', file=sys.stderr)
+            return 1
         if len(pos) > 2:
             name = pos[2]
             o = s[store].get(name if store in ("nodes", "namespaces") else key(ns, name))
@@ -242,12 +275,21 @@ def main(argv):
         save(s)
         return 0
     if cmd == "fake-endpoints":
-        e = {"apiVersion": "v1", "kind": "Endpoints",
+        e = {"apiVersion": "v1", "kind": "Endpoints", "manual": True,
              "metadata": {"name": pos[2], "namespace": pos[1]},
              "subsets": [{"addresses": [{"ip": pos[3]}], "ports": [{"port": int(pos[4])}]}]}
         s["endpoints"][key(pos[1], pos[2])] = e
         save(s)
         return 0
+    if cmd == "fake-exec":
+        o = s["pods"][key(pos[1], pos[2])]
+        pod = kj.pod_from(o)
+        c = pod.containers[0]
+        env = {"PATH": os.environ.get("PATH", "/usr/bin:/bin"), **c.env, "HOSTNAME": pod.hostname}
+        r = subprocess.run(c.command, env=env, capture_output=True, text=True)
+        sys.stdout.write(r.stdout)
+        sys.stderr.write(r.stderr)
+        return r.returncode
     print(f"fake kubectl: unsupported command {argv}", file=sys.stderr)
     return 1
 

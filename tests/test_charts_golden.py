@@ -78,24 +78,65 @@ def test_standalone_properties():
                for v in vols.values())
 
 
+def _env(c):
+    return {e["name"]: e.get("value") for e in c["env"]}
+
+
 def test_tfjob_properties():
+    """Operator-free PS/worker job: a Job + headless Service per task, TF_CONFIG from the
+    Services' stable DNS names, tf-operator's pod labels, cleanPodPolicy by jobmon."""
+    import json
     docs = _render("tfjob")
-    (tf,) = [d for d in docs if d["kind"] == "TFJob"]
-    reps = tf["spec"]["tfReplicaSpecs"]
-    assert reps["PS"]["replicas"] == 1 and reps["Worker"]["replicas"] == 3
-    ps_c = reps["PS"]["template"]["spec"]["containers"][0]
-    wk_c = reps["Worker"]["template"]["spec"]["containers"][0]
-    assert "amd.com/gpu" not in (ps_c.get("resources") or {}).get("limits", {})
-    assert wk_c["resources"]["limits"]["amd.com/gpu"] == 2
-    assert any(p["containerPort"] == 22222 for p in wk_c["ports"])
-    assert any(p["containerPort"] == 22223 for p in ps_c["ports"])
-    kinds = sorted(d["kind"] for d in docs)
-    assert kinds == ["Deployment", "Service", "TFJob"]
+    by = {(d["kind"], d["metadata"]["name"]): d for d in docs}
+    tasks = ["demo-tfjob-ps-0"] + [f"demo-tfjob-worker-{i}" for i in range(3)]
+    assert not [d for d in docs if d["kind"] == "TFJob"]
+    want_cluster = {"ps": ["demo-tfjob-ps-0.team-a.svc:22223"],
+                    "worker": [f"demo-tfjob-worker-{i}.team-a.svc:22222" for i in range(3)]}
+    for t in tasks:
+        job, svc = by[("Job", t)], by[("Service", t)]
+        tpl = job["spec"]["template"]
+        labels = tpl["metadata"]["labels"]
+        rtype, idx = t.split("-")[-2], int(t.split("-")[-1])
+        assert labels["group_name"] == "kubeflow.org" and labels["tf-replica-type"] == rtype
+        assert labels["tf-replica-index"] == str(idx) and labels["app"] == "tfjob"
+        assert svc["spec"]["clusterIP"] == "None"
+        assert all(labels[k] == v for k, v in svc["spec"]["selector"].items())
+        (c,) = tpl["spec"]["containers"]
+        tfc = json.loads(_env(c)["TF_CONFIG"])
+        assert tfc == {"cluster": want_cluster, "task": {"type": rtype, "index": idx},
+                       "environment": "cloud"}
+        assert _env(c)["MX_CLUSTER_SPEC"] == _env(c)["TF_CONFIG"]
+        port = 22223 if rtype == "ps" else 22222
+        assert [p["containerPort"] for p in c["ports"]] == [port]
+        assert svc["spec"]["ports"][0]["port"] == port
+        gpus = (c.get("resources") or {}).get("limits", {}).get("amd.com/gpu")
+        assert gpus == (None if rtype == "ps" else 2)
+        assert tpl["spec"]["hostNetwork"] is True
+        assert tpl["spec"]["dnsPolicy"] == "ClusterFirstWithHostNet"   # Service names resolve
+        assert tpl["spec"]["restartPolicy"] == "Never"
+        init = tpl["spec"].get("initContainers") or []
+        assert init and any("GIT_SYNC_REPO" in str(i) for i in init)   # Q7 fixed: git sync works
+    jm = by[("Job", "demo-tfjob-jobmon")]
+    assert jm["metadata"]["namespace"] == "arena-system"
+    jenv = _env(_containers(jm)[0])
+    assert jenv["TFJOBNAME"] == "demo-tfjob" and jenv["CLEANPODPOLICY"] == "Running"
+    assert jenv["RELEASE"] == "demo" and jenv["NAMESPACE"] == "team-a"
     (dep,) = [d for d in docs if d["kind"] == "Deployment"]
     aff = dep["spec"]["template"]["spec"]["affinity"]["podAffinity"]
-    assert aff  # TensorBoard pinned next to worker-0 (shared hostPath log dir)
-    init = reps["Worker"]["template"]["spec"].get("initContainers") or []
-    assert init and any("GIT_SYNC_REPO" in str(i) for i in init)   # Q7 fixed: git sync works
+    sel = aff["requiredDuringSchedulingIgnoredDuringExecution"][0]["labelSelector"]["matchLabels"]
+    w0 = by[("Job", "demo-tfjob-worker-0")]["spec"]["template"]["metadata"]["labels"]
+    assert all(w0[k] == v for k, v in sel.items())   # TensorBoard pinned next to worker-0
+
+
+def test_tfjob_operator_mode_renders_crd():
+    a = S.TFJobArgs()
+    a.name, a.image, a.workers, a.ps_count, a.tf_operator = "op", "img", 2, 1, True
+    a.prepare(["python", "x.py"])
+    docs = charts.render(a.chart, "op", "default", a.values())
+    (tf,) = [d for d in docs if d["kind"] == "TFJob"]
+    reps = tf["spec"]["tfReplicaSpecs"]
+    assert reps["PS"]["replicas"] == 1 and reps["Worker"]["replicas"] == 2
+    assert not [d for d in docs if d["kind"] == "Job"]
 
 
 def test_mpijob_properties():
@@ -119,7 +160,14 @@ def test_mpijob_properties():
         assert shm and shm[0]["emptyDir"]["sizeLimit"] == "4Gi"
         assert d["spec"]["template"]["spec"].get("hostIPC") is True
     assert "export RANK=0" in " ".join(_containers(job)[0]["command"])
-    assert "HOSTNAME##*-" in " ".join(_containers(ss)[0]["command"])
+    # the worker rank comes from the pod name (downward API), not $HOSTNAME (= node under
+    # hostNetwork); tests/test_k8s_backend.py runs it on a fake node with several workers
+    wc = _containers(ss)[0]
+    assert "POD_NAME##*-" in " ".join(wc["command"]) and "HOSTNAME" not in " ".join(wc["command"])
+    assert {"name": "POD_NAME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}} \
+        in wc["env"]
+    for d in (job, ss):
+        assert d["spec"]["template"]["spec"]["dnsPolicy"] == "ClusterFirstWithHostNet"
 
 
 def test_heartbeat_timeout_renders_liveness_probe():
@@ -139,7 +187,7 @@ def test_heartbeat_timeout_renders_liveness_probe():
         if d["metadata"]["name"].endswith("jobmon"):
             assert "livenessProbe" not in c
             continue
-        env = {e["name"]: e.get("value") for e in c["env"]}
+        env = _env(c)
         assert env["ARENA_HEARTBEAT_FILE"] == "/tmp/arena-heartbeat"
         probe = c["livenessProbe"]
         assert probe["initialDelaySeconds"] == 30 and probe["failureThreshold"] == 1
@@ -161,3 +209,32 @@ def test_heartbeat_timeout_renders_liveness_probe():
     b.prepare(["python", "train.py"])
     assert all("livenessProbe" not in str(d) for d in charts.render(b.chart, "nohb", "default",
                                                                      b.values()))
+
+
+def test_jobmon_image_runs_the_rendered_command():
+    """The jobmon Job's command exists in the image deploy/jobmon.Dockerfile builds: the package
+    is copied onto PYTHONPATH, the module imports without torch (the image has none), and the
+    `arena-jobmon` console script is installed as well."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(GOLDEN))
+    docker = open(os.path.join(root, "deploy", "jobmon.Dockerfile")).read()
+    assert "COPY arena_amd /opt/arena/arena_amd" in docker and "PYTHONPATH=/opt/arena" in docker
+    assert "/usr/local/bin/arena-jobmon" in docker and "kubectl" in docker
+    for d in _render("mpijob"):
+        if d["metadata"]["name"].endswith("jobmon"):
+            cmd = _containers(d)[0]["command"]
+            assert cmd == list(charts.JOBMON_COMMAND)
+            assert _containers(d)[0]["image"] == charts.JOBMON_IMAGE
+    mod = charts.JOBMON_COMMAND[2]
+    probe = ("import sys; sys.modules['torch'] = None; import importlib; "
+             f"importlib.import_module({mod!r}); import arena_amd.cluster.k8s")
+    r = subprocess.run([sys.executable, "-c", probe], cwd=root, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    # without its env it exits 2 with a clear message (no traceback, no hang)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("NAMESPACE", "JOBNAME", "STATEFULSETNAME", "TFJOBNAME")}
+    env["PYTHONPATH"] = root
+    r = subprocess.run([sys.executable, "-m", mod], cwd=root, env=env, capture_output=True,
+                       text=True, timeout=60)
+    assert r.returncode == 2 and "Failed to get namespace" in r.stderr

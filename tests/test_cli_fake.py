@@ -33,13 +33,21 @@ def env(monkeypatch):
     return fake, clock, arena
 
 
+def _task_pod(fake, task):
+    """The pod of a PS/worker task Job ``<release>-tfjob-<type>-<i>`` (Job pods get a suffix)."""
+    (p,) = [p for p in fake.list_pods() if p.name.rsplit("-", 1)[0] == task]
+    return p
+
+
 def test_submit_tf_and_list_get_top(env):
     fake, clock, arena = env
     rc, out = arena("submit", "tf", "--name", "tf-git", "--gpus", "1", "--image", "img",
                     "--syncMode", "git", "--syncSource", "https://x/tensorflow-sample-code.git",
                     "python", "main.py", "--max_steps", "1000")
     assert rc == 0, out
-    assert "tf-git-tfjob" in out and "kubeflow.org/v1alpha2/TFJob" in out
+    # operator-free: one batch Job + headless Service per task (no TFJob CRD needed)
+    assert "==> batch/v1/Job" in out and "==> v1/Service" in out
+    assert "tf-git-tfjob-worker-0" in out and "TFJob" not in out
     rel = fake.get_release("tf-git")
     assert rel.values["syncGitProjectName"] == "tensorflow-sample-code"
     assert rel.values["command"] == "python main.py --max_steps 1000"
@@ -63,8 +71,9 @@ def test_submit_tf_and_list_get_top(env):
                    + "-" * 89 + "\n"
                    "Allocated/Total GPUs In Cluster:\n1/16 (6%)  \n")
     rc, out = arena("get", "tf-git")
-    assert out == ("NAME    STATUS   TRAINER  AGE  INSTANCE               NODE\n"
-                   "tf-git  RUNNING  tfjob    17s  tf-git-tfjob-worker-0  192.168.1.119\n")
+    chief = _task_pod(fake, "tf-git-tfjob-worker-0").name
+    assert out == ("NAME    STATUS   TRAINER  AGE  INSTANCE                     NODE\n"
+                   f"tf-git  RUNNING  tfjob    17s  {chief}  192.168.1.119\n")
     rc, out = arena("get", "tf-git", "-o", "name")
     assert out == "tf-git\n"
     rc, out = arena("get", "nope")
@@ -75,16 +84,16 @@ def test_tf_status_precedence(env):
     fake, clock, arena = env
     arena("submit", "tf", "--name", "dist", "--gpus", "1", "--image", "i", "--workers", "2",
           "--ps", "1", "python", "dist.py")
-    pods = sorted(p.name for p in fake.list_pods())
-    assert pods == ["dist-tfjob-ps-0", "dist-tfjob-worker-0", "dist-tfjob-worker-1"]
-    w0 = fake.get_pod("default", "dist-tfjob-worker-0")
+    tasks = sorted(p.name.rsplit("-", 1)[0] for p in fake.list_pods("default"))
+    assert tasks == ["dist-tfjob-ps-0", "dist-tfjob-worker-0", "dist-tfjob-worker-1"]
+    w0 = _task_pod(fake, "dist-tfjob-worker-0")
     assert w0.meta.labels["group_name"] == "kubeflow.org"
     assert w0.meta.labels["tf-replica-index"] == "0"
     assert arena("list")[1].splitlines()[1].split()[1] == "PENDING"
     fake.schedule()
     assert arena("list")[1].splitlines()[1].split()[1] == "RUNNING"
-    for p in ("dist-tfjob-worker-0", "dist-tfjob-worker-1"):
-        fake.set_phase("default", p, "Succeeded")
+    for t in ("dist-tfjob-worker-0", "dist-tfjob-worker-1"):
+        fake.set_phase("default", _task_pod(fake, t).name, "Succeeded")
     assert arena("list")[1].splitlines()[1].split()[1] == "SUCCEEDED"
     # PS has no GPU; two workers x 1 GPU, completed -> requested 2, allocated 1 (ps not GPU)
     out = arena("top", "job")[1]
@@ -104,11 +113,11 @@ def test_mpi_job_chief_is_newest_job_pod_and_workers_listed(env):
                 and p.meta.labels.get("role") == "mpimaster"]
     assert len(job_pods) == 1
     # the jobmon job lives in arena-system with the reap contract env
-    jm = fake.get_job("arena-system", "hvd-tf-horovod-jobmon")
-    env_ = {c.name: c.env for c in jm and [] or []}
+    assert fake.get_job("arena-system", "hvd-tf-horovod-jobmon") is not None
     jm_pod = [p for p in fake.list_pods("arena-system")][0]
     assert jm_pod.containers[0].env == {"NAMESPACE": "default", "JOBNAME": "hvd-tf-horovod-job",
-                                        "STATEFULSETNAME": "hvd-tf-horovod"}
+                                        "STATEFULSETNAME": "hvd-tf-horovod",
+                                        "ARENA_BACKEND": "k8s", "ARENA_JOBMON_TIMEOUT": "168h"}
     fake.schedule()
     rc, out = arena("get", "hvd")
     lines = out.splitlines()
@@ -178,7 +187,7 @@ def test_env_data_tensorboard_values(env):
     rc, out = arena("get", "tb")
     assert "Your tensorboard will be available on:" in out
     assert "http://192.168.1.116:30000" in out
-    w0 = fake.get_pod("default", "tb-tfjob-worker-0")
+    w0 = _task_pod(fake, "tb-tfjob-worker-0")
     assert w0.containers[0].limits == {"amd.com/gpu": 1}
 
 

@@ -101,25 +101,157 @@ def test_mpijob_discovery_and_gpu_accounting(kube):
     assert not json.load(open(kube.state))["jobs"]
 
 
-def test_tfjob_conditions_and_tensorboard(kube):
+def _pods(kube, ns="default"):
+    return json.load(open(kube.state))["pods"]
+
+
+def _task_pod(kube, task, ns="default"):
+    (name,) = [k.split("/")[1] for k in _pods(kube) if k.startswith(ns + "/")
+               and k.split("/")[1].rsplit("-", 1)[0] == task]
+    return name
+
+
+def test_tfjob_without_operator(kube, monkeypatch):
+    """No tf-operator, no TFJob CRD: per-task Jobs + headless Services, TF_CONFIG from their DNS
+    names, status from the Jobs, PS reaped by jobmon (cleanPodPolicy=Running)."""
+    from arena_amd.runtime import jobmon
+    monkeypatch.setenv("FAKE_KUBE_NO_TFJOB_CRD", "1")
     out = cli(kube, "submit", "tf", "--name", "dist", "--image", "rocm/tf", "--gpus", "1",
               "--workers", "2", "--ps", "1", "--tensorboard", "python dist.py")
+    assert "==> batch/v1/Job" in out and "TFJob" not in out
+    st = json.load(open(kube.state))
+    assert not st["tfjobs"]
+    tasks = {"ps-0": _task_pod(kube, "dist-tfjob-ps-0"),
+             "worker-0": _task_pod(kube, "dist-tfjob-worker-0"),
+             "worker-1": _task_pod(kube, "dist-tfjob-worker-1")}
+    for t, pod in tasks.items():
+        env = {e["name"]: e["value"] for e in
+               st["pods"][f"default/{pod}"]["spec"]["containers"][0]["env"]}
+        tfc = json.loads(env["TF_CONFIG"])
+        assert tfc["task"] == {"type": t.split("-")[0], "index": int(t.split("-")[1])}
+        assert tfc["cluster"]["ps"] == ["dist-tfjob-ps-0.default.svc:22223"]
+        assert tfc["cluster"]["worker"] == ["dist-tfjob-worker-0.default.svc:22222",
+                                            "dist-tfjob-worker-1.default.svc:22222"]
+    assert rows(cli(kube, "list"))[0][:3] == ["dist", "PENDING", "TFJOB"]
+    for pod in tasks.values():
+        kube.fake("fake-phase", "default", pod, "Running", "mi355x-a")
+    assert rows(cli(kube, "list"))[0][:2] == ["dist", "RUNNING"]
+    # each task's headless Service resolves to its pod (endpoints controller)
+    ep = kube.get_endpoints("default", "dist-tfjob-worker-1")
+    assert ep.addresses == ["10.1.0.1"] and ep.ports == [22222]
+    got = cli(kube, "get", "dist")
+    assert tasks["worker-0"] in got and "tensorboard will be available on" in got
+    for t in ("worker-0", "worker-1"):
+        kube.fake("fake-phase", "default", tasks[t], "Succeeded", "mi355x-a", "0")
+    assert rows(cli(kube, "list"))[0][:2] == ["dist", "SUCCEEDED"]
+    # jobmon (as rendered into arena-system) removes the still-running PS task
+    st = json.load(open(kube.state))
+    jm = st["jobs"]["arena-system/dist-tfjob-jobmon"]
+    env = {e["name"]: e["value"]
+           for e in jm["spec"]["template"]["spec"]["containers"][0]["env"]}
+    assert jobmon.run(kube, env, sleep=lambda s: None) == "Succeeded"
+    st = json.load(open(kube.state))
+    assert "default/dist-tfjob-ps-0" not in st["jobs"]
+    assert f"default/{tasks['ps-0']}" not in st["pods"]
+    assert "default/dist-tfjob-worker-0" in st["jobs"]        # finished tasks are kept
+    assert rows(cli(kube, "list"))[0][:2] == ["dist", "SUCCEEDED"]
+    cli(kube, "delete", "dist")
+    assert not [k for k in json.load(open(kube.state))["jobs"] if k.startswith("default/")]
+
+
+def test_tfjob_failed_task(kube):
+    cli(kube, "submit", "tf", "--name", "bad", "--image", "img", "--workers", "2", "--ps", "1",
+        "python x.py")
+    for t in ("bad-tfjob-ps-0", "bad-tfjob-worker-0", "bad-tfjob-worker-1"):
+        kube.fake("fake-phase", "default", _task_pod(kube, t), "Running", "mi355x-b")
+    kube.fake("fake-phase", "default", _task_pod(kube, "bad-tfjob-worker-1"), "Failed",
+              "mi355x-b", "1")
+    assert rows(cli(kube, "list"))[0][:2] == ["bad", "FAILED"]
+
+
+def test_tfjob_operator_mode(kube):
+    """--tfOperator keeps the reference's TFJob path for clusters that run tf-operator."""
+    out = cli(kube, "submit", "tf", "--name", "op", "--image", "rocm/tf", "--gpus", "1",
+              "--workers", "2", "--ps", "1", "--tfOperator", "python dist.py")
     assert "TFJob" in out
     st = json.load(open(kube.state))
     pods = [k.split("/")[1] for k in st["pods"]]
-    assert {"dist-tfjob-ps-0", "dist-tfjob-worker-0", "dist-tfjob-worker-1"} <= set(pods)
-    assert rows(cli(kube, "list"))[0][:2] == ["dist", "PENDING"]   # Created condition
+    assert {"op-tfjob-ps-0", "op-tfjob-worker-0", "op-tfjob-worker-1"} <= set(pods)
+    assert rows(cli(kube, "list"))[0][:2] == ["op", "PENDING"]   # Created condition
     for p in pods:
         kube.fake("fake-phase", "default", p, "Running", "mi355x-a")
-    assert rows(cli(kube, "list"))[0][:2] == ["dist", "RUNNING"]
-    got = cli(kube, "get", "dist")
-    assert "tensorboard will be available on" in got and "10.1.0.1:" in got
-    for p in ("dist-tfjob-worker-0", "dist-tfjob-worker-1"):
+    assert rows(cli(kube, "list"))[0][:2] == ["op", "RUNNING"]
+    for p in ("op-tfjob-worker-0", "op-tfjob-worker-1"):
         kube.fake("fake-phase", "default", p, "Succeeded", "mi355x-a", "0")
-    assert rows(cli(kube, "list"))[0][:2] == ["dist", "SUCCEEDED"]
+    assert rows(cli(kube, "list"))[0][:2] == ["op", "SUCCEEDED"]
     kube.fake("fake-endpoints", "arena-system", "tf-job-dashboard", "10.1.0.9", "8080")
-    lv = cli(kube, "logviewer", "dist")
-    assert "10.1.0.9:8080/tfjobs/ui/#/default/dist-tfjob" in lv
+    lv = cli(kube, "logviewer", "op")
+    assert "10.1.0.9:8080/tfjobs/ui/#/default/op-tfjob" in lv
+
+
+def test_allreduce_ranks_unique_under_host_network(kube):
+    """Every allreduce pod runs on ONE node with hostNetwork (so $HOSTNAME is the node's name
+    in all of them); the rendered command still gives ranks 0..N-1, each exactly once."""
+    cli(kube, "submit", "mpi", "--name", "hn", "--image", "rocm/pytorch", "--gpus", "1",
+        "--workers", "4", "echo RANK=$RANK WORLD=$WORLD_SIZE HOST=$HOSTNAME")
+    st = json.load(open(kube.state))
+    ranks = [k.split("/")[1] for k, p in st["pods"].items() if k.startswith("default/")
+             and p["metadata"]["labels"].get("role") in ("mpimaster", "mpiworker")]
+    assert len(ranks) == 4
+    seen = []
+    for pod in ranks:
+        kube.fake("fake-phase", "default", pod, "Running", "mi355x-a")
+        out = kube.fake("fake-exec", "default", pod).split()
+        kv = dict(x.split("=", 1) for x in out)
+        assert kv["HOST"] == "mi355x-a" and kv["WORLD"] == "4"
+        seen.append(int(kv["RANK"]))
+    assert sorted(seen) == [0, 1, 2, 3]
+
+
+def test_logviewer_deployment_on_k8s(kube):
+    """deploy/logviewer.yaml stands in for kubernetes/dashboard/dashboard.yaml: once its pod runs,
+    `arena logviewer` resolves the kubernetes-dashboard Endpoints to a per-pod log URL."""
+    root = os.path.dirname(HERE)
+    with open(os.path.join(root, "deploy", "logviewer.yaml")) as f:
+        kube._run("apply", "-f", "-", stdin=f.read())
+    cli(kube, "submit", "mpi", "--name", "lv", "--image", "img", "--workers", "2", "python t.py")
+    assert "No LOGVIEWER Installed" in cli(kube, "logviewer", "lv")
+    (lvpod,) = [k.split("/")[1] for k in _pods(kube) if k.startswith("arena-system/kubernetes-")]
+    kube.fake("fake-phase", "arena-system", lvpod, "Running", "mi355x-b")
+    for k, p in _pods(kube).items():
+        if k.startswith("default/"):
+            kube.fake("fake-phase", "default", k.split("/")[1], "Running", "mi355x-a")
+    out = cli(kube, "logviewer", "lv")
+    chief = next(k.split("/")[1] for k, p in _pods(kube).items()
+                 if k.startswith("default/lv-tf-horovod-job-"))
+    assert f"10.1.0.2:9090/#!/log/default/{chief}/mpimaster?namespace=default" in out
+
+
+def test_logviewer_server_with_k8s_backend(kube):
+    """The viewer process itself on the K8s backend: job list with status, and pod logs read
+    through kubectl."""
+    import threading
+    import urllib.request
+    from http.server import ThreadingHTTPServer
+    from arena_amd.runtime.logviewer import make_handler
+    cli(kube, "submit", "sj", "--name", "web", "--image", "img", "python x.py")
+    pod = next(k.split("/")[1] for k in _pods(kube) if k.startswith("default/web-"))
+    kube.fake("fake-phase", "default", pod, "Running", "mi355x-a")
+    kube.fake("fake-log", "default", pod, "step 10 loss 0.5")
+    srv = ThreadingHTTPServer(("127.0.0.1", 0), make_handler(kube))
+    th = threading.Thread(target=srv.serve_forever, daemon=True)
+    th.start()
+    try:
+        base = f"http://127.0.0.1:{srv.server_address[1]}"
+        jobs = json.loads(urllib.request.urlopen(base + "/api/jobs", timeout=30).read())
+        assert jobs[0]["name"] == "web" and jobs[0]["status"] == "RUNNING"
+        assert jobs[0]["pods"][0]["name"] == pod
+        log = urllib.request.urlopen(f"{base}/api/log/default/{pod}?tail=5", timeout=30).read()
+        assert log.decode().strip() == "step 10 loss 0.5"
+        page = urllib.request.urlopen(base + "/", timeout=30).read().decode()
+        assert "#!\\/log" in page or "log/" in page
+    finally:
+        srv.shutdown()
 
 
 def test_codec_roundtrip():
@@ -130,7 +262,8 @@ def test_codec_roundtrip():
     a.prepare(["python", "x.py"])
     st = ClusterState(clock=lambda: 1_700_000_000.0)
     created = st.apply(charts.render(a.chart, "rt", "ns1", a.values()))
-    st.set_pod_phase("ns1", "rt-tfjob-worker-0", "Running")
+    w0 = next(n for (_, n) in st.pods if n.rsplit("-", 1)[0] == "rt-tfjob-worker-0")
+    st.set_pod_phase("ns1", w0, "Running")
     for o in created:
         kind = type(o).__name__
         to = getattr(kj, kind.lower() + "_to", None)

@@ -181,7 +181,9 @@ def test_tfjob_ps_workers_train_mnist(env):
     assert len(tfc[0]["cluster"]["worker"]) == 2 and len(tfc[0]["cluster"]["ps"]) == 1
     st = wait_phase(env, "dist", timeout=180)
     assert st["phase"] == "Succeeded", st
-    w0 = cli(env, "logs", "dist", "-i", "dist-tfjob-worker-0")
+    (w0pod,) = [p.name for p in env.list_pods("default", {"release": "dist"})
+                if p.name.rsplit("-", 1)[0] == "dist-tfjob-worker-0"]
+    w0 = cli(env, "logs", "dist", "-i", w0pod)
     assert "Accuracy at step" in w0 and "test accuracy" in w0
     assert "TFJOB" in cli(env, "list")
     scal = os.path.join(env.job_dir("dist"), "tb", "test")
@@ -261,7 +263,7 @@ def test_logviewer_serves_dashboard_urls(env):
         base = f"http://127.0.0.1:{info['port']}"
         jobs = json.load(urllib.request.urlopen(base + "/api/jobs", timeout=10))
         pod = jobs[0]["pods"][0]["name"]
-        assert jobs[0]["name"] == "lvw" and jobs[0]["status"] == "Succeeded"
+        assert jobs[0]["name"] == "lvw" and jobs[0]["status"] == "SUCCEEDED"   # as `arena list`
         text = urllib.request.urlopen(f"{base}/api/log/default/{pod}", timeout=10).read().decode()
         assert text == "viewer line\n"
         assert b"arena log viewer" in urllib.request.urlopen(base + "/tfjobs/ui/", timeout=10).read()
