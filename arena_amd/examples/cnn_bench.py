@@ -53,11 +53,17 @@ def parse(argv=None):
                          "and replay it (single rank; DP ranks run eagerly)")
     ap.add_argument("--master_weights", choices=["auto", "on", "off"], default="auto",
                     help="bf16 conv/linear weights with fp32 master copies updated by one "
-                         "multi-tensor HIP kernel (auto: on for single-rank bf16 GPU runs)")
+                         "multi-tensor HIP kernel; with several ranks by the sharded xGMI "
+                         "reduce-scatter/SGD/all-gather kernel (auto: on for bf16 GPU runs, "
+                         "data parallel only when the xGMI collective is usable)")
     ap.add_argument("--async_wgrad", choices=["on", "off"], default="off",
                     help="conv weight gradients on a second HIP stream, concurrent with the "
                          "backward-data/BatchNorm chain (single rank; measured slower on "
                          "ResNet-50 bs128: 16.18 vs 15.49 ms/step, docs/perf.md)")
+    ap.add_argument("--verify_every", type=int, default=0,
+                    help="data parallel: every K steps check that all replicas hold bit-identical "
+                         "parameters (and that no xGMI barrier timed out); abort if not. The "
+                         "replicas are always verified once at the end")
     ap.add_argument("--json", action="store_true", help="print one JSON summary line at the end")
     return ap.parse_args(argv)
 
@@ -77,14 +83,37 @@ def build(args, dev, world):
         (no_decay if p.ndim <= 1 else decay).append(p)   # no decay on BN / bias
     mw = getattr(args, "master_weights", "auto")
     master = mw == "on" or (
-        mw == "auto" and world == 1 and dev.type == "cuda"
+        mw == "auto" and dev.type == "cuda"
         and getattr(args, "dtype", "bf16") == "bf16" and all(p.numel() % 4 == 0 for p in decay))
-    if master and world > 1:
-        raise SystemExit("--master_weights on is single-rank only (DP buckets carry fp32 grads)")
     if master and (getattr(args, "dtype", "bf16") != "bf16" or dev.type != "cuda"):
         raise SystemExit("--master_weights on needs --dtype bf16 on a GPU (the weights become "
                          "bf16 and the update runs in the HIP multi-tensor kernel)")
-    if master:
+    if master and world > 1:
+        # data parallel keeps the bf16-weight design through the sharded xGMI optimizer; it
+        # needs every rank's GPU mapped into every rank (one node): decided collectively
+        from ..parallel import xgmi
+        ok = getattr(args, "comm", "auto") != "rccl" and xgmi.usable()
+        if not ok:
+            if mw == "on":
+                raise SystemExit("--master_weights on with several ranks needs the xGMI "
+                                 "collective (single node, --comm auto|xgmi)")
+            master = False   # fp32 weights + DistributedOptimizer (RCCL) instead
+    if master and world > 1:
+        from ..ops.optim import OptimizerGroup
+        from ..parallel.zero import ShardedMasterSGD
+        zero = ShardedMasterSGD(decay, lr=args.learning_rate, momentum=args.momentum,
+                                weight_decay=args.weight_decay, bucket_mb=args.bucket_mb)
+        # BN scales/shifts and biases (fp32, no decay, ~0.1 M values): plain bucketed allreduce
+        names = {id(p): n for n, p in model.named_parameters()}
+        rest = hvd.DistributedOptimizer(
+            torch.optim.SGD(no_decay, lr=args.learning_rate, momentum=args.momentum,
+                            foreach=True),
+            named_parameters=[(names[id(p)], p) for p in no_decay], bucket_mb=args.bucket_mb,
+            comm=args.comm)
+        opt = OptimizerGroup(zero, rest)
+        opt.comm = f"xgmi-sharded-sgd+{rest.comm}"
+        opt.comms = [zero.comm, rest.xgmi]
+    elif master:
         # conv/fc weights live in bf16 (fp32 masters inside MasterSGD): no per-step casts
         from ..ops.optim import MasterSGD, OptimizerGroup
         opt = OptimizerGroup(
@@ -97,7 +126,7 @@ def build(args, dev, world):
                                {"params": no_decay, "weight_decay": 0.0}],
                               lr=args.learning_rate, momentum=args.momentum,
                               foreach=dev.type == "cuda")
-    if world > 1:
+    if world > 1 and not master:
         opt = hvd.DistributedOptimizer(opt, named_parameters=model.named_parameters(),
                                        bucket_mb=args.bucket_mb, comm=args.comm)
     g = torch.Generator(device=dev).manual_seed(hvd.rank())
@@ -194,6 +223,11 @@ def main(argv=None) -> int:
     if world > 1:
         torch.distributed.barrier()
     sync()
+    check = None
+    if world > 1:
+        from ..parallel.verify import ReplicaCheck
+        check = ReplicaCheck(args.verify_every, lambda: list(model.parameters()),
+                             comms=[getattr(opt, "xgmi", None)] + list(getattr(opt, "comms", [])))
     t0 = t_last = time.perf_counter()
     loss = None
     for i in range(1, args.num_batches + 1):
@@ -203,6 +237,8 @@ def main(argv=None) -> int:
         else:
             loss = train_step(model, opt, x, y, amp)
         heartbeat.beat(i)
+        if check is not None:
+            check.maybe(i)
         if i % args.display_every == 0 or i == args.num_batches:
             sync()
             now = time.perf_counter()
@@ -214,6 +250,8 @@ def main(argv=None) -> int:
             t_last = now
     sync()
     elapsed = time.perf_counter() - t0
+    if check is not None:
+        check.verify(args.num_batches)   # every rank raises on divergence: no number printed
     if world > 1:
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)

@@ -108,9 +108,14 @@ class FusedMLPTrainer:
         self.xgmi = None
         if self.distributed:
             import torch.distributed as dist
-            dist.broadcast(self.P, src=0, group=self.pg)
             if dev.type == "cuda" and comm in ("auto", "xgmi"):
                 self._setup_xgmi(n, required=(comm == "xgmi"))
+            if self.xgmi is not None:
+                # rank 0's initial parameters, pulled over xGMI straight into every rank's
+                # registered parameter buffer
+                self.xgmi.broadcast_(self.P, 0)
+            else:
+                dist.broadcast(self.P, src=0, group=self.pg)
         self.comm = "xgmi" if self.xgmi is not None else ("rccl" if self.distributed else "none")
         L = self.layout
         self.W1, self.b1 = L.view(self.P, "W1"), L.view(self.P, "b1")

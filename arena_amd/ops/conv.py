@@ -39,6 +39,8 @@ def kernel_ok(x: Tensor, w: Tensor, stride: int, pad: int) -> bool:
     return (x.is_cuda and x.dim() == 4 and w.dim() == 4 and x.dtype == torch.bfloat16
             and w.dtype == torch.bfloat16 and x.shape[1] % 64 == 0 and w.shape[0] % 64 == 0
             and w.shape[1] == x.shape[1] and stride >= 1 and pad >= 0
+            # the stride-1 backward-data pass is a conv with padding R-1-pad: never negative
+            and pad <= min(w.shape[2], w.shape[3]) - 1
             and x.shape[2] + 2 * pad >= w.shape[2] and x.shape[3] + 2 * pad >= w.shape[3])
 
 
@@ -535,6 +537,13 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
 # side stream before anything reads the weight gradients: ``sync_wgrad()`` (cnn_bench does it
 # between backward and the optimizer step). Off by default; single-process use only (DP bucket
 # hooks read gradients as soon as autograd hands them over).
+#
+# A side-stream dW is handed to autograd before it is complete, so it is only used when nothing
+# on the main stream can read it before ``sync_wgrad()``: the conv's weight input must be the leaf
+# parameter itself (bf16 master-weight training -- with fp32 weights under autocast, the cast's
+# ToCopyBackward would read dW on the main stream) and its ``.grad`` must be unset (AccumulateGrad
+# then stores the tensor; a ``+=`` into an existing gradient would read it). Otherwise the
+# weight gradient runs on the main stream as usual.
 # ------------------------------------------------------------------------------------------------
 _ASYNC_WGRAD = False
 _SIDE: Dict[int, "torch.cuda.Stream"] = {}
@@ -599,6 +608,7 @@ class WeightFlipper:
         self._key = None
         self._src: list = []
         self._dst: list = []
+        self._retired: list = []   # old flip buffers a captured graph may still reference
 
     def scope(self):
         return _FlipScope(self)
@@ -611,10 +621,22 @@ class WeightFlipper:
             return None
         key = tuple((w.data_ptr(), tuple(w.shape)) for w in ws)
         if key != self._key:
-            self._src = ws
-            self._dst = [torch.empty(w.shape[1], w.shape[0], w.shape[2], w.shape[3],
-                                     device=w.device, dtype=w.dtype,
-                                     memory_format=torch.channels_last) for w in ws]
+            # A captured hipGraph keeps writing and reading the flip buffers it was captured
+            # with, so they are never freed while the flipper lives: a destination whose shape
+            # is unchanged is reused in place, and superseded buffers are retired (kept alive)
+            # instead of being handed back to the allocator for other tensors.
+            old = {}
+            for d in self._dst:
+                old.setdefault(tuple(d.shape), []).append(d)
+            dst = []
+            for w in ws:
+                shp = (w.shape[1], w.shape[0], w.shape[2], w.shape[3])
+                pool = old.get(shp)
+                dst.append(pool.pop(0) if pool else
+                           torch.empty(shp, device=w.device, dtype=w.dtype,
+                                       memory_format=torch.channels_last))
+            self._retired.extend(d for pool in old.values() for d in pool)
+            self._src, self._dst = ws, dst
             self._key = key
         _ext.load().conv_flip_multi(self._src, self._dst)
         return {w.data_ptr(): d for w, d in zip(self._src, self._dst)}
@@ -669,6 +691,7 @@ class _ConvFn(torch.autograd.Function):
             y = conv2d_fwd(x, w, stride, pad, plan.fwd)
         ctx.save_for_backward(x, w)
         ctx.conf = (stride, pad, plan)
+        ctx.w_leaf = w.is_leaf
         # W' of a WeightFlipper scope (flipped this step, before this forward)
         ctx.wflip = _active_flip(w) if (stride == 1 and plan.bwd != MIOPEN) else None
         # the backward-data kernel can take a masked addend (a BN's (dy, ReLU bits), see GradJoin)
@@ -723,7 +746,7 @@ class _ConvFn(torch.autograd.Function):
                 dx = None
         if ctx.needs_input_grad[1]:
             side = None
-            if _ASYNC_WGRAD and dy.is_cuda:
+            if _ASYNC_WGRAD and dy.is_cuda and ctx.w_leaf and w.grad is None:
                 main = torch.cuda.current_stream()
                 side = _side_stream(dy.device)
                 side.wait_stream(main)   # dy, x (and w) are complete on the main stream

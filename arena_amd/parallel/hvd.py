@@ -10,6 +10,8 @@ This module provides the same user-facing calls, designed for one process per GP
     hvd.broadcast_parameters(model.state_dict(), root_rank=0)
     opt = hvd.DistributedOptimizer(opt, named_parameters=model.named_parameters())
 
+``broadcast_parameters`` / ``broadcast_`` / ``allgather`` run the xGMI copy kernels when every
+rank's GPU is mapped into every rank (single node, ``xgmi.usable``), else RCCL (gloo on CPU).
 ``DistributedOptimizer`` packs gradients into flat fp32 buckets with the native multi-tensor
 kernel as soon as each bucket's last gradient is produced (post-accumulate hooks), launches an
 async all_reduce per bucket so communication overlaps the rest of backward, and unpacks the
@@ -28,7 +30,28 @@ import torch.distributed as dist
 from .. import ops
 from ..runtime import heartbeat
 
-_STATE = {"pg": None, "local_rank": 0, "local_size": 1}
+_STATE = {"pg": None, "local_rank": 0, "local_size": 1, "xgmi": None}
+# staging floats of the communicator used by broadcast/allgather (64 MB; larger tensors go
+# through it in pieces)
+_XGMI_STAGING = 16 << 20
+
+
+def _xgmi_comm(t: Optional[torch.Tensor] = None):
+    """The job's xGMI communicator for broadcast/allgather (collective on first use), or None to
+    use RCCL/gloo: CPU tensors, ``ARENA_XGMI=0``, or ranks that cannot map each other's GPUs."""
+    if t is not None and not t.is_cuda:
+        return None
+    c = _STATE["xgmi"]
+    if c is None:
+        from . import xgmi
+        c = False
+        if xgmi.usable():
+            try:
+                c = xgmi.XgmiComm(staging_elems=_XGMI_STAGING)
+            except xgmi.XgmiUnavailable:
+                c = False
+        _STATE["xgmi"] = c
+    return c or None
 
 
 def init(backend: Optional[str] = None, timeout_s: float = 600.0):
@@ -77,6 +100,10 @@ def local_size() -> int:
 
 
 def shutdown() -> None:
+    c = _STATE["xgmi"]
+    if c:
+        c.close()
+    _STATE["xgmi"] = None
     if dist.is_initialized():
         dist.destroy_process_group()
 
@@ -107,14 +134,22 @@ def allgather(tensor: torch.Tensor) -> torch.Tensor:
     mx = int(max(int(s.item()) for s in sizes))
     pad = torch.zeros((mx,) + tuple(tensor.shape[1:]), device=tensor.device, dtype=tensor.dtype)
     pad[: tensor.shape[0]] = tensor
-    outs = [torch.empty_like(pad) for _ in range(size())]
-    dist.all_gather(outs, pad)
+    comm = _xgmi_comm(tensor)
+    if comm is not None:
+        outs = list(comm.all_gather(pad))      # one copy kernel over xGMI
+    else:
+        outs = [torch.empty_like(pad) for _ in range(size())]
+        dist.all_gather(outs, pad)
     return torch.cat([o[: int(s.item())] for o, s in zip(outs, sizes)], dim=0)
 
 
 def broadcast_(tensor: torch.Tensor, root_rank: int = 0) -> torch.Tensor:
     if size() > 1:
-        dist.broadcast(tensor, root_rank)
+        comm = _xgmi_comm(tensor)
+        if comm is not None:
+            comm.broadcast_(tensor, root_rank)
+        else:
+            dist.broadcast(tensor, root_rank)
     return tensor
 
 
@@ -133,7 +168,7 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
             by_dtype.setdefault((t.dtype, t.device), []).append(t)
     for (dt, dev), ts in by_dtype.items():
         flat = torch.cat([t.detach().reshape(-1) for t in ts])
-        dist.broadcast(flat, root_rank)
+        broadcast_(flat, root_rank)      # xGMI direct pull / scatter + all-gather, or RCCL
         off = 0
         with torch.no_grad():
             for t in ts:

@@ -12,16 +12,23 @@ RCCL fallback"). Kernels live in csrc/ccl/xgmi_ccl.hip; this module owns the reg
   reduce locally (one barrier instead of two: latency-bound sizes);
 * ``adam_`` = reduce-scatter of the gradient + Adam on the owned chunk + all-gather of the
   updated parameters, in one kernel (ZeRO-1-style sharded optimizer state);
+* ``broadcast_`` / ``all_gather`` = one copy kernel each (direct pull or scatter + all-gather for
+  broadcast; every rank pulls every shard for all-gather), any dtype (moved as raw 4-byte words);
 * construction runs a self-test on every rank and agrees on the outcome over the process group,
   so either ALL ranks use xGMI or all fall back to RCCL (never a split decision). Barrier waits are
   bounded in-kernel; a timeout sets an error flag that ``check()`` raises on.
 
-Only meaningful on a single node (all ranks' GPUs in one xGMI hive); ``usable()`` checks that.
+Only meaningful on a single node (all ranks' GPUs in one xGMI hive, mapped into every rank's
+process). ``usable()`` establishes that collectively: every rank reports its host (name + boot
+id), its own GPU and the GPUs it can see, and xGMI is used only if all ranks share the host and
+each rank's GPU is visible to every other rank -- true for the local backend's ranks, false for
+K8s pods (one device-plugin allocation per pod) or multi-node jobs, which then use RCCL.
 """
 from __future__ import annotations
 
 import os
-from typing import Optional
+import socket
+from typing import List, Optional
 
 import torch
 import torch.distributed as dist
@@ -37,12 +44,64 @@ class XgmiUnavailable(RuntimeError):
 
 
 def _sig_bytes(ext) -> int:
-    return 2 * ext.ccl_max_blocks * ext.ccl_max_ranks * 4
+    return getattr(ext, "ccl_phases", 2) * ext.ccl_max_blocks * ext.ccl_max_ranks * 4
+
+
+def _device_id(i: int) -> str:
+    p = torch.cuda.get_device_properties(i)
+    uuid = getattr(p, "uuid", None)
+    if uuid is not None and str(uuid).strip("0-"):
+        return str(uuid)
+    bus = getattr(p, "pci_bus_id", None)
+    return f"pci:{getattr(p, 'pci_domain_id', 0)}:{bus}" if bus is not None else ""
+
+
+def host_identity() -> dict:
+    """What decides whether two ranks can map each other's GPU memory (see module doc)."""
+    try:
+        with open("/proc/sys/kernel/random/boot_id") as f:
+            boot = f.read().strip()
+    except OSError:
+        boot = ""
+    ident = {"host": socket.gethostname(), "boot": boot, "own": "", "visible": []}
+    if torch.cuda.is_available():
+        try:
+            ident["visible"] = [_device_id(i) for i in range(torch.cuda.device_count())]
+            ident["own"] = ident["visible"][torch.cuda.current_device()]
+        except Exception:  # noqa: BLE001 - no identity: the visibility check is skipped
+            ident["own"], ident["visible"] = "", []
+    return ident
+
+
+def identities_share_node(infos: List[dict]) -> bool:
+    """True iff every rank runs on one host (same name and boot) and, where GPU identities are
+    known, each rank's own GPU is visible in every rank's process."""
+    if not infos or len({(i.get("host"), i.get("boot")) for i in infos}) != 1:
+        return False
+    owns = [i.get("own") for i in infos]
+    if all(owns):
+        if len(set(owns)) != len(owns) and len(set(owns)) != 1:
+            return False          # some ranks share a GPU and others do not: not a layout we map
+        for i in infos:
+            vis = set(i.get("visible") or [])
+            if not all(o in vis for o in owns):
+                return False
+    return True
+
+
+def same_node(group=None) -> bool:
+    """Collective: gather every rank's :func:`host_identity` and check
+    :func:`identities_share_node` (identical answer on all ranks)."""
+    w = dist.get_world_size(group)
+    infos: List[Optional[dict]] = [None] * w
+    dist.all_gather_object(infos, host_identity(), group=group)
+    return identities_share_node(infos)
 
 
 def usable(group=None) -> bool:
-    """Same-node world of 2..8 GPU ranks with the native extension present."""
-    if os.environ.get("ARENA_XGMI", "1") == "0" or not torch.cuda.is_available():
+    """Same-node world of 2..8 GPU ranks with the native extension present on every rank.
+    Collective over ``group`` (all ranks must call it) once the cheap env checks pass."""
+    if os.environ.get("ARENA_XGMI", "1") == "0":
         return False
     if not dist.is_initialized():
         return False
@@ -52,7 +111,21 @@ def usable(group=None) -> bool:
     local = os.environ.get("LOCAL_WORLD_SIZE")
     if local is not None and int(local) != int(os.environ.get("WORLD_SIZE", w)):
         return False  # multi-node job: inter-node traffic belongs to RCCL
-    return _ext.available()
+    ok = bool(torch.cuda.is_available() and _ext.available())
+    infos: List[Optional[dict]] = [None] * w
+    dist.all_gather_object(infos, {"ok": ok, **host_identity()}, group=group)
+    return all(i["ok"] for i in infos) and identities_share_node(infos)
+
+
+def _words(t: torch.Tensor) -> Optional[torch.Tensor]:
+    """1-D float32 view of a dense tensor's bytes (any dtype), or None when its size or address
+    is not a multiple of 16 bytes (the kernels move float4 words)."""
+    if not t.is_contiguous() or t.numel() == 0:
+        return None
+    nbytes = t.numel() * t.element_size()
+    if nbytes % 16 or t.data_ptr() % 16:
+        return None
+    return t.reshape(-1).view(torch.uint8).view(torch.float32)
 
 
 def _round4(n: int) -> int:
@@ -226,6 +299,54 @@ class XgmiComm:
         self.peers.adam(M, V, int(n), float(lr), lr_t, float(betas[0]), float(betas[1]),
                         float(eps), float(weight_decay), t_step, float(grad_scale), bool(tf_style),
                         ctr_dst, ctr_src, int(ctr_add))
+
+    def broadcast_(self, t: torch.Tensor, root: int = 0) -> torch.Tensor:
+        """In-place broadcast of ``t`` (any dtype) from ``root`` -- bit-exact copy."""
+        if not t.is_cuda:
+            raise TypeError("xGMI broadcast takes GPU tensors")
+        w = _words(t)
+        if w is not None and w.numel() <= self.staging_elems:
+            self.peers.broadcast(w, w, int(root))
+            return t
+        src = t if t.is_contiguous() else t.contiguous()
+        raw = src.reshape(-1).view(torch.uint8)
+        stage = self._buf.view(torch.uint8)
+        piece = self.staging_elems * 4
+        for s0 in range(0, raw.numel(), piece):
+            m = min(piece, raw.numel() - s0)
+            m16 = (m + 15) // 16 * 16
+            if self.rank == root:
+                stage[:m].copy_(raw[s0:s0 + m])
+            view = self._buf[:m16 // 4]
+            self.peers.broadcast(view, view, int(root))
+            if self.rank != root:
+                raw[s0:s0 + m].copy_(stage[:m])
+        if src is not t:
+            t.copy_(src)
+        return t
+
+    def all_gather(self, t: torch.Tensor) -> torch.Tensor:
+        """``torch.cat`` over ranks of equally shaped ``t`` along a new leading dim: returns
+        [world, *t.shape] (bit-exact copies)."""
+        if not t.is_cuda:
+            raise TypeError("xGMI all-gather takes GPU tensors")
+        out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        wi, wo = _words(t), _words(out)
+        if wi is not None and wo is not None and wi.numel() <= self.staging_elems:
+            self.peers.allgather(wi, wo)
+            return out
+        raw = t.contiguous().reshape(-1).view(torch.uint8)
+        dst = out.view(self.world, -1).view(torch.uint8)
+        stage = self._buf.view(torch.uint8)
+        piece = self.staging_elems * 4
+        for s0 in range(0, raw.numel(), piece):
+            m = min(piece, raw.numel() - s0)
+            m16 = (m + 15) // 16 * 16
+            stage[:m].copy_(raw[s0:s0 + m])
+            tmp = torch.empty(self.world * m16, dtype=torch.uint8, device=t.device)
+            self.peers.allgather(self._buf[:m16 // 4], tmp.view(torch.float32))
+            dst[:, s0:s0 + m].copy_(tmp.view(self.world, m16)[:, :m])
+        return out
 
     def check(self) -> None:
         """Raise if any barrier wait timed out since construction (host sync)."""

@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto",
                     help="DP gradient path: fused xGMI reduce-scatter/Adam/all-gather kernel or "
                          "RCCL all_reduce + flat Adam (auto = xgmi when its self-test passes)")
+    ap.add_argument("--verify-every", type=int, default=0,
+                    help="N>1: every K timed steps, compare a parameter checksum across ranks "
+                         "(and the xGMI barrier flags) and abort on divergence; adds a host sync "
+                         "per check. The replicas are always verified once after timing.")
     ap.add_argument("--resnet", type=int, default=1,
                     help="1: also time ResNet-50 training (bs128/GPU, bf16, hipGraph) and report "
                          "it as extra resnet50_* keys of the same JSON line (single GPU only)")
@@ -130,9 +134,24 @@ def main():
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    check = None
+    if world > 1:
+        from arena_amd.parallel.verify import ReplicaCheck
+        check = ReplicaCheck(args.verify_every,
+                             lambda: [tr.P] if hasattr(tr, "P") else list(tr.model.parameters()),
+                             group=pg,
+                             comms=[getattr(tr, "xgmi", None)])
     g0, e0 = getattr(tr, "graph_steps", 0), getattr(tr, "eager_steps", 0)
     t0 = time.perf_counter()
-    run(args.steps)
+    if check is not None and args.verify_every > 0:
+        done = 0
+        while done < args.steps:
+            k = min(args.verify_every, args.steps - done)
+            run(k)
+            done += k
+            check.maybe(done)
+    else:
+        run(args.steps)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if args.impl == "fused":
@@ -149,8 +168,11 @@ def main():
         elapsed = float(e.item())
 
     extra = {}
-    if getattr(tr, "xgmi", None) is not None:
-        tr.xgmi.check()  # a timed-out barrier would mean invalid results: fail loudly
+    if check is not None:
+        # replicas bit-identical on every rank and no xGMI barrier timed out, or every rank
+        # raises (ReplicaMismatch) and the run fails loudly instead of printing a number
+        check.verify(args.steps)
+        extra["replicas_verified"] = check.checks
     loss, acc = tr.recent_metrics(100)
     extra["train_loss_last100"] = round(loss, 5)
     extra["train_acc_last100"] = round(acc, 5)

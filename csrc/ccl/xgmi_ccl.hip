@@ -30,6 +30,18 @@
 // and after the barrier reads the whole vector from all peers and reduces it locally (see
 // xgmi_allreduce_oneshot_kernel for why the second barrier is not needed).
 //
+// Broadcast and all-gather (Horovod's broadcast_global_variables / allgather) are pure copies
+// over the same registered buffers:
+//   * broadcast, small vectors: direct pull -- the root stages its vector, barrier, every other
+//     rank reads it over its own link, barrier. Each link carries n bytes.
+//   * broadcast, large vectors: scatter + all-gather -- rank c pulls chunk c from the root into its
+//     own buffer, barrier, every rank pulls chunk q from rank q, barrier. Each link carries 2n/W
+//     bytes (4x less than direct pull at W = 8), for one extra barrier.
+//   * all-gather: every rank stages its shard, barrier, reads shard q from rank q for all q (W
+//     loads in flight per thread), barrier. Each link carries one shard.
+// The last barrier of each call keeps a rank from restaging its buffer while a peer still reads
+// it (the same argument as for the two-shot allreduce).
+//
 // Barrier waits are bounded (timeout_cycles of the 100 MHz s_memrealtime clock): a peer that never
 // arrives sets *err and the kernel drains instead of hanging the GPU; the host checks err.
 #include <hip/hip_runtime.h>
@@ -248,6 +260,237 @@ __global__ __launch_bounds__(kThreads) void xgmi_adam_kernel(ArenaXgmiPeers P, f
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Copies between registered buffers: U float4 slots per thread, all loads before any store.
+template <int NSRC>
+__device__ __forceinline__ void pull_range(float* const* dst, const float* const* src,
+                                           const long long* dst_off, const long long* src_off,
+                                           long long lo, long long hi, const long long* lim) {
+  constexpr int U = kU;
+  for (long long o0 = lo + threadIdx.x * 4; o0 < hi; o0 += (long long)kThreads * 4 * U) {
+    float4 v[U][NSRC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long o = o0 + (long long)u * kThreads * 4;
+#pragma unroll
+      for (int q = 0; q < NSRC; ++q)
+        if (o < hi && o < lim[q]) v[u][q] = ld4(src[q] + src_off[q] + o);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long o = o0 + (long long)u * kThreads * 4;
+#pragma unroll
+      for (int q = 0; q < NSRC; ++q)
+        if (o < hi && o < lim[q]) st4(dst[q] + dst_off[q] + o, v[u][q]);
+    }
+  }
+}
+
+// Direct-pull broadcast: block b moves floats [b*S, b*S+S) of the vector.
+template <int W>
+__global__ __launch_bounds__(kThreads) void xgmi_bcast_direct_kernel(ArenaXgmiPeers P,
+                                                                      const float* __restrict__ in,
+                                                                      float* __restrict__ out,
+                                                                      long long n, int root,
+                                                                      long long S) {
+  const int b = blockIdx.x;
+  const uint32_t e = P.epoch[b] + 1;
+  const long long lo = (long long)b * S;
+  const long long hi = std::min(lo + S, n);
+  const long long zero = 0;
+  const float* src_in = in;  // (restrict-qualified parameters do not bind to T* const*)
+  float* dst_out = out;
+  if (P.rank == root && in != P.buf[root]) {
+    float* d = P.buf[root];
+    pull_range<1>(&d, &src_in, &zero, &zero, lo, hi, &n);
+  }
+  xbarrier<W>(P, 0, b, e);
+  if (P.rank != root) {
+    const float* src = P.buf[root];
+    pull_range<1>(&dst_out, &src, &zero, &zero, lo, hi, &n);   // over the link to the root
+  } else if (out != in) {
+    pull_range<1>(&dst_out, &src_in, &zero, &zero, lo, hi, &n);
+  }
+  xbarrier<W>(P, 1, b, e);
+  if (threadIdx.x == 0) P.epoch[b] = e;
+}
+
+// Scatter + all-gather broadcast: chunk c = [c*L, (c+1)*L); block b owns sub-range
+// [b*S, b*S+S) of every chunk.
+template <int W>
+__global__ __launch_bounds__(kThreads) void xgmi_bcast_twoshot_kernel(ArenaXgmiPeers P,
+                                                                       const float* __restrict__ in,
+                                                                       float* __restrict__ out,
+                                                                       long long n, int root,
+                                                                       long long L, long long S) {
+  const int b = blockIdx.x;
+  const uint32_t e = P.epoch[b] + 1;
+  const long long lo = (long long)b * S;
+  const long long hi = std::min(lo + S, L);
+  const int r = P.rank;
+  if (r == root && in != P.buf[root]) copy_chunks<W>(P.buf[root], in, n, L, lo, hi);
+  xbarrier<W>(P, 0, b, e);
+  if (r != root) {  // scatter: my chunk from the root, into my own buffer
+    float* d = P.buf[r];
+    const float* src = P.buf[root];
+    const long long off = (long long)r * L;
+    const long long lim = n - off;
+    pull_range<1>(&d, &src, &off, &off, lo, hi, &lim);
+  }
+  xbarrier<W>(P, 1, b, e);
+  if (r != root) {  // all-gather: chunk q from rank q (the root's chunk from the root)
+    float* dst[W];
+    const float* src[W];
+    long long off[W], lim[W];
+#pragma unroll
+    for (int q = 0; q < W; ++q) {
+      dst[q] = out;
+      src[q] = P.buf[q];
+      off[q] = (long long)q * L;
+      // my own chunk is already in place when the destination is my staging buffer
+      lim[q] = (q == r && out == P.buf[r]) ? 0 : n - off[q];
+    }
+    pull_range<W>(dst, src, off, off, lo, hi, lim);
+  } else if (out != in) {
+    copy_chunks<W>(out, in, n, L, lo, hi);
+  }
+  xbarrier<W>(P, 2, b, e);
+  if (threadIdx.x == 0) P.epoch[b] = e;
+}
+
+// All-gather: out[q*m + j] = shard of rank q; block b moves floats [b*S, b*S+S) of every shard.
+template <int W>
+__global__ __launch_bounds__(kThreads) void xgmi_allgather_kernel(ArenaXgmiPeers P,
+                                                                   const float* __restrict__ in,
+                                                                   float* __restrict__ out,
+                                                                   long long m, long long S) {
+  const int b = blockIdx.x;
+  const uint32_t e = P.epoch[b] + 1;
+  const long long lo = (long long)b * S;
+  const long long hi = std::min(lo + S, m);
+  const long long zero = 0;
+  float* mine = P.buf[P.rank];
+  const float* src_in = in;
+  if (in != mine) pull_range<1>(&mine, &src_in, &zero, &zero, lo, hi, &m);
+  xbarrier<W>(P, 0, b, e);
+  float* dst[W];
+  const float* src[W];
+  long long doff[W], soff[W], lim[W];
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    dst[q] = out;
+    src[q] = P.buf[q];
+    doff[q] = (long long)q * m;
+    soff[q] = 0;
+    lim[q] = m;
+  }
+  pull_range<W>(dst, src, doff, soff, lo, hi, lim);
+  xbarrier<W>(P, 1, b, e);
+  if (threadIdx.x == 0) P.epoch[b] = e;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Sharded momentum SGD on bf16 weights with fp32 masters (data-parallel CNN training):
+//   reduce-scatter of the bf16 gradients (fp32 sums, fixed rank order) -> SGD on the owned chunk
+//   of the fp32 master weights and momentum -> all-gather of the rounded bf16 weights into every
+//   rank's weight buffer (buf2), one kernel per gradient bucket.
+// Element units are bf16; a bucket [off, off + n) is split into W chunks of L (multiple of 8),
+// block b owns sub-range [b*S, b*S + S) of every chunk. Same update as mt_sgd_master
+// (torch.optim.SGD, dampening 0): d = g + wd*w; m = mu*m + d; w -= lr*m. Masters/momentum are
+// full-length arrays of which each rank only ever updates its own chunks.
+__device__ __forceinline__ float bf_lo(uint32_t v) { return __uint_as_float(v << 16); }
+__device__ __forceinline__ float bf_hi(uint32_t v) { return __uint_as_float(v & 0xffff0000u); }
+__device__ __forceinline__ uint32_t to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (u >> 16) | 0x40u;  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);                                  // round to nearest even
+  return u >> 16;
+}
+
+struct SgdCoef {
+  float lr, mu, wd, scale;
+};
+
+__device__ __forceinline__ void sgd1(const SgdCoef& c, float g, float& w, float& m) {
+  const float d = g * c.scale + c.wd * w;
+  m = c.mu * m + d;
+  w = w - c.lr * m;
+}
+
+template <int W>
+__global__ __launch_bounds__(kThreads) void xgmi_sgd_bf16_kernel(ArenaXgmiPeers P,
+                                                                  float* __restrict__ master,
+                                                                  float* __restrict__ mom,
+                                                                  long long off, long long n,
+                                                                  long long L, long long S,
+                                                                  SgdCoef c) {
+  const int b = blockIdx.x;
+  const uint32_t e = P.epoch[b] + 1;
+  const long long lo = (long long)b * S;
+  const long long hi = std::min(lo + S, L);
+  xbarrier<W>(P, 0, b, e);
+  const long long base = (long long)P.rank * L;
+  constexpr int U = 2;  // 8 bf16 per slot: U * (W + 4) 16-byte operands in flight per thread
+  for (long long o0 = lo + threadIdx.x * 8; o0 < hi; o0 += (long long)kThreads * 8 * U) {
+    uint4 g[U][W];
+    float4 w[U][2], m[U][2];
+    bool ok[U];
+    long long idx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long o = o0 + (long long)u * kThreads * 8;
+      ok[u] = o < hi && base + o < n;
+      idx[u] = off + (ok[u] ? base + o : 0);
+#pragma unroll
+      for (int q = 0; q < W; ++q)
+        g[u][q] = *reinterpret_cast<const uint4*>(
+            reinterpret_cast<const uint16_t*>(P.buf[q]) + idx[u]);
+      w[u][0] = ld4(master + idx[u]);
+      w[u][1] = ld4(master + idx[u] + 4);
+      m[u][0] = ld4(mom + idx[u]);
+      m[u][1] = ld4(mom + idx[u] + 4);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float acc[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const uint32_t x = (&g[u][0].x)[k];
+        acc[2 * k] = bf_lo(x);
+        acc[2 * k + 1] = bf_hi(x);
+      }
+#pragma unroll
+      for (int q = 1; q < W; ++q) {  // fixed order: identical on every rank
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const uint32_t x = (&g[u][q].x)[k];
+          acc[2 * k] += bf_lo(x);
+          acc[2 * k + 1] += bf_hi(x);
+        }
+      }
+      float* wv = &w[u][0].x;
+      float* mv = &m[u][0].x;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) sgd1(c, acc[k], wv[k], mv[k]);
+      uint4 packed;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        (&packed.x)[k] = to_bf16(wv[2 * k]) | (to_bf16(wv[2 * k + 1]) << 16);
+      if (ok[u]) {
+        st4(master + idx[u], w[u][0]);
+        st4(master + idx[u] + 4, w[u][1]);
+        st4(mom + idx[u], m[u][0]);
+        st4(mom + idx[u] + 4, m[u][1]);
+#pragma unroll
+        for (int q = 0; q < W; ++q)
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(P.buf2[q]) + idx[u]) = packed;
+      }
+    }
+  }
+  xbarrier<W>(P, 1, b, e);
+  if (threadIdx.x == 0) P.epoch[b] = e;
+}
+
 // Floats of a chunk per block. Every block pays two cross-rank barriers (one L2 writeback + one
 // invalidate each), so blocks are made fat rather than numerous; tunable for sweeps.
 long long g_block_elems = 4096;
@@ -256,6 +499,19 @@ long long g_block_elems = 4096;
 // (W-1) x n bytes per rank over the links instead of 2 (W-1)/W x n, so the default stays at 32 KB.
 long long g_oneshot_max = ARENA_CCL_ONESHOT_ELEMS / 2;
 static_assert(ARENA_CCL_ONESHOT_ELEMS / kOneSub <= kMaxB, "one-shot blocks exceed the flag slots");
+
+// Broadcasts up to this many floats pull directly from the root (one barrier less); above it the
+// scatter + all-gather form moves 2/W of the bytes per link. W = 2 always pulls directly.
+long long g_bcast_direct_max = 128 << 10;
+
+void range_geometry(long long n, long long* S, int* nb) {
+  int blocks = (int)std::min<long long>(
+      kMaxB, std::max<long long>(1, (n + g_block_elems - 1) / g_block_elems));
+  long long s = (n + blocks - 1) / blocks;
+  s = (s + 3) / 4 * 4;
+  *S = s;
+  *nb = blocks;
+}
 
 void geometry(long long n, int W, long long* L, long long* S, int* nb) {
   long long l = (n + W - 1) / W;
@@ -348,6 +604,86 @@ hipError_t arena_ccl_adam(const ArenaXgmiPeers* P, float* M, float* V, long long
 }
 
 void arena_ccl_set_block_elems(long long e) { g_block_elems = e < 256 ? 256 : e; }
+
+// Broadcast n floats (n % 4 == 0, n <= buf_elems) from `root`: in = the root's source, out =
+// every rank's destination (in == out is allowed; non-roots ignore in).
+hipError_t arena_ccl_broadcast(const ArenaXgmiPeers* P, const float* in, float* out, long long n,
+                               int root, hipStream_t stream) {
+  const int W = P->world;
+  if (W < 2 || W > kMaxR || n <= 0 || n % 4 || n > P->buf_elems || root < 0 || root >= W)
+    return hipErrorInvalidValue;
+  if (W == 2 || n <= g_bcast_direct_max) {
+    long long S;
+    int nb;
+    range_geometry(n, &S, &nb);
+    ARENA_CCL_DISPATCH(W, xgmi_bcast_direct_kernel, dim3(nb), dim3(kThreads), 0, stream, *P, in,
+                       out, n, root, S);
+    return hipGetLastError();
+  }
+  long long L, S;
+  int nb;
+  geometry(n, W, &L, &S, &nb);
+  ARENA_CCL_DISPATCH(W, xgmi_bcast_twoshot_kernel, dim3(nb), dim3(kThreads), 0, stream, *P, in,
+                     out, n, root, L, S);
+  return hipGetLastError();
+}
+
+void arena_ccl_set_bcast_direct_max(long long e) { g_bcast_direct_max = e < 0 ? 0 : e; }
+
+// Chunking of a sharded-SGD bucket (bf16 elements): L per rank (multiple of 8), S per block.
+void sgd_geometry(long long n, int W, long long* L, long long* S, int* nb) {
+  long long l = (n + W - 1) / W;
+  l = (l + 7) / 8 * 8;
+  const long long per_block = std::max<long long>(8, g_block_elems * 2);  // bytes as the fp32 path
+  int blocks = (int)std::min<long long>(kMaxB, std::max<long long>(1, (l + per_block - 1) / per_block));
+  long long s = (l + blocks - 1) / blocks;
+  s = (s + 7) / 8 * 8;
+  *L = l;
+  *S = s;
+  *nb = blocks;
+}
+
+// One bucket [off, off + n) (bf16 elements, off and n multiples of 8) of the sharded SGD: bf16
+// grads staged in every rank's buf, bf16 weights in every rank's buf2, fp32 master/mom local.
+hipError_t arena_ccl_sgd_bf16(const ArenaXgmiPeers* P, float* master, float* mom, long long off,
+                              long long n, float lr, float momentum, float wd, float scale,
+                              hipStream_t stream) {
+  const int W = P->world;
+  if (W < 2 || W > kMaxR || n <= 0 || off < 0 || n % 8 || off % 8 || P->buf2[0] == nullptr)
+    return hipErrorInvalidValue;
+  if ((off + n + 1) / 2 > P->buf_elems || (off + n + 1) / 2 > P->buf2_elems)
+    return hipErrorInvalidValue;
+  long long L, S;
+  int nb;
+  sgd_geometry(n, W, &L, &S, &nb);
+  SgdCoef c{lr, momentum, wd, scale};
+  ARENA_CCL_DISPATCH(W, xgmi_sgd_bf16_kernel, dim3(nb), dim3(kThreads), 0, stream, *P, master, mom,
+                     off, n, L, S, c);
+  return hipGetLastError();
+}
+
+// The [lo, hi) bf16 elements of bucket [off, off + n) whose masters rank r updates.
+void arena_ccl_sgd_shard(long long off, long long n, int world, int r, long long* lo,
+                         long long* hi) {
+  long long L, S;
+  int nb;
+  sgd_geometry(n, world, &L, &S, &nb);
+  *lo = off + std::min(n, (long long)r * L);
+  *hi = off + std::min(n, (long long)(r + 1) * L);
+}
+
+// All-gather m floats per rank (m % 4 == 0, m <= buf_elems) into out[W * m].
+hipError_t arena_ccl_allgather(const ArenaXgmiPeers* P, const float* in, float* out, long long m,
+                               hipStream_t stream) {
+  const int W = P->world;
+  if (W < 2 || W > kMaxR || m <= 0 || m % 4 || m > P->buf_elems) return hipErrorInvalidValue;
+  long long S;
+  int nb;
+  range_geometry(m, &S, &nb);
+  ARENA_CCL_DISPATCH(W, xgmi_allgather_kernel, dim3(nb), dim3(kThreads), 0, stream, *P, in, out,
+                     m, S);
+  return hipGetLastError();
+}
 
 // The slice of the flat vector whose optimizer state rank `r` owns under arena_ccl_adam.
 void arena_ccl_shard(long long n, int world, int r, long long* lo, long long* hi) {

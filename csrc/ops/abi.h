@@ -109,10 +109,12 @@ struct ArenaBNBwd {
 // One-shot allreduce region: 2 x ONESHOT_ELEMS floats (double-buffered by call parity) that sit
 // right after the buf_elems floats of every staging buffer (the host allocates them).
 #define ARENA_CCL_ONESHOT_ELEMS 16384
+// barrier phases per call (the scatter + all-gather broadcast uses three)
+#define ARENA_CCL_PHASES 3
 struct ArenaXgmiPeers {
   float* buf[ARENA_CCL_MAX_RANKS];    // staging / gradient buffer of each rank (+ one-shot tail)
   float* buf2[ARENA_CCL_MAX_RANKS];   // second buffer (parameters for the fused Adam step)
-  uint32_t* sig[ARENA_CCL_MAX_RANKS]; // uncached flags: [2 phases][MAX_BLOCKS][MAX_RANKS]
+  uint32_t* sig[ARENA_CCL_MAX_RANKS]; // uncached flags: [3 phases][MAX_BLOCKS][MAX_RANKS]
   uint32_t* epoch;                    // local, per block: calls completed
   int* err;                           // local: set to 1 when a barrier wait timed out
   long long buf_elems;                // capacity of buf[] (floats)

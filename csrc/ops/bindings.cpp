@@ -44,6 +44,14 @@ hipError_t arena_ccl_allreduce(const ArenaXgmiPeers*, const float*, float*, long
 hipError_t arena_ccl_adam(const ArenaXgmiPeers*, float*, float*, long long, ArenaAdam,
                           ArenaCounterOp, hipStream_t);
 void arena_ccl_shard(long long, int, int, long long*, long long*);
+hipError_t arena_ccl_broadcast(const ArenaXgmiPeers*, const float*, float*, long long, int,
+                               hipStream_t);
+hipError_t arena_ccl_allgather(const ArenaXgmiPeers*, const float*, float*, long long,
+                               hipStream_t);
+void arena_ccl_set_bcast_direct_max(long long);
+hipError_t arena_ccl_sgd_bf16(const ArenaXgmiPeers*, float*, float*, long long, long long, float,
+                              float, float, float, hipStream_t);
+void arena_ccl_sgd_shard(long long, long long, int, int, long long*, long long*);
 void arena_ccl_set_block_elems(long long);
 void arena_ccl_set_oneshot_max(long long);
 long long arena_ccl_get_oneshot_max();
@@ -1325,6 +1333,54 @@ class XgmiPeers {
               "xgmi_adam");
   }
 
+  // Pure copies: the tensors are raw 4-byte words (any dtype viewed as float32 by the caller).
+  void broadcast(Tensor in, Tensor out, int64_t root) {
+    check_f32(in, "in");
+    check_f32(out, "out");
+    const int64_t n = out.numel();
+    TORCH_CHECK(in.numel() == n, "broadcast: in/out size mismatch");
+    TORCH_CHECK(n % 4 == 0 && n <= p_.buf_elems, "broadcast: numel must be a multiple of 4 and <= ",
+                p_.buf_elems);
+    TORCH_CHECK(root >= 0 && root < p_.world, "broadcast: root out of range");
+    TORCH_CHECK(in.data_ptr<float>() != nullptr && ((uintptr_t)in.data_ptr() % 16) == 0 &&
+                    ((uintptr_t)out.data_ptr() % 16) == 0,
+                "broadcast: 16-byte aligned tensors required");
+    check_hip(arena_ccl_broadcast(&p_, in.data_ptr<float>(), out.data_ptr<float>(), n, (int)root,
+                                  cur_stream()),
+              "xgmi_broadcast");
+  }
+
+  void allgather(Tensor in, Tensor out) {
+    check_f32(in, "in");
+    check_f32(out, "out");
+    const int64_t m = in.numel();
+    TORCH_CHECK(out.numel() == m * p_.world, "allgather: out must hold world * numel(in)");
+    TORCH_CHECK(m % 4 == 0 && m <= p_.buf_elems, "allgather: numel must be a multiple of 4 and <= ",
+                p_.buf_elems);
+    TORCH_CHECK(((uintptr_t)in.data_ptr() % 16) == 0 && ((uintptr_t)out.data_ptr() % 16) == 0,
+                "allgather: 16-byte aligned tensors required");
+    check_hip(arena_ccl_allgather(&p_, in.data_ptr<float>(), out.data_ptr<float>(), m,
+                                  cur_stream()),
+              "xgmi_allgather");
+  }
+
+  // Sharded momentum SGD over one bucket [off, off + n) of bf16 elements (see xgmi_ccl.hip).
+  void sgd_bf16(Tensor master, Tensor mom, int64_t off, int64_t n, double lr, double momentum,
+                double wd, double scale) {
+    check_f32(master, "master");
+    check_f32(mom, "mom");
+    TORCH_CHECK(p_.buf2[0] != nullptr, "sgd_bf16 needs the weight buffers (buf2)");
+    TORCH_CHECK(off >= 0 && n > 0 && off % 8 == 0 && n % 8 == 0, "sgd_bf16: off/n must be "
+                "multiples of 8");
+    TORCH_CHECK(master.numel() >= off + n && mom.numel() >= off + n, "sgd_bf16: master/mom too "
+                "short");
+    TORCH_CHECK((off + n + 1) / 2 <= p_.buf_elems && (off + n + 1) / 2 <= p_.buf2_elems,
+                "sgd_bf16: bucket exceeds the registered buffers");
+    check_hip(arena_ccl_sgd_bf16(&p_, master.data_ptr<float>(), mom.data_ptr<float>(), off, n,
+                                 (float)lr, (float)momentum, (float)wd, (float)scale, cur_stream()),
+              "xgmi_sgd_bf16");
+  }
+
   int64_t world() const { return p_.world; }
 
  private:
@@ -1381,11 +1437,20 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ccl_set_block_elems", [](int64_t e) { arena_ccl_set_block_elems(e); });
   m.def("ccl_set_oneshot_max", [](int64_t e) { arena_ccl_set_oneshot_max(e); });
   m.def("ccl_get_oneshot_max", []() { return (int64_t)arena_ccl_get_oneshot_max(); });
+  m.def("ccl_set_bcast_direct_max", [](int64_t e) { arena_ccl_set_bcast_direct_max(e); });
+  m.def("ccl_sgd_shard", [](int64_t off, int64_t n, int64_t world, int64_t rank) {
+    long long lo = 0, hi = 0;
+    arena_ccl_sgd_shard(off, n, (int)world, (int)rank, &lo, &hi);
+    return std::vector<int64_t>{lo, hi};
+  });
   py::class_<XgmiPeers>(m, "XgmiPeers")
       .def(py::init<std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, Tensor,
                     Tensor, int64_t, int64_t, int64_t, double>())
       .def("allreduce", &XgmiPeers::allreduce)
       .def("adam", &XgmiPeers::adam)
+      .def("broadcast", &XgmiPeers::broadcast)
+      .def("allgather", &XgmiPeers::allgather)
+      .def("sgd_bf16", &XgmiPeers::sgd_bf16)
       .def_property_readonly("world", &XgmiPeers::world);
 #ifdef ARENA_TIMELINE
   m.def("timeline_read", [](bool clear) {
@@ -1398,6 +1463,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.attr("ccl_max_blocks") = ARENA_CCL_MAX_BLOCKS;
   m.attr("ccl_max_ranks") = ARENA_CCL_MAX_RANKS;
   m.attr("ccl_oneshot_elems") = ARENA_CCL_ONESHOT_ELEMS;
+  m.attr("ccl_phases") = ARENA_CCL_PHASES;
   m.attr("arch") = "gfx950";
 #ifndef ARENA_SRC_HASH
 #define ARENA_SRC_HASH "unknown"

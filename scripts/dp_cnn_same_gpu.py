@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
-"""Rehearse the data-parallel ResNet step (hvd.DistributedOptimizer over the xGMI kernel) on ONE
-GPU: W ranks share GPU 0, gloo process group for setup (RCCL refuses two ranks on one device).
+"""Rehearse the data-parallel ResNet step on ONE GPU: W ranks share GPU 0, gloo process group for
+setup (RCCL refuses two ranks on one device). Default: bf16 weights with the sharded xGMI SGD
+(arena_amd.parallel.zero); --master_weights off: fp32 weights + hvd.DistributedOptimizer.
 
 What it checks:
 
@@ -43,9 +44,9 @@ def rank_main(rank, world, port, a, q):
     args = types.SimpleNamespace(model=a.model, batch_size=a.batch_size, image_size=a.image_size,
                                  num_classes=1000, width=64, learning_rate=0.1, momentum=0.9,
                                  weight_decay=4e-5, bucket_mb=a.bucket_mb, comm="xgmi",
-                                 data_format="NHWC")
+                                 data_format="NHWC", dtype="bf16", master_weights=a.master_weights)
     model, opt, x, y = cnn_bench.build(args, torch.device("cuda", 0), world)
-    assert opt.comm == "xgmi", opt.comm
+    assert opt.comm.startswith("xgmi"), opt.comm
     for i in range(a.warmup):
         cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
         torch.cuda.synchronize()
@@ -67,10 +68,14 @@ def rank_main(rank, world, port, a, q):
             loss = cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    opt.xgmi.check()
-    flat = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
-    digest = float(flat.double().sum().item()), float(flat.double().abs().sum().item())
-    q.put((rank, dt, float(loss), digest, len(opt.buckets)))
+    comms = list(getattr(opt, "comms", [])) or [opt.xgmi]
+    for c in comms:
+        if c is not None:
+            c.check()
+    flat = torch.cat([p.detach().double().reshape(-1) for p in model.parameters()])
+    digest = float(flat.sum().item()), float(flat.abs().sum().item())
+    nb = len(opt.opts[0].buckets) if hasattr(opt, "opts") else len(opt.buckets)
+    q.put((rank, dt, float(loss), digest, nb, opt.comm))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -85,6 +90,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step as a hipGraph")
+    ap.add_argument("--master_weights", choices=["auto", "on", "off"], default="auto",
+                    help="auto/on: bf16 weights + ShardedMasterSGD (xGMI reduce-scatter / SGD / "
+                         "all-gather); off: fp32 weights + DistributedOptimizer buckets")
     a = ap.parse_args()
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -102,6 +110,7 @@ def main():
     print(json.dumps({"world": a.world, "same_gpu": True, "model": a.model,
                       "batch_per_rank": a.batch_size, "steps": a.steps,
                       "exec": "hipgraph" if a.graph else "eager", "buckets": res[0][4],
+                      "comm": res[0][5],
                       "images_per_s_all_ranks": round(a.world * a.batch_size * a.steps / dt, 1),
                       "ms_per_step": round(dt / a.steps * 1e3, 3), "final_loss": round(res[0][2], 4),
                       "replicas_identical": same}), flush=True)

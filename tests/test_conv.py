@@ -111,6 +111,97 @@ def test_conv_kernel_rejects_bad_shapes():
     x, wt = _data(1, 64, 8, 8, 64, 3, "cuda")
     with pytest.raises(RuntimeError, match="Cout % 128"):
         _ext.load().conv_fwd(x, wt, 1, 1, 0, False)
+    # pad > R-1 would need a negative backward-data padding: not a kernel shape (MIOpen runs it)
+    x, wt = _data(2, 64, 8, 8, 128, 1, "cuda")
+    assert conv.kernel_ok(x, wt, 1, 0) and not conv.kernel_ok(x, wt, 1, 1)
+    x3, w3 = _data(2, 64, 8, 8, 128, 3, "cuda")
+    assert conv.kernel_ok(x3, w3, 1, 2) and not conv.kernel_ok(x3, w3, 1, 3)
+
+
+@pytest.mark.gpu
+def test_conv_module_oversized_padding_falls_back(monkeypatch):
+    """A 1x1 conv with padding=1 is a legal nn.Conv2d: it trains (through MIOpen) instead of
+    failing in the kernel's autotuning or backward."""
+    monkeypatch.setenv("ARENA_CONV", "auto")
+    torch.manual_seed(0)
+    m = conv.Conv2dNHWC(64, 128, 1, stride=1, padding=1, bias=False).cuda().to(
+        memory_format=torch.channels_last)
+    ref = torch.nn.Conv2d(64, 128, 1, stride=1, padding=1, bias=False).cuda()
+    ref.weight.data.copy_(m.weight.data)
+    x = torch.randn(2, 64, 8, 8, device="cuda").contiguous(memory_format=torch.channels_last)
+    x.requires_grad_()
+    xr = x.detach().clone().requires_grad_()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x)
+        yr = ref(xr)
+    assert y.shape == (2, 128, 10, 10)
+    y.float().square().sum().backward()
+    yr.float().square().sum().backward()
+    assert _rel(y, yr) < 2e-2 and _rel(x.grad, xr.grad) < 2e-2
+    assert _rel(m.weight.grad, ref.weight.grad) < 2e-2
+
+
+@pytest.mark.gpu
+def test_async_wgrad_with_fp32_weights_under_autocast(monkeypatch):
+    """with fp32 parameters under bf16 autocast the cast's backward reads dW on the main
+    stream, and a second backward accumulates into .grad: async wgrad must give exactly the
+    gradients of the synchronous path (it falls back to the main stream there)."""
+    from arena_amd.models import resnet as R
+    monkeypatch.setenv("ARENA_CONV", "ours")
+    torch.manual_seed(0)
+    net = R.resnet("resnet_tiny", num_classes=10).cuda().to(memory_format=torch.channels_last)
+    x = torch.randn(4, 3, 64, 64, device="cuda").contiguous(memory_format=torch.channels_last)
+    grads = {}
+    try:
+        for mode in (False, True):
+            conv.set_async_wgrad(mode)
+            net.zero_grad(set_to_none=True)
+            for _ in range(2):        # the second pass accumulates into existing .grad
+                with torch.autocast("cuda", dtype=torch.bfloat16):
+                    out = net(x)
+                out.float().square().mean().backward()
+            conv.sync_wgrad()
+            torch.cuda.synchronize()
+            grads[mode] = {n: p.grad.clone() for n, p in net.named_parameters()}
+    finally:
+        conv.set_async_wgrad(False)
+    for n, g in grads[False].items():
+        assert torch.equal(grads[True][n], g), n
+
+
+@pytest.mark.gpu
+def test_weight_flipper_keeps_buffers_for_captured_graphs():
+    """a key change (weights re-bound, train/eval toggled) must not free the flip
+    buffers a captured graph still uses: same-shape buffers are reused in place and the rest are
+    retired, not released."""
+    from arena_amd.models import resnet as R
+    conv.set_mode("ours")
+    try:
+        torch.manual_seed(0)
+        net = R.resnet("resnet_tiny", num_classes=10).cuda().to(memory_format=torch.channels_last)
+        for m in net.modules():
+            if isinstance(m, torch.nn.Conv2d):
+                m.weight.data = m.weight.data.to(torch.bfloat16).contiguous(
+                    memory_format=torch.channels_last)
+        fl = net._flipper
+        with torch.enable_grad():
+            assert fl._prepare() is not None
+        before = [d.data_ptr() for d in fl._dst]
+        assert before
+        first = fl.convs[0]
+        first.weight.data = first.weight.data.clone()      # re-bound: the key changes
+        with torch.enable_grad():
+            flips = fl._prepare()
+        after = [d.data_ptr() for d in fl._dst]
+        assert sorted(after) == sorted(before)              # same buffers, no new allocation
+        assert flips[first.weight.data_ptr()].data_ptr() in before
+        first.train(False)                                   # fewer convs: one buffer retired
+        with torch.enable_grad():
+            fl._prepare()
+        live = {d.data_ptr() for d in fl._dst} | {d.data_ptr() for d in fl._retired}
+        assert set(before) <= live
+    finally:
+        conv.set_mode(None)
 
 
 @pytest.mark.gpu

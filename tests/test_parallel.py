@@ -256,3 +256,99 @@ def test_hvd_channels_last_gradients_average_correctly():
     opt.step()
     ref = torch.cat([p.detach().reshape(-1) for p in model.parameters()]).numpy()
     np.testing.assert_allclose(f0, ref, rtol=1e-5, atol=1e-6)
+
+
+def test_identities_share_node_rules():
+    from arena_amd.parallel.xgmi import identities_share_node as share
+    a = {"host": "n1", "boot": "b", "own": "g0", "visible": ["g0", "g1"]}
+    b = {"host": "n1", "boot": "b", "own": "g1", "visible": ["g0", "g1"]}
+    assert share([a, b])
+    assert not share([a, {**b, "host": "n2"}])                  # another host
+    assert not share([a, {**b, "boot": "other"}])               # same name, another machine boot
+    # K8s pods: each process sees only its own device-plugin GPU
+    assert not share([{**a, "visible": ["g0"]}, {**b, "visible": ["g1"]}])
+    # ranks time-sharing one GPU (the same-GPU test setup) are mappable
+    assert share([{**a, "visible": ["g0"]}, {**a, "visible": ["g0"]}])
+    # unknown GPU identities: the host check decides
+    assert share([{**a, "own": "", "visible": []}, {**b, "own": "", "visible": []}])
+    assert not share([])
+
+
+def _guard_worker(rank, world, port, q, hosts):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from arena_amd.parallel import xgmi
+    socket.gethostname = lambda: hosts[rank]        # what each rank reports as its host
+    dist.init_process_group("gloo")
+    try:
+        q.put((rank, xgmi.same_node(), xgmi.usable()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("hosts,want", [(("a", "a"), True), (("a", "b"), False)])
+def test_xgmi_same_host_guard_gloo(hosts, want, monkeypatch):
+    """The collective guard on real gloo ranks: mixed hostnames refuse xGMI on every rank (and
+    without a GPU, usable() is False everywhere, decided collectively)."""
+    monkeypatch.delenv("LOCAL_WORLD_SIZE", raising=False)
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_guard_worker, args=(r, 2, port, q, hosts)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = dict((r, (s, u)) for r, s, u in (q.get(timeout=120) for _ in range(2)))
+    for p in procs:
+        p.join(30)
+    assert got[0] == got[1] == (want, False)
+
+
+def _verify_worker(rank, world, port, q, perturb):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    import torch.distributed as dist
+    from arena_amd.parallel.verify import ReplicaCheck, ReplicaMismatch, param_checksum
+    dist.init_process_group("gloo")
+    try:
+        ps = [torch.arange(12, dtype=torch.float32).view(3, 4), torch.ones(5, dtype=torch.bfloat16)]
+        chk = ReplicaCheck(2, lambda: ps)
+        out = []
+        for step in range(1, 5):
+            if perturb and step == 3 and rank == 1:
+                ps[0][1, 2] += 1e-3            # one element off on one rank
+            try:
+                chk.maybe(step)
+                out.append("ok")
+            except ReplicaMismatch as e:
+                out.append(str(e))
+        # a swap of two elements keeps the plain sum but not the checksum
+        a = torch.tensor([1.0, 2.0, 3.0])
+        swapped = not torch.equal(param_checksum([a]), param_checksum([a.flip(0)]))
+        q.put((rank, out, chk.checks, swapped))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("perturb", [False, True])
+def test_replica_check_gloo(perturb):
+    """--verify-every: replicas compared every K steps; one perturbed element on one rank makes
+    EVERY rank raise at the next check (no rank left waiting in a collective)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_verify_worker, args=(r, 2, port, q, perturb)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {r: (o, n, s) for r, o, n, s in (q.get(timeout=120) for _ in range(2))}
+    for p in procs:
+        p.join(30)
+    for r in (0, 1):
+        out, n, swapped = got[r]
+        assert swapped and n == 2
+        assert out[0] == out[2] == "ok"                 # steps 1, 3: no check
+        assert out[1] == "ok"                           # step 2: agree
+        if perturb:
+            assert "diverged at step 4" in out[3]
+        else:
+            assert out[3] == "ok"

@@ -264,7 +264,8 @@ def _cnn_graph(rank, world, port, q):
         hvd.init()
         args = types.SimpleNamespace(model="resnet_tiny", data_format="NHWC", batch_size=8,
                                      image_size=32, num_classes=10, width=16, learning_rate=0.05,
-                                     momentum=0.9, weight_decay=1e-3, bucket_mb=0.05, comm="xgmi")
+                                     momentum=0.9, weight_decay=1e-3, bucket_mb=0.05, comm="xgmi",
+                                     master_weights="off", dtype="fp32")
         dev = torch.device("cuda", 0)
         flats = []
         for graph in (False, True):
@@ -293,6 +294,183 @@ def _cnn_graph(rank, world, port, q):
         q.put((rank, None, traceback.format_exc()))
 
 
+def _zero_sgd(rank, world, port, q):
+    """Data-parallel ResNet with bf16 weights: ShardedMasterSGD (reduce-scatter bf16 grads ->
+    fp32 master SGD on the owned chunk -> all-gather bf16 weights, one xGMI kernel per bucket).
+    Replicas stay bit-identical, eager == hipGraph replay, and the weights follow a single
+    process that averages both ranks' gradients (fp32 sums of the bf16 grads) and applies the
+    same momentum SGD in torch."""
+    try:
+        dist = _init(rank, world, port)
+        import types
+        from arena_amd.examples import cnn_bench
+        from arena_amd.parallel import hvd
+        from arena_amd.parallel.zero import ShardedMasterSGD
+        hvd.init()
+        args = types.SimpleNamespace(model="resnet_tiny", data_format="NHWC", batch_size=8,
+                                     image_size=32, num_classes=10, width=64, learning_rate=0.05,
+                                     momentum=0.9, weight_decay=1e-3, bucket_mb=0.05, comm="xgmi",
+                                     master_weights="auto", dtype="bf16")
+        dev = torch.device("cuda", 0)
+        bf = torch.bfloat16
+        res = {}
+        flats = []
+        for graph in (False, True):
+            model, opt, x, y = cnn_bench.build(args, dev, world)
+            zero = opt.opts[0]
+            assert isinstance(zero, ShardedMasterSGD) and len(zero.buckets) > 1, opt.comm
+            assert all(p.dtype == bf for p in zero.params)
+            # reference replica (this rank computes it too): same init, both ranks' batches
+            ref = [p.detach().clone() for p in model.parameters()]
+            names = [n for n, _ in model.named_parameters()]
+            decay = {id(p) for p in zero.params}
+            kinds = [id(p) in decay for p in model.parameters()]
+            master = [r.float() for r in ref]
+            mom = [torch.zeros_like(m) for m in master]
+            if not graph:
+                batches = []
+                for r in range(world):
+                    gg = torch.Generator(device=dev).manual_seed(r)
+                    xr = torch.randn(x.shape, device=dev, generator=gg).contiguous(
+                        memory_format=torch.channels_last)
+                    yr = torch.randint(0, 10, (x.shape[0],), device=dev, generator=gg)
+                    batches.append((xr, yr))
+                assert torch.equal(batches[rank][0], x) and torch.equal(batches[rank][1], y)
+            for step in range(5):
+                if graph and step == 2:
+                    g, _ = cnn_bench.capture_step(model, opt, x, y, bf)
+                    dist.barrier()
+                if graph and step >= 2:
+                    g.replay()
+                    continue
+                if not graph:
+                    # the reference step, from the replica's current weights
+                    state = [p.detach().clone() for p in model.parameters()]
+                    grads = []
+                    params = list(model.parameters())
+                    for xr, yr in batches:
+                        # autograd.grad: no .grad accumulation, so the optimizers' gradient
+                        # hooks (which launch the collectives) stay silent
+                        with torch.autocast("cuda", dtype=bf):
+                            loss = torch.nn.functional.cross_entropy(model(xr), yr)
+                        gr = torch.autograd.grad(loss, params)
+                        grads.append([gi.float().clone() for gi in gr])
+                    with torch.no_grad():
+                        for p, w in zip(model.parameters(), state):
+                            p.copy_(w)
+                    for i, dk in enumerate(kinds):
+                        gsum = grads[0][i]
+                        for gr in grads[1:]:
+                            gsum = gsum + gr[i]
+                        gavg = gsum * (1.0 / world)
+                        if dk:
+                            gavg = gavg + 1e-3 * master[i]
+                        mom[i] = 0.9 * mom[i] + gavg
+                        master[i] = master[i] - 0.05 * mom[i]
+                cnn_bench.train_step(model, opt, x, y, bf)
+            torch.cuda.synchronize()
+            for c in opt.comms:
+                if c is not None:
+                    c.check()
+            flats.append(torch.cat([p.detach().float().reshape(-1) for p in model.parameters()]))
+            if not graph:
+                worst = 0.0
+                for p, m, n in zip(model.parameters(), master, names):
+                    d = float((p.detach().float() - m.to(p.dtype).float()).abs().max())
+                    worst = max(worst, d / max(1e-3, float(m.abs().max())))
+                res["vs_reference"] = worst
+            zero.close()
+            dist.barrier()
+        res["graph_vs_eager"] = float((flats[0] - flats[1]).abs().max())
+        res["digest"] = float(flats[1].double().sum())
+        res["digest_eager"] = float(flats[0].double().sum())
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
+def _bcast_gather(rank, world, port, q):
+    """Broadcast (direct pull and scatter + all-gather) and all-gather: bit-exact copies of
+    host-known data, every dtype, ragged sizes through the staging buffer, graph capture, and the
+    Horovod API (hvd.broadcast_parameters / allgather) on top."""
+    try:
+        dist = _init(rank, world, port)
+        from arena_amd.parallel import hvd
+        from arena_amd.parallel.xgmi import XgmiComm
+        comm = XgmiComm(staging_elems=1 << 16, timeout_s=30.0)
+        res = {}
+        g = torch.Generator(device="cuda").manual_seed(99)
+        # sizes straddle the direct/two-shot switch (forced both ways below) and the staging size
+        sizes = [4, 12, 1000, 4096, 65536, 70001, 3 * (1 << 16) + 5]
+        for direct_max in (1 << 30, 0):
+            comm.ext.ccl_set_bcast_direct_max(direct_max)
+            for root in (0, world - 1):
+                for dt in (torch.float32, torch.bfloat16, torch.int64, torch.uint8):
+                    for n in sizes:
+                        want = torch.randint(-100, 100, (n,), device="cuda", generator=g).to(dt)
+                        x = want.clone() if rank == root else torch.zeros_like(want)
+                        comm.broadcast_(x, root)
+                        res[("b", direct_max > 0, root, str(dt), n)] = bool(torch.equal(x, want))
+        comm.ext.ccl_set_bcast_direct_max(128 << 10)
+        for dt in (torch.float32, torch.bfloat16, torch.int32):
+            for n in (4, 1000, 8192, 70001, (1 << 16) + 7):
+                shards = [torch.randint(-9, 9, (n, 3), device="cuda", generator=g).to(dt)
+                          for _ in range(world)]
+                out = comm.all_gather(shards[rank])
+                res[("g", str(dt), n)] = bool(torch.equal(out, torch.stack(shards)))
+        # back-to-back calls of all kinds without host sync, then inside a captured graph
+        seq = []
+        for i in range(12):
+            n = (1000, 70000, 4096)[i % 3]
+            w = torch.randint(-50, 50, (n,), device="cuda", generator=g).float()
+            seq.append((i % world, w, w.clone() if rank == i % world else torch.zeros_like(w)))
+        for root, _, x in seq:
+            comm.broadcast_(x, root)
+            comm.all_reduce_(x)                 # interleave with the allreduce kernels
+        torch.cuda.synchronize()
+        res["mixed"] = all(bool(torch.equal(x, w * world)) for _, w, x in seq)
+        y = torch.zeros(4096, device="cuda")
+        src = torch.arange(4096, device="cuda", dtype=torch.float32)
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            comm.broadcast_(y, 0)
+        torch.cuda.current_stream().wait_stream(s)
+        gr = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gr, capture_error_mode="thread_local"):
+            comm.broadcast_(y, 0)
+            z = comm.all_gather(y[:1024])
+        for k in range(3):
+            if rank == 0:
+                y.copy_(src + k)
+            torch.cuda.synchronize()
+            dist.barrier()
+            gr.replay()
+            torch.cuda.synchronize()
+            res[("graph", k)] = bool(torch.equal(y, src + k)) and \
+                bool(torch.equal(z, (src[:1024] + k).expand(world, 1024)))
+        comm.check()
+        comm.close()
+        # the Horovod API on top (its own communicator, created collectively on first use)
+        hvd.init()
+        assert hvd._xgmi_comm(torch.zeros(1, device="cuda")) is not None
+        sd = {"w": torch.full((33, 7), float(rank), device="cuda"),
+              "h": torch.full((5,), float(rank), device="cuda", dtype=torch.bfloat16),
+              "n": torch.full((3,), rank, device="cuda", dtype=torch.int64)}
+        hvd.broadcast_parameters(sd, root_rank=world - 1)
+        res["hvd_bcast"] = all(bool(torch.all(t == world - 1)) for t in sd.values())
+        part = torch.full((rank + 1, 2), float(rank), device="cuda")
+        cat = hvd.allgather(part)
+        want = torch.cat([torch.full((r + 1, 2), float(r), device="cuda") for r in range(world)])
+        res["hvd_allgather"] = bool(torch.equal(cat, want))
+        hvd.shutdown()
+        q.put((rank, res, None))
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
 def _run(fn, world, timeout=240):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -312,6 +490,23 @@ def _run(fn, world, timeout=240):
             if p.is_alive():
                 p.kill()
     return out
+
+
+def test_dp_resnet_sharded_bf16_sgd():
+    out = _run(_zero_sgd, 2, timeout=300)
+    for r, res in out.items():
+        assert res["vs_reference"] < 2e-2, (r, res)
+        assert res["graph_vs_eager"] < 1e-2, (r, res)
+    assert out[0]["digest"] == out[1]["digest"], out                # replicas bit-identical
+    assert out[0]["digest_eager"] == out[1]["digest_eager"], out
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+def test_xgmi_broadcast_allgather_bit_exact(world):
+    out = _run(_bcast_gather, world, timeout=300)
+    for r, res in out.items():
+        bad = [k for k, v in res.items() if not v]
+        assert not bad, f"rank {r}: {bad[:8]}"
 
 
 # world 8 = the 8-GPU node's kernel instantiation (W = 8 register footprint, 7 peers), here as 8
