@@ -323,8 +323,9 @@ class FusedMLPTrainer:
         self._graph_parity0 = start_parity & 1
         # warm up on a side stream (allocator / collective communicators initialised outside
         # capture), then restore the state so warm-up steps do not count as training.
-        snap = [t.clone() for t in (self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2,
-                                    self.rows)]
+        state = (self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2, self.rows,
+                 self.loss_hist, self.corr_hist)
+        snap = [t.clone() for t in state]
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -332,11 +333,18 @@ class FusedMLPTrainer:
                 self._launch_step(parity=(self.steps_done + k) & 1)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
-        for t, v in zip((self.P, self.M, self.V, self.ctrA, self.ctrB, self.logits2, self.rows),
-                        snap):
+        for t, v in zip(state, snap):
             t.copy_(v)
         try:
-            self._graphs[steps_per_graph] = self._capture(steps_per_graph)
+            g = self._capture(steps_per_graph)
+            # one replay now, undone: the first launch of an instantiated graph uploads it to
+            # the device, which would otherwise land in the first timed replay (the baked step
+            # parity may not match step 0 here; every buffer it touches is restored anyway)
+            g.replay()
+            torch.cuda.synchronize()
+            for t, v in zip(state, snap):
+                t.copy_(v)
+            self._graphs[steps_per_graph] = g
             self.graph_mode = "full"
         except Exception as e:  # noqa: BLE001
             self._graph_error = repr(e)

@@ -5,9 +5,13 @@ and apply ReLU: ``y = relu(bn(x) + residual)``. That is the whole tail of a ResN
 one module. On an MI355X, with a channels_last bf16/fp32 input and a supported channel count,
 it runs the HIP kernels in ``csrc/ops/bn_kernels.hip``:
 
-* forward: 2 launches (statistics, then apply + ReLU mask bits); the statistics come from the
-  producing convolution's epilogue when it ran on the MFMA kernel (then only a finalize);
-* backward: 2 launches (reductions, then dx and the residual gradient) plus a finalize.
+* forward: 2 launches (statistics, then apply + ReLU mask bits); the statistics come finished
+  from the producing convolution's epilogue when it ran on the MFMA kernel (then 1 launch).
+  The statistics pass and the conv epilogue accumulate fp64 sums with memory-side atomics and
+  their last block finishes them, and the apply kernel derives its coefficients: no finalize
+  launch (one per layer and direction before, ~10 us each);
+* backward: 2 launches (reductions, whose last block writes the dx coefficients, then dx and the
+  residual gradient).
 
 Otherwise it runs the same math as stock PyTorch ops. That includes CPU tensors, which serve as
 the reference.
@@ -51,6 +55,17 @@ def reference(x, residual, weight, bias, running_mean, running_var, training, mo
     return F.relu(y) if relu else y
 
 
+class FinishedStats:
+    """Batch statistics of a conv output finished inside the conv kernel (fp64 [2, C]: mean,
+    biased variance; ``conv2d_fwd(..., with_stats=True, final=True)``): the BN layer consuming it
+    runs only its apply kernel, which derives invstd/scale/shift and updates the running
+    statistics itself."""
+    __slots__ = ("fin",)
+
+    def __init__(self, fin: torch.Tensor):
+        self.fin = fin
+
+
 class ResidualMask:
     """The residual gradient of ``relu(bn3(x) + r)`` is dy * ReLU mask. When r is the output of
     another fused BN (a downsample block's ``down_bn``), bn3's backward returns dy itself for r and
@@ -78,9 +93,15 @@ class _BNActFn(torch.autograd.Function):
                 eps, relu, num_batches=None, stats=None, join=None, link=None, res_out=None,
                 res_in=None):
         ext = _ext.load()
-        part, rpb = stats if (stats is not None and training) else (None, 0)
+        part, rpb, fin = None, 0, None
+        if stats is not None and training:
+            if isinstance(stats, FinishedStats):
+                fin = stats.fin       # finished by the conv epilogue: apply only
+            else:
+                part, rpb = stats
         y, mean, invstd, mask = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
-                                           training, momentum, eps, relu, num_batches, part, rpb)
+                                           training, momentum, eps, relu, num_batches, part, rpb,
+                                           fin)
         # the ReLU mask is kept as bits (M*C/8 bytes), not as a reference to y
         ctx.save_for_backward(x, mask if relu and training else None, mean, invstd, weight)
         ctx.relu, ctx.has_res, ctx.training = relu, residual is not None, training

@@ -65,7 +65,7 @@ def pick_variant(m: int, cout: int) -> int:
 
 def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int = -1,
                with_stats: bool = False, addend: Tensor | None = None, bn=None,
-               addmask: Tensor | None = None):
+               addmask: Tensor | None = None, final: bool = False):
     """y = conv2d(x, w) (+ addend) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S].
 
     with_stats: returns (y, (part, rpb)) where part holds per-tile BatchNorm partials of y
@@ -76,7 +76,9 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
     only the addend elements whose bit is set are added (a ReLU'd gradient, see GradJoin).
     bn: (bn_x, bn_mask or None, bn_mean) when y is the gradient of a BatchNorm layer's output:
     returns (y, (part, rpb)) with that BN's backward partials (sum g, sum g (bn_x - mean) per
-    tile, g = y * mask) for its backward, which then skips its reduction pass."""
+    tile, g = y * mask) for its backward, which then skips its reduction pass.
+    final (with with_stats): the statistics come back finished, ``(y, FinishedStats)`` -- the
+    epilogue's fp64 atomics + last-tile ticket replace the BN's finalize launch."""
     x = x.contiguous(memory_format=torch.channels_last)
     w = w.contiguous(memory_format=torch.channels_last)
     if variant < 0:
@@ -88,8 +90,13 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
     if bn is not None:
         bx, bm, bmu = bn
         with_stats = True
+    fin = bool(final and with_stats and bn is None and addend is None)
     out = _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant), bool(with_stats),
-                               addend, bx, bm, bmu, addmask if addend is not None else None)
+                               addend, bx, bm, bmu, addmask if addend is not None else None,
+                               stats_final=fin)
+    if fin:
+        from .batchnorm import FinishedStats
+        return out[0], FinishedStats(out[1])
     if with_stats:
         return out[0], (out[1], TILES[variant][0])
     return out[0]
@@ -124,6 +131,29 @@ def set_bn_links(on: bool) -> None:
     """Enable/disable BNGradLink fusion (off by default; ARENA_BN_LINKS=1)."""
     global _BN_LINKS
     _BN_LINKS = bool(on)
+
+
+# BatchNorm statistics finished inside the conv kernel (fp64 atomics + last-tile ticket) instead
+# of per-tile partials plus a finalize launch in the BN layer (on by default; ARENA_BN_FINAL=0 for
+# A/Bs). Also switches the BN kernels' own statistics/backward reductions to the same acc mode.
+_BN_FINAL = os.environ.get("ARENA_BN_FINAL", "1") == "1"
+
+
+def set_bn_final(on: bool) -> None:
+    global _BN_FINAL
+    _BN_FINAL = bool(on)
+    if torch.cuda.is_available() and _ext.available():
+        _ext.load().bn_set_acc(bool(on))
+
+
+def _stats_out(want: bool, part: Tensor, rpb: int):
+    """What ``forward_stats`` hands the BN layer: finished statistics (fp64) or partials."""
+    if not want:
+        return None
+    if part.dtype == torch.float64:
+        from .batchnorm import FinishedStats
+        return FinishedStats(part)
+    return (part, rpb)
 
 
 def conv2d_bwd_data_strided(dy: Tensor, w: Tensor, x_hw: Tuple[int, int], stride: int, pad: int,
@@ -225,7 +255,8 @@ class _StemFn(torch.autograd.Function):
     def forward(ctx, z, w16, want_stats, fwd_variant, wgrad_cfg):
         Ho, Wo = z.shape[2], z.shape[3]
         out = _ext.load().conv_fwd_ex(z, w16, 1, 2, 2, Ho, Wo, int(fwd_variant), bool(want_stats),
-                                      None, None, [], True)
+                                      None, None, [], True, stats_final=bool(want_stats and
+                                                                            _BN_FINAL))
         ctx.save_for_backward(z)
         ctx.wgrad_cfg = wgrad_cfg
         ctx.set_materialize_grads(False)
@@ -685,6 +716,9 @@ class _ConvFn(torch.autograd.Function):
         part = x.new_empty(0, dtype=torch.float32)
         if plan.fwd == MIOPEN:
             y = F.conv2d(x, w, stride=stride, padding=pad)
+        elif want_stats and _BN_FINAL:
+            y, st = conv2d_fwd(x, w, stride, pad, plan.fwd, with_stats=True, final=True)
+            part = st.fin
         elif want_stats:
             y, (part, _) = conv2d_fwd(x, w, stride, pad, plan.fwd, with_stats=True)
         else:
@@ -804,7 +838,7 @@ class Conv2dNHWC(nn.Conv2d):
         want = want_stats and plan.fwd != MIOPEN and torch.is_grad_enabled() and self.training
         with torch.autocast("cuda", enabled=False):
             y, part = _ConvFn.apply(x, w, s, p, plan, want, join, bn_link)
-        return y, ((part, TILES[plan.fwd][0]) if want else None)
+        return y, _stats_out(want, part, TILES[plan.fwd][0])
 
 
 class StemConv2d(Conv2dNHWC):
@@ -839,7 +873,7 @@ class StemConv2d(Conv2dNHWC):
             w16 = _StemWeightFn.apply(w) if fuse else stem_weight(w.to(torch.bfloat16))
             fv, wcfg = _stem_plan(z, w16)
             y, part = _StemFn.apply(z, w16, want, fv, wcfg)
-        return y, ((part, TILES[fv][0]) if want else None)
+        return y, _stats_out(want, part, TILES[fv][0])
 
 
 _STEM_PLANS: Dict[tuple, Tuple[int, Tuple[int, int]]] = {}

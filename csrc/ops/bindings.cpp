@@ -64,7 +64,8 @@ hipError_t arena_conv_flip_multi(int, const void* const*, void* const*, const in
                                  const int*, hipStream_t);
 hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void*, const uint8_t*,
                              const void*, const uint8_t*, const float*, int, int, int, int, int,
-                             int, int, int, int, int, int, int, const int*, int, int, hipStream_t);
+                             int, int, int, int, int, int, int, const int*, int, int, double*,
+                             unsigned*, double*, int, hipStream_t);
 hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
                                int, int, int, int, int, int, int, int, int, int, int, float,
                                hipStream_t);
@@ -91,9 +92,11 @@ hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, i
 hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, int, int, int, int,
                              int, hipStream_t);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, uint8_t*, long long, int, int, int,
-                        float*, int, long long, double*, unsigned*, ArenaBNStats, hipStream_t);
+                        float*, int, long long, double*, unsigned*, ArenaBNStats, double*, int,
+                        double*, unsigned*, int, hipStream_t);
 hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, void*, long long, int,
-                        int, float*, int, double*, unsigned*, ArenaBNBwd, hipStream_t);
+                        int, float*, int, double*, unsigned*, ArenaBNBwd, double*, unsigned*, int,
+                        hipStream_t);
 #ifdef ARENA_TIMELINE
 hipError_t arena_timeline_read(long long*, int);
 #endif
@@ -716,6 +719,46 @@ unsigned* bn_tickets(const Tensor& like) {
   return reinterpret_cast<unsigned*>(pools[dev].data_ptr<int32_t>()) + set * kTicketsPerSet;
 }
 
+// Finished-statistics accumulators (conv_kernels.hip ConvArgs::bn_acc, bn_kernels.hip acc mode):
+// a rotating pool of zeroed sets, each [kAccSlots][2][2048] doubles + 32 tickets. Every kernel
+// that uses a set leaves it zeroed, so sets are reused without a memset (and graph replays stay
+// valid); consecutive users of one set are ordered by the stream.
+constexpr int kAccSets = 128, kAccSlots = 4, kAccC = 2048, kAccTickets = 32;
+struct AccSet {
+  double* acc;
+  unsigned* tickets;
+};
+AccSet bn_acc_set(const Tensor& like) {
+  static std::vector<Tensor> accs, tks;
+  static std::vector<unsigned> next;
+  const int dev = like.get_device();
+  if ((int)accs.size() <= dev) {
+    accs.resize(dev + 1);
+    tks.resize(dev + 1);
+    next.resize(dev + 1, 0);
+  }
+  if (!accs[dev].defined()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    check_hip(hipStreamIsCapturing(cur_stream(), &cs), "bn_acc_set");
+    TORCH_CHECK(cs == hipStreamCaptureStatusNone,
+                "arena BatchNorm: run one eager step before capturing a graph (its statistics "
+                "accumulators are allocated and zeroed on first use)");
+    accs[dev] = torch::zeros({(int64_t)kAccSets * kAccSlots * 2 * kAccC},
+                             like.options().dtype(torch::kFloat64));
+    tks[dev] = torch::zeros({kAccSets * kAccTickets}, like.options().dtype(torch::kInt32));
+    check_hip(hipStreamSynchronize(cur_stream()), "bn_acc_set zero");
+  }
+  const unsigned set = next[dev]++ % kAccSets;
+  return {accs[dev].data_ptr<double>() + (size_t)set * kAccSlots * 2 * kAccC,
+          reinterpret_cast<unsigned*>(tks[dev].data_ptr<int32_t>()) + set * kAccTickets};
+}
+
+// finished statistics / acc-mode reductions in the BN kernels (runtime switch for A/Bs)
+bool g_bn_acc = [] {
+  const char* e = getenv("ARENA_BN_FINAL");
+  return e == nullptr || e[0] != '0';
+}();
+
 Tensor bn_lvl2(int64_t nblk, int64_t C, const Tensor& like) {
   return torch::empty({arena_bn_lvl2_doubles(nblk, (int)C)}, like.options().dtype(torch::kFloat64));
 }
@@ -723,9 +766,12 @@ Tensor bn_lvl2(int64_t nblk, int64_t C, const Tensor& like) {
 // Returns (y, mean, invstd, mask). Eval mode normalises with the running statistics. mask (relu
 // in training, else empty): uint8 [M * C / 8], bit i of byte v = (y.flat[8 v + i] > 0).
 // stats_part/stats_rpb: BatchNorm partials of x from conv_fwd(with_stats=True) (training only).
+// stats_fin (training): finished fp64 [2][C] (mean, biased variance) from conv_fwd(...,
+// stats_final=True): no statistics pass and no finalize launch.
 std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT running_mean,
                            OptT running_var, bool training, double momentum, double eps,
-                           bool relu, OptT num_batches, OptT stats_part, int64_t stats_rpb) {
+                           bool relu, OptT num_batches, OptT stats_part, int64_t stats_rpb,
+                           OptT stats_fin) {
   const BNGeom g = bn_geom(x, "x");
   if (res.has_value()) bn_same(x, *res, "residual");
   auto f32 = x.options().dtype(torch::kFloat32);
@@ -754,14 +800,19 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
                   "num_batches_tracked must be an int64 scalar tensor");
       st.batches = reinterpret_cast<long long*>(num_batches->data_ptr<int64_t>());
     }
-    if (stats_part.has_value()) {
+    if (stats_fin.has_value()) {
+      TORCH_CHECK(stats_fin->is_cuda() && stats_fin->device() == x.device() &&
+                      stats_fin->scalar_type() == torch::kFloat64 && stats_fin->is_contiguous() &&
+                      stats_fin->numel() == 2 * g.C && !stats_part.has_value(),
+                  "stats_fin must be a contiguous fp64 [2, C] tensor (and excludes stats_part)");
+    } else if (stats_part.has_value()) {
       check_f32(*stats_part, "stats_part");
       TORCH_CHECK(stats_rpb > 0 && stats_part->is_contiguous(), "stats_part: bad layout");
       const int64_t nblk = (g.M + stats_rpb - 1) / stats_rpb;
       TORCH_CHECK(stats_part->numel() == nblk * 2 * g.C, "stats_part has ", stats_part->numel(),
                   " floats, expected ", nblk * 2 * g.C);
       part = *stats_part;
-    } else {
+    } else if (!g_bn_acc) {
       part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
     }
   } else {
@@ -779,9 +830,17 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
                                    : Tensor();
   const int ext_nblk = training && stats_part.has_value()
                            ? (int)((g.M + stats_rpb - 1) / stats_rpb) : 0;
-  Tensor lvl2;
+  Tensor lvl2, fin;
   unsigned* tickets = nullptr;
-  if (training) {
+  AccSet as{nullptr, nullptr};
+  int fin_ready = 0;
+  if (training && stats_fin.has_value()) {
+    fin = *stats_fin;
+    fin_ready = 1;
+  } else if (training && !stats_part.has_value() && g_bn_acc) {
+    fin = torch::empty({2, g.C}, x.options().dtype(torch::kFloat64));
+    as = bn_acc_set(x);
+  } else if (training) {
     const int64_t nblk = ext_nblk > 0 ? ext_nblk : part.numel() / (2 * g.C);
     lvl2 = bn_lvl2(nblk, g.C, x);
     tickets = bn_tickets(x);
@@ -789,9 +848,10 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
   check_hip(arena_bn_fwd(g.dtype, x.data_ptr(), res.has_value() ? res->data_ptr() : nullptr,
                          y.data_ptr(), mask.defined() ? mask.data_ptr<uint8_t>() : nullptr, g.M,
                          g.C, relu ? 1 : 0, training ? 1 : 0,
-                         training ? part.data_ptr<float>() : nullptr, ext_nblk,
-                         (long long)stats_rpb, training ? lvl2.data_ptr<double>() : nullptr,
-                         tickets, st, cur_stream()),
+                         part.defined() ? part.data_ptr<float>() : nullptr, ext_nblk,
+                         (long long)stats_rpb, lvl2.defined() ? lvl2.data_ptr<double>() : nullptr,
+                         tickets, st, fin.defined() ? fin.data_ptr<double>() : nullptr, fin_ready,
+                         as.acc, as.tickets, kAccSlots, cur_stream()),
             "bn_fwd");
   return {y, mean, invstd, mask};
 }
@@ -838,17 +898,26 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
                 " floats, expected ", nblk * 2 * g.C);
     part = *ext_part;
     ext_nblk = (int)nblk;
-  } else {
+  } else if (!g_bn_acc) {
     part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
   }
-  Tensor lvl2 = bn_lvl2(part.numel() / (2 * g.C), g.C, x);
+  AccSet as{nullptr, nullptr};
+  Tensor lvl2;
+  unsigned* tickets = nullptr;
+  if (part.defined()) {
+    lvl2 = bn_lvl2(part.numel() / (2 * g.C), g.C, x);
+    tickets = bn_tickets(x);
+  } else {
+    as = bn_acc_set(x);   // acc mode: the reduction's last block writes the coefficients
+  }
   Tensor dx = torch::empty_like(x);
   Tensor dres = with_res ? torch::empty_like(x) : Tensor();
   check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(),
                          relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(), dx.data_ptr(),
                          with_res ? dres.data_ptr() : nullptr, g.M, g.C, relu ? 1 : 0,
-                         part.data_ptr<float>(), ext_nblk, lvl2.data_ptr<double>(), bn_tickets(x), b,
-                         cur_stream()),
+                         part.defined() ? part.data_ptr<float>() : nullptr, ext_nblk,
+                         lvl2.defined() ? lvl2.data_ptr<double>() : nullptr, tickets, b, as.acc,
+                         as.tickets, kAccSlots, cur_stream()),
             "bn_bwd");
   return {dx, dres, dgamma, dbeta};
 }
@@ -873,9 +942,12 @@ void pool_check(const Tensor& t, const char* name) {
 // bn_x/bn_mask/bn_mean (optional, backward-data use): y is the gradient of a BatchNorm layer's
 // output; with with_stats the returned partials are that BN's backward partials (g = y * mask,
 // sum g, sum g * (bn_x - bn_mean)) for bn_bwd(..., ext_part, BM) instead of forward statistics.
+// stats_final (with with_stats, forward statistics only): the second output is the finished
+// batch statistics [2][Cout] fp64 (mean, biased variance) for bn_fwd(stats_fin=...) instead of
+// the per-tile partials.
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant,
                              bool with_stats, OptT addend, OptT bn_x, OptT bn_mask,
-                             OptT bn_mean, OptT addmask) {
+                             OptT bn_mean, OptT addmask, bool stats_final) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4,
               "conv_fwd: x and w must be 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16,
@@ -898,8 +970,15 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
   static const int bm[4] = {128, 128, 64, 64};
   const int64_t m_tiles = (N * Ho * Wo + bm[variant & 3] - 1) / bm[variant & 3];
-  Tensor part = with_stats ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
-                           : Tensor();
+  const bool fin = with_stats && stats_final;
+  TORCH_CHECK(!fin || (!bn_x.has_value() && !addend.has_value() && Cout <= kAccC),
+              "conv_fwd: stats_final is forward statistics without an addend");
+  Tensor part = with_stats && !fin
+                    ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
+                    : Tensor();
+  Tensor fin_t = fin ? torch::empty({2, Cout}, x.options().dtype(torch::kFloat64)) : Tensor();
+  AccSet as{nullptr, nullptr};
+  if (fin) as = bn_acc_set(x);
   if (addend.has_value()) {
     TORCH_CHECK(addend->sizes() == y.sizes() && addend->scalar_type() == torch::kBFloat16 &&
                     addend->device() == y.device() &&
@@ -927,7 +1006,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                 "conv_fwd: addmask needs an addend and numel(y) / 8 uint8 bytes");
   }
   check_hip(arena_conv_fwd_ex(x.data_ptr(), w.data_ptr(), y.data_ptr(),
-                              with_stats ? part.data_ptr<float>() : nullptr,
+                              with_stats && !fin ? part.data_ptr<float>() : nullptr,
                               addend.has_value() ? addend->data_ptr() : nullptr,
                               addmask.has_value() ? addmask->data_ptr<uint8_t>() : nullptr,
                               bn_x.has_value() ? bn_x->data_ptr() : nullptr,
@@ -937,8 +1016,10 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                               bn_x.has_value() ? bn_mean->data_ptr<float>() : nullptr,
                               (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R, (int)S,
                               (int)stride, (int)pad, (int)pad, 0, 0, nullptr, 0, (int)variant,
-                              cur_stream()),
+                              as.acc, as.tickets, fin ? fin_t.data_ptr<double>() : nullptr,
+                              kAccSlots, cur_stream()),
             "conv_fwd");
+  if (fin) return {y, fin_t};
   if (with_stats) return {y, part};
   return {y};
 }
@@ -1035,7 +1116,8 @@ std::vector<Tensor> conv_phase_weights(Tensor w, int64_t stride, int64_t pad) {
 // (in-place accumulate: each element is read and written by the same lane).
 std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_h, int64_t pad_w,
                                 int64_t Ho, int64_t Wo, int64_t variant, bool with_stats,
-                                OptT addend, OptT y_out, std::vector<int64_t> y_map, bool c16) {
+                                OptT addend, OptT y_out, std::vector<int64_t> y_map, bool c16,
+                                bool stats_final) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4 &&
                   x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16 &&
                   x.device() == w.device(),
@@ -1084,17 +1166,26 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
   static const int bm[4] = {128, 128, 64, 64};
   const int64_t m_tiles = (N * Ho * Wo + bm[variant & 3] - 1) / bm[variant & 3];
   TORCH_CHECK(!(with_stats && y_out.has_value()), "conv_fwd_ex: statistics need a dense output");
-  Tensor part = with_stats ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
-                           : Tensor();
+  const bool fin = with_stats && stats_final;
+  TORCH_CHECK(!fin || (!addend.has_value() && Cout <= kAccC),
+              "conv_fwd_ex: stats_final is forward statistics without an addend");
+  Tensor part = with_stats && !fin
+                    ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
+                    : Tensor();
+  Tensor fin_t = fin ? torch::empty({2, Cout}, x.options().dtype(torch::kFloat64)) : Tensor();
+  AccSet as{nullptr, nullptr};
+  if (fin) as = bn_acc_set(x);
   check_hip(arena_conv_fwd_ex(x.data_ptr(), w.data_ptr(), y.data_ptr(),
-                              with_stats ? part.data_ptr<float>() : nullptr,
+                              with_stats && !fin ? part.data_ptr<float>() : nullptr,
                               addend.has_value() ? addend->data_ptr() : nullptr, nullptr, nullptr,
                               nullptr, nullptr, (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R,
                               (int)S,
                               (int)stride, (int)pad_h, (int)pad_w, (int)Ho, (int)Wo,
                               y_out.has_value() ? map6.data() : nullptr, c16 ? 1 : 0,
-                              (int)variant, cur_stream()),
+                              (int)variant, as.acc, as.tickets,
+                              fin ? fin_t.data_ptr<double>() : nullptr, kAccSlots, cur_stream()),
             "conv_fwd_ex");
+  if (fin) return {y, fin_t};
   if (with_stats) return {y, part};
   return {y};
 }
@@ -1393,11 +1484,17 @@ class XgmiPeers {
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "arena_amd native HIP kernels (gfx950)";
   m.def("linear_fwd", &linear_fwd);
-  m.def("bn_fwd", &bn_fwd);
+  m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
+        py::arg("running_mean"), py::arg("running_var"), py::arg("training"),
+        py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("num_batches"),
+        py::arg("stats_part"), py::arg("stats_rpb"), py::arg("stats_fin") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
   m.def("conv_flip_multi", &conv_flip_multi);
   m.def("conv_phase_weights", &conv_phase_weights);
-  m.def("conv_fwd_ex", &conv_fwd_ex);
+  m.def("conv_fwd_ex", &conv_fwd_ex, py::arg("x"), py::arg("w"), py::arg("stride"),
+        py::arg("pad_h"), py::arg("pad_w"), py::arg("Ho"), py::arg("Wo"), py::arg("variant"),
+        py::arg("with_stats"), py::arg("addend"), py::arg("y_out"), py::arg("y_map"),
+        py::arg("c16"), py::arg("stats_final") = false);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);
   m.def("s2d_stem", &s2d_stem);
   m.def("stem_weight", &stem_weight);
@@ -1408,12 +1505,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("variant"), py::arg("with_stats"), py::arg("addend") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
-        py::arg("bn_mean") = py::none(), py::arg("addmask") = py::none());
+        py::arg("bn_mean") = py::none(), py::arg("addmask") = py::none(),
+        py::arg("stats_final") = false);
   m.def("conv_wgrad", &conv_wgrad);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_set_fin_max_blocks", [](int64_t p) { arena_bn_set_fin_max_blocks((int)p); });
   m.def("bn_set_nt", [](int64_t on) { arena_bn_set_nt((int)on); });
+  m.def("bn_set_acc", [](bool on) { g_bn_acc = on; });
   m.def("conv_set_wgrad_nt", [](int64_t on) { arena_conv_set_wgrad_nt((int)on); });
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
     arena_bn_set_reduce_geometry(max_blocks, min_rounds);

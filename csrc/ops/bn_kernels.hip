@@ -127,6 +127,49 @@ __device__ __forceinline__ void load8f(const float* p, float v[kVec]) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
+// ---------------------------------------------------------------------- finished statistics
+// "acc mode" (conv_kernels.hip ConvArgs::bn_acc has the same protocol): every block adds its
+// per-channel fp64 sums into acc[blockIdx % slots][2][C] with memory-side atomics and draws one
+// ticket; the last block reads the sums back with atomic swaps (leaving the slots zero for the next
+// user of the set) and finishes the per-channel results itself -- no finalize launch. The ticket
+// hand-off is the split-K slab reducer's (cdna_hip_programming.md §5).
+struct AccMode {
+  double* acc;        // [slots][2][C], zero on entry and on exit
+  unsigned* ticket;   // one counter, zero on entry and on exit
+  int slots;
+};
+
+// All threads: returns true in the last block (after the acquire), false elsewhere.
+__device__ __forceinline__ bool acc_ticket(const AccMode& am) {
+  __shared__ unsigned s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned old = __hip_atomic_fetch_add(am.ticket, 1u, __ATOMIC_RELAXED,
+                                                __HIP_MEMORY_SCOPE_AGENT);
+    s_last = old == gridDim.x - 1 ? 1u : 0u;
+    if (s_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(am.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return s_last != 0;
+}
+
+// Sum of channel c's two accumulators over the slots, swapping them back to zero.
+__device__ __forceinline__ void acc_take(const AccMode& am, int C, int c, double& s0, double& s1) {
+  s0 = s1 = 0.0;
+  for (int k = 0; k < am.slots; ++k) {
+    double* p = am.acc + (size_t)k * 2 * C + c;
+    s0 += __hip_atomic_exchange(p, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s1 += __hip_atomic_exchange(p + C, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 struct Geo {
   int cg;    // channel groups (C / 8)
   int rip;   // rows in parallel per block round
@@ -151,9 +194,11 @@ __device__ __forceinline__ void block_rows(long long M, long long rpb, long long
 
 // ------------------------------------------------------------------------------------ stats
 // part: [nblk][2][C] (block mean, block M2)
+// acc mode (am.acc != null): instead of part, finished (mean, biased var) into fin [2][C] doubles.
 template <typename T>
 __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, long long M, int C,
-                                                      long long rpb, float* __restrict__ part) {
+                                                      long long rpb, float* __restrict__ part,
+                                                      AccMode am, double* __restrict__ fin) {
   const Geo q = geo(C);
   long long r0, r1;
   block_rows(M, rpb, &r0, &r1);
@@ -205,6 +250,7 @@ __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, l
     if (q.g == 0) s_n[q.slot] = n;
   }
   __syncthreads();
+  double* acc = am.acc != nullptr ? am.acc + (size_t)(blockIdx.x % am.slots) * 2 * C : nullptr;
   for (int c = threadIdx.x; c < C; c += kT) {
     float na = s_n[0], ma = s_mean[c], sa = s_m2[c];
     for (int s = 1; s < q.rip; ++s) {
@@ -216,8 +262,23 @@ __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, l
       sa += s_m2[s * C + c] + d * d * (na * nb / nab);
       na = nab;
     }
-    part[(long long)blockIdx.x * 2 * C + c] = ma;
-    part[(long long)blockIdx.x * 2 * C + C + c] = sa;
+    if (acc != nullptr) {
+      const double nd = (double)na, mu = (double)ma;
+      unsafeAtomicAdd(acc + c, nd * mu);                        // sum x
+      unsafeAtomicAdd(acc + C + c, (double)sa + nd * mu * mu);  // sum x^2
+    } else {
+      part[(long long)blockIdx.x * 2 * C + c] = ma;
+      part[(long long)blockIdx.x * 2 * C + C + c] = sa;
+    }
+  }
+  if (acc == nullptr || !acc_ticket(am)) return;
+  const double inv_m = 1.0 / (double)M;
+  for (int c = threadIdx.x; c < C; c += kT) {
+    double s1, s2;
+    acc_take(am, C, c, s1, s2);
+    const double mean = s1 * inv_m, var = s2 * inv_m - mean * mean;
+    fin[c] = mean;
+    fin[C + c] = var > 0.0 ? var : 0.0;
   }
 }
 
@@ -358,23 +419,65 @@ __global__ __launch_bounds__(kT) void bn_stats_finalize_kernel(const float* __re
 // (V8::store_pos).
 
 // NT: non-temporal loads of x (and res) -- their last read before the backward pass
-template <typename T, bool RELU, bool RES, bool NT>
+// FIN: the batch statistics arrive finished as fp64 (mean, biased var) in `fin` [2][C] (from the
+// producing conv's epilogue or the acc-mode statistics kernel): every thread derives invstd,
+// scale and shift of its 8 channels, and block 0 writes st's outputs (mean, invstd, scale, shift
+// for the backward; running statistics; the batch counter) -- the finalize launch's work.
+template <bool FIN>
+__device__ __forceinline__ void apply_coefs(int c0, int cg, long long M, const double* fin,
+                                            const ArenaBNStats& st, float mu[kVec],
+                                            float sc[kVec], float sh[kVec]) {
+  if constexpr (!FIN) {
+    load8f(st.mean + c0, mu);
+    load8f(st.scale + c0, sc);
+    load8f(st.shift + c0, sh);
+  } else {
+    const int C = cg * kVec;
+    float inv[kVec];
+    double var[kVec];
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      const double m = fin[c0 + i];
+      var[i] = fin[C + c0 + i];
+      mu[i] = (float)m;
+      inv[i] = (float)(1.0 / sqrt(var[i] + (double)st.eps));
+      sc[i] = (st.gamma ? st.gamma[c0 + i] : 1.f) * inv[i];
+      sh[i] = st.beta ? st.beta[c0 + i] : 0.f;
+    }
+    if (blockIdx.x == 0 && (int)threadIdx.x < cg) {
+      const float mom = st.momentum;
+      const double unb = M > 1 ? (double)M / (double)(M - 1) : 1.0;
+#pragma unroll
+      for (int i = 0; i < kVec; ++i) {
+        st.mean[c0 + i] = mu[i];
+        st.invstd[c0 + i] = inv[i];
+        st.scale[c0 + i] = sc[i];
+        st.shift[c0 + i] = sh[i];
+        if (st.running_mean) {
+          st.running_mean[c0 + i] = (1.f - mom) * st.running_mean[c0 + i] + mom * mu[i];
+          st.running_var[c0 + i] = (1.f - mom) * st.running_var[c0 + i] +
+                                   mom * (float)(var[i] * unb);
+        }
+      }
+      if (threadIdx.x == 0 && st.batches != nullptr) *st.batches += 1;
+    }
+  }
+}
+
+template <typename T, bool RELU, bool RES, bool NT, bool FIN>
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
                                                       const T* __restrict__ res,
                                                       T* __restrict__ y,
                                                       uint8_t* __restrict__ mask,
-                                                      const float* __restrict__ mean,
-                                                      const float* __restrict__ scale,
-                                                      const float* __restrict__ shift,
-                                                      long long nvec, int cg) {
+                                                      ArenaBNStats st,
+                                                      const double* __restrict__ fin,
+                                                      long long M, long long nvec, int cg) {
   const long long stride = (long long)gridDim.x * kT;
   // every vector this thread touches has the same channel group: the grid stride is a multiple
   // of kT, and cg divides kT (host-checked), so the per-channel coefficients load once
   const int c0 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1)) * kVec;
   float mu[kVec], sc[kVec], sh[kVec];
-  load8f(mean + c0, mu);
-  load8f(scale + c0, sc);
-  load8f(shift + c0, sh);
+  apply_coefs<FIN>(c0, cg, M, fin, st, mu, sc, sh);
   for (long long v0 = (long long)blockIdx.x * kT + threadIdx.x; v0 < nvec; v0 += 2 * stride) {
     float a[2][kVec], b[2][kVec];
     bool ok[2];
@@ -413,13 +516,28 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
 
 // ---------------------------------------------------------------------------- backward sums
 // g = RELU ? dy * mask : dy;  per channel: sum g, sum g * (x - mean).  part: [nblk][2][C]
+// bn_bwd_finish: the backward finalize of channel c from its sums (sum g, sum g (x - mean)).
+__device__ __forceinline__ void bn_bwd_finish(const ArenaBNBwd& out, int c, double a, double b,
+                                              long long M) {
+  const float invstd = out.invstd[c];
+  const float gam = out.gamma ? out.gamma[c] : 1.f;
+  if (out.dgamma) out.dgamma[c] = (float)(b * invstd);
+  if (out.dbeta) out.dbeta[c] = (float)a;
+  // dx = gamma*invstd * (g - sum_g/M - (x - mean) * invstd^2 * sum_gx/M)
+  out.ca[c] = gam * invstd;
+  out.cb[c] = (float)(a / (double)M);
+  out.cc[c] = (float)(b / (double)M) * invstd * invstd;
+}
+
+// acc mode (am.acc != null): the block sums go to fp64 accumulators and the last block writes the
+// finished coefficients (no finalize launch); else the per-block partials go to part.
 template <typename T, bool RELU>
 __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__ dy,
                                                            const uint8_t* __restrict__ mask,
                                                            const T* __restrict__ x, long long M,
                                                            int C, long long rpb,
                                                            float* __restrict__ part,
-                                                           ArenaBNBwd out) {
+                                                           ArenaBNBwd out, AccMode am) {
   const Geo q = geo(C);
   long long r0, r1;
   block_rows(M, rpb, &r0, &r1);
@@ -474,14 +592,26 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
     }
   }
   __syncthreads();
+  double* acc = am.acc != nullptr ? am.acc + (size_t)(blockIdx.x % am.slots) * 2 * C : nullptr;
   for (int c = threadIdx.x; c < C; c += kT) {
     float a = 0.f, b = 0.f;
     for (int s = 0; s < q.rip; ++s) {
       a += s_g[s * C + c];
       b += s_gx[s * C + c];
     }
-    part[(long long)blockIdx.x * 2 * C + c] = a;
-    part[(long long)blockIdx.x * 2 * C + C + c] = b;
+    if (acc != nullptr) {
+      unsafeAtomicAdd(acc + c, (double)a);
+      unsafeAtomicAdd(acc + C + c, (double)b);
+    } else {
+      part[(long long)blockIdx.x * 2 * C + c] = a;
+      part[(long long)blockIdx.x * 2 * C + C + c] = b;
+    }
+  }
+  if (acc == nullptr || !acc_ticket(am)) return;
+  for (int c = threadIdx.x; c < C; c += kT) {
+    double a, b;
+    acc_take(am, C, c, a, b);
+    bn_bwd_finish(out, c, a, b, M);
   }
 }
 
@@ -512,14 +642,7 @@ __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const float* __rest
   if (!fin_block_sum(a, b, unused)) return;
   if (gridDim.y > 1 && !fin_level2(a, b, unused, lvl2, tickets)) return;
   if (c >= C) return;
-  const float invstd = out.invstd[c];
-  const float gam = out.gamma ? out.gamma[c] : 1.f;
-  if (out.dgamma) out.dgamma[c] = (float)(b * invstd);
-  if (out.dbeta) out.dbeta[c] = (float)a;
-  // dx = gamma*invstd * (g - sum_g/M - (x - mean) * invstd^2 * sum_gx/M)
-  out.ca[c] = gam * invstd;
-  out.cb[c] = (float)(a / (double)M);
-  out.cc[c] = (float)(b / (double)M) * invstd * invstd;
+  bn_bwd_finish(out, c, a, b, M);
 }
 
 // --------------------------------------------------------------------------------- backward dx
@@ -612,35 +735,58 @@ long long arena_bn_workspace_floats(long long M, int C) {
 // ext_nblk > 0: `part` already holds the statistics partials of x ([ext_nblk][2][C], ext_rpb rows
 // each), written by the producing convolution's epilogue (conv_kernels.hip): no statistics pass.
 // mask (optional, relu only): [M * C / 8] bytes, bit i of byte v = (y[v * 8 + i] > 0)
+// fin (training): fp64 [2][C] batch (mean, biased var). fin_ready: already finished by the
+// producing convolution (no statistics pass); else with acc != null the statistics kernel runs in
+// acc mode and fills fin (no finalize launch), and the apply kernel finishes the coefficients.
 hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint8_t* mask,
                         long long M, int C, int relu, int training, float* part, int ext_nblk,
                         long long ext_rpb,
-                        double* lvl2, unsigned* tickets, ArenaBNStats st, hipStream_t stream) {
+                        double* lvl2, unsigned* tickets, ArenaBNStats st, double* fin,
+                        int fin_ready, double* acc, unsigned* acc_ticket_ptr, int acc_slots,
+                        hipStream_t stream) {
   if (bad_shape(M, C)) return hipErrorInvalidValue;
   const int groups = (C + 63) / 64;
-  if (training && ext_nblk > 0) {
+  bool use_fin = false;
+  if (training && fin != nullptr && fin_ready) {
+    use_fin = true;
+  } else if (training && fin != nullptr && acc != nullptr && ext_nblk <= 0) {
+    long long rpb;
+    const long long nb = reduce_blocks(M, C, &rpb);
+    const AccMode am{acc, acc_ticket_ptr, acc_slots};
+    if (dtype == 1)
+      hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb), dim3(kT), 0, stream,
+                         static_cast<const uint16_t*>(x), M, C, rpb, nullptr, am, fin);
+    else
+      hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kT), 0, stream,
+                         static_cast<const float*>(x), M, C, rpb, nullptr, am, fin);
+    use_fin = true;
+  } else if (training && ext_nblk > 0) {
     if (ext_rpb <= 0 || (long long)ext_nblk * ext_rpb < M) return hipErrorInvalidValue;
     hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups, fin_blocks_per_group(ext_nblk)),
                        dim3(kT), 0, stream, part, ext_nblk, M, C, ext_rpb, lvl2, tickets, st);
   } else if (training) {
     long long rpb;
     const long long nb = reduce_blocks(M, C, &rpb);
+    const AccMode none{nullptr, nullptr, 0};
     if (dtype == 1)
       hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb), dim3(kT), 0, stream,
-                         static_cast<const uint16_t*>(x), M, C, rpb, part);
+                         static_cast<const uint16_t*>(x), M, C, rpb, part, none, nullptr);
     else
       hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kT), 0, stream,
-                         static_cast<const float*>(x), M, C, rpb, part);
+                         static_cast<const float*>(x), M, C, rpb, part, none, nullptr);
     hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups, fin_blocks_per_group((int)nb)),
                        dim3(kT), 0, stream, part, (int)nb, M, C, rpb, lvl2, tickets, st);
   }
   const long long nvec = M * (C / kVec);
   const int nb = elementwise_blocks(nvec);
   const int cg = C / kVec;
-#define ARENA_BN_APPLY_NT(TT, R, S, NT)                                                      \
-  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S, NT>), dim3(nb), dim3(kT), 0, stream,       \
+#define ARENA_BN_APPLY_K(TT, R, S, NT, F)                                                    \
+  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S, NT, F>), dim3(nb), dim3(kT), 0, stream,    \
                      static_cast<const TT*>(x), static_cast<const TT*>(res), static_cast<TT*>(y), \
-                     mask, st.mean, st.scale, st.shift, nvec, cg)
+                     mask, st, fin, M, nvec, cg)
+#define ARENA_BN_APPLY_NT(TT, R, S, NT) \
+  do { if (use_fin) ARENA_BN_APPLY_K(TT, R, S, NT, true); \
+       else ARENA_BN_APPLY_K(TT, R, S, NT, false); } while (0)
 #define ARENA_BN_APPLY(TT, R, S) \
   do { if (g_bn_nt) ARENA_BN_APPLY_NT(TT, R, S, true); else ARENA_BN_APPLY_NT(TT, R, S, false); } \
   while (0)
@@ -658,25 +804,31 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
   }
 #undef ARENA_BN_APPLY
 #undef ARENA_BN_APPLY_NT
+#undef ARENA_BN_APPLY_K
   return hipGetLastError();
 }
 
 // ext_nblk > 0: `part` already holds the backward partials of (dy, x) ([ext_nblk][2][C]), written
 // by the epilogue of the backward-data convolution that produced dy (conv_kernels.hip, EPI 2):
 // no reduction pass.
+// acc != null (and no external partials): the reduction runs in acc mode and its last block
+// writes the coefficients -- no finalize launch.
 hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const void* x, void* dx,
                         void* dres, long long M, int C, int relu, float* part, int ext_nblk,
-                        double* lvl2, unsigned* tickets, ArenaBNBwd co, hipStream_t stream) {
+                        double* lvl2, unsigned* tickets, ArenaBNBwd co, double* acc,
+                        unsigned* acc_ticket_ptr, int acc_slots, hipStream_t stream) {
   if (bad_shape(M, C) || (relu && mask == nullptr)) return hipErrorInvalidValue;
   long long rpb;
   long long nb = reduce_blocks(M, C, &rpb);
+  const bool acc_mode = acc != nullptr && ext_nblk <= 0;
+  const AccMode am{acc_mode ? acc : nullptr, acc_ticket_ptr, acc_slots};
   if (ext_nblk > 0) {
     nb = ext_nblk;
   } else {
 #define ARENA_BN_RED(TT, R)                                                                  \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, R>), dim3(nb), dim3(kT), 0, stream,         \
                      static_cast<const TT*>(dy), mask, static_cast<const TT*>(x), M, C, rpb, \
-                     part, co)
+                     part, co, am)
     if (dtype == 1) {
       if (relu) ARENA_BN_RED(uint16_t, true); else ARENA_BN_RED(uint16_t, false);
     } else {
@@ -684,8 +836,9 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
     }
 #undef ARENA_BN_RED
   }
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64, fin_blocks_per_group((int)nb)),
-                     dim3(kT), 0, stream, part, (int)nb, M, C, lvl2, tickets, co);
+  if (!acc_mode)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64, fin_blocks_per_group((int)nb)),
+                       dim3(kT), 0, stream, part, (int)nb, M, C, lvl2, tickets, co);
   const long long nvec = M * (C / kVec);
   long long ne = (nvec + kT - 1) / kT;
   ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);

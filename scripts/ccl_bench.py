@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Collective microbenchmark: xGMI one-kernel allreduce / fused Adam vs RCCL.
+"""Collective microbenchmark: xGMI one-kernel allreduce / fused Adam / broadcast (direct pull and
+scatter + all-gather) / all-gather / sharded bf16 SGD vs RCCL.
 
     # 8x MI355X node: one rank per GPU, RCCL process group
     python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 scripts/ccl_bench.py
@@ -8,7 +9,8 @@
     python scripts/ccl_bench.py --same-gpu 2
 
 Prints one JSON line per (op, size) from rank 0: time per call (graph-replayed, 50 calls per
-graph) and algorithm / bus bandwidth (busbw = 2 (W-1)/W * bytes / t, the ring-equivalent figure).
+graph) and algorithm / bus bandwidth. busbw uses the ring-equivalent factor of each op: allreduce
+2 (W-1)/W, broadcast 1, all-gather (W-1)/W (of the gathered bytes).
 """
 from __future__ import annotations
 
@@ -90,6 +92,38 @@ def bench(rank: int, world: int, sizes, rccl: bool,
         if rccl:
             t = timed(lambda: dist.all_reduce(x))
             rows.append(("rccl_allreduce", nbytes, t))
+    # broadcast (both algorithms forced, then the default switch) and all-gather
+    for nbytes in sizes:
+        n = nbytes // 4
+        x = torch.randn(n, device="cuda")
+        for kind, cap in (("direct", 1 << 40), ("scatter_allgather", 0)):
+            comm.ext.ccl_set_bcast_direct_max(cap)
+            t = timed(lambda: comm.broadcast_(x, 0))
+            rows.append((f"xgmi_broadcast({kind})", nbytes, t))
+        comm.ext.ccl_set_bcast_direct_max(128 << 10)
+        if rccl:
+            t = timed(lambda: dist.broadcast(x, 0))
+            rows.append(("rccl_broadcast", nbytes, t))
+        m = max(4, n // world // 4 * 4)
+        shard = x[:m]
+        if m <= comm.staging_elems:
+            t = timed(lambda: comm.all_gather(shard))
+            rows.append(("xgmi_allgather", m * 4 * world, t))
+            if rccl:
+                out = torch.empty(m * world, device="cuda")
+                t = timed(lambda: dist.all_gather_into_tensor(out, shard))
+                rows.append(("rccl_allgather", m * 4 * world, t))
+    # the sharded bf16 SGD step of data-parallel ResNet-50 (25.5 M bf16 weights in 32 MB buckets)
+    from arena_amd.parallel.xgmi import XgmiComm as _C
+    nw = 25_557_032 // 8 * 8
+    zc = _C(staging_elems=nw // 2, param_elems=nw // 2, timeout_s=30.0)
+    master = torch.zeros(nw, device="cuda")
+    mom = torch.zeros(nw, device="cuda")
+    bucket = 16 << 20
+    t = timed(lambda: [zc.peers.sgd_bf16(master, mom, o, min(bucket, nw - o), 0.1, 0.9, 4e-5,
+                                         1.0 / world) for o in range(0, nw, bucket)], iters=10)
+    rows.append(("xgmi_sharded_sgd_bf16(resnet50, 32MB buckets)", nw * 2, t))
+    zc.close()
     # the DP trainer's fused step collective on the MNIST MLP's flat parameter vector, swept over
     # the per-block chunk size (fewer, fatter blocks = fewer barrier fences)
     n = 397520
@@ -108,9 +142,11 @@ def bench(rank: int, world: int, sizes, rccl: bool,
     if rank == 0:
         for op, nb, t in rows:
             algbw = nb / t / 1e9
+            f = 1.0 if "broadcast" in op else ((world - 1) / world if "allgather" in op
+                                               else 2 * (world - 1) / world)
             print(json.dumps({"op": op, "bytes": nb, "world": world, "us": round(t * 1e6, 2),
                               "algbw_GBs": round(algbw, 2),
-                              "busbw_GBs": round(algbw * 2 * (world - 1) / world, 2)}), flush=True)
+                              "busbw_GBs": round(algbw * f, 2)}), flush=True)
     comm.close()
 
 

@@ -144,3 +144,77 @@ def test_cnn_bench_example_runs_with_graph_capture(tmp_path):
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["exec"] == "hipgraph" and res["images_per_s"] > 0
     assert (tmp_path / "hb").exists()          # progress heartbeats were written
+
+
+@pytest.mark.parametrize("shape", [(4, 128, 14, 14), (2, 256, 7, 7), (8, 64, 28, 28)])
+def test_conv_finished_stats_feed_bn(shape):
+    """Finished statistics from the conv epilogue (fp64 atomics + last-tile ticket) give the same
+    BN forward/backward and running statistics as the fp32 reference, and leave the accumulator
+    set zeroed: many back-to-back layers reuse the pool without a memset."""
+    from arena_amd.ops import conv
+    from arena_amd.ops.batchnorm import BatchNormAct2d, FinishedStats
+    torch.manual_seed(1)
+    N, C, H, W = shape
+    x = _nhwc(torch.randn(N, 64, H, W, device="cuda").to(torch.bfloat16))
+    w = _nhwc((torch.randn(C, 64, 3, 3, device="cuda") * 0.05).to(torch.bfloat16))
+    for rep in range(130):   # more uses than the pool has sets (128)
+        y, st = conv.conv2d_fwd(x, w, 1, 1, with_stats=True, final=True)
+        assert isinstance(st, FinishedStats) and st.fin.dtype == torch.float64
+        yf = y.float()
+        mean = yf.mean(dim=(0, 2, 3))
+        var = yf.var(dim=(0, 2, 3), unbiased=False)
+        assert torch.allclose(st.fin[0].float(), mean, rtol=1e-5, atol=1e-5)
+        assert torch.allclose(st.fin[1].float(), var, rtol=1e-4, atol=1e-6)
+    m = BatchNormAct2d(C).cuda()
+    ref = torch.nn.BatchNorm2d(C).cuda()
+    ref.load_state_dict(m.state_dict())
+    y.requires_grad_()
+    yr = y.detach().float().requires_grad_()
+    out = m(y, stats=st)
+    outr = F.relu(ref(yr))
+    assert (out.float() - outr).abs().max() < 3e-2
+    assert torch.allclose(m.running_mean, ref.running_mean, rtol=1e-4, atol=1e-5)
+    assert torch.allclose(m.running_var, ref.running_var, rtol=1e-4, atol=1e-5)
+    assert int(m.num_batches_tracked) == 1
+    g = torch.randn_like(outr)
+    out.backward(g.to(out.dtype))
+    outr.backward(g)
+    assert (y.grad.float() - yr.grad).abs().max() / yr.grad.abs().max() < 3e-2
+    assert torch.allclose(m.weight.grad, ref.weight.grad, rtol=2e-2, atol=1e-2)
+    assert torch.allclose(m.bias.grad, ref.bias.grad, rtol=2e-2, atol=1e-2)
+
+
+def test_resnet_step_finished_stats_match_partials():
+    """A ResNet training step with the finished-statistics path (default) against the per-tile
+    partials + finalize path: same loss, gradients and running statistics to rounding, and a
+    captured hipGraph replays it consistently."""
+    from arena_amd.models import resnet as R
+    from arena_amd.ops import conv
+    torch.manual_seed(0)
+    out = {}
+    try:
+        for final in (False, True):
+            conv.set_bn_final(final)
+            torch.manual_seed(0)
+            net = R.resnet("resnet_tiny", num_classes=10, width=64).cuda().to(
+                memory_format=torch.channels_last)
+            x = _nhwc(torch.randn(8, 3, 64, 64, device="cuda"))
+            y = torch.randint(0, 10, (8,), device="cuda")
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                loss = F.cross_entropy(net(x), y)
+            loss.backward()
+            out[final] = (float(loss), {n: p.grad.float().clone() for n, p in net.named_parameters()},
+                          {n: b.clone() for n, b in net.named_buffers()})
+    finally:
+        conv.set_bn_final(True)
+    la, ga, ba = out[False]
+    lb, gb, bb = out[True]
+    assert abs(la - lb) < 1e-3 * max(1.0, abs(la))
+    for n in ga:
+        d = float((ga[n] - gb[n]).abs().max())
+        assert d <= 2e-2 * max(1e-3, float(ga[n].abs().max())), (n, d)
+    for n in ba:
+        if ba[n].dtype.is_floating_point:
+            assert torch.allclose(ba[n], bb[n], rtol=1e-3, atol=1e-4), n
+        else:
+            assert torch.equal(ba[n], bb[n]), n
