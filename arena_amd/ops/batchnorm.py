@@ -7,11 +7,11 @@ it runs the HIP kernels in ``csrc/ops/bn_kernels.hip``:
 
 * forward: 2 launches (statistics, then apply + ReLU mask bits); the statistics come finished
   from the producing convolution's epilogue when it ran on the MFMA kernel (then 1 launch).
-  The statistics pass and the conv epilogue accumulate fp64 sums with memory-side atomics and
-  their last block finishes them, and the apply kernel derives its coefficients: no finalize
-  launch (one per layer and direction before, ~10 us each);
-* backward: 2 launches (reductions, whose last block writes the dx coefficients, then dx and the
-  residual gradient).
+  The statistics pass and the conv epilogue accumulate fp64 sums with fire-and-forget
+  memory-side atomics; a one-thread-per-channel finalize turns them into the coefficients
+  (instead of a two-level merge of up to 3136 per-tile partials per channel);
+* backward: 2 launches (reductions, then dx and the residual gradient) plus the same small
+  finalize.
 
 Otherwise it runs the same math as stock PyTorch ops. That includes CPU tensors, which serve as
 the reference.
@@ -56,14 +56,19 @@ def reference(x, residual, weight, bias, running_mean, running_var, training, mo
 
 
 class FinishedStats:
-    """Batch statistics of a conv output finished inside the conv kernel (fp64 [2, C]: mean,
-    biased variance; ``conv2d_fwd(..., with_stats=True, final=True)``): the BN layer consuming it
-    runs only its apply kernel, which derives invstd/scale/shift and updates the running
-    statistics itself."""
+    """Batch statistics of a conv output accumulated inside the conv kernel: the fp64 [2, C]
+    accumulator set (sum y, sum y^2) its epilogue added into with memory-side atomics
+    (``conv2d_fwd(..., with_stats=True, final=True)``). The BN layer consuming it skips its
+    statistics pass; its one-thread-per-channel finalize reads the sums and zeroes the set, which
+    returns to a rotating pool. Statistics obtained this way must reach a BN layer, or be
+    ``discard()``ed (zeroed), before the pool comes round again."""
     __slots__ = ("fin",)
 
     def __init__(self, fin: torch.Tensor):
         self.fin = fin
+
+    def discard(self) -> None:
+        self.fin.zero_()
 
 
 class ResidualMask:

@@ -137,6 +137,20 @@ def set_bn_links(on: bool) -> None:
 # of per-tile partials plus a finalize launch in the BN layer (on by default; ARENA_BN_FINAL=0 for
 # A/Bs). Also switches the BN kernels' own statistics/backward reductions to the same acc mode.
 _BN_FINAL = os.environ.get("ARENA_BN_FINAL", "1") == "1"
+# Above this many (tile, channel) pairs the epilogue's atomics (16 B each, at the ~1.3 TB/s
+# memory-side atomic rate, competing with the tile's output stores) cost more than the partial
+# merge they replace: the 56x56 and 28x28 ResNet-50 layers (3136 / 784 tiles) keep the partials,
+# the 14x14 and 7x7 ones take the accumulators (profiles/r3_bn_acc_ab.jsonl).
+_ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_ACC_MAX_PAIRS", str(64 << 10)))
+
+
+def _use_acc(m: int, bm: int, cout: int) -> bool:
+    return _BN_FINAL and -(-m // bm) * cout <= _ACC_MAX_PAIRS
+
+
+def _out_pixels(x: Tensor, w: Tensor, stride: int, pad: int) -> int:
+    ho, wo = out_hw(x.shape[2], x.shape[3], w.shape[2], w.shape[3], stride, pad)
+    return x.shape[0] * ho * wo
 
 
 def set_bn_final(on: bool) -> None:
@@ -147,10 +161,11 @@ def set_bn_final(on: bool) -> None:
 
 
 def _stats_out(want: bool, part: Tensor, rpb: int):
-    """What ``forward_stats`` hands the BN layer: finished statistics (fp64) or partials."""
+    """What ``forward_stats`` hands the BN layer: finished statistics ([2, C]: mean, variance)
+    or the flat per-tile partials."""
     if not want:
         return None
-    if part.dtype == torch.float64:
+    if part.dim() == 2:
         from .batchnorm import FinishedStats
         return FinishedStats(part)
     return (part, rpb)
@@ -254,9 +269,10 @@ class _StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, w16, want_stats, fwd_variant, wgrad_cfg):
         Ho, Wo = z.shape[2], z.shape[3]
+        fin = bool(want_stats and _use_acc(z.shape[0] * Ho * Wo, TILES[fwd_variant][0],
+                                            w16.shape[0]))
         out = _ext.load().conv_fwd_ex(z, w16, 1, 2, 2, Ho, Wo, int(fwd_variant), bool(want_stats),
-                                      None, None, [], True, stats_final=bool(want_stats and
-                                                                            _BN_FINAL))
+                                      None, None, [], True, stats_final=fin)
         ctx.save_for_backward(z)
         ctx.wgrad_cfg = wgrad_cfg
         ctx.set_materialize_grads(False)
@@ -716,7 +732,8 @@ class _ConvFn(torch.autograd.Function):
         part = x.new_empty(0, dtype=torch.float32)
         if plan.fwd == MIOPEN:
             y = F.conv2d(x, w, stride=stride, padding=pad)
-        elif want_stats and _BN_FINAL:
+        elif want_stats and _use_acc(_out_pixels(x, w, stride, pad), TILES[plan.fwd][0],
+                                     w.shape[0]):
             y, st = conv2d_fwd(x, w, stride, pad, plan.fwd, with_stats=True, final=True)
             part = st.fin
         elif want_stats:
@@ -838,7 +855,7 @@ class Conv2dNHWC(nn.Conv2d):
         want = want_stats and plan.fwd != MIOPEN and torch.is_grad_enabled() and self.training
         with torch.autocast("cuda", enabled=False):
             y, part = _ConvFn.apply(x, w, s, p, plan, want, join, bn_link)
-        return y, _stats_out(want, part, TILES[plan.fwd][0])
+        return y, _stats_out(want, part, TILES[plan.fwd][0] if want else 0)
 
 
 class StemConv2d(Conv2dNHWC):
@@ -873,7 +890,7 @@ class StemConv2d(Conv2dNHWC):
             w16 = _StemWeightFn.apply(w) if fuse else stem_weight(w.to(torch.bfloat16))
             fv, wcfg = _stem_plan(z, w16)
             y, part = _StemFn.apply(z, w16, want, fv, wcfg)
-        return y, _stats_out(want, part, TILES[fv][0])
+        return y, _stats_out(want, part, TILES[fv][0] if want else 0)
 
 
 _STEM_PLANS: Dict[tuple, Tuple[int, Tuple[int, int]]] = {}

@@ -65,7 +65,7 @@ hipError_t arena_conv_flip_multi(int, const void* const*, void* const*, const in
 hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void*, const uint8_t*,
                              const void*, const uint8_t*, const float*, int, int, int, int, int,
                              int, int, int, int, int, int, int, const int*, int, int, double*,
-                             unsigned*, double*, int, hipStream_t);
+                             hipStream_t);
 hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
                                int, int, int, int, int, int, int, int, int, int, int, float,
                                hipStream_t);
@@ -93,10 +93,9 @@ hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, 
                              int, hipStream_t);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, uint8_t*, long long, int, int, int,
                         float*, int, long long, double*, unsigned*, ArenaBNStats, double*, int,
-                        double*, unsigned*, int, hipStream_t);
-hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, void*, long long, int,
-                        int, float*, int, double*, unsigned*, ArenaBNBwd, double*, unsigned*, int,
                         hipStream_t);
+hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, void*, long long, int,
+                        int, float*, int, double*, unsigned*, ArenaBNBwd, double*, hipStream_t);
 #ifdef ARENA_TIMELINE
 hipError_t arena_timeline_read(long long*, int);
 #endif
@@ -719,38 +718,32 @@ unsigned* bn_tickets(const Tensor& like) {
   return reinterpret_cast<unsigned*>(pools[dev].data_ptr<int32_t>()) + set * kTicketsPerSet;
 }
 
-// Finished-statistics accumulators (conv_kernels.hip ConvArgs::bn_acc, bn_kernels.hip acc mode):
-// a rotating pool of zeroed sets, each [kAccSlots][2][2048] doubles + 32 tickets. Every kernel
-// that uses a set leaves it zeroed, so sets are reused without a memset (and graph replays stay
-// valid); consecutive users of one set are ordered by the stream.
-constexpr int kAccSets = 128, kAccSlots = 4, kAccC = 2048, kAccTickets = 32;
-struct AccSet {
-  double* acc;
-  unsigned* tickets;
-};
-AccSet bn_acc_set(const Tensor& like) {
-  static std::vector<Tensor> accs, tks;
+// Statistics accumulators of acc mode (conv_kernels.hip ConvArgs::bn_acc, bn_kernels.hip): a
+// rotating pool of zeroed fp64 [2][C] sets. The finalize kernel that consumes a set zeroes it
+// again, so sets are reused without a memset (and graph replays stay valid); one set is only in
+// use between a producer (conv epilogue / statistics pass / backward reduction) and its finalize,
+// which follow each other on the stream.
+constexpr int kAccSets = 128, kAccC = 2048;
+Tensor bn_acc_set(const Tensor& like, int64_t C) {
+  static std::vector<Tensor> pools;
   static std::vector<unsigned> next;
+  TORCH_CHECK(C > 0 && C <= kAccC, "BatchNorm acc mode: C must be <= ", kAccC);
   const int dev = like.get_device();
-  if ((int)accs.size() <= dev) {
-    accs.resize(dev + 1);
-    tks.resize(dev + 1);
+  if ((int)pools.size() <= dev) {
+    pools.resize(dev + 1);
     next.resize(dev + 1, 0);
   }
-  if (!accs[dev].defined()) {
+  if (!pools[dev].defined()) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     check_hip(hipStreamIsCapturing(cur_stream(), &cs), "bn_acc_set");
     TORCH_CHECK(cs == hipStreamCaptureStatusNone,
                 "arena BatchNorm: run one eager step before capturing a graph (its statistics "
                 "accumulators are allocated and zeroed on first use)");
-    accs[dev] = torch::zeros({(int64_t)kAccSets * kAccSlots * 2 * kAccC},
-                             like.options().dtype(torch::kFloat64));
-    tks[dev] = torch::zeros({kAccSets * kAccTickets}, like.options().dtype(torch::kInt32));
+    pools[dev] = torch::zeros({kAccSets, 2 * kAccC}, like.options().dtype(torch::kFloat64));
     check_hip(hipStreamSynchronize(cur_stream()), "bn_acc_set zero");
   }
-  const unsigned set = next[dev]++ % kAccSets;
-  return {accs[dev].data_ptr<double>() + (size_t)set * kAccSlots * 2 * kAccC,
-          reinterpret_cast<unsigned*>(tks[dev].data_ptr<int32_t>()) + set * kAccTickets};
+  const int64_t set = next[dev]++ % kAccSets;
+  return pools[dev][set].narrow(0, 0, 2 * C).view({2, C});
 }
 
 // finished statistics / acc-mode reductions in the BN kernels (runtime switch for A/Bs)
@@ -766,8 +759,8 @@ Tensor bn_lvl2(int64_t nblk, int64_t C, const Tensor& like) {
 // Returns (y, mean, invstd, mask). Eval mode normalises with the running statistics. mask (relu
 // in training, else empty): uint8 [M * C / 8], bit i of byte v = (y.flat[8 v + i] > 0).
 // stats_part/stats_rpb: BatchNorm partials of x from conv_fwd(with_stats=True) (training only).
-// stats_fin (training): finished fp64 [2][C] (mean, biased variance) from conv_fwd(...,
-// stats_final=True): no statistics pass and no finalize launch.
+// stats_fin (training): the fp64 [2][C] accumulators conv_fwd(..., stats_final=True) filled: no
+// statistics pass, a one-thread-per-channel finalize instead of the partial merge.
 std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT running_mean,
                            OptT running_var, bool training, double momentum, double eps,
                            bool relu, OptT num_batches, OptT stats_part, int64_t stats_rpb,
@@ -812,7 +805,8 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
       TORCH_CHECK(stats_part->numel() == nblk * 2 * g.C, "stats_part has ", stats_part->numel(),
                   " floats, expected ", nblk * 2 * g.C);
       part = *stats_part;
-    } else if (!g_bn_acc) {
+    } else {
+      // (acc mode may still fall back to partials for layers with many blocks x channels)
       part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
     }
   } else {
@@ -830,17 +824,14 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
                                    : Tensor();
   const int ext_nblk = training && stats_part.has_value()
                            ? (int)((g.M + stats_rpb - 1) / stats_rpb) : 0;
-  Tensor lvl2, fin;
+  Tensor lvl2, acc;
   unsigned* tickets = nullptr;
-  AccSet as{nullptr, nullptr};
-  int fin_ready = 0;
+  int acc_ready = 0;
   if (training && stats_fin.has_value()) {
-    fin = *stats_fin;
-    fin_ready = 1;
-  } else if (training && !stats_part.has_value() && g_bn_acc) {
-    fin = torch::empty({2, g.C}, x.options().dtype(torch::kFloat64));
-    as = bn_acc_set(x);
+    acc = *stats_fin;
+    acc_ready = 1;
   } else if (training) {
+    if (!stats_part.has_value() && g_bn_acc) acc = bn_acc_set(x, g.C);
     const int64_t nblk = ext_nblk > 0 ? ext_nblk : part.numel() / (2 * g.C);
     lvl2 = bn_lvl2(nblk, g.C, x);
     tickets = bn_tickets(x);
@@ -850,8 +841,8 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
                          g.C, relu ? 1 : 0, training ? 1 : 0,
                          part.defined() ? part.data_ptr<float>() : nullptr, ext_nblk,
                          (long long)stats_rpb, lvl2.defined() ? lvl2.data_ptr<double>() : nullptr,
-                         tickets, st, fin.defined() ? fin.data_ptr<double>() : nullptr, fin_ready,
-                         as.acc, as.tickets, kAccSlots, cur_stream()),
+                         tickets, st, acc.defined() ? acc.data_ptr<double>() : nullptr, acc_ready,
+                         cur_stream()),
             "bn_fwd");
   return {y, mean, invstd, mask};
 }
@@ -898,26 +889,24 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
                 " floats, expected ", nblk * 2 * g.C);
     part = *ext_part;
     ext_nblk = (int)nblk;
-  } else if (!g_bn_acc) {
+  } else {
     part = torch::empty({arena_bn_workspace_floats(g.M, g.C)}, f32);
   }
-  AccSet as{nullptr, nullptr};
-  Tensor lvl2;
+  Tensor lvl2, acc;
   unsigned* tickets = nullptr;
-  if (part.defined()) {
-    lvl2 = bn_lvl2(part.numel() / (2 * g.C), g.C, x);
-    tickets = bn_tickets(x);
-  } else {
-    as = bn_acc_set(x);   // acc mode: the reduction's last block writes the coefficients
-  }
+  lvl2 = bn_lvl2(part.numel() / (2 * g.C), g.C, x);
+  tickets = bn_tickets(x);
+  // acc mode: atomics in the reduction + per-channel finalize (the kernel side keeps the
+  // partials for layers with many blocks x channels)
+  if (!ext_part.has_value() && g_bn_acc) acc = bn_acc_set(x, g.C);
   Tensor dx = torch::empty_like(x);
   Tensor dres = with_res ? torch::empty_like(x) : Tensor();
   check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(),
                          relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(), dx.data_ptr(),
                          with_res ? dres.data_ptr() : nullptr, g.M, g.C, relu ? 1 : 0,
                          part.defined() ? part.data_ptr<float>() : nullptr, ext_nblk,
-                         lvl2.defined() ? lvl2.data_ptr<double>() : nullptr, tickets, b, as.acc,
-                         as.tickets, kAccSlots, cur_stream()),
+                         lvl2.defined() ? lvl2.data_ptr<double>() : nullptr, tickets, b,
+                         acc.defined() ? acc.data_ptr<double>() : nullptr, cur_stream()),
             "bn_bwd");
   return {dx, dres, dgamma, dbeta};
 }
@@ -942,8 +931,8 @@ void pool_check(const Tensor& t, const char* name) {
 // bn_x/bn_mask/bn_mean (optional, backward-data use): y is the gradient of a BatchNorm layer's
 // output; with with_stats the returned partials are that BN's backward partials (g = y * mask,
 // sum g, sum g * (bn_x - bn_mean)) for bn_bwd(..., ext_part, BM) instead of forward statistics.
-// stats_final (with with_stats, forward statistics only): the second output is the finished
-// batch statistics [2][Cout] fp64 (mean, biased variance) for bn_fwd(stats_fin=...) instead of
+// stats_final (with with_stats, forward statistics only): the second output is the fp64 [2][Cout]
+// accumulator set (sum y, sum y^2) the epilogue added into, for bn_fwd(stats_fin=...), instead of
 // the per-tile partials.
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant,
                              bool with_stats, OptT addend, OptT bn_x, OptT bn_mask,
@@ -976,9 +965,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
   Tensor part = with_stats && !fin
                     ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
                     : Tensor();
-  Tensor fin_t = fin ? torch::empty({2, Cout}, x.options().dtype(torch::kFloat64)) : Tensor();
-  AccSet as{nullptr, nullptr};
-  if (fin) as = bn_acc_set(x);
+  Tensor acc_t = fin ? bn_acc_set(x, Cout) : Tensor();
   if (addend.has_value()) {
     TORCH_CHECK(addend->sizes() == y.sizes() && addend->scalar_type() == torch::kBFloat16 &&
                     addend->device() == y.device() &&
@@ -1016,10 +1003,9 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                               bn_x.has_value() ? bn_mean->data_ptr<float>() : nullptr,
                               (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R, (int)S,
                               (int)stride, (int)pad, (int)pad, 0, 0, nullptr, 0, (int)variant,
-                              as.acc, as.tickets, fin ? fin_t.data_ptr<double>() : nullptr,
-                              kAccSlots, cur_stream()),
+                              fin ? acc_t.data_ptr<double>() : nullptr, cur_stream()),
             "conv_fwd");
-  if (fin) return {y, fin_t};
+  if (fin) return {y, acc_t};
   if (with_stats) return {y, part};
   return {y};
 }
@@ -1172,9 +1158,7 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
   Tensor part = with_stats && !fin
                     ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
                     : Tensor();
-  Tensor fin_t = fin ? torch::empty({2, Cout}, x.options().dtype(torch::kFloat64)) : Tensor();
-  AccSet as{nullptr, nullptr};
-  if (fin) as = bn_acc_set(x);
+  Tensor acc_t = fin ? bn_acc_set(x, Cout) : Tensor();
   check_hip(arena_conv_fwd_ex(x.data_ptr(), w.data_ptr(), y.data_ptr(),
                               with_stats && !fin ? part.data_ptr<float>() : nullptr,
                               addend.has_value() ? addend->data_ptr() : nullptr, nullptr, nullptr,
@@ -1182,10 +1166,10 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
                               (int)S,
                               (int)stride, (int)pad_h, (int)pad_w, (int)Ho, (int)Wo,
                               y_out.has_value() ? map6.data() : nullptr, c16 ? 1 : 0,
-                              (int)variant, as.acc, as.tickets,
-                              fin ? fin_t.data_ptr<double>() : nullptr, kAccSlots, cur_stream()),
+                              (int)variant, fin ? acc_t.data_ptr<double>() : nullptr,
+                              cur_stream()),
             "conv_fwd_ex");
-  if (fin) return {y, fin_t};
+  if (fin) return {y, acc_t};
   if (with_stats) return {y, part};
   return {y};
 }

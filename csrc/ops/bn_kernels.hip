@@ -127,48 +127,13 @@ __device__ __forceinline__ void load8f(const float* p, float v[kVec]) {
   v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
 
-// ---------------------------------------------------------------------- finished statistics
-// "acc mode" (conv_kernels.hip ConvArgs::bn_acc has the same protocol): every block adds its
-// per-channel fp64 sums into acc[blockIdx % slots][2][C] with memory-side atomics and draws one
-// ticket; the last block reads the sums back with atomic swaps (leaving the slots zero for the next
-// user of the set) and finishes the per-channel results itself -- no finalize launch. The ticket
-// hand-off is the split-K slab reducer's (cdna_hip_programming.md §5).
-struct AccMode {
-  double* acc;        // [slots][2][C], zero on entry and on exit
-  unsigned* ticket;   // one counter, zero on entry and on exit
-  int slots;
-};
-
-// All threads: returns true in the last block (after the acquire), false elsewhere.
-__device__ __forceinline__ bool acc_ticket(const AccMode& am) {
-  __shared__ unsigned s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(am.ticket, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == gridDim.x - 1 ? 1u : 0u;
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(am.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-  __syncthreads();
-  return s_last != 0;
-}
-
-// Sum of channel c's two accumulators over the slots, swapping them back to zero.
-__device__ __forceinline__ void acc_take(const AccMode& am, int C, int c, double& s0, double& s1) {
-  s0 = s1 = 0.0;
-  for (int k = 0; k < am.slots; ++k) {
-    double* p = am.acc + (size_t)k * 2 * C + c;
-    s0 += __hip_atomic_exchange(p, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s1 += __hip_atomic_exchange(p + C, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
+// ------------------------------------------------------------------ accumulated statistics
+// "acc mode": the statistics pass, the backward reduction and the producing conv's epilogue
+// (conv_kernels.hip ConvArgs::bn_acc) add their per-block fp64 sums straight into acc [2][C] with
+// fire-and-forget memory-side atomics (consecutive threads on consecutive channels: contiguous
+// 512-byte wave instructions). A small finalize kernel -- one thread per channel -- then swaps
+// the sums back to zero and writes the results. That replaces the two-level merge of per-block
+// partials (up to 3136 per channel) in the partial-based finalize kernels below.
 
 struct Geo {
   int cg;    // channel groups (C / 8)
@@ -194,11 +159,11 @@ __device__ __forceinline__ void block_rows(long long M, long long rpb, long long
 
 // ------------------------------------------------------------------------------------ stats
 // part: [nblk][2][C] (block mean, block M2)
-// acc mode (am.acc != null): instead of part, finished (mean, biased var) into fin [2][C] doubles.
+// acc != null: the block's (sum x, sum x^2) go to acc [2][C] (acc mode) instead of part.
 template <typename T>
 __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, long long M, int C,
                                                       long long rpb, float* __restrict__ part,
-                                                      AccMode am, double* __restrict__ fin) {
+                                                      double* __restrict__ acc) {
   const Geo q = geo(C);
   long long r0, r1;
   block_rows(M, rpb, &r0, &r1);
@@ -250,7 +215,6 @@ __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, l
     if (q.g == 0) s_n[q.slot] = n;
   }
   __syncthreads();
-  double* acc = am.acc != nullptr ? am.acc + (size_t)(blockIdx.x % am.slots) * 2 * C : nullptr;
   for (int c = threadIdx.x; c < C; c += kT) {
     float na = s_n[0], ma = s_mean[c], sa = s_m2[c];
     for (int s = 1; s < q.rip; ++s) {
@@ -270,15 +234,6 @@ __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, l
       part[(long long)blockIdx.x * 2 * C + c] = ma;
       part[(long long)blockIdx.x * 2 * C + C + c] = sa;
     }
-  }
-  if (acc == nullptr || !acc_ticket(am)) return;
-  const double inv_m = 1.0 / (double)M;
-  for (int c = threadIdx.x; c < C; c += kT) {
-    double s1, s2;
-    acc_take(am, C, c, s1, s2);
-    const double mean = s1 * inv_m, var = s2 * inv_m - mean * mean;
-    fin[c] = mean;
-    fin[C + c] = var > 0.0 ? var : 0.0;
   }
 }
 
@@ -413,71 +368,57 @@ __global__ __launch_bounds__(kT) void bn_stats_finalize_kernel(const float* __re
   }
 }
 
+// Forward finalize of acc mode: channel c's (sum x, sum x^2) -> the same outputs as
+// bn_stats_finalize_kernel (fp64 arithmetic), accumulators zeroed for the next user.
+__global__ __launch_bounds__(kT) void bn_acc_finalize_kernel(double* __restrict__ acc, long long M,
+                                                             int C, ArenaBNStats out) {
+  const int c = blockIdx.x * kT + threadIdx.x;
+  if (out.batches != nullptr && c == 0) *out.batches += 1;
+  if (c >= C) return;
+  const double s1 = __hip_atomic_exchange(acc + c, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double s2 = __hip_atomic_exchange(acc + C + c, 0.0, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+  const double n = (double)M;
+  const double mean = s1 / n;
+  double m2 = s2 - s1 * mean;
+  m2 = m2 > 0.0 ? m2 : 0.0;
+  const double var = m2 / n;
+  const float invstd = (float)(1.0 / sqrt(var + (double)out.eps));
+  out.mean[c] = (float)mean;
+  out.invstd[c] = invstd;
+  out.scale[c] = (out.gamma ? out.gamma[c] : 1.f) * invstd;
+  out.shift[c] = out.beta ? out.beta[c] : 0.f;
+  if (out.running_mean) {
+    const float mom = out.momentum;
+    out.running_mean[c] = (1.f - mom) * out.running_mean[c] + mom * (float)mean;
+    const double unbiased = n > 1.0 ? m2 / (n - 1.0) : var;
+    out.running_var[c] = (1.f - mom) * out.running_var[c] + mom * (float)unbiased;
+  }
+}
+
 // ------------------------------------------------------------------------------------ apply
 // y = act((x - mean) * scale + shift (+ res)), 2 vectors per thread per round for load ILP.
 // The mask bits are those of the stored (rounded) outputs that are > 0: exactly "saved y > 0"
 // (V8::store_pos).
 
 // NT: non-temporal loads of x (and res) -- their last read before the backward pass
-// FIN: the batch statistics arrive finished as fp64 (mean, biased var) in `fin` [2][C] (from the
-// producing conv's epilogue or the acc-mode statistics kernel): every thread derives invstd,
-// scale and shift of its 8 channels, and block 0 writes st's outputs (mean, invstd, scale, shift
-// for the backward; running statistics; the batch counter) -- the finalize launch's work.
-template <bool FIN>
-__device__ __forceinline__ void apply_coefs(int c0, int cg, long long M, const double* fin,
-                                            const ArenaBNStats& st, float mu[kVec],
-                                            float sc[kVec], float sh[kVec]) {
-  if constexpr (!FIN) {
-    load8f(st.mean + c0, mu);
-    load8f(st.scale + c0, sc);
-    load8f(st.shift + c0, sh);
-  } else {
-    const int C = cg * kVec;
-    float inv[kVec];
-    double var[kVec];
-#pragma unroll
-    for (int i = 0; i < kVec; ++i) {
-      const double m = fin[c0 + i];
-      var[i] = fin[C + c0 + i];
-      mu[i] = (float)m;
-      inv[i] = (float)(1.0 / sqrt(var[i] + (double)st.eps));
-      sc[i] = (st.gamma ? st.gamma[c0 + i] : 1.f) * inv[i];
-      sh[i] = st.beta ? st.beta[c0 + i] : 0.f;
-    }
-    if (blockIdx.x == 0 && (int)threadIdx.x < cg) {
-      const float mom = st.momentum;
-      const double unb = M > 1 ? (double)M / (double)(M - 1) : 1.0;
-#pragma unroll
-      for (int i = 0; i < kVec; ++i) {
-        st.mean[c0 + i] = mu[i];
-        st.invstd[c0 + i] = inv[i];
-        st.scale[c0 + i] = sc[i];
-        st.shift[c0 + i] = sh[i];
-        if (st.running_mean) {
-          st.running_mean[c0 + i] = (1.f - mom) * st.running_mean[c0 + i] + mom * mu[i];
-          st.running_var[c0 + i] = (1.f - mom) * st.running_var[c0 + i] +
-                                   mom * (float)(var[i] * unb);
-        }
-      }
-      if (threadIdx.x == 0 && st.batches != nullptr) *st.batches += 1;
-    }
-  }
-}
-
-template <typename T, bool RELU, bool RES, bool NT, bool FIN>
+template <typename T, bool RELU, bool RES, bool NT>
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
                                                       const T* __restrict__ res,
                                                       T* __restrict__ y,
                                                       uint8_t* __restrict__ mask,
-                                                      ArenaBNStats st,
-                                                      const double* __restrict__ fin,
-                                                      long long M, long long nvec, int cg) {
+                                                      const float* __restrict__ mean,
+                                                      const float* __restrict__ scale,
+                                                      const float* __restrict__ shift,
+                                                      long long nvec, int cg) {
   const long long stride = (long long)gridDim.x * kT;
   // every vector this thread touches has the same channel group: the grid stride is a multiple
   // of kT, and cg divides kT (host-checked), so the per-channel coefficients load once
   const int c0 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1)) * kVec;
   float mu[kVec], sc[kVec], sh[kVec];
-  apply_coefs<FIN>(c0, cg, M, fin, st, mu, sc, sh);
+  load8f(mean + c0, mu);
+  load8f(scale + c0, sc);
+  load8f(shift + c0, sh);
   for (long long v0 = (long long)blockIdx.x * kT + threadIdx.x; v0 < nvec; v0 += 2 * stride) {
     float a[2][kVec], b[2][kVec];
     bool ok[2];
@@ -529,15 +470,15 @@ __device__ __forceinline__ void bn_bwd_finish(const ArenaBNBwd& out, int c, doub
   out.cc[c] = (float)(b / (double)M) * invstd * invstd;
 }
 
-// acc mode (am.acc != null): the block sums go to fp64 accumulators and the last block writes the
-// finished coefficients (no finalize launch); else the per-block partials go to part.
+// acc != null (acc mode): the block sums go to acc [2][C]; else the per-block partials to part.
 template <typename T, bool RELU>
 __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__ dy,
                                                            const uint8_t* __restrict__ mask,
                                                            const T* __restrict__ x, long long M,
                                                            int C, long long rpb,
                                                            float* __restrict__ part,
-                                                           ArenaBNBwd out, AccMode am) {
+                                                           ArenaBNBwd out,
+                                                           double* __restrict__ acc) {
   const Geo q = geo(C);
   long long r0, r1;
   block_rows(M, rpb, &r0, &r1);
@@ -592,7 +533,6 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
     }
   }
   __syncthreads();
-  double* acc = am.acc != nullptr ? am.acc + (size_t)(blockIdx.x % am.slots) * 2 * C : nullptr;
   for (int c = threadIdx.x; c < C; c += kT) {
     float a = 0.f, b = 0.f;
     for (int s = 0; s < q.rip; ++s) {
@@ -607,12 +547,18 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
       part[(long long)blockIdx.x * 2 * C + C + c] = b;
     }
   }
-  if (acc == nullptr || !acc_ticket(am)) return;
-  for (int c = threadIdx.x; c < C; c += kT) {
-    double a, b;
-    acc_take(am, C, c, a, b);
-    bn_bwd_finish(out, c, a, b, M);
-  }
+}
+
+// Backward finalize of acc mode: one thread per channel, accumulators zeroed again.
+__global__ __launch_bounds__(kT) void bn_bwd_acc_finalize_kernel(double* __restrict__ acc,
+                                                                 long long M, int C,
+                                                                 ArenaBNBwd out) {
+  const int c = blockIdx.x * kT + threadIdx.x;
+  if (c >= C) return;
+  const double a = __hip_atomic_exchange(acc + c, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double b = __hip_atomic_exchange(acc + C + c, 0.0, __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+  bn_bwd_finish(out, c, a, b, M);
 }
 
 __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const float* __restrict__ part,
@@ -686,6 +632,11 @@ long long g_max_reduce_blocks = 512;
 int g_bn_nt = 1;           // non-temporal loads in the apply / dx passes (runtime switch for A/Bs)
 long long g_min_rounds = 8;
 
+// acc mode pays one fp64 (a, b) atomic pair per block and channel at the end of the pass; above
+// this many pairs their drain costs more than the partial merge it replaces (ResNet-50: the
+// 2048-channel 7x7 layers run 512 blocks = 1 M pairs), so those layers keep the partials.
+long long g_acc_max_pairs = 32 << 10;
+
 long long reduce_blocks(long long M, int C, long long* rpb) {
   const int rip = kT / (C / kVec);
   long long rounds = (M + rip - 1) / rip;
@@ -714,6 +665,9 @@ void arena_bn_set_fin_max_blocks(int p) { g_fin_max_p = p < 1 ? 1 : (p > 64 ? 64
 
 void arena_bn_set_nt(int on) { g_bn_nt = on ? 1 : 0; }
 
+void arena_bn_set_acc_max_pairs(long long p) { g_acc_max_pairs = p < 0 ? 0 : p; }
+long long arena_bn_acc_max_pairs() { return g_acc_max_pairs; }
+
 void arena_bn_set_reduce_geometry(long long max_blocks, long long min_rounds) {
   g_max_reduce_blocks = max_blocks < 1 ? 1 : (max_blocks > 4096 ? 4096 : max_blocks);
   g_min_rounds = min_rounds < 1 ? 1 : min_rounds;
@@ -735,31 +689,33 @@ long long arena_bn_workspace_floats(long long M, int C) {
 // ext_nblk > 0: `part` already holds the statistics partials of x ([ext_nblk][2][C], ext_rpb rows
 // each), written by the producing convolution's epilogue (conv_kernels.hip): no statistics pass.
 // mask (optional, relu only): [M * C / 8] bytes, bit i of byte v = (y[v * 8 + i] > 0)
-// fin (training): fp64 [2][C] batch (mean, biased var). fin_ready: already finished by the
-// producing convolution (no statistics pass); else with acc != null the statistics kernel runs in
-// acc mode and fills fin (no finalize launch), and the apply kernel finishes the coefficients.
+// acc (training, optional): fp64 [2][C] accumulators (zero on entry, zero on exit). acc_ready:
+// the producing convolution already added the statistics of x (no statistics pass); else the
+// statistics pass runs in acc mode. Either way a one-thread-per-channel finalize follows.
 hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint8_t* mask,
                         long long M, int C, int relu, int training, float* part, int ext_nblk,
                         long long ext_rpb,
-                        double* lvl2, unsigned* tickets, ArenaBNStats st, double* fin,
-                        int fin_ready, double* acc, unsigned* acc_ticket_ptr, int acc_slots,
-                        hipStream_t stream) {
+                        double* lvl2, unsigned* tickets, ArenaBNStats st, double* acc,
+                        int acc_ready, hipStream_t stream) {
   if (bad_shape(M, C)) return hipErrorInvalidValue;
   const int groups = (C + 63) / 64;
-  bool use_fin = false;
-  if (training && fin != nullptr && fin_ready) {
-    use_fin = true;
-  } else if (training && fin != nullptr && acc != nullptr && ext_nblk <= 0) {
+  if (training && acc != nullptr && !acc_ready) {
     long long rpb;
-    const long long nb = reduce_blocks(M, C, &rpb);
-    const AccMode am{acc, acc_ticket_ptr, acc_slots};
-    if (dtype == 1)
-      hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb), dim3(kT), 0, stream,
-                         static_cast<const uint16_t*>(x), M, C, rpb, nullptr, am, fin);
-    else
-      hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kT), 0, stream,
-                         static_cast<const float*>(x), M, C, rpb, nullptr, am, fin);
-    use_fin = true;
+    if (reduce_blocks(M, C, &rpb) * C > g_acc_max_pairs) acc = nullptr;   // partials instead
+  }
+  if (training && acc != nullptr) {
+    if (!acc_ready) {
+      long long rpb;
+      const long long nb = reduce_blocks(M, C, &rpb);
+      if (dtype == 1)
+        hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb), dim3(kT), 0, stream,
+                           static_cast<const uint16_t*>(x), M, C, rpb, nullptr, acc);
+      else
+        hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kT), 0, stream,
+                           static_cast<const float*>(x), M, C, rpb, nullptr, acc);
+    }
+    hipLaunchKernelGGL(bn_acc_finalize_kernel, dim3((C + kT - 1) / kT), dim3(kT), 0, stream, acc,
+                       M, C, st);
   } else if (training && ext_nblk > 0) {
     if (ext_rpb <= 0 || (long long)ext_nblk * ext_rpb < M) return hipErrorInvalidValue;
     hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups, fin_blocks_per_group(ext_nblk)),
@@ -767,26 +723,22 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
   } else if (training) {
     long long rpb;
     const long long nb = reduce_blocks(M, C, &rpb);
-    const AccMode none{nullptr, nullptr, 0};
     if (dtype == 1)
       hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb), dim3(kT), 0, stream,
-                         static_cast<const uint16_t*>(x), M, C, rpb, part, none, nullptr);
+                         static_cast<const uint16_t*>(x), M, C, rpb, part, nullptr);
     else
       hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kT), 0, stream,
-                         static_cast<const float*>(x), M, C, rpb, part, none, nullptr);
+                         static_cast<const float*>(x), M, C, rpb, part, nullptr);
     hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups, fin_blocks_per_group((int)nb)),
                        dim3(kT), 0, stream, part, (int)nb, M, C, rpb, lvl2, tickets, st);
   }
   const long long nvec = M * (C / kVec);
   const int nb = elementwise_blocks(nvec);
   const int cg = C / kVec;
-#define ARENA_BN_APPLY_K(TT, R, S, NT, F)                                                    \
-  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S, NT, F>), dim3(nb), dim3(kT), 0, stream,    \
+#define ARENA_BN_APPLY_NT(TT, R, S, NT)                                                      \
+  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S, NT>), dim3(nb), dim3(kT), 0, stream,       \
                      static_cast<const TT*>(x), static_cast<const TT*>(res), static_cast<TT*>(y), \
-                     mask, st, fin, M, nvec, cg)
-#define ARENA_BN_APPLY_NT(TT, R, S, NT) \
-  do { if (use_fin) ARENA_BN_APPLY_K(TT, R, S, NT, true); \
-       else ARENA_BN_APPLY_K(TT, R, S, NT, false); } while (0)
+                     mask, st.mean, st.scale, st.shift, nvec, cg)
 #define ARENA_BN_APPLY(TT, R, S) \
   do { if (g_bn_nt) ARENA_BN_APPLY_NT(TT, R, S, true); else ARENA_BN_APPLY_NT(TT, R, S, false); } \
   while (0)
@@ -804,24 +756,23 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
   }
 #undef ARENA_BN_APPLY
 #undef ARENA_BN_APPLY_NT
-#undef ARENA_BN_APPLY_K
   return hipGetLastError();
 }
 
 // ext_nblk > 0: `part` already holds the backward partials of (dy, x) ([ext_nblk][2][C]), written
 // by the epilogue of the backward-data convolution that produced dy (conv_kernels.hip, EPI 2):
 // no reduction pass.
-// acc != null (and no external partials): the reduction runs in acc mode and its last block
-// writes the coefficients -- no finalize launch.
+// acc != null (and no external partials): the reduction runs in acc mode and a one-thread-per-
+// channel finalize writes the coefficients.
 hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const void* x, void* dx,
                         void* dres, long long M, int C, int relu, float* part, int ext_nblk,
                         double* lvl2, unsigned* tickets, ArenaBNBwd co, double* acc,
-                        unsigned* acc_ticket_ptr, int acc_slots, hipStream_t stream) {
+                        hipStream_t stream) {
   if (bad_shape(M, C) || (relu && mask == nullptr)) return hipErrorInvalidValue;
   long long rpb;
   long long nb = reduce_blocks(M, C, &rpb);
-  const bool acc_mode = acc != nullptr && ext_nblk <= 0;
-  const AccMode am{acc_mode ? acc : nullptr, acc_ticket_ptr, acc_slots};
+  const bool acc_mode = acc != nullptr && ext_nblk <= 0 && nb * C <= g_acc_max_pairs;
+  double* am = acc_mode ? acc : nullptr;
   if (ext_nblk > 0) {
     nb = ext_nblk;
   } else {
@@ -836,7 +787,10 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
     }
 #undef ARENA_BN_RED
   }
-  if (!acc_mode)
+  if (acc_mode)
+    hipLaunchKernelGGL(bn_bwd_acc_finalize_kernel, dim3((C + kT - 1) / kT), dim3(kT), 0, stream,
+                       acc, M, C, co);
+  else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64, fin_blocks_per_group((int)nb)),
                        dim3(kT), 0, stream, part, (int)nb, M, C, lvl2, tickets, co);
   const long long nvec = M * (C / kVec);

@@ -85,16 +85,13 @@ struct ConvArgs {
   // (4 pixels x 16 channels = 128 contiguous bytes of an NHWC row). S is a multiple of 4. The
   // space-to-depth form of the 7x7/2 stem runs on it.
   int c16;
-  // EPI 1, finished statistics (bn_acc != null, part unused): every tile adds its moment sums
-  // (n*mean, M2 + n*mean^2 = sum y, sum y^2 of its rows) into fp64 accumulators
-  // bn_acc[mt % bn_slots][2][Cout] with memory-side atomics and draws a ticket of its column
-  // block; the last tile of the column block swaps the slots back to zero and writes the batch
-  // (mean, biased variance) of its channels to bn_fin [2][Cout]. The BN layer then needs no
-  // finalize launch: its apply kernel derives invstd/scale from bn_fin.
+  // EPI 1, accumulated statistics (bn_acc != null, part unused): every tile adds its moment
+  // sums (n*mean = sum y, M2 + n*mean^2 = sum y^2 over its rows) into fp64 accumulators
+  // bn_acc [2][Cout] with memory-side atomics, fire-and-forget. A one-block-per-256-channels
+  // finalize (bn_kernels.hip bn_acc_finalize) reads them back, zeroes them and writes the
+  // BatchNorm coefficients: cheaper than merging per-tile partials (3136 per channel for a
+  // 56x56 layer at batch 128) in a two-level reduction.
   double* bn_acc;
-  unsigned* bn_tickets;   // [n_tiles], zero on entry, left zero
-  double* bn_fin;
-  int bn_slots;
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -167,53 +164,29 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
-// EPI 1 finished-statistics tail (see ConvArgs::bn_acc). `emit(add)` calls add(c, mean, m2) for
-// the block's channels c in [0, BN) whose tile statistics this thread holds. Ticket protocol of
-// a split-K slab reducer (cdna_hip_programming.md §5): every wave waits for its atomics, block
-// barrier, one lane releases and draws the ticket; the last tile acquires and reads the sums
-// with atomic swaps (executed at the memory side like the adds, so no stale cache line can be
-// read, and the slots are zero again for the next use).
+// EPI 1 accumulated-statistics tail (see ConvArgs::bn_acc). `emit(add)` calls add(c, mean, m2)
+// for the block's channels c in [0, BN) whose tile statistics this thread holds. The values are
+// restaged in LDS so that consecutive lanes add to consecutive channels: 64 fp64 adds = 512
+// contiguous bytes per wave instruction (scattered few-lane atomics cost one 64-B memory-side
+// request each). No wait and no fence: the kernel's end makes the sums visible to the finalize.
 template <int BM, int BN, typename Emit>
-__device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int mt, int nt, int n0,
-                                                int nrows, Emit&& emit) {
-  double* acc = a.bn_acc + (size_t)(mt % a.bn_slots) * 2 * a.Cout;
-  const double n = (double)nrows;
+__device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int n0, int nrows,
+                                                Emit&& emit) {
+  __shared__ float s_st[2][BN];
   emit([&](int c, float mean, float m2) {
-    const double mu = (double)mean;
-    unsafeAtomicAdd(acc + n0 + c, n * mu);                       // sum y
-    unsafeAtomicAdd(acc + a.Cout + n0 + c, (double)m2 + n * mu * mu);  // sum y^2
+    s_st[0][c] = mean;
+    s_st[1][c] = m2;
   });
-  __shared__ unsigned s_last;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(a.bn_tickets + nt, 1u, __ATOMIC_RELAXED,
-                                                __HIP_MEMORY_SCOPE_AGENT);
-    s_last = old == (unsigned)(a.m_tiles - 1) ? 1u : 0u;
-    if (s_last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  }
-  __syncthreads();
-  if (!s_last) return;
-  const double inv_m = 1.0 / (double)a.M;
+  // LDS-only barrier: __syncthreads() would also wait for the tile's output stores (vmcnt(0)),
+  // holding the CU slot for their whole latency (measured +16 us on a 56x56 1x1 layer)
+  lds_barrier();
+  double* acc = a.bn_acc + n0;
+  const double n = (double)nrows;
   for (int c = threadIdx.x; c < BN; c += kThreads) {
-    double s1 = 0.0, s2 = 0.0;
-    for (int k = 0; k < a.bn_slots; ++k) {
-      double* sl = a.bn_acc + (size_t)k * 2 * a.Cout + n0 + c;
-      s1 += __hip_atomic_exchange(sl, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s2 += __hip_atomic_exchange(sl + a.Cout, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    const double mean = s1 * inv_m;
-    const double var = s2 * inv_m - mean * mean;
-    a.bn_fin[n0 + c] = mean;
-    a.bn_fin[a.Cout + n0 + c] = var > 0.0 ? var : 0.0;
+    const double mu = (double)s_st[0][c];
+    unsafeAtomicAdd(acc + c, n * mu);                                     // sum y
+    unsafeAtomicAdd(acc + a.Cout + c, (double)s_st[1][c] + n * mu * mu);  // sum y^2
   }
-  if (threadIdx.x == 0)
-    __hip_atomic_store(a.bn_tickets + nt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // NBUF = LDS stage buffers: 2 (double-buffered K loop) or 1 for a single 64-deep K step (1x1
@@ -677,7 +650,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
           }
       }
     } else {
-      bn_acc_epilogue<BM, BN>(a, mt, nt, n0, nrows, [&](auto&& add) {
+      bn_acc_epilogue<BM, BN>(a, n0, nrows, [&](auto&& add) {
         if (wm == 0 && fr == 0) {
 #pragma unroll
           for (int j = 0; j < NI; ++j)
@@ -744,15 +717,14 @@ extern "C" {
 // see ConvArgs.
 // bnx/bnmask/bnmean (optional, with part): the backward-data form, part = BatchNorm-backward
 // partials of y instead of forward statistics (see ConvArgs).
-// bn_acc/bn_tickets/bn_fin (optional, instead of part): finished BatchNorm statistics, see
-// ConvArgs::bn_acc; bn_acc [bn_slots][2][Cout] doubles and bn_tickets [Cout / 64] zero on entry.
+// bn_acc (optional, instead of part): accumulated BatchNorm statistics, see ConvArgs::bn_acc;
+// [2][Cout] doubles, zero on entry (the finalize that consumes them zeroes them again).
 hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part, const void* add,
                              const uint8_t* addmask,
                              const void* bnx, const uint8_t* bnmask, const float* bnmean, int N,
                              int H, int W, int C, int Cout, int R, int S, int stride, int pad_h,
                              int pad_w, int Ho, int Wo, const int* y_map, int c16, int variant,
-                             double* bn_acc, unsigned* bn_tickets, double* bn_fin, int bn_slots,
-                             hipStream_t st) {
+                             double* bn_acc, hipStream_t st) {
   if (Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0) return hipErrorInvalidValue;
   if (c16 ? (C != 16 || S % 4) : (C % kBK)) return hipErrorInvalidValue;
   ConvArgs a{};
@@ -771,13 +743,8 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   // forward statistics are taken from the accumulators before the epilogue adds an addend
   if (part != nullptr && bnx == nullptr && add != nullptr) return hipErrorInvalidValue;
   if (bn_acc != nullptr) {
-    if (part != nullptr || bnx != nullptr || add != nullptr || bn_tickets == nullptr ||
-        bn_fin == nullptr || bn_slots < 1)
-      return hipErrorInvalidValue;
+    if (part != nullptr || bnx != nullptr || add != nullptr) return hipErrorInvalidValue;
     a.bn_acc = bn_acc;
-    a.bn_tickets = bn_tickets;
-    a.bn_fin = bn_fin;
-    a.bn_slots = bn_slots;
   }
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
   a.stride = stride; a.pad = pad_h; a.pad_w = pad_w;
@@ -822,8 +789,7 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
                           int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad,
                           int variant, hipStream_t st) {
   return arena_conv_fwd_ex(x, w, y, part, add, nullptr, bnx, bnmask, bnmean, N, H, W, C, Cout, R, S,
-                           stride, pad, pad, 0, 0, nullptr, 0, variant, nullptr, nullptr, nullptr,
-                           0, st);
+                           stride, pad, pad, 0, 0, nullptr, 0, variant, nullptr, st);
 }
 
 }  // extern "C"

@@ -148,9 +148,9 @@ def test_cnn_bench_example_runs_with_graph_capture(tmp_path):
 
 @pytest.mark.parametrize("shape", [(4, 128, 14, 14), (2, 256, 7, 7), (8, 64, 28, 28)])
 def test_conv_finished_stats_feed_bn(shape):
-    """Finished statistics from the conv epilogue (fp64 atomics + last-tile ticket) give the same
-    BN forward/backward and running statistics as the fp32 reference, and leave the accumulator
-    set zeroed: many back-to-back layers reuse the pool without a memset."""
+    """Statistics accumulated by the conv epilogue (fp64 memory-side atomics) and finished by the
+    BN layer's per-channel finalize give the same BN forward/backward and running statistics as
+    the fp32 reference; the pool of accumulator sets wraps around correctly."""
     from arena_amd.ops import conv
     from arena_amd.ops.batchnorm import BatchNormAct2d, FinishedStats
     torch.manual_seed(1)
@@ -159,12 +159,15 @@ def test_conv_finished_stats_feed_bn(shape):
     w = _nhwc((torch.randn(C, 64, 3, 3, device="cuda") * 0.05).to(torch.bfloat16))
     for rep in range(130):   # more uses than the pool has sets (128)
         y, st = conv.conv2d_fwd(x, w, 1, 1, with_stats=True, final=True)
-        assert isinstance(st, FinishedStats) and st.fin.dtype == torch.float64
-        yf = y.float()
-        mean = yf.mean(dim=(0, 2, 3))
-        var = yf.var(dim=(0, 2, 3), unbiased=False)
-        assert torch.allclose(st.fin[0].float(), mean, rtol=1e-5, atol=1e-5)
-        assert torch.allclose(st.fin[1].float(), var, rtol=1e-4, atol=1e-6)
+        assert isinstance(st, FinishedStats) and st.fin.shape == (2, C)
+        assert st.fin.dtype == torch.float64
+        yf = y.double()
+        Mrows = N * H * W
+        assert torch.allclose(st.fin[0] / Mrows, yf.mean(dim=(0, 2, 3)), rtol=1e-5, atol=1e-6)
+        assert torch.allclose(st.fin[1] / Mrows, (yf * yf).mean(dim=(0, 2, 3)), rtol=1e-5,
+                              atol=1e-6)
+        if rep < 129:
+            st.discard()      # what a BN layer's finalize does: the set is zero again
     m = BatchNormAct2d(C).cuda()
     ref = torch.nn.BatchNorm2d(C).cuda()
     ref.load_state_dict(m.state_dict())
@@ -180,8 +183,9 @@ def test_conv_finished_stats_feed_bn(shape):
     out.backward(g.to(out.dtype))
     outr.backward(g)
     assert (y.grad.float() - yr.grad).abs().max() / yr.grad.abs().max() < 3e-2
-    assert torch.allclose(m.weight.grad, ref.weight.grad, rtol=2e-2, atol=1e-2)
-    assert torch.allclose(m.bias.grad, ref.bias.grad, rtol=2e-2, atol=1e-2)
+    # (bf16 output gradient in, fp32 reference: compare at the scale of the largest entry)
+    for a, b in ((m.weight.grad, ref.weight.grad), (m.bias.grad, ref.bias.grad)):
+        assert (a - b).abs().max() / b.abs().max() < 1e-2
 
 
 def test_resnet_step_finished_stats_match_partials():
