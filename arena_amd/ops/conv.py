@@ -28,7 +28,20 @@ Tensor = torch.Tensor
 TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
 # + 4: three-stage K pipeline; + 8: single stage buffer, serial K loop, high occupancy
 TILES.update({v + d: t for v, t in list(TILES.items()) for d in (4, 8)})
+# + 16 * (k - 1): the same tile with its K steps split over k blocks (in-kernel ticket reduction,
+# bit-reproducible): for the layers whose tile count leaves CUs idle (14x14 / 7x7 at batch 128)
+KSPLITS = (2, 3, 4, 6, 8)
+TILES.update({v + 16 * (k - 1): TILES[v] for v in range(12) for k in KSPLITS})
 _CUS = 256
+
+
+def kvariant(v: int, ks: int) -> int:
+    """Variant code of tile variant ``v`` (0..11) with its K steps split over ``ks`` blocks."""
+    return v + 16 * (ks - 1)
+
+
+def split_of(v: int) -> int:
+    return v // 16 + 1
 
 
 def out_hw(h: int, w: int, r: int, s: int, stride: int, pad: int) -> Tuple[int, int]:
@@ -45,7 +58,33 @@ def kernel_ok(x: Tensor, w: Tensor, stride: int, pad: int) -> bool:
 
 
 def variants_for(cout: int):
-    return [v for v, (_, bn) in TILES.items() if cout % bn == 0]
+    """Unsplit tile variants for ``cout`` output channels."""
+    return [v for v, (_, bn) in TILES.items() if v < 16 and cout % bn == 0]
+
+
+def split_variants_for(m: int, cout: int, ktot: int):
+    """Split-K candidates for a GEMM of ``m`` rows, ``cout`` columns and ``ktot`` reduction: for
+    tiles whose grid gives fewer than two blocks per CU, the splits that bring it to about 2 or 4
+    blocks per CU with at least 4 K steps per slice."""
+    out = []
+    if os.environ.get("ARENA_CONV_KSPLIT", "1") == "0":
+        return out
+    steps = ktot // 64
+    for v in variants_for(cout):
+        if v >= 4 and v < 8:
+            continue   # the three-stage pipeline needs long K loops: not a split candidate
+        bm, bn = TILES[v]
+        tiles = -(-m // bm) * (cout // bn)
+        if tiles >= 2 * _CUS or tiles > 65536:
+            continue
+        ks_set = set()
+        for want in (2 * _CUS, 4 * _CUS):
+            need = -(-want // tiles)
+            ks = next((k for k in KSPLITS if k >= need), KSPLITS[-1])
+            if steps // ks >= 4:
+                ks_set.add(ks)
+        out += [kvariant(v, k) for k in sorted(ks_set)]
+    return out
 
 
 def pick_variant(m: int, cout: int) -> int:
@@ -555,10 +594,12 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
         y = F.conv2d(x, w, stride=stride, padding=pad)
         dy = torch.randn_like(y)
         t = {}
-        for v in variants_for(cout):
+        m_out = x.shape[0] * ho * wo
+        for v in variants_for(cout) + split_variants_for(m_out, cout, cin * k[0] * k[1]):
             t[("fwd", v)] = _time(lambda: conv2d_fwd(x, w, stride, pad, v, with_stats=True))
         if stride == 1:
-            for v in variants_for(cin):
+            m_in = x.shape[0] * x.shape[2] * x.shape[3]
+            for v in variants_for(cin) + split_variants_for(m_in, cin, cout * k[0] * k[1]):
                 t[("bwd", v)] = _time(lambda: conv2d_bwd_data(dy, w, pad, v))
         else:   # phase decomposition: per-phase heuristic (-1) or one tile for every phase
             hw = (x.shape[2], x.shape[3])

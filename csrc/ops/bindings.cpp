@@ -65,7 +65,9 @@ hipError_t arena_conv_flip_multi(int, const void* const*, void* const*, const in
 hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void*, const uint8_t*,
                              const void*, const uint8_t*, const float*, int, int, int, int, int,
                              int, int, int, int, int, int, int, const int*, int, int, double*,
-                             hipStream_t);
+                             int, void*, unsigned*, hipStream_t);
+long long arena_conv_fwd_ksplit_floats(long long, int, int, int);
+long long arena_conv_fwd_tiles(long long, int, int);
 hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
                                int, int, int, int, int, int, int, int, int, int, int, float,
                                hipStream_t);
@@ -746,6 +748,60 @@ Tensor bn_acc_set(const Tensor& like, int64_t C) {
   return pools[dev][set].narrow(0, 0, 2 * C).view({2, C});
 }
 
+// Split-K tickets of the conv kernel (ConvArgs::kcnt): one ring of zeroed counters per device;
+// each launch takes `tiles` consecutive counters from a cursor and its last-arriving blocks zero
+// them again, so the ring needs no memset and graph replays stay valid. Consecutive launches get
+// disjoint ranges, so launches on concurrent streams do not share tickets unless more than
+// kConvTickets / 65536 of them are in flight at once.
+constexpr int64_t kConvTickets = 1 << 22, kConvMaxTiles = 1 << 16;
+unsigned* conv_tickets(const Tensor& like, int64_t tiles) {
+  static std::vector<Tensor> pools;
+  static std::vector<int64_t> next;
+  TORCH_CHECK(tiles > 0 && tiles <= kConvMaxTiles, "conv split-K: too many output tiles");
+  const int dev = like.get_device();
+  if ((int)pools.size() <= dev) {
+    pools.resize(dev + 1);
+    next.resize(dev + 1, 0);
+  }
+  if (!pools[dev].defined()) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    check_hip(hipStreamIsCapturing(cur_stream(), &cs), "conv_tickets");
+    TORCH_CHECK(cs == hipStreamCaptureStatusNone,
+                "arena conv split-K: run one eager step before capturing a graph (its ticket "
+                "counters are allocated and zeroed on first use)");
+    pools[dev] = torch::zeros({kConvTickets}, like.options().dtype(torch::kInt32));
+    check_hip(hipStreamSynchronize(cur_stream()), "conv_tickets zero");
+  }
+  if (next[dev] + tiles > kConvTickets) next[dev] = 0;
+  unsigned* p = reinterpret_cast<unsigned*>(pools[dev].data_ptr<int32_t>()) + next[dev];
+  next[dev] += (tiles + 63) / 64 * 64;
+  return p;
+}
+
+// conv variant code: tile/pipeline variant (0..11) + 16 * (ksplit - 1)
+struct ConvSplit {
+  int base = 0, ks = 1;
+  Tensor ws;
+  unsigned* cnt = nullptr;
+};
+
+ConvSplit conv_split(const Tensor& x, int64_t variant, int64_t M, int64_t Cout, int64_t Ktot) {
+  ConvSplit s;
+  TORCH_CHECK(variant >= 0, "conv: bad variant ", variant);
+  s.base = (int)(variant % 16);
+  s.ks = (int)(variant / 16) + 1;
+  TORCH_CHECK(s.base <= 11 && ((s.base & 1) || Cout % 128 == 0), "conv: variant ", variant,
+              " is not a tile variant for Cout = ", Cout);
+  if (s.ks > 1) {
+    TORCH_CHECK(s.ks <= Ktot / 64, "conv: split-K ", s.ks, " exceeds the ", Ktot / 64,
+                " K steps");
+    const long long nf = arena_conv_fwd_ksplit_floats(M, (int)Cout, s.base, s.ks);
+    s.ws = torch::empty({nf}, x.options().dtype(torch::kFloat32));
+    s.cnt = conv_tickets(x, arena_conv_fwd_tiles(M, (int)Cout, s.base));
+  }
+  return s;
+}
+
 // finished statistics / acc-mode reductions in the BN kernels (runtime switch for A/Bs)
 bool g_bn_acc = [] {
   const char* e = getenv("ARENA_BN_FINAL");
@@ -951,14 +1007,13 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
   TORCH_CHECK(C % 64 == 0 && Cout % 64 == 0, "conv_fwd: C and Cout must be multiples of 64");
   TORCH_CHECK(stride >= 1 && pad >= 0 && H + 2 * pad >= R && W + 2 * pad >= S,
               "conv_fwd: bad stride/padding");
-  TORCH_CHECK(variant >= 0 && variant <= 11 && ((variant & 1) || Cout % 128 == 0),
-              "conv_fwd: variant ", variant, " needs Cout % 128 == 0");
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_fwd: too many output pixels");
+  const ConvSplit ks = conv_split(x, variant, N * Ho * Wo, Cout, R * S * C);
   Tensor y = torch::empty({N, Cout, Ho, Wo},
                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
   static const int bm[4] = {128, 128, 64, 64};
-  const int64_t m_tiles = (N * Ho * Wo + bm[variant & 3] - 1) / bm[variant & 3];
+  const int64_t m_tiles = (N * Ho * Wo + bm[ks.base & 3] - 1) / bm[ks.base & 3];
   const bool fin = with_stats && stats_final;
   TORCH_CHECK(!fin || (!bn_x.has_value() && !addend.has_value() && Cout <= kAccC),
               "conv_fwd: stats_final is forward statistics without an addend");
@@ -1002,8 +1057,9 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                                   : nullptr,
                               bn_x.has_value() ? bn_mean->data_ptr<float>() : nullptr,
                               (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R, (int)S,
-                              (int)stride, (int)pad, (int)pad, 0, 0, nullptr, 0, (int)variant,
-                              fin ? acc_t.data_ptr<double>() : nullptr, cur_stream()),
+                              (int)stride, (int)pad, (int)pad, 0, 0, nullptr, 0, ks.base,
+                              fin ? acc_t.data_ptr<double>() : nullptr, ks.ks,
+                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, cur_stream()),
             "conv_fwd");
   if (fin) return {y, acc_t};
   if (with_stats) return {y, part};
@@ -1116,10 +1172,9 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
   TORCH_CHECK(w.size(1) == C, "conv_fwd_ex: weight/input channel mismatch");
   TORCH_CHECK(Cout % 64 == 0 && (c16 ? (C == 16 && S % 4 == 0) : C % 64 == 0),
               "conv_fwd_ex: Cout % 64, and C % 64 (or C == 16, S % 4 == 0 in c16 mode)");
-  TORCH_CHECK(variant >= 0 && variant <= 11 && ((variant & 1) || Cout % 128 == 0),
-              "conv_fwd_ex: bad variant");
   TORCH_CHECK(stride >= 1 && Ho >= 1 && Wo >= 1, "conv_fwd_ex: bad geometry");
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_fwd_ex: too many output pixels");
+  const ConvSplit ks = conv_split(x, variant, N * Ho * Wo, Cout, R * S * C);
   Tensor y;
   std::vector<int> map6;
   if (y_out.has_value()) {
@@ -1150,7 +1205,7 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
                 "conv_fwd_ex: addend must be shaped like the output tensor");
   }
   static const int bm[4] = {128, 128, 64, 64};
-  const int64_t m_tiles = (N * Ho * Wo + bm[variant & 3] - 1) / bm[variant & 3];
+  const int64_t m_tiles = (N * Ho * Wo + bm[ks.base & 3] - 1) / bm[ks.base & 3];
   TORCH_CHECK(!(with_stats && y_out.has_value()), "conv_fwd_ex: statistics need a dense output");
   const bool fin = with_stats && stats_final;
   TORCH_CHECK(!fin || (!addend.has_value() && Cout <= kAccC),
@@ -1166,8 +1221,8 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
                               (int)S,
                               (int)stride, (int)pad_h, (int)pad_w, (int)Ho, (int)Wo,
                               y_out.has_value() ? map6.data() : nullptr, c16 ? 1 : 0,
-                              (int)variant, fin ? acc_t.data_ptr<double>() : nullptr,
-                              cur_stream()),
+                              ks.base, fin ? acc_t.data_ptr<double>() : nullptr, ks.ks,
+                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, cur_stream()),
             "conv_fwd_ex");
   if (fin) return {y, acc_t};
   if (with_stats) return {y, part};

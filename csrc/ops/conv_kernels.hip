@@ -92,6 +92,15 @@ struct ConvArgs {
   // BatchNorm coefficients: cheaper than merging per-tile partials (3136 per channel for a
   // 56x56 layer at batch 128) in a two-level reduction.
   double* bn_acc;
+  // Split-K (ksplit > 1): the K steps of every output tile are divided over ksplit blocks. Each
+  // writes its fp32 accumulators to kws [tile][slice][acc][thread] (16-byte stores, thread-
+  // contiguous), publishes them (agent release, then a relaxed ticket on kcnt[tile]), and the
+  // block drawing the last ticket sums all slices in slice order -- the same order whichever
+  // block arrives last, so results are bit-reproducible -- resets the ticket and runs the
+  // epilogue. For the layers whose tile count leaves CUs idle (14x14 and 7x7 stages at batch 128).
+  int ksplit;
+  float4* kws;
+  unsigned* kcnt;
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -207,10 +216,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
 
   // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin dispatch), so give each XCD
   // a contiguous range of tiles (bijective for any grid size).
-  const int nwg = a.m_tiles * a.n_tiles;
+  const int ks = a.ksplit;
+  const int nwg = a.m_tiles * a.n_tiles * ks;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
-  const int tile = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
+  const int lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
+  // a tile's K slices are consecutive in the XCD order: the last arriver reads same-XCD slabs
+  const int tile = ks > 1 ? lin / ks : lin, slice = ks > 1 ? lin - tile * ks : 0;
   const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
   const int m0 = mt * BM, n0 = nt * BN;
 
@@ -243,8 +255,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     b_src[i] = a.w + (size_t)(n0 + row) * a.Ktot + (pos ^ swz(row)) * 8;
   }
   const int CB = a.c16 ? 1 : a.C / kBK;  // 64-channel blocks per tap
+  // this block's K steps: [t0, t0 + T) of the Ktot / kBK (split-K: slice `slice` of ks)
+  const int Tall = a.Ktot / kBK;
+  const int t0 = (int)((long long)Tall * slice / ks);
+  const int T = (int)((long long)Tall * (slice + 1) / ks) - t0;
 
-  auto stage = [&](int t, int buf) {
+  auto stage = [&](int tl, int buf) {
+    const int t = t0 + tl;
     uint8_t* base = lds + buf * kBufBytes;
     if (a.c16) {
       // K step t = filter row r, columns 4*sb .. 4*sb+3; 16-byte chunk c = pixel c/2, half c%2
@@ -286,7 +303,6 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
 
   const int wm = wave >> 1, wn = wave & 1;
   const int fr = lane & 15, fq = lane >> 4;
-  const int T = a.Ktot / kBK;
 
   auto compute = [&](int buf) {
     const uint8_t* abuf = lds + buf * kBufBytes;
@@ -356,6 +372,57 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+    }
+  }
+
+  if (ks > 1) {
+    // ---- split-K hand-off (cdna_hip_programming.md §5 "In-launch split-K reduction") ----
+    constexpr int NA = MI * NI;
+    float4* slab = a.kws + (size_t)tile * ks * NA * kThreads;
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+        slab[((size_t)slice * NA + i * NI + j) * kThreads + tid] =
+            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // the flag travels through the stage LDS (free: the K loop ended on a barrier); a second
+    // __shared__ object would perturb the K loop's waits (cdna_hip_programming.md §5 item 4a)
+    volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(lds);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned old =
+          __hip_atomic_fetch_add(a.kcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned last = old == (unsigned)(ks - 1) ? 1u : 0u;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        a.kcnt[tile] = 0u;   // ready for the next launch (kernel boundary orders it)
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      flag[0] = last;
+    }
+    __syncthreads();
+    const unsigned last = flag[0];
+    __syncthreads();   // every wave has read the flag before the epilogue reuses the LDS
+    if (!last) return;
+    // sum the slices in slice order (this block's own slab re-read from memory: the order, and
+    // so the rounding, is independent of which block arrived last)
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const float4 v = slab[(size_t)(i * NI + j) * kThreads + tid];
+        acc[i][j] = f32x4v{v.x, v.y, v.z, v.w};
+      }
+      for (int s = 1; s < ks; ++s) {
+        float4 v[NI];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) v[j] = slab[((size_t)s * NA + i * NI + j) * kThreads + tid];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) acc[i][j] += f32x4v{v[j].x, v[j].y, v[j].z, v[j].w};
+      }
     }
   }
 
@@ -681,7 +748,7 @@ hipError_t launch(const ConvArgs& a0, int pipe, hipStream_t st) {
   ConvArgs a = a0;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  const int nwg = a.m_tiles * a.n_tiles;
+  const int nwg = a.m_tiles * a.n_tiles * a.ksplit;
   // stage buffers: pipe 0 (variants 0..3) two, pipe 1 (4..7) three, pipe 2 (8..11) one (serial,
   // high occupancy); a single K step always one
   const int nb = a.Ktot == kBK || pipe == 2 ? 1 : (pipe == 1 ? 3 : 2);
@@ -724,7 +791,8 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
                              const void* bnx, const uint8_t* bnmask, const float* bnmean, int N,
                              int H, int W, int C, int Cout, int R, int S, int stride, int pad_h,
                              int pad_w, int Ho, int Wo, const int* y_map, int c16, int variant,
-                             double* bn_acc, hipStream_t st) {
+                             double* bn_acc, int ksplit, void* kws, unsigned* kcnt,
+                             hipStream_t st) {
   if (Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0) return hipErrorInvalidValue;
   if (c16 ? (C != 16 || S % 4) : (C % kBK)) return hipErrorInvalidValue;
   ConvArgs a{};
@@ -774,6 +842,13 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.M = (int)M;
   a.Ktot = R * S * C;
   if (variant < 0 || variant > 11) return hipErrorInvalidValue;
+  // split-K: every slice gets at least one K step; the caller sized kws with
+  // arena_conv_fwd_ksplit_floats and zeroed kcnt once (the kernel re-zeroes what it uses)
+  if (ksplit < 1 || ksplit > a.Ktot / kBK || (ksplit > 1 && (kws == nullptr || kcnt == nullptr)))
+    return hipErrorInvalidValue;
+  a.ksplit = ksplit;
+  a.kws = (float4*)kws;
+  a.kcnt = kcnt;
   const int pipe = variant >> 2;
   switch (variant & 3) {
     case 0: return Cout % 128 ? hipErrorInvalidValue : launch<128, 128>(a, pipe, st);
@@ -789,7 +864,22 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
                           int N, int H, int W, int C, int Cout, int R, int S, int stride, int pad,
                           int variant, hipStream_t st) {
   return arena_conv_fwd_ex(x, w, y, part, add, nullptr, bnx, bnmask, bnmean, N, H, W, C, Cout, R, S,
-                           stride, pad, pad, 0, 0, nullptr, 0, variant, nullptr, st);
+                           stride, pad, pad, 0, 0, nullptr, 0, variant, nullptr, 1, nullptr, nullptr,
+                           st);
+}
+
+// Split-K workspace of one launch, in floats (0 when ksplit == 1), and its ticket count (tiles).
+long long arena_conv_fwd_ksplit_floats(long long M, int Cout, int variant, int ksplit) {
+  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
+  if (ksplit <= 1 || variant < 0 || variant > 11) return 0;
+  const long long tiles = ((M + bm[variant & 3] - 1) / bm[variant & 3]) * (Cout / bn[variant & 3]);
+  return tiles * ksplit * bm[variant & 3] * bn[variant & 3];
+}
+
+long long arena_conv_fwd_tiles(long long M, int Cout, int variant) {
+  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
+  if (variant < 0 || variant > 11) return 0;
+  return ((M + bm[variant & 3] - 1) / bm[variant & 3]) * (Cout / bn[variant & 3]);
 }
 
 }  // extern "C"

@@ -103,6 +103,62 @@ def test_conv_fwd_bwd_wgrad_match_fp32(shape):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 256, 7, 7, 128, 3, 1), (3, 128, 6, 5, 256, 1, 1),
+                                   (2, 64, 9, 11, 64, 3, 1), (4, 128, 7, 7, 128, 3, 2)])
+def test_conv_split_k_matches_unsplit(shape):
+    """Split-K variants (in-kernel ticket reduction): fp32-close to the reference, bit-identical
+    run to run (slices summed in slice order whichever block arrives last), the same BatchNorm
+    partials / finished statistics and epilogue addend as the unsplit kernel."""
+    from arena_amd.ops.batchnorm import BatchNormAct2d
+    n, cin, h, w, cout, k, st = shape
+    pad = k // 2
+    x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=5)
+    ref = F.conv2d(x.float(), wt.float(), stride=st, padding=pad)
+    steps = cin * k * k // 64
+    for v in conv.variants_for(cout):
+        for ks in [s for s in conv.KSPLITS if s <= steps][:3]:
+            kv = conv.kvariant(v, ks)
+            assert conv.split_of(kv) == ks and conv.TILES[kv] == conv.TILES[v]
+            y = conv.conv2d_fwd(x, wt, st, pad, kv)
+            assert _rel(y, ref) < 1e-2, (v, ks, _rel(y, ref))
+            for _ in range(2):
+                assert torch.equal(conv.conv2d_fwd(x, wt, st, pad, kv), y)
+            # statistics epilogue on the summed tile: partials and finished (acc) statistics
+            y2, stats = conv.conv2d_fwd(x, wt, st, pad, kv, with_stats=True)
+            assert torch.equal(y2, y)
+            y3, fin = conv.conv2d_fwd(x, wt, st, pad, kv, with_stats=True, final=True)
+            assert torch.equal(y3, y)
+            bns = [BatchNormAct2d(cout).cuda() for _ in range(3)]
+            r = bns[0](y)
+            assert _rel(bns[1](y, stats=stats), r) < 1e-2
+            assert _rel(bns[2](y, stats=fin), r) < 1e-2
+            torch.testing.assert_close(bns[2].running_var, bns[0].running_var, rtol=1e-3,
+                                       atol=1e-5)
+    if st == 1:
+        dy = torch.randn(ref.shape, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        dx_ref = torch.ops.aten.convolution_backward(
+            dy.float(), x.float(), wt.float(), None, [1, 1], [pad, pad], [1, 1], False, [0, 0], 1,
+            [True, False, False])[0]
+        addend = torch.randn(x.shape, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        for v in conv.variants_for(cin):
+            kv = conv.kvariant(v, 2)
+            dxa = conv.conv2d_bwd_data(dy, wt, pad, kv, addend=addend)
+            assert _rel(dxa, dx_ref + addend.float()) < 1e-2, (v, _rel(dxa, dx_ref + addend.float()))
+
+
+def test_split_variants_for_only_underfilled_grids():
+    # 56x56 at batch 128: thousands of tiles, no split; 7x7 x 512 with K = 4608: splits offered
+    assert conv.split_variants_for(128 * 56 * 56, 64, 576) == []
+    sv = conv.split_variants_for(128 * 7 * 7, 512, 4608)
+    assert sv and all(conv.split_of(v) > 1 and v % 16 in conv.variants_for(512) for v in sv)
+    # every slice keeps at least 4 K steps
+    assert all(4608 // 64 // conv.split_of(v) >= 4 for v in sv)
+    assert conv.split_variants_for(128 * 7 * 7, 512, 256) == []
+
+
+@pytest.mark.gpu
 def test_conv_kernel_rejects_bad_shapes():
     from arena_amd.ops import _ext
     x, wt = _data(1, 32, 8, 8, 64, 3, "cuda")
