@@ -28,15 +28,17 @@ Tensor = torch.Tensor
 TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
 # + 4: three-stage K pipeline; + 8: single stage buffer, serial K loop, high occupancy
 TILES.update({v + d: t for v, t in list(TILES.items()) for d in (4, 8)})
+# 12 / 13: 256x128 / 256x64 tiles on 8 waves, two stage buffers; 14 / 15: three
+TILES.update({12: (256, 128), 13: (256, 64), 14: (256, 128), 15: (256, 64)})
 # + 16 * (k - 1): the same tile with its K steps split over k blocks (in-kernel ticket reduction,
 # bit-reproducible): for the layers whose tile count leaves CUs idle (14x14 / 7x7 at batch 128)
 KSPLITS = (2, 3, 4, 6, 8)
-TILES.update({v + 16 * (k - 1): TILES[v] for v in range(12) for k in KSPLITS})
+TILES.update({v + 16 * (k - 1): TILES[v] for v in range(16) for k in KSPLITS})
 _CUS = 256
 
 
 def kvariant(v: int, ks: int) -> int:
-    """Variant code of tile variant ``v`` (0..11) with its K steps split over ``ks`` blocks."""
+    """Variant code of tile variant ``v`` (0..15) with its K steps split over ``ks`` blocks."""
     return v + 16 * (ks - 1)
 
 
@@ -71,8 +73,8 @@ def split_variants_for(m: int, cout: int, ktot: int):
         return out
     steps = ktot // 64
     for v in variants_for(cout):
-        if v >= 4 and v < 8:
-            continue   # the three-stage pipeline needs long K loops: not a split candidate
+        if 4 <= v < 8 or v >= 14:
+            continue   # the three-stage pipelines need long K loops: not split candidates
         bm, bn = TILES[v]
         tiles = -(-m // bm) * (cout // bn)
         if tiles >= 2 * _CUS or tiles > 65536:
@@ -947,7 +949,7 @@ def _stem_plan(z: Tensor, w16: Tensor) -> Tuple[int, Tuple[int, int]]:
         return plan
     ext = _ext.load()
     ho, wo = z.shape[2], z.shape[3]
-    fvs = [v for v in variants_for(w16.shape[0]) if TILES[v][1] == 64]
+    fvs = [v for v in variants_for(w16.shape[0]) if TILES[v][1] == 64 and v < 12]   # c16: 4 waves
     wcs = [(3, 0), (7, 0)]
     if _mode() == "ours" or torch.cuda.is_current_stream_capturing():
         fv = pick_variant(z.shape[0] * ho * wo, w16.shape[0])

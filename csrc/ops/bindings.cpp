@@ -68,6 +68,7 @@ hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void
                              int, void*, unsigned*, hipStream_t);
 long long arena_conv_fwd_ksplit_floats(long long, int, int, int);
 long long arena_conv_fwd_tiles(long long, int, int);
+int arena_conv_fwd_tile_rows(int);
 hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
                                int, int, int, int, int, int, int, int, int, int, int, float,
                                hipStream_t);
@@ -87,7 +88,6 @@ long long arena_bn_lvl2_doubles(long long, int);
 void arena_bn_set_reduce_geometry(long long, long long);
 void arena_bn_set_fin_max_blocks(int);
 void arena_bn_set_nt(int);
-void arena_conv_set_wgrad_nt(int);
 // csrc/ops/pool_kernels.hip
 hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, int, int, int, int,
                              hipStream_t);
@@ -790,8 +790,9 @@ ConvSplit conv_split(const Tensor& x, int64_t variant, int64_t M, int64_t Cout, 
   TORCH_CHECK(variant >= 0, "conv: bad variant ", variant);
   s.base = (int)(variant % 16);
   s.ks = (int)(variant / 16) + 1;
-  TORCH_CHECK(s.base <= 11 && ((s.base & 1) || Cout % 128 == 0), "conv: variant ", variant,
-              " is not a tile variant for Cout = ", Cout);
+  TORCH_CHECK(s.base <= 15, "conv: variant ", variant, " is not a tile variant");
+  TORCH_CHECK((s.base & 1) || Cout % 128 == 0, "conv: variant ", variant,
+              " needs Cout % 128 == 0 (Cout = ", Cout, ")");
   if (s.ks > 1) {
     TORCH_CHECK(s.ks <= Ktot / 64, "conv: split-K ", s.ks, " exceeds the ", Ktot / 64,
                 " K steps");
@@ -1012,8 +1013,8 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
   const ConvSplit ks = conv_split(x, variant, N * Ho * Wo, Cout, R * S * C);
   Tensor y = torch::empty({N, Cout, Ho, Wo},
                           x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  static const int bm[4] = {128, 128, 64, 64};
-  const int64_t m_tiles = (N * Ho * Wo + bm[ks.base & 3] - 1) / bm[ks.base & 3];
+  const int rows = arena_conv_fwd_tile_rows(ks.base);
+  const int64_t m_tiles = (N * Ho * Wo + rows - 1) / rows;
   const bool fin = with_stats && stats_final;
   TORCH_CHECK(!fin || (!bn_x.has_value() && !addend.has_value() && Cout <= kAccC),
               "conv_fwd: stats_final is forward statistics without an addend");
@@ -1204,8 +1205,8 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
                     addend->is_contiguous(at::MemoryFormat::ChannelsLast),
                 "conv_fwd_ex: addend must be shaped like the output tensor");
   }
-  static const int bm[4] = {128, 128, 64, 64};
-  const int64_t m_tiles = (N * Ho * Wo + bm[ks.base & 3] - 1) / bm[ks.base & 3];
+  const int rows = arena_conv_fwd_tile_rows(ks.base);
+  const int64_t m_tiles = (N * Ho * Wo + rows - 1) / rows;
   TORCH_CHECK(!(with_stats && y_out.has_value()), "conv_fwd_ex: statistics need a dense output");
   const bool fin = with_stats && stats_final;
   TORCH_CHECK(!fin || (!addend.has_value() && Cout <= kAccC),
@@ -1552,7 +1553,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_set_fin_max_blocks", [](int64_t p) { arena_bn_set_fin_max_blocks((int)p); });
   m.def("bn_set_nt", [](int64_t on) { arena_bn_set_nt((int)on); });
   m.def("bn_set_acc", [](bool on) { g_bn_acc = on; });
-  m.def("conv_set_wgrad_nt", [](int64_t on) { arena_conv_set_wgrad_nt((int)on); });
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
     arena_bn_set_reduce_geometry(max_blocks, min_rounds);
   });

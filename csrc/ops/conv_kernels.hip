@@ -101,6 +101,7 @@ struct ConvArgs {
   int ksplit;
   float4* kws;
   unsigned* kcnt;
+  int xbytes, wbytes;  // buffer-descriptor ranges of x and w (both < 2^31 bytes, host-checked)
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -178,7 +179,7 @@ __device__ __forceinline__ float row16_sum(float v) {
 // restaged in LDS so that consecutive lanes add to consecutive channels: 64 fp64 adds = 512
 // contiguous bytes per wave instruction (scattered few-lane atomics cost one 64-B memory-side
 // request each). No wait and no fence: the kernel's end makes the sums visible to the finalize.
-template <int BM, int BN, typename Emit>
+template <int BM, int BN, int NT, typename Emit>
 __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int n0, int nrows,
                                                 Emit&& emit) {
   __shared__ float s_st[2][BN];
@@ -191,7 +192,7 @@ __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int n0, int n
   lds_barrier();
   double* acc = a.bn_acc + n0;
   const double n = (double)nrows;
-  for (int c = threadIdx.x; c < BN; c += kThreads) {
+  for (int c = threadIdx.x; c < BN; c += NT) {
     const double mu = (double)s_st[0][c];
     unsafeAtomicAdd(acc + c, n * mu);                                     // sum y
     unsafeAtomicAdd(acc + a.Cout + c, (double)s_st[1][c] + n * mu * mu);  // sum y^2
@@ -203,12 +204,25 @@ __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int n0, int n
 // with other blocks' epilogues -- those shapes are bound by the output write.
 // EPI: 0 = plain, 1 = BatchNorm statistics of Y (forward), 2 = BatchNorm-backward partials of Y
 // (see ConvArgs::bnx).
-template <int BM, int BN, int EPI, int NBUF = 2>
+// NWM x NWN waves (NT = 64 NWM NWN threads): 2 x 2 for the 128- and 64-wide tiles, 4 x 2 for the
+// 256-row tiles (per-wave 64 x BN/2), so a block's MFMA work per staged byte grows with the tile.
+//
+// C16 selects the staging form: false (every C % 64 shape) stages through buffer descriptors --
+// each glds slot's byte offset is fixed per block, a 64-deep K step moves only scalars (tap and
+// channel-block offsets, kept incrementally: no divisions in the loop), and a padded tap or a
+// row past M gets an out-of-range offset, which the descriptor's range check turns into zeros.
+// That leaves ~3 VALU per A slot per filter tap and none per weight slot, where the address
+// arithmetic of the flat form (a tap division, bounds checks and 64-bit addresses per slot per
+// step) issued ~115 VALU and ~140 SALU per K step against 16 MFMAs (the kernels were
+// issue-bound, not load-bound). C16 = true is the stem's space-to-depth form on flat loads.
+template <int BM, int BN, int EPI, int NBUF = 2, int NWM = 2, int NWN = 2, bool C16 = false>
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
-  constexpr int WM = BM / 2, WN = BN / 2;        // per-wave output tile (2 x 2 waves)
+  constexpr int NT = 64 * NWM * NWN;
+  constexpr int WM = BM / NWM, WN = BN / NWN;    // per-wave output tile
   constexpr int MI = WM / 16, NI = WN / 16;      // 16x16 MFMA tiles per wave
-  constexpr int AI = BM * 8 / kThreads;          // A staging instructions per thread
-  constexpr int BI = BN * 8 / kThreads;
+  constexpr int AI = BM * 8 / NT;                // A staging instructions per thread
+  constexpr int BI = BN * 8 / NT;
+  static_assert(AI >= 1 && BI >= 1 && MI >= 1 && NI >= 1, "tile too small for the wave grid");
   constexpr int kBufBytes = (BM + BN) * kRowBytes;
   __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBufBytes];
 
@@ -254,16 +268,88 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     const int row = (wave * BI + i) * 8 + (lane >> 3);
     b_src[i] = a.w + (size_t)(n0 + row) * a.Ktot + (pos ^ swz(row)) * 8;
   }
-  const int CB = a.c16 ? 1 : a.C / kBK;  // 64-channel blocks per tap
+  const int CB = C16 ? 1 : a.C / kBK;  // 64-channel blocks per tap
   // this block's K steps: [t0, t0 + T) of the Ktot / kBK (split-K: slice `slice` of ks)
   const int Tall = a.Ktot / kBK;
   const int t0 = (int)((long long)Tall * slice / ks);
   const int T = (int)((long long)Tall * (slice + 1) / ks) - t0;
 
+  // ---- descriptor staging state (C16 == false) ----
+  constexpr uint32_t kOOB = 0x80000000u;   // >= num_records: the load returns zeros
+  const __amdgpu_buffer_rsrc_t xrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+  int a_lane[AI];          // byte offset of the slot's 16-byte chunk at tap (0, 0), channel block 0
+  uint32_t a_mask[AI];     // bit r*S+s: tap (r, s) inside the image for this slot's pixel
+  uint32_t a_cur[AI];      // the current tap's offset, or kOOB
+  uint32_t b_voff[BI];
+  int s_tap = 0, s_cb = 0, s_s = 0, s_tapoff = 0, s_t = t0;   // scalar K-step state
+  if constexpr (!C16) {
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int row = (wave * AI + i) * 8 + (lane >> 3);
+      uint32_t mk = 0u;
+      int off = 0;
+      if (a_hb[i] > -(1 << 27)) {
+        for (int r = 0; r < a.R; ++r) {
+          if ((unsigned)(a_hb[i] + r) >= (unsigned)a.H) continue;
+          for (int s2 = 0; s2 < a.S; ++s2)
+            if ((unsigned)(a_wb[i] + s2) < (unsigned)a.W) mk |= 1u << (r * a.S + s2);
+        }
+        off = (((a_nb[i] + a_hb[i]) * a.W + a_wb[i]) * a.C + a_chunk[i] * 8) * 2;
+      }
+      (void)row;
+      a_lane[i] = off;
+      a_mask[i] = mk;
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = (wave * BI + i) * 8 + (lane >> 3);
+      b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
+    }
+    s_tap = t0 / CB;
+    s_cb = t0 - s_tap * CB;
+    const int r0 = s_tap / a.S;
+    s_s = s_tap - r0 * a.S;
+    s_tapoff = (r0 * a.W + s_s) * a.C * 2;
+#pragma unroll
+    for (int i = 0; i < AI; ++i)
+      a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
+  }
+
   auto stage = [&](int tl, int buf) {
     const int t = t0 + tl;
     uint8_t* base = lds + buf * kBufBytes;
-    if (a.c16) {
+    if constexpr (!C16) {
+      (void)t;
+      const int coff = s_cb * kRowBytes;   // channel block within the tap (scalar)
+#pragma unroll
+      for (int i = 0; i < AI; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_ptr_t)(base + (wave * AI + i) * 64 * 16),
+                                                 16, a_cur[i], coff, 0, 0);
+      uint8_t* bb = base + BM * kRowBytes;
+#pragma unroll
+      for (int i = 0; i < BI; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
+                                                 16, b_voff[i], s_t * kRowBytes, 0, 0);
+      // advance the scalar state to the next K step
+      ++s_t;
+      if (++s_cb == CB) {
+        s_cb = 0;
+        ++s_tap;
+        s_tapoff += a.C * 2;
+        if (++s_s == a.S) {
+          s_s = 0;
+          s_tapoff += (a.W - a.S) * a.C * 2;
+        }
+#pragma unroll
+        for (int i = 0; i < AI; ++i)
+          a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
+      }
+      return;
+    }
+    if (C16) {
       // K step t = filter row r, columns 4*sb .. 4*sb+3; 16-byte chunk c = pixel c/2, half c%2
       const int SB = a.S >> 2;
       const int r = t / SB, sb = t - r * SB;
@@ -294,6 +380,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
 #pragma unroll
     for (int i = 0; i < BI; ++i) glds16(b_src[i] + (size_t)t * kBK, bbase + (wave * BI + i) * 64 * 16);
   };
+  (void)a_cur;
 
   f32x4v acc[MI][NI];
 #pragma unroll
@@ -301,7 +388,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
 #pragma unroll
     for (int j = 0; j < NI; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
 
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / NWN, wn = wave % NWN;
   const int fr = lane & 15, fq = lane >> 4;
 
   auto compute = [&](int buf) {
@@ -378,12 +465,12 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
   if (ks > 1) {
     // ---- split-K hand-off (cdna_hip_programming.md §5 "In-launch split-K reduction") ----
     constexpr int NA = MI * NI;
-    float4* slab = a.kws + (size_t)tile * ks * NA * kThreads;
+    float4* slab = a.kws + (size_t)tile * ks * NA * NT;
 #pragma unroll
     for (int i = 0; i < MI; ++i)
 #pragma unroll
       for (int j = 0; j < NI; ++j)
-        slab[((size_t)slice * NA + i * NI + j) * kThreads + tid] =
+        slab[((size_t)slice * NA + i * NI + j) * NT + tid] =
             make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -413,13 +500,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     for (int i = 0; i < MI; ++i) {
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        const float4 v = slab[(size_t)(i * NI + j) * kThreads + tid];
+        const float4 v = slab[(size_t)(i * NI + j) * NT + tid];
         acc[i][j] = f32x4v{v.x, v.y, v.z, v.w};
       }
       for (int s = 1; s < ks; ++s) {
         float4 v[NI];
 #pragma unroll
-        for (int j = 0; j < NI; ++j) v[j] = slab[((size_t)s * NA + i * NI + j) * kThreads + tid];
+        for (int j = 0; j < NI; ++j) v[j] = slab[((size_t)s * NA + i * NI + j) * NT + tid];
 #pragma unroll
         for (int j = 0; j < NI; ++j) acc[i][j] += f32x4v{v[j].x, v[j].y, v[j].z, v[j].w};
       }
@@ -468,7 +555,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     constexpr int F4R = BN / 4;   // float4 slots per staged row (>= 16: the XOR below stays inside)
     constexpr int CPR = BN / 8;   // 16-byte bf16 output chunks per row
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
+    for (int h = 0; h < NWM; ++h) {
       if (h) lds_barrier();       // every reader of the first half is done
       if (wm == h) {
 #pragma unroll
@@ -482,7 +569,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         }
       }
       lds_barrier();              // the staged half is complete (global stores may be in flight)
-      for (int q = tid; q < WM * CPR; q += kThreads) {
+      for (int q = tid; q < WM * CPR; q += NT) {
         const int row = q / CPR, cc = q - row * CPR;
         const int m = m0 + h * WM + row;
         if (m >= a.M) continue;
@@ -587,7 +674,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     // per channel over the tile's valid rows: sum g, sum g * (x - mean), g = stored dY * mask.
     // Per element: the stored (bf16-rounded) value via one v_cvt_pk_bf16_f32 per pair, the mask
     // select (rows past M were cleared from the mask bits at load), packed fp32 sums.
-    float* red = reinterpret_cast<float*>(lds);   // [2 (wm)][2][BN]
+    float* red = reinterpret_cast<float*>(lds);   // [NWM][2][BN]
     float s1[NI][4], s2[NI][4];
 #pragma unroll
     for (int j = 0; j < NI; ++j) {
@@ -634,8 +721,14 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = wn * WN + j * 16 + 4 * fq + r;
-          a.part[(size_t)mt * 2 * a.Cout + n0 + c] = red[c] + red[2 * BN + c];
-          a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = red[BN + c] + red[3 * BN + c];
+          float r1 = red[c], r2 = red[BN + c];
+#pragma unroll
+          for (int h = 1; h < NWM; ++h) {
+            r1 += red[h * 2 * BN + c];
+            r2 += red[h * 2 * BN + BN + c];
+          }
+          a.part[(size_t)mt * 2 * a.Cout + n0 + c] = r1;
+          a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = r2;
         }
     }
   }
@@ -650,7 +743,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     // batch 128: 94 -> 85 us; profiles/r2_conv_epi_{before,after}.jsonl).
     const int nrows = min(BM, a.M - m0);
     const bool full = nrows == BM;
-    float* red = reinterpret_cast<float*>(lds);   // [2 (wm)][BN]
+    float* red = reinterpret_cast<float*>(lds);   // [NWM][BN]
     float mean[NI][4], s[NI][4];
     auto exchange = [&](bool first) {   // s (row-16 sums of this wave) -> per-block channel sums
       if (!first) lds_barrier();        // every wave has read the previous sums
@@ -666,7 +759,10 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int c = wn * WN + j * 16 + 4 * fq + r;
-          s[j][r] = red[c] + red[BN + c];
+          float v = red[c];
+#pragma unroll
+          for (int h = 1; h < NWM; ++h) v += red[h * BN + c];
+          s[j][r] = v;
         }
     };
 #pragma unroll
@@ -717,7 +813,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
           }
       }
     } else {
-      bn_acc_epilogue<BM, BN>(a, n0, nrows, [&](auto&& add) {
+      bn_acc_epilogue<BM, BN, NT>(a, n0, nrows, [&](auto&& add) {
         if (wm == 0 && fr == 0) {
 #pragma unroll
           for (int j = 0; j < NI; ++j)
@@ -729,22 +825,56 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
   }
 }
 
-template <int BM, int BN, int EPI, int NBUF>
+template <int BM, int BN, int EPI, int NBUF, bool C16>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
-  conv_fwd_body<BM, BN, EPI, NBUF>(a);
+#if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
+  conv_fwd_body<BM, BN, EPI, NBUF, 2, 2, C16>(a);
+#endif
 }
 
 // Single stage buffer (one K step -- 1x1 over 64 channels -- or the serial variants 8..11): the
 // shapes that want it are bound by streaming the output, so it trades registers for occupancy --
 // four waves per SIMD (<= 128 VGPRs) instead of two, up to five blocks per CU by LDS.
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, bool C16>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 void conv_fwd_kernel_occ4(ConvArgs a) {
-  conv_fwd_body<BM, BN, EPI, 1>(a);
+#if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
+  conv_fwd_body<BM, BN, EPI, 1, 2, 2, C16>(a);
+#endif
+}
+
+// 256-row tiles on 8 waves (4 x 2, per-wave 64 x BN/2): twice the MFMA work of a 128-row tile per
+// staged weight byte, 2 waves per SIMD at one block per CU (96 KB of LDS double-buffered, 144 KB
+// triple-buffered at BN = 128).
+template <int BM, int BN, int EPI, int NBUF>
+__global__ __launch_bounds__(512) void conv_fwd_kernel_w8(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
+  conv_fwd_body<BM, BN, EPI, NBUF, 4, 2>(a);
+#endif
 }
 
 template <int BM, int BN>
-hipError_t launch(const ConvArgs& a0, int pipe, hipStream_t st) {
+hipError_t launch_w8(const ConvArgs& a0, int nb, hipStream_t st) {
+  ConvArgs a = a0;
+  if (a.c16) return hipErrorInvalidValue;
+  a.m_tiles = (a.M + BM - 1) / BM;
+  a.n_tiles = a.Cout / BN;
+  const int nwg = a.m_tiles * a.n_tiles * a.ksplit;
+  if (a.Ktot == kBK) nb = 1;
+  const int epi = (a.part == nullptr && a.bn_acc == nullptr) ? 0 : (a.bnx != nullptr ? 2 : 1);
+#define ARENA_CONV_W8(E) \
+  do { if (nb == 1) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 1>), dim3(nwg), dim3(512), 0, st, a); \
+       else if (nb == 2) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 2>), dim3(nwg), dim3(512), 0, st, a); \
+       else hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 3>), dim3(nwg), dim3(512), 0, st, a); } while (0)
+  if (epi == 0) ARENA_CONV_W8(0);
+  else if (epi == 1) ARENA_CONV_W8(1);
+  else ARENA_CONV_W8(2);
+#undef ARENA_CONV_W8
+  return hipGetLastError();
+}
+
+template <int BM, int BN, bool C16>
+hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
   ConvArgs a = a0;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
@@ -754,19 +884,30 @@ hipError_t launch(const ConvArgs& a0, int pipe, hipStream_t st) {
   const int nb = a.Ktot == kBK || pipe == 2 ? 1 : (pipe == 1 ? 3 : 2);
   const int epi = (a.part == nullptr && a.bn_acc == nullptr) ? 0 : (a.bnx != nullptr ? 2 : 1);
 #define ARENA_CONV_LAUNCH(E, NB) \
-  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, E, NB>), dim3(nwg), dim3(kThreads), 0, st, a)
+  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, E, NB, C16>), dim3(nwg), dim3(kThreads), 0, st, a)
 #define ARENA_CONV_NB(E) \
   do { if (nb == 1 && (E == 0 || BM * BN < 128 * 128)) /* fits 128 VGPRs without spills */ \
-         hipLaunchKernelGGL((conv_fwd_kernel_occ4<BM, BN, E>), dim3(nwg), dim3(kThreads), 0, st, a); \
+         hipLaunchKernelGGL((conv_fwd_kernel_occ4<BM, BN, E, C16>), dim3(nwg), dim3(kThreads), 0, st, a); \
        else if (nb == 1) ARENA_CONV_LAUNCH(E, 1); \
        else if (nb == 2) ARENA_CONV_LAUNCH(E, 2); \
        else ARENA_CONV_LAUNCH(E, 3); } while (0)
   if (epi == 0) ARENA_CONV_NB(0);
   else if (epi == 1) ARENA_CONV_NB(1);
-  else ARENA_CONV_NB(2);
+  else if constexpr (!C16) ARENA_CONV_NB(2);
+  else return hipErrorInvalidValue;
 #undef ARENA_CONV_NB
 #undef ARENA_CONV_LAUNCH
   return hipGetLastError();
+}
+
+// the stem's c16 form only exists for 64-wide tiles (its Cout is 64)
+template <int BM, int BN>
+hipError_t launch(const ConvArgs& a, int pipe, hipStream_t st) {
+  if (a.c16) {
+    if constexpr (BN == 64) return launch_t<BM, BN, true>(a, pipe, st);
+    else return hipErrorInvalidValue;
+  }
+  return launch_t<BM, BN, false>(a, pipe, st);
 }
 
 }  // namespace
@@ -778,6 +919,7 @@ extern "C" {
 // variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (BM x BN output tile per block);
 // variant + 4: the same tile with a three-stage K pipeline (two glds steps in flight);
 // variant + 8: one stage buffer, serial K loop, high occupancy (streaming-bound 1x1 shapes).
+// 12 / 13: 256x128 / 256x64 on 8 waves, two stage buffers; 14 / 15: the same, three.
 // part (optional): BatchNorm partials of y, [ceil(M / BM)][2][Cout] (EPI 1 / EPI 2 epilogues).
 // General form. pad_h/pad_w: top/left padding; Ho/Wo: output size (<= 0: derived from a symmetric
 // padding); y_map {Hy, Wy, osh, osw, ooh, oow, fill_sib} (null: dense output); c16, fill_sib:
@@ -841,7 +983,13 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   if (M >= (1LL << 31) || (long long)N * H * W * C >= (1LL << 40)) return hipErrorInvalidValue;
   a.M = (int)M;
   a.Ktot = R * S * C;
-  if (variant < 0 || variant > 11) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 15) return hipErrorInvalidValue;
+  if (!c16) {   // descriptor staging: 31-bit byte offsets, a 32-bit tap mask
+    const long long xb = (long long)N * H * W * C * 2, wb = (long long)Cout * a.Ktot * 2;
+    if (xb >= (1LL << 31) || wb >= (1LL << 31) || R * S > 32) return hipErrorInvalidValue;
+    a.xbytes = (int)xb;
+    a.wbytes = (int)wb;
+  }
   // split-K: every slice gets at least one K step; the caller sized kws with
   // arena_conv_fwd_ksplit_floats and zeroed kcnt once (the kernel re-zeroes what it uses)
   if (ksplit < 1 || ksplit > a.Ktot / kBK || (ksplit > 1 && (kws == nullptr || kcnt == nullptr)))
@@ -849,6 +997,12 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.ksplit = ksplit;
   a.kws = (float4*)kws;
   a.kcnt = kcnt;
+  if (variant >= 12) {   // 256-row tiles, 8 waves: 12/13 two stage buffers, 14/15 three
+    const int nb = variant >= 14 ? 3 : 2;
+    if ((variant & 1) == 0)
+      return Cout % 128 ? hipErrorInvalidValue : launch_w8<256, 128>(a, nb, st);
+    return launch_w8<256, 64>(a, nb, st);
+  }
   const int pipe = variant >> 2;
   switch (variant & 3) {
     case 0: return Cout % 128 ? hipErrorInvalidValue : launch<128, 128>(a, pipe, st);
@@ -869,17 +1023,35 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
 }
 
 // Split-K workspace of one launch, in floats (0 when ksplit == 1), and its ticket count (tiles).
+static void conv_tile(int variant, int* bm, int* bn) {
+  static const int tm[4] = {128, 128, 64, 64}, tn[4] = {128, 64, 128, 64};
+  if (variant >= 12) {
+    *bm = 256;
+    *bn = (variant & 1) ? 64 : 128;
+  } else {
+    *bm = tm[variant & 3];
+    *bn = tn[variant & 3];
+  }
+}
+
 long long arena_conv_fwd_ksplit_floats(long long M, int Cout, int variant, int ksplit) {
-  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (ksplit <= 1 || variant < 0 || variant > 11) return 0;
-  const long long tiles = ((M + bm[variant & 3] - 1) / bm[variant & 3]) * (Cout / bn[variant & 3]);
-  return tiles * ksplit * bm[variant & 3] * bn[variant & 3];
+  if (ksplit <= 1 || variant < 0 || variant > 15) return 0;
+  int bm, bn;
+  conv_tile(variant, &bm, &bn);
+  return ((M + bm - 1) / bm) * (Cout / bn) * ksplit * bm * bn;
 }
 
 long long arena_conv_fwd_tiles(long long M, int Cout, int variant) {
-  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (variant < 0 || variant > 11) return 0;
-  return ((M + bm[variant & 3] - 1) / bm[variant & 3]) * (Cout / bn[variant & 3]);
+  if (variant < 0 || variant > 15) return 0;
+  int bm, bn;
+  conv_tile(variant, &bm, &bn);
+  return ((M + bm - 1) / bm) * (Cout / bn);
+}
+
+int arena_conv_fwd_tile_rows(int variant) {
+  int bm, bn;
+  conv_tile(variant, &bm, &bn);
+  return bm;
 }
 
 }  // extern "C"
@@ -1243,7 +1415,8 @@ struct WgradArgs {
   FastDiv div_hw, div_w;
   int pad_w;           // left padding (pad is the top one)
   int c16;             // C == 16, a BN = 64 column tile = one filter row x 4 columns x 16 channels
-  int nt;              // stage dY and X with the non-temporal policy (this pass is their last read)
+  int xbytes, dybytes; // buffer-descriptor ranges (both < 2^31 bytes, host-checked)
+  int aff;             // 1x1, stride 1, no padding: X pixel m is output pixel m (affine staging)
 };
 
 // chunk permutation of a pixel row of RB bytes (bit 0 of the chunk index is kept: 32-B pairs)
@@ -1296,25 +1469,54 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
   const int a_row_l = lane / CA, a_pos = lane % CA;
   const int b_row_l = lane / CB, b_pos = lane % CB;
 
+  // Staging through buffer descriptors (see conv_fwd_body): a dY row is affine in the pixel
+  // index, so its slot offset is fixed and the step moves the scalar soffset; rows past M get an
+  // out-of-range offset (zeros). X rows are affine too for 1x1 stride-1 unpadded convolutions
+  // (a.aff); otherwise the pixel is decomposed per slot and padded taps go out of range.
+  constexpr uint32_t kOOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t dyr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dybytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  uint32_t a_voff[AI], b_voff[BI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (wave * AI + i) * RPI_A + a_row_l;
+    a_voff[i] = (uint32_t)((row * a.Cout + co0 + (a_pos ^ wswz<RA>(row)) * 8) * 2);
+  }
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = (wave * BI + i) * RPI_B + b_row_l;
+    b_voff[i] = (uint32_t)((row * a.C + ci0 + (b_pos ^ wswz<RBB>(row)) * 8) * 2);
+  }
+
   auto stage = [&](int step, int buf) {
     uint8_t* base = lds + buf * kBuf;
     const int p0 = (step0 + step) * kPix;
+    const bool full = p0 + kPix <= a.M;   // no row of this step is past M (uniform)
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int row = (wave * AI + i) * RPI_A + a_row_l;
-      const int m = p0 + row;
-      const void* src = m < a.M ? (const void*)(a.dy + (size_t)m * a.Cout + co0 +
-                                                (a_pos ^ wswz<RA>(row)) * 8)
-                                : (const void*)g_zero_page;
-      if (a.nt) glds16nt(src, base + (wave * AI + i) * 1024);
-      else glds16(src, base + (wave * AI + i) * 1024);
+      const uint32_t vo = (full || p0 + row < a.M) ? a_voff[i] : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (lds_ptr_t)(base + (wave * AI + i) * 1024), 16,
+                                               vo, p0 * a.Cout * 2, 0, 0);
     }
     uint8_t* bb = base + kPix * RA;
+    if (a.aff) {
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        const int row = (wave * BI + i) * RPI_B + b_row_l;
+        const uint32_t vo = (full || p0 + row < a.M) ? b_voff[i] : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(bb + (wave * BI + i) * 1024), 16,
+                                                 vo, p0 * a.C * 2, 0, 0);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int row = (wave * BI + i) * RPI_B + b_row_l;
       const int m = p0 + row;
-      const void* src = (const void*)g_zero_page;
+      uint32_t vo = kOOB;
       if (m < a.M) {
         const int n = (int)fdiv((uint32_t)m, a.div_hw);
         const int rem = m - n * a.Ho * a.Wo;
@@ -1324,13 +1526,11 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
         const int hi = ho * a.stride - a.pad + rr;
         const int wi = wo * a.stride - a.pad_w + ss + (a.c16 ? (cch >> 1) : 0);
         if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
-          src = a.c16 ? (const void*)(a.x + ((size_t)(n * a.H + hi) * a.W + wi) * 16 +
-                                      (cch & 1) * 8)
-                      : (const void*)(a.x + ((size_t)(n * a.H + hi) * a.W + wi) * a.C + ci0 +
-                                      cch * 8);
+          vo = a.c16 ? (uint32_t)((((n * a.H + hi) * a.W + wi) * 16 + (cch & 1) * 8) * 2)
+                     : (uint32_t)((((n * a.H + hi) * a.W + wi) * a.C + ci0 + cch * 8) * 2);
       }
-      if (a.nt) glds16nt(src, bb + (wave * BI + i) * 1024);
-      else glds16(src, bb + (wave * BI + i) * 1024);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(bb + (wave * BI + i) * 1024), 16, vo,
+                                               0, 0, 0);
     }
   };
 
@@ -1407,13 +1607,17 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
 
 template <int BM, int BN>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
   conv_wgrad_body<BM, BN, 2>(a);
+#endif
 }
 
 template <int BM, int BN>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 void conv_wgrad_kernel_occ4(WgradArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
   conv_wgrad_body<BM, BN, 1>(a);
+#endif
 }
 
 // out = sum over splits of ws, bf16 and/or fp32. Thread (col, grp) of a block sums float4 column
@@ -1497,11 +1701,9 @@ hipError_t launch_wgrad(WgradArgs a, int splits_hint, bool serial, hipStream_t s
 
 }  // namespace
 
-int g_wgrad_nt = 0;   // non-temporal staging in the wgrad kernel (runtime switch for A/Bs)
 
 extern "C" {
 
-void arena_conv_set_wgrad_nt(int on) { g_wgrad_nt = on ? 1 : 0; }
 
 // Number of split slabs the wgrad launch will use (the caller sizes the workspace with it).
 int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int variant,
@@ -1537,7 +1739,17 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
   a.ws = ws;
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;
   a.stride = stride; a.pad = pad_h; a.pad_w = pad_w; a.c16 = c16;
-  a.nt = g_wgrad_nt;
+  {
+    const long long xb = (long long)N * H * W * C * 2;
+    const long long Ho_ = Ho > 0 ? Ho : (H + 2 * pad_h - R) / stride + 1;
+    const long long Wo_ = Wo > 0 ? Wo : (W + 2 * pad_w - S) / stride + 1;
+    const long long db = (long long)N * Ho_ * Wo_ * Cout * 2;
+    if (xb >= (1LL << 31) || db >= (1LL << 31)) return hipErrorInvalidValue;
+    a.xbytes = (int)xb;
+    a.dybytes = (int)db;
+    a.aff = (!c16 && R == 1 && S == 1 && stride == 1 && pad_h == 0 && pad_w == 0 &&
+             Ho_ == H && Wo_ == W) ? 1 : 0;
+  }
   a.Ho = Ho > 0 ? Ho : (H + 2 * pad_h - R) / stride + 1;
   a.Wo = Wo > 0 ? Wo : (W + 2 * pad_w - S) / stride + 1;
   if (a.Ho <= 0 || a.Wo <= 0) return hipErrorInvalidValue;

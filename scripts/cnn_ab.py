@@ -59,7 +59,6 @@ def main():
         from arena_amd.ops import _ext as _e
         _e.load().bn_set_fin_max_blocks(finp[0] if finp else 64)
         _e.load().bn_set_nt(0 if "bnnt0" in opt_s.split("+") else 1)   # BN non-temporal loads
-        _e.load().conv_set_wgrad_nt(1 if "wgnt" in opt_s.split("+") else 0)
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
             cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
