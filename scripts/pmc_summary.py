@@ -25,14 +25,31 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--top", type=int, default=30)
     ap.add_argument("--width", type=int, default=90)
+    ap.add_argument("--last-frac", type=float, default=1.0,
+                    help="only the dispatches in the last fraction of the run (by dispatch id): "
+                         "drops autotuning and warmup from a steady-state summary")
     a = ap.parse_args()
     cc = glob.glob(os.path.join(a.dir, "**", "*counter_collection.csv"), recursive=True)
     kt = glob.glob(os.path.join(a.dir, "**", "*kernel_trace.csv"), recursive=True)
     counters = defaultdict(lambda: defaultdict(float))
     names = set()
+
+    def cut_of(files):
+        ids = []
+        for f in files:
+            with open(f, newline="") as fh:
+                ids += [int(r["Dispatch_Id"]) for r in csv.DictReader(fh) if r.get("Dispatch_Id")]
+        if not ids or a.last_frac >= 1.0:
+            return -1
+        ids = sorted(set(ids))
+        return ids[int(len(ids) * (1.0 - a.last_frac))]
+
+    cut_c, cut_k = cut_of(cc), cut_of(kt)
     for f in cc:
         with open(f, newline="") as fh:
             for row in csv.DictReader(fh):
+                if cut_c >= 0 and int(row.get("Dispatch_Id") or 0) < cut_c:
+                    continue
                 k = row.get("Kernel_Name", "?")[: a.width]
                 counters[k][row["Counter_Name"]] += float(row["Counter_Value"])
                 names.add(row["Counter_Name"])
@@ -41,6 +58,8 @@ def main():
     for f in kt:
         with open(f, newline="") as fh:
             for row in csv.DictReader(fh):
+                if cut_k >= 0 and int(row.get("Dispatch_Id") or 0) < cut_k:
+                    continue
                 k = row.get("Kernel_Name", "?")[: a.width]
                 time_ns[k] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
                 calls[k] += 1
