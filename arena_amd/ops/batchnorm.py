@@ -5,13 +5,17 @@ and apply ReLU: ``y = relu(bn(x) + residual)``. That is the whole tail of a ResN
 one module. On an MI355X, with a channels_last bf16/fp32 input and a supported channel count,
 it runs the HIP kernels in ``csrc/ops/bn_kernels.hip``:
 
-* forward: 2 launches (statistics, then apply + ReLU mask bits); the statistics come finished
-  from the producing convolution's epilogue when it ran on the MFMA kernel (then 1 launch).
+* forward: 2 launches (statistics, then apply + ReLU mask bits); the statistics come from the
+  producing convolution's epilogue when it ran on the MFMA kernel (then 1 launch).
   The statistics pass and the conv epilogue accumulate fp64 sums with fire-and-forget
-  memory-side atomics; a one-thread-per-channel finalize turns them into the coefficients
-  (instead of a two-level merge of up to 3136 per-tile partials per channel);
-* backward: 2 launches (reductions, then dx and the residual gradient) plus the same small
-  finalize.
+  memory-side atomics, and the apply pass derives its coefficients from those sums itself: no
+  finalize launch between them (it used to merge up to 3136 per-tile partials per channel);
+* backward: 2 launches (reduction into this layer's own fp64 sums, then dx and the residual
+  gradient, which derives its coefficients from the sums).
+
+The sums are zeroed by a later kernel of the same layer instead of a launch of their own: the
+forward's by the backward dx pass, the backward's (``_BwdAcc``, one set per module) by the
+next forward's apply pass.
 
 Otherwise it runs the same math as stock PyTorch ops. That includes CPU tensors, which serve as
 the reference.
@@ -59,9 +63,9 @@ class FinishedStats:
     """Batch statistics of a conv output accumulated inside the conv kernel: the fp64 [2, C]
     accumulator set (sum y, sum y^2) its epilogue added into with memory-side atomics
     (``conv2d_fwd(..., with_stats=True, final=True)``). The BN layer consuming it skips its
-    statistics pass; its one-thread-per-channel finalize reads the sums and zeroes the set, which
-    returns to a rotating pool. Statistics obtained this way must reach a BN layer, or be
-    ``discard()``ed (zeroed), before the pool comes round again."""
+    statistics pass; its apply pass derives the coefficients from the sums, and its backward dx
+    pass zeroes the set, which returns to a rotating pool (a set whose backward never ran is
+    zeroed on the stream before the pool hands it out again)."""
     __slots__ = ("fin",)
 
     def __init__(self, fin: torch.Tensor):
@@ -92,21 +96,61 @@ class ResidualMask:
         return m
 
 
+_FIN_BWD = True
+
+
+def set_fin_bwd(on: bool) -> None:
+    """A/B switch: backward sums in the layer's own set, coefficients derived in the dx pass (on,
+    default) or a pool set and a finalize launch (off)."""
+    global _FIN_BWD
+    _FIN_BWD = bool(on)
+
+
+class _BwdAcc:
+    """A BN layer's own fp64 [2, C] backward sums (``bn_bwd(acc_b=...)``). The backward's dx pass
+    leaves them in place; the layer's next forward apply pass zeroes them (``bn_fwd(zero_b=...)``).
+    ``dirty`` tracks that on the host: a backward that finds the set still dirty (no forward ran in
+    between) zeroes it first. One set per module keeps captured graphs valid: every replay's
+    forward zeroes the set its previous replay's backward filled."""
+    __slots__ = ("t", "dirty")
+
+    def __init__(self):
+        self.t, self.dirty = None, False
+
+    def take_zero(self):
+        """The set for the forward apply pass to zero, or None."""
+        if self.t is None or not self.dirty:
+            return None
+        self.dirty = False
+        return self.t
+
+    def for_backward(self, like: torch.Tensor, c: int) -> torch.Tensor:
+        if self.t is None or self.t.device != like.device or self.t.numel() != 2 * c:
+            self.t = torch.zeros(2 * c, dtype=torch.float64, device=like.device)
+        elif self.dirty:
+            self.t.zero_()
+        self.dirty = True
+        return self.t
+
+
 class _BNActFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, residual, weight, bias, running_mean, running_var, training, momentum,
                 eps, relu, num_batches=None, stats=None, join=None, link=None, res_out=None,
-                res_in=None):
+                res_in=None, bacc=None):
         ext = _ext.load()
         part, rpb, fin = None, 0, None
         if stats is not None and training:
             if isinstance(stats, FinishedStats):
-                fin = stats.fin       # finished by the conv epilogue: apply only
+                fin = stats.fin       # summed by the conv epilogue: apply only
             else:
                 part, rpb = stats
-        y, mean, invstd, mask = ext.bn_fwd(x, residual, weight, bias, running_mean, running_var,
-                                           training, momentum, eps, relu, num_batches, part, rpb,
-                                           fin)
+        y, mean, invstd, mask, facc = ext.bn_fwd(
+            x, residual, weight, bias, running_mean, running_var, training, momentum, eps, relu,
+            num_batches, part, rpb, fin, zero_b=bacc.take_zero() if bacc is not None else None)
+        # the statistics sums stay in place until this layer's backward dx pass zeroes them
+        ctx.facc = facc if (facc is not None and facc.numel() > 0) else None
+        ctx.bacc = bacc
         # the ReLU mask is kept as bits (M*C/8 bytes), not as a reference to y
         ctx.save_for_backward(x, mask if relu and training else None, mean, invstd, weight)
         ctx.relu, ctx.has_res, ctx.training = relu, residual is not None, training
@@ -148,10 +192,13 @@ class _BNActFn(torch.autograd.Function):
                   and ctx.join.other() is None and ctx.join.peer_takes_masked())
         to_res = (not masked and ctx.res_out is not None and ctx.has_res and mask is not None
                   and ctx.needs_input_grad[1] and ctx.join is None)
+        acc_b = ctx.bacc.for_backward(x, x.shape[1]) \
+            if (ctx.bacc is not None and not ext and _FIN_BWD) else None
         dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, mask, x, mean, invstd, weight, relu,
                                                      ctx.has_res and not masked and not to_res,
                                                      ctx.affine, ext[0] if ext else None,
-                                                     ext[1] if ext else 0)
+                                                     ext[1] if ext else 0, acc_b=acc_b,
+                                                     zero_f=ctx.facc)
         if to_res:
             ctx.res_out.publish(mask)
             dres = dy
@@ -169,7 +216,7 @@ class _BNActFn(torch.autograd.Function):
                 dres = None
         return (dx, dres, dgamma if ctx.affine else None,
                 dbeta if ctx.affine else None, None, None, None, None, None, None, None, None,
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 def bn_act(x, residual=None, weight=None, bias=None, running_mean=None, running_var=None,
@@ -190,6 +237,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
         if act not in ("relu", "none"):
             raise ValueError(f"act must be 'relu' or 'none', got {act!r}")
         self.relu = act == "relu"
+        self._bacc = _BwdAcc()
 
     def forward(self, x: torch.Tensor, residual: Optional[torch.Tensor] = None,
                 stats=None, join=None, link=None, res_out=None, res_in=None) -> torch.Tensor:
@@ -210,7 +258,7 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, True,
                                   self.momentum, self.eps, self.relu,
                                   self.num_batches_tracked if tracking else None, stats, join,
-                                  link, res_out, res_in)
+                                  link, res_out, res_in, self._bacc)
         if tracking:
             self.num_batches_tracked.add_(1)
         mom = self.momentum if self.momentum is not None else \
@@ -220,4 +268,5 @@ class BatchNormAct2d(nn.BatchNorm2d):
             return reference(x, residual, self.weight, self.bias, rm, rv, training, mom,
                              self.eps, self.relu)
         return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, training, mom,
-                              self.eps, self.relu, None, None, join, link, res_out, res_in)
+                              self.eps, self.relu, None, None, join, link, res_out, res_in,
+                              self._bacc)

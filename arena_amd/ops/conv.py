@@ -174,15 +174,22 @@ def set_bn_links(on: bool) -> None:
     _BN_LINKS = bool(on)
 
 
-# BatchNorm statistics finished inside the conv kernel (fp64 atomics + last-tile ticket) instead
-# of per-tile partials plus a finalize launch in the BN layer (on by default; ARENA_BN_FINAL=0 for
-# A/Bs). Also switches the BN kernels' own statistics/backward reductions to the same acc mode.
+# BatchNorm statistics summed inside the conv kernel (fp64 fire-and-forget atomics into an [2, C]
+# set the BN apply pass derives its coefficients from) instead of per-tile partials plus a
+# finalize launch in the BN layer (on by default; ARENA_BN_FINAL=0 for A/Bs). Also switches the BN
+# kernels' own statistics/backward reductions to the same acc mode.
 _BN_FINAL = os.environ.get("ARENA_BN_FINAL", "1") == "1"
 # Above this many (tile, channel) pairs the epilogue's atomics (16 B each, at the ~1.3 TB/s
 # memory-side atomic rate, competing with the tile's output stores) cost more than the partial
-# merge they replace: the 56x56 and 28x28 ResNet-50 layers (3136 / 784 tiles) keep the partials,
-# the 14x14 and 7x7 ones take the accumulators (profiles/r3_bn_acc_ab.jsonl).
+# merge + finalize launch they replace (profiles/r3_bn_acc_ab.jsonl, r3_bn_fin_ab.jsonl).
 _ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_ACC_MAX_PAIRS", str(64 << 10)))
+
+
+def set_acc_max_pairs(n: int) -> None:
+    """Epilogue-statistics threshold (see _ACC_MAX_PAIRS); decided per call, so a captured graph
+    keeps the mode it was captured with."""
+    global _ACC_MAX_PAIRS
+    _ACC_MAX_PAIRS = int(n)
 
 
 def _use_acc(m: int, bm: int, cout: int) -> bool:

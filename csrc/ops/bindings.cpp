@@ -95,9 +95,11 @@ hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, 
                              int, hipStream_t);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, uint8_t*, long long, int, int, int,
                         float*, int, long long, double*, unsigned*, ArenaBNStats, double*, int,
-                        hipStream_t);
+                        double*, int, hipStream_t);
 hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, void*, long long, int,
-                        int, float*, int, double*, unsigned*, ArenaBNBwd, double*, hipStream_t);
+                        int, float*, int, double*, unsigned*, ArenaBNBwd, double*, int, double*,
+                        int, hipStream_t);
+int arena_bn_acc_ok(long long, int);
 #ifdef ARENA_TIMELINE
 hipError_t arena_timeline_read(long long*, int);
 #endif
@@ -721,31 +723,55 @@ unsigned* bn_tickets(const Tensor& like) {
 }
 
 // Statistics accumulators of acc mode (conv_kernels.hip ConvArgs::bn_acc, bn_kernels.hip): a
-// rotating pool of zeroed fp64 [2][C] sets. The finalize kernel that consumes a set zeroes it
-// again, so sets are reused without a memset (and graph replays stay valid); one set is only in
-// use between a producer (conv epilogue / statistics pass / backward reduction) and its finalize,
-// which follow each other on the stream.
+// rotating pool of fp64 [2][C] sets, zero when handed out. A forward set (conv epilogue or
+// statistics pass -> apply pass) is zeroed by its layer's backward dx pass (bn_bwd zero_f); a
+// backward set from the pool by its finalize. The host tracks which sets may still hold sums (a
+// training forward whose backward never ran): such a set is zeroed on the stream before it is
+// handed out again. Graph replays stay valid because every captured step zeroes the sets it
+// dirtied (forward and backward are captured together).
 constexpr int kAccSets = 128, kAccC = 2048;
+struct AccPool {
+  Tensor t;
+  unsigned next = 0;
+  std::vector<char> dirty;
+};
+std::vector<AccPool>& acc_pools() {
+  static std::vector<AccPool> pools;
+  return pools;
+}
+
 Tensor bn_acc_set(const Tensor& like, int64_t C) {
-  static std::vector<Tensor> pools;
-  static std::vector<unsigned> next;
   TORCH_CHECK(C > 0 && C <= kAccC, "BatchNorm acc mode: C must be <= ", kAccC);
+  auto& pools = acc_pools();
   const int dev = like.get_device();
-  if ((int)pools.size() <= dev) {
-    pools.resize(dev + 1);
-    next.resize(dev + 1, 0);
-  }
-  if (!pools[dev].defined()) {
+  if ((int)pools.size() <= dev) pools.resize(dev + 1);
+  AccPool& p = pools[dev];
+  if (!p.t.defined()) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     check_hip(hipStreamIsCapturing(cur_stream(), &cs), "bn_acc_set");
     TORCH_CHECK(cs == hipStreamCaptureStatusNone,
                 "arena BatchNorm: run one eager step before capturing a graph (its statistics "
                 "accumulators are allocated and zeroed on first use)");
-    pools[dev] = torch::zeros({kAccSets, 2 * kAccC}, like.options().dtype(torch::kFloat64));
+    p.t = torch::zeros({kAccSets, 2 * kAccC}, like.options().dtype(torch::kFloat64));
+    p.dirty.assign(kAccSets, 0);
     check_hip(hipStreamSynchronize(cur_stream()), "bn_acc_set zero");
   }
-  const int64_t set = next[dev]++ % kAccSets;
-  return pools[dev][set].narrow(0, 0, 2 * C).view({2, C});
+  const int64_t set = p.next++ % kAccSets;
+  Tensor row = p.t[set];
+  if (p.dirty[set]) row.zero_();
+  p.dirty[set] = 1;
+  return row.narrow(0, 0, 2 * C).view({2, C});
+}
+
+// A kernel that zeroes `t` (a pool set) has been enqueued: the set is clean for its next user.
+void bn_acc_clean(const Tensor& t) {
+  auto& pools = acc_pools();
+  const int dev = t.get_device();
+  if (dev < 0 || (int)pools.size() <= dev || !pools[dev].t.defined()) return;
+  const AccPool& p = pools[dev];
+  const int64_t off = (const double*)t.data_ptr() - (const double*)p.t.data_ptr();
+  if (off < 0 || off >= (int64_t)kAccSets * 2 * kAccC) return;
+  pools[dev].dirty[off / (2 * kAccC)] = 0;
 }
 
 // Split-K tickets of the conv kernel (ConvArgs::kcnt): one ring of zeroed counters per device;
@@ -813,15 +839,18 @@ Tensor bn_lvl2(int64_t nblk, int64_t C, const Tensor& like) {
   return torch::empty({arena_bn_lvl2_doubles(nblk, (int)C)}, like.options().dtype(torch::kFloat64));
 }
 
-// Returns (y, mean, invstd, mask). Eval mode normalises with the running statistics. mask (relu
+// Returns (y, mean, invstd, mask, acc). Eval mode normalises with the running statistics. mask (relu
 // in training, else empty): uint8 [M * C / 8], bit i of byte v = (y.flat[8 v + i] > 0).
+// acc: the fp64 [2][C] statistics sums the apply pass derived its coefficients from (acc mode), or
+// empty. They stay in place: pass it to this layer's bn_bwd as zero_f, which zeroes it.
+// zero_b (optional): fp64 tensor the apply pass zeroes (this layer's backward sums, bn_bwd acc_b).
 // stats_part/stats_rpb: BatchNorm partials of x from conv_fwd(with_stats=True) (training only).
 // stats_fin (training): the fp64 [2][C] accumulators conv_fwd(..., stats_final=True) filled: no
 // statistics pass, a one-thread-per-channel finalize instead of the partial merge.
 std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT running_mean,
                            OptT running_var, bool training, double momentum, double eps,
                            bool relu, OptT num_batches, OptT stats_part, int64_t stats_rpb,
-                           OptT stats_fin) {
+                           OptT stats_fin, OptT zero_b) {
   const BNGeom g = bn_geom(x, "x");
   if (res.has_value()) bn_same(x, *res, "residual");
   auto f32 = x.options().dtype(torch::kFloat32);
@@ -884,11 +913,21 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
   Tensor lvl2, acc;
   unsigned* tickets = nullptr;
   int acc_ready = 0;
+  double* zb = nullptr;
+  int nzb = 0;
+  if (zero_b.has_value()) {
+    TORCH_CHECK(zero_b->is_cuda() && zero_b->device() == x.device() &&
+                    zero_b->scalar_type() == torch::kFloat64 && zero_b->is_contiguous(),
+                "zero_b must be a contiguous fp64 tensor on x's device");
+    zb = zero_b->data_ptr<double>();
+    nzb = (int)zero_b->numel();
+  }
   if (training && stats_fin.has_value()) {
     acc = *stats_fin;
     acc_ready = 1;
   } else if (training) {
-    if (!stats_part.has_value() && g_bn_acc) acc = bn_acc_set(x, g.C);
+    if (!stats_part.has_value() && g_bn_acc && arena_bn_acc_ok(g.M, (int)g.C))
+      acc = bn_acc_set(x, g.C);
     const int64_t nblk = ext_nblk > 0 ? ext_nblk : part.numel() / (2 * g.C);
     lvl2 = bn_lvl2(nblk, g.C, x);
     tickets = bn_tickets(x);
@@ -899,16 +938,20 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
                          part.defined() ? part.data_ptr<float>() : nullptr, ext_nblk,
                          (long long)stats_rpb, lvl2.defined() ? lvl2.data_ptr<double>() : nullptr,
                          tickets, st, acc.defined() ? acc.data_ptr<double>() : nullptr, acc_ready,
-                         cur_stream()),
+                         zb, nzb, cur_stream()),
             "bn_fwd");
-  return {y, mean, invstd, mask};
+  return {y, mean, invstd, mask, acc};
 }
 
 // Returns (dx, dres or empty, dgamma or empty, dbeta or empty). mask: bn_fwd's ReLU bits (relu).
 // ext_part/ext_rpb: the (dy, x) partials from conv_fwd(..., bn_x=x, ...) that produced dy.
+// acc_b (optional): this layer's own fp64 [2][C] backward sums, zero on entry: the reduction adds
+// into it and the dx pass derives its coefficients from it (no finalize launch); the sums stay in
+// place until the layer's next bn_fwd(zero_b=acc_b). Without it a pool set and a finalize are used.
+// zero_f (optional): the forward's statistics sums (bn_fwd's acc output), zeroed by the dx pass.
 std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor invstd, OptT gamma,
                            bool relu, bool with_res, bool affine_grads, OptT ext_part,
-                           int64_t ext_rpb) {
+                           int64_t ext_rpb, OptT acc_b, OptT zero_f) {
   const BNGeom g = bn_geom(x, "x");
   bn_same(x, dy, "grad_output");
   if (relu) {
@@ -955,7 +998,28 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
   tickets = bn_tickets(x);
   // acc mode: atomics in the reduction + per-channel finalize (the kernel side keeps the
   // partials for layers with many blocks x channels)
-  if (!ext_part.has_value() && g_bn_acc) acc = bn_acc_set(x, g.C);
+  int fin_dx = 0;
+  if (!ext_part.has_value() && g_bn_acc && arena_bn_acc_ok(g.M, (int)g.C)) {
+    if (acc_b.has_value()) {
+      TORCH_CHECK(acc_b->is_cuda() && acc_b->device() == x.device() &&
+                      acc_b->scalar_type() == torch::kFloat64 && acc_b->is_contiguous() &&
+                      acc_b->numel() == 2 * g.C,
+                  "acc_b must be a contiguous fp64 tensor of 2*C elements on x's device");
+      acc = *acc_b;
+      fin_dx = 1;
+    } else {
+      acc = bn_acc_set(x, g.C);
+    }
+  }
+  double* zf = nullptr;
+  int nzf = 0;
+  if (zero_f.has_value() && zero_f->defined() && zero_f->numel() > 0) {
+    TORCH_CHECK(zero_f->is_cuda() && zero_f->device() == x.device() &&
+                    zero_f->scalar_type() == torch::kFloat64 && zero_f->is_contiguous(),
+                "zero_f must be a contiguous fp64 tensor on x's device");
+    zf = zero_f->data_ptr<double>();
+    nzf = (int)zero_f->numel();
+  }
   Tensor dx = torch::empty_like(x);
   Tensor dres = with_res ? torch::empty_like(x) : Tensor();
   check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(),
@@ -963,8 +1027,11 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
                          with_res ? dres.data_ptr() : nullptr, g.M, g.C, relu ? 1 : 0,
                          part.defined() ? part.data_ptr<float>() : nullptr, ext_nblk,
                          lvl2.defined() ? lvl2.data_ptr<double>() : nullptr, tickets, b,
-                         acc.defined() ? acc.data_ptr<double>() : nullptr, cur_stream()),
+                         acc.defined() ? acc.data_ptr<double>() : nullptr, fin_dx, zf, nzf,
+                         cur_stream()),
             "bn_bwd");
+  if (acc.defined() && !fin_dx) bn_acc_clean(acc);   // the finalize zeroed the pool set
+  if (zf != nullptr) bn_acc_clean(*zero_f);
   return {dx, dres, dgamma, dbeta};
 }
 
@@ -1527,7 +1594,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_fwd", &bn_fwd, py::arg("x"), py::arg("res"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("training"),
         py::arg("momentum"), py::arg("eps"), py::arg("relu"), py::arg("num_batches"),
-        py::arg("stats_part"), py::arg("stats_rpb"), py::arg("stats_fin") = py::none());
+        py::arg("stats_part"), py::arg("stats_rpb"), py::arg("stats_fin") = py::none(),
+        py::arg("zero_b") = py::none());
   m.def("conv_flip_weight", &conv_flip_weight);
   m.def("conv_flip_multi", &conv_flip_multi);
   m.def("conv_phase_weights", &conv_phase_weights);
@@ -1541,7 +1609,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stem_weight_grad", &stem_weight_grad);
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("mean"),
         py::arg("invstd"), py::arg("gamma"), py::arg("relu"), py::arg("with_res"),
-        py::arg("affine_grads"), py::arg("ext_part") = py::none(), py::arg("ext_rpb") = 0);
+        py::arg("affine_grads"), py::arg("ext_part") = py::none(), py::arg("ext_rpb") = 0,
+        py::arg("acc_b") = py::none(), py::arg("zero_f") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("variant"), py::arg("with_stats"), py::arg("addend") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),

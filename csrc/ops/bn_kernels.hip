@@ -131,22 +131,35 @@ __device__ __forceinline__ void load8f(const float* p, float v[kVec]) {
 // "acc mode": the statistics pass, the backward reduction and the producing conv's epilogue
 // (conv_kernels.hip ConvArgs::bn_acc) add their per-block fp64 sums straight into acc [2][C] with
 // fire-and-forget memory-side atomics (consecutive threads on consecutive channels: contiguous
-// 512-byte wave instructions). A small finalize kernel -- one thread per channel -- then swaps
-// the sums back to zero and writes the results. That replaces the two-level merge of per-block
-// partials (up to 3136 per channel) in the partial-based finalize kernels below.
+// 512-byte wave instructions). The CONSUMING pass (apply forward, dx backward) derives each
+// thread's per-channel coefficients from the sums in its prologue, so no finalize launch sits
+// between producer and consumer; a later kernel of the same layer zeroes the set again (block 0,
+// plain stores: its last reader has finished by stream order). That replaces the two-level merge
+// of per-block partials (up to 3136 per channel) in the partial-based finalize kernels below.
 
+// Reduction geometry. A block covers `cg` channel groups (all C / 8 of them, or a 32-group slice
+// for C > 256: blockIdx.y picks the slice) and kT / cg row slots. The channel split keeps the
+// number of (row block, channel) pairs -- the per-block sums a reduction emits -- at <= 512 x 256
+// for every C, so the acc-mode atomics stay ~2 MB per pass (a 2048-channel layer used to emit 1 M
+// pairs from 512 full-width blocks).
 struct Geo {
-  int cg;    // channel groups (C / 8)
+  int cg;    // channel groups of this block
   int rip;   // rows in parallel per block round
-  int g;     // this thread's channel group
+  int g;     // this thread's channel group (global index)
+  int gl;    // ... within the block's slice
   int slot;  // this thread's row slot (active iff slot < rip)
+  int cw;    // channels of the block's slice (8 cg)
+  int cb;    // first channel of the slice
 };
 __device__ __forceinline__ Geo geo(int C) {
   Geo q;
-  q.cg = C / kVec;
+  q.cg = C / kVec / (int)gridDim.y;
   q.rip = kT / q.cg;
-  q.g = threadIdx.x % q.cg;
+  q.gl = threadIdx.x % q.cg;
   q.slot = threadIdx.x / q.cg;
+  q.cw = q.cg * kVec;
+  q.cb = (int)blockIdx.y * q.cw;
+  q.g = (int)blockIdx.y * q.cg + q.gl;
   return q;
 }
 
@@ -209,21 +222,22 @@ __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, l
   if (q.slot < q.rip) {
 #pragma unroll
     for (int i = 0; i < kVec; ++i) {
-      s_mean[q.slot * C + q.g * kVec + i] = mean[i];
-      s_m2[q.slot * C + q.g * kVec + i] = m2[i];
+      s_mean[q.slot * q.cw + q.gl * kVec + i] = mean[i];
+      s_m2[q.slot * q.cw + q.gl * kVec + i] = m2[i];
     }
-    if (q.g == 0) s_n[q.slot] = n;
+    if (q.gl == 0) s_n[q.slot] = n;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += kT) {
-    float na = s_n[0], ma = s_mean[c], sa = s_m2[c];
+  for (int cl = threadIdx.x; cl < q.cw; cl += kT) {
+    const int c = q.cb + cl;
+    float na = s_n[0], ma = s_mean[cl], sa = s_m2[cl];
     for (int s = 1; s < q.rip; ++s) {
       const float nb = s_n[s];
       if (nb == 0.f) continue;
       const float nab = na + nb;
-      const float d = s_mean[s * C + c] - ma;
+      const float d = s_mean[s * q.cw + cl] - ma;
       ma += d * (nb / nab);
-      sa += s_m2[s * C + c] + d * d * (na * nb / nab);
+      sa += s_m2[s * q.cw + cl] + d * d * (na * nb / nab);
       na = nab;
     }
     if (acc != nullptr) {
@@ -368,57 +382,99 @@ __global__ __launch_bounds__(kT) void bn_stats_finalize_kernel(const float* __re
   }
 }
 
-// Forward finalize of acc mode: channel c's (sum x, sum x^2) -> the same outputs as
-// bn_stats_finalize_kernel (fp64 arithmetic), accumulators zeroed for the next user.
-__global__ __launch_bounds__(kT) void bn_acc_finalize_kernel(double* __restrict__ acc, long long M,
-                                                             int C, ArenaBNStats out) {
-  const int c = blockIdx.x * kT + threadIdx.x;
-  if (out.batches != nullptr && c == 0) *out.batches += 1;
-  if (c >= C) return;
-  const double s1 = __hip_atomic_exchange(acc + c, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const double s2 = __hip_atomic_exchange(acc + C + c, 0.0, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-  const double n = (double)M;
-  const double mean = s1 / n;
-  double m2 = s2 - s1 * mean;
-  m2 = m2 > 0.0 ? m2 : 0.0;
-  const double var = m2 / n;
-  const float invstd = (float)(1.0 / sqrt(var + (double)out.eps));
-  out.mean[c] = (float)mean;
-  out.invstd[c] = invstd;
-  out.scale[c] = (out.gamma ? out.gamma[c] : 1.f) * invstd;
-  out.shift[c] = out.beta ? out.beta[c] : 0.f;
-  if (out.running_mean) {
-    const float mom = out.momentum;
-    out.running_mean[c] = (1.f - mom) * out.running_mean[c] + mom * (float)mean;
-    const double unbiased = n > 1.0 ? m2 / (n - 1.0) : var;
-    out.running_var[c] = (1.f - mom) * out.running_var[c] + mom * (float)unbiased;
-  }
-}
-
 // ------------------------------------------------------------------------------------ apply
 // y = act((x - mean) * scale + shift (+ res)), 2 vectors per thread per round for load ILP.
 // The mask bits are those of the stored (rounded) outputs that are > 0: exactly "saved y > 0"
 // (V8::store_pos).
 
+// Block 0 clears `zero` [nzero] doubles: the accumulator set of an earlier pass whose last reader
+// has finished (kernel order on the stream), made ready for its next producer without a launch.
+__device__ __forceinline__ void zero_duty(double* zero, int nzero) {
+  if (zero == nullptr || blockIdx.x != 0 || blockIdx.y != 0) return;
+  for (int i = threadIdx.x; i < nzero; i += kT) zero[i] = 0.0;
+}
+
+// Per-channel coefficients of the apply / dx passes are computed ONCE PER BLOCK, one thread per
+// channel, into LDS (`s_co`, [k][C] floats, dynamic shared memory), and each thread then reads its
+// 8 channels from there. Every thread loading its own 8 channels from global memory put up to
+// 4096 x 256 requests for the same few hundred bytes on one L2 channel per layer: with the 176
+// bytes per thread the fp64 sums need, the dx pass ran at half speed (51 vs 27 us per layer).
+__device__ __forceinline__ void lds8(const float* p, float v[kVec]) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+// FIN: the batch statistics arrive as the fp64 sums (sum x, sum x^2) of acc mode in `fin` [2][C]
+// (from the producing conv's epilogue or the acc-mode statistics pass) and the block derives mean,
+// invstd, scale and shift itself -- the work of a finalize launch, which this replaces. Block 0
+// also writes st's outputs (mean / invstd for the backward, scale / shift, running statistics,
+// the batch counter). The sums stay in place: the backward's dx pass of this layer zeroes them
+// (arena_bn_bwd `zero`), after their last reader here has finished.
+template <bool FIN>
+__device__ __forceinline__ void apply_coefs(int C, long long M, const double* fin,
+                                            const ArenaBNStats& st, float* s_co) {
+  const double inv_m = 1.0 / (double)M;
+  for (int c = threadIdx.x; c < C; c += kT) {
+    float mu, sc, sh;
+    if constexpr (!FIN) {
+      mu = st.mean[c];
+      sc = st.scale[c];
+      sh = st.shift[c];
+    } else {
+      const double s1 = fin[c], s2 = fin[C + c];
+      const double mean = s1 * inv_m;
+      const double d = s2 - s1 * mean;
+      const double m2 = d > 0.0 ? d : 0.0;
+      const float inv = (float)(1.0 / sqrt(m2 * inv_m + (double)st.eps));
+      mu = (float)mean;
+      sc = (st.gamma ? st.gamma[c] : 1.f) * inv;
+      sh = st.beta ? st.beta[c] : 0.f;
+      if (blockIdx.x == 0) {
+        st.mean[c] = mu;
+        st.invstd[c] = inv;
+        st.scale[c] = sc;
+        st.shift[c] = sh;
+        if (st.running_mean) {
+          const float mom = st.momentum;
+          const double unbiased = M > 1 ? m2 / (double)(M - 1) : m2 * inv_m;
+          st.running_mean[c] = (1.f - mom) * st.running_mean[c] + mom * mu;
+          st.running_var[c] = (1.f - mom) * st.running_var[c] + mom * (float)unbiased;
+        }
+        if (c == 0 && st.batches != nullptr) *st.batches += 1;
+      }
+    }
+    s_co[c] = mu;
+    s_co[C + c] = sc;
+    s_co[2 * C + c] = sh;
+  }
+  __syncthreads();
+}
+
 // NT: non-temporal loads of x (and res) -- their last read before the backward pass
-template <typename T, bool RELU, bool RES, bool NT>
+// dynamic shared memory: 3 * C floats
+template <typename T, bool RELU, bool RES, bool NT, bool FIN>
 __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
                                                       const T* __restrict__ res,
                                                       T* __restrict__ y,
                                                       uint8_t* __restrict__ mask,
-                                                      const float* __restrict__ mean,
-                                                      const float* __restrict__ scale,
-                                                      const float* __restrict__ shift,
-                                                      long long nvec, int cg) {
+                                                      ArenaBNStats st,
+                                                      const double* __restrict__ fin,
+                                                      long long M, long long nvec, int cg,
+                                                      double* __restrict__ zero, int nzero) {
+  extern __shared__ __attribute__((aligned(16))) float s_co[];
   const long long stride = (long long)gridDim.x * kT;
   // every vector this thread touches has the same channel group: the grid stride is a multiple
   // of kT, and cg divides kT (host-checked), so the per-channel coefficients load once
   const int c0 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1)) * kVec;
+  const int C = cg * kVec;
+  apply_coefs<FIN>(C, M, fin, st, s_co);
   float mu[kVec], sc[kVec], sh[kVec];
-  load8f(mean + c0, mu);
-  load8f(scale + c0, sc);
-  load8f(shift + c0, sh);
+  lds8(s_co + c0, mu);
+  lds8(s_co + C + c0, sc);
+  lds8(s_co + 2 * C + c0, sh);
+  zero_duty(zero, nzero);
   for (long long v0 = (long long)blockIdx.x * kT + threadIdx.x; v0 < nvec; v0 += 2 * stride) {
     float a[2][kVec], b[2][kVec];
     bool ok[2];
@@ -498,7 +554,7 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
         const long long rr = r + (long long)u * q.rip;
         const long long p = rr * C + off;
         V8<T>::load(dy + p, d[u]);
-        if (RELU) mb[u] = mask[rr * q.cg + q.g];
+        if (RELU) mb[u] = mask[rr * (C / kVec) + q.g];
         V8<T>::load(x + p, v[u]);
       }
 #pragma unroll
@@ -514,7 +570,7 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
       float d[kVec], v[kVec];
       const long long p = r * C + off;
       V8<T>::load(dy + p, d);
-      const uint32_t mb = RELU ? (uint32_t)mask[r * q.cg + q.g] : 0xffu;
+      const uint32_t mb = RELU ? (uint32_t)mask[r * (C / kVec) + q.g] : 0xffu;
       V8<T>::load(x + p, v);
 #pragma unroll
       for (int i = 0; i < kVec; ++i) {
@@ -528,16 +584,17 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
   if (q.slot < q.rip) {
 #pragma unroll
     for (int i = 0; i < kVec; ++i) {
-      s_g[q.slot * C + q.g * kVec + i] = sg[i];
-      s_gx[q.slot * C + q.g * kVec + i] = sgx[i];
+      s_g[q.slot * q.cw + q.gl * kVec + i] = sg[i];
+      s_gx[q.slot * q.cw + q.gl * kVec + i] = sgx[i];
     }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += kT) {
+  for (int cl = threadIdx.x; cl < q.cw; cl += kT) {
+    const int c = q.cb + cl;
     float a = 0.f, b = 0.f;
     for (int s = 0; s < q.rip; ++s) {
-      a += s_g[s * C + c];
-      b += s_gx[s * C + c];
+      a += s_g[s * q.cw + cl];
+      b += s_gx[s * q.cw + cl];
     }
     if (acc != nullptr) {
       unsafeAtomicAdd(acc + c, (double)a);
@@ -593,20 +650,55 @@ __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const float* __rest
 
 // --------------------------------------------------------------------------------- backward dx
 // NT: non-temporal loads of dy and x (their last read in the step)
-template <typename T, bool RELU, bool RES, bool NT>
+// FIN: the reduction ran in acc mode into `acc` [2][C] (sum g, sum g (x - mean)) and the block
+// derives the coefficients, one thread per channel (bn_bwd_finish's arithmetic, with 1/M
+// multiplied instead of divided); block 0 writes dgamma / dbeta. The sums are left in place: the layer's
+// next forward apply pass zeroes them (arena_bn_fwd `zero`).
+// dynamic shared memory: 4 * C floats
+template <typename T, bool RELU, bool RES, bool NT, bool FIN>
 __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
                                                        const uint8_t* __restrict__ mask,
                                                        const T* __restrict__ x,
                                                        T* __restrict__ dx, T* __restrict__ dres,
-                                                       long long nvec, int cg, ArenaBNBwd co) {
+                                                       long long nvec, int cg, ArenaBNBwd co,
+                                                       const double* __restrict__ acc, long long M,
+                                                       double* __restrict__ zero, int nzero) {
+  extern __shared__ __attribute__((aligned(16))) float s_co[];
   const long long stride = (long long)gridDim.x * kT;
   // fixed channel group per thread (grid stride = multiple of kT, cg | kT): coefficients once
   const int c0 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1)) * kVec;
+  const int C = cg * kVec;
+  const double inv_m = 1.0 / (double)M;
+  for (int c = threadIdx.x; c < C; c += kT) {   // one thread per channel (see lds8)
+    float a_, b_, c_;
+    if constexpr (FIN) {
+      const double a = acc[c], b = acc[C + c];
+      const float invstd = co.invstd[c];
+      const float gam = co.gamma ? co.gamma[c] : 1.f;
+      a_ = gam * invstd;
+      b_ = (float)(a * inv_m);
+      c_ = (float)(b * inv_m) * invstd * invstd;
+      if (blockIdx.x == 0) {
+        if (co.dgamma) co.dgamma[c] = (float)(b * invstd);
+        if (co.dbeta) co.dbeta[c] = (float)a;
+      }
+    } else {
+      a_ = co.ca[c];
+      b_ = co.cb[c];
+      c_ = co.cc[c];
+    }
+    s_co[c] = a_;
+    s_co[C + c] = b_;
+    s_co[2 * C + c] = c_;
+    s_co[3 * C + c] = co.mean[c];
+  }
+  __syncthreads();
   float ca[kVec], cb[kVec], cc[kVec], mu[kVec];
-  load8f(co.ca + c0, ca);
-  load8f(co.cb + c0, cb);
-  load8f(co.cc + c0, cc);
-  load8f(co.mean + c0, mu);
+  lds8(s_co + c0, ca);
+  lds8(s_co + C + c0, cb);
+  lds8(s_co + 2 * C + c0, cc);
+  lds8(s_co + 3 * C + c0, mu);
+  zero_duty(zero, nzero);
   for (long long v = (long long)blockIdx.x * kT + threadIdx.x; v < nvec; v += stride) {
     float d[kVec], xv[kVec];
     if (NT) V8<T>::loadnt(dy + v * kVec, d); else V8<T>::load(dy + v * kVec, d);
@@ -633,15 +725,25 @@ int g_bn_nt = 1;           // non-temporal loads in the apply / dx passes (runti
 long long g_min_rounds = 8;
 
 // acc mode pays one fp64 (a, b) atomic pair per block and channel at the end of the pass; above
-// this many pairs their drain costs more than the partial merge it replaces (ResNet-50: the
-// 2048-channel 7x7 layers run 512 blocks = 1 M pairs), so those layers keep the partials.
-long long g_acc_max_pairs = 32 << 10;
+// this many pairs their drain would cost more than the partial merge. With the channel-sliced
+// grid (Geo) a reduction emits at most 512 x 256 pairs, so every layer takes acc mode.
+long long g_acc_max_pairs = 1 << 18;
 
+// Channel slices of a reduction block row (Geo): one up to 256 channels, else 32-group slices.
+int chan_slices(int C) {
+  const int cg = C / kVec;
+  return cg > 32 ? cg / 32 : 1;
+}
+
+// Row blocks of a reduction over M rows (the grid is row blocks x chan_slices(C)).
 long long reduce_blocks(long long M, int C, long long* rpb) {
-  const int rip = kT / (C / kVec);
+  const int ns = chan_slices(C);
+  const int rip = kT / (C / kVec / ns);
   long long rounds = (M + rip - 1) / rip;
   long long nb = (rounds + g_min_rounds - 1) / g_min_rounds;
-  nb = nb < 1 ? 1 : (nb > g_max_reduce_blocks ? g_max_reduce_blocks : nb);
+  long long maxb = g_max_reduce_blocks / ns;
+  maxb = maxb < 1 ? 1 : maxb;
+  nb = nb < 1 ? 1 : (nb > maxb ? maxb : nb);
   long long r = (M + nb - 1) / nb;
   r = (r + rip - 1) / rip * rip;  // whole rounds per block
   *rpb = r;
@@ -668,6 +770,13 @@ void arena_bn_set_nt(int on) { g_bn_nt = on ? 1 : 0; }
 void arena_bn_set_acc_max_pairs(long long p) { g_acc_max_pairs = p < 0 ? 0 : p; }
 long long arena_bn_acc_max_pairs() { return g_acc_max_pairs; }
 
+// 1 when a pass over M x C takes acc mode (its reduction emits few enough sums).
+int arena_bn_acc_ok(long long M, int C) {
+  if (bad_shape(M, C)) return 0;
+  long long rpb;
+  return reduce_blocks(M, C, &rpb) * C <= g_acc_max_pairs ? 1 : 0;
+}
+
 void arena_bn_set_reduce_geometry(long long max_blocks, long long min_rounds) {
   g_max_reduce_blocks = max_blocks < 1 ? 1 : (max_blocks > 4096 ? 4096 : max_blocks);
   g_min_rounds = min_rounds < 1 ? 1 : min_rounds;
@@ -689,33 +798,37 @@ long long arena_bn_workspace_floats(long long M, int C) {
 // ext_nblk > 0: `part` already holds the statistics partials of x ([ext_nblk][2][C], ext_rpb rows
 // each), written by the producing convolution's epilogue (conv_kernels.hip): no statistics pass.
 // mask (optional, relu only): [M * C / 8] bytes, bit i of byte v = (y[v * 8 + i] > 0)
-// acc (training, optional): fp64 [2][C] accumulators (zero on entry, zero on exit). acc_ready:
-// the producing convolution already added the statistics of x (no statistics pass); else the
-// statistics pass runs in acc mode. Either way a one-thread-per-channel finalize follows.
+// acc (training, optional): fp64 [2][C] accumulators, zero on entry. acc_ready: the producing
+// convolution already added the statistics of x (no statistics pass); else the statistics pass
+// runs in acc mode. Either way the apply pass derives the coefficients from the sums (no finalize
+// launch) and LEAVES THEM IN PLACE: the caller hands `acc` to this layer's arena_bn_bwd as its
+// `zero` set (or zeroes it itself when no backward follows).
+// zero / nzero (optional): doubles block 0 of the apply pass clears (this layer's backward
+// accumulators of the previous step, see arena_bn_bwd fin_dx).
 hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint8_t* mask,
                         long long M, int C, int relu, int training, float* part, int ext_nblk,
                         long long ext_rpb,
                         double* lvl2, unsigned* tickets, ArenaBNStats st, double* acc,
-                        int acc_ready, hipStream_t stream) {
+                        int acc_ready, double* zero, int nzero, hipStream_t stream) {
   if (bad_shape(M, C)) return hipErrorInvalidValue;
   const int groups = (C + 63) / 64;
+  const int ns = chan_slices(C);
   if (training && acc != nullptr && !acc_ready) {
     long long rpb;
     if (reduce_blocks(M, C, &rpb) * C > g_acc_max_pairs) acc = nullptr;   // partials instead
   }
-  if (training && acc != nullptr) {
+  const bool fin = training && acc != nullptr;
+  if (fin) {
     if (!acc_ready) {
       long long rpb;
       const long long nb = reduce_blocks(M, C, &rpb);
       if (dtype == 1)
-        hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb), dim3(kT), 0, stream,
+        hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb, ns), dim3(kT), 0, stream,
                            static_cast<const uint16_t*>(x), M, C, rpb, nullptr, acc);
       else
-        hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kT), 0, stream,
+        hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb, ns), dim3(kT), 0, stream,
                            static_cast<const float*>(x), M, C, rpb, nullptr, acc);
     }
-    hipLaunchKernelGGL(bn_acc_finalize_kernel, dim3((C + kT - 1) / kT), dim3(kT), 0, stream, acc,
-                       M, C, st);
   } else if (training && ext_nblk > 0) {
     if (ext_rpb <= 0 || (long long)ext_nblk * ext_rpb < M) return hipErrorInvalidValue;
     hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups, fin_blocks_per_group(ext_nblk)),
@@ -724,10 +837,10 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
     long long rpb;
     const long long nb = reduce_blocks(M, C, &rpb);
     if (dtype == 1)
-      hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb), dim3(kT), 0, stream,
+      hipLaunchKernelGGL(bn_stats_kernel<uint16_t>, dim3(nb, ns), dim3(kT), 0, stream,
                          static_cast<const uint16_t*>(x), M, C, rpb, part, nullptr);
     else
-      hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb), dim3(kT), 0, stream,
+      hipLaunchKernelGGL(bn_stats_kernel<float>, dim3(nb, ns), dim3(kT), 0, stream,
                          static_cast<const float*>(x), M, C, rpb, part, nullptr);
     hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3(groups, fin_blocks_per_group((int)nb)),
                        dim3(kT), 0, stream, part, (int)nb, M, C, rpb, lvl2, tickets, st);
@@ -735,12 +848,15 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
   const long long nvec = M * (C / kVec);
   const int nb = elementwise_blocks(nvec);
   const int cg = C / kVec;
-#define ARENA_BN_APPLY_NT(TT, R, S, NT)                                                      \
-  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S, NT>), dim3(nb), dim3(kT), 0, stream,       \
+#define ARENA_BN_APPLY_NT(TT, R, S, NT, F)                                                   \
+  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S, NT, F>), dim3(nb), dim3(kT), 3 * C * 4, stream, \
                      static_cast<const TT*>(x), static_cast<const TT*>(res), static_cast<TT*>(y), \
-                     mask, st.mean, st.scale, st.shift, nvec, cg)
-#define ARENA_BN_APPLY(TT, R, S) \
-  do { if (g_bn_nt) ARENA_BN_APPLY_NT(TT, R, S, true); else ARENA_BN_APPLY_NT(TT, R, S, false); } \
+                     mask, st, acc, M, nvec, cg, zero, nzero)
+#define ARENA_BN_APPLY_F(TT, R, S, F)                                                        \
+  do { if (g_bn_nt) ARENA_BN_APPLY_NT(TT, R, S, true, F);                                    \
+       else ARENA_BN_APPLY_NT(TT, R, S, false, F); } while (0)
+#define ARENA_BN_APPLY(TT, R, S)                                                             \
+  do { if (fin) ARENA_BN_APPLY_F(TT, R, S, true); else ARENA_BN_APPLY_F(TT, R, S, false); }  \
   while (0)
   const bool r = relu != 0, s = res != nullptr;
   if (dtype == 1) {
@@ -755,6 +871,7 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
     else ARENA_BN_APPLY(float, false, false);
   }
 #undef ARENA_BN_APPLY
+#undef ARENA_BN_APPLY_F
 #undef ARENA_BN_APPLY_NT
   return hipGetLastError();
 }
@@ -762,22 +879,27 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
 // ext_nblk > 0: `part` already holds the backward partials of (dy, x) ([ext_nblk][2][C]), written
 // by the epilogue of the backward-data convolution that produced dy (conv_kernels.hip, EPI 2):
 // no reduction pass.
-// acc != null (and no external partials): the reduction runs in acc mode and a one-thread-per-
-// channel finalize writes the coefficients.
+// acc != null (and no external partials): the reduction runs in acc mode. fin_dx: the dx pass
+// derives the coefficients from the sums (no finalize launch) and leaves them in place -- the
+// caller owns `acc` per layer and hands it to the layer's next arena_bn_fwd as its `zero` set;
+// else a one-thread-per-channel finalize writes the coefficients and zeroes `acc`.
+// zero / nzero (optional): doubles block 0 of the dx pass clears (the forward's statistics sums
+// of this layer, whose last reader -- the apply pass -- has finished).
 hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const void* x, void* dx,
                         void* dres, long long M, int C, int relu, float* part, int ext_nblk,
-                        double* lvl2, unsigned* tickets, ArenaBNBwd co, double* acc,
-                        hipStream_t stream) {
+                        double* lvl2, unsigned* tickets, ArenaBNBwd co, double* acc, int fin_dx,
+                        double* zero, int nzero, hipStream_t stream) {
   if (bad_shape(M, C) || (relu && mask == nullptr)) return hipErrorInvalidValue;
   long long rpb;
   long long nb = reduce_blocks(M, C, &rpb);
+  const int ns = chan_slices(C);
   const bool acc_mode = acc != nullptr && ext_nblk <= 0 && nb * C <= g_acc_max_pairs;
   double* am = acc_mode ? acc : nullptr;
   if (ext_nblk > 0) {
     nb = ext_nblk;
   } else {
 #define ARENA_BN_RED(TT, R)                                                                  \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, R>), dim3(nb), dim3(kT), 0, stream,         \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, R>), dim3(nb, ns), dim3(kT), 0, stream,     \
                      static_cast<const TT*>(dy), mask, static_cast<const TT*>(x), M, C, rpb, \
                      part, co, am)
     if (dtype == 1) {
@@ -787,22 +909,27 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
     }
 #undef ARENA_BN_RED
   }
-  if (acc_mode)
+  const bool fin = acc_mode && fin_dx;
+  if (acc_mode && !fin)
     hipLaunchKernelGGL(bn_bwd_acc_finalize_kernel, dim3((C + kT - 1) / kT), dim3(kT), 0, stream,
                        acc, M, C, co);
-  else
+  else if (!acc_mode)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64, fin_blocks_per_group((int)nb)),
                        dim3(kT), 0, stream, part, (int)nb, M, C, lvl2, tickets, co);
   const long long nvec = M * (C / kVec);
   long long ne = (nvec + kT - 1) / kT;
   ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);
   const int cg = C / kVec;
-#define ARENA_BN_DX_NT(TT, R, S, NT)                                                         \
-  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S, NT>), dim3(ne), dim3(kT), 0, stream,      \
+#define ARENA_BN_DX_NT(TT, R, S, NT, F)                                                      \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S, NT, F>), dim3(ne), dim3(kT), 4 * C * 4, stream, \
                      static_cast<const TT*>(dy), mask, static_cast<const TT*>(x),            \
-                     static_cast<TT*>(dx), static_cast<TT*>(dres), nvec, cg, co)
-#define ARENA_BN_DX(TT, R, S) \
-  do { if (g_bn_nt) ARENA_BN_DX_NT(TT, R, S, true); else ARENA_BN_DX_NT(TT, R, S, false); } \
+                     static_cast<TT*>(dx), static_cast<TT*>(dres), nvec, cg, co, acc, M,     \
+                     zero, nzero)
+#define ARENA_BN_DX_F(TT, R, S, F)                                                           \
+  do { if (g_bn_nt) ARENA_BN_DX_NT(TT, R, S, true, F);                                       \
+       else ARENA_BN_DX_NT(TT, R, S, false, F); } while (0)
+#define ARENA_BN_DX(TT, R, S)                                                                \
+  do { if (fin) ARENA_BN_DX_F(TT, R, S, true); else ARENA_BN_DX_F(TT, R, S, false); }        \
   while (0)
   const bool r = relu != 0, s = dres != nullptr;
   if (dtype == 1) {
@@ -817,6 +944,7 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
     else ARENA_BN_DX(float, false, false);
   }
 #undef ARENA_BN_DX
+#undef ARENA_BN_DX_F
 #undef ARENA_BN_DX_NT
   return hipGetLastError();
 }

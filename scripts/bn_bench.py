@@ -76,7 +76,7 @@ def main():
         ext.bn_set_reduce_geometry(mb, mr)
         rows, tot_us, tot_bytes = [], 0.0, 0.0
         for M, C, uses, relu, res, x, dy, r, w, bias, rm, rv in data:
-            y, mean, invstd, mask = ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None,
+            y, mean, invstd, mask, _ = ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None,
                                                None, 0)
             f = timed(lambda: ext.bn_fwd(x, r, w, bias, rm, rv, True, 0.1, 1e-5, relu, None, None, 0))
             bk = timed(lambda: ext.bn_bwd(dy, mask if relu else None, x, mean, invstd, w, relu, res, True))

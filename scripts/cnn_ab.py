@@ -9,7 +9,9 @@ every variant alike (cdna_hip_programming.md §5.4 rule 24). Variants are conv m
 ``:link`` (BN-backward partials in the dgrad epilogues), ``:torchstem`` (the stem's
 input/weight casts and weight transform as torch ops) and/or ``:nomask`` (the last BN writes
 dy * mask for the residual join instead of parking (dy, bits)) and/or ``:finP<n>`` (at most n
-level-1 blocks per channel group in the BN finalize kernels), joined with ``+``.
+level-1 blocks per channel group in the BN finalize kernels) and/or ``:accP<n>`` (conv-epilogue
+BN statistics as fp64 sums up to n tile-channel pairs) and/or ``:finbwd0`` (BN backward sums
+from the pool plus a finalize launch), joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
     python scripts/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
@@ -46,6 +48,7 @@ def main():
     hvd.init("gloo")
     args = cnn_bench.parse(["--model", a.model, "--batch_size", str(a.batch)])
     variants = {}
+    conv_acc_default = conv._ACC_MAX_PAIRS
     for i, name in enumerate(a.modes.split(",")):
         mode, _, opt_s = name.partition(":")
         conv.set_mode(mode)
@@ -59,6 +62,12 @@ def main():
         from arena_amd.ops import _ext as _e
         _e.load().bn_set_fin_max_blocks(finp[0] if finp else 64)
         _e.load().bn_set_nt(0 if "bnnt0" in opt_s.split("+") else 1)   # BN non-temporal loads
+        # accP<n>: conv-epilogue BN statistics as fp64 sums up to n (tile, channel) pairs
+        accp = [int(o[4:]) for o in opt_s.split("+") if o.startswith("accP")]
+        conv.set_acc_max_pairs(accp[0] if accp else conv_acc_default)
+        # finbwd0: BN backward sums from the pool + a finalize launch (not the layer's own set)
+        from arena_amd.ops import batchnorm as _bn
+        _bn.set_fin_bwd("finbwd0" not in opt_s.split("+"))
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
             cnn_bench.train_step(model, opt, x, y, torch.bfloat16)

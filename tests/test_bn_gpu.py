@@ -222,3 +222,42 @@ def test_resnet_step_finished_stats_match_partials():
             assert torch.allclose(ba[n], bb[n], rtol=1e-3, atol=1e-4), n
         else:
             assert torch.equal(ba[n], bb[n]), n
+
+
+@pytest.mark.parametrize("C", [64, 512, 2048])
+def test_bn_accumulators_rezeroed_across_steps(C):
+    """The statistics sums are zeroed by later kernels of the same layer (forward sums by the
+    backward dx pass, backward sums by the next forward apply pass), not by a finalize launch:
+    repeated training steps, training-mode forwards with no backward in between, and a graph
+    replay must all see clean sums (checked against nn.BatchNorm2d at every step)."""
+    from arena_amd.ops.batchnorm import BatchNormAct2d
+    torch.manual_seed(3)
+    shape = (4, C, 7, 7)
+    m = BatchNormAct2d(C).cuda()
+    ref = torch.nn.BatchNorm2d(C).cuda()
+    ref.load_state_dict(m.state_dict())
+
+    def step(i):
+        x = _nhwc(torch.randn(shape, device="cuda") * (1 + i) + i)
+        g = _nhwc(torch.randn(shape, device="cuda"))
+        xk = x.clone().requires_grad_(True)
+        xr = x.clone().requires_grad_(True)
+        y = m(xk)
+        yr = F.relu(ref(xr))
+        torch.testing.assert_close(y, yr, rtol=1e-4, atol=1e-4)
+        y.backward(g)
+        yr.backward(g)
+        torch.testing.assert_close(xk.grad, xr.grad, rtol=2e-3, atol=2e-3)
+        torch.testing.assert_close(m.weight.grad, ref.weight.grad, rtol=2e-3, atol=2e-3)
+        m.weight.grad = m.bias.grad = ref.weight.grad = ref.bias.grad = None
+
+    for i in range(3):
+        step(i)
+    with torch.no_grad():   # training-mode forwards whose backward never runs
+        for i in range(2):
+            x = _nhwc(torch.randn(shape, device="cuda"))
+            torch.testing.assert_close(m(x), F.relu(ref(x)), rtol=1e-4, atol=1e-4)
+    step(5)
+    torch.testing.assert_close(m.running_mean, ref.running_mean, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(m.running_var, ref.running_var, rtol=1e-4, atol=1e-5)
+    assert int(m.num_batches_tracked) == int(ref.num_batches_tracked)
