@@ -34,6 +34,11 @@ TILES.update({12: (256, 128), 13: (256, 64), 14: (256, 128), 15: (256, 64)})
 # bit-reproducible): for the layers whose tile count leaves CUs idle (14x14 / 7x7 at batch 128)
 KSPLITS = (2, 3, 4, 6, 8)
 TILES.update({v + 16 * (k - 1): TILES[v] for v in range(16) for k in KSPLITS})
+# + 256 * p (p = 1..4, unsplit tiles only): the persistent form, 2^p output tiles of one column
+# tile per block -- the block's BatchNorm sums are merged in LDS and flushed once (see
+# conv_kernels.hip conv_fwd_body), and the per-block prologue is paid once per 2^p tiles
+PERSIST = (1, 2, 3, 4)
+TILES.update({v + 256 * p: TILES[v] for v in range(16) for p in PERSIST})
 _CUS = 256
 
 
@@ -43,7 +48,34 @@ def kvariant(v: int, ks: int) -> int:
 
 
 def split_of(v: int) -> int:
-    return v // 16 + 1
+    return v % 256 // 16 + 1
+
+
+def tiles_per_block(v: int) -> int:
+    return 1 << (v // 256)
+
+
+_PERSIST_ON = os.environ.get("ARENA_CONV_PERSIST", "1") != "0"
+
+
+def set_persist(on: bool) -> None:
+    """A/B switch: offer the persistent forms to the autotuner (part of the plan key)."""
+    global _PERSIST_ON
+    _PERSIST_ON = bool(on)
+
+
+def persist_variants_for(m: int, cout: int, bases):
+    """Persistent forms of the tile variants ``bases`` that keep at least one block per CU."""
+    out = []
+    if not _PERSIST_ON:
+        return out
+    for v in bases:
+        if v >= 16:
+            continue
+        bm, bn = TILES[v]
+        tiles = -(-m // bm) * (cout // bn)
+        out += [v + 256 * p for p in PERSIST if tiles >> p >= _CUS]
+    return out
 
 
 def out_hw(h: int, w: int, r: int, s: int, stride: int, pad: int) -> Tuple[int, int]:
@@ -182,7 +214,7 @@ _BN_FINAL = os.environ.get("ARENA_BN_FINAL", "1") == "1"
 # Above this many (tile, channel) pairs the epilogue's atomics (16 B each, at the ~1.3 TB/s
 # memory-side atomic rate, competing with the tile's output stores) cost more than the partial
 # merge + finalize launch they replace (profiles/r3_bn_acc_ab.jsonl, r3_bn_fin_ab.jsonl).
-_ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_ACC_MAX_PAIRS", str(64 << 10)))
+_ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_ACC_MAX_PAIRS", str(128 << 10)))
 
 
 def set_acc_max_pairs(n: int) -> None:
@@ -192,8 +224,11 @@ def set_acc_max_pairs(n: int) -> None:
     _ACC_MAX_PAIRS = int(n)
 
 
-def _use_acc(m: int, bm: int, cout: int) -> bool:
-    return _BN_FINAL and -(-m // bm) * cout <= _ACC_MAX_PAIRS
+def _use_acc(m: int, variant: int, cout: int) -> bool:
+    """Whether a forward of ``m`` output pixels on tile variant ``variant`` sums its BatchNorm
+    statistics in the epilogue (fp64 atomics, one set per block) instead of per-tile partials."""
+    bm, tpb = TILES[variant][0], tiles_per_block(variant)
+    return _BN_FINAL and -(-(-(-m // bm)) // tpb) * cout <= _ACC_MAX_PAIRS
 
 
 def _out_pixels(x: Tensor, w: Tensor, stride: int, pad: int) -> int:
@@ -317,7 +352,7 @@ class _StemFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z, w16, want_stats, fwd_variant, wgrad_cfg):
         Ho, Wo = z.shape[2], z.shape[3]
-        fin = bool(want_stats and _use_acc(z.shape[0] * Ho * Wo, TILES[fwd_variant][0],
+        fin = bool(want_stats and _use_acc(z.shape[0] * Ho * Wo, fwd_variant,
                                             w16.shape[0]))
         out = _ext.load().conv_fwd_ex(z, w16, 1, 2, 2, Ho, Wo, int(fwd_variant), bool(want_stats),
                                       None, None, [], True, stats_final=fin)
@@ -573,8 +608,19 @@ def _wgrad_candidates(cin, cout, k):
     return sorted(set(out))
 
 
+# what a forward whose statistics come as per-tile partials pays on top of its own time: the BN
+# layer's partial-merge finalize launch (bn_stats_finalize, ~12 us per layer at batch 128)
+_FIN_PENALTY_US = float(os.environ.get("ARENA_CONV_FIN_PENALTY_US", "8"))
+
+
+def _best(t: dict, kind: str, n: int):
+    """The n fastest variant codes timed so far for direction ``kind``."""
+    return [c for (kd, c), _ in sorted(((k, v) for k, v in t.items() if k[0] == kind),
+                                       key=lambda kv: kv[1])][:n]
+
+
 def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
-    key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode())
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _PERSIST_ON)
     plan = _PLANS.get(key)
     if plan is not None and (plan.tuned or torch.cuda.is_current_stream_capturing()):
         return plan
@@ -604,11 +650,29 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
         dy = torch.randn_like(y)
         t = {}
         m_out = x.shape[0] * ho * wo
-        for v in variants_for(cout) + split_variants_for(m_out, cout, cin * k[0] * k[1]):
-            t[("fwd", v)] = _time(lambda: conv2d_fwd(x, w, stride, pad, v, with_stats=True))
+
+        def fwd_time(v):
+            # timed the way the step runs it: statistics summed in the epilogue where _use_acc
+            # says so (into a scratch set), else per-tile partials plus the BN finalize launch
+            # that consumes them (charged as _FIN_PENALTY_US)
+            fin = _use_acc(m_out, v, cout)
+            us = _time(lambda: conv2d_fwd(x, w, stride, pad, v, with_stats=True, final=fin))
+            return us if fin else us + _FIN_PENALTY_US
+
+        ext = _ext.load()
+        ext.bn_acc_scratch(True)
+        try:
+            for v in variants_for(cout) + split_variants_for(m_out, cout, cin * k[0] * k[1]):
+                t[("fwd", v)] = fwd_time(v)
+            for v in persist_variants_for(m_out, cout, _best(t, "fwd", 3)):
+                t[("fwd", v)] = fwd_time(v)
+        finally:
+            ext.bn_acc_scratch(False)
         if stride == 1:
             m_in = x.shape[0] * x.shape[2] * x.shape[3]
             for v in variants_for(cin) + split_variants_for(m_in, cin, cout * k[0] * k[1]):
+                t[("bwd", v)] = _time(lambda: conv2d_bwd_data(dy, w, pad, v))
+            for v in persist_variants_for(m_in, cin, _best(t, "bwd", 3)):
                 t[("bwd", v)] = _time(lambda: conv2d_bwd_data(dy, w, pad, v))
         else:   # phase decomposition: per-phase heuristic (-1) or one tile for every phase
             hw = (x.shape[2], x.shape[3])
@@ -782,7 +846,7 @@ class _ConvFn(torch.autograd.Function):
         part = x.new_empty(0, dtype=torch.float32)
         if plan.fwd == MIOPEN:
             y = F.conv2d(x, w, stride=stride, padding=pad)
-        elif want_stats and _use_acc(_out_pixels(x, w, stride, pad), TILES[plan.fwd][0],
+        elif want_stats and _use_acc(_out_pixels(x, w, stride, pad), plan.fwd,
                                      w.shape[0]):
             y, st = conv2d_fwd(x, w, stride, pad, plan.fwd, with_stats=True, final=True)
             part = st.fin

@@ -65,7 +65,7 @@ hipError_t arena_conv_flip_multi(int, const void* const*, void* const*, const in
 hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void*, const uint8_t*,
                              const void*, const uint8_t*, const float*, int, int, int, int, int,
                              int, int, int, int, int, int, int, const int*, int, int, double*,
-                             int, void*, unsigned*, hipStream_t);
+                             int, void*, unsigned*, int, hipStream_t);
 long long arena_conv_fwd_ksplit_floats(long long, int, int, int);
 long long arena_conv_fwd_tiles(long long, int, int);
 int arena_conv_fwd_tile_rows(int);
@@ -740,12 +740,23 @@ std::vector<AccPool>& acc_pools() {
   return pools;
 }
 
+// Scratch mode (conv autotuning, ops/conv.py plan_for): every request gets one fixed set that is
+// never zeroed -- timed launches only need somewhere to add, and must not dirty the pool.
+bool g_acc_scratch = false;
+
 Tensor bn_acc_set(const Tensor& like, int64_t C) {
   TORCH_CHECK(C > 0 && C <= kAccC, "BatchNorm acc mode: C must be <= ", kAccC);
   auto& pools = acc_pools();
   const int dev = like.get_device();
   if ((int)pools.size() <= dev) pools.resize(dev + 1);
   AccPool& p = pools[dev];
+  if (g_acc_scratch) {
+    static std::vector<Tensor> scratch;
+    if ((int)scratch.size() <= dev) scratch.resize(dev + 1);
+    if (!scratch[dev].defined())
+      scratch[dev] = torch::zeros({2 * kAccC}, like.options().dtype(torch::kFloat64));
+    return scratch[dev].narrow(0, 0, 2 * C).view({2, C});
+  }
   if (!p.t.defined()) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     check_hip(hipStreamIsCapturing(cur_stream(), &cs), "bn_acc_set");
@@ -804,9 +815,10 @@ unsigned* conv_tickets(const Tensor& like, int64_t tiles) {
   return p;
 }
 
-// conv variant code: tile/pipeline variant (0..11) + 16 * (ksplit - 1)
+// conv variant code: tile/pipeline variant (0..15) + 16 * (ksplit - 1) + 256 * p, where p > 0
+// selects the persistent form with 2^p output tiles per block (not with split-K)
 struct ConvSplit {
-  int base = 0, ks = 1;
+  int base = 0, ks = 1, tpb = 1;
   Tensor ws;
   unsigned* cnt = nullptr;
 };
@@ -815,7 +827,10 @@ ConvSplit conv_split(const Tensor& x, int64_t variant, int64_t M, int64_t Cout, 
   ConvSplit s;
   TORCH_CHECK(variant >= 0, "conv: bad variant ", variant);
   s.base = (int)(variant % 16);
-  s.ks = (int)(variant / 16) + 1;
+  s.ks = (int)(variant % 256 / 16) + 1;
+  const int p = (int)(variant / 256);
+  TORCH_CHECK(p <= 4 && (p == 0 || s.ks == 1), "conv: bad persistent variant ", variant);
+  s.tpb = 1 << p;
   TORCH_CHECK(s.base <= 15, "conv: variant ", variant, " is not a tile variant");
   TORCH_CHECK((s.base & 1) || Cout % 128 == 0, "conv: variant ", variant,
               " needs Cout % 128 == 0 (Cout = ", Cout, ")");
@@ -1127,7 +1142,8 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                               (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R, (int)S,
                               (int)stride, (int)pad, (int)pad, 0, 0, nullptr, 0, ks.base,
                               fin ? acc_t.data_ptr<double>() : nullptr, ks.ks,
-                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, cur_stream()),
+                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, ks.tpb,
+                              cur_stream()),
             "conv_fwd");
   if (fin) return {y, acc_t};
   if (with_stats) return {y, part};
@@ -1290,7 +1306,8 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
                               (int)stride, (int)pad_h, (int)pad_w, (int)Ho, (int)Wo,
                               y_out.has_value() ? map6.data() : nullptr, c16 ? 1 : 0,
                               ks.base, fin ? acc_t.data_ptr<double>() : nullptr, ks.ks,
-                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, cur_stream()),
+                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, ks.tpb,
+                              cur_stream()),
             "conv_fwd_ex");
   if (fin) return {y, acc_t};
   if (with_stats) return {y, part};
@@ -1622,6 +1639,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_set_fin_max_blocks", [](int64_t p) { arena_bn_set_fin_max_blocks((int)p); });
   m.def("bn_set_nt", [](int64_t on) { arena_bn_set_nt((int)on); });
   m.def("bn_set_acc", [](bool on) { g_bn_acc = on; });
+  m.def("bn_acc_scratch", [](bool on) { g_acc_scratch = on; });
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
     arena_bn_set_reduce_geometry(max_blocks, min_rounds);
   });

@@ -102,6 +102,7 @@ struct ConvArgs {
   float4* kws;
   unsigned* kcnt;
   int xbytes, wbytes;  // buffer-descriptor ranges of x and w (both < 2^31 bytes, host-checked)
+  int tpb;             // output tiles per block (persistent form, see conv_fwd_body); 1 = one
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -179,9 +180,17 @@ __device__ __forceinline__ float row16_sum(float v) {
 // restaged in LDS so that consecutive lanes add to consecutive channels: 64 fp64 adds = 512
 // contiguous bytes per wave instruction (scattered few-lane atomics cost one 64-B memory-side
 // request each). No wait and no fence: the kernel's end makes the sums visible to the finalize.
+template <int BN>
+__device__ __forceinline__ double* bn_lacc_storage() {
+  __shared__ double s[2 * BN];
+  return s;
+}
+
+// lacc != null (persistent tiles): the sums are added into the block's LDS set lacc [2][BN] by
+// the same owner thread per channel instead, and flushed once after the last tile.
 template <int BM, int BN, int NT, typename Emit>
 __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int n0, int nrows,
-                                                Emit&& emit) {
+                                                double* lacc, Emit&& emit) {
   __shared__ float s_st[2][BN];
   emit([&](int c, float mean, float m2) {
     s_st[0][c] = mean;
@@ -194,8 +203,14 @@ __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int n0, int n
   const double n = (double)nrows;
   for (int c = threadIdx.x; c < BN; c += NT) {
     const double mu = (double)s_st[0][c];
-    unsafeAtomicAdd(acc + c, n * mu);                                     // sum y
-    unsafeAtomicAdd(acc + a.Cout + c, (double)s_st[1][c] + n * mu * mu);  // sum y^2
+    const double s1 = n * mu, s2 = (double)s_st[1][c] + n * mu * mu;
+    if (lacc != nullptr) {
+      lacc[c] += s1;
+      lacc[BN + c] += s2;
+    } else {
+      unsafeAtomicAdd(acc + c, s1);             // sum y
+      unsafeAtomicAdd(acc + a.Cout + c, s2);    // sum y^2
+    }
   }
 }
 
@@ -215,7 +230,11 @@ __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int n0, int n
 // arithmetic of the flat form (a tap division, bounds checks and 64-bit addresses per slot per
 // step) issued ~115 VALU and ~140 SALU per K step against 16 MFMAs (the kernels were
 // issue-bound, not load-bound). C16 = true is the stem's space-to-depth form on flat loads.
-template <int BM, int BN, int EPI, int NBUF = 2, int NWM = 2, int NWN = 2, bool C16 = false>
+// PT: the persistent form (a.tpb output tiles per block); a separate instantiation, because the
+// tile loop costs 30-60 VGPRs even when it runs once (hipcc keeps the per-tile staging state live
+// across the back edge), which spilled the high-occupancy variants.
+template <int BM, int BN, int EPI, int NBUF = 2, int NWM = 2, int NWN = 2, bool C16 = false,
+          bool PT = false>
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WM = BM / NWM, WN = BN / NWN;    // per-wave output tile
@@ -231,625 +250,658 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
   // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin dispatch), so give each XCD
   // a contiguous range of tiles (bijective for any grid size).
   const int ks = a.ksplit;
-  const int nwg = a.m_tiles * a.n_tiles * ks;
+  // Persistent tiles (a.tpb > 1, never with split-K): block `lin` computes the output tiles
+  // (mt0 + i, nt), i < tpb, of one column tile, so its BatchNorm sums (acc mode) are merged in LDS
+  // across them and reach memory once per block: 1/tpb of the fp64 atomics onto the [2][Cout]
+  // set, which per-tile flushing made too slow for the 56x56 / 28x28 layers (~800 k pairs). The
+  // lin order keeps a row chunk's column tiles consecutive (one XCD: the A rows hit its L2).
+  const int tpb = PT ? a.tpb : 1;
+  const int nwg = tpb > 1 ? (a.m_tiles + tpb - 1) / tpb * a.n_tiles : a.m_tiles * a.n_tiles * ks;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
   const int lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
   // a tile's K slices are consecutive in the XCD order: the last arriver reads same-XCD slabs
-  const int tile = ks > 1 ? lin / ks : lin, slice = ks > 1 ? lin - tile * ks : 0;
-  const int mt = tile / a.n_tiles, nt = tile - mt * a.n_tiles;
-  const int m0 = mt * BM, n0 = nt * BN;
-
-  // ---- per-thread staging descriptors: row and (swizzled) source chunk of every glds ----
-  // slot s = (wave*AI + i)*64 + lane -> LDS row s/8, chunk position s%8 (= lane%8)
-  const int pos = lane & 7;
-  int a_hb[AI], a_wb[AI], a_nb[AI], a_chunk[AI];
-#pragma unroll
-  for (int i = 0; i < AI; ++i) {
-    const int row = (wave * AI + i) * 8 + (lane >> 3);
-    a_chunk[i] = pos ^ swz(row);
-    const int m = m0 + row;
-    if (m < a.M) {
-      const int hw = a.Ho * a.Wo;
-      const int n = m / hw, rem = m - n * hw;
-      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-      a_hb[i] = ho * a.stride - a.pad;
-      a_wb[i] = wo * a.stride - a.pad_w;
-      a_nb[i] = n * a.H;
-    } else {
-      a_hb[i] = -(1 << 28);  // every tap invalid -> zero page
-      a_wb[i] = 0;
-      a_nb[i] = 0;
+  const int tile0 = tpb > 1 ? lin : (ks > 1 ? lin / ks : lin);
+  const int slice = (tpb == 1 && ks > 1) ? lin - tile0 * ks : 0;
+  const int nt = tile0 % a.n_tiles;
+  const int mt0 = tpb > 1 ? tile0 / a.n_tiles * tpb : tile0 / a.n_tiles;
+  const int n0 = nt * BN;
+  // block-level BatchNorm sums of the persistent form (EPI 1, acc mode): [2][BN], one owner
+  // thread per channel (the same thread in every tile's epilogue, so no barrier between them)
+  double* lacc = nullptr;
+  if constexpr (EPI == 1) {
+    if (tpb > 1 && a.bn_acc != nullptr) {
+      lacc = bn_lacc_storage<BN>();
+      for (int c = threadIdx.x; c < BN; c += NT) lacc[c] = lacc[BN + c] = 0.0;
     }
   }
-  const uint16_t* b_src[BI];
-#pragma unroll
-  for (int i = 0; i < BI; ++i) {
-    const int row = (wave * BI + i) * 8 + (lane >> 3);
-    b_src[i] = a.w + (size_t)(n0 + row) * a.Ktot + (pos ^ swz(row)) * 8;
-  }
-  const int CB = C16 ? 1 : a.C / kBK;  // 64-channel blocks per tap
-  // this block's K steps: [t0, t0 + T) of the Ktot / kBK (split-K: slice `slice` of ks)
-  const int Tall = a.Ktot / kBK;
-  const int t0 = (int)((long long)Tall * slice / ks);
-  const int T = (int)((long long)Tall * (slice + 1) / ks) - t0;
 
-  // ---- descriptor staging state (C16 == false) ----
-  constexpr uint32_t kOOB = 0x80000000u;   // >= num_records: the load returns zeros
-  const __amdgpu_buffer_rsrc_t xrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
-  int a_lane[AI];          // byte offset of the slot's 16-byte chunk at tap (0, 0), channel block 0
-  uint32_t a_mask[AI];     // bit r*S+s: tap (r, s) inside the image for this slot's pixel
-  uint32_t a_cur[AI];      // the current tap's offset, or kOOB
-  uint32_t b_voff[BI];
-  int s_tap = 0, s_cb = 0, s_s = 0, s_tapoff = 0, s_t = t0;   // scalar K-step state
-  if constexpr (!C16) {
+#pragma unroll 1
+  for (int it = 0; it < tpb; ++it) {
+    const int mt = mt0 + it;
+    if (mt >= a.m_tiles) break;
+    if (it > 0) lds_barrier();   // the previous tile's epilogue is done with the stage LDS
+    const int tile = mt * a.n_tiles + nt;
+    const int m0 = mt * BM;
+
+    // ---- per-thread staging descriptors: row and (swizzled) source chunk of every glds ----
+    // slot s = (wave*AI + i)*64 + lane -> LDS row s/8, chunk position s%8 (= lane%8)
+    const int pos = lane & 7;
+    int a_hb[AI], a_wb[AI], a_nb[AI], a_chunk[AI];
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
       const int row = (wave * AI + i) * 8 + (lane >> 3);
-      uint32_t mk = 0u;
-      int off = 0;
-      if (a_hb[i] > -(1 << 27)) {
-        for (int r = 0; r < a.R; ++r) {
-          if ((unsigned)(a_hb[i] + r) >= (unsigned)a.H) continue;
-          for (int s2 = 0; s2 < a.S; ++s2)
-            if ((unsigned)(a_wb[i] + s2) < (unsigned)a.W) mk |= 1u << (r * a.S + s2);
-        }
-        off = (((a_nb[i] + a_hb[i]) * a.W + a_wb[i]) * a.C + a_chunk[i] * 8) * 2;
+      a_chunk[i] = pos ^ swz(row);
+      const int m = m0 + row;
+      if (m < a.M) {
+        const int hw = a.Ho * a.Wo;
+        const int n = m / hw, rem = m - n * hw;
+        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+        a_hb[i] = ho * a.stride - a.pad;
+        a_wb[i] = wo * a.stride - a.pad_w;
+        a_nb[i] = n * a.H;
+      } else {
+        a_hb[i] = -(1 << 28);  // every tap invalid -> zero page
+        a_wb[i] = 0;
+        a_nb[i] = 0;
       }
-      (void)row;
-      a_lane[i] = off;
-      a_mask[i] = mk;
     }
+    const uint16_t* b_src[BI];
 #pragma unroll
     for (int i = 0; i < BI; ++i) {
       const int row = (wave * BI + i) * 8 + (lane >> 3);
-      b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
+      b_src[i] = a.w + (size_t)(n0 + row) * a.Ktot + (pos ^ swz(row)) * 8;
     }
-    s_tap = t0 / CB;
-    s_cb = t0 - s_tap * CB;
-    const int r0 = s_tap / a.S;
-    s_s = s_tap - r0 * a.S;
-    s_tapoff = (r0 * a.W + s_s) * a.C * 2;
-#pragma unroll
-    for (int i = 0; i < AI; ++i)
-      a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
-  }
+    const int CB = C16 ? 1 : a.C / kBK;  // 64-channel blocks per tap
+    // this block's K steps: [t0, t0 + T) of the Ktot / kBK (split-K: slice `slice` of ks)
+    const int Tall = a.Ktot / kBK;
+    const int t0 = (int)((long long)Tall * slice / ks);
+    const int T = (int)((long long)Tall * (slice + 1) / ks) - t0;
 
-  auto stage = [&](int tl, int buf) {
-    const int t = t0 + tl;
-    uint8_t* base = lds + buf * kBufBytes;
+    // ---- descriptor staging state (C16 == false) ----
+    constexpr uint32_t kOOB = 0x80000000u;   // >= num_records: the load returns zeros
+    const __amdgpu_buffer_rsrc_t xrsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+    const __amdgpu_buffer_rsrc_t wrsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+    int a_lane[AI];          // byte offset of the slot's 16-byte chunk at tap (0, 0), channel block 0
+    uint32_t a_mask[AI];     // bit r*S+s: tap (r, s) inside the image for this slot's pixel
+    uint32_t a_cur[AI];      // the current tap's offset, or kOOB
+    uint32_t b_voff[BI];
+    int s_tap = 0, s_cb = 0, s_s = 0, s_tapoff = 0, s_t = t0;   // scalar K-step state
     if constexpr (!C16) {
-      (void)t;
-      const int coff = s_cb * kRowBytes;   // channel block within the tap (scalar)
+#pragma unroll
+      for (int i = 0; i < AI; ++i) {
+        const int row = (wave * AI + i) * 8 + (lane >> 3);
+        uint32_t mk = 0u;
+        int off = 0;
+        if (a_hb[i] > -(1 << 27)) {
+          for (int r = 0; r < a.R; ++r) {
+            if ((unsigned)(a_hb[i] + r) >= (unsigned)a.H) continue;
+            for (int s2 = 0; s2 < a.S; ++s2)
+              if ((unsigned)(a_wb[i] + s2) < (unsigned)a.W) mk |= 1u << (r * a.S + s2);
+          }
+          off = (((a_nb[i] + a_hb[i]) * a.W + a_wb[i]) * a.C + a_chunk[i] * 8) * 2;
+        }
+        (void)row;
+        a_lane[i] = off;
+        a_mask[i] = mk;
+      }
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        const int row = (wave * BI + i) * 8 + (lane >> 3);
+        b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
+      }
+      s_tap = t0 / CB;
+      s_cb = t0 - s_tap * CB;
+      const int r0 = s_tap / a.S;
+      s_s = s_tap - r0 * a.S;
+      s_tapoff = (r0 * a.W + s_s) * a.C * 2;
 #pragma unroll
       for (int i = 0; i < AI; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_ptr_t)(base + (wave * AI + i) * 64 * 16),
-                                                 16, a_cur[i], coff, 0, 0);
-      uint8_t* bb = base + BM * kRowBytes;
-#pragma unroll
-      for (int i = 0; i < BI; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
-                                                 16, b_voff[i], s_t * kRowBytes, 0, 0);
-      // advance the scalar state to the next K step
-      ++s_t;
-      if (++s_cb == CB) {
-        s_cb = 0;
-        ++s_tap;
-        s_tapoff += a.C * 2;
-        if (++s_s == a.S) {
-          s_s = 0;
-          s_tapoff += (a.W - a.S) * a.C * 2;
-        }
+        a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
+    }
+
+    auto stage = [&](int tl, int buf) {
+      const int t = t0 + tl;
+      uint8_t* base = lds + buf * kBufBytes;
+      if constexpr (!C16) {
+        (void)t;
+        const int coff = s_cb * kRowBytes;   // channel block within the tap (scalar)
 #pragma unroll
         for (int i = 0; i < AI; ++i)
-          a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
-      }
-      return;
-    }
-    if (C16) {
-      // K step t = filter row r, columns 4*sb .. 4*sb+3; 16-byte chunk c = pixel c/2, half c%2
-      const int SB = a.S >> 2;
-      const int r = t / SB, sb = t - r * SB;
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_ptr_t)(base + (wave * AI + i) * 64 * 16),
+                                                   16, a_cur[i], coff, 0, 0);
+        uint8_t* bb = base + BM * kRowBytes;
 #pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        const int c = a_chunk[i];
-        const int hi = a_hb[i] + r, wi = a_wb[i] + sb * 4 + (c >> 1);
-        const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-        const void* src = ok ? (const void*)(a.x + ((size_t)(a_nb[i] + hi) * a.W + wi) * 16 +
-                                             (c & 1) * 8)
-                             : (const void*)g_zero_page;
-        glds16(src, base + (wave * AI + i) * 64 * 16);
+        for (int i = 0; i < BI; ++i)
+          __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
+                                                   16, b_voff[i], s_t * kRowBytes, 0, 0);
+        // advance the scalar state to the next K step
+        ++s_t;
+        if (++s_cb == CB) {
+          s_cb = 0;
+          ++s_tap;
+          s_tapoff += a.C * 2;
+          if (++s_s == a.S) {
+            s_s = 0;
+            s_tapoff += (a.W - a.S) * a.C * 2;
+          }
+#pragma unroll
+          for (int i = 0; i < AI; ++i)
+            a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
+        }
+        return;
+      }
+      if (C16) {
+        // K step t = filter row r, columns 4*sb .. 4*sb+3; 16-byte chunk c = pixel c/2, half c%2
+        const int SB = a.S >> 2;
+        const int r = t / SB, sb = t - r * SB;
+#pragma unroll
+        for (int i = 0; i < AI; ++i) {
+          const int c = a_chunk[i];
+          const int hi = a_hb[i] + r, wi = a_wb[i] + sb * 4 + (c >> 1);
+          const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+          const void* src = ok ? (const void*)(a.x + ((size_t)(a_nb[i] + hi) * a.W + wi) * 16 +
+                                               (c & 1) * 8)
+                               : (const void*)g_zero_page;
+          glds16(src, base + (wave * AI + i) * 64 * 16);
+        }
+      } else {
+        const int tap = t / CB, cb = t - tap * CB;
+        const int r = tap / a.S, s = tap - r * a.S;
+#pragma unroll
+        for (int i = 0; i < AI; ++i) {
+          const int hi = a_hb[i] + r, wi = a_wb[i] + s;
+          const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
+          const void* src = ok ? (const void*)(a.x + ((size_t)(a_nb[i] + hi) * a.W + wi) * a.C +
+                                               cb * kBK + a_chunk[i] * 8)
+                               : (const void*)g_zero_page;
+          glds16(src, base + (wave * AI + i) * 64 * 16);
+        }
+      }
+      uint8_t* bbase = base + BM * kRowBytes;
+#pragma unroll
+      for (int i = 0; i < BI; ++i) glds16(b_src[i] + (size_t)t * kBK, bbase + (wave * BI + i) * 64 * 16);
+    };
+    (void)a_cur;
+
+    f32x4v acc[MI][NI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
+
+    const int wm = wave / NWN, wn = wave % NWN;
+    const int fr = lane & 15, fq = lane >> 4;
+
+    auto compute = [&](int buf) {
+      const uint8_t* abuf = lds + buf * kBufBytes;
+      const uint8_t* bbuf = abuf + BM * kRowBytes;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        bf16x8 af[MI], bfr[NI];
+        const int c = kk * 4 + fq;  // global 16-byte chunk of this lane's 8 k values
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int row = wm * WM + i * 16 + fr;
+          af[i] = *reinterpret_cast<const bf16x8*>(abuf + row * kRowBytes + ((c ^ swz(row)) << 4));
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int row = wn * WN + j * 16 + fr;
+          bfr[j] = *reinterpret_cast<const bf16x8*>(bbuf + row * kRowBytes + ((c ^ swz(row)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    };
+
+    if constexpr (NBUF == 3) {
+      // Three stage buffers, two K steps in flight: the glds of step t+2 stay outstanding across
+      // the barrier that publishes step t+1 (counted vmcnt = this thread's glds of ONE stage, raw
+      // s_barrier: __syncthreads() would drain every outstanding LDS-DMA with a vmcnt(0)).
+      // RAW: stage t+1 is read in iteration t+1, after the vmcnt that retired it and a barrier.
+      // WAR: stage t+2 overwrites buffer (t-1)%3, whose reads finished before iteration t-1's barrier.
+      constexpr int kLps = AI + BI;   // glds per thread per stage
+      stage(0, 0);
+      if (T > 1) {
+        stage(1, 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLps) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      int cur = 0;
+      for (int t = 0; t < T; ++t) {
+        if (t + 2 < T) stage(t + 2, cur == 0 ? 2 : cur - 1);
+        compute(cur);
+        if (t + 2 < T)
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kLps) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        cur = cur == 2 ? 0 : cur + 1;
       }
     } else {
-      const int tap = t / CB, cb = t - tap * CB;
-      const int r = tap / a.S, s = tap - r * a.S;
-#pragma unroll
-      for (int i = 0; i < AI; ++i) {
-        const int hi = a_hb[i] + r, wi = a_wb[i] + s;
-        const bool ok = (unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W;
-        const void* src = ok ? (const void*)(a.x + ((size_t)(a_nb[i] + hi) * a.W + wi) * a.C +
-                                             cb * kBK + a_chunk[i] * 8)
-                             : (const void*)g_zero_page;
-        glds16(src, base + (wave * AI + i) * 64 * 16);
+      stage(0, 0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+
+      for (int t = 0; t < T; ++t) {
+        const int cur = NBUF == 1 ? 0 : (t & 1);
+        if (NBUF == 2 && t + 1 < T) stage(t + 1, cur ^ 1);
+        compute(cur);
+        if (NBUF == 1 && t + 1 < T) {   // serial: every wave is done with the buffer, restage it
+          __syncthreads();
+          stage(t + 1, 0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
       }
     }
-    uint8_t* bbase = base + BM * kRowBytes;
-#pragma unroll
-    for (int i = 0; i < BI; ++i) glds16(b_src[i] + (size_t)t * kBK, bbase + (wave * BI + i) * 64 * 16);
-  };
-  (void)a_cur;
 
-  f32x4v acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j) acc[i][j] = f32x4v{0.f, 0.f, 0.f, 0.f};
-
-  const int wm = wave / NWN, wn = wave % NWN;
-  const int fr = lane & 15, fq = lane >> 4;
-
-  auto compute = [&](int buf) {
-    const uint8_t* abuf = lds + buf * kBufBytes;
-    const uint8_t* bbuf = abuf + BM * kRowBytes;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[MI], bfr[NI];
-      const int c = kk * 4 + fq;  // global 16-byte chunk of this lane's 8 k values
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int row = wm * WM + i * 16 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(abuf + row * kRowBytes + ((c ^ swz(row)) << 4));
-      }
-#pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int row = wn * WN + j * 16 + fr;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(bbuf + row * kRowBytes + ((c ^ swz(row)) << 4));
-      }
+    if (ks > 1) {
+      // ---- split-K hand-off (cdna_hip_programming.md §5 "In-launch split-K reduction") ----
+      constexpr int NA = MI * NI;
+      float4* slab = a.kws + (size_t)tile * ks * NA * NT;
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-  };
-
-  if constexpr (NBUF == 3) {
-    // Three stage buffers, two K steps in flight: the glds of step t+2 stay outstanding across
-    // the barrier that publishes step t+1 (counted vmcnt = this thread's glds of ONE stage, raw
-    // s_barrier: __syncthreads() would drain every outstanding LDS-DMA with a vmcnt(0)).
-    // RAW: stage t+1 is read in iteration t+1, after the vmcnt that retired it and a barrier.
-    // WAR: stage t+2 overwrites buffer (t-1)%3, whose reads finished before iteration t-1's barrier.
-    constexpr int kLps = AI + BI;   // glds per thread per stage
-    stage(0, 0);
-    if (T > 1) {
-      stage(1, 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLps) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    int cur = 0;
-    for (int t = 0; t < T; ++t) {
-      if (t + 2 < T) stage(t + 2, cur == 0 ? 2 : cur - 1);
-      compute(cur);
-      if (t + 2 < T)
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kLps) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      cur = cur == 2 ? 0 : cur + 1;
-    }
-  } else {
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-
-    for (int t = 0; t < T; ++t) {
-      const int cur = NBUF == 1 ? 0 : (t & 1);
-      if (NBUF == 2 && t + 1 < T) stage(t + 1, cur ^ 1);
-      compute(cur);
-      if (NBUF == 1 && t + 1 < T) {   // serial: every wave is done with the buffer, restage it
-        __syncthreads();
-        stage(t + 1, 0);
-      }
+          slab[((size_t)slice * NA + i * NI + j) * NT + tid] =
+              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-    }
-  }
-
-  if (ks > 1) {
-    // ---- split-K hand-off (cdna_hip_programming.md §5 "In-launch split-K reduction") ----
-    constexpr int NA = MI * NI;
-    float4* slab = a.kws + (size_t)tile * ks * NA * NT;
+      // the flag travels through the stage LDS (free: the K loop ended on a barrier); a second
+      // __shared__ object would perturb the K loop's waits (cdna_hip_programming.md §5 item 4a)
+      volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(lds);
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned old =
+            __hip_atomic_fetch_add(a.kcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned last = old == (unsigned)(ks - 1) ? 1u : 0u;
+        if (last) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          a.kcnt[tile] = 0u;   // ready for the next launch (kernel boundary orders it)
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        flag[0] = last;
+      }
+      __syncthreads();
+      const unsigned last = flag[0];
+      __syncthreads();   // every wave has read the flag before the epilogue reuses the LDS
+      if (!last) return;
+      // sum the slices in slice order (this block's own slab re-read from memory: the order, and
+      // so the rounding, is independent of which block arrived last)
 #pragma unroll
-    for (int i = 0; i < MI; ++i)
+      for (int i = 0; i < MI; ++i) {
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const float4 v = slab[(size_t)(i * NI + j) * NT + tid];
+          acc[i][j] = f32x4v{v.x, v.y, v.z, v.w};
+        }
+        for (int s = 1; s < ks; ++s) {
+          float4 v[NI];
+#pragma unroll
+          for (int j = 0; j < NI; ++j) v[j] = slab[((size_t)s * NA + i * NI + j) * NT + tid];
+#pragma unroll
+          for (int j = 0; j < NI; ++j) acc[i][j] += f32x4v{v[j].x, v[j].y, v[j].z, v[j].w};
+        }
+      }
+    }
+
+    // ---- epilogue: lane holds channels n0+wn*WN+j*16+4*fq .. +3 of pixel m0+wm*WM+i*16+fr ----
+    // EPI 2 operands, issued before the stores so their latency overlaps them (clamped addresses)
+    uint2 bx[EPI == 2 ? MI : 1][EPI == 2 ? NI : 1];
+    uint32_t bm[EPI == 2 ? MI : 1][EPI == 2 ? NI : 1];
+    float4 bmu[EPI == 2 ? NI : 1];
+    if constexpr (EPI == 2) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = min(m0 + wm * WM + i * 16 + fr, a.M - 1);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int c0 = n0 + wn * WN + j * 16 + 4 * fq;
+          bx[i][j] = *reinterpret_cast<const uint2*>(a.bnx + (size_t)m * a.Cout + c0);
+          bm[i][j] = a.bnmask ? ((uint32_t)a.bnmask[(size_t)m * (a.Cout >> 3) + (c0 >> 3)] >>
+                                 (c0 & 7)) : 0xfu;
+          if (m0 + wm * WM + i * 16 + fr >= a.M) bm[i][j] = 0u;   // rows past M: no contribution
+        }
+      }
 #pragma unroll
       for (int j = 0; j < NI; ++j)
-        slab[((size_t)slice * NA + i * NI + j) * NT + tid] =
-            make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    // the flag travels through the stage LDS (free: the K loop ended on a barrier); a second
-    // __shared__ object would perturb the K loop's waits (cdna_hip_programming.md §5 item 4a)
-    volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(lds);
-    if (tid == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned old =
-          __hip_atomic_fetch_add(a.kcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned last = old == (unsigned)(ks - 1) ? 1u : 0u;
-      if (last) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        a.kcnt[tile] = 0u;   // ready for the next launch (kernel boundary orders it)
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      flag[0] = last;
+        bmu[j] = *reinterpret_cast<const float4*>(a.bnmean + n0 + wn * WN + j * 16 + 4 * fq);
     }
-    __syncthreads();
-    const unsigned last = flag[0];
-    __syncthreads();   // every wave has read the flag before the epilogue reuses the LDS
-    if (!last) return;
-    // sum the slices in slice order (this block's own slab re-read from memory: the order, and
-    // so the rounding, is independent of which block arrived last)
+    // EPI 1: round the accumulators to their stored bf16 values once; the stores (whose own
+    // rounding is then exact) and the statistics below both read them.
+    if constexpr (EPI == 1) {
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const float4 v = slab[(size_t)(i * NI + j) * NT + tid];
-        acc[i][j] = f32x4v{v.x, v.y, v.z, v.w};
-      }
-      for (int s = 1; s < ks; ++s) {
-        float4 v[NI];
+        for (int j = 0; j < NI; ++j)
 #pragma unroll
-        for (int j = 0; j < NI; ++j) v[j] = slab[((size_t)s * NA + i * NI + j) * NT + tid];
-#pragma unroll
-        for (int j = 0; j < NI; ++j) acc[i][j] += f32x4v{v[j].x, v[j].y, v[j].z, v[j].w};
-      }
+          for (int r = 0; r < 4; r += 2) {
+            const uint32_t u = pack_bf16x2(acc[i][j][r], acc[i][j][r + 1]);
+            acc[i][j][r] = __uint_as_float(u << 16);
+            acc[i][j][r + 1] = __uint_as_float(u & 0xffff0000u);
+          }
     }
-  }
-
-  // ---- epilogue: lane holds channels n0+wn*WN+j*16+4*fq .. +3 of pixel m0+wm*WM+i*16+fr ----
-  // EPI 2 operands, issued before the stores so their latency overlaps them (clamped addresses)
-  uint2 bx[EPI == 2 ? MI : 1][EPI == 2 ? NI : 1];
-  uint32_t bm[EPI == 2 ? MI : 1][EPI == 2 ? NI : 1];
-  float4 bmu[EPI == 2 ? NI : 1];
-  if constexpr (EPI == 2) {
+    if (a.coal && !(EPI != 0 && a.add != nullptr)) {
+      // ---- coalesced store through LDS (stage buffers are free: the K loop ended on a barrier) ----
+      float* stg = reinterpret_cast<float*>(lds);
+      constexpr int F4R = BN / 4;   // float4 slots per staged row (>= 16: the XOR below stays inside)
+      constexpr int CPR = BN / 8;   // 16-byte bf16 output chunks per row
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int m = min(m0 + wm * WM + i * 16 + fr, a.M - 1);
+      for (int h = 0; h < NWM; ++h) {
+        if (h) lds_barrier();       // every reader of the first half is done
+        if (wm == h) {
 #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int c0 = n0 + wn * WN + j * 16 + 4 * fq;
-        bx[i][j] = *reinterpret_cast<const uint2*>(a.bnx + (size_t)m * a.Cout + c0);
-        bm[i][j] = a.bnmask ? ((uint32_t)a.bnmask[(size_t)m * (a.Cout >> 3) + (c0 >> 3)] >>
-                               (c0 & 7)) : 0xfu;
-        if (m0 + wm * WM + i * 16 + fr >= a.M) bm[i][j] = 0u;   // rows past M: no contribution
-      }
-    }
+          for (int i = 0; i < MI; ++i) {
+            const int row = i * 16 + fr;
 #pragma unroll
-    for (int j = 0; j < NI; ++j)
-      bmu[j] = *reinterpret_cast<const float4*>(a.bnmean + n0 + wn * WN + j * 16 + 4 * fq);
-  }
-  // EPI 1: round the accumulators to their stored bf16 values once; the stores (whose own
-  // rounding is then exact) and the statistics below both read them.
-  if constexpr (EPI == 1) {
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          const uint32_t u = pack_bf16x2(acc[i][j][r], acc[i][j][r + 1]);
-          acc[i][j][r] = __uint_as_float(u << 16);
-          acc[i][j][r + 1] = __uint_as_float(u & 0xffff0000u);
-        }
-  }
-  if (a.coal && !(EPI != 0 && a.add != nullptr)) {
-    // ---- coalesced store through LDS (stage buffers are free: the K loop ended on a barrier) ----
-    float* stg = reinterpret_cast<float*>(lds);
-    constexpr int F4R = BN / 4;   // float4 slots per staged row (>= 16: the XOR below stays inside)
-    constexpr int CPR = BN / 8;   // 16-byte bf16 output chunks per row
-#pragma unroll
-    for (int h = 0; h < NWM; ++h) {
-      if (h) lds_barrier();       // every reader of the first half is done
-      if (wm == h) {
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int row = i * 16 + fr;
-#pragma unroll
-          for (int j = 0; j < NI; ++j) {
-            const int slot = (wn * WN + j * 16) / 4 + fq;
-            *reinterpret_cast<f32x4v*>(stg + (row * F4R + (slot ^ (row & 7))) * 4) = acc[i][j];
+            for (int j = 0; j < NI; ++j) {
+              const int slot = (wn * WN + j * 16) / 4 + fq;
+              *reinterpret_cast<f32x4v*>(stg + (row * F4R + (slot ^ (row & 7))) * 4) = acc[i][j];
+            }
           }
         }
-      }
-      lds_barrier();              // the staged half is complete (global stores may be in flight)
-      for (int q = tid; q < WM * CPR; q += NT) {
-        const int row = q / CPR, cc = q - row * CPR;
-        const int m = m0 + h * WM + row;
-        if (m >= a.M) continue;
-        const f32x4v lo = *reinterpret_cast<const f32x4v*>(stg + (row * F4R + ((2 * cc) ^ (row & 7))) * 4);
-        const f32x4v hi =
-            *reinterpret_cast<const f32x4v*>(stg + (row * F4R + ((2 * cc + 1) ^ (row & 7))) * 4);
-        float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-        size_t pix = (size_t)m;
-        int n = 0, ho = 0, wo = 0;
-        if (a.mapped) {
-          const int hw = a.Ho * a.Wo;
-          n = m / hw;
-          const int rem = m - n * hw;
-          ho = rem / a.Wo;
-          wo = rem - ho * a.Wo;
-          pix = ((size_t)n * a.Hy + ho * a.osh + a.ooh) * a.Wy + wo * a.osw + a.oow;
-        }
-        const size_t off = pix * a.Cout + n0 + cc * 8;
-        if (a.add != nullptr) {
-          const uint4 qa = masked_add8(a.add, a.addmask, off);
-          const uint32_t u[4] = {qa.x, qa.y, qa.z, qa.w};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            v[2 * e] += __uint_as_float(u[e] << 16);
-            v[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
+        lds_barrier();              // the staged half is complete (global stores may be in flight)
+        for (int q = tid; q < WM * CPR; q += NT) {
+          const int row = q / CPR, cc = q - row * CPR;
+          const int m = m0 + h * WM + row;
+          if (m >= a.M) continue;
+          const f32x4v lo = *reinterpret_cast<const f32x4v*>(stg + (row * F4R + ((2 * cc) ^ (row & 7))) * 4);
+          const f32x4v hi =
+              *reinterpret_cast<const f32x4v*>(stg + (row * F4R + ((2 * cc + 1) ^ (row & 7))) * 4);
+          float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+          size_t pix = (size_t)m;
+          int n = 0, ho = 0, wo = 0;
+          if (a.mapped) {
+            const int hw = a.Ho * a.Wo;
+            n = m / hw;
+            const int rem = m - n * hw;
+            ho = rem / a.Wo;
+            wo = rem - ho * a.Wo;
+            pix = ((size_t)n * a.Hy + ho * a.osh + a.ooh) * a.Wy + wo * a.osw + a.oow;
           }
-        }
-        *reinterpret_cast<uint4*>(a.y + off) =
-            make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                       pack_bf16x2(v[6], v[7]));
-        if (a.fill_sib) {
-          for (int da = 0; da < a.osh; ++da) {
-            const int hy = ho * a.osh + da;
-            if (hy >= a.Hy) break;
-            for (int db = 0; db < a.osw; ++db) {
-              const int wy = wo * a.osw + db;
-              if ((da == 0 && db == 0) || wy >= a.Wy) continue;
-              const size_t so = (((size_t)n * a.Hy + hy) * a.Wy + wy) * a.Cout + n0 + cc * 8;
-              *reinterpret_cast<uint4*>(a.y + so) =
-                  a.add ? masked_add8(a.add, a.addmask, so) : make_uint4(0u, 0u, 0u, 0u);
+          const size_t off = pix * a.Cout + n0 + cc * 8;
+          if (a.add != nullptr) {
+            const uint4 qa = masked_add8(a.add, a.addmask, off);
+            const uint32_t u[4] = {qa.x, qa.y, qa.z, qa.w};
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              v[2 * e] += __uint_as_float(u[e] << 16);
+              v[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
+            }
+          }
+          *reinterpret_cast<uint4*>(a.y + off) =
+              make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                         pack_bf16x2(v[6], v[7]));
+          if (a.fill_sib) {
+            for (int da = 0; da < a.osh; ++da) {
+              const int hy = ho * a.osh + da;
+              if (hy >= a.Hy) break;
+              for (int db = 0; db < a.osw; ++db) {
+                const int wy = wo * a.osw + db;
+                if ((da == 0 && db == 0) || wy >= a.Wy) continue;
+                const size_t so = (((size_t)n * a.Hy + hy) * a.Wy + wy) * a.Cout + n0 + cc * 8;
+                *reinterpret_cast<uint4*>(a.y + so) =
+                    a.add ? masked_add8(a.add, a.addmask, so) : make_uint4(0u, 0u, 0u, 0u);
+              }
             }
           }
         }
       }
-    }
-  } else {
+    } else {
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = m0 + wm * WM + i * 16 + fr;
-    if (m >= a.M) continue;
-    size_t pix = (size_t)m;
-    int n = 0, ho = 0, wo = 0;
-    if (a.mapped) {
-      const int hw = a.Ho * a.Wo;
-      n = m / hw;
-      const int rem = m - n * hw;
-      ho = rem / a.Wo;
-      wo = rem - ho * a.Wo;
-      pix = ((size_t)n * a.Hy + ho * a.osh + a.ooh) * a.Wy + wo * a.osw + a.oow;
-    }
-    uint16_t* yrow = a.y + pix * a.Cout + n0 + wn * WN + 4 * fq;
-    if (a.fill_sib) {
-      for (int da = 0; da < a.osh; ++da) {
-        const int hy = ho * a.osh + da;
-        if (hy >= a.Hy) break;
-        for (int db = 0; db < a.osw; ++db) {
-          const int wy = wo * a.osw + db;
-          if ((da == 0 && db == 0) || wy >= a.Wy) continue;
-          const size_t off = (((size_t)n * a.Hy + hy) * a.Wy + wy) * a.Cout + n0 + wn * WN + 4 * fq;
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * WM + i * 16 + fr;
+      if (m >= a.M) continue;
+      size_t pix = (size_t)m;
+      int n = 0, ho = 0, wo = 0;
+      if (a.mapped) {
+        const int hw = a.Ho * a.Wo;
+        n = m / hw;
+        const int rem = m - n * hw;
+        ho = rem / a.Wo;
+        wo = rem - ho * a.Wo;
+        pix = ((size_t)n * a.Hy + ho * a.osh + a.ooh) * a.Wy + wo * a.osw + a.oow;
+      }
+      uint16_t* yrow = a.y + pix * a.Cout + n0 + wn * WN + 4 * fq;
+      if (a.fill_sib) {
+        for (int da = 0; da < a.osh; ++da) {
+          const int hy = ho * a.osh + da;
+          if (hy >= a.Hy) break;
+          for (int db = 0; db < a.osw; ++db) {
+            const int wy = wo * a.osw + db;
+            if ((da == 0 && db == 0) || wy >= a.Wy) continue;
+            const size_t off = (((size_t)n * a.Hy + hy) * a.Wy + wy) * a.Cout + n0 + wn * WN + 4 * fq;
 #pragma unroll
-          for (int j = 0; j < NI; ++j) {
-            const uint2 v = a.add ? masked_add4(a.add, a.addmask, off + j * 16)
-                                  : make_uint2(0u, 0u);
-            *reinterpret_cast<uint2*>(a.y + off + j * 16) = v;
+            for (int j = 0; j < NI; ++j) {
+              const uint2 v = a.add ? masked_add4(a.add, a.addmask, off + j * 16)
+                                    : make_uint2(0u, 0u);
+              *reinterpret_cast<uint2*>(a.y + off + j * 16) = v;
+            }
           }
         }
       }
-    }
-    if (a.add != nullptr) {
-      const size_t aoff = (size_t)(yrow - a.y);
-      uint2 q[NI];
+      if (a.add != nullptr) {
+        const size_t aoff = (size_t)(yrow - a.y);
+        uint2 q[NI];
 #pragma unroll
-      for (int j = 0; j < NI; ++j) q[j] = masked_add4(a.add, a.addmask, aoff + j * 16);
+        for (int j = 0; j < NI; ++j) q[j] = masked_add4(a.add, a.addmask, aoff + j * 16);
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          acc[i][j][0] += __uint_as_float(q[j].x << 16);
+          acc[i][j][1] += __uint_as_float(q[j].x & 0xffff0000u);
+          acc[i][j][2] += __uint_as_float(q[j].y << 16);
+          acc[i][j][3] += __uint_as_float(q[j].y & 0xffff0000u);
+        }
+      }
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
-        acc[i][j][0] += __uint_as_float(q[j].x << 16);
-        acc[i][j][1] += __uint_as_float(q[j].x & 0xffff0000u);
-        acc[i][j][2] += __uint_as_float(q[j].y << 16);
-        acc[i][j][3] += __uint_as_float(q[j].y & 0xffff0000u);
+        uint2 v;
+        v.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+        v.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+        *reinterpret_cast<uint2*>(yrow + j * 16) = v;
       }
     }
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      uint2 v;
-      v.x = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
-      v.y = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-      *reinterpret_cast<uint2*>(yrow + j * 16) = v;
     }
-  }
-  }
-  if constexpr (EPI == 2) {
-    // per channel over the tile's valid rows: sum g, sum g * (x - mean), g = stored dY * mask.
-    // Per element: the stored (bf16-rounded) value via one v_cvt_pk_bf16_f32 per pair, the mask
-    // select (rows past M were cleared from the mask bits at load), packed fp32 sums.
-    float* red = reinterpret_cast<float*>(lds);   // [NWM][2][BN]
-    float s1[NI][4], s2[NI][4];
+    if constexpr (EPI == 2) {
+      // per channel over the tile's valid rows: sum g, sum g * (x - mean), g = stored dY * mask.
+      // Per element: the stored (bf16-rounded) value via one v_cvt_pk_bf16_f32 per pair, the mask
+      // select (rows past M were cleared from the mask bits at load), packed fp32 sums.
+      float* red = reinterpret_cast<float*>(lds);   // [NWM][2][BN]
+      float s1[NI][4], s2[NI][4];
 #pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const f32x2 mu01 = {bmu[j].x, bmu[j].y}, mu23 = {bmu[j].z, bmu[j].w};
-      f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f}, b01 = {0.f, 0.f}, b23 = {0.f, 0.f};
+      for (int j = 0; j < NI; ++j) {
+        const f32x2 mu01 = {bmu[j].x, bmu[j].y}, mu23 = {bmu[j].z, bmu[j].w};
+        f32x2 a01 = {0.f, 0.f}, a23 = {0.f, 0.f}, b01 = {0.f, 0.f}, b23 = {0.f, 0.f};
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const uint32_t u01 = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
-        const uint32_t u23 = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
-        const uint32_t mk = bm[i][j];
-        const f32x2 g01 = {(mk & 1u) ? __uint_as_float(u01 << 16) : 0.f,
-                           (mk & 2u) ? __uint_as_float(u01 & 0xffff0000u) : 0.f};
-        const f32x2 g23 = {(mk & 4u) ? __uint_as_float(u23 << 16) : 0.f,
-                           (mk & 8u) ? __uint_as_float(u23 & 0xffff0000u) : 0.f};
-        const f32x2 x01 = {__uint_as_float(bx[i][j].x << 16),
-                           __uint_as_float(bx[i][j].x & 0xffff0000u)};
-        const f32x2 x23 = {__uint_as_float(bx[i][j].y << 16),
-                           __uint_as_float(bx[i][j].y & 0xffff0000u)};
-        a01 += g01;
-        a23 += g23;
-        b01 = __builtin_elementwise_fma(g01, x01 - mu01, b01);
-        b23 = __builtin_elementwise_fma(g23, x23 - mu23, b23);
+        for (int i = 0; i < MI; ++i) {
+          const uint32_t u01 = pack_bf16x2(acc[i][j][0], acc[i][j][1]);
+          const uint32_t u23 = pack_bf16x2(acc[i][j][2], acc[i][j][3]);
+          const uint32_t mk = bm[i][j];
+          const f32x2 g01 = {(mk & 1u) ? __uint_as_float(u01 << 16) : 0.f,
+                             (mk & 2u) ? __uint_as_float(u01 & 0xffff0000u) : 0.f};
+          const f32x2 g23 = {(mk & 4u) ? __uint_as_float(u23 << 16) : 0.f,
+                             (mk & 8u) ? __uint_as_float(u23 & 0xffff0000u) : 0.f};
+          const f32x2 x01 = {__uint_as_float(bx[i][j].x << 16),
+                             __uint_as_float(bx[i][j].x & 0xffff0000u)};
+          const f32x2 x23 = {__uint_as_float(bx[i][j].y << 16),
+                             __uint_as_float(bx[i][j].y & 0xffff0000u)};
+          a01 += g01;
+          a23 += g23;
+          b01 = __builtin_elementwise_fma(g01, x01 - mu01, b01);
+          b23 = __builtin_elementwise_fma(g23, x23 - mu23, b23);
+        }
+        s1[j][0] = row16_sum(a01.x); s1[j][1] = row16_sum(a01.y);
+        s1[j][2] = row16_sum(a23.x); s1[j][3] = row16_sum(a23.y);
+        s2[j][0] = row16_sum(b01.x); s2[j][1] = row16_sum(b01.y);
+        s2[j][2] = row16_sum(b23.x); s2[j][3] = row16_sum(b23.y);
       }
-      s1[j][0] = row16_sum(a01.x); s1[j][1] = row16_sum(a01.y);
-      s1[j][2] = row16_sum(a23.x); s1[j][3] = row16_sum(a23.y);
-      s2[j][0] = row16_sum(b01.x); s2[j][1] = row16_sum(b01.y);
-      s2[j][2] = row16_sum(b23.x); s2[j][3] = row16_sum(b23.y);
-    }
-    lds_barrier();   // every wave is past its last read of the staging LDS (stores may be in flight)
-    if (fr == 0) {
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = wn * WN + j * 16 + 4 * fq + r;
-          red[wm * 2 * BN + c] = s1[j][r];
-          red[wm * 2 * BN + BN + c] = s2[j][r];
-        }
-    }
-    lds_barrier();
-    if (wm == 0 && fr == 0) {
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = wn * WN + j * 16 + 4 * fq + r;
-          float r1 = red[c], r2 = red[BN + c];
-#pragma unroll
-          for (int h = 1; h < NWM; ++h) {
-            r1 += red[h * 2 * BN + c];
-            r2 += red[h * 2 * BN + BN + c];
-          }
-          a.part[(size_t)mt * 2 * a.Cout + n0 + c] = r1;
-          a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = r2;
-        }
-    }
-  }
-  if constexpr (EPI == 1) {
-    // BatchNorm statistics of this tile's (rounded) outputs, two-pass -- mean, then sum of
-    // squared deviations -- over the valid rows: the partial format of bn_stats_kernel with
-    // rpb = BM, so the BN layer that consumes this output skips its statistics pass over HBM.
-    // Every output element passes through it, which on the streaming-bound 1x1 shapes made its
-    // scalar per-element math (a rounding sequence per pass, selects) a measurable cost: the
-    // values are rounded once before the stores, the sums are packed fp32 (two channels per op)
-    // and the row-validity selects only run on the last, partial tile (1x1 64->256 @56x56,
-    // batch 128: 94 -> 85 us; profiles/r2_conv_epi_{before,after}.jsonl).
-    const int nrows = min(BM, a.M - m0);
-    const bool full = nrows == BM;
-    float* red = reinterpret_cast<float*>(lds);   // [NWM][BN]
-    float mean[NI][4], s[NI][4];
-    auto exchange = [&](bool first) {   // s (row-16 sums of this wave) -> per-block channel sums
-      if (!first) lds_barrier();        // every wave has read the previous sums
+      lds_barrier();   // every wave is past its last read of the staging LDS (stores may be in flight)
       if (fr == 0) {
 #pragma unroll
         for (int j = 0; j < NI; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r) red[wm * BN + wn * WN + j * 16 + 4 * fq + r] = s[j][r];
+          for (int r = 0; r < 4; ++r) {
+            const int c = wn * WN + j * 16 + 4 * fq + r;
+            red[wm * 2 * BN + c] = s1[j][r];
+            red[wm * 2 * BN + BN + c] = s2[j][r];
+          }
       }
       lds_barrier();
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int c = wn * WN + j * 16 + 4 * fq + r;
-          float v = red[c];
-#pragma unroll
-          for (int h = 1; h < NWM; ++h) v += red[h * BN + c];
-          s[j][r] = v;
-        }
-    };
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      f32x2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        f32x2 v0 = {acc[i][j][0], acc[i][j][1]}, v1 = {acc[i][j][2], acc[i][j][3]};
-        if (!full && m0 + wm * WM + i * 16 + fr >= a.M) v0 = v1 = f32x2{0.f, 0.f};
-        t0 += v0;
-        t1 += v1;
-      }
-      s[j][0] = row16_sum(t0.x); s[j][1] = row16_sum(t0.y);
-      s[j][2] = row16_sum(t1.x); s[j][3] = row16_sum(t1.y);
-    }
-    lds_barrier();   // the coalesced store path's last reads of the staging LDS are done
-    exchange(true);
-    const float inv_n = 1.f / (float)nrows;
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) mean[j][r] = s[j][r] * inv_n;
-#pragma unroll
-    for (int j = 0; j < NI; ++j) {
-      const f32x2 mu0 = {mean[j][0], mean[j][1]}, mu1 = {mean[j][2], mean[j][3]};
-      f32x2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f};
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        f32x2 d0 = f32x2{acc[i][j][0], acc[i][j][1]} - mu0;
-        f32x2 d1 = f32x2{acc[i][j][2], acc[i][j][3]} - mu1;
-        if (!full && m0 + wm * WM + i * 16 + fr >= a.M) d0 = d1 = f32x2{0.f, 0.f};
-        t0 = __builtin_elementwise_fma(d0, d0, t0);
-        t1 = __builtin_elementwise_fma(d1, d1, t1);
-      }
-      s[j][0] = row16_sum(t0.x); s[j][1] = row16_sum(t0.y);
-      s[j][2] = row16_sum(t1.x); s[j][3] = row16_sum(t1.y);
-    }
-    exchange(false);
-    if (a.bn_acc == nullptr) {
       if (wm == 0 && fr == 0) {
 #pragma unroll
         for (int j = 0; j < NI; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int c = wn * WN + j * 16 + 4 * fq + r;
-            a.part[(size_t)mt * 2 * a.Cout + n0 + c] = mean[j][r];
-            a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = s[j][r];
+            float r1 = red[c], r2 = red[BN + c];
+#pragma unroll
+            for (int h = 1; h < NWM; ++h) {
+              r1 += red[h * 2 * BN + c];
+              r2 += red[h * 2 * BN + BN + c];
+            }
+            a.part[(size_t)mt * 2 * a.Cout + n0 + c] = r1;
+            a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = r2;
           }
       }
-    } else {
-      bn_acc_epilogue<BM, BN, NT>(a, n0, nrows, [&](auto&& add) {
+    }
+    if constexpr (EPI == 1) {
+      // BatchNorm statistics of this tile's (rounded) outputs, two-pass -- mean, then sum of
+      // squared deviations -- over the valid rows: the partial format of bn_stats_kernel with
+      // rpb = BM, so the BN layer that consumes this output skips its statistics pass over HBM.
+      // Every output element passes through it, which on the streaming-bound 1x1 shapes made its
+      // scalar per-element math (a rounding sequence per pass, selects) a measurable cost: the
+      // values are rounded once before the stores, the sums are packed fp32 (two channels per op)
+      // and the row-validity selects only run on the last, partial tile (1x1 64->256 @56x56,
+      // batch 128: 94 -> 85 us; profiles/r2_conv_epi_{before,after}.jsonl).
+      const int nrows = min(BM, a.M - m0);
+      const bool full = nrows == BM;
+      float* red = reinterpret_cast<float*>(lds);   // [NWM][BN]
+      float mean[NI][4], s[NI][4];
+      auto exchange = [&](bool first) {   // s (row-16 sums of this wave) -> per-block channel sums
+        if (!first) lds_barrier();        // every wave has read the previous sums
+        if (fr == 0) {
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[wm * BN + wn * WN + j * 16 + 4 * fq + r] = s[j][r];
+        }
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = wn * WN + j * 16 + 4 * fq + r;
+            float v = red[c];
+#pragma unroll
+            for (int h = 1; h < NWM; ++h) v += red[h * BN + c];
+            s[j][r] = v;
+          }
+      };
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        f32x2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          f32x2 v0 = {acc[i][j][0], acc[i][j][1]}, v1 = {acc[i][j][2], acc[i][j][3]};
+          if (!full && m0 + wm * WM + i * 16 + fr >= a.M) v0 = v1 = f32x2{0.f, 0.f};
+          t0 += v0;
+          t1 += v1;
+        }
+        s[j][0] = row16_sum(t0.x); s[j][1] = row16_sum(t0.y);
+        s[j][2] = row16_sum(t1.x); s[j][3] = row16_sum(t1.y);
+      }
+      lds_barrier();   // the coalesced store path's last reads of the staging LDS are done
+      exchange(true);
+      const float inv_n = 1.f / (float)nrows;
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mean[j][r] = s[j][r] * inv_n;
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const f32x2 mu0 = {mean[j][0], mean[j][1]}, mu1 = {mean[j][2], mean[j][3]};
+        f32x2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          f32x2 d0 = f32x2{acc[i][j][0], acc[i][j][1]} - mu0;
+          f32x2 d1 = f32x2{acc[i][j][2], acc[i][j][3]} - mu1;
+          if (!full && m0 + wm * WM + i * 16 + fr >= a.M) d0 = d1 = f32x2{0.f, 0.f};
+          t0 = __builtin_elementwise_fma(d0, d0, t0);
+          t1 = __builtin_elementwise_fma(d1, d1, t1);
+        }
+        s[j][0] = row16_sum(t0.x); s[j][1] = row16_sum(t0.y);
+        s[j][2] = row16_sum(t1.x); s[j][3] = row16_sum(t1.y);
+      }
+      exchange(false);
+      if (a.bn_acc == nullptr) {
         if (wm == 0 && fr == 0) {
 #pragma unroll
           for (int j = 0; j < NI; ++j)
 #pragma unroll
-            for (int r = 0; r < 4; ++r) add(wn * WN + j * 16 + 4 * fq + r, mean[j][r], s[j][r]);
+            for (int r = 0; r < 4; ++r) {
+              const int c = wn * WN + j * 16 + 4 * fq + r;
+              a.part[(size_t)mt * 2 * a.Cout + n0 + c] = mean[j][r];
+              a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = s[j][r];
+            }
         }
-      });
+      } else {
+        bn_acc_epilogue<BM, BN, NT>(a, n0, nrows, lacc, [&](auto&& add) {
+          if (wm == 0 && fr == 0) {
+#pragma unroll
+            for (int j = 0; j < NI; ++j)
+#pragma unroll
+              for (int r = 0; r < 4; ++r) add(wn * WN + j * 16 + 4 * fq + r, mean[j][r], s[j][r]);
+          }
+        });
+      }
+    }
+  }   // tile loop
+  if (lacc != nullptr) {   // the block's sums, once (each channel by the thread that summed it)
+    double* acc = a.bn_acc + n0;
+    for (int c = threadIdx.x; c < BN; c += NT) {
+      unsafeAtomicAdd(acc + c, lacc[c]);
+      unsafeAtomicAdd(acc + a.Cout + c, lacc[BN + c]);
     }
   }
 }
 
-template <int BM, int BN, int EPI, int NBUF, bool C16>
+template <int BM, int BN, int EPI, int NBUF, bool C16, bool PT = false>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
-  conv_fwd_body<BM, BN, EPI, NBUF, 2, 2, C16>(a);
+  conv_fwd_body<BM, BN, EPI, NBUF, 2, 2, C16, PT>(a);
 #endif
 }
 
 // Single stage buffer (one K step -- 1x1 over 64 channels -- or the serial variants 8..11): the
 // shapes that want it are bound by streaming the output, so it trades registers for occupancy --
 // four waves per SIMD (<= 128 VGPRs) instead of two, up to five blocks per CU by LDS.
-template <int BM, int BN, int EPI, bool C16>
+template <int BM, int BN, int EPI, bool C16, bool PT = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 void conv_fwd_kernel_occ4(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
-  conv_fwd_body<BM, BN, EPI, 1, 2, 2, C16>(a);
+  conv_fwd_body<BM, BN, EPI, 1, 2, 2, C16, PT>(a);
 #endif
 }
 
 // 256-row tiles on 8 waves (4 x 2, per-wave 64 x BN/2): twice the MFMA work of a 128-row tile per
 // staged weight byte, 2 waves per SIMD at one block per CU (96 KB of LDS double-buffered, 144 KB
 // triple-buffered at BN = 128).
-template <int BM, int BN, int EPI, int NBUF>
+template <int BM, int BN, int EPI, int NBUF, bool PT = false>
 __global__ __launch_bounds__(512) void conv_fwd_kernel_w8(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
-  conv_fwd_body<BM, BN, EPI, NBUF, 4, 2>(a);
+  conv_fwd_body<BM, BN, EPI, NBUF, 4, 2, false, PT>(a);
 #endif
 }
 
@@ -859,17 +911,21 @@ hipError_t launch_w8(const ConvArgs& a0, int nb, hipStream_t st) {
   if (a.c16) return hipErrorInvalidValue;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  const int nwg = a.m_tiles * a.n_tiles * a.ksplit;
+  const int nwg = a.tpb > 1 ? (a.m_tiles + a.tpb - 1) / a.tpb * a.n_tiles
+                            : a.m_tiles * a.n_tiles * a.ksplit;
   if (a.Ktot == kBK) nb = 1;
   const int epi = (a.part == nullptr && a.bn_acc == nullptr) ? 0 : (a.bnx != nullptr ? 2 : 1);
+#define ARENA_CONV_W8P(E, P) \
+  do { if (nb == 1) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 1, P>), dim3(nwg), dim3(512), 0, st, a); \
+       else if (nb == 2) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 2, P>), dim3(nwg), dim3(512), 0, st, a); \
+       else hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 3, P>), dim3(nwg), dim3(512), 0, st, a); } while (0)
 #define ARENA_CONV_W8(E) \
-  do { if (nb == 1) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 1>), dim3(nwg), dim3(512), 0, st, a); \
-       else if (nb == 2) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 2>), dim3(nwg), dim3(512), 0, st, a); \
-       else hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 3>), dim3(nwg), dim3(512), 0, st, a); } while (0)
+  do { if (a.tpb > 1) ARENA_CONV_W8P(E, true); else ARENA_CONV_W8P(E, false); } while (0)
   if (epi == 0) ARENA_CONV_W8(0);
   else if (epi == 1) ARENA_CONV_W8(1);
   else ARENA_CONV_W8(2);
 #undef ARENA_CONV_W8
+#undef ARENA_CONV_W8P
   return hipGetLastError();
 }
 
@@ -878,24 +934,30 @@ hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
   ConvArgs a = a0;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  const int nwg = a.m_tiles * a.n_tiles * a.ksplit;
+  const int nwg = a.tpb > 1 ? (a.m_tiles + a.tpb - 1) / a.tpb * a.n_tiles
+                            : a.m_tiles * a.n_tiles * a.ksplit;
   // stage buffers: pipe 0 (variants 0..3) two, pipe 1 (4..7) three, pipe 2 (8..11) one (serial,
   // high occupancy); a single K step always one
   const int nb = a.Ktot == kBK || pipe == 2 ? 1 : (pipe == 1 ? 3 : 2);
   const int epi = (a.part == nullptr && a.bn_acc == nullptr) ? 0 : (a.bnx != nullptr ? 2 : 1);
-#define ARENA_CONV_LAUNCH(E, NB) \
-  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, E, NB, C16>), dim3(nwg), dim3(kThreads), 0, st, a)
-#define ARENA_CONV_NB(E) \
+#define ARENA_CONV_LAUNCH(E, NB, P) \
+  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, E, NB, C16, P>), dim3(nwg), dim3(kThreads), 0, st, a)
+#define ARENA_CONV_NBP(E, P) \
   do { if (nb == 1 && (E == 0 || BM * BN < 128 * 128)) /* fits 128 VGPRs without spills */ \
-         hipLaunchKernelGGL((conv_fwd_kernel_occ4<BM, BN, E, C16>), dim3(nwg), dim3(kThreads), 0, st, a); \
-       else if (nb == 1) ARENA_CONV_LAUNCH(E, 1); \
-       else if (nb == 2) ARENA_CONV_LAUNCH(E, 2); \
-       else ARENA_CONV_LAUNCH(E, 3); } while (0)
+         hipLaunchKernelGGL((conv_fwd_kernel_occ4<BM, BN, E, C16, P>), dim3(nwg), dim3(kThreads), 0, st, a); \
+       else if (nb == 1) ARENA_CONV_LAUNCH(E, 1, P); \
+       else if (nb == 2) ARENA_CONV_LAUNCH(E, 2, P); \
+       else ARENA_CONV_LAUNCH(E, 3, P); } while (0)
+#define ARENA_CONV_NB(E) \
+  do { if constexpr (C16) ARENA_CONV_NBP(E, false); \
+       else if (a.tpb > 1) ARENA_CONV_NBP(E, true); else ARENA_CONV_NBP(E, false); } while (0)
+  if (a.tpb > 1 && C16) return hipErrorInvalidValue;
   if (epi == 0) ARENA_CONV_NB(0);
   else if (epi == 1) ARENA_CONV_NB(1);
   else if constexpr (!C16) ARENA_CONV_NB(2);
   else return hipErrorInvalidValue;
 #undef ARENA_CONV_NB
+#undef ARENA_CONV_NBP
 #undef ARENA_CONV_LAUNCH
   return hipGetLastError();
 }
@@ -927,15 +989,17 @@ extern "C" {
 // bnx/bnmask/bnmean (optional, with part): the backward-data form, part = BatchNorm-backward
 // partials of y instead of forward statistics (see ConvArgs).
 // bn_acc (optional, instead of part): accumulated BatchNorm statistics, see ConvArgs::bn_acc;
-// [2][Cout] doubles, zero on entry (the finalize that consumes them zeroes them again).
+// [2][Cout] doubles, zero on entry (the BN layer that consumes them zeroes them again).
+// tpb: output tiles per block (the persistent form, see conv_fwd_body; 1 with split-K).
 hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part, const void* add,
                              const uint8_t* addmask,
                              const void* bnx, const uint8_t* bnmask, const float* bnmean, int N,
                              int H, int W, int C, int Cout, int R, int S, int stride, int pad_h,
                              int pad_w, int Ho, int Wo, const int* y_map, int c16, int variant,
-                             double* bn_acc, int ksplit, void* kws, unsigned* kcnt,
+                             double* bn_acc, int ksplit, void* kws, unsigned* kcnt, int tpb,
                              hipStream_t st) {
   if (Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0) return hipErrorInvalidValue;
+  if (tpb < 1 || (tpb > 1 && ksplit != 1)) return hipErrorInvalidValue;
   if (c16 ? (C != 16 || S % 4) : (C % kBK)) return hipErrorInvalidValue;
   ConvArgs a{};
   a.x = (const uint16_t*)x;
@@ -997,6 +1061,7 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.ksplit = ksplit;
   a.kws = (float4*)kws;
   a.kcnt = kcnt;
+  a.tpb = tpb;
   if (variant >= 12) {   // 256-row tiles, 8 waves: 12/13 two stage buffers, 14/15 three
     const int nb = variant >= 14 ? 3 : 2;
     if ((variant & 1) == 0)
@@ -1019,7 +1084,7 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
                           int variant, hipStream_t st) {
   return arena_conv_fwd_ex(x, w, y, part, add, nullptr, bnx, bnmask, bnmean, N, H, W, C, Cout, R, S,
                            stride, pad, pad, 0, 0, nullptr, 0, variant, nullptr, 1, nullptr, nullptr,
-                           st);
+                           1, st);
 }
 
 // Split-K workspace of one launch, in floats (0 when ksplit == 1), and its ticket count (tiles).

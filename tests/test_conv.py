@@ -148,6 +148,51 @@ def test_conv_split_k_matches_unsplit(shape):
             assert _rel(dxa, dx_ref + addend.float()) < 1e-2, (v, _rel(dxa, dx_ref + addend.float()))
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(4, 64, 14, 14, 128, 3, 1), (3, 128, 9, 7, 256, 1, 1),
+                                   (2, 64, 17, 17, 64, 3, 2)])
+def test_conv_persistent_tiles_match_one_tile_per_block(shape):
+    """Persistent variants (2^p output tiles of one column tile per block, BatchNorm sums merged
+    in LDS and flushed once): outputs and per-tile partials bit-identical to the one-tile form,
+    epilogue-summed statistics equal to rounding, ragged last row chunks and tail rows included;
+    the backward-data pass too."""
+    n, cin, h, w, cout, k, st = shape
+    pad = k // 2
+    x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=7)
+    for v in conv.variants_for(cout):
+        y, (part, rpb) = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True)
+        _, fin = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True, final=True)
+        ref_sums = fin.fin.clone()
+        fin.discard()
+        for p in (1, 2, 3):
+            pv = v + 256 * p
+            assert conv.tiles_per_block(pv) == 1 << p and conv.TILES[pv] == conv.TILES[v]
+            y2, (part2, rpb2) = conv.conv2d_fwd(x, wt, st, pad, pv, with_stats=True)
+            assert torch.equal(y2, y) and rpb2 == rpb and torch.equal(part2, part), (v, p)
+            y3, fin3 = conv.conv2d_fwd(x, wt, st, pad, pv, with_stats=True, final=True)
+            assert torch.equal(y3, y)
+            torch.testing.assert_close(fin3.fin, ref_sums, rtol=1e-9, atol=1e-6)
+            fin3.discard()
+    if st == 1:
+        dy = torch.randn(n, cout, h, w, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        for v in conv.variants_for(cin):
+            dx = conv.conv2d_bwd_data(dy, wt, pad, v)
+            for p in (1, 2):
+                assert torch.equal(conv.conv2d_bwd_data(dy, wt, pad, v + 256 * p), dx), (v, p)
+
+
+def test_persist_variants_keep_the_chip_filled():
+    # 56x56 x 256 at batch 128 (3136 row tiles of 128): up to 16 tiles per block still fills it
+    pv = conv.persist_variants_for(128 * 56 * 56, 256, [0, 9])
+    assert {conv.tiles_per_block(v) for v in pv} == {2, 4, 8, 16}
+    assert all(-(-128 * 56 * 56 // conv.TILES[v][0]) * (256 // conv.TILES[v][1])
+               // conv.tiles_per_block(v) >= conv._CUS for v in pv)
+    # 7x7 x 512: too few tiles for any
+    assert conv.persist_variants_for(128 * 7 * 7, 512, [0]) == []
+    assert conv.persist_variants_for(128 * 56 * 56, 256, [0 + 16]) == []   # split-K: never
+
+
 def test_split_variants_for_only_underfilled_grids():
     # 56x56 at batch 128: thousands of tiles, no split; 7x7 x 512 with K = 4608: splits offered
     assert conv.split_variants_for(128 * 56 * 56, 64, 576) == []
