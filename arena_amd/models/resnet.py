@@ -23,7 +23,7 @@ from typing import List
 import torch
 from torch import nn
 
-from ..ops.batchnorm import BatchNormAct2d, ResidualMask
+from ..ops.batchnorm import BatchNormAct2d, ResidualMask, bn_relu_maxpool
 from ..ops.conv import BNGradLink, Conv2dNHWC, GradJoin, StemConv2d, WeightFlipper
 from ..ops.pool import MaxPool2dNHWC
 
@@ -102,7 +102,8 @@ class ResNet(nn.Module):
     def forward(self, x):
         with self._flipper.scope():
             y, st = self.stem[0].forward_stats(x)    # epilogue BN statistics, as in the blocks
-            x = self.stem[2](self.stem[1](y, stats=st))
+            # BN + ReLU + max pool as one pass each way when the statistics come summed
+            x = bn_relu_maxpool(self.stem[1], self.stem[2], y, st)
             link = None
             for blk in self.layers:
                 out_link = BNGradLink() if torch.is_grad_enabled() else None

@@ -26,7 +26,8 @@ from . import _ext
 
 Tensor = torch.Tensor
 TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
-# + 4: three-stage K pipeline; + 8: single stage buffer, serial K loop, high occupancy
+# + 4: four-stage K pipeline (3 steps in flight); + 8: single stage buffer, serial K loop, high
+# occupancy
 TILES.update({v + d: t for v, t in list(TILES.items()) for d in (4, 8)})
 # 12 / 13: 256x128 / 256x64 tiles on 8 waves, two stage buffers; 14 / 15: three
 TILES.update({12: (256, 128), 13: (256, 64), 14: (256, 128), 15: (256, 64)})
@@ -106,7 +107,7 @@ def split_variants_for(m: int, cout: int, ktot: int):
     steps = ktot // 64
     for v in variants_for(cout):
         if 4 <= v < 8 or v >= 14:
-            continue   # the three-stage pipelines need long K loops: not split candidates
+            continue   # the deep pipelines need long K loops: not split candidates
         bm, bn = TILES[v]
         tiles = -(-m // bm) * (cout // bn)
         if tiles >= 2 * _CUS or tiles > 65536:
@@ -609,8 +610,9 @@ def _wgrad_candidates(cin, cout, k):
 
 
 # what a forward whose statistics come as per-tile partials pays on top of its own time: the BN
-# layer's partial-merge finalize launch (bn_stats_finalize, ~12 us per layer at batch 128)
-_FIN_PENALTY_US = float(os.environ.get("ARENA_CONV_FIN_PENALTY_US", "8"))
+# layer's partial-merge finalize launch (bn_stats_finalize, 14 us per layer on average at batch 128,
+# profiles/r3_persist_steady_kernels.csv)
+_FIN_PENALTY_US = float(os.environ.get("ARENA_CONV_FIN_PENALTY_US", "14"))
 
 
 def _best(t: dict, kind: str, n: int):

@@ -100,6 +100,9 @@ struct ArenaBNBwd {
   float* dgamma;          // optional outputs
   float* dbeta;
   float* ca; float* cb; float* cc;  // workspace [C] each: dx = ca * (g - cb - (x - mean) * cc)
+  // the forward's y = act((x - mean) * scale + shift): the fused stem (BN + ReLU + max pool,
+  // arena_bn_pool_bwd) recomputes its ReLU mask from x with them
+  const float* scale; const float* shift;
 };
 
 // Intra-node xGMI collective (csrc/ccl/xgmi_ccl.hip): every rank's registered buffers, mapped into

@@ -100,6 +100,10 @@ hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, vo
                         int, float*, int, double*, unsigned*, ArenaBNBwd, double*, int, double*,
                         int, hipStream_t);
 int arena_bn_acc_ok(long long, int);
+hipError_t arena_bn_pool_fwd(int, const void*, void*, uint8_t*, int, int, int, int, int, int, int,
+                             ArenaBNStats, const double*, double*, int, hipStream_t);
+hipError_t arena_bn_pool_bwd(int, const void*, const uint8_t*, const void*, void*, int, int, int,
+                             int, int, int, int, ArenaBNBwd, double*, double*, int, hipStream_t);
 #ifdef ARENA_TIMELINE
 hipError_t arena_timeline_read(long long*, int);
 #endif
@@ -1050,6 +1054,115 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
   return {dx, dres, dgamma, dbeta};
 }
 
+// Fused stem BatchNorm + ReLU + k x k / s max pool (training; bn_kernels.hip arena_bn_pool_fwd):
+// x is the BN input with its statistics summed by the producing conv (fin, fp64 [2][C]).
+// Returns (y, pos, mean, invstd, scale, shift): the pooled output, its uint8 in-window argmax,
+// and the saved statistics. fin stays in place until bn_pool_bwd(zero_f=fin) zeroes it; zero_b:
+// as in bn_fwd.
+std::vector<Tensor> bn_pool_fwd(Tensor x, OptT gamma, OptT beta, OptT running_mean,
+                                OptT running_var, double momentum, double eps, OptT num_batches,
+                                Tensor fin, int64_t k, int64_t s, int64_t p, OptT zero_b) {
+  const BNGeom g = bn_geom(x, "x");
+  TORCH_CHECK(fin.is_cuda() && fin.device() == x.device() &&
+                  fin.scalar_type() == torch::kFloat64 && fin.is_contiguous() &&
+                  fin.numel() == 2 * g.C,
+              "bn_pool_fwd: fin must be the fp64 [2, C] statistics sums");
+  auto f32 = x.options().dtype(torch::kFloat32);
+  Tensor mean = torch::empty({g.C}, f32), invstd = torch::empty({g.C}, f32);
+  Tensor scale = torch::empty({g.C}, f32), shift = torch::empty({g.C}, f32);
+  ArenaBNStats st{};
+  st.eps = (float)eps;
+  st.momentum = (float)momentum;
+  st.gamma = bn_vec(gamma, g.C, "weight");
+  st.beta = bn_vec(beta, g.C, "bias");
+  st.mean = mean.data_ptr<float>();
+  st.invstd = invstd.data_ptr<float>();
+  st.scale = scale.data_ptr<float>();
+  st.shift = shift.data_ptr<float>();
+  if (running_mean.has_value() || running_var.has_value()) {
+    TORCH_CHECK(running_mean.has_value() && running_var.has_value(),
+                "running_mean and running_var go together");
+    st.running_mean = const_cast<float*>(bn_vec(running_mean, g.C, "running_mean"));
+    st.running_var = const_cast<float*>(bn_vec(running_var, g.C, "running_var"));
+  }
+  if (num_batches.has_value()) {
+    check_dev(*num_batches, "num_batches_tracked");
+    st.batches = reinterpret_cast<long long*>(num_batches->data_ptr<int64_t>());
+  }
+  const int64_t N = x.size(0), H = x.size(2), W = x.size(3);
+  const int64_t OH = (H + 2 * p - k) / s + 1, OW = (W + 2 * p - k) / s + 1;
+  TORCH_CHECK(OH > 0 && OW > 0, "bn_pool_fwd: bad pool geometry");
+  Tensor y = torch::empty({N, g.C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor pos = torch::empty({N * OH * OW * g.C}, x.options().dtype(torch::kUInt8));
+  double* zb = nullptr;
+  int nzb = 0;
+  if (zero_b.has_value()) {
+    TORCH_CHECK(zero_b->is_cuda() && zero_b->device() == x.device() &&
+                    zero_b->scalar_type() == torch::kFloat64 && zero_b->is_contiguous(),
+                "zero_b must be a contiguous fp64 tensor on x's device");
+    zb = zero_b->data_ptr<double>();
+    nzb = (int)zero_b->numel();
+  }
+  check_hip(arena_bn_pool_fwd(g.dtype, x.data_ptr(), y.data_ptr(), pos.data_ptr<uint8_t>(), (int)N,
+                              (int)H, (int)W, (int)g.C, (int)k, (int)s, (int)p, st,
+                              fin.data_ptr<double>(), zb, nzb, cur_stream()),
+            "bn_pool_fwd");
+  return {y, pos, mean, invstd, scale, shift};
+}
+
+// Backward of bn_pool_fwd: returns (dx, dgamma or empty, dbeta or empty). acc_b: the layer's own
+// fp64 [2, C] backward sums (zero on entry, left for the next forward's zero_b); zero_f: the
+// forward's fin, zeroed by the dx pass.
+std::vector<Tensor> bn_pool_bwd(Tensor dy, Tensor pos, Tensor x, Tensor mean, Tensor invstd,
+                                Tensor scale, Tensor shift, OptT gamma, bool affine_grads,
+                                int64_t k, int64_t s, int64_t p, Tensor acc_b, OptT zero_f) {
+  const BNGeom g = bn_geom(x, "x");
+  for (const Tensor* t : {&mean, &invstd, &scale, &shift}) {
+    check_f32(*t, "saved statistics");
+    TORCH_CHECK(t->numel() == g.C, "saved statistics must have C elements");
+  }
+  TORCH_CHECK(dy.is_cuda() && dy.scalar_type() == x.scalar_type() && dy.size(0) == x.size(0) &&
+                  dy.size(1) == g.C && dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "bn_pool_bwd: dy must be a channels_last tensor like the pooled output");
+  TORCH_CHECK(pos.scalar_type() == torch::kUInt8 && pos.numel() == dy.numel() && pos.is_contiguous(),
+              "bn_pool_bwd: pos must be the forward's argmax bytes");
+  TORCH_CHECK(acc_b.is_cuda() && acc_b.device() == x.device() &&
+                  acc_b.scalar_type() == torch::kFloat64 && acc_b.is_contiguous() &&
+                  acc_b.numel() == 2 * g.C,
+              "acc_b must be a contiguous fp64 tensor of 2*C elements on x's device");
+  auto f32 = x.options().dtype(torch::kFloat32);
+  ArenaBNBwd b{};
+  b.mean = mean.data_ptr<float>();
+  b.invstd = invstd.data_ptr<float>();
+  b.scale = scale.data_ptr<float>();
+  b.shift = shift.data_ptr<float>();
+  b.gamma = bn_vec(gamma, g.C, "weight");
+  Tensor dgamma, dbeta;
+  if (affine_grads) {
+    dgamma = torch::empty({g.C}, f32);
+    dbeta = torch::empty({g.C}, f32);
+    b.dgamma = dgamma.data_ptr<float>();
+    b.dbeta = dbeta.data_ptr<float>();
+  }
+  double* zf = nullptr;
+  int nzf = 0;
+  if (zero_f.has_value() && zero_f->defined() && zero_f->numel() > 0) {
+    TORCH_CHECK(zero_f->is_cuda() && zero_f->device() == x.device() &&
+                    zero_f->scalar_type() == torch::kFloat64 && zero_f->is_contiguous(),
+                "zero_f must be a contiguous fp64 tensor on x's device");
+    zf = zero_f->data_ptr<double>();
+    nzf = (int)zero_f->numel();
+  }
+  Tensor dx = torch::empty_like(x);
+  check_hip(arena_bn_pool_bwd(g.dtype, dy.data_ptr(), pos.data_ptr<uint8_t>(), x.data_ptr(),
+                              dx.data_ptr(), (int)x.size(0), (int)x.size(2), (int)x.size(3),
+                              (int)g.C, (int)k, (int)s, (int)p, b, acc_b.data_ptr<double>(), zf,
+                              nzf, cur_stream()),
+            "bn_pool_bwd");
+  if (zf != nullptr) bn_acc_clean(*zero_f);
+  return {dx, dgamma, dbeta};
+}
+
 // ------------------------------------------------------------------- NHWC max pooling
 void pool_check(const Tensor& t, const char* name) {
   TORCH_CHECK(t.is_cuda() && t.dim() == 4, name, " must be a 4-D GPU tensor");
@@ -1640,6 +1753,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_set_nt", [](int64_t on) { arena_bn_set_nt((int)on); });
   m.def("bn_set_acc", [](bool on) { g_bn_acc = on; });
   m.def("bn_acc_scratch", [](bool on) { g_acc_scratch = on; });
+  m.def("bn_pool_fwd", &bn_pool_fwd);
+  m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
     arena_bn_set_reduce_geometry(max_blocks, min_rounds);
   });

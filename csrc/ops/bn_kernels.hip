@@ -431,7 +431,7 @@ __device__ __forceinline__ void apply_coefs(int C, long long M, const double* fi
       mu = (float)mean;
       sc = (st.gamma ? st.gamma[c] : 1.f) * inv;
       sh = st.beta ? st.beta[c] : 0.f;
-      if (blockIdx.x == 0) {
+      if (blockIdx.x == 0 && blockIdx.y == 0) {
         st.mean[c] = mu;
         st.invstd[c] = inv;
         st.scale[c] = sc;
@@ -715,6 +715,239 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
   }
 }
 
+// ------------------------------------------------------------------------ fused stem: BN + ReLU + max pool
+// The ResNet stem's BatchNorm + ReLU feeds a 3x3 / 2 max pool and nothing else, so the pool reads
+// the BN input x and normalises on the fly: the forward writes only the pooled output and its
+// in-window argmax (no y, no mask bits: 205 MB written and read back less at batch 128), and the
+// backward gathers each input's gradient from the windows that picked it (maxpool_bwd's rule,
+// pool_kernels.hip) inside the BN reduction and dx passes, recomputing the ReLU mask from x,
+// instead of materialising the pool's dx (another 205 MB write + 2 reads). Values, argmax ties and
+// gradients are those of bn_apply + maxpool_fwd / maxpool_bwd + bn_bwd on the rounded output.
+struct PoolG {
+  int N, H, W, C, OH, OW, k, s, p;
+};
+
+template <typename T>
+__device__ __forceinline__ float stored_val(float v) {   // the value bn_apply would have stored
+  if constexpr (sizeof(T) == 2) return __uint_as_float(V8<uint16_t>::pack2(v, 0.f) << 16);
+  else return v;
+}
+
+// dynamic shared memory: 3 * C floats. grid: (N * OH output rows, ceil(OW * C/8 / kT))
+template <typename T>
+__global__ __launch_bounds__(kT) void bn_pool_fwd_kernel(const T* __restrict__ x,
+                                                         T* __restrict__ y,
+                                                         uint8_t* __restrict__ pos,
+                                                         ArenaBNStats st,
+                                                         const double* __restrict__ fin,
+                                                         long long M, PoolG g,
+                                                         double* __restrict__ zero, int nzero) {
+  extern __shared__ __attribute__((aligned(16))) float s_co[];
+  const int C = g.C, cg = C / kVec;
+  apply_coefs<true>(C, M, fin, st, s_co);
+  zero_duty(zero, nzero);
+  const int row = blockIdx.x;
+  const int t = blockIdx.y * kT + threadIdx.x;
+  if (t >= g.OW * cg) return;
+  const int ow = t / cg, c8 = t - ow * cg;
+  float mu[kVec], sc[kVec], sh[kVec];
+  lds8(s_co + c8 * kVec, mu);
+  lds8(s_co + C + c8 * kVec, sc);
+  lds8(s_co + 2 * C + c8 * kVec, sh);
+  const int n32 = row / g.OH, oh = row - n32 * g.OH;
+  const long long n = n32;
+  const int h0 = oh * g.s - g.p, w0 = ow * g.s - g.p;
+  float m[kVec];
+  int best[kVec];
+#pragma unroll
+  for (int i = 0; i < kVec; ++i) { m[i] = -INFINITY; best[i] = -1; }
+  for (int kh = 0; kh < g.k; ++kh) {
+    const int h = h0 + kh;
+    if (h < 0 || h >= g.H) continue;
+    for (int kw = 0; kw < g.k; ++kw) {
+      const int w = w0 + kw;
+      if (w < 0 || w >= g.W) continue;
+      float a[kVec];
+      V8<T>::load(x + (((n * g.H + h) * g.W + w) * C + (long long)c8 * kVec), a);
+      const int q = kh * g.k + kw;
+#pragma unroll
+      for (int i = 0; i < kVec; ++i) {
+        const float v = stored_val<T>(fmaxf(fmaf(a[i] - mu[i], sc[i], sh[i]), 0.f));
+        if (v > m[i] || __builtin_isnan(v) || best[i] < 0) { m[i] = v; best[i] = q; }
+      }
+    }
+  }
+  const long long v = (long long)row * g.OW * cg + t;
+  V8<T>::store(y + v * kVec, m);
+  uint2 pk;
+  pk.x = (uint32_t)(best[0] & 0xff) | ((uint32_t)(best[1] & 0xff) << 8) |
+         ((uint32_t)(best[2] & 0xff) << 16) | ((uint32_t)(best[3] & 0xff) << 24);
+  pk.y = (uint32_t)(best[4] & 0xff) | ((uint32_t)(best[5] & 0xff) << 8) |
+         ((uint32_t)(best[6] & 0xff) << 16) | ((uint32_t)(best[7] & 0xff) << 24);
+  *reinterpret_cast<uint2*>(pos + v * kVec) = pk;
+}
+
+// The pool's gradient at input pixel r (row-major n, h, w), channels 8 c8 .. 8 c8 + 7: the sum of
+// dy over the (at most 2 x 2 for the 3x3 / 2 pool) windows whose saved argmax is this pixel.
+template <typename T>
+__device__ __forceinline__ void pool_grad8(const T* __restrict__ dy,
+                                           const uint8_t* __restrict__ pos, const PoolG& g,
+                                           long long r, int c8, float out[kVec]) {
+  constexpr int CW = 2;
+  const int w = (int)(r % g.W);
+  const long long nh = r / g.W;
+  const int h = (int)(nh % g.H);
+  const long long n = nh / g.H;
+  const int th = h + g.p - g.k + 1, tw = w + g.p - g.k + 1;
+  const int oh_lo = th <= 0 ? 0 : (th + g.s - 1) / g.s;
+  const int ow_lo = tw <= 0 ? 0 : (tw + g.s - 1) / g.s;
+  const int oh_hi = min(g.OH - 1, (h + g.p) / g.s);
+  const int ow_hi = min(g.OW - 1, (w + g.p) / g.s);
+  long long off[CW * CW];
+  int q[CW * CW];
+  uint2 pk[CW * CW];
+#pragma unroll
+  for (int a = 0; a < CW; ++a)
+#pragma unroll
+    for (int b = 0; b < CW; ++b) {
+      const int j = a * CW + b;
+      const bool ok = oh_lo + a <= oh_hi && ow_lo + b <= ow_hi;
+      const int oh = ok ? oh_lo + a : min(oh_lo, g.OH - 1);
+      const int ow = ok ? ow_lo + b : min(ow_lo, g.OW - 1);
+      q[j] = ok ? (h - (oh * g.s - g.p)) * g.k + (w - (ow * g.s - g.p)) : 0xff;
+      off[j] = ((n * g.OH + oh) * g.OW + ow) * g.C + (long long)c8 * kVec;
+      pk[j] = *reinterpret_cast<const uint2*>(pos + off[j]);
+    }
+  float d[CW * CW][kVec];
+#pragma unroll
+  for (int j = 0; j < CW * CW; ++j) V8<T>::load(dy + off[j], d[j]);
+#pragma unroll
+  for (int i = 0; i < kVec; ++i) out[i] = 0.f;
+#pragma unroll
+  for (int j = 0; j < CW * CW; ++j) {
+    const uint32_t ps[2] = {pk[j].x, pk[j].y};
+#pragma unroll
+    for (int i = 0; i < kVec; ++i)
+      out[i] += ((ps[i >> 2] >> (8 * (i & 3))) & 0xff) == (uint32_t)q[j] ? d[j][i] : 0.f;
+  }
+}
+
+// Backward reduction of the fused stem (acc mode into `acc`, zero on entry): g = pool gradient
+// masked by the recomputed ReLU bit; per channel sum g, sum g (x - mean). Rows r of x are split
+// over blocks like bn_bwd_reduce_kernel (C <= 256: one channel slice).
+template <typename T>
+__global__ __launch_bounds__(kT) void bn_pool_bwd_reduce_kernel(const T* __restrict__ dy,
+                                                                const uint8_t* __restrict__ pos,
+                                                                const T* __restrict__ x,
+                                                                long long M, long long rpb,
+                                                                PoolG g, ArenaBNBwd co,
+                                                                double* __restrict__ acc) {
+  __shared__ __attribute__((aligned(16))) float s_c[3 * 256];
+  const int C = g.C;
+  for (int c = threadIdx.x; c < C; c += kT) {
+    s_c[c] = co.mean[c];
+    s_c[C + c] = co.scale[c];
+    s_c[2 * C + c] = co.shift[c];
+  }
+  __syncthreads();
+  const Geo q = geo(C);
+  long long r0, r1;
+  block_rows(M, rpb, &r0, &r1);
+  float sg[kVec], sgx[kVec], mu[kVec], sc[kVec], sh[kVec];
+#pragma unroll
+  for (int i = 0; i < kVec; ++i) sg[i] = sgx[i] = 0.f;
+  lds8(s_c + q.g * kVec, mu);
+  lds8(s_c + C + q.g * kVec, sc);
+  lds8(s_c + 2 * C + q.g * kVec, sh);
+  if (q.slot < q.rip) {
+    for (long long r = r0 + q.slot; r < r1; r += q.rip) {
+      float gv[kVec], v[kVec];
+      V8<T>::load(x + r * C + (long long)q.g * kVec, v);
+      pool_grad8<T>(dy, pos, g, r, q.g, gv);
+#pragma unroll
+      for (int i = 0; i < kVec; ++i) {
+        const bool on = stored_val<T>(fmaxf(fmaf(v[i] - mu[i], sc[i], sh[i]), 0.f)) > 0.f;
+        const float gg = on ? gv[i] : 0.f;
+        sg[i] += gg;
+        sgx[i] = fmaf(gg, v[i] - mu[i], sgx[i]);
+      }
+    }
+  }
+  __shared__ float s_g[kT * kVec], s_gx[kT * kVec];
+  if (q.slot < q.rip) {
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      s_g[q.slot * q.cw + q.gl * kVec + i] = sg[i];
+      s_gx[q.slot * q.cw + q.gl * kVec + i] = sgx[i];
+    }
+  }
+  __syncthreads();
+  for (int cl = threadIdx.x; cl < q.cw; cl += kT) {
+    float a = 0.f, b = 0.f;
+    for (int s2 = 0; s2 < q.rip; ++s2) {
+      a += s_g[s2 * q.cw + cl];
+      b += s_gx[s2 * q.cw + cl];
+    }
+    unsafeAtomicAdd(acc + q.cb + cl, (double)a);
+    unsafeAtomicAdd(acc + C + q.cb + cl, (double)b);
+  }
+}
+
+// dx of the fused stem from the reduction's sums (FIN as in bn_bwd_dx_kernel); dynamic shared
+// memory: 6 * C floats
+template <typename T>
+__global__ __launch_bounds__(kT) void bn_pool_bwd_dx_kernel(const T* __restrict__ dy,
+                                                            const uint8_t* __restrict__ pos,
+                                                            const T* __restrict__ x,
+                                                            T* __restrict__ dx, long long nvec,
+                                                            PoolG g, ArenaBNBwd co,
+                                                            const double* __restrict__ acc,
+                                                            long long M,
+                                                            double* __restrict__ zero, int nzero) {
+  extern __shared__ __attribute__((aligned(16))) float s_co[];
+  const int C = g.C, cg = C / kVec;
+  const long long stride = (long long)gridDim.x * kT;
+  const int c8 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1));
+  const double inv_m = 1.0 / (double)M;
+  for (int c = threadIdx.x; c < C; c += kT) {
+    const double a = acc[c], b = acc[C + c];
+    const float invstd = co.invstd[c];
+    const float gam = co.gamma ? co.gamma[c] : 1.f;
+    s_co[c] = gam * invstd;
+    s_co[C + c] = (float)(a * inv_m);
+    s_co[2 * C + c] = (float)(b * inv_m) * invstd * invstd;
+    s_co[3 * C + c] = co.mean[c];
+    s_co[4 * C + c] = co.scale[c];
+    s_co[5 * C + c] = co.shift[c];
+    if (blockIdx.x == 0) {
+      if (co.dgamma) co.dgamma[c] = (float)(b * invstd);
+      if (co.dbeta) co.dbeta[c] = (float)a;
+    }
+  }
+  __syncthreads();
+  zero_duty(zero, nzero);
+  float ca[kVec], cb[kVec], cc[kVec], mu[kVec], sc[kVec], sh[kVec];
+  lds8(s_co + c8 * kVec, ca);
+  lds8(s_co + C + c8 * kVec, cb);
+  lds8(s_co + 2 * C + c8 * kVec, cc);
+  lds8(s_co + 3 * C + c8 * kVec, mu);
+  lds8(s_co + 4 * C + c8 * kVec, sc);
+  lds8(s_co + 5 * C + c8 * kVec, sh);
+  for (long long v = (long long)blockIdx.x * kT + threadIdx.x; v < nvec; v += stride) {
+    const long long r = v / cg;
+    float gv[kVec], xv[kVec], o[kVec];
+    V8<T>::load(x + v * kVec, xv);
+    pool_grad8<T>(dy, pos, g, r, c8, gv);
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      const bool on = stored_val<T>(fmaxf(fmaf(xv[i] - mu[i], sc[i], sh[i]), 0.f)) > 0.f;
+      const float gg = on ? gv[i] : 0.f;
+      o[i] = ca[i] * (gg - cb[i] - (xv[i] - mu[i]) * cc[i]);
+    }
+    V8<T>::store(dx + v * kVec, o);
+  }
+}
+
 // Blocks for a reduction over M rows: >= 8 row rounds per thread (the loops issue 4 or 2 rounds
 // of loads at once), as many blocks as that allows up to 512 partials. The 7x7 ResNet layers
 // (M = 6272) need the small per-thread share to fill the chip: at 32 rounds per thread they ran
@@ -946,6 +1179,65 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
 #undef ARENA_BN_DX
 #undef ARENA_BN_DX_F
 #undef ARENA_BN_DX_NT
+  return hipGetLastError();
+}
+
+// Fused stem forward (training, acc-mode statistics `fin` from the producing conv): y = the
+// max pool of relu(bn(x)), pos = its in-window argmax. Only the 3x3 / 2 style pools whose inputs
+// have <= 2 x 2 candidate windows, C % 8 == 0, C <= 256. zero / nzero: see arena_bn_fwd.
+hipError_t arena_bn_pool_fwd(int dtype, const void* x, void* y, uint8_t* pos, int N, int H, int W,
+                             int C, int k, int s, int p, ArenaBNStats st, const double* fin,
+                             double* zero, int nzero, hipStream_t stream) {
+  PoolG g{N, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
+  if (bad_shape((long long)N * H * W, C) || C > 256 || fin == nullptr || (k + s - 1) / s != 2 ||
+      2 * p > k || g.OH <= 0 || g.OW <= 0)
+    return hipErrorInvalidValue;
+  const int cg = C / kVec;
+  const dim3 grid((unsigned)(N * g.OH), (unsigned)((g.OW * cg + kT - 1) / kT));
+  const long long M = (long long)N * H * W;
+  if (dtype == 1)
+    hipLaunchKernelGGL(bn_pool_fwd_kernel<uint16_t>, grid, dim3(kT), 3 * C * 4, stream,
+                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), pos, st, fin,
+                       M, g, zero, nzero);
+  else
+    hipLaunchKernelGGL(bn_pool_fwd_kernel<float>, grid, dim3(kT), 3 * C * 4, stream,
+                       static_cast<const float*>(x), static_cast<float*>(y), pos, st, fin, M, g,
+                       zero, nzero);
+  return hipGetLastError();
+}
+
+// Fused stem backward: dy is the pooled output's gradient, pos the forward's argmax; the
+// reduction adds into acc (fp64 [2][C], zero on entry: the layer's own backward set, left in
+// place for its next forward to zero) and the dx pass derives its coefficients from it.
+// co.scale / co.shift: the forward's (ReLU mask recomputed from x). zero / nzero: see arena_bn_bwd.
+hipError_t arena_bn_pool_bwd(int dtype, const void* dy, const uint8_t* pos, const void* x, void* dx,
+                             int N, int H, int W, int C, int k, int s, int p, ArenaBNBwd co,
+                             double* acc, double* zero, int nzero, hipStream_t stream) {
+  PoolG g{N, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
+  const long long M = (long long)N * H * W;
+  if (bad_shape(M, C) || C > 256 || acc == nullptr || co.scale == nullptr ||
+      co.shift == nullptr || (k + s - 1) / s != 2 || 2 * p > k || g.OH <= 0 || g.OW <= 0)
+    return hipErrorInvalidValue;
+  long long rpb;
+  const long long nb = reduce_blocks(M, C, &rpb);
+  const long long nvec = M * (C / kVec);
+  long long ne = (nvec + kT - 1) / kT;
+  ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);
+  if (dtype == 1) {
+    hipLaunchKernelGGL(bn_pool_bwd_reduce_kernel<uint16_t>, dim3(nb, 1), dim3(kT), 0, stream,
+                       static_cast<const uint16_t*>(dy), pos, static_cast<const uint16_t*>(x), M,
+                       rpb, g, co, acc);
+    hipLaunchKernelGGL(bn_pool_bwd_dx_kernel<uint16_t>, dim3(ne), dim3(kT), 6 * C * 4, stream,
+                       static_cast<const uint16_t*>(dy), pos, static_cast<const uint16_t*>(x),
+                       static_cast<uint16_t*>(dx), nvec, g, co, acc, M, zero, nzero);
+  } else {
+    hipLaunchKernelGGL(bn_pool_bwd_reduce_kernel<float>, dim3(nb, 1), dim3(kT), 0, stream,
+                       static_cast<const float*>(dy), pos, static_cast<const float*>(x), M, rpb,
+                       g, co, acc);
+    hipLaunchKernelGGL(bn_pool_bwd_dx_kernel<float>, dim3(ne), dim3(kT), 6 * C * 4, stream,
+                       static_cast<const float*>(dy), pos, static_cast<const float*>(x),
+                       static_cast<float*>(dx), nvec, g, co, acc, M, zero, nzero);
+  }
   return hipGetLastError();
 }
 

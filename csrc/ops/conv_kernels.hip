@@ -460,33 +460,37 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
       }
     };
 
-    if constexpr (NBUF == 3) {
-      // Three stage buffers, two K steps in flight: the glds of step t+2 stay outstanding across
-      // the barrier that publishes step t+1 (counted vmcnt = this thread's glds of ONE stage, raw
-      // s_barrier: __syncthreads() would drain every outstanding LDS-DMA with a vmcnt(0)).
+    if constexpr (NBUF >= 3) {
+      // NBUF stage buffers, S = NBUF - 1 K steps in flight: the glds of steps t+2 .. t+S stay
+      // outstanding across the barrier that publishes step t+1 (counted vmcnt = this thread's glds
+      // of S - 1 stages, raw s_barrier: __syncthreads() would drain every outstanding LDS-DMA
+      // with a vmcnt(0)). The deep-K layers (3x3 at 14x14 / 7x7: 36-72 K steps of ~500 MFMA
+      // cycles each) wait ~700 ns per staged step, so one step in flight leaves them latency-bound.
       // RAW: stage t+1 is read in iteration t+1, after the vmcnt that retired it and a barrier.
-      // WAR: stage t+2 overwrites buffer (t-1)%3, whose reads finished before iteration t-1's barrier.
+      // WAR: stage t+S overwrites buffer (t-1) % NBUF, whose reads finished before iteration
+      // t-1's barrier.
+      constexpr int S = NBUF - 1;
       constexpr int kLps = AI + BI;   // glds per thread per stage
-      stage(0, 0);
-      if (T > 1) {
-        stage(1, 1);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kLps) : "memory");
-      } else {
+#pragma unroll
+      for (int i = 0; i < S; ++i)
+        if (i < T) stage(i, i);
+      if (T >= S)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * kLps) : "memory");
+      else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       int cur = 0;
       for (int t = 0; t < T; ++t) {
-        if (t + 2 < T) stage(t + 2, cur == 0 ? 2 : cur - 1);
+        if (t + S < T) stage(t + S, cur == 0 ? NBUF - 1 : cur - 1);
         compute(cur);
-        if (t + 2 < T)
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kLps) : "memory");
+        if (t + S < T)
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((S - 1) * kLps) : "memory");
         else
           asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
-        cur = cur == 2 ? 0 : cur + 1;
+        cur = cur == NBUF - 1 ? 0 : cur + 1;
       }
     } else {
       stage(0, 0);
@@ -938,7 +942,7 @@ hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
                             : a.m_tiles * a.n_tiles * a.ksplit;
   // stage buffers: pipe 0 (variants 0..3) two, pipe 1 (4..7) three, pipe 2 (8..11) one (serial,
   // high occupancy); a single K step always one
-  const int nb = a.Ktot == kBK || pipe == 2 ? 1 : (pipe == 1 ? 3 : 2);
+  const int nb = a.Ktot == kBK || pipe == 2 ? 1 : (pipe == 1 ? 4 : 2);
   const int epi = (a.part == nullptr && a.bn_acc == nullptr) ? 0 : (a.bnx != nullptr ? 2 : 1);
 #define ARENA_CONV_LAUNCH(E, NB, P) \
   hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, E, NB, C16, P>), dim3(nwg), dim3(kThreads), 0, st, a)
@@ -947,7 +951,7 @@ hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
          hipLaunchKernelGGL((conv_fwd_kernel_occ4<BM, BN, E, C16, P>), dim3(nwg), dim3(kThreads), 0, st, a); \
        else if (nb == 1) ARENA_CONV_LAUNCH(E, 1, P); \
        else if (nb == 2) ARENA_CONV_LAUNCH(E, 2, P); \
-       else ARENA_CONV_LAUNCH(E, 3, P); } while (0)
+       else ARENA_CONV_LAUNCH(E, 4, P); } while (0)
 #define ARENA_CONV_NB(E) \
   do { if constexpr (C16) ARENA_CONV_NBP(E, false); \
        else if (a.tpb > 1) ARENA_CONV_NBP(E, true); else ARENA_CONV_NBP(E, false); } while (0)
@@ -979,7 +983,7 @@ extern "C" {
 // Returns hipErrorInvalidValue for shapes the kernel does not cover (the caller falls back to
 // MIOpen): C % 64 != 0, Cout % 64 != 0, or an unknown tile variant.
 // variant: 0 = 128x128, 1 = 128x64, 2 = 64x128, 3 = 64x64 (BM x BN output tile per block);
-// variant + 4: the same tile with a three-stage K pipeline (two glds steps in flight);
+// variant + 4: the same tile with a four-stage K pipeline (three glds steps in flight);
 // variant + 8: one stage buffer, serial K loop, high occupancy (streaming-bound 1x1 shapes).
 // 12 / 13: 256x128 / 256x64 on 8 waves, two stage buffers; 14 / 15: the same, three.
 // part (optional): BatchNorm partials of y, [ceil(M / BM)][2][Cout] (EPI 1 / EPI 2 epilogues).

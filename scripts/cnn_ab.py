@@ -11,8 +11,8 @@ input/weight casts and weight transform as torch ops) and/or ``:nomask`` (the la
 dy * mask for the residual join instead of parking (dy, bits)) and/or ``:finP<n>`` (at most n
 level-1 blocks per channel group in the BN finalize kernels) and/or ``:accP<n>`` (conv-epilogue
 BN statistics as fp64 sums up to n tile-channel pairs) and/or ``:finbwd0`` (BN backward sums
-from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv forms), joined
-with ``+``.
+from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv forms) and/or
+``:nostempool`` (stem BN and max pool unfused), joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
     python scripts/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
@@ -71,6 +71,8 @@ def main():
         _bn.set_fin_bwd("finbwd0" not in opt_s.split("+"))
         # nopersist: no persistent conv forms among the autotuner's candidates
         conv.set_persist("nopersist" not in opt_s.split("+"))
+        # nostempool: stem BN apply + max pool kernels instead of the fused pass
+        _bn.set_stem_pool_fused("nostempool" not in opt_s.split("+"))
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
             cnn_bench.train_step(model, opt, x, y, torch.bfloat16)

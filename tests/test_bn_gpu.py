@@ -261,3 +261,57 @@ def test_bn_accumulators_rezeroed_across_steps(C):
     torch.testing.assert_close(m.running_mean, ref.running_mean, rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(m.running_var, ref.running_var, rtol=1e-4, atol=1e-5)
     assert int(m.num_batches_tracked) == int(ref.num_batches_tracked)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_bn_relu_maxpool_fused_matches_modules(dtype):
+    """The fused stem (BN + ReLU + 3x3/2 max pool, statistics summed by the conv epilogue):
+    pooled output bit-identical to BatchNormAct2d + MaxPool2dNHWC, same running statistics,
+    gradients equal to rounding (the fused backward does not round the pooled gradient to the
+    activation dtype before the BN reduction), over repeated steps (accumulator re-zeroing)."""
+    from arena_amd.ops import batchnorm, conv
+    from arena_amd.ops.pool import MaxPool2dNHWC
+    torch.manual_seed(4)
+    N, Cin, C, H, W = 4, 64, 64, 18, 17
+    mods = []
+    for _ in range(2):
+        bn = batchnorm.BatchNormAct2d(C).cuda()
+        with torch.no_grad():
+            bn.weight.copy_(torch.linspace(0.5, 1.5, C))
+            bn.bias.copy_(torch.linspace(-0.2, 0.3, C))
+        mods.append((bn, MaxPool2dNHWC(3, 2, 1)))
+    wt = _nhwc((torch.randn(C, Cin, 3, 3, device="cuda") * 0.05).to(torch.bfloat16))
+    try:
+        for step in range(3):
+            xin = _nhwc(torch.randn(N, Cin, H, W, device="cuda").to(torch.bfloat16))
+            g = None
+            outs = []
+            for fused, (bn, pool) in zip((True, False), mods):
+                batchnorm.set_stem_pool_fused(fused)
+                y, st = conv.conv2d_fwd(xin, wt, 1, 1, with_stats=True, final=True)
+                y = y.to(dtype).detach().requires_grad_(True) if dtype != torch.bfloat16 else \
+                    y.detach().requires_grad_(True)
+                if dtype != torch.bfloat16:     # fp32 BN input: a statistics pass, not the sums
+                    st.discard()
+                    st = batchnorm.FinishedStats(st.fin)
+                    with torch.no_grad():
+                        yf = y.double()
+                        st.fin[0].copy_(yf.sum(dim=(0, 2, 3)))
+                        st.fin[1].copy_((yf * yf).sum(dim=(0, 2, 3)))
+                out = batchnorm.bn_relu_maxpool(bn, pool, y, st)
+                if g is None:
+                    g = _nhwc(torch.randn(out.shape, device="cuda").to(out.dtype))
+                out.backward(g)
+                outs.append((out.detach(), y.grad, bn.weight.grad.clone(), bn.bias.grad.clone()))
+                bn.weight.grad = bn.bias.grad = None
+            (o1, dx1, dw1, db1), (o2, dx2, dw2, db2) = outs
+            assert torch.equal(o1, o2), step
+            tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4,
+                                                                                   atol=1e-5)
+            torch.testing.assert_close(dx1.float(), dx2.float(), **tol)
+            torch.testing.assert_close(dw1, dw2, rtol=1e-3, atol=1e-3)
+            torch.testing.assert_close(db1, db2, rtol=1e-3, atol=1e-3)
+            torch.testing.assert_close(mods[0][0].running_var, mods[1][0].running_var)
+            assert int(mods[0][0].num_batches_tracked) == step + 1
+    finally:
+        batchnorm.set_stem_pool_fused(True)
