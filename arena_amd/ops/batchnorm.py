@@ -289,10 +289,10 @@ def set_stem_pool_fused(on: bool) -> None:
 class _BNPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, num_batches,
-                fin, bacc, k, s, p):
+                fin, part, rpb, bacc, k, s, p):
         y, pos, mean, invstd, scale, shift = _ext.load().bn_pool_fwd(
-            x, weight, bias, running_mean, running_var, momentum, eps, num_batches, fin, k, s, p,
-            bacc.take_zero())
+            x, weight, bias, running_mean, running_var, momentum, eps, num_batches, fin, part,
+            rpb, k, s, p, bacc.take_zero())
         ctx.save_for_backward(x, pos, mean, invstd, scale, shift, weight)
         ctx.fin, ctx.bacc, ctx.geom = fin, bacc, (k, s, p)
         ctx.affine = weight is not None
@@ -307,21 +307,23 @@ class _BNPoolFn(torch.autograd.Function):
             dy, pos, x, mean, invstd, scale, shift, weight, ctx.affine, *ctx.geom,
             ctx.bacc.for_backward(x, x.shape[1]), ctx.fin)
         return (dx, dgamma if ctx.affine else None, dbeta if ctx.affine else None, None, None,
-                None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None)
 
 
 def bn_relu_maxpool(bn: BatchNormAct2d, pool: nn.Module, x: torch.Tensor, stats=None):
     """``pool(bn(x, stats=stats))`` for a ReLU ``BatchNormAct2d`` followed by a max pool
-    (``MaxPool2dNHWC``: kernel_size / stride / padding), fused on MI355X when the statistics come
-    summed from the producing conv (``FinishedStats``) in training mode; the two modules otherwise.
-    """
+    (``MaxPool2dNHWC``: kernel_size / stride / padding), fused on MI355X in training mode when the
+    statistics come from the producing conv (``FinishedStats`` sums or per-tile partials); the
+    two modules otherwise."""
     k, s, p = pool.kernel_size, pool.stride, pool.padding
     fused = (_STEM_POOL_FUSED and bn.training and bn.relu and bn.track_running_stats
-             and bn.momentum is not None and isinstance(stats, FinishedStats)
+             and bn.momentum is not None and stats is not None
              and kernel_ok(x) and x.shape[1] <= 256 and isinstance(k, int) and isinstance(s, int)
              and isinstance(p, int) and (k + s - 1) // s == 2 and 2 * p <= k
              and x.shape[2] + 2 * p >= k and x.shape[3] + 2 * p >= k)
     if not fused:
         return pool(bn(x, stats=stats))
+    fin, part, rpb = (stats.fin, None, 0) if isinstance(stats, FinishedStats) else \
+        (None, stats[0], int(stats[1]))
     return _BNPoolFn.apply(x, bn.weight, bn.bias, bn.running_mean, bn.running_var, bn.momentum,
-                           bn.eps, bn.num_batches_tracked, stats.fin, bn._bacc, k, s, p)
+                           bn.eps, bn.num_batches_tracked, fin, part, rpb, bn._bacc, k, s, p)

@@ -101,7 +101,8 @@ hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, vo
                         int, hipStream_t);
 int arena_bn_acc_ok(long long, int);
 hipError_t arena_bn_pool_fwd(int, const void*, void*, uint8_t*, int, int, int, int, int, int, int,
-                             ArenaBNStats, const double*, double*, int, hipStream_t);
+                             ArenaBNStats, const double*, const float*, int, long long, double*,
+                             unsigned*, double*, int, hipStream_t);
 hipError_t arena_bn_pool_bwd(int, const void*, const uint8_t*, const void*, void*, int, int, int,
                              int, int, int, int, ArenaBNBwd, double*, double*, int, hipStream_t);
 #ifdef ARENA_TIMELINE
@@ -1055,18 +1056,36 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
 }
 
 // Fused stem BatchNorm + ReLU + k x k / s max pool (training; bn_kernels.hip arena_bn_pool_fwd):
-// x is the BN input with its statistics summed by the producing conv (fin, fp64 [2][C]).
+// x is the BN input with its statistics from the producing conv: summed (fin, fp64 [2][C]) or as
+// per-tile partials (stats_part, stats_rpb rows per partial; fin then empty).
 // Returns (y, pos, mean, invstd, scale, shift): the pooled output, its uint8 in-window argmax,
 // and the saved statistics. fin stays in place until bn_pool_bwd(zero_f=fin) zeroes it; zero_b:
 // as in bn_fwd.
 std::vector<Tensor> bn_pool_fwd(Tensor x, OptT gamma, OptT beta, OptT running_mean,
                                 OptT running_var, double momentum, double eps, OptT num_batches,
-                                Tensor fin, int64_t k, int64_t s, int64_t p, OptT zero_b) {
+                                OptT fin, OptT stats_part, int64_t stats_rpb, int64_t k, int64_t s,
+                                int64_t p, OptT zero_b) {
   const BNGeom g = bn_geom(x, "x");
-  TORCH_CHECK(fin.is_cuda() && fin.device() == x.device() &&
-                  fin.scalar_type() == torch::kFloat64 && fin.is_contiguous() &&
-                  fin.numel() == 2 * g.C,
-              "bn_pool_fwd: fin must be the fp64 [2, C] statistics sums");
+  TORCH_CHECK(fin.has_value() != stats_part.has_value(),
+              "bn_pool_fwd: give the statistics as fin sums or as stats_part partials");
+  if (fin.has_value())
+    TORCH_CHECK(fin->is_cuda() && fin->device() == x.device() &&
+                    fin->scalar_type() == torch::kFloat64 && fin->is_contiguous() &&
+                    fin->numel() == 2 * g.C,
+                "bn_pool_fwd: fin must be the fp64 [2, C] statistics sums");
+  int ext_nblk = 0;
+  Tensor lvl2;
+  unsigned* tickets = nullptr;
+  if (stats_part.has_value()) {
+    check_f32(*stats_part, "stats_part");
+    TORCH_CHECK(stats_rpb > 0 && stats_part->is_contiguous(), "stats_part: bad layout");
+    const int64_t nblk = (g.M + stats_rpb - 1) / stats_rpb;
+    TORCH_CHECK(stats_part->numel() == nblk * 2 * g.C, "stats_part has ", stats_part->numel(),
+                " floats, expected ", nblk * 2 * g.C);
+    ext_nblk = (int)nblk;
+    lvl2 = bn_lvl2(nblk, g.C, x);
+    tickets = bn_tickets(x);
+  }
   auto f32 = x.options().dtype(torch::kFloat32);
   Tensor mean = torch::empty({g.C}, f32), invstd = torch::empty({g.C}, f32);
   Tensor scale = torch::empty({g.C}, f32), shift = torch::empty({g.C}, f32);
@@ -1105,7 +1124,11 @@ std::vector<Tensor> bn_pool_fwd(Tensor x, OptT gamma, OptT beta, OptT running_me
   }
   check_hip(arena_bn_pool_fwd(g.dtype, x.data_ptr(), y.data_ptr(), pos.data_ptr<uint8_t>(), (int)N,
                               (int)H, (int)W, (int)g.C, (int)k, (int)s, (int)p, st,
-                              fin.data_ptr<double>(), zb, nzb, cur_stream()),
+                              fin.has_value() ? fin->data_ptr<double>() : nullptr,
+                              stats_part.has_value() ? stats_part->data_ptr<float>() : nullptr,
+                              ext_nblk, (long long)stats_rpb,
+                              lvl2.defined() ? lvl2.data_ptr<double>() : nullptr, tickets, zb, nzb,
+                              cur_stream()),
             "bn_pool_fwd");
   return {y, pos, mean, invstd, scale, shift};
 }

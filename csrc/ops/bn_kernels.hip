@@ -733,8 +733,9 @@ __device__ __forceinline__ float stored_val(float v) {   // the value bn_apply w
   else return v;
 }
 
-// dynamic shared memory: 3 * C floats. grid: (N * OH output rows, ceil(OW * C/8 / kT))
-template <typename T>
+// dynamic shared memory: 3 * C floats. grid: (N * OH output rows, ceil(OW * C/8 / kT)).
+// FIN: coefficients from the fp64 sums `fin`; else from st (a partial-merge finalize ran first).
+template <typename T, bool FIN>
 __global__ __launch_bounds__(kT) void bn_pool_fwd_kernel(const T* __restrict__ x,
                                                          T* __restrict__ y,
                                                          uint8_t* __restrict__ pos,
@@ -744,7 +745,7 @@ __global__ __launch_bounds__(kT) void bn_pool_fwd_kernel(const T* __restrict__ x
                                                          double* __restrict__ zero, int nzero) {
   extern __shared__ __attribute__((aligned(16))) float s_co[];
   const int C = g.C, cg = C / kVec;
-  apply_coefs<true>(C, M, fin, st, s_co);
+  apply_coefs<FIN>(C, M, fin, st, s_co);
   zero_duty(zero, nzero);
   const int row = blockIdx.x;
   const int t = blockIdx.y * kT + threadIdx.x;
@@ -794,10 +795,14 @@ __device__ __forceinline__ void pool_grad8(const T* __restrict__ dy,
                                            const uint8_t* __restrict__ pos, const PoolG& g,
                                            long long r, int c8, float out[kVec]) {
   constexpr int CW = 2;
-  const int w = (int)(r % g.W);
-  const long long nh = r / g.W;
-  const int h = (int)(nh % g.H);
-  const long long n = nh / g.H;
+  // 32-bit index math (M < 2^31, host-checked): a 64-bit division is a ~100-instruction
+  // software sequence, and these run once per 8-channel vector
+  const unsigned ru = (unsigned)r;
+  const unsigned nh = ru / (unsigned)g.W;
+  const int w = (int)(ru - nh * (unsigned)g.W);
+  const unsigned n32 = nh / (unsigned)g.H;
+  const int h = (int)(nh - n32 * (unsigned)g.H);
+  const long long n = n32;
   const int th = h + g.p - g.k + 1, tw = w + g.p - g.k + 1;
   const int oh_lo = th <= 0 ? 0 : (th + g.s - 1) / g.s;
   const int ow_lo = tw <= 0 ? 0 : (tw + g.s - 1) / g.s;
@@ -860,7 +865,27 @@ __global__ __launch_bounds__(kT) void bn_pool_bwd_reduce_kernel(const T* __restr
   lds8(s_c + C + q.g * kVec, sc);
   lds8(s_c + 2 * C + q.g * kVec, sh);
   if (q.slot < q.rip) {
-    for (long long r = r0 + q.slot; r < r1; r += q.rip) {
+    // two rows per step: both rows' gathers (8 position + 8 gradient loads) and x loads are in
+    // flight together (one row per step: 170 us at batch 128, two: 151 us)
+    long long r = r0 + q.slot;
+    for (; r + q.rip < r1; r += 2LL * q.rip) {
+      float gv[2][kVec], v[2][kVec];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        V8<T>::load(x + (r + u * q.rip) * C + (long long)q.g * kVec, v[u]);
+        pool_grad8<T>(dy, pos, g, r + u * q.rip, q.g, gv[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < kVec; ++i) {
+          const bool on = stored_val<T>(fmaxf(fmaf(v[u][i] - mu[i], sc[i], sh[i]), 0.f)) > 0.f;
+          const float gg = on ? gv[u][i] : 0.f;
+          sg[i] += gg;
+          sgx[i] = fmaf(gg, v[u][i] - mu[i], sgx[i]);
+        }
+    }
+    for (; r < r1; r += q.rip) {
       float gv[kVec], v[kVec];
       V8<T>::load(x + r * C + (long long)q.g * kVec, v);
       pool_grad8<T>(dy, pos, g, r, q.g, gv);
@@ -933,11 +958,12 @@ __global__ __launch_bounds__(kT) void bn_pool_bwd_dx_kernel(const T* __restrict_
   lds8(s_co + 3 * C + c8 * kVec, mu);
   lds8(s_co + 4 * C + c8 * kVec, sc);
   lds8(s_co + 5 * C + c8 * kVec, sh);
+  const int sh_cg = __builtin_ctz(cg);   // cg is a power of two
+  // (two vectors per step measured slower here: 146 vs 131 us at batch 128)
   for (long long v = (long long)blockIdx.x * kT + threadIdx.x; v < nvec; v += stride) {
-    const long long r = v / cg;
     float gv[kVec], xv[kVec], o[kVec];
     V8<T>::load(x + v * kVec, xv);
-    pool_grad8<T>(dy, pos, g, r, c8, gv);
+    pool_grad8<T>(dy, pos, g, (long long)((unsigned long long)v >> sh_cg), c8, gv);
 #pragma unroll
     for (int i = 0; i < kVec; ++i) {
       const bool on = stored_val<T>(fmaxf(fmaf(xv[i] - mu[i], sc[i], sh[i]), 0.f)) > 0.f;
@@ -1182,27 +1208,38 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
   return hipGetLastError();
 }
 
-// Fused stem forward (training, acc-mode statistics `fin` from the producing conv): y = the
-// max pool of relu(bn(x)), pos = its in-window argmax. Only the 3x3 / 2 style pools whose inputs
-// have <= 2 x 2 candidate windows, C % 8 == 0, C <= 256. zero / nzero: see arena_bn_fwd.
+// Fused stem forward (training): y = the max pool of relu(bn(x)), pos = its in-window argmax.
+// Statistics: acc-mode sums `fin` from the producing conv, or (fin == null) its per-tile partials
+// `part` [ext_nblk][2][C] (ext_rpb rows each), merged first by the finalize kernel (lvl2 /
+// tickets as in arena_bn_fwd). Only the 3x3 / 2 style pools whose inputs have <= 2 x 2 candidate
+// windows, C % 8 == 0, C <= 256. zero / nzero: see arena_bn_fwd.
 hipError_t arena_bn_pool_fwd(int dtype, const void* x, void* y, uint8_t* pos, int N, int H, int W,
                              int C, int k, int s, int p, ArenaBNStats st, const double* fin,
-                             double* zero, int nzero, hipStream_t stream) {
+                             const float* part, int ext_nblk, long long ext_rpb, double* lvl2,
+                             unsigned* tickets, double* zero, int nzero, hipStream_t stream) {
   PoolG g{N, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
-  if (bad_shape((long long)N * H * W, C) || C > 256 || fin == nullptr || (k + s - 1) / s != 2 ||
-      2 * p > k || g.OH <= 0 || g.OW <= 0)
+  const long long M = (long long)N * H * W;
+  if (bad_shape(M, C) || C > 256 || (k + s - 1) / s != 2 || 2 * p > k || g.OH <= 0 || g.OW <= 0)
     return hipErrorInvalidValue;
+  if (fin == nullptr) {
+    if (part == nullptr || ext_nblk <= 0 || ext_rpb <= 0 || (long long)ext_nblk * ext_rpb < M ||
+        lvl2 == nullptr || tickets == nullptr)
+      return hipErrorInvalidValue;
+    hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 63) / 64, fin_blocks_per_group(ext_nblk)),
+                       dim3(kT), 0, stream, part, ext_nblk, M, C, ext_rpb, lvl2, tickets, st);
+  }
   const int cg = C / kVec;
   const dim3 grid((unsigned)(N * g.OH), (unsigned)((g.OW * cg + kT - 1) / kT));
-  const long long M = (long long)N * H * W;
-  if (dtype == 1)
-    hipLaunchKernelGGL(bn_pool_fwd_kernel<uint16_t>, grid, dim3(kT), 3 * C * 4, stream,
-                       static_cast<const uint16_t*>(x), static_cast<uint16_t*>(y), pos, st, fin,
-                       M, g, zero, nzero);
-  else
-    hipLaunchKernelGGL(bn_pool_fwd_kernel<float>, grid, dim3(kT), 3 * C * 4, stream,
-                       static_cast<const float*>(x), static_cast<float*>(y), pos, st, fin, M, g,
-                       zero, nzero);
+#define ARENA_BN_POOL(TT, F)                                                                   \
+  hipLaunchKernelGGL((bn_pool_fwd_kernel<TT, F>), grid, dim3(kT), 3 * C * 4, stream,          \
+                     static_cast<const TT*>(x), static_cast<TT*>(y), pos, st, fin, M, g, zero, \
+                     nzero)
+  if (dtype == 1) {
+    if (fin) ARENA_BN_POOL(uint16_t, true); else ARENA_BN_POOL(uint16_t, false);
+  } else {
+    if (fin) ARENA_BN_POOL(float, true); else ARENA_BN_POOL(float, false);
+  }
+#undef ARENA_BN_POOL
   return hipGetLastError();
 }
 
@@ -1215,11 +1252,16 @@ hipError_t arena_bn_pool_bwd(int dtype, const void* dy, const uint8_t* pos, cons
                              double* acc, double* zero, int nzero, hipStream_t stream) {
   PoolG g{N, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
   const long long M = (long long)N * H * W;
-  if (bad_shape(M, C) || C > 256 || acc == nullptr || co.scale == nullptr ||
+  if (bad_shape(M, C) || C > 256 || M >= (1LL << 31) || acc == nullptr || co.scale == nullptr ||
       co.shift == nullptr || (k + s - 1) / s != 2 || 2 * p > k || g.OH <= 0 || g.OW <= 0)
     return hipErrorInvalidValue;
+  // up to 4x the usual reduction grid: the stem's C = 64 leaves 512 row blocks latency-bound
+  // on their gathers, and 2048 x 64 sums are still few atomics
+  const long long saved_max = g_max_reduce_blocks;
+  g_max_reduce_blocks = saved_max * 4;
   long long rpb;
   const long long nb = reduce_blocks(M, C, &rpb);
+  g_max_reduce_blocks = saved_max;
   const long long nvec = M * (C / kVec);
   long long ne = (nvec + kT - 1) / kT;
   ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);

@@ -263,8 +263,9 @@ def test_bn_accumulators_rezeroed_across_steps(C):
     assert int(m.num_batches_tracked) == int(ref.num_batches_tracked)
 
 
-@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
-def test_bn_relu_maxpool_fused_matches_modules(dtype):
+@pytest.mark.parametrize("dtype,partials", [(torch.bfloat16, False), (torch.float32, False),
+                                            (torch.bfloat16, True)])
+def test_bn_relu_maxpool_fused_matches_modules(dtype, partials):
     """The fused stem (BN + ReLU + 3x3/2 max pool, statistics summed by the conv epilogue):
     pooled output bit-identical to BatchNormAct2d + MaxPool2dNHWC, same running statistics,
     gradients equal to rounding (the fused backward does not round the pooled gradient to the
@@ -288,7 +289,7 @@ def test_bn_relu_maxpool_fused_matches_modules(dtype):
             outs = []
             for fused, (bn, pool) in zip((True, False), mods):
                 batchnorm.set_stem_pool_fused(fused)
-                y, st = conv.conv2d_fwd(xin, wt, 1, 1, with_stats=True, final=True)
+                y, st = conv.conv2d_fwd(xin, wt, 1, 1, with_stats=True, final=not partials)
                 y = y.to(dtype).detach().requires_grad_(True) if dtype != torch.bfloat16 else \
                     y.detach().requires_grad_(True)
                 if dtype != torch.bfloat16:     # fp32 BN input: a statistics pass, not the sums
@@ -309,8 +310,11 @@ def test_bn_relu_maxpool_fused_matches_modules(dtype):
             tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-4,
                                                                                    atol=1e-5)
             torch.testing.assert_close(dx1.float(), dx2.float(), **tol)
-            torch.testing.assert_close(dw1, dw2, rtol=1e-3, atol=1e-3)
-            torch.testing.assert_close(db1, db2, rtol=1e-3, atol=1e-3)
+            # per-channel sums over bf16-rounded vs fp32 pool gradients: compare at the scale of
+            # the largest entry
+            lim = 1e-2 if dtype == torch.bfloat16 else 1e-4
+            for a, b in ((dw1, dw2), (db1, db2)):
+                assert float((a - b).abs().max()) <= lim * float(b.abs().max()), (step, a, b)
             torch.testing.assert_close(mods[0][0].running_var, mods[1][0].running_var)
             assert int(mods[0][0].num_batches_tracked) == step + 1
     finally:
