@@ -974,6 +974,196 @@ __global__ __launch_bounds__(kT) void bn_pool_bwd_dx_kernel(const T* __restrict_
   }
 }
 
+// ---- the ResNet stem's 3x3 / stride 2 / pad 1 pool: gradients per 2x2 input quad ----
+// Input row 2i is in window row i only, row 2i+1 in rows i and i+1 (same for columns), so the
+// quad {2i, 2i+1} x {2j, 2j+1} needs exactly the 4 windows (i..i+1) x (j..j+1), and the window
+// position each pixel has in each of them is fixed: one gather of 4 windows serves 4 pixels.
+// Per pixel that is 24 bytes of position + gradient reads instead of 96 (4 clamped windows each
+// in pool_grad8) -- the generic path was gather-bound at ~3x its x-stream time.
+struct Quad8 {
+  float g[4][kVec];   // pixel (2i + a, 2j + b) -> g[2a + b]
+};
+
+template <typename T>
+__device__ __forceinline__ void quad_grad8(const T* __restrict__ dy,
+                                           const uint8_t* __restrict__ pos, const PoolG& g,
+                                           int n, int i, int j, int c8, Quad8& o) {
+  uint2 pk[4];
+  float d[4][kVec];
+  bool ok[4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) {
+      const int w = 2 * a + b;
+      ok[w] = i + a < g.OH && j + b < g.OW;
+      const int oh = ok[w] ? i + a : i, ow = ok[w] ? j + b : j;   // clamped: always a window
+      const long long off = (((long long)n * g.OH + oh) * g.OW + ow) * g.C + (long long)c8 * kVec;
+      pk[w] = *reinterpret_cast<const uint2*>(pos + off);
+      V8<T>::load(dy + off, d[w]);
+    }
+  // (window, in-window position) that points at each pixel of the quad
+  constexpr int kPosOf[4][4] = {{4, -1, -1, -1}, {5, 3, -1, -1}, {7, -1, 1, -1}, {8, 6, 2, 0}};
+#pragma unroll
+  for (int px = 0; px < 4; ++px)
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) o.g[px][e] = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) {
+    const uint32_t ps[2] = {pk[w].x, pk[w].y};
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const int want = kPosOf[px][w];
+      if (want < 0) continue;
+#pragma unroll
+      for (int e = 0; e < kVec; ++e)
+        o.g[px][e] += (ok[w] && ((ps[e >> 2] >> (8 * (e & 3))) & 0xff) == (uint32_t)want)
+                          ? d[w][e] : 0.f;
+    }
+  }
+}
+
+__device__ __forceinline__ void quad_of(unsigned qd, int QH, int QW, int* n, int* i, int* j) {
+  const unsigned nq = qd / (unsigned)QW;
+  *j = (int)(qd - nq * (unsigned)QW);
+  const unsigned nn = nq / (unsigned)QH;
+  *i = (int)(nq - nn * (unsigned)QH);
+  *n = (int)nn;
+}
+
+// Backward reduction over quads (rows of the Geo layout are quads; 4 pixel vectors each).
+template <typename T>
+__global__ __launch_bounds__(kT) void bn_pool_bwd_reduce_q_kernel(const T* __restrict__ dy,
+                                                                  const uint8_t* __restrict__ pos,
+                                                                  const T* __restrict__ x,
+                                                                  long long NQ, long long rpb,
+                                                                  PoolG g, ArenaBNBwd co,
+                                                                  double* __restrict__ acc) {
+  __shared__ __attribute__((aligned(16))) float s_c[3 * 256];
+  const int C = g.C;
+  for (int c = threadIdx.x; c < C; c += kT) {
+    s_c[c] = co.mean[c];
+    s_c[C + c] = co.scale[c];
+    s_c[2 * C + c] = co.shift[c];
+  }
+  __syncthreads();
+  const Geo q = geo(C);
+  long long r0, r1;
+  block_rows(NQ, rpb, &r0, &r1);
+  const int QH = (g.H + 1) / 2, QW = (g.W + 1) / 2;
+  float sg[kVec], sgx[kVec], mu[kVec], sc[kVec], sh[kVec];
+#pragma unroll
+  for (int e = 0; e < kVec; ++e) sg[e] = sgx[e] = 0.f;
+  lds8(s_c + q.g * kVec, mu);
+  lds8(s_c + C + q.g * kVec, sc);
+  lds8(s_c + 2 * C + q.g * kVec, sh);
+  if (q.slot < q.rip) {
+    for (long long r = r0 + q.slot; r < r1; r += q.rip) {
+      int n, i, j;
+      quad_of((unsigned)r, QH, QW, &n, &i, &j);
+      Quad8 gq;
+      quad_grad8<T>(dy, pos, g, n, i, j, q.g, gq);
+#pragma unroll
+      for (int px = 0; px < 4; ++px) {
+        const int h = 2 * i + (px >> 1), w = 2 * j + (px & 1);
+        if (h >= g.H || w >= g.W) continue;
+        float v[kVec];
+        V8<T>::load(x + (((long long)n * g.H + h) * g.W + w) * C + (long long)q.g * kVec, v);
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) {
+          const bool on = stored_val<T>(fmaxf(fmaf(v[e] - mu[e], sc[e], sh[e]), 0.f)) > 0.f;
+          const float gg = on ? gq.g[px][e] : 0.f;
+          sg[e] += gg;
+          sgx[e] = fmaf(gg, v[e] - mu[e], sgx[e]);
+        }
+      }
+    }
+  }
+  __shared__ float s_g[kT * kVec], s_gx[kT * kVec];
+  if (q.slot < q.rip) {
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) {
+      s_g[q.slot * q.cw + q.gl * kVec + e] = sg[e];
+      s_gx[q.slot * q.cw + q.gl * kVec + e] = sgx[e];
+    }
+  }
+  __syncthreads();
+  for (int cl = threadIdx.x; cl < q.cw; cl += kT) {
+    float a = 0.f, b = 0.f;
+    for (int s2 = 0; s2 < q.rip; ++s2) {
+      a += s_g[s2 * q.cw + cl];
+      b += s_gx[s2 * q.cw + cl];
+    }
+    unsafeAtomicAdd(acc + q.cb + cl, (double)a);
+    unsafeAtomicAdd(acc + C + q.cb + cl, (double)b);
+  }
+}
+
+// dx over quads; dynamic shared memory: 6 * C floats (as bn_pool_bwd_dx_kernel)
+template <typename T>
+__global__ __launch_bounds__(kT) void bn_pool_bwd_dx_q_kernel(const T* __restrict__ dy,
+                                                              const uint8_t* __restrict__ pos,
+                                                              const T* __restrict__ x,
+                                                              T* __restrict__ dx, long long nqv,
+                                                              PoolG g, ArenaBNBwd co,
+                                                              const double* __restrict__ acc,
+                                                              long long M,
+                                                              double* __restrict__ zero,
+                                                              int nzero) {
+  extern __shared__ __attribute__((aligned(16))) float s_co[];
+  const int C = g.C, cg = C / kVec;
+  const long long stride = (long long)gridDim.x * kT;
+  const int c8 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1));
+  const double inv_m = 1.0 / (double)M;
+  for (int c = threadIdx.x; c < C; c += kT) {
+    const double a = acc[c], b = acc[C + c];
+    const float invstd = co.invstd[c];
+    const float gam = co.gamma ? co.gamma[c] : 1.f;
+    s_co[c] = gam * invstd;
+    s_co[C + c] = (float)(a * inv_m);
+    s_co[2 * C + c] = (float)(b * inv_m) * invstd * invstd;
+    s_co[3 * C + c] = co.mean[c];
+    s_co[4 * C + c] = co.scale[c];
+    s_co[5 * C + c] = co.shift[c];
+    if (blockIdx.x == 0) {
+      if (co.dgamma) co.dgamma[c] = (float)(b * invstd);
+      if (co.dbeta) co.dbeta[c] = (float)a;
+    }
+  }
+  __syncthreads();
+  zero_duty(zero, nzero);
+  float ca[kVec], cb[kVec], cc[kVec], mu[kVec], sc[kVec], sh[kVec];
+  lds8(s_co + c8 * kVec, ca);
+  lds8(s_co + C + c8 * kVec, cb);
+  lds8(s_co + 2 * C + c8 * kVec, cc);
+  lds8(s_co + 3 * C + c8 * kVec, mu);
+  lds8(s_co + 4 * C + c8 * kVec, sc);
+  lds8(s_co + 5 * C + c8 * kVec, sh);
+  const int sh_cg = __builtin_ctz(cg);
+  const int QH = (g.H + 1) / 2, QW = (g.W + 1) / 2;
+  for (long long v = (long long)blockIdx.x * kT + threadIdx.x; v < nqv; v += stride) {
+    int n, i, j;
+    quad_of((unsigned)((unsigned long long)v >> sh_cg), QH, QW, &n, &i, &j);
+    Quad8 gq;
+    quad_grad8<T>(dy, pos, g, n, i, j, c8, gq);
+#pragma unroll
+    for (int px = 0; px < 4; ++px) {
+      const int h = 2 * i + (px >> 1), w = 2 * j + (px & 1);
+      if (h >= g.H || w >= g.W) continue;
+      const long long off = (((long long)n * g.H + h) * g.W + w) * C + (long long)c8 * kVec;
+      float xv[kVec], o[kVec];
+      V8<T>::load(x + off, xv);
+#pragma unroll
+      for (int e = 0; e < kVec; ++e) {
+        const bool on = stored_val<T>(fmaxf(fmaf(xv[e] - mu[e], sc[e], sh[e]), 0.f)) > 0.f;
+        const float gg = on ? gq.g[px][e] : 0.f;
+        o[e] = ca[e] * (gg - cb[e] - (xv[e] - mu[e]) * cc[e]);
+      }
+      V8<T>::store(dx + off, o);
+    }
+  }
+}
+
 // Blocks for a reduction over M rows: >= 8 row rounds per thread (the loops issue 4 or 2 rounds
 // of loads at once), as many blocks as that allows up to 512 partials. The 7x7 ResNet layers
 // (M = 6272) need the small per-thread share to fill the chip: at 32 rounds per thread they ran
@@ -1265,6 +1455,26 @@ hipError_t arena_bn_pool_bwd(int dtype, const void* dy, const uint8_t* pos, cons
   const long long nvec = M * (C / kVec);
   long long ne = (nvec + kT - 1) / kT;
   ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);
+  if (k == 3 && s == 2 && p == 1) {   // the ResNet stem pool: 2x2 input quads per gather
+    const long long NQ = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);
+    g_max_reduce_blocks = saved_max * 4;
+    long long qrpb;
+    const long long qnb = reduce_blocks(NQ, C, &qrpb);
+    g_max_reduce_blocks = saved_max;
+    const long long nqv = NQ * (C / kVec);
+    long long qne = (nqv + kT - 1) / kT;
+    qne = qne < 1 ? 1 : (qne > 4096 ? 4096 : qne);
+#define ARENA_BN_POOL_Q(TT)                                                                     \
+    hipLaunchKernelGGL(bn_pool_bwd_reduce_q_kernel<TT>, dim3(qnb, 1), dim3(kT), 0, stream,     \
+                       static_cast<const TT*>(dy), pos, static_cast<const TT*>(x), NQ, qrpb, g, \
+                       co, acc);                                                                \
+    hipLaunchKernelGGL(bn_pool_bwd_dx_q_kernel<TT>, dim3(qne), dim3(kT), 6 * C * 4, stream,    \
+                       static_cast<const TT*>(dy), pos, static_cast<const TT*>(x),              \
+                       static_cast<TT*>(dx), nqv, g, co, acc, M, zero, nzero)
+    if (dtype == 1) { ARENA_BN_POOL_Q(uint16_t); } else { ARENA_BN_POOL_Q(float); }
+#undef ARENA_BN_POOL_Q
+    return hipGetLastError();
+  }
   if (dtype == 1) {
     hipLaunchKernelGGL(bn_pool_bwd_reduce_kernel<uint16_t>, dim3(nb, 1), dim3(kT), 0, stream,
                        static_cast<const uint16_t*>(dy), pos, static_cast<const uint16_t*>(x), M,

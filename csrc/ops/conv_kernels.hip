@@ -1694,38 +1694,44 @@ void conv_wgrad_kernel_occ4(WgradArgs a) {
 // are combined in LDS in a fixed order (bit-reproducible). Splitting the split dimension over the
 // block's waves keeps a small dW (4096 floats for a 64x64 1x1 conv, summed over hundreds of slabs)
 // from being a serial chain of dependent load batches (16 us per layer on average before).
-constexpr int kRedCols = 32, kRedGroups = 8, kRedU = 8;
+// COLS x GROUPS = 256 threads. Small weights (a 64x64 1x1 conv has 1024 float4 columns) use the
+// 8 x 32 shape: 32 blocks of the 32 x 8 shape left 224 CUs idle and each thread summed 64 slabs
+// behind one another (7+ us per layer); 8 columns per block give 4x the blocks and a quarter of
+// the chain. The sum order is fixed per shape (bit-reproducible).
+constexpr int kRedU = 8;
 
+template <int COLS, int GROUPS>
 __global__ __launch_bounds__(256) void conv_wgrad_reduce_kernel(const float4* __restrict__ ws,
                                                                 int splits, long long n4,
                                                                 uint2* __restrict__ out_bf,
                                                                 float4* __restrict__ out_f,
                                                                 float scale) {
-  const int col = threadIdx.x % kRedCols, grp = threadIdx.x / kRedCols;
-  const long long i = (long long)blockIdx.x * kRedCols + col;
+  static_assert(COLS * GROUPS == 256, "one block is 256 threads");
+  const int col = threadIdx.x % COLS, grp = threadIdx.x / COLS;
+  const long long i = (long long)blockIdx.x * COLS + col;
   const float4* src = ws + (i < n4 ? i : 0);
   float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
   int k = grp;
-  for (; k + (kRedU - 1) * kRedGroups < splits; k += kRedU * kRedGroups) {
+  for (; k + (kRedU - 1) * GROUPS < splits; k += kRedU * GROUPS) {
     float4 v[kRedU];
 #pragma unroll
-    for (int u = 0; u < kRedU; ++u) v[u] = src[(long long)(k + u * kRedGroups) * n4];
+    for (int u = 0; u < kRedU; ++u) v[u] = src[(long long)(k + u * GROUPS) * n4];
 #pragma unroll
     for (int u = 0; u < kRedU; ++u) {
       acc.x += v[u].x; acc.y += v[u].y; acc.z += v[u].z; acc.w += v[u].w;
     }
   }
-  for (; k < splits; k += kRedGroups) {
+  for (; k < splits; k += GROUPS) {
     const float4 v = src[(long long)k * n4];
     acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
   }
-  __shared__ float4 red[kRedGroups][kRedCols];
+  __shared__ float4 red[GROUPS][COLS];
   red[grp][col] = acc;
   __syncthreads();
   if (grp != 0 || i >= n4) return;
   float4 s = red[0][col];
 #pragma unroll
-  for (int g = 1; g < kRedGroups; ++g) {
+  for (int g = 1; g < GROUPS; ++g) {
     const float4 v = red[g][col];
     s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
   }
@@ -1838,10 +1844,15 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
   if (e != hipSuccess) return e;
   const int splits = arena_conv_wgrad_splits(N, a.Ho, a.Wo, Cout, a.Ktot, variant, splits_hint);
   const long long n4 = (long long)Cout * a.Ktot / 4;  // Cout % 64 == 0
-  const int blocks = (int)((n4 + kRedCols - 1) / kRedCols);
-  hipLaunchKernelGGL(conv_wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, st,
-                     reinterpret_cast<const float4*>(ws), splits, n4,
-                     reinterpret_cast<uint2*>(dw_bf16), reinterpret_cast<float4*>(dw_f32), scale);
+  // the 8 x 32 shape while 32-column blocks would not give every CU a block
+  if (n4 < 32LL * 256 && splits >= 64)
+    hipLaunchKernelGGL((conv_wgrad_reduce_kernel<8, 32>), dim3((unsigned)((n4 + 7) / 8)), dim3(256),
+                       0, st, reinterpret_cast<const float4*>(ws), splits, n4,
+                       reinterpret_cast<uint2*>(dw_bf16), reinterpret_cast<float4*>(dw_f32), scale);
+  else
+    hipLaunchKernelGGL((conv_wgrad_reduce_kernel<32, 8>), dim3((unsigned)((n4 + 31) / 32)),
+                       dim3(256), 0, st, reinterpret_cast<const float4*>(ws), splits, n4,
+                       reinterpret_cast<uint2*>(dw_bf16), reinterpret_cast<float4*>(dw_f32), scale);
   return hipGetLastError();
 }
 

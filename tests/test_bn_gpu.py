@@ -263,9 +263,9 @@ def test_bn_accumulators_rezeroed_across_steps(C):
     assert int(m.num_batches_tracked) == int(ref.num_batches_tracked)
 
 
-@pytest.mark.parametrize("dtype,partials", [(torch.bfloat16, False), (torch.float32, False),
-                                            (torch.bfloat16, True)])
-def test_bn_relu_maxpool_fused_matches_modules(dtype, partials):
+@pytest.mark.parametrize("dtype,partials,pad", [(torch.bfloat16, False, 1), (torch.float32, False, 1),
+                                                (torch.bfloat16, True, 1), (torch.bfloat16, False, 0)])
+def test_bn_relu_maxpool_fused_matches_modules(dtype, partials, pad):
     """The fused stem (BN + ReLU + 3x3/2 max pool, statistics summed by the conv epilogue):
     pooled output bit-identical to BatchNormAct2d + MaxPool2dNHWC, same running statistics,
     gradients equal to rounding (the fused backward does not round the pooled gradient to the
@@ -280,7 +280,7 @@ def test_bn_relu_maxpool_fused_matches_modules(dtype, partials):
         with torch.no_grad():
             bn.weight.copy_(torch.linspace(0.5, 1.5, C))
             bn.bias.copy_(torch.linspace(-0.2, 0.3, C))
-        mods.append((bn, MaxPool2dNHWC(3, 2, 1)))
+        mods.append((bn, MaxPool2dNHWC(3, 2, pad)))   # pad 1: the 2x2-quad backward kernels
     wt = _nhwc((torch.randn(C, Cin, 3, 3, device="cuda") * 0.05).to(torch.bfloat16))
     try:
         for step in range(3):

@@ -18,6 +18,7 @@ SHAPES = [  # n, cin, h, w, cout, k, stride
     (1, 128, 15, 13, 64, 1, 2),
     (2, 192, 6, 5, 256, 3, 1),
     (8, 64, 28, 28, 64, 3, 1),   # 98 pixel steps: the split reduce's unrolled path, 49 BN tiles
+    (8, 64, 28, 28, 64, 1, 1),   # 98 splits of a 64x64 weight: the 8 x 32 split-reduce shape
 ]
 
 
