@@ -648,8 +648,10 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
         # step on these kernels alone stayed bit-identical run to run (scripts/graph_mem_*.py,
         # docs/perf.md "MIOpen inside a captured step"). ARENA_CONV=miopen keeps the library
         # path for comparisons.
-        y = F.conv2d(x, w, stride=stride, padding=pad)
-        dy = torch.randn_like(y)
+        # (a random output gradient of the conv's output shape; no library call: F.conv2d here
+        # ran MIOpen's Find -- its naive and CK kernels -- once per shape, ~0.5 s of startup)
+        dy = torch.randn(x.shape[0], cout, ho, wo, device=x.device, dtype=x.dtype).contiguous(
+            memory_format=torch.channels_last)
         t = {}
         m_out = x.shape[0] * ho * wo
 
