@@ -67,6 +67,7 @@ hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void
                              int, int, int, int, int, int, int, const int*, int, int, double*,
                              int, void*, unsigned*, int, hipStream_t);
 long long arena_conv_fwd_ksplit_floats(long long, int, int, int);
+void arena_conv_set_stats_one_pass(int);
 long long arena_conv_fwd_tiles(long long, int, int);
 int arena_conv_fwd_tile_rows(int);
 hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
@@ -1777,6 +1778,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_set_acc", [](bool on) { g_bn_acc = on; });
   m.def("bn_acc_scratch", [](bool on) { g_acc_scratch = on; });
   m.def("bn_pool_fwd", &bn_pool_fwd);
+  m.def("conv_set_stats_one_pass", [](bool on) { arena_conv_set_stats_one_pass(on ? 1 : 0); });
   m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
     arena_bn_set_reduce_geometry(max_blocks, min_rounds);

@@ -103,6 +103,7 @@ struct ConvArgs {
   unsigned* kcnt;
   int xbytes, wbytes;  // buffer-descriptor ranges of x and w (both < 2^31 bytes, host-checked)
   int tpb;             // output tiles per block (persistent form, see conv_fwd_body); 1 = one
+  int st1p;            // EPI 1 statistics in one pass (sum, sum of squares) instead of two
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -791,7 +792,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
       // batch 128: 94 -> 85 us; profiles/r2_conv_epi_{before,after}.jsonl).
       const int nrows = min(BM, a.M - m0);
       const bool full = nrows == BM;
-      float* red = reinterpret_cast<float*>(lds);   // [NWM][BN]
+      float* red = reinterpret_cast<float*>(lds);   // [NWM][BN] ([NWM][2][BN] single-pass)
       float mean[NI][4], s[NI][4];
       auto exchange = [&](bool first) {   // s (row-16 sums of this wave) -> per-block channel sums
         if (!first) lds_barrier();        // every wave has read the previous sums
@@ -813,6 +814,56 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
             s[j][r] = v;
           }
       };
+      const float inv_n = 1.f / (float)nrows;
+      if (a.st1p) {
+        // single pass (ConvArgs::st1p): sums and sums of squares together, ONE LDS exchange;
+        // M2 = sum y^2 - n mean^2 over the tile's <= 256 rows in fp32 (the cross-tile merge is
+        // fp64): the two-pass form's second exchange and barrier are the epilogue's cost
+        float ss[NI][4];
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          f32x2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f}, q0 = {0.f, 0.f}, q1 = {0.f, 0.f};
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            f32x2 v0 = {acc[i][j][0], acc[i][j][1]}, v1 = {acc[i][j][2], acc[i][j][3]};
+            if (!full && m0 + wm * WM + i * 16 + fr >= a.M) v0 = v1 = f32x2{0.f, 0.f};
+            t0 += v0;
+            t1 += v1;
+            q0 = __builtin_elementwise_fma(v0, v0, q0);
+            q1 = __builtin_elementwise_fma(v1, v1, q1);
+          }
+          s[j][0] = row16_sum(t0.x); s[j][1] = row16_sum(t0.y);
+          s[j][2] = row16_sum(t1.x); s[j][3] = row16_sum(t1.y);
+          ss[j][0] = row16_sum(q0.x); ss[j][1] = row16_sum(q0.y);
+          ss[j][2] = row16_sum(q1.x); ss[j][3] = row16_sum(q1.y);
+        }
+        lds_barrier();   // the coalesced store path's last reads of the staging LDS are done
+        if (fr == 0) {
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int c = wn * WN + j * 16 + 4 * fq + r;
+              red[wm * 2 * BN + c] = s[j][r];
+              red[wm * 2 * BN + BN + c] = ss[j][r];
+            }
+        }
+        lds_barrier();
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int c = wn * WN + j * 16 + 4 * fq + r;
+            float v = red[c], q = red[BN + c];
+#pragma unroll
+            for (int h = 1; h < NWM; ++h) {
+              v += red[h * 2 * BN + c];
+              q += red[h * 2 * BN + BN + c];
+            }
+            mean[j][r] = v * inv_n;
+            s[j][r] = fmaxf(q - v * mean[j][r], 0.f);
+          }
+      } else {
 #pragma unroll
       for (int j = 0; j < NI; ++j) {
         f32x2 t0 = {0.f, 0.f}, t1 = {0.f, 0.f};
@@ -828,7 +879,6 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
       }
       lds_barrier();   // the coalesced store path's last reads of the staging LDS are done
       exchange(true);
-      const float inv_n = 1.f / (float)nrows;
 #pragma unroll
       for (int j = 0; j < NI; ++j)
 #pragma unroll
@@ -849,6 +899,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         s[j][2] = row16_sum(t1.x); s[j][3] = row16_sum(t1.y);
       }
       exchange(false);
+      }
       if (a.bn_acc == nullptr) {
         if (wm == 0 && fr == 0) {
 #pragma unroll
@@ -978,7 +1029,11 @@ hipError_t launch(const ConvArgs& a, int pipe, hipStream_t st) {
 
 }  // namespace
 
+int g_conv_st1p = 0;   // see ConvArgs::st1p (runtime switch: arena_conv_set_stats_one_pass)
+
 extern "C" {
+
+void arena_conv_set_stats_one_pass(int on) { g_conv_st1p = on ? 1 : 0; }
 
 // Returns hipErrorInvalidValue for shapes the kernel does not cover (the caller falls back to
 // MIOpen): C % 64 != 0, Cout % 64 != 0, or an unknown tile variant.
@@ -1066,6 +1121,7 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.kws = (float4*)kws;
   a.kcnt = kcnt;
   a.tpb = tpb;
+  a.st1p = g_conv_st1p;
   if (variant >= 12) {   // 256-row tiles, 8 waves: 12/13 two stage buffers, 14/15 three
     const int nb = variant >= 14 ? 3 : 2;
     if ((variant & 1) == 0)

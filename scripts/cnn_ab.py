@@ -73,6 +73,8 @@ def main():
         conv.set_persist("nopersist" not in opt_s.split("+"))
         # nostempool: stem BN apply + max pool kernels instead of the fused pass
         _bn.set_stem_pool_fused("nostempool" not in opt_s.split("+"))
+        # st1p: conv-epilogue BN statistics in one pass (the launch args bake the switch)
+        _e.load().conv_set_stats_one_pass("st1p" in opt_s.split("+"))
         model, opt, x, y = cnn_bench.build(args, dev, 1)
         for _ in range(a.warmup):
             cnn_bench.train_step(model, opt, x, y, torch.bfloat16)

@@ -371,11 +371,14 @@ def test_resnet_step_kernels_match_miopen(monkeypatch):
 def test_conv_fused_bn_statistics(shape):
     """The conv epilogue's BatchNorm partials give the same BN output, batch statistics and
     running statistics as the BN's own statistics pass (tail tiles included)."""
+    from arena_amd.ops import _ext
     from arena_amd.ops.batchnorm import BatchNormAct2d
     n, cin, h, w, cout, k, st = shape
     pad = k // 2
     x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=3)
-    for v in conv.variants_for(cout):
+    for v, one_pass in [(v, p) for v in conv.variants_for(cout) for p in (False, True)]:
+        # one_pass: sums and sums of squares in one exchange (ConvArgs::st1p)
+        _ext.load().conv_set_stats_one_pass(one_pass)
         y0 = conv.conv2d_fwd(x, wt, st, pad, v)
         y, stats = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True)
         assert torch.equal(y, y0)
@@ -393,6 +396,7 @@ def test_conv_fused_bn_statistics(shape):
         torch.testing.assert_close(bns[1].running_mean, bns[0].running_mean, rtol=1e-4, atol=1e-5)
         torch.testing.assert_close(bns[1].running_var, bns[0].running_var, rtol=1e-3, atol=1e-5)
         assert int(bns[1].num_batches_tracked) == 1
+    _ext.load().conv_set_stats_one_pass(False)
 
 
 @pytest.mark.gpu
