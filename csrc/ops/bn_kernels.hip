@@ -262,7 +262,7 @@ __global__ __launch_bounds__(kT) void bn_stats_kernel(const T* __restrict__ x, l
 // M2 = S2 - S1^2/N without cancellation. (The previous form, a serial fp64 Chan merge per thread,
 // was latency-bound: 13.5 us per layer on average, 43 us behind a 56x56 conv.)
 constexpr int kFinWaves = kT / 64;
-constexpr int kFinU = 8;        // partials per lane per load batch
+constexpr int kFinU = 16;       // partials per lane per load batch (one batch up to 4096 partials)
 int g_fin_max_p = 64;           // level-1 blocks per channel group (runtime-tunable; 1 = no tickets)
 
 int fin_blocks_per_group(int nblk) {
@@ -305,6 +305,18 @@ __device__ __forceinline__ bool fin_level2(double& a, double& b, double& c, doub
   const double* base = lvl2 + (long long)g * P * 3 * 64;
   double sa = 0.0, sb = 0.0, sc = 0.0;
   int q = 0;
+  // 16 published rows per batch (48 loads in flight per lane): the level-2 merge of P <= 64 rows
+  // is 4 dependent round trips instead of 16 (same summation order)
+  for (; q + 16 <= P; q += 16) {
+    double va[16], vb[16], vc[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const double* r = base + (long long)(q + u) * 3 * 64;
+      va[u] = r[lane]; vb[u] = r[64 + lane]; vc[u] = r[128 + lane];
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) { sa += va[u]; sb += vb[u]; sc += vc[u]; }
+  }
   for (; q + 4 <= P; q += 4) {
     double va[4], vb[4], vc[4];
 #pragma unroll
