@@ -610,9 +610,9 @@ def _wgrad_candidates(cin, cout, k):
 
 
 # what a forward whose statistics come as per-tile partials pays on top of its own time: the BN
-# layer's partial-merge finalize launch (bn_stats_finalize, 14 us per layer on average at batch 128,
-# profiles/r3_persist_steady_kernels.csv)
-_FIN_PENALTY_US = float(os.environ.get("ARENA_CONV_FIN_PENALTY_US", "14"))
+# layer's partial-merge finalize launch (bn_stats_finalize, ~11 us per layer at batch 128,
+# profiles/r3_finalize16_steady_kernels.csv)
+_FIN_PENALTY_US = float(os.environ.get("ARENA_CONV_FIN_PENALTY_US", "11"))
 
 
 def _best(t: dict, kind: str, n: int):
