@@ -867,7 +867,7 @@ Tensor bn_lvl2(int64_t nblk, int64_t C, const Tensor& like) {
 // zero_b (optional): fp64 tensor the apply pass zeroes (this layer's backward sums, bn_bwd acc_b).
 // stats_part/stats_rpb: BatchNorm partials of x from conv_fwd(with_stats=True) (training only).
 // stats_fin (training): the fp64 [2][C] accumulators conv_fwd(..., stats_final=True) filled: no
-// statistics pass, a one-thread-per-channel finalize instead of the partial merge.
+// statistics pass and no finalize (the apply pass derives its coefficients from the sums).
 std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT running_mean,
                            OptT running_var, bool training, double momentum, double eps,
                            bool relu, OptT num_batches, OptT stats_part, int64_t stats_rpb,

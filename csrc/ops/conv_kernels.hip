@@ -87,10 +87,10 @@ struct ConvArgs {
   int c16;
   // EPI 1, accumulated statistics (bn_acc != null, part unused): every tile adds its moment
   // sums (n*mean = sum y, M2 + n*mean^2 = sum y^2 over its rows) into fp64 accumulators
-  // bn_acc [2][Cout] with memory-side atomics, fire-and-forget. A one-block-per-256-channels
-  // finalize (bn_kernels.hip bn_acc_finalize) reads them back, zeroes them and writes the
-  // BatchNorm coefficients: cheaper than merging per-tile partials (3136 per channel for a
-  // 56x56 layer at batch 128) in a two-level reduction.
+  // bn_acc [2][Cout] with memory-side atomics, fire-and-forget (the persistent form: once per
+  // block). The consuming BN apply pass derives its coefficients from the sums (bn_kernels.hip
+  // apply_coefs) and the layer's backward zeroes them: no finalize launch, where per-tile
+  // partials (3136 per channel for a 56x56 layer at batch 128) need a two-level merge.
   double* bn_acc;
   // Split-K (ksplit > 1): the K steps of every output tile are divided over ksplit blocks. Each
   // writes its fp32 accumulators to kws [tile][slice][acc][thread] (16-byte stores, thread-
