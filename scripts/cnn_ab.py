@@ -9,7 +9,7 @@ every variant alike (cdna_hip_programming.md §5.4 rule 24). Variants are conv m
 ``:link`` (BN-backward partials in the dgrad epilogues), ``:torchstem`` (the stem's
 input/weight casts and weight transform as torch ops) and/or ``:nomask`` (the last BN writes
 dy * mask for the residual join instead of parking (dy, bits)) and/or ``:finP<n>`` (at most n
-level-1 blocks per channel group in the BN finalize kernels) and/or ``:accP<n>`` (conv-epilogue
+level-1 blocks per channel group in the BN finalize kernels) and/or ``:redG<b>x<r>`` (BN reduction grid) and/or ``:accP<n>`` (conv-epilogue
 BN statistics as fp64 sums up to n tile-channel pairs) and/or ``:finbwd0`` (BN backward sums
 from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv forms) and/or
 ``:nostempool`` (stem BN and max pool unfused), joined with ``+``.
@@ -63,6 +63,10 @@ def main():
         from arena_amd.ops import _ext as _e
         _e.load().bn_set_fin_max_blocks(finp[0] if finp else 64)
         _e.load().bn_set_nt(0 if "bnnt0" in opt_s.split("+") else 1)   # BN non-temporal loads
+        # redG<blocks>x<rounds>: BN reduction grid (at most <blocks> blocks, >= <rounds> row rounds
+        # per block); default 512x8
+        redg = [o[4:].split("x") for o in opt_s.split("+") if o.startswith("redG")]
+        _e.load().bn_set_reduce_geometry(*(map(int, redg[0]) if redg else (512, 8)))
         # accP<n>: conv-epilogue BN statistics as fp64 sums up to n (tile, channel) pairs
         accp = [int(o[4:]) for o in opt_s.split("+") if o.startswith("accP")]
         conv.set_acc_max_pairs(accp[0] if accp else conv_acc_default)
