@@ -56,7 +56,7 @@ def parse():
 def bench_resnet50(dev, steps: int, batch: int) -> dict:
     """ResNet-50 v1.5 training step (fwd + bwd + momentum-SGD on fp32 masters, bf16 MFMA convs,
     synthetic 224x224 ImageNet batch) as ONE hipGraph: 8 eager warmup steps (the conv kernels'
-    per-shape autotuning runs in the first), capture, one untimed replay, then ``steps`` timed
+    per-shape autotuning runs in the first), capture, five untimed replays, then ``steps`` timed
     replays bracketed by device synchronisation. Same code path as
     ``arena_amd.examples.cnn_bench``."""
     import torch
@@ -69,7 +69,8 @@ def bench_resnet50(dev, steps: int, batch: int) -> dict:
         cnn_bench.train_step(model, opt, x, y, amp)
     torch.cuda.synchronize()
     graph, g_loss = cnn_bench.capture_step(model, opt, x, y, amp)
-    graph.replay()
+    for _ in range(5):   # untimed replays, so the timed ones start from a steady state
+        graph.replay()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(steps):
