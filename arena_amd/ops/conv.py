@@ -598,13 +598,18 @@ def _miopen_bwd(dy, x, w, stride, pad, mask):
                                                [1, 1], False, [0, 0], 1, mask)
 
 
+# blocks per CU the weight-gradient split counts aim at (ARENA_WGRAD_BPC, for A/Bs)
+_WGRAD_BPC = tuple(float(b) for b in os.environ.get("ARENA_WGRAD_BPC", "1,2,4").split(","))
+
+
 def _wgrad_candidates(cin, cout, k):
     """(tile variant, split count) pairs: splits that give ~1, 2 or 4 blocks per CU."""
     out = []
     for v in wgrad_variants_for(cin, cout):
         bm, bn = WGRAD_TILES[v]
         tiles = (cout // bm) * (k[0] * k[1] * cin // bn)
-        for blocks in (_CUS, 2 * _CUS, 4 * _CUS):
+        for bpc in _WGRAD_BPC:
+            blocks = int(bpc * _CUS)
             out.append((v, max(1, -(-blocks // tiles))))
     return sorted(set(out))
 
