@@ -194,6 +194,17 @@ def test_persist_variants_keep_the_chip_filled():
     assert conv.persist_variants_for(128 * 56 * 56, 256, [0 + 16]) == []   # split-K: never
 
 
+def test_wgrad_candidates_aim_at_blocks_per_cu():
+    # 3x3 512 -> 512 (K = 4608): every candidate's grid (tiles x splits) reaches its target
+    cands = conv._wgrad_candidates(512, 512, (3, 3))
+    assert cands == sorted(set(cands)) and cands
+    for v, splits in cands:
+        bm, bn = conv.WGRAD_TILES[v]
+        tiles = (512 // bm) * (9 * 512 // bn)
+        assert any(tiles * splits >= b * conv._CUS and tiles * (splits - 1) < b * conv._CUS
+                   for b in conv._WGRAD_BPC)
+
+
 def test_split_variants_for_only_underfilled_grids():
     # 56x56 at batch 128: thousands of tiles, no split; 7x7 x 512 with K = 4608: splits offered
     assert conv.split_variants_for(128 * 56 * 56, 64, 576) == []
