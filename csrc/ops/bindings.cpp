@@ -89,6 +89,7 @@ long long arena_bn_lvl2_doubles(long long, int);
 void arena_bn_set_reduce_geometry(long long, long long);
 void arena_bn_set_fin_max_blocks(int);
 void arena_bn_set_nt(int);
+void arena_bn_set_pool_quad_mult(int);
 // csrc/ops/pool_kernels.hip
 hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, int, int, int, int,
                              hipStream_t);
@@ -1775,6 +1776,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_set_fin_max_blocks", [](int64_t p) { arena_bn_set_fin_max_blocks((int)p); });
   m.def("bn_set_nt", [](int64_t on) { arena_bn_set_nt((int)on); });
+  m.def("bn_set_pool_quad_mult", [](int64_t m) { arena_bn_set_pool_quad_mult((int)m); });
   m.def("bn_set_acc", [](bool on) { g_bn_acc = on; });
   m.def("bn_acc_scratch", [](bool on) { g_acc_scratch = on; });
   m.def("bn_pool_fwd", &bn_pool_fwd);

@@ -1183,6 +1183,9 @@ __global__ __launch_bounds__(kT) void bn_pool_bwd_dx_q_kernel(const T* __restric
 // Both limits are runtime-tunable for sweeps (scripts/bn_bench.py); the workspace size follows.
 long long g_max_reduce_blocks = 512;
 int g_bn_nt = 1;           // non-temporal loads in the apply / dx passes (runtime switch for A/Bs)
+// stem-pool quad reduction grid, x the usual (A/B switch): 1-2x measured ~15 us/step faster than
+// 4x, 8x 56 us slower (profiles/r3_stem_quad_grid_ab.jsonl): fewer blocks, fewer same-address atomics
+long long g_pool_quad_mult = 2;
 long long g_min_rounds = 8;
 
 // acc mode pays one fp64 (a, b) atomic pair per block and channel at the end of the pass; above
@@ -1227,6 +1230,8 @@ extern "C" {
 void arena_bn_set_fin_max_blocks(int p) { g_fin_max_p = p < 1 ? 1 : (p > 64 ? 64 : p); }
 
 void arena_bn_set_nt(int on) { g_bn_nt = on ? 1 : 0; }
+
+void arena_bn_set_pool_quad_mult(int m) { g_pool_quad_mult = m < 1 ? 1 : (m > 16 ? 16 : m); }
 
 void arena_bn_set_acc_max_pairs(long long p) { g_acc_max_pairs = p < 0 ? 0 : p; }
 long long arena_bn_acc_max_pairs() { return g_acc_max_pairs; }
@@ -1469,7 +1474,7 @@ hipError_t arena_bn_pool_bwd(int dtype, const void* dy, const uint8_t* pos, cons
   ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);
   if (k == 3 && s == 2 && p == 1) {   // the ResNet stem pool: 2x2 input quads per gather
     const long long NQ = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);
-    g_max_reduce_blocks = saved_max * 4;
+    g_max_reduce_blocks = saved_max * g_pool_quad_mult;
     long long qrpb;
     const long long qnb = reduce_blocks(NQ, C, &qrpb);
     g_max_reduce_blocks = saved_max;

@@ -67,6 +67,9 @@ def main():
         # per block); default 512x8
         redg = [o[4:].split("x") for o in opt_s.split("+") if o.startswith("redG")]
         _e.load().bn_set_reduce_geometry(*(map(int, redg[0]) if redg else (512, 8)))
+        # pqm<n>: stem-pool quad reduction grid at n x the usual reduction grid (default 2)
+        pqm = [int(o[3:]) for o in opt_s.split("+") if o.startswith("pqm")]
+        _e.load().bn_set_pool_quad_mult(pqm[0] if pqm else 2)
         # accP<n>: conv-epilogue BN statistics as fp64 sums up to n (tile, channel) pairs
         accp = [int(o[4:]) for o in opt_s.split("+") if o.startswith("accP")]
         conv.set_acc_max_pairs(accp[0] if accp else conv_acc_default)
