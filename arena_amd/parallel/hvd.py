@@ -36,6 +36,17 @@ _STATE = {"pg": None, "local_rank": 0, "local_size": 1, "xgmi": None}
 _XGMI_STAGING = 16 << 20
 
 
+def _new_comm(staging_elems: int):
+    """A fresh xGMI communicator (collective), or None when the ranks cannot map each other."""
+    from . import xgmi
+    if not xgmi.usable():
+        return None
+    try:
+        return xgmi.XgmiComm(staging_elems=staging_elems)
+    except xgmi.XgmiUnavailable:
+        return None
+
+
 def _xgmi_comm(t: Optional[torch.Tensor] = None):
     """The job's xGMI communicator for broadcast/allgather (collective on first use), or None to
     use RCCL/gloo: CPU tensors, ``ARENA_XGMI=0``, or ranks that cannot map each other's GPUs."""
@@ -43,13 +54,7 @@ def _xgmi_comm(t: Optional[torch.Tensor] = None):
         return None
     c = _STATE["xgmi"]
     if c is None:
-        from . import xgmi
-        c = False
-        if xgmi.usable():
-            try:
-                c = xgmi.XgmiComm(staging_elems=_XGMI_STAGING)
-            except xgmi.XgmiUnavailable:
-                c = False
+        c = _new_comm(_XGMI_STAGING) or False
         _STATE["xgmi"] = c
     return c or None
 
@@ -155,7 +160,12 @@ def broadcast_(tensor: torch.Tensor, root_rank: int = 0) -> torch.Tensor:
 
 def broadcast_parameters(params, root_rank: int = 0) -> None:
     """Broadcast a state_dict / named_parameters / list of tensors from root (in place), packed
-    into one flat buffer per dtype so it is a handful of collectives, not one per tensor."""
+    into one flat buffer per dtype so it is a handful of collectives, not one per tensor.
+
+    Runs before training, when no job communicator exists yet: the xGMI path then uses a
+    temporary communicator whose staging buffer is sized to the largest flat buffer (capped at
+    the job communicator's 64 MB) and released right after, instead of keeping a 64 MB
+    registered buffer alive next to the optimizer's own communicator for the whole job."""
     if size() == 1:
         return
     if isinstance(params, dict):
@@ -166,25 +176,55 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
     for t in tensors:
         if torch.is_tensor(t):
             by_dtype.setdefault((t.dtype, t.device), []).append(t)
-    for (dt, dev), ts in by_dtype.items():
-        flat = torch.cat([t.detach().reshape(-1) for t in ts])
-        broadcast_(flat, root_rank)      # xGMI direct pull / scatter + all-gather, or RCCL
-        off = 0
-        with torch.no_grad():
-            for t in ts:
-                n = t.numel()
-                t.copy_(flat[off:off + n].view_as(t))
-                off += n
+    flats = {k: torch.cat([t.detach().reshape(-1) for t in ts]) for k, ts in by_dtype.items()}
+    comm, temp = _STATE["xgmi"] or None, False
+    if _STATE["xgmi"] is None and any(dev.type == "cuda" for _, dev in flats):
+        words = max(((f.numel() * f.element_size() + 15) // 16 * 4) for (_, dev), f in
+                    flats.items() if dev.type == "cuda")
+        comm, temp = _new_comm(min(words, _XGMI_STAGING)), True
+    try:
+        for (dt, dev), ts in by_dtype.items():
+            flat = flats[(dt, dev)]
+            if comm is not None and flat.is_cuda:
+                comm.broadcast_(flat, root_rank)   # xGMI direct pull / scatter + all-gather
+            else:
+                dist.broadcast(flat, root_rank)
+            off = 0
+            with torch.no_grad():
+                for t in ts:
+                    n = t.numel()
+                    t.copy_(flat[off:off + n].view_as(t))
+                    off += n
+    finally:
+        if temp and comm is not None:
+            comm.close()
 
 
-def broadcast_optimizer_state(optimizer: torch.optim.Optimizer, root_rank: int = 0) -> None:
-    state = []
+def _optimizer_state_tensors(optimizer) -> List[torch.Tensor]:
+    subs = getattr(optimizer, "opts", None)          # OptimizerGroup: its members, in order
+    if subs is not None:
+        return [t for o in subs for t in _optimizer_state_tensors(o)]
+    inner = getattr(optimizer, "opt", None)          # DistributedOptimizer wraps one
+    if inner is not None and not hasattr(optimizer, "param_groups"):
+        return _optimizer_state_tensors(inner)
+    state = getattr(optimizer, "state", None)
+    if not state:        # nothing to send (e.g. ShardedMasterSGD: masters derive from weights)
+        return []
+    out = []
     for group in optimizer.param_groups:
         for p in group["params"]:
-            for v in optimizer.state.get(p, {}).values():
+            for v in state.get(p, {}).values():
                 if torch.is_tensor(v):
-                    state.append(v)
-    broadcast_parameters(state, root_rank)
+                    out.append(v)
+    return out
+
+
+def broadcast_optimizer_state(optimizer, root_rank: int = 0) -> None:
+    """Broadcast the root's optimizer state tensors (momentum buffers, Adam moments) in place.
+    Recurses into ``OptimizerGroup`` members; optimizers without per-parameter state are
+    skipped. Every rank must hold the same state structure (call after a first step or on
+    freshly built optimizers)."""
+    broadcast_parameters(_optimizer_state_tensors(optimizer), root_rank)
 
 
 def _raw(t: torch.Tensor) -> Optional[torch.Tensor]:

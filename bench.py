@@ -13,8 +13,9 @@ gradient all-reduce when N>1, Adam update, device-side data gather + epoch reshu
 
 The MNIST steps run as replays of one hipGraph whose length divides the warmup, the timed step
 count and the epoch; ``config.exec`` reports how many timed steps were replayed vs run eagerly.
-On one GPU the same line also carries ``resnet50_images_per_s`` / ``resnet50_ms_per_step``
-(ResNet-50 bs128 bf16, whole training step in one hipGraph; ``--resnet 0`` skips it).
+The same line also carries ``resnet50_images_per_s`` (all ranks) / ``resnet50_ms_per_step``
+(ResNet-50 bs128 per GPU, bf16, whole training step in one hipGraph, data parallel over the
+sharded xGMI optimizer at N>1; ``--resnet 0`` skips it).
 
 Rank 0 prints ONE JSON line.
 """
@@ -46,46 +47,90 @@ def parse():
                          "(and the xGMI barrier flags) and abort on divergence; adds a host sync "
                          "per check. The replicas are always verified once after timing.")
     ap.add_argument("--resnet", type=int, default=1,
-                    help="1: also time ResNet-50 training (bs128/GPU, bf16, hipGraph) and report "
-                         "it as extra resnet50_* keys of the same JSON line (single GPU only)")
+                    help="1: also time ResNet-50 training (bs128/GPU, bf16, hipGraph; data "
+                         "parallel over all ranks at N>1) and report it as extra resnet50_* keys "
+                         "of the same JSON line")
     ap.add_argument("--resnet-steps", type=int, default=20)
     ap.add_argument("--resnet-batch", type=int, default=128)
+    ap.add_argument("--resnet-verify-every", type=int, default=10,
+                    help="N>1: replica bit-identity check every K timed ResNet steps (untimed)")
     return ap.parse_args()
 
 
-def bench_resnet50(dev, steps: int, batch: int) -> dict:
+def bench_resnet50(dev, steps: int, batch: int, world: int = 1, verify_every: int = 10) -> dict:
     """ResNet-50 v1.5 training step (fwd + bwd + momentum-SGD on fp32 masters, bf16 MFMA convs,
-    synthetic 224x224 ImageNet batch) as ONE hipGraph: 8 eager warmup steps (the conv kernels'
-    per-shape autotuning runs in the first), capture, five untimed replays, then ``steps`` timed
-    replays bracketed by device synchronisation. Same code path as
-    ``arena_amd.examples.cnn_bench``."""
+    synthetic 224x224 ImageNet batch of ``batch`` per GPU) as ONE hipGraph: 8 eager warmup steps
+    (the conv kernels' per-shape autotuning runs in the first), capture, five untimed replays,
+    then ``steps`` timed replays bracketed by barrier + device synchronisation, max over ranks.
+    Same code path as ``arena_amd.examples.cnn_bench``.
+
+    Data parallel (world > 1, one process per GPU): on one node the optimizer is
+    ``ShardedMasterSGD`` -- gradient buckets reduce-scattered, applied and all-gathered by one
+    xGMI kernel each, on a comm stream overlapping backward, captured in the same graph; where
+    the ranks cannot map each other's GPUs, fp32 weights + ``hvd.DistributedOptimizer`` over
+    RCCL. Every ``verify_every`` timed steps (and once after) all replicas must hold
+    bit-identical parameters (``ReplicaCheck``) or the run fails; the checks run outside the
+    timed segments."""
     import torch
+    import torch.distributed as dist
     from arena_amd.examples import cnn_bench
+    from arena_amd.parallel import hvd
     args = cnn_bench.parse(["--model", "resnet50", "--batch_size", str(batch), "--dtype", "bf16"])
     torch.backends.cudnn.benchmark = True
-    model, opt, x, y = cnn_bench.build(args, dev, 1)
+    if world > 1:
+        hvd.init()
+    model, opt, x, y = cnn_bench.build(args, dev, world)
     amp = torch.bfloat16
     for _ in range(8):
         cnn_bench.train_step(model, opt, x, y, amp)
     torch.cuda.synchronize()
     graph, g_loss = cnn_bench.capture_step(model, opt, x, y, amp)
+    if world > 1:
+        dist.barrier()
     for _ in range(5):   # untimed replays, so the timed ones start from a steady state
         graph.replay()
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        graph.replay()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    check = None
+    if world > 1:
+        from arena_amd.parallel.verify import ReplicaCheck
+        check = ReplicaCheck(verify_every, lambda: list(model.parameters()),
+                             comms=cnn_bench.comms_of(opt))
+    dt, done = 0.0, 0
+    seg = verify_every if (world > 1 and verify_every > 0) else steps
+    while done < steps:
+        k = min(seg, steps - done)
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            graph.replay()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        dt += time.perf_counter() - t0
+        done += k
+        if check is not None:
+            check.maybe(done)
+    if world > 1:
+        e = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        dt = float(e.item())
+        check.verify(steps)
     loss = float(g_loss)
     if not loss == loss:
         raise RuntimeError("ResNet-50 bench: non-finite loss")
-    return {"resnet50_images_per_s": round(steps * batch / dt, 1),
-            "resnet50_ms_per_step": round(dt / steps * 1e3, 3),
-            "resnet50_config": {"batch_per_gpu": batch, "image": 224, "dtype": "bf16",
-                                "optimizer": "momentum-sgd fp32 masters", "timed_steps": steps,
-                                "exec": f"hipgraph[whole step] {steps}/{steps} replays",
-                                "final_loss": round(loss, 4)}}
+    out = {"resnet50_images_per_s": round(steps * batch * world / dt, 1),
+           "resnet50_ms_per_step": round(dt / steps * 1e3, 3),
+           "resnet50_config": {"batch_per_gpu": batch, "global_batch": batch * world,
+                               "image": 224, "dtype": "bf16", "parallelism": f"dp{world}",
+                               "optimizer": "momentum-sgd fp32 masters", "timed_steps": steps,
+                               "comm": cnn_bench.comm_name(opt) if world > 1 else "none",
+                               "exec": f"hipgraph[whole step] {steps}/{steps} replays",
+                               "final_loss": round(loss, 4)}}
+    if check is not None:
+        out["resnet50_config"]["replicas_verified"] = check.checks
+    return out
 
 
 def main():
@@ -183,11 +228,12 @@ def main():
         extra["test_loss"] = round(tl, 5)
         extra["test_acc"] = round(ta, 5)
 
-    if args.resnet and world == 1 and args.impl == "fused":
+    if args.resnet and args.impl == "fused":
         del tr
         torch.cuda.empty_cache()
         try:
-            extra.update(bench_resnet50(dev, args.resnet_steps, args.resnet_batch))
+            extra.update(bench_resnet50(dev, args.resnet_steps, args.resnet_batch, world,
+                                        args.resnet_verify_every))
         except Exception as e:   # the headline (already measured) is still reported
             print(f"[bench] ResNet-50 extra keys failed: {e!r}", file=sys.stderr)
             extra["resnet50_error"] = repr(e)[:300]

@@ -491,6 +491,59 @@ __global__ __launch_bounds__(kThreads) void xgmi_sgd_bf16_kernel(ArenaXgmiPeers 
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
+// The fp32 tail of the same optimizer (BatchNorm scales/shifts, biases: ~0.1 M values in a
+// ResNet-50): fp32 gradients staged at buf[off, off + n) of every rank are reduce-scattered (fixed
+// rank order), momentum SGD runs on the owned chunk of the fp32 weights -- which live in buf2 and
+// ARE the masters (no rounding on the way out) -- and the chunk is written to every rank's buf2.
+// `mom` is indexed relative to the bucket (mom[0] <-> element off). Element units are floats.
+template <int W>
+__global__ __launch_bounds__(kThreads) void xgmi_sgd_f32_kernel(ArenaXgmiPeers P,
+                                                                 float* __restrict__ mom,
+                                                                 long long off, long long n,
+                                                                 long long L, long long S,
+                                                                 SgdCoef c) {
+  const int b = blockIdx.x;
+  const uint32_t e = P.epoch[b] + 1;
+  const long long lo = (long long)b * S;
+  const long long hi = std::min(lo + S, L);
+  xbarrier<W>(P, 0, b, e);
+  const long long base = (long long)P.rank * L;
+  const float* wmine = P.buf2[P.rank];
+  constexpr int U = kU;
+  for (long long o0 = lo + threadIdx.x * 4; o0 < hi; o0 += (long long)kThreads * 4 * U) {
+    float4 v[U][W], w[U], m[U];
+    bool ok[U];
+    long long idx[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long o = o0 + (long long)u * kThreads * 4;
+      ok[u] = o < hi && base + o < n;
+      idx[u] = ok[u] ? base + o : 0;
+#pragma unroll
+      for (int q = 0; q < W; ++q) v[u][q] = ld4(P.buf[q] + off + idx[u]);
+      w[u] = ld4(wmine + off + idx[u]);
+      m[u] = ld4(mom + idx[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      float4 g = v[u][0];
+#pragma unroll
+      for (int q = 1; q < W; ++q) g = add4(g, v[u][q]);  // fixed order: identical on every rank
+      sgd1(c, g.x, w[u].x, m[u].x);
+      sgd1(c, g.y, w[u].y, m[u].y);
+      sgd1(c, g.z, w[u].z, m[u].z);
+      sgd1(c, g.w, w[u].w, m[u].w);
+      if (ok[u]) {
+        st4(mom + idx[u], m[u]);
+#pragma unroll
+        for (int q = 0; q < W; ++q) st4(P.buf2[q] + off + idx[u], w[u]);
+      }
+    }
+  }
+  xbarrier<W>(P, 1, b, e);
+  if (threadIdx.x == 0) P.epoch[b] = e;
+}
+
 // Floats of a chunk per block. Every block pays two cross-rank barriers (one L2 writeback + one
 // invalidate each), so blocks are made fat rather than numerous; tunable for sweeps.
 long long g_block_elems = 4096;
@@ -668,6 +721,33 @@ void arena_ccl_sgd_shard(long long off, long long n, int world, int r, long long
   long long L, S;
   int nb;
   sgd_geometry(n, world, &L, &S, &nb);
+  *lo = off + std::min(n, (long long)r * L);
+  *hi = off + std::min(n, (long long)(r + 1) * L);
+}
+
+// One fp32 bucket [off, off + n) (floats, multiples of 4) of the sharded SGD: fp32 grads staged in
+// every rank's buf, fp32 weights (= masters) in every rank's buf2, momentum local (bucket-relative).
+hipError_t arena_ccl_sgd_f32(const ArenaXgmiPeers* P, float* mom, long long off, long long n,
+                             float lr, float momentum, float wd, float scale, hipStream_t stream) {
+  const int W = P->world;
+  if (W < 2 || W > kMaxR || n <= 0 || off < 0 || n % 4 || off % 4 || P->buf2[0] == nullptr)
+    return hipErrorInvalidValue;
+  if (off + n > P->buf_elems || off + n > P->buf2_elems) return hipErrorInvalidValue;
+  long long L, S;
+  int nb;
+  geometry(n, W, &L, &S, &nb);
+  SgdCoef c{lr, momentum, wd, scale};
+  ARENA_CCL_DISPATCH(W, xgmi_sgd_f32_kernel, dim3(nb), dim3(kThreads), 0, stream, *P, mom, off, n,
+                     L, S, c);
+  return hipGetLastError();
+}
+
+// The [lo, hi) floats of fp32 bucket [off, off + n) whose weights/momentum rank r updates.
+void arena_ccl_sgd_f32_shard(long long off, long long n, int world, int r, long long* lo,
+                             long long* hi) {
+  long long L, S;
+  int nb;
+  geometry(n, world, &L, &S, &nb);
   *lo = off + std::min(n, (long long)r * L);
   *hi = off + std::min(n, (long long)(r + 1) * L);
 }

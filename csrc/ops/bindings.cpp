@@ -52,6 +52,9 @@ void arena_ccl_set_bcast_direct_max(long long);
 hipError_t arena_ccl_sgd_bf16(const ArenaXgmiPeers*, float*, float*, long long, long long, float,
                               float, float, float, hipStream_t);
 void arena_ccl_sgd_shard(long long, long long, int, int, long long*, long long*);
+hipError_t arena_ccl_sgd_f32(const ArenaXgmiPeers*, float*, long long, long long, float, float,
+                             float, float, hipStream_t);
+void arena_ccl_sgd_f32_shard(long long, long long, int, int, long long*, long long*);
 void arena_ccl_set_block_elems(long long);
 void arena_ccl_set_oneshot_max(long long);
 long long arena_ccl_get_oneshot_max();
@@ -1734,6 +1737,22 @@ class XgmiPeers {
               "xgmi_sgd_bf16");
   }
 
+  // The fp32 tail bucket [off, off + n) (floats) of the same optimizer; `mom` holds the bucket's
+  // momentum (bucket-relative, n floats).
+  void sgd_f32(Tensor mom, int64_t off, int64_t n, double lr, double momentum, double wd,
+               double scale) {
+    check_f32(mom, "mom");
+    TORCH_CHECK(p_.buf2[0] != nullptr, "sgd_f32 needs the weight buffers (buf2)");
+    TORCH_CHECK(off >= 0 && n > 0 && off % 4 == 0 && n % 4 == 0, "sgd_f32: off/n must be "
+                "multiples of 4");
+    TORCH_CHECK(mom.numel() >= n, "sgd_f32: mom too short");
+    TORCH_CHECK(off + n <= p_.buf_elems && off + n <= p_.buf2_elems,
+                "sgd_f32: bucket exceeds the registered buffers");
+    check_hip(arena_ccl_sgd_f32(&p_, mom.data_ptr<float>(), off, n, (float)lr, (float)momentum,
+                                (float)wd, (float)scale, cur_stream()),
+              "xgmi_sgd_f32");
+  }
+
   int64_t world() const { return p_.world; }
 
  private:
@@ -1810,6 +1829,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     arena_ccl_sgd_shard(off, n, (int)world, (int)rank, &lo, &hi);
     return std::vector<int64_t>{lo, hi};
   });
+  m.def("ccl_sgd_f32_shard", [](int64_t off, int64_t n, int64_t world, int64_t rank) {
+    long long lo = 0, hi = 0;
+    arena_ccl_sgd_f32_shard(off, n, (int)world, (int)rank, &lo, &hi);
+    return std::vector<int64_t>{lo, hi};
+  });
   py::class_<XgmiPeers>(m, "XgmiPeers")
       .def(py::init<std::vector<int64_t>, std::vector<int64_t>, std::vector<int64_t>, Tensor,
                     Tensor, int64_t, int64_t, int64_t, double>())
@@ -1818,6 +1842,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("broadcast", &XgmiPeers::broadcast)
       .def("allgather", &XgmiPeers::allgather)
       .def("sgd_bf16", &XgmiPeers::sgd_bf16)
+      .def("sgd_f32", &XgmiPeers::sgd_f32)
       .def_property_readonly("world", &XgmiPeers::world);
 #ifdef ARENA_TIMELINE
   m.def("timeline_read", [](bool clear) {

@@ -5,8 +5,9 @@ setup (RCCL refuses two ranks on one device). Default: bf16 weights with the sha
 
 What it checks:
 
-* large fusion buckets (64 MB) through the xGMI allreduce staging buffer, issued on the comm
-  stream while backward is still running;
+* gradient buckets (12 MB default: 5 buckets for ResNet-50's bf16 weights + an fp32 BN/bias
+  tail bucket) through the registered xGMI staging buffer, issued on the comm stream while
+  backward is still running;
 * fused BN kernels under bf16 autocast in every rank;
 * that all replicas stay bit-identical after the steps (same averaged gradient everywhere).
 
@@ -46,7 +47,8 @@ def rank_main(rank, world, port, a, q):
                                  weight_decay=4e-5, bucket_mb=a.bucket_mb, comm="xgmi",
                                  data_format="NHWC", dtype="bf16", master_weights=a.master_weights)
     model, opt, x, y = cnn_bench.build(args, torch.device("cuda", 0), world)
-    assert opt.comm.startswith("xgmi"), opt.comm
+    name = cnn_bench.comm_name(opt)
+    assert name.startswith("xgmi"), name
     for i in range(a.warmup):
         cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
         torch.cuda.synchronize()
@@ -68,14 +70,12 @@ def rank_main(rank, world, port, a, q):
             loss = cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    comms = list(getattr(opt, "comms", [])) or [opt.xgmi]
-    for c in comms:
+    for c in cnn_bench.comms_of(opt):
         if c is not None:
             c.check()
     flat = torch.cat([p.detach().double().reshape(-1) for p in model.parameters()])
     digest = float(flat.sum().item()), float(flat.abs().sum().item())
-    nb = len(opt.opts[0].buckets) if hasattr(opt, "opts") else len(opt.buckets)
-    q.put((rank, dt, float(loss), digest, nb, opt.comm))
+    q.put((rank, dt, float(loss), digest, len(opt.buckets), name))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -86,7 +86,7 @@ def main():
     ap.add_argument("--model", default="resnet50")
     ap.add_argument("--batch_size", type=int, default=32)
     ap.add_argument("--image_size", type=int, default=224)
-    ap.add_argument("--bucket_mb", type=float, default=64.0)
+    ap.add_argument("--bucket_mb", type=float, default=12.0)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step as a hipGraph")
