@@ -162,6 +162,8 @@ def cmd_submit_mpi(ctx, ns) -> int:
     a.ssh_port = ns.sshPort
     a.rdzv_port = ns.rdzvPort
     a.shm_size = ns.shmSize
+    a.ranks_per_pod = ns.ranksPerPod
+    a.jupyter = ns.jupyter
     _fill_sync_tb(a, ns)
     return _submit(ctx, a, _command_args(ns))
 
@@ -388,6 +390,13 @@ def build_parser() -> argparse.ArgumentParser:
     mpi.add_argument("--rdzvPort", type=int, default=29500,
                      help="TCPStore rendezvous port served by rank 0")
     mpi.add_argument("--shmSize", default="2Gi", help="size of the /dev/shm tmpfs per rank")
+    mpi.add_argument("--ranksPerPod", type=int, default=-1,
+                     help="data-parallel ranks per pod (default: one per GPU, as hvd-distribute.sh "
+                          "<hosts> <gpus>; 1 for CPU pods). WORLD_SIZE = workers x ranksPerPod")
+    mpi.add_argument("--jupyter", action="store_true",
+                     help="run the launcher pod as a Jupyter notebook server (port 8888, "
+                          "<job>-tf-horovod-jupyter Service) instead of the command; the worker "
+                          "pods idle until ranks are started from the notebook")
     mpi.set_defaults(func=cmd_submit_mpi)
 
     sj = ssub.add_parser("standalonejob", aliases=["sj"], help="Submit a standalone job.")

@@ -183,17 +183,43 @@ def render_training(release: str, ns: str, values: dict) -> List[dict]:
     return out + _tensorboard(release, ns, values, "training")
 
 
+def task_ports(values: dict) -> Dict[str, List[int]]:
+    """Port of every PS/worker task. Under hostNetwork (the default) every task binds a port on
+    its NODE, so tasks that may share a node must not share a port: worker i gets
+    ``workerPort + i`` and the PS tasks take the next free ports from ``psPort`` upwards, skipping
+    the workers' range. With the reference's single port per type (submit_tfjob.go:64-65,
+    charts/tfjob/templates/tfjob.yaml:25-340) at most one worker and one PS fit on a node, so
+    `--workers 8 --gpus 1` needed 8 nodes instead of one 8-GPU MI355X node. With pod networking
+    every pod has its own IP and the base ports are kept."""
+    wp, pp = int(values.get("workerPort", 22222)), int(values.get("psPort", 22223))
+    nw, nps = int(values.get("workers", 1)), int(values.get("ps", 0))
+    if not bool(values.get("useHostNetwork", True)):
+        return {"worker": [wp] * nw, "ps": [pp] * nps}
+    workers = [wp + i for i in range(nw)]
+    used, ps, port = set(workers), [], pp
+    for _ in range(nps):
+        while port in used:
+            port += 1
+        ps.append(port)
+        used.add(port)
+    return {"worker": workers, "ps": ps}
+
+
+def task_port(values: dict, rtype: str, index: int) -> int:
+    return task_ports(values)[rtype][index]
+
+
 def tf_cluster_spec(release: str, ns: str, values: dict) -> Dict[str, List[str]]:
     """The TF_CONFIG ``cluster`` of a PS/worker job: one stable DNS name per task, the headless
     Service ``<release>-tfjob-<type>-<i>`` rendered next to each task's Job (what tf-operator
-    generates; trainer_tensorflow.go:357-418 relies on the same per-replica identity)."""
+    generates; trainer_tensorflow.go:357-418 relies on the same per-replica identity), each on
+    its own port (:func:`task_port`)."""
     name = f"{release}-tfjob"
     out: Dict[str, List[str]] = {}
-    for t, n, port in (("ps", int(values.get("ps", 0)), int(values.get("psPort", 22223))),
-                       ("worker", int(values.get("workers", 1)),
-                        int(values.get("workerPort", 22222)))):
-        if n > 0:
-            out[t] = [f"{name}-{t}-{i}.{ns}.svc:{port}" for i in range(n)]
+    ports = task_ports(values)
+    for t in ("ps", "worker"):
+        if ports[t]:
+            out[t] = [f"{name}-{t}-{i}.{ns}.svc:{port}" for i, port in enumerate(ports[t])]
     return out
 
 
@@ -205,7 +231,7 @@ def _tf_task_pod(release: str, ns: str, values: dict, rtype: str, index: int,
               "tf-replica-type": rtype, "tf-replica-index": str(index), "tf_job_name": name}
     tf_config = json.dumps({"cluster": cluster, "task": {"type": rtype, "index": index},
                             "environment": "cloud"}, sort_keys=True)
-    port = int(values.get("psPort" if is_ps else "workerPort", 22223 if is_ps else 22222))
+    port = task_port(values, rtype, index)
     lv, lm = ([], []) if is_ps else _log_mount(values)
     ctr = _container("tensorflow", values,
                      values.get("psImage" if is_ps else "workerImage", ""),
@@ -339,31 +365,72 @@ def _jobmon(release: str, ns: str, values: dict, app: str, env: Dict[str, str]) 
                                                "env": _env_list(full_env)}]}}}}
 
 
+POD_LAUNCHER = "exec python3 -m arena_amd.runtime.podlaunch"
+
+
+def jupyter_command(values: dict) -> List[str]:
+    """The launcher pod as a notebook server (charts/tf-horovod/templates/job.yaml:148-153): the
+    TF images' ``/run_jupyter.sh`` when present (it reads ``PASSWORD``: pass ``-e PASSWORD=..``),
+    plain ``jupyter notebook`` otherwise."""
+    wd = values.get("workingDir", "/root")
+    return ["sh", "-c",
+            f"if [ -x /run_jupyter.sh ]; then exec /run_jupyter.sh --allow-root {wd}; else exec "
+            f"jupyter notebook --ip=0.0.0.0 --port=8888 --no-browser --allow-root "
+            f"--notebook-dir={wd}; fi"]
+
+
 def render_tf_horovod(release: str, ns: str, values: dict) -> List[dict]:
     """Allreduce job (charts/tf-horovod/templates): launcher Job + worker StatefulSet + headless
-    Services + jobmon. Ranks rendezvous on a TCPStore served by the launcher (rank 0) at
-    `<fullname>-master:rdzvPort`; the StatefulSet ordinal i is rank i+1.
+    Services + jobmon. Ranks rendezvous on a TCPStore served by rank 0 at
+    `<fullname>-master:rdzvPort`.
+
+    Ranks per pod (``ranksPerPod``, default one per GPU): the reference's ``hvd-distribute.sh
+    <hosts> <gpus>`` runs hosts x GPUs ranks (charts/tf-horovod/README.md:66-69). With one rank
+    per pod the pod's shell exports ``RANK`` itself (pod index = 0 for the launcher, ordinal + 1
+    for StatefulSet pod ``<fullname>-<ordinal>``); with several, every pod's entry process is the
+    in-pod launcher (``arena_amd.runtime.podlaunch``), which starts ``ranksPerPod`` children with
+    ``RANK = pod_index * ranksPerPod + LOCAL_RANK``, ``LOCAL_WORLD_SIZE = ranksPerPod`` and
+    ``WORLD_SIZE = pods * ranksPerPod`` before any GPU call. A one-pod job with 8 GPUs is then 8
+    ranks that all see all 8 devices, so the xGMI collectives apply.
 
     The ordinal comes from the pod's own name through the downward API (``POD_NAME`` =
     ``metadata.name`` = ``<fullname>-<i>``), never from ``$HOSTNAME``: under ``hostNetwork`` (the
     default, as in the reference chart) the hostname is the NODE's name, identical for every
     worker on a node. The reference's hostfile used per-pod DNS names for the same reason
-    (charts/tf-horovod/templates/config.yaml:13-17)."""
+    (charts/tf-horovod/templates/config.yaml:13-17).
+
+    ``jupyter``: the launcher pod serves a notebook on 8888 behind a ``<fullname>-jupyter``
+    Service instead of running the command (charts/tf-horovod/templates/service.yaml:47-67); the
+    worker pods start their ranks, which wait at the rendezvous for rank 0 started from the
+    notebook."""
     fn = fullname(release, "tf-horovod")
     labels = {"app": "tf-horovod", "release": release}
-    world = int(values.get("workers", 0)) + 1
+    pods = int(values.get("workers", 0)) + 1
+    rpp = max(1, int(values.get("ranksPerPod", 1)))
     port = int(values.get("rdzvPort", 29500))
     vols, mounts = _volumes_and_mounts(values)
     lv, lm = _log_mount(values)
     shm = [{"name": "dshm", "emptyDir": {"medium": "Memory",
                                           "sizeLimit": values.get("shmSize", "2Gi")}}]
     shm_m = [{"name": "dshm", "mountPath": "/dev/shm"}]
-    rdzv = {"MASTER_ADDR": f"{fn}-master", "MASTER_PORT": str(port), "WORLD_SIZE": str(world),
+    rdzv = {"MASTER_ADDR": f"{fn}-master", "MASTER_PORT": str(port),
+            "WORLD_SIZE": str(pods * rpp),
             "HSA_ENABLE_IPC_MODE_LEGACY": "0", "NCCL_SOCKET_IFNAME": "^lo,docker"}
     gpus = int(values.get("gpuCount", 0))
     common_spec = _net_spec(values, hostIPC=True, volumes=vols + lv + shm)
-    master_cmd = ["sh", "-c", "export RANK=0; " + values.get("command", "")]
-    worker_cmd = ["sh", "-c", "export RANK=$(( ${POD_NAME##*-} + 1 )); " + values.get("command", "")]
+    if rpp == 1:
+        master_cmd = ["sh", "-c", "export RANK=0; " + values.get("command", "")]
+        worker_cmd = ["sh", "-c",
+                      "export RANK=$(( ${POD_NAME##*-} + 1 )); " + values.get("command", "")]
+    else:
+        rdzv.update({"ARENA_RANK_COMMAND": values.get("command", ""),
+                     "ARENA_RANKS_PER_POD": str(rpp), "ARENA_PODS": str(pods)})
+        master_cmd = ["sh", "-c", "export ARENA_POD_INDEX=0; " + POD_LAUNCHER]
+        worker_cmd = ["sh", "-c", POD_LAUNCHER]          # index from POD_NAME
+    master_ports = None
+    if values.get("jupyter"):
+        master_cmd = jupyter_command(values)
+        master_ports = [{"name": "jupyter", "containerPort": 8888}]
     out = [
         {"apiVersion": "v1", "kind": "Service",
          "metadata": {"name": fn, "namespace": ns, "labels": labels},
@@ -374,11 +441,17 @@ def render_tf_horovod(release: str, ns: str, values: dict) -> List[dict]:
          "spec": {"clusterIP": "None", "selector": {**labels, "role": "mpimaster"},
                   "ports": [{"port": port, "name": "rdzv"}]}},
     ]
-    if world > 1:
+    if values.get("jupyter"):
+        out.append({"apiVersion": "v1", "kind": "Service",
+                    "metadata": {"name": f"{fn}-jupyter", "namespace": ns, "labels": labels},
+                    "spec": {"type": values.get("jupyterServiceType", "NodePort"),
+                             "selector": {**labels, "role": "mpimaster"},
+                             "ports": [{"name": "jupyter", "port": 8888, "targetPort": 8888}]}})
+    if pods > 1:
         out.append({
             "apiVersion": "apps/v1", "kind": "StatefulSet",
             "metadata": {"name": fn, "namespace": ns, "labels": labels},
-            "spec": {"replicas": world - 1, "podManagementPolicy": "Parallel",
+            "spec": {"replicas": pods - 1, "podManagementPolicy": "Parallel",
                      "serviceName": fn, "selector": {"matchLabels": {**labels, "role": "mpiworker"}},
                      "template": {"metadata": {"labels": {**labels, "role": "mpiworker"}},
                                   "spec": {**copy.deepcopy(common_spec),
@@ -400,7 +473,7 @@ def render_tf_horovod(release: str, ns: str, values: dict) -> List[dict]:
                                            "mpimaster", values, values.get("image", ""), gpus,
                                            values.get("cpu", ""), values.get("memory", ""),
                                            extra_env=rdzv, mounts=mounts + lm + shm_m,
-                                           command=master_cmd)]}}}})
+                                           command=master_cmd, ports=master_ports)]}}}})
     out.append(_jobmon(release, ns, values, "tf-horovod",
                        {"NAMESPACE": ns, "JOBNAME": f"{fn}-job", "STATEFULSETNAME": fn}))
     return out + _tensorboard(release, ns, values, "tf-horovod",

@@ -328,6 +328,7 @@ class LocalBackend(Backend):
                                                if os.environ.get("PYTHONPATH") else ""),
                     "HSA_ENABLE_IPC_MODE_LEGACY": "0", **data_env}
         launcher = ""
+        rpp = max(1, int(values.get("ranksPerPod", 1)))
         if kind == "allreduce":
             ranks = [p for p in pods if p.meta.labels.get("role") in ("mpimaster", "mpiworker")]
             union = sorted({i for p in ranks for i in gpus.get(p.name, [])})
@@ -362,18 +363,31 @@ class LocalBackend(Backend):
                 argv = self._argv(c.command, values, jd, p.name)
             own = gpus.get(p.name, [])
             if kind == "allreduce" and role in ("mpimaster", "mpiworker"):
-                # the chart's `export RANK=...` prefix, resolved here as well: a --profile-gpu
-                # rank runs without the shell (rocprofv3 execs the program directly)
-                env["RANK"] = "0" if role == "mpimaster" else str(int(p.name.rsplit("-", 1)[1]) + 1)
+                pidx = 0 if role == "mpimaster" else int(p.name.rsplit("-", 1)[1]) + 1
                 env["MASTER_ADDR"] = "127.0.0.1"
                 env["MASTER_PORT"] = str(ports["rdzv"])
-                env["LOCAL_WORLD_SIZE"] = str(len(ranks))   # every rank is on this node
+                # every rank of every pod runs on this node
+                env["LOCAL_WORLD_SIZE"] = str(len(ranks) * rpp)
                 if union:
                     env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, union))
-                    env["LOCAL_RANK"] = str(union.index(own[0])) if own else "0"
-                    env["ARENA_LOCAL_GPUS"] = ",".join(str(union.index(i)) for i in own)
+                    env["ARENA_RANK_GPUS"] = ",".join(str(union.index(i)) for i in own)
+                if rpp == 1:
+                    # the chart's `export RANK=...` prefix, resolved here as well: a
+                    # --profile-gpu rank runs without the shell (rocprofv3 execs the program)
+                    env["RANK"] = str(pidx)
+                    env["LOCAL_RANK"] = str(union.index(own[0])) if (union and own) else "0"
                 else:
-                    env["LOCAL_RANK"] = "0"
+                    # in-pod launcher (arena_amd.runtime.podlaunch) with node-wide local ranks:
+                    # all ranks of the job see the job's whole GPU set and can map each other
+                    env["ARENA_POD_INDEX"] = str(pidx)
+                    env["ARENA_NODE_RANKS"] = str(len(ranks) * rpp)
+                    env["ARENA_RANK_LOCAL_IDS"] = ",".join(
+                        str(union.index(i)) for i in own[:rpp]) if (union and own) else \
+                        ",".join(str(pidx * rpp + lr) for lr in range(rpp))
+                    if not (role == "mpimaster" and values.get("jupyter")):
+                        argv = [sys.executable, "-m", "arena_amd.runtime.podlaunch"]
+                        if values.get("profileGPU"):
+                            env["ARENA_RANK_PROFILE_DIR"] = os.path.join(jd, "traces", p.name)
             elif own:
                 env["HIP_VISIBLE_DEVICES"] = ",".join(map(str, own))
                 env["LOCAL_RANK"] = "0"

@@ -222,9 +222,16 @@ class MPIJobArgs(SubmitArgs):
     cpu: str = ""
     memory: str = ""
     shm_size: str = "2Gi"
+    ranks_per_pod: int = -1     # -1: one rank per GPU (hvd-distribute.sh <hosts> <gpus>)
+    jupyter: bool = False       # launcher pod runs Jupyter (charts/tf-horovod/values.yaml:23-27)
     tensorboard: TensorboardArgs = field(default_factory=TensorboardArgs)
     sync: SyncCodeArgs = field(default_factory=SyncCodeArgs)
     chart: str = MPI_CHART
+
+    def effective_ranks_per_pod(self) -> int:
+        if self.ranks_per_pod > 0:
+            return self.ranks_per_pod
+        return max(1, self.gpu_count)
 
     def prepare(self, args: List[str]) -> None:
         self.command = " ".join(args)
@@ -240,12 +247,20 @@ class MPIJobArgs(SubmitArgs):
             raise ValidationError("--image must be set ")
         if self.workers < 1:
             raise ValidationError("--workers must be greater than 0")
+        if self.ranks_per_pod == 0 or self.ranks_per_pod < -1:
+            raise ValidationError("--ranksPerPod must be >= 1 (or -1: one per GPU)")
+        if self.gpu_count > 0 and self.effective_ranks_per_pod() > self.gpu_count:
+            raise ValidationError(f"--ranksPerPod {self.ranks_per_pod} exceeds --gpus "
+                                  f"{self.gpu_count}: every rank needs its own GPU")
 
     def values(self) -> dict:
         v = super().values()
         v["workers"] = self.workers - 1   # master is a rank too
         v.update({"sshPort": self.ssh_port, "rdzvPort": self.rdzv_port, "cpu": self.cpu,
-                  "memory": self.memory, "shmSize": self.shm_size})
+                  "memory": self.memory, "shmSize": self.shm_size,
+                  "ranksPerPod": self.effective_ranks_per_pod()})
+        if self.jupyter:
+            v["jupyter"] = True
         v.update(self.tensorboard.values())
         v.update(self.sync.values())
         return v

@@ -285,7 +285,10 @@ def main(argv):
         o = s["pods"][key(pos[1], pos[2])]
         pod = kj.pod_from(o)
         c = pod.containers[0]
-        env = {"PATH": os.environ.get("PATH", "/usr/bin:/bin"), **c.env, "HOSTNAME": pod.hostname}
+        # the image ships arena_amd (the in-pod rank launcher of several-ranks-per-pod jobs)
+        env = {"PATH": os.environ.get("PATH", "/usr/bin:/bin"),
+               "PYTHONPATH": os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+               **c.env, "HOSTNAME": pod.hostname}
         r = subprocess.run(c.command, env=env, capture_output=True, text=True)
         sys.stdout.write(r.stdout)
         sys.stderr.write(r.stderr)

@@ -90,8 +90,9 @@ def test_tfjob_properties():
     by = {(d["kind"], d["metadata"]["name"]): d for d in docs}
     tasks = ["demo-tfjob-ps-0"] + [f"demo-tfjob-worker-{i}" for i in range(3)]
     assert not [d for d in docs if d["kind"] == "TFJob"]
-    want_cluster = {"ps": ["demo-tfjob-ps-0.team-a.svc:22223"],
-                    "worker": [f"demo-tfjob-worker-{i}.team-a.svc:22222" for i in range(3)]}
+    # hostNetwork: per-task ports (workers 22222.., the PS skips the workers' range)
+    want_cluster = {"ps": ["demo-tfjob-ps-0.team-a.svc:22225"],
+                    "worker": [f"demo-tfjob-worker-{i}.team-a.svc:{22222 + i}" for i in range(3)]}
     for t in tasks:
         job, svc = by[("Job", t)], by[("Service", t)]
         tpl = job["spec"]["template"]
@@ -106,7 +107,7 @@ def test_tfjob_properties():
         assert tfc == {"cluster": want_cluster, "task": {"type": rtype, "index": idx},
                        "environment": "cloud"}
         assert _env(c)["MX_CLUSTER_SPEC"] == _env(c)["TF_CONFIG"]
-        port = 22223 if rtype == "ps" else 22222
+        port = 22225 if rtype == "ps" else 22222 + idx
         assert [p["containerPort"] for p in c["ports"]] == [port]
         assert svc["spec"]["ports"][0]["port"] == port
         gpus = (c.get("resources") or {}).get("limits", {}).get("amd.com/gpu")
@@ -153,19 +154,34 @@ def test_mpijob_properties():
     for d in (job, ss):
         c = _containers(d)[0]
         env = {e["name"]: e.get("value") for e in c["env"]}
-        assert env["WORLD_SIZE"] == "3" and env["MASTER_PORT"] == "29500"
+        # 3 pods x 2 GPUs: one rank per GPU through the in-pod launcher
+        assert env["WORLD_SIZE"] == "6" and env["MASTER_PORT"] == "29500"
+        assert env["ARENA_RANKS_PER_POD"] == "2" and env["ARENA_PODS"] == "3"
+        assert env["ARENA_RANK_COMMAND"] == "python train.py"
         assert env["MASTER_ADDR"] == "demo-tf-horovod-master"
         vols = d["spec"]["template"]["spec"]["volumes"]
         shm = [v for v in vols if v.get("emptyDir", {}).get("medium") == "Memory"]
         assert shm and shm[0]["emptyDir"]["sizeLimit"] == "4Gi"
         assert d["spec"]["template"]["spec"].get("hostIPC") is True
-    assert "export RANK=0" in " ".join(_containers(job)[0]["command"])
-    # the worker rank comes from the pod name (downward API), not $HOSTNAME (= node under
+    assert "export ARENA_POD_INDEX=0" in " ".join(_containers(job)[0]["command"])
+    assert "arena_amd.runtime.podlaunch" in " ".join(_containers(job)[0]["command"])
+    # the worker pod index comes from the pod name (downward API), not $HOSTNAME (= node under
     # hostNetwork); tests/test_k8s_backend.py runs it on a fake node with several workers
     wc = _containers(ss)[0]
-    assert "POD_NAME##*-" in " ".join(wc["command"]) and "HOSTNAME" not in " ".join(wc["command"])
+    assert "arena_amd.runtime.podlaunch" in " ".join(wc["command"])
+    assert "HOSTNAME" not in " ".join(wc["command"])
     assert {"name": "POD_NAME", "valueFrom": {"fieldRef": {"fieldPath": "metadata.name"}}} \
         in wc["env"]
+    # one rank per pod keeps the launcher-free form (any image, no arena_amd inside)
+    a = S.MPIJobArgs()
+    a.name, a.image, a.gpu_count, a.workers, a.ranks_per_pod = "one", "img", 2, 3, 1
+    a.prepare(["python", "train.py"])
+    one = {(d["kind"], d["metadata"]["name"]): d
+           for d in charts.render(a.chart, "one", "default", a.values())}
+    assert "export RANK=0" in " ".join(_containers(one[("Job", "one-tf-horovod-job")])[0]["command"])
+    wc1 = _containers(one[("StatefulSet", "one-tf-horovod")])[0]
+    assert "POD_NAME##*-" in " ".join(wc1["command"])
+    assert {e["name"]: e.get("value") for e in wc1["env"]}["WORLD_SIZE"] == "3"
     for d in (job, ss):
         assert d["spec"]["template"]["spec"]["dnsPolicy"] == "ClusterFirstWithHostNet"
 
@@ -238,3 +254,62 @@ def test_jobmon_image_runs_the_rendered_command():
     r = subprocess.run([sys.executable, "-m", mod], cwd=root, env=env, capture_output=True,
                        text=True, timeout=60)
     assert r.returncode == 2 and "Failed to get namespace" in r.stderr
+
+
+def test_mpijob_ranks_per_pod_validation():
+    from arena_amd.jobs.spec import ValidationError
+    for rpp, gpus in ((3, 2), (0, 1), (-2, 1)):
+        a = S.MPIJobArgs()
+        a.name, a.image, a.gpu_count, a.ranks_per_pod = "x", "img", gpus, rpp
+        with pytest.raises(ValidationError):
+            a.prepare(["true"])
+    a = S.MPIJobArgs()
+    a.name, a.image, a.gpu_count, a.ranks_per_pod = "x", "img", 0, 4   # CPU ranks: allowed
+    a.prepare(["true"])
+    assert a.values()["ranksPerPod"] == 4
+
+
+def test_mpijob_jupyter_master():
+    """--jupyter: the launcher pod serves a notebook on 8888 behind <fullname>-jupyter
+    (charts/tf-horovod/templates/service.yaml:47-67, job.yaml:148-153)."""
+    a = S.MPIJobArgs()
+    a.name, a.image, a.gpu_count, a.workers, a.jupyter = "nb", "img", 1, 2, True
+    a.prepare(["python", "train.py"])
+    docs = {(d["kind"], d["metadata"]["name"]): d
+            for d in charts.render(a.chart, "nb", "default", a.values())}
+    svc = docs[("Service", "nb-tf-horovod-jupyter")]
+    assert svc["spec"]["type"] == "NodePort" and svc["spec"]["ports"][0]["port"] == 8888
+    assert svc["spec"]["selector"]["role"] == "mpimaster"
+    mc = _containers(docs[("Job", "nb-tf-horovod-job")])[0]
+    assert "jupyter notebook" in mc["command"][2] and "/run_jupyter.sh" in mc["command"][2]
+    assert mc["ports"] == [{"name": "jupyter", "containerPort": 8888}]
+    wc = _containers(docs[("StatefulSet", "nb-tf-horovod")])[0]
+    assert "train.py" in " ".join(wc["command"])         # workers still start their ranks
+
+
+def test_tfjob_eight_workers_fit_one_node():
+    """hostNetwork PS/worker job with 8 workers + 1 PS: every task on one 8-GPU node binds its
+    own port, and TF_CONFIG, the Services and the containerPorts agree."""
+    import json
+    a = S.TFJobArgs()
+    a.name, a.image, a.gpu_count, a.workers, a.ps_count = "big", "img", 1, 8, 1
+    a.prepare(["python", "dist.py"])
+    docs = charts.render(a.chart, "big", "default", a.values())
+    ports, cluster = {}, None
+    for d in docs:
+        if d["kind"] == "Job" and "tf-replica-type" in d["metadata"]["labels"]:
+            c = _containers(d)[0]
+            ports[d["metadata"]["name"]] = c["ports"][0]["containerPort"]
+            tfc = json.loads(_env(c)["TF_CONFIG"])
+            cluster = cluster or tfc["cluster"]
+            assert tfc["cluster"] == cluster
+    assert len(ports) == 9 and len(set(ports.values())) == 9        # no two tasks share a port
+    svc = {d["metadata"]["name"]: d["spec"]["ports"][0]["port"] for d in docs
+           if d["kind"] == "Service" and d["metadata"]["name"] in ports}
+    assert svc == ports
+    for t, addrs in cluster.items():
+        for i, addr in enumerate(addrs):
+            assert int(addr.rsplit(":", 1)[1]) == ports[f"big-tfjob-{t}-{i}"]
+    # pod networking: every pod has its own IP, the base ports are kept
+    v = dict(a.values(), useHostNetwork=False)
+    assert set(charts.task_ports(v)["worker"]) == {22222}

@@ -124,7 +124,8 @@ def test_mpi_job_chief_is_newest_job_pod_and_workers_listed(env):
     assert lines[-1].split()[4].startswith("hvd-tf-horovod-job-")  # chief listed last
     master_env = job_pods[0].containers[0].env
     assert master_env["MASTER_ADDR"] == "hvd-tf-horovod-master"
-    assert master_env["WORLD_SIZE"] == "3"
+    assert master_env["WORLD_SIZE"] == "6"        # 3 pods x 2 GPUs: one rank per GPU
+    assert master_env["ARENA_RANKS_PER_POD"] == "2"
     out = arena("top", "job")[1]
     assert out.splitlines()[1].split()[-2:] == ["6", "6"]
 

@@ -129,16 +129,17 @@ def test_tfjob_without_operator(kube, monkeypatch):
                st["pods"][f"default/{pod}"]["spec"]["containers"][0]["env"]}
         tfc = json.loads(env["TF_CONFIG"])
         assert tfc["task"] == {"type": t.split("-")[0], "index": int(t.split("-")[1])}
-        assert tfc["cluster"]["ps"] == ["dist-tfjob-ps-0.default.svc:22223"]
+        # hostNetwork: one port per task (workers 22222, 22223; the PS the next free one)
+        assert tfc["cluster"]["ps"] == ["dist-tfjob-ps-0.default.svc:22224"]
         assert tfc["cluster"]["worker"] == ["dist-tfjob-worker-0.default.svc:22222",
-                                            "dist-tfjob-worker-1.default.svc:22222"]
+                                            "dist-tfjob-worker-1.default.svc:22223"]
     assert rows(cli(kube, "list"))[0][:3] == ["dist", "PENDING", "TFJOB"]
     for pod in tasks.values():
         kube.fake("fake-phase", "default", pod, "Running", "mi355x-a")
     assert rows(cli(kube, "list"))[0][:2] == ["dist", "RUNNING"]
     # each task's headless Service resolves to its pod (endpoints controller)
     ep = kube.get_endpoints("default", "dist-tfjob-worker-1")
-    assert ep.addresses == ["10.1.0.1"] and ep.ports == [22222]
+    assert ep.addresses == ["10.1.0.1"] and ep.ports == [22223]
     got = cli(kube, "get", "dist")
     assert tasks["worker-0"] in got and "tensorboard will be available on" in got
     for t in ("worker-0", "worker-1"):
@@ -206,6 +207,40 @@ def test_allreduce_ranks_unique_under_host_network(kube):
         assert kv["HOST"] == "mi355x-a" and kv["WORLD"] == "4"
         seen.append(int(kv["RANK"]))
     assert sorted(seen) == [0, 1, 2, 3]
+
+
+def test_allreduce_several_ranks_per_pod(kube):
+    """`--workers 2 --gpus 4`: 2 pods x 4 ranks (hvd-distribute.sh <hosts> <gpus>). Each pod's
+    entry process is the in-pod launcher; run as the kubelet would (fake-exec), the 8 ranks are
+    0..7 exactly once, LOCAL_RANK 0..3 within each pod, LOCAL_WORLD_SIZE 4, WORLD_SIZE 8."""
+    cli(kube, "submit", "mpi", "--name", "rpp", "--image", "rocm/pytorch", "--gpus", "4",
+        "--workers", "2", "echo RANK=$RANK LOCAL=$LOCAL_RANK LWS=$LOCAL_WORLD_SIZE "
+        "WORLD=$WORLD_SIZE GROUP=$GROUP_RANK")
+    st = json.load(open(kube.state))
+    pods = [k.split("/")[1] for k, p in st["pods"].items() if k.startswith("default/")
+            and p["metadata"]["labels"].get("role") in ("mpimaster", "mpiworker")]
+    assert len(pods) == 2
+    for pod in pods:
+        ctr = st["pods"][f"default/{pod}"]["spec"]["containers"][0]
+        assert ctr["resources"]["limits"]["amd.com/gpu"] == 4
+    seen = []
+    for pod in pods:
+        kube.fake("fake-phase", "default", pod, "Running", "mi355x-a")
+        lines = kube.fake("fake-exec", "default", pod).strip().splitlines()
+        assert len(lines) == 4, lines
+        kvs = [dict(x.split("=", 1) for x in ln.split()) for ln in lines]
+        assert {kv["LWS"] for kv in kvs} == {"4"} and {kv["WORLD"] for kv in kvs} == {"8"}
+        assert sorted(int(kv["LOCAL"]) for kv in kvs) == [0, 1, 2, 3]
+        group = {kv["GROUP"] for kv in kvs}
+        assert len(group) == 1
+        for kv in kvs:
+            assert int(kv["RANK"]) == 4 * int(kv["GROUP"]) + int(kv["LOCAL"])
+        seen += [int(kv["RANK"]) for kv in kvs]
+    assert sorted(seen) == list(range(8))
+    # env `workers` keeps the reference's meaning (pods, submit.go:100-101)
+    ctr = st["pods"][f"default/{pods[0]}"]["spec"]["containers"][0]
+    env = {e["name"]: e.get("value") for e in ctr["env"]}
+    assert env["workers"] == "2" and env["gpus"] == "4"
 
 
 def test_logviewer_deployment_on_k8s(kube):

@@ -150,6 +150,57 @@ def test_allreduce_job_ranks_rendezvous_and_reap(env):
     assert cli(env, "list").splitlines()[1].split()[:3] == ["ar", "SUCCEEDED", "MPIJOB"]
 
 
+RANKS = (
+    "import os, torch, torch.distributed as d; d.init_process_group('gloo'); "
+    "t = torch.tensor([float(d.get_rank() + 1)]); d.all_reduce(t); "
+    "e = os.environ; print('rank', d.get_rank(), 'of', d.get_world_size(), 'sum', t.item(), "
+    "'local', e['LOCAL_RANK'], 'lws', e['LOCAL_WORLD_SIZE'], 'group', e['GROUP_RANK'], "
+    "'vis', e.get('HIP_VISIBLE_DEVICES')); d.destroy_process_group()")
+
+
+def test_allreduce_several_ranks_per_pod(env, monkeypatch):
+    """`--workers 2 --gpus 4` on an 8-GPU node: 2 pods x 4 ranks (one per GPU), rendezvous of all
+    8 over gloo; every rank sees the job's 8 GPUs and picks its own with a node-wide LOCAL_RANK
+    (so one-node jobs keep the xGMI collectives)."""
+    monkeypatch.setenv("ARENA_LOCAL_GPUS", "8")
+    cli(env, "submit", "mpi", "--name", "rpp", "--workers", "2", "--gpus", "4",
+        f'{PY} -c "{RANKS}"')
+    plan = json.load(open(os.path.join(env.job_dir("rpp"), "plan.json")))
+    assert len(plan["pods"]) == 2 and all("podlaunch" in " ".join(p["argv"]) for p in plan["pods"])
+    st = wait_phase(env, "rpp", timeout=180)
+    assert st["phase"] == "Succeeded", st
+    logs = "".join(open(os.path.join(env.job_dir("rpp"), "logs", f)).read()
+                   for f in os.listdir(os.path.join(env.job_dir("rpp"), "logs")))
+    seen = {}
+    for line in logs.splitlines():
+        w = line.split()
+        if "rank" in w and "sum" in w:
+            i = w.index("rank")
+            seen[int(w[i + 1])] = dict(zip(w[i + 2::2], w[i + 3::2]))
+    assert sorted(seen) == list(range(8)), logs
+    for r, kv in seen.items():
+        assert kv["of"] == "8" and kv["sum"] == "36.0" and kv["lws"] == "8"
+        assert kv["group"] == str(r // 4) and kv["vis"] == "0,1,2,3,4,5,6,7"
+    assert sorted(int(kv["local"]) for kv in seen.values()) == list(range(8))
+
+
+def test_podlaunch_failing_rank_takes_the_gang_down(tmp_path):
+    """The in-pod launcher: one rank exits 7 -> its siblings (blocked, as in a collective) are
+    terminated and the pod exits 7 quickly instead of hanging."""
+    import subprocess
+    env = dict(os.environ, ARENA_RANKS_PER_POD="3", ARENA_PODS="1", ARENA_POD_INDEX="0",
+               ARENA_RANK_GRACE_S="2", PYTHONPATH=REPO,
+               ARENA_RANK_COMMAND='if [ "$RANK" = 1 ]; then exit 7; fi; sleep 60')
+    t0 = time.time()
+    r = subprocess.run([PY, "-m", "arena_amd.runtime.podlaunch"], env=env, timeout=60)
+    assert r.returncode == 7 and time.time() - t0 < 20
+    from arena_amd.runtime import podlaunch
+    envs = podlaunch.rank_envs({"ARENA_RANKS_PER_POD": "4", "ARENA_PODS": "3",
+                                "POD_NAME": "job-tf-horovod-1"})
+    assert [e["RANK"] for e in envs] == ["8", "9", "10", "11"]
+    assert {e["WORLD_SIZE"] for e in envs} == {"12"} and envs[0]["GROUP_RANK"] == "2"
+
+
 def test_allreduce_worker_fault_fails_job_and_reaps(env, monkeypatch):
     monkeypatch.setenv("ARENA_FAULT_POD", "fi-tf-horovod-0")
     monkeypatch.setenv("ARENA_FAULT_AFTER_MS", "300")
