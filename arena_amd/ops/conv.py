@@ -40,6 +40,15 @@ TILES.update({v + 16 * (k - 1): TILES[v] for v in range(16) for k in KSPLITS})
 # conv_kernels.hip conv_fwd_body), and the per-block prologue is paid once per 2^p tiles
 PERSIST = (1, 2, 3, 4)
 TILES.update({v + 256 * p: TILES[v] for v in range(16) for p in PERSIST})
+# 4096 + i: the v2 tile kernel (conv_kernels.hip conv2_body): 32x32x16 MFMAs, 8-wave 256-row
+# tiles (4-wave 128x128), two K steps in flight, epilogue through an fp32 LDS tile. Forward and
+# stride-1 backward-data only (plain, masked addend, BatchNorm statistics); never split or
+# persistent.
+V2 = 4096
+V2_TILES = {V2 + 0: (256, 128), V2 + 1: (256, 256), V2 + 2: (128, 128), V2 + 3: (256, 64),
+            V2 + 4: (128, 256)}
+TILES.update(V2_TILES)
+_V2_ON = os.environ.get("ARENA_CONV_V2", "1") != "0"
 _CUS = 256
 
 
@@ -53,7 +62,18 @@ def split_of(v: int) -> int:
 
 
 def tiles_per_block(v: int) -> int:
-    return 1 << (v // 256)
+    return 1 if v >= V2 else 1 << (v // 256)
+
+
+def set_v2(on: bool) -> None:
+    """A/B switch: offer the v2 tile kernel to the autotuner (part of the plan key)."""
+    global _V2_ON
+    _V2_ON = bool(on)
+
+
+def v2_variants_for(cout: int):
+    """v2 tile variants for ``cout`` output channels (forward / stride-1 backward-data)."""
+    return [v for v, (_, bn) in V2_TILES.items() if cout % bn == 0] if _V2_ON else []
 
 
 _PERSIST_ON = os.environ.get("ARENA_CONV_PERSIST", "1") != "0"
@@ -627,7 +647,8 @@ def _best(t: dict, kind: str, n: int):
 
 
 def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
-    key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _PERSIST_ON)
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _PERSIST_ON,
+           _V2_ON)
     plan = _PLANS.get(key)
     if plan is not None and (plan.tuned or torch.cuda.is_current_stream_capturing()):
         return plan
@@ -669,11 +690,13 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
             return us if fin else us + _FIN_PENALTY_US
 
         fns = {}
-        for v in variants_for(cout) + split_variants_for(m_out, cout, cin * k[0] * k[1]):
+        for v in (variants_for(cout) + v2_variants_for(cout)
+                  + split_variants_for(m_out, cout, cin * k[0] * k[1])):
             fns[("fwd", v)] = (lambda v=v: fwd_time(v))
         if stride == 1:
             m_in = x.shape[0] * x.shape[2] * x.shape[3]
-            for v in variants_for(cin) + split_variants_for(m_in, cin, cout * k[0] * k[1]):
+            for v in (variants_for(cin) + v2_variants_for(cin)
+                      + split_variants_for(m_in, cin, cout * k[0] * k[1])):
                 fns[("bwd", v)] = (lambda v=v: _time(lambda: conv2d_bwd_data(dy, w, pad, v)))
         else:   # phase decomposition: per-phase heuristic (-1) or one tile for every phase
             hw = (x.shape[2], x.shape[3])
@@ -918,7 +941,7 @@ class _ConvFn(torch.autograd.Function):
             lk = ctx.bn_link
             # the BN partials need the COMPLETE gradient of x: not from a join's first arriver
             use_bn = (lk is not None and plan.bwd != MIOPEN and stride == 1
-                      and lk.x.shape == x.shape
+                      and plan.bwd < V2 and lk.x.shape == x.shape
                       and (join is None or other is not None))
             if plan.bwd == MIOPEN:
                 dx = _miopen_bwd(dy, x, w, stride, pad, [True, False, False])[0]

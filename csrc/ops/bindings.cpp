@@ -826,7 +826,8 @@ unsigned* conv_tickets(const Tensor& like, int64_t tiles) {
 }
 
 // conv variant code: tile/pipeline variant (0..15) + 16 * (ksplit - 1) + 256 * p, where p > 0
-// selects the persistent form with 2^p output tiles per block (not with split-K)
+// selects the persistent form with 2^p output tiles per block (not with split-K); 4096 + i: the v2
+// tile kernel's variant i
 struct ConvSplit {
   int base = 0, ks = 1, tpb = 1;
   Tensor ws;
@@ -836,6 +837,11 @@ struct ConvSplit {
 ConvSplit conv_split(const Tensor& x, int64_t variant, int64_t M, int64_t Cout, int64_t Ktot) {
   ConvSplit s;
   TORCH_CHECK(variant >= 0, "conv: bad variant ", variant);
+  if (variant >= 4096) {   // v2 tile kernel (conv_kernels.hip conv2_body): never split/persistent
+    TORCH_CHECK(variant < 4096 + 5, "conv: unknown v2 variant ", variant);
+    s.base = (int)variant;
+    return s;
+  }
   s.base = (int)(variant % 16);
   s.ks = (int)(variant % 256 / 16) + 1;
   const int p = (int)(variant / 256);

@@ -1017,6 +1017,369 @@ hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
   return hipGetLastError();
 }
 
+// ================================================================================================
+// Tile kernel v2 (variant codes 4096 + i): 32x32x16 MFMAs on 256-row tiles, a deeper LDS-DMA
+// pipeline, and an epilogue that works on an fp32 copy of the output tile in LDS.
+//
+// Why (docs/perf.md "Where the ResNet-50 step stands"): the v1 kernel issues 16x16x32 MFMAs on
+// 128x128 tiles and stages 32 KB per 2 MFLOP. v2 stages (256 + BN) rows per 64-deep K step --
+// 48 KB per 4.2 MFLOP at 256x128 -- and its 32x32x16 MFMA reads half the LDS bytes per FLOP of
+// the 16x16x32 one (per wave and k16 step MI + NI fragments of 1 KB feed MI * NI MFMAs of
+// 32 K-FLOP). With NBUF = 3 two K steps are in flight across each barrier (counted vmcnt, raw
+// s_barrier: __syncthreads() would drain the LDS-DMA, cdna_hip_programming.md §5).
+//
+// Operands are staged exactly as in v1 (descriptor-based buffer_load ... lds, 128-byte rows with
+// the chunk ^ ((row >> 1) & 7) swizzle, which also makes the 32x32 fragment reads conflict-free:
+// every 16-lane ds_read_b128 group covers 16 distinct (row & 1, (row >> 1) & 7) pairs).
+//
+// The MFMA runs as W-fragment x X-fragment: D[row = channel][col = pixel], so lane l, register r
+// holds pixel (l & 31) and channel 8 (r >> 2) + 4 (l >> 5) + (r & 3) of its 32x32 block. The
+// epilogue writes those to an fp32 [row][channel] tile in LDS (16-byte slots, slot ^ (row & 7):
+// conflict-free ds_write_b128), then every feature reads the tile in a layout of its own:
+// coalesced 16-byte bf16 stores (+ optional masked addend, the residual join), and the BatchNorm
+// statistics (EPI 1) as column sums over the tile's valid rows -- per-tile partials (mean, M2) or
+// fp64 acc-mode atomics, the formats the v1 kernel emits. Tiles that do not fit LDS at once are
+// processed in bands of one wave-row (EH = WM rows), statistics merged across bands (Chan).
+// Not covered (v1 handles them): c16, mapped outputs (strided dgrad phases), split-K, persistent
+// tiles, EPI 2.
+// ================================================================================================
+typedef float f32x16v __attribute__((ext_vector_type(16)));
+
+constexpr int kLdsMax = 160 * 1024;
+
+template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI>
+struct Conv2Geo {
+  static constexpr int NT = 64 * NWM * NWN;
+  static constexpr int WM = BM / NWM, WN = BN / NWN;
+  static constexpr int MI = WM / 32, NI = WN / 32;
+  static constexpr int AI = BM * 8 / NT, BI = BN * 8 / NT;
+  static constexpr int kBufBytes = (BM + BN) * kRowBytes;
+  static constexpr int kStage = NBUF * kBufBytes;
+  static constexpr int SL = BN / 4;       // float4 slots per tile row
+  static constexpr int RG = NT / SL;      // row groups of the statistics passes
+  static constexpr int kRed = EPI == 1 ? (RG * BN + BN) * 4 : 0;
+  static constexpr int EH = BM * BN * 4 + kRed <= kLdsMax - 1024 ? BM : WM;   // rows per band
+  static constexpr int kEpi = EH * BN * 4 + kRed;
+  static constexpr int kLds = kStage > kEpi ? kStage : kEpi;
+  static_assert(MI >= 1 && NI >= 1 && AI >= 1 && BI >= 1, "tile too small for the wave grid");
+  static_assert(AI * NT == BM * 8 && BI * NT == BN * 8, "staging slots must cover the tile");
+  static_assert(SL >= 8 && NT % SL == 0, "epilogue layout");
+  static_assert(kLds <= kLdsMax, "LDS budget");
+};
+
+template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI>
+__device__ __forceinline__ void conv2_body(const ConvArgs& a) {
+  using G = Conv2Geo<BM, BN, NWM, NWN, NBUF, EPI>;
+  constexpr int NT = G::NT, WM = G::WM, WN = G::WN, MI = G::MI, NI = G::NI;
+  constexpr int AI = G::AI, BI = G::BI, kBufBytes = G::kBufBytes;
+  constexpr int SL = G::SL, RG = G::RG, EH = G::EH;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G::kLds];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-aware order (as v1): each XCD gets a contiguous range of tiles, column tiles of one row
+  // tile consecutive (their A rows stay in that XCD's L2)
+  const int nwg = a.m_tiles * a.n_tiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int nt = lin % a.n_tiles, mt = lin / a.n_tiles;
+  const int n0 = nt * BN, m0 = mt * BM;
+
+  // ---- staging descriptors (v1's descriptor form): slot s = (wave*AI + i)*64 + lane -> LDS row
+  // s / 8, chunk position s % 8 = lane % 8 ----
+  const int pos = lane & 7;
+  constexpr uint32_t kOOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t xrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+  int a_lane[AI];
+  uint32_t a_mask[AI], a_cur[AI], b_voff[BI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (wave * AI + i) * 8 + (lane >> 3);
+    const int m = m0 + row;
+    uint32_t mk = 0u;
+    int off = 0;
+    if (m < a.M) {
+      const int hw = a.Ho * a.Wo;
+      const int n = m / hw, rem = m - n * hw;
+      const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+      const int hb = ho * a.stride - a.pad, wb = wo * a.stride - a.pad_w;
+      for (int r = 0; r < a.R; ++r) {
+        if ((unsigned)(hb + r) >= (unsigned)a.H) continue;
+        for (int s2 = 0; s2 < a.S; ++s2)
+          if ((unsigned)(wb + s2) < (unsigned)a.W) mk |= 1u << (r * a.S + s2);
+      }
+      off = (((n * a.H + hb) * a.W + wb) * a.C + (pos ^ swz(row)) * 8) * 2;
+    }
+    a_lane[i] = off;
+    a_mask[i] = mk;
+  }
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = (wave * BI + i) * 8 + (lane >> 3);
+    b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
+  }
+  const int CB = a.C / kBK;
+  const int T = a.Ktot / kBK;
+  int s_tap = 0, s_cb = 0, s_s = 0, s_tapoff = 0, s_t = 0;
+#pragma unroll
+  for (int i = 0; i < AI; ++i) a_cur[i] = (a_mask[i] & 1u) ? (uint32_t)a_lane[i] : kOOB;
+
+  auto stage = [&](int buf) {
+    uint8_t* base = lds + buf * kBufBytes;
+    const int coff = s_cb * kRowBytes;
+#pragma unroll
+    for (int i = 0; i < AI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_ptr_t)(base + (wave * AI + i) * 64 * 16),
+                                               16, a_cur[i], coff, 0, 0);
+    uint8_t* bb = base + BM * kRowBytes;
+#pragma unroll
+    for (int i = 0; i < BI; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
+                                               16, b_voff[i], s_t * kRowBytes, 0, 0);
+    ++s_t;
+    if (++s_cb == CB) {
+      s_cb = 0;
+      ++s_tap;
+      s_tapoff += a.C * 2;
+      if (++s_s == a.S) {
+        s_s = 0;
+        s_tapoff += (a.W - a.S) * a.C * 2;
+      }
+#pragma unroll
+      for (int i = 0; i < AI; ++i)
+        a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
+    }
+  };
+
+  f32x16v acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int wm = wave / NWN, wn = wave % NWN;
+  const int fr = lane & 31, hh = lane >> 5;
+
+  auto compute = [&](int buf) {
+    const uint8_t* abuf = lds + buf * kBufBytes;
+    const uint8_t* bbuf = abuf + BM * kRowBytes;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {
+      bf16x8 af[MI], bfr[NI];
+      const int c = kk * 2 + hh;   // 16-byte chunk of this lane's 8 k values
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * WM + i * 32 + fr;
+        af[i] = *reinterpret_cast<const bf16x8*>(abuf + row * kRowBytes + ((c ^ swz(row)) << 4));
+      }
+#pragma unroll
+      for (int j = 0; j < NI; ++j) {
+        const int row = wn * WN + j * 32 + fr;
+        bfr[j] = *reinterpret_cast<const bf16x8*>(bbuf + row * kRowBytes + ((c ^ swz(row)) << 4));
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  // ---- K loop: S = NBUF - 1 steps in flight ----
+  {
+    constexpr int S = NBUF - 1;
+    constexpr int kLps = AI + BI;   // LDS-DMA instructions per thread per stage
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if (i < T) stage(i);
+    if (T >= S)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * kLps) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    int cur = 0;
+    for (int t = 0; t < T; ++t) {
+      // RAW: stage t + 1 was retired by the vmcnt before the last barrier. WAR: stage t + S
+      // overwrites buffer (t - 1) % NBUF, whose reads completed before that barrier.
+      if (t + S < T) stage(cur == 0 ? NBUF - 1 : cur - 1);
+      compute(cur);
+      if (t + S < T)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((S - 1) * kLps) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      cur = cur == NBUF - 1 ? 0 : cur + 1;
+    }
+  }
+
+  // ---- epilogue through the fp32 LDS tile (the stage buffers are free: the loop ended on a
+  // barrier after every wave's last read) ----
+  float* tile = reinterpret_cast<float*>(lds);
+  float* red = tile + EH * BN;          // [RG][BN] partial column sums (EPI 1)
+  float* cmean = red + RG * BN;         // [BN] band mean (EPI 1)
+  constexpr int CPR = BN / 8;           // 16-byte bf16 output chunks per row
+  if constexpr (EPI == 1) {
+    // statistics of the stored (bf16-rounded) values: round once, the stores re-round exactly
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) {
+          const uint32_t u = pack_bf16x2(acc[i][j][r], acc[i][j][r + 1]);
+          acc[i][j][r] = __uint_as_float(u << 16);
+          acc[i][j][r + 1] = __uint_as_float(u & 0xffff0000u);
+        }
+  }
+  float st_n = 0.f, st_mean = 0.f, st_m2 = 0.f;   // running statistics of channel tid (< BN)
+#pragma unroll
+  for (int band = 0; band < BM / EH; ++band) {
+    if (band > 0) lds_barrier();   // every reader of the previous band is done
+    if (EH == BM || wm == band) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int row = wm * WM + i * 32 + fr - band * EH;
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int slot = (wn * WN + j * 32 + 8 * g + 4 * hh) >> 2;
+            *reinterpret_cast<f32x4v*>(tile + (row * SL + (slot ^ (row & 7))) * 4) =
+                f32x4v{acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                       acc[i][j][4 * g + 3]};
+          }
+      }
+    }
+    lds_barrier();
+    const int rbase = m0 + band * EH;
+    const int nvalid = min(EH, a.M - rbase);
+    // coalesced stores: consecutive lanes on consecutive 16-byte chunks of a row
+    for (int qq = tid; qq < EH * CPR; qq += NT) {
+      const int row = qq / CPR, cc = qq - row * CPR;
+      if (row >= nvalid) break;
+      const f32x4v lo = *reinterpret_cast<const f32x4v*>(tile + (row * SL + ((2 * cc) ^ (row & 7))) * 4);
+      const f32x4v hi = *reinterpret_cast<const f32x4v*>(tile + (row * SL + ((2 * cc + 1) ^ (row & 7))) * 4);
+      float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      const size_t off = (size_t)(rbase + row) * a.Cout + n0 + cc * 8;
+      if (EPI == 0 && a.add != nullptr) {
+        const uint4 qa = masked_add8(a.add, a.addmask, off);
+        const uint32_t u[4] = {qa.x, qa.y, qa.z, qa.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += __uint_as_float(u[e] << 16);
+          v[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
+        }
+      }
+      *reinterpret_cast<uint4*>(a.y + off) =
+          make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
+                     pack_bf16x2(v[6], v[7]));
+    }
+    if constexpr (EPI == 1) {
+      if (nvalid > 0) {
+        // two-pass column statistics over the band's valid rows: thread = (row group, slot)
+        const int sl = tid % SL, rg = tid / SL;
+        f32x4v s4 = {0.f, 0.f, 0.f, 0.f};
+        for (int row = rg; row < nvalid; row += RG)
+          s4 += *reinterpret_cast<const f32x4v*>(tile + (row * SL + (sl ^ (row & 7))) * 4);
+        *reinterpret_cast<f32x4v*>(red + rg * BN + sl * 4) = s4;
+        lds_barrier();
+        if (tid < BN) {
+          float sum = 0.f;
+#pragma unroll 8
+          for (int g2 = 0; g2 < RG; ++g2) sum += red[g2 * BN + tid];
+          cmean[tid] = sum / (float)nvalid;
+        }
+        lds_barrier();
+        const f32x4v mu = *reinterpret_cast<const f32x4v*>(cmean + sl * 4);
+        f32x4v q4 = {0.f, 0.f, 0.f, 0.f};
+        for (int row = rg; row < nvalid; row += RG) {
+          const f32x4v d = *reinterpret_cast<const f32x4v*>(tile + (row * SL + (sl ^ (row & 7))) * 4) - mu;
+          q4 += d * d;
+        }
+        lds_barrier();   // every thread has read cmean's band sums (red is rewritten below)
+        *reinterpret_cast<f32x4v*>(red + rg * BN + sl * 4) = q4;
+        lds_barrier();
+        if (tid < BN) {
+          float m2 = 0.f;
+#pragma unroll 8
+          for (int g2 = 0; g2 < RG; ++g2) m2 += red[g2 * BN + tid];
+          const float bmean = cmean[tid], nb = (float)nvalid;
+          if (st_n == 0.f) {
+            st_n = nb; st_mean = bmean; st_m2 = m2;
+          } else {   // Chan's merge of two bands
+            const float ntot = st_n + nb, d = bmean - st_mean;
+            st_mean += d * nb / ntot;
+            st_m2 += m2 + d * d * st_n * nb / ntot;
+            st_n = ntot;
+          }
+        }
+      }
+    }
+  }
+  if constexpr (EPI == 1) {
+    if (tid < BN) {
+      const int c = n0 + tid;
+      if (a.bn_acc == nullptr) {
+        a.part[(size_t)mt * 2 * a.Cout + c] = st_mean;
+        a.part[(size_t)mt * 2 * a.Cout + a.Cout + c] = st_m2;
+      } else {
+        const double n = (double)st_n, mu = (double)st_mean;
+        unsafeAtomicAdd(a.bn_acc + c, n * mu);                                 // sum y
+        unsafeAtomicAdd(a.bn_acc + a.Cout + c, (double)st_m2 + n * mu * mu);   // sum y^2
+      }
+    }
+  }
+}
+
+template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI>
+__global__ __launch_bounds__(64 * NWM * NWN) void conv2_kernel(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
+  conv2_body<BM, BN, NWM, NWN, NBUF, EPI>(a);
+#endif
+}
+
+template <int BM, int BN, int NWM, int NWN, int NBUF>
+hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
+  ConvArgs a = a0;
+  if (a.c16 || a.mapped || a.bnx != nullptr || a.ksplit != 1 || a.tpb != 1 || a.Cout % BN)
+    return hipErrorInvalidValue;
+  if ((a.part != nullptr || a.bn_acc != nullptr) && a.add != nullptr) return hipErrorInvalidValue;
+  a.m_tiles = (a.M + BM - 1) / BM;
+  a.n_tiles = a.Cout / BN;
+  const int nwg = a.m_tiles * a.n_tiles;
+  const bool stats = a.part != nullptr || a.bn_acc != nullptr;
+  if (stats)
+    hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 1>), dim3(nwg),
+                       dim3(64 * NWM * NWN), 0, st, a);
+  else
+    hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 0>), dim3(nwg),
+                       dim3(64 * NWM * NWN), 0, st, a);
+  return hipGetLastError();
+}
+
+// v2 variant table (code 1024 + index): BM x BN tile, waves NWM x NWN, stage buffers
+constexpr int kV2Base = 4096;   // above every v1 code (split + 16 k, persistent + 256 p <= 1039)
+constexpr int kV2Count = 5;
+constexpr int kV2Tiles[kV2Count][2] = {{256, 128}, {256, 256}, {128, 128}, {256, 64}, {128, 256}};
+
+hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
+  switch (idx) {
+    case 0: return launch2_t<256, 128, 4, 2, 3>(a, st);
+    case 1: return launch2_t<256, 256, 2, 4, 2>(a, st);
+    case 2: return launch2_t<128, 128, 2, 2, 2>(a, st);
+    case 3: return launch2_t<256, 64, 4, 2, 3>(a, st);
+    case 4: return launch2_t<128, 256, 2, 4, 3>(a, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 // the stem's c16 form only exists for 64-wide tiles (its Cout is 64)
 template <int BM, int BN>
 hipError_t launch(const ConvArgs& a, int pipe, hipStream_t st) {
@@ -1106,7 +1469,8 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   if (M >= (1LL << 31) || (long long)N * H * W * C >= (1LL << 40)) return hipErrorInvalidValue;
   a.M = (int)M;
   a.Ktot = R * S * C;
-  if (variant < 0 || variant > 15) return hipErrorInvalidValue;
+  const bool v2 = variant >= kV2Base && variant < kV2Base + kV2Count;
+  if (!v2 && (variant < 0 || variant > 15)) return hipErrorInvalidValue;
   if (!c16) {   // descriptor staging: 31-bit byte offsets, a 32-bit tap mask
     const long long xb = (long long)N * H * W * C * 2, wb = (long long)Cout * a.Ktot * 2;
     if (xb >= (1LL << 31) || wb >= (1LL << 31) || R * S > 32) return hipErrorInvalidValue;
@@ -1122,6 +1486,10 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.kcnt = kcnt;
   a.tpb = tpb;
   a.st1p = g_conv_st1p;
+  if (v2) {
+    if (c16) return hipErrorInvalidValue;
+    return launch2(a, variant - kV2Base, st);
+  }
   if (variant >= 12) {   // 256-row tiles, 8 waves: 12/13 two stage buffers, 14/15 three
     const int nb = variant >= 14 ? 3 : 2;
     if ((variant & 1) == 0)
@@ -1150,7 +1518,10 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
 // Split-K workspace of one launch, in floats (0 when ksplit == 1), and its ticket count (tiles).
 static void conv_tile(int variant, int* bm, int* bn) {
   static const int tm[4] = {128, 128, 64, 64}, tn[4] = {128, 64, 128, 64};
-  if (variant >= 12) {
+  if (variant >= kV2Base && variant < kV2Base + kV2Count) {
+    *bm = kV2Tiles[variant - kV2Base][0];
+    *bn = kV2Tiles[variant - kV2Base][1];
+  } else if (variant >= 12) {
     *bm = 256;
     *bn = (variant & 1) ? 64 : 128;
   } else {
@@ -1160,14 +1531,15 @@ static void conv_tile(int variant, int* bm, int* bn) {
 }
 
 long long arena_conv_fwd_ksplit_floats(long long M, int Cout, int variant, int ksplit) {
-  if (ksplit <= 1 || variant < 0 || variant > 15) return 0;
+  if (ksplit <= 1 || variant < 0 || variant > 15) return 0;   // v2 tiles never split
   int bm, bn;
   conv_tile(variant, &bm, &bn);
   return ((M + bm - 1) / bm) * (Cout / bn) * ksplit * bm * bn;
 }
 
 long long arena_conv_fwd_tiles(long long M, int Cout, int variant) {
-  if (variant < 0 || variant > 15) return 0;
+  if (variant < 0 || (variant > 15 && !(variant >= kV2Base && variant < kV2Base + kV2Count)))
+    return 0;
   int bm, bn;
   conv_tile(variant, &bm, &bn);
   return ((M + bm - 1) / bm) * (Cout / bn);

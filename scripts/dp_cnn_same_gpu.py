@@ -33,6 +33,32 @@ import torch.multiprocessing as mp
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
+def trace_overlap(model, opt, x, y, path):
+    """One eager DP step under torch.profiler (ROCm kernel activity): the optimizer kernels
+    (``xgmi_sgd``) that START before the step's last backward kernel ENDS ran concurrently with
+    backward. Writes the kernel timeline (name, start, end in us) to ``path``."""
+    from torch.profiler import ProfilerActivity, profile
+    from arena_amd.examples import cnn_bench
+    torch.cuda.synchronize()
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
+        torch.cuda.synchronize()
+    ks = [(e.name, e.time_range.start, e.time_range.end) for e in prof.events()
+          if e.device_type.name == "CUDA"]
+    ks.sort(key=lambda k: k[1])
+    opt_k = [k for k in ks if "xgmi_sgd" in k[0]]
+    other = [k for k in ks if "xgmi_sgd" not in k[0] and "copy" not in k[0].lower()]
+    last_bwd_end = max(k[2] for k in other) if other else 0
+    early = [k for k in opt_k if k[1] < last_bwd_end]
+    with open(path, "w") as f:
+        for k in ks:
+            f.write(json.dumps({"name": k[0][:120], "start_us": k[1], "end_us": k[2]}) + "\n")
+    return {"optimizer_kernels": len(opt_k), "started_before_backward_end": len(early),
+            "kernels": len(ks),
+            "first_opt_start_vs_last_bwd_end_us": (round(opt_k[0][1] - last_bwd_end, 1)
+                                                  if opt_k else None)}
+
+
 def rank_main(rank, world, port, a, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0", LOCAL_WORLD_SIZE=str(world))
@@ -54,6 +80,14 @@ def rank_main(rank, world, port, a, q):
         torch.cuda.synchronize()
         if rank == 0:  # the first steps include the solver search: show progress
             print(f"warmup {i + 1}/{a.warmup}", file=sys.stderr, flush=True)
+    overlap = None
+    if a.trace:   # a collective step: every rank runs it, rank 0 under the profiler
+        if rank == 0:
+            overlap = trace_overlap(model, opt, x, y, a.trace)
+        else:
+            cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
+            torch.cuda.synchronize()
+        dist.barrier()
     graph = None
     if a.graph:  # the whole DP step (bucket hooks + xGMI kernels on the comm stream) as a hipGraph
         graph, g_loss = cnn_bench.capture_step(model, opt, x, y, torch.bfloat16)
@@ -75,7 +109,7 @@ def rank_main(rank, world, port, a, q):
             c.check()
     flat = torch.cat([p.detach().double().reshape(-1) for p in model.parameters()])
     digest = float(flat.sum().item()), float(flat.abs().sum().item())
-    q.put((rank, dt, float(loss), digest, len(opt.buckets), name))
+    q.put((rank, dt, float(loss), digest, len(opt.buckets), name, overlap))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -90,6 +124,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step as a hipGraph")
+    ap.add_argument("--trace", default="", help="rank 0 writes one eager step's kernel timeline "
+                    "(torch.profiler) here and reports how many optimizer kernels overlapped "
+                    "backward")
     ap.add_argument("--master_weights", choices=["auto", "on", "off"], default="auto",
                     help="auto/on: bf16 weights + ShardedMasterSGD (xGMI reduce-scatter / SGD / "
                          "all-gather); off: fp32 weights + DistributedOptimizer buckets")
@@ -113,7 +150,7 @@ def main():
                       "comm": res[0][5],
                       "images_per_s_all_ranks": round(a.world * a.batch_size * a.steps / dt, 1),
                       "ms_per_step": round(dt / a.steps * 1e3, 3), "final_loss": round(res[0][2], 4),
-                      "replicas_identical": same}), flush=True)
+                      "replicas_identical": same, "overlap": res[0][6]}), flush=True)
     if not same:
         sys.exit(1)
 

@@ -103,6 +103,87 @@ def test_conv_fwd_bwd_wgrad_match_fp32(shape):
         assert dwb.dtype == torch.bfloat16 and dwb.is_contiguous(memory_format=torch.channels_last)
 
 
+V2_SHAPES = [  # n, cin, h, w, cout, k, stride
+    (2, 64, 9, 11, 64, 3, 1),       # M = 198 < one 256-row tile
+    (3, 128, 7, 7, 128, 1, 1),
+    (2, 64, 10, 10, 128, 3, 2),
+    (2, 192, 6, 5, 256, 3, 1),
+    (8, 64, 28, 28, 64, 3, 1),      # 6272 rows: tail tile of 128 rows
+    (2, 256, 14, 14, 512, 1, 1),    # BN = 256 tiles, two row bands in the 256x256 epilogue
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", V2_SHAPES)
+def test_conv_v2_matches_fp32(shape):
+    """v2 tile kernel (32x32x16 MFMA, LDS epilogue): forward, stride-1 backward-data with the
+    residual-join addend (dense and bit-masked), against fp32 F.conv2d; its BatchNorm statistics
+    (per-tile partials and acc-mode sums) against the BN layer's own statistics pass."""
+    from arena_amd.ops import _ext
+    from arena_amd.ops.batchnorm import BatchNormAct2d
+    _ext.load()
+    n, cin, h, w, cout, k, st = shape
+    pad = k // 2
+    x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=5)
+    ref = F.conv2d(x.float(), wt.float(), stride=st, padding=pad)
+    vs = conv.v2_variants_for(cout)
+    assert vs
+    for v in vs:
+        y = conv.conv2d_fwd(x, wt, st, pad, v)
+        assert y.shape == ref.shape and y.is_contiguous(memory_format=torch.channels_last)
+        assert _rel(y, ref) < 1e-2, (v, _rel(y, ref))
+        y1 = conv.conv2d_fwd(x, wt, st, pad, 0 if cout % 128 == 0 else 1)
+        # same products, same K order per output: equal to v1 to rounding (fp32 sum order of
+        # the MFMA shapes differs)
+        assert _rel(y, y1) < 1e-2
+        yp, (part, rpb) = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True)
+        assert torch.equal(yp, y) and rpb == conv.TILES[v][0]
+        m = y.shape[0] * y.shape[2] * y.shape[3]
+        assert part.numel() == -(-m // rpb) * 2 * cout
+        yf, fin = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True, final=True)
+        assert torch.equal(yf, y)
+        for stats in ((part, rpb), fin):
+            bns = [BatchNormAct2d(cout).cuda() for _ in range(2)]
+            for b in bns:
+                b.weight.data.uniform_(0.5, 1.5)
+                b.bias.data.uniform_(-0.5, 0.5)
+            bns[1].load_state_dict(bns[0].state_dict())
+            out_ref = bns[0](y)
+            out = bns[1](y, stats=stats)
+            assert _rel(out, out_ref) < 1e-2, v
+            torch.testing.assert_close(bns[1].running_mean, bns[0].running_mean, rtol=1e-4,
+                                       atol=1e-5)
+            torch.testing.assert_close(bns[1].running_var, bns[0].running_var, rtol=1e-3,
+                                       atol=1e-5)
+    if st != 1:
+        return
+    dy = torch.randn(ref.shape, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dx_ref, _, _ = torch.ops.aten.convolution_backward(
+        dy.float(), x.float(), wt.float(), None, [1, 1], [pad, pad], [1, 1], False, [0, 0], 1,
+        [True, False, False])
+    addend = torch.randn(x.shape, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    bits = torch.randint(0, 256, (addend.numel() // 8,), device="cuda", dtype=torch.uint8)
+    dense = conv.MaskedGrad(addend, bits).materialize()
+    for v in conv.v2_variants_for(cin):
+        dx = conv.conv2d_bwd_data(dy, wt, pad, v)
+        assert _rel(dx, dx_ref) < 1e-2, (v, _rel(dx, dx_ref))
+        dxa = conv.conv2d_bwd_data(dy, wt, pad, v, addend=addend)
+        assert _rel(dxa, dx_ref + addend.float()) < 1e-2, v
+        a = conv.conv2d_bwd_data(dy, wt, pad, v, addend=addend, addmask=bits)
+        b = conv.conv2d_bwd_data(dy, wt, pad, v, addend=dense)
+        assert torch.equal(a, b), v
+
+
+def test_v2_variants_are_forward_and_dgrad_only():
+    assert conv.v2_variants_for(64) == [conv.V2 + 3]
+    assert set(conv.v2_variants_for(256)) == set(conv.V2_TILES)
+    assert all(conv.tiles_per_block(v) == 1 and conv.split_of(v) == 1 for v in conv.V2_TILES)
+    assert not set(conv.variants_for(256)) & set(conv.V2_TILES)   # strided dgrad phases: v1
+    assert conv.persist_variants_for(128 * 56 * 56, 256, list(conv.V2_TILES)) == []
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("shape", [(2, 256, 7, 7, 128, 3, 1), (3, 128, 6, 5, 256, 1, 1),
                                    (2, 64, 9, 11, 64, 3, 1), (4, 128, 7, 7, 128, 3, 2)])
