@@ -40,7 +40,7 @@ bench: all
 	$(PYTHON) bench.py
 
 e2e: all
-	bash scripts/e2e_mnist.sh
+	bash tools/e2e_mnist.sh
 
 version:
 	$(PYTHON) -m arena_amd version

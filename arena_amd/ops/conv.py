@@ -671,7 +671,7 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
     else:
         # Only the MFMA kernels are candidates: a captured step with MIOpen convolutions in it
         # returned wrong gradients on replays that followed other GPU/host work, while the same
-        # step on these kernels alone stayed bit-identical run to run (scripts/graph_mem_*.py,
+        # step on these kernels alone stayed bit-identical run to run (tools/graph_mem_*.py,
         # docs/perf.md "MIOpen inside a captured step"). ARENA_CONV=miopen keeps the library
         # path for comparisons.
         # (a random output gradient of the conv's output shape; no library call: F.conv2d here

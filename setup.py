@@ -22,9 +22,9 @@ if ARCH != "gfx950":
 HIP_SOURCES = ["csrc/ops/mlp_kernels.hip", "csrc/ops/bn_kernels.hip", "csrc/ops/pool_kernels.hip",
                "csrc/ops/conv_kernels.hip",
                "csrc/ccl/xgmi_ccl.hip"]
-# ARENA_TIMELINE=1: instrumented build for scripts/timeline.py (never the default)
+# ARENA_TIMELINE=1: instrumented build for tools/timeline.py (never the default)
 TIMELINE = ["-DARENA_TIMELINE"] if os.environ.get("ARENA_TIMELINE") == "1" else []
-if TIMELINE:  # ARENA_EXP ablation switches, instrumented builds only (see scripts/timeline.py)
+if TIMELINE:  # ARENA_EXP ablation switches, instrumented builds only (see tools/timeline.py)
     TIMELINE += os.environ.get("ARENA_EXP_FLAGS", "").split()
 CPP_SOURCES = ["csrc/ops/bindings.cpp"]
 

@@ -7,7 +7,7 @@ minimum row rounds per thread; csrc/ops/bn_kernels.hip::reduce_blocks), and prin
 per geometry with per-shape microseconds, the total weighted by how often ResNet-50 uses each
 shape, and the effective HBM bandwidth of the whole set.
 
-    python scripts/bn_bench.py --geoms 512:8,1024:8,2048:8,2048:4
+    python tools/bn_bench.py --geoms 512:8,1024:8,2048:8,2048:4
 """
 from __future__ import annotations
 

@@ -3,10 +3,10 @@
 scatter + all-gather) / all-gather / sharded bf16 SGD vs RCCL.
 
     # 8x MI355X node: one rank per GPU, RCCL process group
-    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 scripts/ccl_bench.py
+    python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 tools/ccl_bench.py
     # 1-GPU box: W ranks share GPU 0 (gloo process group, xGMI path only; "remote" reads are
     # local HBM, so this measures the protocol's barrier + launch cost, not link bandwidth)
-    python scripts/ccl_bench.py --same-gpu 2
+    python tools/ccl_bench.py --same-gpu 2
 
 Prints one JSON line per (op, size) from rank 0: time per call (graph-replayed, 50 calls per
 graph) and algorithm / bus bandwidth. busbw uses the ring-equivalent factor of each op: allreduce

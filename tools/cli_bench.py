@@ -4,7 +4,7 @@
 * submit -> RUNNING: wall time from `arena submit` until `arena list` shows RUNNING;
 * `arena list` / `arena top job` latency with N finished jobs in the store.
 
-    python scripts/cli_bench.py --jobs 100
+    python tools/cli_bench.py --jobs 100
 """
 from __future__ import annotations
 

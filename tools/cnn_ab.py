@@ -15,7 +15,7 @@ from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv 
 ``:nostempool`` (stem BN and max pool unfused), joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
-    python scripts/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
+    python tools/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
 """
 from __future__ import annotations
 

@@ -3,7 +3,7 @@
 adds, flips)? Runs eager steps under torch.profiler and prints, per aten op that launched GPU
 work outside the arena/MIOpen kernels, its device time per step and the Python frames above it.
 
-    python scripts/cnn_glue_prof.py [--model resnet50] [--batch 128] > gpurun_out/glue.txt
+    python tools/cnn_glue_prof.py [--model resnet50] [--batch 128] > gpurun_out/glue.txt
 """
 from __future__ import annotations
 

@@ -6,7 +6,7 @@ kernel against an fp32 F.conv2d of the same bf16 inputs (every tile variant), th
 forward (and, for stride-1 convs, backward-data through the flipped weight) against MIOpen
 (torch, cudnn.benchmark). One JSON line per layer; a summary line weighted by layer count.
 
-    python scripts/conv_bench.py --batch 128 > gpurun_out/conv_bench.jsonl
+    python tools/conv_bench.py --batch 128 > gpurun_out/conv_bench.jsonl
 """
 from __future__ import annotations
 

@@ -4,7 +4,7 @@
 For every conv with C % 64 == 0 and every tile variant: graph-replayed GPU time of the plain
 forward and of the forward that also writes the per-tile BN partials. One JSON line per layer.
 
-    python scripts/conv_epi_bench.py --batch 128 > gpurun_out/conv_epi.jsonl
+    python tools/conv_epi_bench.py --batch 128 > gpurun_out/conv_epi.jsonl
 """
 from __future__ import annotations
 

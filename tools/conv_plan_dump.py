@@ -6,7 +6,7 @@ prints one JSON line per distinct conv shape: the chosen forward / backward-data
 variant, its time, the layer count, and a roofline floor (FLOPs at 1.3 PFLOP/s vs minimum bytes at
 5 TB/s), plus a summary line. Tells which layers hold the conv share of the step.
 
-    python scripts/conv_plan_dump.py > gpurun_out/conv_plan.jsonl
+    python tools/conv_plan_dump.py > gpurun_out/conv_plan.jsonl
 """
 from __future__ import annotations
 

@@ -8,7 +8,7 @@ TFLOP/s and the effective bandwidth over the minimum bytes (inputs read once, ou
 once), weighted by how often the layer occurs in the network, so the table says which layers
 are compute- or memory-bound and where the step's conv time goes.
 
-    python scripts/conv_roofline.py --batch 128 > gpurun_out/conv_roofline.jsonl
+    python tools/conv_roofline.py --batch 128 > gpurun_out/conv_roofline.jsonl
 """
 from __future__ import annotations
 

@@ -3,7 +3,7 @@
 data (phase decomposition into stride-1 convs) and the space-to-depth 7x7/2 stem (forward +
 weight gradient), each against MIOpen at the same shapes. One JSON line per layer.
 
-    python scripts/conv_s2_bench.py --batch 128 > gpurun_out/conv_s2.jsonl
+    python tools/conv_s2_bench.py --batch 128 > gpurun_out/conv_s2.jsonl
 """
 from __future__ import annotations
 

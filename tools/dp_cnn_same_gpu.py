@@ -14,7 +14,7 @@ What it checks:
 The ranks time-share the CUs, so images/s is a lower bound of what W GPUs do; the allreduce
 runs over same-device hipIpc mappings (protocol cost, not xGMI bandwidth).
 
-    python scripts/dp_cnn_same_gpu.py --world 2 --model resnet50 --batch_size 32 --steps 20
+    python tools/dp_cnn_same_gpu.py --world 2 --model resnet50 --batch_size 32 --steps 20
 """
 from __future__ import annotations
 

@@ -4,7 +4,7 @@ xGMI collective's hipIpc protocol (gloo process group for setup only; RCCL refus
 one device). The ranks time-share the GPU's CUs, so ms/step is an upper bound of what W GPUs do;
 it checks that the DP path (graph-captured fused reduce-scatter/Adam/all-gather) runs end to end.
 
-    python scripts/dp_same_gpu.py --world 2 --steps 600 --warmup 60
+    python tools/dp_same_gpu.py --world 2 --steps 600 --warmup 60
 """
 from __future__ import annotations
 

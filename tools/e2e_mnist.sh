@@ -1,7 +1,7 @@
 #!/bin/bash
 # SURVEY §7.4 minimum end-to-end slice on a real MI355X: the LocalBackend runs the bundled MNIST
 # workloads on the GPU through the CLI, then every read command is exercised.
-# Usage: bash scripts/e2e_mnist.sh   (outputs under gpurun_out/e2e/)
+# Usage: bash tools/e2e_mnist.sh   (outputs under gpurun_out/e2e/)
 set -u -o pipefail
 cd "$(dirname "$0")/.."
 OUT=gpurun_out/e2e

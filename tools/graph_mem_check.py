@@ -6,7 +6,7 @@ ordinary pool) and free them, and replay again. A graph that only touches its ow
 and live tensors is unaffected; one that kept a pointer to freed memory now reads NaN.
 Feature switches bisect which component holds such a pointer.
 
-    python scripts/graph_mem_check.py --mode auto [--no_master] [--bn_ref] [--no_join]
+    python tools/graph_mem_check.py --mode auto [--no_master] [--bn_ref] [--no_join]
 """
 from __future__ import annotations
 

@@ -4,7 +4,7 @@ list memcpy nodes whose source is host memory: a captured host->device copy read
 REPLAY time, so a library that stages kernel arguments in a host buffer it later frees makes the
 graph replay read whatever the host heap holds then.
 
-    python scripts/graph_nodes.py --mode auto
+    python tools/graph_nodes.py --mode auto
 """
 from __future__ import annotations
 

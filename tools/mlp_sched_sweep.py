@@ -6,7 +6,7 @@ starts only after its packets are written, while a short graph pays the fixed pe
 few steps. This times 20 training steps run as different sequences of graph replays (dynamic
 step parity, so any sequence is valid) and prints samples/s per schedule (median of reps).
 
-    python scripts/mlp_sched_sweep.py
+    python tools/mlp_sched_sweep.py
 """
 import json
 import os

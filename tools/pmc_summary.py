@@ -9,7 +9,7 @@ counters are present:
   wait_frac   = SQ_WAIT_ANY / SQ_WAVE_CYCLES, issue_stall = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES
   l2_hit      = TCC_HIT / (TCC_HIT + TCC_MISS), lds_conf = SQ_LDS_BANK_CONFLICT / SQ_INSTS_LDS
 
-    python scripts/pmc_summary.py gpurun_out/r3_pmc1 --top 25 > summary.txt
+    python tools/pmc_summary.py gpurun_out/r3_pmc1 --top 25 > summary.txt
 """
 from __future__ import annotations
 

@@ -2,7 +2,7 @@
 """Steady-state kernel breakdown from a rocprofv3 kernel trace: drops everything up to the last
 MIOpen find-mode ("naive_conv") kernel, then groups kernels by category.
 
-    python scripts/steady_kernels.py gpurun_out/cnn/prof/r50_kernel_trace.csv [--top 40] [--csv out]
+    python tools/steady_kernels.py gpurun_out/cnn/prof/r50_kernel_trace.csv [--top 40] [--csv out]
 """
 import argparse
 import collections

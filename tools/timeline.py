@@ -2,7 +2,7 @@
 """Phase timeline of the two training-step kernels (needs the instrumented build):
 
     rm -rf build/hip_objs && ARENA_TIMELINE=1 python setup.py build_ext --inplace
-    python scripts/timeline.py
+    python tools/timeline.py
 
 Replays the captured step graph, then reads the per-block s_memrealtime stamps (100 MHz, 10 ns)
 of the LAST step's forward (kid 0) and weight-gradient (kid 1) kernels. Reports, per phase, the

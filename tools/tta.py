@@ -8,7 +8,7 @@ evaluation -- and reports the accuracy at step 990, the first step reaching 97 %
 time to get there (training + evaluations, synchronised), for the fused HIP trainer and for the
 eager PyTorch version of the same model.
 
-    python scripts/tta.py [--impl fused|torch|both] [--max_steps 1000] [--target 0.97]
+    python tools/tta.py [--impl fused|torch|both] [--max_steps 1000] [--target 0.97]
 
 Data: synthetic MNIST-shaped digits (arena_amd.data.mnist), no download on the GPU box.
 """
