@@ -32,6 +32,29 @@ def _job_failed(j: Job) -> bool:
     return j.failed > 0 and j.active == 0 and j.failed > j.backoff_limit and j.succeeded == 0
 
 
+def task_jobs_phase(jobs: List[Job]) -> Optional[str]:
+    """Terminal phase of an operator-free PS/worker job from its per-task Jobs, or None while it
+    runs. The ONE rule both the CLI status (:func:`tfjob_from_jobs`) and jobmon's clean-up wait
+    (``runtime.jobmon.wait_tfjob_done``) use:
+
+    * ``Succeeded`` once EVERY worker task Job succeeded (the all-workers rule: a finished
+      worker 0 with other workers still training is still running);
+    * ``Failed`` once any task Job (worker or PS) failed for good (failures past its
+      backoffLimit, nothing active, never succeeded);
+    * None otherwise (including no worker Jobs yet).
+
+    tf-operator's controller source is not vendored in the reference, so whether its v1alpha2
+    condition used this all-workers rule or a chief/worker-0 rule is parity unpinned; the
+    all-workers rule matches what `arena get`/`list` in the reference's docs show for finished
+    distributed jobs (docs/userguide/3-tfjob-distributed.md:56-77)."""
+    workers = [j for j in jobs if j.meta.labels.get("tf-replica-type") == "worker"]
+    if workers and all(j.succeeded > 0 for j in workers):
+        return "Succeeded"
+    if any(_job_failed(j) for j in jobs):
+        return "Failed"
+    return None
+
+
 def tfjob_from_jobs(release: str, namespace: str, jobs: List[Job], pods) -> Optional[TFJob]:
     """The TFJob status tf-operator would report, computed from the per-task Jobs."""
     if not jobs:
@@ -45,11 +68,9 @@ def tfjob_from_jobs(release: str, namespace: str, jobs: List[Job], pods) -> Opti
         tf.replicas[key] = tf.replicas.get(key, 0) + 1
     starts = [j.start_time for j in jobs if j.start_time]
     tf.start_time = min(starts) if starts else None
-    workers = [j for j in jobs if j.meta.labels.get("tf-replica-type") == "worker"]
-    if workers and all(j.succeeded > 0 for j in workers):
-        tf.conditions.append(Condition("Succeeded", "True"))
-    elif any(_job_failed(j) for j in jobs):
-        tf.conditions.append(Condition("Failed", "True"))
+    phase = task_jobs_phase(jobs)
+    if phase is not None:
+        tf.conditions.append(Condition(phase, "True"))
     elif any(p.phase == POD_RUNNING for p in pods):
         tf.conditions.append(Condition("Running", "True"))
     else:

@@ -105,7 +105,10 @@ def _task_jobs(backend, namespace, release):
 
 def wait_tfjob_done(backend, namespace, release, duration_s=float("inf"), tick_s=5.0,
                     clock=time.monotonic, sleep=time.sleep) -> str:
-    """'Succeeded' once every worker task Job succeeded, 'Failed' once any task Job failed."""
+    """The job's terminal phase by the same rule as its CLI status
+    (``arena_amd.jobs.tensorflow.task_jobs_phase``: Succeeded once EVERY worker task Job
+    succeeded, Failed once any task Job failed for good)."""
+    from ..jobs.tensorflow import task_jobs_phase
     result = {}
 
     def check():
@@ -113,16 +116,10 @@ def wait_tfjob_done(backend, namespace, release, duration_s=float("inf"), tick_s
             jobs = _task_jobs(backend, namespace, release)
         except Exception as e:  # noqa: BLE001 - API hiccup: keep waiting
             raise RuntimeError(NEED_WAIT) from e
-        workers = [j for j in jobs if j.meta.labels.get("tf-replica-type") == "worker"]
-        if not workers:
+        phase = task_jobs_phase(jobs)
+        if phase is None:
             raise RuntimeError(NEED_WAIT)
-        if all(j.succeeded > 0 for j in workers):
-            result["phase"] = "Succeeded"
-            return
-        if any(j.failed > j.backoff_limit and j.active == 0 and j.succeeded == 0 for j in jobs):
-            result["phase"] = "Failed"
-            return
-        raise RuntimeError(NEED_WAIT)
+        result["phase"] = phase
 
     try:
         retry_during(duration_s, tick_s, check, clock=clock, sleep=sleep)

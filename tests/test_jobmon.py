@@ -127,3 +127,31 @@ def test_tfjob_clean_pod_policy(outcome):
     assert fake.get_job("default", "d-tfjob-ps-0") is None
     assert not [p for p in fake.list_pods("default") if p.name.startswith("d-tfjob-ps-0-")]
     assert fake.get_job("default", "d-tfjob-worker-0") is not None
+
+
+def test_tfjob_status_rule_shared_by_cli_and_jobmon():
+    """Worker 0 finished while worker 1 still trains: the job is RUNNING for `arena list` and
+    not finished for jobmon (one rule, arena_amd.jobs.tensorflow.task_jobs_phase)."""
+    from arena_amd.jobs.tensorflow import task_jobs_phase
+    fake = FakeBackend([make_node("n", "10.0.0.1", 8)])
+    assert arena(["submit", "tf", "--name", "d", "--workers", "2", "--ps", "1", "--gpus", "1",
+                  "--image", "i", "python", "t.py"], backend=fake, out=io.StringIO()) == 0
+    fake.schedule()
+
+    def task(t):
+        return next(p.name for p in fake.list_pods("default") if p.name.rsplit("-", 1)[0] == t)
+
+    for t in ("d-tfjob-ps-0", "d-tfjob-worker-0", "d-tfjob-worker-1"):
+        fake.set_phase("default", task(t), "Running")
+    fake.set_phase("default", task("d-tfjob-worker-0"), "Succeeded")
+    jobs = fake.list_jobs("default", {"release": "d", "app": "tfjob"})
+    assert task_jobs_phase(jobs) is None
+    out = io.StringIO()
+    assert arena(["list"], backend=fake, out=out) == 0
+    assert out.getvalue().splitlines()[1].split()[1] == "RUNNING"
+    fake.set_phase("default", task("d-tfjob-worker-1"), "Succeeded")
+    jobs = fake.list_jobs("default", {"release": "d", "app": "tfjob"})
+    assert task_jobs_phase(jobs) == "Succeeded"
+    out = io.StringIO()
+    assert arena(["list"], backend=fake, out=out) == 0
+    assert out.getvalue().splitlines()[1].split()[1] == "SUCCEEDED"
