@@ -96,6 +96,52 @@ def test_hvd_api_world2_matches_single_process():
     np.testing.assert_allclose(flat0, ref, rtol=1e-5, atol=1e-6)
 
 
+def _hvd_optstate_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from torch import nn
+    from arena_amd.ops.optim import OptimizerGroup
+    from arena_amd.parallel import hvd
+    hvd.init("gloo")
+    try:
+        torch.manual_seed(3)
+        m = nn.Linear(3, 5)
+        o = torch.optim.SGD(m.parameters(), lr=0.1, momentum=0.9)
+        m(torch.ones(2, 3) * (rank + 1)).sum().backward()   # momentum differs per rank
+        o.step()
+
+        class Stateless:       # e.g. ShardedMasterSGD: masters derive from the weights
+            param_groups: list = []
+            state: dict = {}
+
+        hvd.broadcast_optimizer_state(OptimizerGroup(o, Stateless()), root_rank=1)
+        bufs = torch.cat([o.state[p]["momentum_buffer"].reshape(-1) for p in m.parameters()])
+        q.put((rank, bufs.numpy()))
+    finally:
+        hvd.shutdown()
+
+
+@pytest.mark.timeout(120)
+def test_hvd_broadcast_optimizer_state_recurses_groups():
+    """broadcast_optimizer_state walks OptimizerGroup members and skips state-less optimizers:
+    every rank ends with the root's momentum buffers."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hvd_optstate_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0], res[1])
+    # root (rank 1) weight gradient: input 2 per sample x 2 samples -> 4 (rank 0 had 2)
+    assert res[0][0] == 4.0
+
+
 def test_cluster_spec_parsing():
     env = {"TF_CONFIG": '{"cluster":{"ps":["h:1"],"worker":["a:2","b:3"]},'
                         '"task":{"type":"worker","index":1}}'}
