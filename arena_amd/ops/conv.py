@@ -522,10 +522,14 @@ class GradJoin:
 
 WGRAD_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}   # Cout x R*S*C
 WGRAD_TILES.update({v + 4: t for v, t in list(WGRAD_TILES.items())})   # + 4: serial
+# 8..11: the v2 weight-gradient kernel (32x32x16 MFMAs, 128/256-wide tiles, two steps in flight)
+WGRAD_V2 = {8: (128, 128), 9: (256, 128), 10: (128, 256), 11: (256, 256)}
+WGRAD_TILES.update(WGRAD_V2)
 
 
 def wgrad_variants_for(cin: int, cout: int):
-    return [v for v, (bm, bn) in WGRAD_TILES.items() if cout % bm == 0 and cin % bn == 0]
+    return [v for v, (bm, bn) in WGRAD_TILES.items() if cout % bm == 0 and cin % bn == 0
+            and (v < 8 or _V2_ON)]
 
 
 def conv2d_wgrad(x: Tensor, dy: Tensor, kernel: Tuple[int, int], stride: int = 1, pad: int = 0,

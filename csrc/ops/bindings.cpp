@@ -1463,6 +1463,23 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
 
 // dW [Cout, C, R, S] (channels_last) of a convolution with top/left padding and an explicit
 // output size (dy's), c16 mode as conv_fwd_ex.
+// wgrad tile (Cout x R*S*C) of a variant: 0..3 (+4 serial) v1, 8..11 the v2 32x32x16 kernel
+static bool wgrad_tile(int64_t variant, int* tbm, int* tbn) {
+  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
+  static const int bm2[4] = {128, 256, 128, 256}, bn2[4] = {128, 128, 256, 256};
+  if (variant >= 0 && variant <= 7) {
+    *tbm = bm[variant & 3];
+    *tbn = bn[variant & 3];
+    return true;
+  }
+  if (variant >= 8 && variant <= 11) {
+    *tbm = bm2[variant - 8];
+    *tbn = bn2[variant - 8];
+    return true;
+  }
+  return false;
+}
+
 Tensor conv_wgrad_ex(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int64_t pad_h,
                      int64_t pad_w, int64_t variant, int64_t splits_hint, bool out_fp32,
                      double scale, bool c16) {
@@ -1476,10 +1493,9 @@ Tensor conv_wgrad_ex(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, 
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   const int64_t Cout = dy.size(1), Ho = dy.size(2), Wo = dy.size(3);
   TORCH_CHECK(dy.size(0) == N && R >= 1 && S >= 1 && stride >= 1, "conv_wgrad_ex: bad geometry");
-  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  TORCH_CHECK(variant >= 0 && variant <= 7 && Cout % bm[variant & 3] == 0 &&
-                  (c16 ? (C == 16 && S % 4 == 0 && bn[variant & 3] == 64)
-                       : C % bn[variant & 3] == 0),
+  int tbm = 0, tbn = 0;
+  TORCH_CHECK(wgrad_tile(variant, &tbm, &tbn) && Cout % tbm == 0 &&
+                  (c16 ? (variant <= 7 && C == 16 && S % 4 == 0 && tbn == 64) : C % tbn == 0),
               "conv_wgrad_ex: variant ", variant, " does not fit C=", C, " Cout=", Cout);
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad_ex: too many output pixels");
   const int64_t Ktot = R * S * C;
@@ -1574,11 +1590,10 @@ Tensor conv_wgrad(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int
   const int64_t Ho = (H + 2 * pad - R) / stride + 1, Wo = (W + 2 * pad - S) / stride + 1;
   TORCH_CHECK(dy.size(0) == N && dy.size(2) == Ho && dy.size(3) == Wo,
               "conv_wgrad: dy shape does not match the convolution geometry");
-  static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  TORCH_CHECK(variant >= 0 && variant <= 7, "conv_wgrad: variant must be 0..7");
-  TORCH_CHECK(C % bn[variant & 3] == 0 && Cout % bm[variant & 3] == 0, "conv_wgrad: variant ",
-              variant, " needs C % ", bn[variant & 3], " == 0 and Cout % ", bm[variant & 3],
-              " == 0");
+  int tbm = 0, tbn = 0;
+  TORCH_CHECK(wgrad_tile(variant, &tbm, &tbn), "conv_wgrad: variant must be 0..11");
+  TORCH_CHECK(C % tbn == 0 && Cout % tbm == 0, "conv_wgrad: variant ", variant, " needs C % ",
+              tbn, " == 0 and Cout % ", tbm, " == 0");
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad: too many output pixels");
   const int64_t Ktot = R * S * C;
   const int splits = arena_conv_wgrad_splits((int)N, (int)Ho, (int)Wo, (int)Cout, (int)Ktot,

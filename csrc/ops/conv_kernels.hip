@@ -2183,6 +2183,223 @@ FastDiv make_fastdiv(uint32_t d) {
   return f;
 }
 
+// ------------------------------------------------------------------------------------------------
+// Backward-weight v2 (variants 8..11): 32x32x16 MFMAs on 128/256-wide tiles, two K steps... the
+// same split-K slab scheme as v1, the same pixel-major staging by LDS-DMA, but the fragments of
+// the 32x32x16 operands: lane l of a 16-lane group g needs channel l & 31 of pixels
+// 8 (l >> 5) + 0..7, i.e. two ds_read_b64_tr_b16 per fragment whose 4-row x 16-column blocks are
+// rows 8 (g >> 1) + 4 h + q and columns 16 (g & 1) + 4 p (lane 4q + p of the group). A 32-lane
+// half then reads 4 pixel rows x 64 bytes, so the image permutes 64-byte granules per row
+// (16-byte chunk c -> c ^ 4 (row & 3)): the 4 rows land on 4 distinct granules of the 256-byte
+// bank row (rows need >= 256 bytes: tiles of >= 128 channels). The permutation is applied on the
+// LDS-DMA source address and undone on the read, as everywhere in this file.
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ int wswz2(int row) { return 4 * (row & 3); }
+
+template <int BM, int BN, int NWM, int NWN, int NBUF>
+__device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
+  constexpr int NT = 64 * NWM * NWN;
+  constexpr int RA = BM * 2, RBB = BN * 2;        // row bytes of the dY and X images
+  constexpr int CA = RA / 16, CB = RBB / 16;
+  constexpr int kPix = 64;
+  constexpr int AI = kPix * CA / NT, BI = kPix * CB / NT;
+  constexpr int kBuf = kPix * (RA + RBB);
+  constexpr int WM = BM / NWM, WN = BN / NWN, MI = WM / 32, NI = WN / 32;
+  static_assert(CA >= 16 && CB >= 16, "the 64-byte granule permutation needs >= 256-byte rows");
+  static_assert(AI >= 1 && BI >= 1 && MI >= 1 && NI >= 1, "tile too small for the wave grid");
+  static_assert(AI * NT == kPix * CA && BI * NT == kPix * CB, "staging slots must cover the tile");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles = a.m_tiles * a.n_tiles;
+  const int nwg = tiles * a.splits;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = lin / tiles, t2 = lin - split * tiles;
+  const int mt = t2 / a.n_tiles, nt = t2 - mt * a.n_tiles;
+  const int co0 = mt * BM, kk0 = nt * BN;
+  const int tap = kk0 / a.C, ci0 = kk0 - tap * a.C;
+  const int rr = tap / a.S, ss = tap - rr * a.S;
+  const int step0 = split * a.sps;
+  const int nsteps = min(a.sps, (a.M + kPix - 1) / kPix - step0);
+
+  constexpr int RPI_A = 64 / CA, RPI_B = 64 / CB;   // rows per wave-instruction (1 KB)
+  const int a_row_l = lane / CA, a_pos = lane % CA;
+  const int b_row_l = lane / CB, b_pos = lane % CB;
+  constexpr uint32_t kOOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t dyr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.dy, (short)0, a.dybytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  uint32_t a_voff[AI], b_voff[BI];
+#pragma unroll
+  for (int i = 0; i < AI; ++i) {
+    const int row = (wave * AI + i) * RPI_A + a_row_l;
+    a_voff[i] = (uint32_t)((row * a.Cout + co0 + (a_pos ^ wswz2(row)) * 8) * 2);
+  }
+#pragma unroll
+  for (int i = 0; i < BI; ++i) {
+    const int row = (wave * BI + i) * RPI_B + b_row_l;
+    b_voff[i] = (uint32_t)((row * a.C + ci0 + (b_pos ^ wswz2(row)) * 8) * 2);
+  }
+
+  auto stage = [&](int step, int buf) {
+    uint8_t* base = lds + buf * kBuf;
+    const int p0 = (step0 + step) * kPix;
+    const bool full = p0 + kPix <= a.M;
+#pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int row = (wave * AI + i) * RPI_A + a_row_l;
+      const uint32_t vo = (full || p0 + row < a.M) ? a_voff[i] : kOOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (lds_ptr_t)(base + (wave * AI + i) * 1024), 16,
+                                               vo, p0 * a.Cout * 2, 0, 0);
+    }
+    uint8_t* bb = base + kPix * RA;
+    if (a.aff) {
+#pragma unroll
+      for (int i = 0; i < BI; ++i) {
+        const int row = (wave * BI + i) * RPI_B + b_row_l;
+        const uint32_t vo = (full || p0 + row < a.M) ? b_voff[i] : kOOB;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(bb + (wave * BI + i) * 1024), 16,
+                                                 vo, p0 * a.C * 2, 0, 0);
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = (wave * BI + i) * RPI_B + b_row_l;
+      const int m = p0 + row;
+      uint32_t vo = kOOB;
+      if (m < a.M) {
+        const int n = (int)fdiv((uint32_t)m, a.div_hw);
+        const int rem = m - n * a.Ho * a.Wo;
+        const int ho = (int)fdiv((uint32_t)rem, a.div_w);
+        const int wo = rem - ho * a.Wo;
+        const int cch = b_pos ^ wswz2(row);
+        const int hi = ho * a.stride - a.pad + rr;
+        const int wi = wo * a.stride - a.pad_w + ss;
+        if ((unsigned)hi < (unsigned)a.H && (unsigned)wi < (unsigned)a.W)
+          vo = (uint32_t)((((n * a.H + hi) * a.W + wi) * a.C + ci0 + cch * 8) * 2);
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (lds_ptr_t)(bb + (wave * BI + i) * 1024), 16, vo,
+                                               0, 0, 0);
+    }
+  };
+
+  f32x16v acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int wm = wave / NWN, wn = wave % NWN;
+  const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
+
+  auto compute = [&](int buf) {
+    const uint8_t* abuf = lds + buf * kBuf;
+    const uint8_t* bbuf = abuf + kPix * RA;
+#pragma unroll
+    for (int kk = 0; kk < 4; ++kk) {   // 16 pixels per 32x32x16 MFMA
+      bf16x8 af[MI], bfr[NI];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = kk * 16 + 8 * (g >> 1) + 4 * h + qq;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int byte = 2 * (wm * WM + i * 32 + 16 * (g & 1) + 4 * pp);
+          const int off = row * RA + (((byte >> 4) ^ wswz2(row)) << 4) + (byte & 15);
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(abuf + off));
+          af[i][4 * h + 0] = v[0]; af[i][4 * h + 1] = v[1];
+          af[i][4 * h + 2] = v[2]; af[i][4 * h + 3] = v[3];
+        }
+#pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int byte = 2 * (wn * WN + j * 32 + 16 * (g & 1) + 4 * pp);
+          const int off = row * RBB + (((byte >> 4) ^ wswz2(row)) << 4) + (byte & 15);
+          const s16x4 v = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s4_t)(bbuf + off));
+          bfr[j][4 * h + 0] = v[0]; bfr[j][4 * h + 1] = v[1];
+          bfr[j][4 * h + 2] = v[2]; bfr[j][4 * h + 3] = v[3];
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (nsteps > 0) {
+    constexpr int S = NBUF - 1;
+    constexpr int kLps = AI + BI;
+#pragma unroll
+    for (int i = 0; i < S; ++i)
+      if (i < nsteps) stage(i, i);
+    if (nsteps >= S)
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * kLps) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    int cur = 0;
+    for (int t = 0; t < nsteps; ++t) {
+      if (t + S < nsteps) stage(t + S, cur == 0 ? NBUF - 1 : cur - 1);
+      compute(cur);
+      if (t + S < nsteps)
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((S - 1) * kLps) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      cur = cur == NBUF - 1 ? 0 : cur + 1;
+    }
+  }
+
+  // D[row = co][col = k column]: lane holds column (lane & 31), rows (r & 3) + 8 (r >> 2) +
+  // 4 (lane >> 5): 32 consecutive floats per half-wave store
+  float* slab = a.ws + (size_t)split * a.Cout * a.Ktot;
+  const int hh = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j) {
+      const int col = kk0 + wn * WN + j * 32 + (lane & 31);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int co = co0 + wm * WM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * hh;
+        slab[(size_t)co * a.Ktot + col] = acc[i][j][r];
+      }
+    }
+}
+
+template <int BM, int BN, int NWM, int NWN, int NBUF>
+__global__ __launch_bounds__(64 * NWM * NWN) void conv_wgrad2_kernel(WgradArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  conv_wgrad2_body<BM, BN, NWM, NWN, NBUF>(a);
+#endif
+}
+
+// v2 wgrad variant table (variant 8 + i): BM x BN (Cout x R*S*C), waves, stage buffers
+constexpr int kWg2Tiles[4][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}};
+
+template <int BM, int BN, int NWM, int NWN, int NBUF>
+hipError_t launch_wgrad2(WgradArgs a, int splits_hint, hipStream_t st) {
+  a.m_tiles = a.Cout / BM;
+  a.n_tiles = a.Ktot / BN;
+  const int tiles = a.m_tiles * a.n_tiles;
+  const int total = (a.M + 63) / 64;
+  int splits = splits_hint > 0 ? splits_hint : std::max(1, (1024 + tiles / 2) / tiles);
+  splits = std::min(splits, total);
+  a.sps = (total + splits - 1) / splits;
+  a.splits = (total + a.sps - 1) / a.sps;
+  hipLaunchKernelGGL((conv_wgrad2_kernel<BM, BN, NWM, NWN, NBUF>), dim3(tiles * a.splits),
+                     dim3(64 * NWM * NWN), 0, st, a);
+  return hipGetLastError();
+}
+
 template <int BM, int BN>
 hipError_t launch_wgrad(WgradArgs a, int splits_hint, bool serial, hipStream_t st) {
   a.m_tiles = a.Cout / BM;
@@ -2212,8 +2429,10 @@ extern "C" {
 int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int variant,
                             int splits_hint) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (variant < 0 || variant > 7) return -1;
-  const int tiles = (Cout / bm[variant & 3]) * (Ktot / bn[variant & 3]);
+  if (variant < 0 || variant > 11) return -1;
+  const int tbm = variant >= 8 ? kWg2Tiles[variant - 8][0] : bm[variant & 3];
+  const int tbn = variant >= 8 ? kWg2Tiles[variant - 8][1] : bn[variant & 3];
+  const int tiles = (Cout / tbm) * (Ktot / tbn);
   const long long M = (long long)N * Ho * Wo;
   const int total = (int)((M + 63) / 64);
   int splits = splits_hint > 0 ? splits_hint : std::max(1, (1024 + tiles / 2) / tiles);
@@ -2231,11 +2450,15 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
                                int stride, int pad_h, int pad_w, int Ho, int Wo, int c16,
                                int variant, int splits_hint, float scale, hipStream_t st) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (variant < 0 || variant > 7) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 11) return hipErrorInvalidValue;
+  const bool v2 = variant >= 8;
   const int tv = variant & 3;
-  const bool serial = variant >= 4;
-  if (c16 ? (C != 16 || S % 4 || bn[tv] != 64) : (C % bn[tv] != 0)) return hipErrorInvalidValue;
-  if (Cout % bm[tv] || N <= 0 || stride <= 0) return hipErrorInvalidValue;
+  const bool serial = !v2 && variant >= 4;
+  const int tbm = v2 ? kWg2Tiles[variant - 8][0] : bm[tv];
+  const int tbn = v2 ? kWg2Tiles[variant - 8][1] : bn[tv];
+  if (v2 && c16) return hipErrorInvalidValue;
+  if (c16 ? (C != 16 || S % 4 || tbn != 64) : (C % tbn != 0)) return hipErrorInvalidValue;
+  if (Cout % tbm || N <= 0 || stride <= 0) return hipErrorInvalidValue;
   WgradArgs a{};
   a.x = (const uint16_t*)x;
   a.dy = (const uint16_t*)dy;
@@ -2263,7 +2486,14 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
   a.div_hw = make_fastdiv((uint32_t)(a.Ho * a.Wo));
   a.div_w = make_fastdiv((uint32_t)a.Wo);
   hipError_t e;
-  switch (tv) {
+  if (v2) {
+    switch (variant - 8) {
+      case 0: e = launch_wgrad2<128, 128, 2, 2, 2>(a, splits_hint, st); break;
+      case 1: e = launch_wgrad2<256, 128, 4, 2, 2>(a, splits_hint, st); break;
+      case 2: e = launch_wgrad2<128, 256, 2, 4, 2>(a, splits_hint, st); break;
+      default: e = launch_wgrad2<256, 256, 2, 4, 2>(a, splits_hint, st); break;
+    }
+  } else switch (tv) {
     case 0: e = launch_wgrad<128, 128>(a, splits_hint, serial, st); break;
     case 1: e = launch_wgrad<128, 64>(a, splits_hint, serial, st); break;
     case 2: e = launch_wgrad<64, 128>(a, splits_hint, serial, st); break;

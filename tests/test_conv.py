@@ -176,12 +176,45 @@ def test_conv_v2_matches_fp32(shape):
         assert torch.equal(a, b), v
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(3, 128, 7, 7, 128, 1, 1), (2, 256, 7, 7, 256, 3, 1),
+                                   (4, 128, 14, 14, 256, 3, 2), (2, 256, 9, 9, 512, 1, 1),
+                                   (3, 256, 5, 7, 128, 3, 1)])
+def test_conv_wgrad_v2_matches_fp32(shape):
+    """v2 weight-gradient kernel (32x32x16 MFMA, transposed fragment reads of the granule-permuted
+    pixel-major images): fp32-close to torch, bit-reproducible, every split count."""
+    from arena_amd.ops import _ext
+    _ext.load()
+    n, cin, h, w, cout, k, st = shape
+    pad = k // 2
+    x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=11)
+    ho, wo = conv.out_hw(h, w, k, k, st, pad)
+    dy = torch.randn(n, cout, ho, wo, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    _, dw_ref, _ = torch.ops.aten.convolution_backward(
+        dy.float(), x.float(), wt.float(), None, [st, st], [pad, pad], [1, 1], False, [0, 0], 1,
+        [False, True, False])
+    vs = [v for v in conv.wgrad_variants_for(cin, cout) if v in conv.WGRAD_V2]
+    assert vs
+    for v in vs:
+        for sp in (1, 2, 5, 0):
+            dw = conv.conv2d_wgrad(x, dy, (k, k), st, pad, v, sp, out_dtype=torch.float32)
+            assert _rel(dw, dw_ref) < 5e-3, (v, sp, _rel(dw, dw_ref))
+            assert torch.equal(dw, conv.conv2d_wgrad(x, dy, (k, k), st, pad, v, sp,
+                                                     out_dtype=torch.float32))
+        dwb = conv.conv2d_wgrad(x, dy, (k, k), st, pad, v, 0)
+        assert dwb.dtype == torch.bfloat16 and _rel(dwb, dw_ref) < 1e-2
+
+
 def test_v2_variants_are_forward_and_dgrad_only():
     assert conv.v2_variants_for(64) == [conv.V2 + 3]
     assert set(conv.v2_variants_for(256)) == set(conv.V2_TILES)
     assert all(conv.tiles_per_block(v) == 1 and conv.split_of(v) == 1 for v in conv.V2_TILES)
     assert not set(conv.variants_for(256)) & set(conv.V2_TILES)   # strided dgrad phases: v1
     assert conv.persist_variants_for(128 * 56 * 56, 256, list(conv.V2_TILES)) == []
+    # v2 weight gradients need >= 128-channel tiles on both sides
+    assert not set(conv.wgrad_variants_for(64, 256)) & set(conv.WGRAD_V2)
+    assert set(conv.wgrad_variants_for(256, 256)) >= set(conv.WGRAD_V2)
 
 
 @pytest.mark.gpu
