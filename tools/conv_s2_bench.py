@@ -17,7 +17,7 @@ import torch.nn.functional as F
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from arena_amd.ops import _ext, conv  # noqa: E402
-from scripts.conv_roofline import resnet50_convs, timeit  # noqa: E402
+from tools.conv_roofline import resnet50_convs, timeit  # noqa: E402
 
 
 def main():
