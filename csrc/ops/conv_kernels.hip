@@ -1366,8 +1366,9 @@ hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
 
 // v2 variant table (code 1024 + index): BM x BN tile, waves NWM x NWN, stage buffers
 constexpr int kV2Base = 4096;   // above every v1 code (split + 16 k, persistent + 256 p <= 1039)
-constexpr int kV2Count = 5;
-constexpr int kV2Tiles[kV2Count][2] = {{256, 128}, {256, 256}, {128, 128}, {256, 64}, {128, 256}};
+constexpr int kV2Count = 8;
+constexpr int kV2Tiles[kV2Count][2] = {{256, 128}, {256, 256}, {128, 128}, {256, 64}, {128, 256},
+                                       {128, 64}, {64, 64}, {64, 128}};
 
 hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
   switch (idx) {
@@ -1376,6 +1377,11 @@ hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
     case 2: return launch2_t<128, 128, 2, 2, 2>(a, st);
     case 3: return launch2_t<256, 64, 4, 2, 3>(a, st);
     case 4: return launch2_t<128, 256, 2, 4, 3>(a, st);
+    // 4-wave small tiles: several blocks per CU (48 / 32 / 48 KB of LDS) for the 64-channel
+    // layers, where the 8-wave 256-row tiles leave each SIMD with two waves to hide latency
+    case 5: return launch2_t<128, 64, 2, 2, 2>(a, st);
+    case 6: return launch2_t<64, 64, 2, 2, 2>(a, st);
+    case 7: return launch2_t<64, 128, 2, 2, 2>(a, st);
     default: return hipErrorInvalidValue;
   }
 }

@@ -34,29 +34,50 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
 def trace_overlap(model, opt, x, y, path):
-    """One eager DP step under torch.profiler (ROCm kernel activity): the optimizer kernels
-    (``xgmi_sgd``) that START before the step's last backward kernel ENDS ran concurrently with
-    backward. Writes the kernel timeline (name, start, end in us) to ``path``."""
-    from torch.profiler import ProfilerActivity, profile
+    """One eager DP step with HIP events: a start event on the main stream before the forward,
+    one on the comm stream right after every bucket's optimizer kernel (ShardedMasterSGD:
+    ``xgmi_sgd_*``), and one on the main stream when backward has issued its last kernel. A bucket
+    whose completion time is earlier than the backward's end ran concurrently with backward.
+    Writes the per-bucket times (ms after the forward's start) to ``path``."""
     from arena_amd.examples import cnn_bench
+    from arena_amd.parallel.zero import ShardedMasterSGD
+    assert isinstance(opt, ShardedMasterSGD)
+    marks = []
+    orig = opt._launch
+
+    def launch(b):
+        orig(b)
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(opt.stream)
+        marks.append((len(marks), b.dtype, b.end - b.start, e))
+
+    opt._launch = launch
     torch.cuda.synchronize()
-    with profile(activities=[ProfilerActivity.CUDA]) as prof:
-        cnn_bench.train_step(model, opt, x, y, torch.bfloat16)
-        torch.cuda.synchronize()
-    ks = [(e.name, e.time_range.start, e.time_range.end) for e in prof.events()
-          if e.device_type.name == "CUDA"]
-    ks.sort(key=lambda k: k[1])
-    opt_k = [k for k in ks if "xgmi_sgd" in k[0]]
-    other = [k for k in ks if "xgmi_sgd" not in k[0] and "copy" not in k[0].lower()]
-    last_bwd_end = max(k[2] for k in other) if other else 0
-    early = [k for k in opt_k if k[1] < last_bwd_end]
+    start = torch.cuda.Event(enable_timing=True)
+    bwd_end = torch.cuda.Event(enable_timing=True)
+    step_end = torch.cuda.Event(enable_timing=True)
+    start.record()
+    with torch.autocast("cuda", dtype=torch.bfloat16, cache_enabled=False):
+        loss = torch.nn.functional.cross_entropy(model(x), y)
+    opt.zero_grad(set_to_none=True)
+    loss.backward()
+    bwd_end.record()
+    opt.step()
+    step_end.record()
+    torch.cuda.synchronize()
+    opt._launch = orig
+    t_bwd = start.elapsed_time(bwd_end)
+    rows = [{"bucket": i, "dtype": str(dt), "elems": n, "done_ms": round(start.elapsed_time(e), 3)}
+            for i, dt, n, e in marks]
     with open(path, "w") as f:
-        for k in ks:
-            f.write(json.dumps({"name": k[0][:120], "start_us": k[1], "end_us": k[2]}) + "\n")
-    return {"optimizer_kernels": len(opt_k), "started_before_backward_end": len(early),
-            "kernels": len(ks),
-            "first_opt_start_vs_last_bwd_end_us": (round(opt_k[0][1] - last_bwd_end, 1)
-                                                  if opt_k else None)}
+        for r in rows:
+            f.write(json.dumps(r) + "\n")
+        f.write(json.dumps({"backward_end_ms": round(t_bwd, 3),
+                            "step_end_ms": round(start.elapsed_time(step_end), 3)}) + "\n")
+    return {"buckets": len(rows), "finished_before_backward_end":
+            sum(1 for r in rows if r["done_ms"] < t_bwd),
+            "backward_end_ms": round(t_bwd, 3),
+            "bucket_done_ms": [r["done_ms"] for r in rows]}
 
 
 def rank_main(rank, world, port, a, q):
@@ -124,9 +145,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--graph", type=int, default=0, help="1: replay the whole step as a hipGraph")
-    ap.add_argument("--trace", default="", help="rank 0 writes one eager step's kernel timeline "
-                    "(torch.profiler) here and reports how many optimizer kernels overlapped "
-                    "backward")
+    ap.add_argument("--trace", default="", help="rank 0 times one eager step with HIP events "
+                    "(per-bucket optimizer-kernel completion vs the end of backward), writes them "
+                    "here and reports how many buckets finished while backward was running")
     ap.add_argument("--master_weights", choices=["auto", "on", "off"], default="auto",
                     help="auto/on: bf16 weights + ShardedMasterSGD (xGMI reduce-scatter / SGD / "
                          "all-gather); off: fp32 weights + DistributedOptimizer buckets")
