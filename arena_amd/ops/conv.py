@@ -46,7 +46,9 @@ TILES.update({v + 256 * p: TILES[v] for v in range(16) for p in PERSIST})
 # persistent.
 V2 = 4096
 V2_TILES = {V2 + 0: (256, 128), V2 + 1: (256, 256), V2 + 2: (128, 128), V2 + 3: (256, 64),
-            V2 + 4: (128, 256), V2 + 5: (128, 64), V2 + 6: (64, 64), V2 + 7: (64, 128)}
+            V2 + 4: (128, 256), V2 + 5: (128, 64), V2 + 6: (64, 64), V2 + 7: (64, 128),
+            # serial single-buffer forms with wave-row epilogue bands: 4 waves per SIMD
+            V2 + 8: (128, 128), V2 + 9: (128, 64), V2 + 10: (64, 128), V2 + 11: (64, 64)}
 TILES.update(V2_TILES)
 _V2_ON = os.environ.get("ARENA_CONV_V2", "1") != "0"
 _CUS = 256

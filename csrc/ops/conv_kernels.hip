@@ -1047,7 +1047,7 @@ typedef float f32x16v __attribute__((ext_vector_type(16)));
 
 constexpr int kLdsMax = 160 * 1024;
 
-template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI>
+template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false>
 struct Conv2Geo {
   static constexpr int NT = 64 * NWM * NWN;
   static constexpr int WM = BM / NWM, WN = BN / NWN;
@@ -1058,7 +1058,9 @@ struct Conv2Geo {
   static constexpr int SL = BN / 4;       // float4 slots per tile row
   static constexpr int RG = NT / SL;      // row groups of the statistics passes
   static constexpr int kRed = EPI == 1 ? (RG * BN + BN) * 4 : 0;
-  static constexpr int EH = BM * BN * 4 + kRed <= kLdsMax - 1024 ? BM : WM;   // rows per band
+  // rows per epilogue band: the whole tile when it fits, else one wave-row; BAND forces the
+  // wave-row bands to keep the block's LDS small (the high-occupancy serial variants)
+  static constexpr int EH = !BAND && BM * BN * 4 + kRed <= kLdsMax - 1024 ? BM : WM;
   static constexpr int kEpi = EH * BN * 4 + kRed;
   static constexpr int kLds = kStage > kEpi ? kStage : kEpi;
   static_assert(MI >= 1 && NI >= 1 && AI >= 1 && BI >= 1, "tile too small for the wave grid");
@@ -1067,9 +1069,9 @@ struct Conv2Geo {
   static_assert(kLds <= kLdsMax, "LDS budget");
 };
 
-template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI>
+template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false>
 __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
-  using G = Conv2Geo<BM, BN, NWM, NWN, NBUF, EPI>;
+  using G = Conv2Geo<BM, BN, NWM, NWN, NBUF, EPI, BAND>;
   constexpr int NT = G::NT, WM = G::WM, WN = G::WN, MI = G::MI, NI = G::NI;
   constexpr int AI = G::AI, BI = G::BI, kBufBytes = G::kBufBytes;
   constexpr int SL = G::SL, RG = G::RG, EH = G::EH;
@@ -1191,7 +1193,21 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
   };
 
   // ---- K loop: S = NBUF - 1 steps in flight ----
-  {
+  if constexpr (NBUF == 1) {
+    // serial form (high occupancy: several blocks per CU overlap each other's staging)
+    if (T > 0) stage(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < T; ++t) {
+      compute(0);
+      if (t + 1 < T) {
+        __syncthreads();   // every wave is done reading the buffer: restage it
+        stage(0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
     constexpr int S = NBUF - 1;
     constexpr int kLps = AI + BI;   // LDS-DMA instructions per thread per stage
 #pragma unroll
@@ -1345,7 +1361,17 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv2_kernel(ConvArgs a) {
 #endif
 }
 
-template <int BM, int BN, int NWM, int NWN, int NBUF>
+// serial, wave-row epilogue bands, <= 128 VGPRs: four waves per SIMD (up to four 4-wave blocks
+// per CU by LDS), the structure that wins the streaming-bound layers in v1 (variants 8..11)
+template <int BM, int BN, int EPI>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void conv2_kernel_occ4(ConvArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  conv2_body<BM, BN, 2, 2, 1, EPI, true>(a);
+#endif
+}
+
+template <int BM, int BN, int NWM, int NWN, int NBUF, bool OCC4 = false>
 hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   if (a.c16 || a.mapped || a.bnx != nullptr || a.ksplit != 1 || a.tpb != 1 || a.Cout % BN)
@@ -1355,20 +1381,27 @@ hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
   const bool stats = a.part != nullptr || a.bn_acc != nullptr;
-  if (stats)
+  if constexpr (OCC4) {
+    if (stats)
+      hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 1>), dim3(nwg), dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 0>), dim3(nwg), dim3(256), 0, st, a);
+  } else if (stats) {
     hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 1>), dim3(nwg),
                        dim3(64 * NWM * NWN), 0, st, a);
-  else
+  } else {
     hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 0>), dim3(nwg),
                        dim3(64 * NWM * NWN), 0, st, a);
+  }
   return hipGetLastError();
 }
 
 // v2 variant table (code 1024 + index): BM x BN tile, waves NWM x NWN, stage buffers
 constexpr int kV2Base = 4096;   // above every v1 code (split + 16 k, persistent + 256 p <= 1039)
-constexpr int kV2Count = 8;
+constexpr int kV2Count = 12;
 constexpr int kV2Tiles[kV2Count][2] = {{256, 128}, {256, 256}, {128, 128}, {256, 64}, {128, 256},
-                                       {128, 64}, {64, 64}, {64, 128}};
+                                       {128, 64}, {64, 64}, {64, 128},
+                                       {128, 128}, {128, 64}, {64, 128}, {64, 64}};
 
 hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
   switch (idx) {
@@ -1382,6 +1415,11 @@ hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
     case 5: return launch2_t<128, 64, 2, 2, 2>(a, st);
     case 6: return launch2_t<64, 64, 2, 2, 2>(a, st);
     case 7: return launch2_t<64, 128, 2, 2, 2>(a, st);
+    // serial high-occupancy forms of the 4-wave tiles (conv2_kernel_occ4)
+    case 8: return launch2_t<128, 128, 2, 2, 1, true>(a, st);
+    case 9: return launch2_t<128, 64, 2, 2, 1, true>(a, st);
+    case 10: return launch2_t<64, 128, 2, 2, 1, true>(a, st);
+    case 11: return launch2_t<64, 64, 2, 2, 1, true>(a, st);
     default: return hipErrorInvalidValue;
   }
 }
