@@ -74,7 +74,8 @@ def set_v2(on: bool) -> None:
 
 
 def v2_variants_for(cout: int):
-    """v2 tile variants for ``cout`` output channels (forward / stride-1 backward-data)."""
+    """v2 tile variants for ``cout`` output channels (forward / backward-data, incl. the strided
+    phases)."""
     return [v for v, (_, bn) in V2_TILES.items() if cout % bn == 0] if _V2_ON else []
 
 
@@ -525,7 +526,8 @@ class GradJoin:
 WGRAD_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}   # Cout x R*S*C
 WGRAD_TILES.update({v + 4: t for v, t in list(WGRAD_TILES.items())})   # + 4: serial
 # 8..11: the v2 weight-gradient kernel (32x32x16 MFMAs, 128/256-wide tiles, two steps in flight)
-WGRAD_V2 = {8: (128, 128), 9: (256, 128), 10: (128, 256), 11: (256, 256)}
+WGRAD_V2 = {8: (128, 128), 9: (256, 128), 10: (128, 256), 11: (256, 256),
+            12: (128, 128)}   # 12: serial single-buffer, four waves per SIMD
 WGRAD_TILES.update(WGRAD_V2)
 
 
@@ -706,7 +708,7 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                 fns[("bwd", v)] = (lambda v=v: _time(lambda: conv2d_bwd_data(dy, w, pad, v)))
         else:   # phase decomposition: per-phase heuristic (-1) or one tile for every phase
             hw = (x.shape[2], x.shape[3])
-            for v in [-1] + variants_for(cin):
+            for v in [-1] + variants_for(cin) + v2_variants_for(cin):
                 fns[("bwd", v)] = (lambda v=v: _time(
                     lambda: conv2d_bwd_data_strided(dy, w, hw, stride, pad, v)))
         for c in wg:

@@ -1466,13 +1466,13 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
 // wgrad tile (Cout x R*S*C) of a variant: 0..3 (+4 serial) v1, 8..11 the v2 32x32x16 kernel
 static bool wgrad_tile(int64_t variant, int* tbm, int* tbn) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  static const int bm2[4] = {128, 256, 128, 256}, bn2[4] = {128, 128, 256, 256};
+  static const int bm2[5] = {128, 256, 128, 256, 128}, bn2[5] = {128, 128, 256, 256, 128};
   if (variant >= 0 && variant <= 7) {
     *tbm = bm[variant & 3];
     *tbn = bn[variant & 3];
     return true;
   }
-  if (variant >= 8 && variant <= 11) {
+  if (variant >= 8 && variant <= 12) {
     *tbm = bm2[variant - 8];
     *tbn = bn2[variant - 8];
     return true;
@@ -1591,7 +1591,7 @@ Tensor conv_wgrad(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int
   TORCH_CHECK(dy.size(0) == N && dy.size(2) == Ho && dy.size(3) == Wo,
               "conv_wgrad: dy shape does not match the convolution geometry");
   int tbm = 0, tbn = 0;
-  TORCH_CHECK(wgrad_tile(variant, &tbm, &tbn), "conv_wgrad: variant must be 0..11");
+  TORCH_CHECK(wgrad_tile(variant, &tbm, &tbn), "conv_wgrad: variant must be 0..12");
   TORCH_CHECK(C % tbn == 0 && Cout % tbm == 0, "conv_wgrad: variant ", variant, " needs C % ",
               tbn, " == 0 and Cout % ", tbm, " == 0");
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad: too many output pixels");

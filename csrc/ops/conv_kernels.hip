@@ -1040,8 +1040,8 @@ hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
 // statistics (EPI 1) as column sums over the tile's valid rows -- per-tile partials (mean, M2) or
 // fp64 acc-mode atomics, the formats the v1 kernel emits. Tiles that do not fit LDS at once are
 // processed in bands of one wave-row (EH = WM rows), statistics merged across bands (Chan).
-// Not covered (v1 handles them): c16, mapped outputs (strided dgrad phases), split-K, persistent
-// tiles, EPI 2.
+// Mapped outputs (strided dgrad phases, incl. fill_sib) are stored by the plain epilogue.
+// Not covered (v1 handles them): c16, split-K, persistent tiles, EPI 2.
 // ================================================================================================
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 
@@ -1283,7 +1283,17 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
       const f32x4v lo = *reinterpret_cast<const f32x4v*>(tile + (row * SL + ((2 * cc) ^ (row & 7))) * 4);
       const f32x4v hi = *reinterpret_cast<const f32x4v*>(tile + (row * SL + ((2 * cc + 1) ^ (row & 7))) * 4);
       float v[8] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
-      const size_t off = (size_t)(rbase + row) * a.Cout + n0 + cc * 8;
+      size_t pix = (size_t)(rbase + row);
+      int n = 0, ho = 0, wo = 0;
+      if (EPI == 0 && a.mapped) {   // a strided-dgrad phase: scatter into the full dX image
+        const int m = rbase + row, hw = a.Ho * a.Wo;
+        n = m / hw;
+        const int rem = m - n * hw;
+        ho = rem / a.Wo;
+        wo = rem - ho * a.Wo;
+        pix = ((size_t)n * a.Hy + ho * a.osh + a.ooh) * a.Wy + wo * a.osw + a.oow;
+      }
+      const size_t off = pix * a.Cout + n0 + cc * 8;
       if (EPI == 0 && a.add != nullptr) {
         const uint4 qa = masked_add8(a.add, a.addmask, off);
         const uint32_t u[4] = {qa.x, qa.y, qa.z, qa.w};
@@ -1296,6 +1306,19 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
       *reinterpret_cast<uint4*>(a.y + off) =
           make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
                      pack_bf16x2(v[6], v[7]));
+      if (EPI == 0 && a.fill_sib) {   // 1x1 stride-2 dgrad: the tapless pixels get add (or 0)
+        for (int da = 0; da < a.osh; ++da) {
+          const int hy = ho * a.osh + da;
+          if (hy >= a.Hy) break;
+          for (int db = 0; db < a.osw; ++db) {
+            const int wy = wo * a.osw + db;
+            if ((da == 0 && db == 0) || wy >= a.Wy) continue;
+            const size_t so = (((size_t)n * a.Hy + hy) * a.Wy + wy) * a.Cout + n0 + cc * 8;
+            *reinterpret_cast<uint4*>(a.y + so) =
+                a.add ? masked_add8(a.add, a.addmask, so) : make_uint4(0u, 0u, 0u, 0u);
+          }
+        }
+      }
     }
     if constexpr (EPI == 1) {
       if (nvalid > 0) {
@@ -1374,9 +1397,10 @@ void conv2_kernel_occ4(ConvArgs a) {
 template <int BM, int BN, int NWM, int NWN, int NBUF, bool OCC4 = false>
 hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
-  if (a.c16 || a.mapped || a.bnx != nullptr || a.ksplit != 1 || a.tpb != 1 || a.Cout % BN)
+  if (a.c16 || a.bnx != nullptr || a.ksplit != 1 || a.tpb != 1 || a.Cout % BN)
     return hipErrorInvalidValue;
-  if ((a.part != nullptr || a.bn_acc != nullptr) && a.add != nullptr) return hipErrorInvalidValue;
+  if ((a.part != nullptr || a.bn_acc != nullptr) && (a.add != nullptr || a.mapped))
+    return hipErrorInvalidValue;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
@@ -2376,8 +2400,22 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
     }
   };
 
-  if (nsteps > 0) {
-    constexpr int S = NBUF - 1;
+  if (NBUF == 1 && nsteps > 0) {
+    // serial form (high occupancy): stage, wait, compute, restage
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int t = 0; t < nsteps; ++t) {
+      compute(0);
+      if (t + 1 < nsteps) {
+        __syncthreads();
+        stage(t + 1, 0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else if (nsteps > 0) {
+    constexpr int S = NBUF > 1 ? NBUF - 1 : 1;
     constexpr int kLps = AI + BI;
 #pragma unroll
     for (int i = 0; i < S; ++i)
@@ -2426,10 +2464,19 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv_wgrad2_kernel(WgradArgs a
 #endif
 }
 
-// v2 wgrad variant table (variant 8 + i): BM x BN (Cout x R*S*C), waves, stage buffers
-constexpr int kWg2Tiles[4][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}};
+// serial single-buffer form, <= 128 VGPRs: four waves per SIMD (v1's variants 4..7 structure)
+template <int BM, int BN>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+void conv_wgrad2_kernel_occ4(WgradArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  conv_wgrad2_body<BM, BN, 2, 2, 1>(a);
+#endif
+}
 
-template <int BM, int BN, int NWM, int NWN, int NBUF>
+// v2 wgrad variant table (variant 8 + i): BM x BN (Cout x R*S*C), waves, stage buffers
+constexpr int kWg2Tiles[5][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}, {128, 128}};
+
+template <int BM, int BN, int NWM, int NWN, int NBUF, bool OCC4 = false>
 hipError_t launch_wgrad2(WgradArgs a, int splits_hint, hipStream_t st) {
   a.m_tiles = a.Cout / BM;
   a.n_tiles = a.Ktot / BN;
@@ -2439,8 +2486,12 @@ hipError_t launch_wgrad2(WgradArgs a, int splits_hint, hipStream_t st) {
   splits = std::min(splits, total);
   a.sps = (total + splits - 1) / splits;
   a.splits = (total + a.sps - 1) / a.sps;
-  hipLaunchKernelGGL((conv_wgrad2_kernel<BM, BN, NWM, NWN, NBUF>), dim3(tiles * a.splits),
-                     dim3(64 * NWM * NWN), 0, st, a);
+  if constexpr (OCC4)
+    hipLaunchKernelGGL((conv_wgrad2_kernel_occ4<BM, BN>), dim3(tiles * a.splits), dim3(256), 0, st,
+                       a);
+  else
+    hipLaunchKernelGGL((conv_wgrad2_kernel<BM, BN, NWM, NWN, NBUF>), dim3(tiles * a.splits),
+                       dim3(64 * NWM * NWN), 0, st, a);
   return hipGetLastError();
 }
 
@@ -2473,7 +2524,7 @@ extern "C" {
 int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int variant,
                             int splits_hint) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (variant < 0 || variant > 11) return -1;
+  if (variant < 0 || variant > 12) return -1;
   const int tbm = variant >= 8 ? kWg2Tiles[variant - 8][0] : bm[variant & 3];
   const int tbn = variant >= 8 ? kWg2Tiles[variant - 8][1] : bn[variant & 3];
   const int tiles = (Cout / tbm) * (Ktot / tbn);
@@ -2494,7 +2545,7 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
                                int stride, int pad_h, int pad_w, int Ho, int Wo, int c16,
                                int variant, int splits_hint, float scale, hipStream_t st) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (variant < 0 || variant > 11) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 12) return hipErrorInvalidValue;
   const bool v2 = variant >= 8;
   const int tv = variant & 3;
   const bool serial = !v2 && variant >= 4;
@@ -2535,7 +2586,8 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
       case 0: e = launch_wgrad2<128, 128, 2, 2, 2>(a, splits_hint, st); break;
       case 1: e = launch_wgrad2<256, 128, 4, 2, 2>(a, splits_hint, st); break;
       case 2: e = launch_wgrad2<128, 256, 2, 4, 2>(a, splits_hint, st); break;
-      default: e = launch_wgrad2<256, 256, 2, 4, 2>(a, splits_hint, st); break;
+      case 3: e = launch_wgrad2<256, 256, 2, 4, 2>(a, splits_hint, st); break;
+      default: e = launch_wgrad2<128, 128, 2, 2, 1, true>(a, splits_hint, st); break;
     }
   } else switch (tv) {
     case 0: e = launch_wgrad<128, 128>(a, splits_hint, serial, st); break;

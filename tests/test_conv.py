@@ -210,7 +210,7 @@ def test_v2_variants_are_forward_and_dgrad_only():
     assert set(conv.v2_variants_for(64)) == {conv.V2 + v for v in (3, 5, 6, 9, 11)}
     assert set(conv.v2_variants_for(256)) == set(conv.V2_TILES)
     assert all(conv.tiles_per_block(v) == 1 and conv.split_of(v) == 1 for v in conv.V2_TILES)
-    assert not set(conv.variants_for(256)) & set(conv.V2_TILES)   # strided dgrad phases: v1
+    assert not set(conv.variants_for(256)) & set(conv.V2_TILES)   # disjoint code ranges
     assert conv.persist_variants_for(128 * 56 * 56, 256, list(conv.V2_TILES)) == []
     # v2 weight gradients need >= 128-channel tiles on both sides
     assert not set(conv.wgrad_variants_for(64, 256)) & set(conv.WGRAD_V2)
@@ -688,6 +688,12 @@ def test_strided_dgrad_phases_match_fp32(k, pad, h, st):
     assert _rel(dxa, dx_ref + addend.float()) < 1e-2
     for v in conv.variants_for(cin):   # every tile variant of the phases
         assert _rel(conv.conv2d_bwd_data_strided(dy, wt, (h, h), st, pad, v), dx_ref) < 1e-2
+    vs2 = conv.v2_variants_for(cin)
+    assert vs2
+    for v in vs2:                      # v2 tiles: the mapped store in their plain epilogue
+        assert _rel(conv.conv2d_bwd_data_strided(dy, wt, (h, h), st, pad, v), dx_ref) < 1e-2, v
+        got = conv.conv2d_bwd_data_strided(dy, wt, (h, h), st, pad, v, addend=addend)
+        assert _rel(got, dx_ref + addend.float()) < 1e-2, v
 
 
 @pytest.mark.gpu
