@@ -160,7 +160,7 @@ class _BNActFn(torch.autograd.Function):
         # the conv consuming y computes this layer's backward partials (ops/conv.py BNGradLink)
         ctx.link = None
         if link is not None and training and x.dtype == torch.bfloat16:
-            link.set_bn(x, mask if relu else None, mean)
+            link.set_bn(x, mask if relu else None, mean, bacc if _FIN_BWD else None)
             ctx.link = link
         # res_out: this BN's residual is another fused BN's output (see ResidualMask);
         # res_in: this BN's output is that residual
@@ -192,13 +192,17 @@ class _BNActFn(torch.autograd.Function):
                   and ctx.join.other() is None and ctx.join.peer_takes_masked())
         to_res = (not masked and ctx.res_out is not None and ctx.has_res and mask is not None
                   and ctx.needs_input_grad[1] and ctx.join is None)
-        acc_b = ctx.bacc.for_backward(x, x.shape[1]) \
-            if (ctx.bacc is not None and not ext and _FIN_BWD) else None
+        ready = bool(ext) and isinstance(ext[0], str)   # ("acc", sums): the conv summed
+        if ready:
+            acc_b, ext = ext[1], None
+        else:
+            acc_b = ctx.bacc.for_backward(x, x.shape[1]) \
+                if (ctx.bacc is not None and not ext and _FIN_BWD) else None
         dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, mask, x, mean, invstd, weight, relu,
                                                      ctx.has_res and not masked and not to_res,
                                                      ctx.affine, ext[0] if ext else None,
                                                      ext[1] if ext else 0, acc_b=acc_b,
-                                                     zero_f=ctx.facc)
+                                                     zero_f=ctx.facc, acc_ready=ready)
         if to_res:
             ctx.res_out.publish(mask)
             dres = dy

@@ -42,8 +42,8 @@ PERSIST = (1, 2, 3, 4)
 TILES.update({v + 256 * p: TILES[v] for v in range(16) for p in PERSIST})
 # 4096 + i: the v2 tile kernel (conv_kernels.hip conv2_body): 32x32x16 MFMAs, 8-wave 256-row
 # tiles (4-wave 128x128), two K steps in flight, epilogue through an fp32 LDS tile. Forward and
-# stride-1 backward-data only (plain, masked addend, BatchNorm statistics); never split or
-# persistent.
+# backward-data (incl. the strided phases): plain, masked addend, BatchNorm statistics, BatchNorm-
+# backward partials or sums (BNGradLink); never split or persistent.
 V2 = 4096
 V2_TILES = {V2 + 0: (256, 128), V2 + 1: (256, 256), V2 + 2: (128, 128), V2 + 3: (256, 64),
             V2 + 4: (128, 256), V2 + 5: (128, 64), V2 + 6: (64, 64), V2 + 7: (64, 128),
@@ -162,7 +162,8 @@ def pick_variant(m: int, cout: int) -> int:
 
 def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int = -1,
                with_stats: bool = False, addend: Tensor | None = None, bn=None,
-               addmask: Tensor | None = None, final: bool = False):
+               addmask: Tensor | None = None, final: bool = False,
+               bn_acc: Tensor | None = None):
     """y = conv2d(x, w) (+ addend) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S].
 
     with_stats: returns (y, (part, rpb)) where part holds per-tile BatchNorm partials of y
@@ -173,7 +174,9 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
     only the addend elements whose bit is set are added (a ReLU'd gradient, see GradJoin).
     bn: (bn_x, bn_mask or None, bn_mean) when y is the gradient of a BatchNorm layer's output:
     returns (y, (part, rpb)) with that BN's backward partials (sum g, sum g (bn_x - mean) per
-    tile, g = y * mask) for its backward, which then skips its reduction pass.
+    tile, g = y * mask) for its backward, which then skips its reduction pass; with ``bn_acc``
+    (that BN's fp64 [2, C] backward sums) the epilogue adds them there instead and returns
+    (y, None).
     final (with with_stats): the statistics come back finished, ``(y, FinishedStats)`` -- the
     epilogue's fp64 atomics + last-tile ticket replace the BN's finalize launch."""
     x = x.contiguous(memory_format=torch.channels_last)
@@ -190,7 +193,9 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
     fin = bool(final and with_stats and bn is None and addend is None)
     out = _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant), bool(with_stats),
                                addend, bx, bm, bmu, addmask if addend is not None else None,
-                               stats_final=fin)
+                               stats_final=fin, bn_acc=bn_acc if bn is not None else None)
+    if bn is not None and bn_acc is not None:
+        return out[0], None          # the sums went into the caller's bn_acc
     if fin:
         from .batchnorm import FinishedStats
         return out[0], FinishedStats(out[1])
@@ -209,23 +214,26 @@ def flip_weight(w: Tensor) -> Tensor:
 
 def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1,
                     addend: Tensor | None = None, bn=None, wflip: Tensor | None = None,
-                    addmask: Tensor | None = None):
+                    addmask: Tensor | None = None, bn_acc: Tensor | None = None):
     """dX (+ addend) of a stride-1 convolution (same spatial size when pad = (R-1)/2).
     With ``bn`` (see conv2d_fwd) returns (dX, (part, rpb)): the backward partials of the
     BatchNorm layer whose output is this convolution's input. ``wflip``: ``flip_weight(w)``
     computed ahead of time (``WeightFlipper``)."""
     r = w.shape[2]
     wf = wflip if wflip is not None else flip_weight(w)
-    return conv2d_fwd(dy, wf, 1, r - 1 - pad, variant, addend=addend, bn=bn, addmask=addmask)
+    return conv2d_fwd(dy, wf, 1, r - 1 - pad, variant, addend=addend, bn=bn, addmask=addmask,
+                      bn_acc=bn_acc)
 
 
-# Off by default: on ResNet-50 bs128 the heavier dgrad epilogue cost more than the reduction pass
-# it saves (15.69 / 15.74 vs 15.37 / 15.53 ms per step, same-process A/B, docs/perf.md).
-_BN_LINKS = os.environ.get("ARENA_BN_LINKS", "0") == "1"
+# On by default since the v2 tiles carry the partials in their coalesced store loop and the plan
+# times the linked backward-data form separately (ConvPlan.bwd_bn): ResNet-50 bs128 12.67 ->
+# 12.22 / 12.32 ms per step (profiles/r4_bn_links_v2_tuned_ab.log). Round 3's v1-only form lost
+# (15.69 vs 15.37 ms): its 128x128 EPI 2 kernel ran at one wave per SIMD.
+_BN_LINKS = os.environ.get("ARENA_BN_LINKS", "1") == "1"
 
 
 def set_bn_links(on: bool) -> None:
-    """Enable/disable BNGradLink fusion (off by default; ARENA_BN_LINKS=1)."""
+    """Enable/disable BNGradLink fusion (on by default; ARENA_BN_LINKS=0 turns it off)."""
     global _BN_LINKS
     _BN_LINKS = bool(on)
 
@@ -239,6 +247,21 @@ _BN_FINAL = os.environ.get("ARENA_BN_FINAL", "1") == "1"
 # memory-side atomic rate, competing with the tile's output stores) cost more than the partial
 # merge + finalize launch they replace (profiles/r3_bn_acc_ab.jsonl, r3_bn_fin_ab.jsonl).
 _ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_ACC_MAX_PAIRS", str(128 << 10)))
+
+
+# the same rule for the dgrad epilogue's BN-backward sums (BNGradLink acc form), separately
+# switchable for A/Bs (ARENA_BN_LINK_ACC_MAX_PAIRS; 0: always per-tile partials + BN finalize)
+_LINK_ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_LINK_ACC_MAX_PAIRS", str(_ACC_MAX_PAIRS)))
+
+
+def set_link_acc_max_pairs(n: int) -> None:
+    global _LINK_ACC_MAX_PAIRS
+    _LINK_ACC_MAX_PAIRS = int(n)
+
+
+def _use_link_acc(m: int, variant: int, c: int) -> bool:
+    bm, tpb = TILES[variant][0], tiles_per_block(variant)
+    return -(-(-(-m // bm)) // tpb) * c <= _LINK_ACC_MAX_PAIRS
 
 
 def set_acc_max_pairs(n: int) -> None:
@@ -410,17 +433,21 @@ class BNGradLink:
     computes the BN backward's per-channel partial sums (sum g, sum g * (x - mean), g = dY *
     ReLU mask) and the BN skips its reduction pass over dY and x. The BN's forward fills
     ``set_bn``; the conv's backward ``publish``es; the BN's backward ``take``s, which checks that
-    it received the very tensor the partials describe (else it runs its own reduction)."""
-    __slots__ = ("x", "mask", "mean", "part", "rpb", "dy_ptr")
+    it received the very tensor the partials describe (else it runs its own reduction).
+
+    With the BN's own backward-sum set (``bacc``, batchnorm._BwdAcc) and few enough (tile,
+    channel) pairs (``_use_acc``), the epilogue adds fp64 sums into that set instead of writing
+    per-tile partials, and the BN's dx pass reads them directly: no reduction, no finalize."""
+    __slots__ = ("x", "mask", "mean", "bacc", "part", "rpb", "acc", "dy_ptr")
 
     def __init__(self):
-        self.x = self.mask = self.mean = self.part = None
+        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = None
         self.rpb = 0
         self.dy_ptr = 0
 
-    def set_bn(self, x: Tensor, mask: Tensor | None, mean: Tensor) -> None:
+    def set_bn(self, x: Tensor, mask: Tensor | None, mean: Tensor, bacc=None) -> None:
         if _BN_LINKS:
-            self.x, self.mask, self.mean = x, mask, mean
+            self.x, self.mask, self.mean, self.bacc = x, mask, mean, bacc
 
     def ready(self) -> bool:
         return self.x is not None
@@ -428,13 +455,19 @@ class BNGradLink:
     def publish(self, part: Tensor, rpb: int, dy: Tensor) -> None:
         self.part, self.rpb, self.dy_ptr = part, int(rpb), dy.data_ptr()
 
+    def publish_acc(self, acc: Tensor, dy: Tensor) -> None:
+        self.acc, self.dy_ptr = acc, dy.data_ptr()
+
     def take(self, dy: Tensor):
-        """(part, rpb) if the partials describe ``dy``, else None. Releases the references."""
+        """(part, rpb) or ("acc", sums) if the link's result describes ``dy``, else None.
+        Releases the references."""
         out = None
-        if self.part is not None and dy.data_ptr() == self.dy_ptr and self.x is not None \
-                and dy.shape == self.x.shape:
-            out = (self.part, self.rpb)
-        self.x = self.mask = self.mean = self.part = None
+        if dy.data_ptr() == self.dy_ptr and self.x is not None and dy.shape == self.x.shape:
+            if self.acc is not None:
+                out = ("acc", self.acc)
+            elif self.part is not None:
+                out = (self.part, self.rpb)
+        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = None
         self.dy_ptr = 0
         return out
 
@@ -585,6 +618,10 @@ class ConvPlan:
     fwd: object = MIOPEN            # MIOPEN or a tile variant
     bwd: object = MIOPEN
     wgrad: object = MIOPEN          # MIOPEN or (variant, splits)
+    # backward-data with the BN-backward partials in its epilogue (BNGradLink; stride 1): timed
+    # in that form, since the extra epilogue reorders the tiles (v1's 128x128 form drops to one
+    # wave per SIMD, 196 VGPRs + 72 AGPRs)
+    bwd_bn: object = MIOPEN
     tuned: bool = False
     times: Dict[str, float] = field(default_factory=dict)
 
@@ -656,7 +693,7 @@ def _best(t: dict, kind: str, n: int):
 
 def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
     key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _PERSIST_ON,
-           _V2_ON)
+           _V2_ON, _BN_LINKS)
     plan = _PLANS.get(key)
     if plan is not None and (plan.tuned or torch.cuda.is_current_stream_capturing()):
         return plan
@@ -675,6 +712,7 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
         plan.bwd = ((pick_variant(x.shape[0] * x.shape[2] * x.shape[3], cin) if stride == 1
                      else -1) if "bwd" in dirs else MIOPEN)
         plan.wgrad = wg[len(wg) // 2] if (wg and "wgrad" in dirs) else MIOPEN
+        plan.bwd_bn = plan.bwd if stride == 1 else MIOPEN
         plan.tuned = mode == "ours"
     else:
         # Only the MFMA kernels are candidates: a captured step with MIOpen convolutions in it
@@ -706,6 +744,14 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
             for v in (variants_for(cin) + v2_variants_for(cin)
                       + split_variants_for(m_in, cin, cout * k[0] * k[1])):
                 fns[("bwd", v)] = (lambda v=v: _time(lambda: conv2d_bwd_data(dy, w, pad, v)))
+            if _BN_LINKS:   # the linked form: a BN input, ReLU bits and mean of x's shape
+                bnx = torch.randn_like(x)
+                bmask = torch.randint(0, 256, (m_in * cin // 8,), device=x.device,
+                                      dtype=torch.uint8)
+                bmean = torch.zeros(cin, device=x.device)
+                for v in variants_for(cin) + v2_variants_for(cin):
+                    fns[("bwdbn", v)] = (lambda v=v: _time(lambda: conv2d_bwd_data(
+                        dy, w, pad, v, bn=(bnx, bmask, bmean))))
         else:   # phase decomposition: per-phase heuristic (-1) or one tile for every phase
             hw = (x.shape[2], x.shape[3])
             for v in [-1] + variants_for(cin) + v2_variants_for(cin):
@@ -730,7 +776,9 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
             # One timing per candidate picks the lucky one among near-equal variants (the
             # choices moved run to run by ~1 % of the step): the 3 fastest of each direction are
             # timed twice more, interleaved, and ranked by their median.
-            finals = {kind: _best(t, kind, 3) for kind in ("fwd", "bwd", "wgrad")}
+            kinds = ("fwd", "bwd", "wgrad") + (
+                ("bwdbn",) if any(k[0] == "bwdbn" for k in fns) else ())
+            finals = {kind: _best(t, kind, 3) for kind in kinds}
             reps = {(kind, c): [t[(kind, c)]] for kind, cs in finals.items() for c in cs}
             for _ in range(2):
                 for key_ in reps:
@@ -739,10 +787,10 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                 t[key_] = sorted(vs)[1]
         finally:
             ext.bn_acc_scratch(False)
-        for kind in ("fwd", "bwd", "wgrad"):
+        for kind in kinds:
             best = min(t[(kind, c)] for c in finals[kind])
             choice = next(c for c in finals[kind] if t[(kind, c)] == best)
-            setattr(plan, kind, choice)
+            setattr(plan, "bwd_bn" if kind == "bwdbn" else kind, choice)
         plan.times = {f"{kd}:{c}": round(v, 1) for (kd, c), v in t.items()}
         plan.tuned = True
     _PLANS[key] = plan
@@ -949,7 +997,7 @@ class _ConvFn(torch.autograd.Function):
             lk = ctx.bn_link
             # the BN partials need the COMPLETE gradient of x: not from a join's first arriver
             use_bn = (lk is not None and plan.bwd != MIOPEN and stride == 1
-                      and plan.bwd < V2 and lk.x.shape == x.shape
+                      and lk.x.shape == x.shape
                       and (join is None or other is not None))
             if plan.bwd == MIOPEN:
                 dx = _miopen_bwd(dy, x, w, stride, pad, [True, False, False])[0]
@@ -959,10 +1007,19 @@ class _ConvFn(torch.autograd.Function):
                 dx = conv2d_bwd_data_strided(dy, w, (x.shape[2], x.shape[3]), stride, pad,
                                              plan.bwd, addend=other)
             elif use_bn:
-                dx, (part, rpb) = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other,
-                                                  bn=(lk.x, lk.mask, lk.mean), wflip=ctx.wflip,
-                                                  addmask=omask)
-                lk.publish(part, rpb, dx)
+                vb = plan.bwd if plan.bwd_bn == MIOPEN else plan.bwd_bn
+                m_in = x.shape[0] * x.shape[2] * x.shape[3]
+                if lk.bacc is not None and _use_link_acc(m_in, vb, x.shape[1]):
+                    acc = lk.bacc.for_backward(x, x.shape[1])
+                    dx, _ = conv2d_bwd_data(dy, w, pad, vb, addend=other,
+                                            bn=(lk.x, lk.mask, lk.mean), wflip=ctx.wflip,
+                                            addmask=omask, bn_acc=acc)
+                    lk.publish_acc(acc, dx)
+                else:
+                    dx, (part, rpb) = conv2d_bwd_data(dy, w, pad, vb, addend=other,
+                                                      bn=(lk.x, lk.mask, lk.mean),
+                                                      wflip=ctx.wflip, addmask=omask)
+                    lk.publish(part, rpb, dx)
             else:
                 dx = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other, wflip=ctx.wflip,
                                      addmask=omask)

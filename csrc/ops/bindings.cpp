@@ -982,7 +982,7 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
 // zero_f (optional): the forward's statistics sums (bn_fwd's acc output), zeroed by the dx pass.
 std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor invstd, OptT gamma,
                            bool relu, bool with_res, bool affine_grads, OptT ext_part,
-                           int64_t ext_rpb, OptT acc_b, OptT zero_f) {
+                           int64_t ext_rpb, OptT acc_b, OptT zero_f, bool acc_ready) {
   const BNGeom g = bn_geom(x, "x");
   bn_same(x, dy, "grad_output");
   if (relu) {
@@ -1030,7 +1030,19 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
   // acc mode: atomics in the reduction + per-channel finalize (the kernel side keeps the
   // partials for layers with many blocks x channels)
   int fin_dx = 0;
-  if (!ext_part.has_value() && g_bn_acc && arena_bn_acc_ok(g.M, (int)g.C)) {
+  // acc_ready: the producing conv's backward-data epilogue already summed into acc_b (BNGradLink
+  // acc mode): no reduction pass, the dx pass derives its coefficients from the sums
+  TORCH_CHECK(!acc_ready || (acc_b.has_value() && !ext_part.has_value()),
+              "bn_bwd: acc_ready needs acc_b and no ext_part");
+  if (acc_ready) {
+    TORCH_CHECK(acc_b->is_cuda() && acc_b->device() == x.device() &&
+                    acc_b->scalar_type() == torch::kFloat64 && acc_b->is_contiguous() &&
+                    acc_b->numel() == 2 * g.C,
+                "acc_b must be a contiguous fp64 tensor of 2*C elements on x's device");
+    acc = *acc_b;
+    fin_dx = 1;
+    ext_nblk = -1;
+  } else if (!ext_part.has_value() && g_bn_acc && arena_bn_acc_ok(g.M, (int)g.C)) {
     if (acc_b.has_value()) {
       TORCH_CHECK(acc_b->is_cuda() && acc_b->device() == x.device() &&
                       acc_b->scalar_type() == torch::kFloat64 && acc_b->is_contiguous() &&
@@ -1222,7 +1234,7 @@ void pool_check(const Tensor& t, const char* name) {
 // the per-tile partials.
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant,
                              bool with_stats, OptT addend, OptT bn_x, OptT bn_mask,
-                             OptT bn_mean, OptT addmask, bool stats_final) {
+                             OptT bn_mean, OptT addmask, bool stats_final, OptT bn_acc) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4,
               "conv_fwd: x and w must be 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16,
@@ -1247,10 +1259,19 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
   const bool fin = with_stats && stats_final;
   TORCH_CHECK(!fin || (!bn_x.has_value() && !addend.has_value() && Cout <= kAccC),
               "conv_fwd: stats_final is forward statistics without an addend");
-  Tensor part = with_stats && !fin
+  // bn_acc (backward-data form): the BN layer's fp64 [2][Cout] backward sums, added into
+  const bool bacc = bn_acc.has_value() && bn_acc->defined();
+  if (bacc) {
+    TORCH_CHECK(bn_x.has_value() && with_stats && !fin, "conv_fwd: bn_acc is the bn_x form's");
+    TORCH_CHECK(bn_acc->is_cuda() && bn_acc->device() == x.device() &&
+                    bn_acc->scalar_type() == torch::kFloat64 && bn_acc->is_contiguous() &&
+                    bn_acc->numel() == 2 * Cout,
+                "conv_fwd: bn_acc must be a contiguous fp64 tensor of 2*Cout elements");
+  }
+  Tensor part = with_stats && !fin && !bacc
                     ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
                     : Tensor();
-  Tensor acc_t = fin ? bn_acc_set(x, Cout) : Tensor();
+  Tensor acc_t = fin ? bn_acc_set(x, Cout) : (bacc ? *bn_acc : Tensor());
   if (addend.has_value()) {
     TORCH_CHECK(addend->sizes() == y.sizes() && addend->scalar_type() == torch::kBFloat16 &&
                     addend->device() == y.device() &&
@@ -1278,7 +1299,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                 "conv_fwd: addmask needs an addend and numel(y) / 8 uint8 bytes");
   }
   check_hip(arena_conv_fwd_ex(x.data_ptr(), w.data_ptr(), y.data_ptr(),
-                              with_stats && !fin ? part.data_ptr<float>() : nullptr,
+                              part.defined() ? part.data_ptr<float>() : nullptr,
                               addend.has_value() ? addend->data_ptr() : nullptr,
                               addmask.has_value() ? addmask->data_ptr<uint8_t>() : nullptr,
                               bn_x.has_value() ? bn_x->data_ptr() : nullptr,
@@ -1288,11 +1309,11 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                               bn_x.has_value() ? bn_mean->data_ptr<float>() : nullptr,
                               (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R, (int)S,
                               (int)stride, (int)pad, (int)pad, 0, 0, nullptr, 0, ks.base,
-                              fin ? acc_t.data_ptr<double>() : nullptr, ks.ks,
+                              acc_t.defined() ? acc_t.data_ptr<double>() : nullptr, ks.ks,
                               ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, ks.tpb,
                               cur_stream()),
             "conv_fwd");
-  if (fin) return {y, acc_t};
+  if (acc_t.defined()) return {y, acc_t};
   if (with_stats) return {y, part};
   return {y};
 }
@@ -1805,12 +1826,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_bwd", &bn_bwd, py::arg("dy"), py::arg("mask"), py::arg("x"), py::arg("mean"),
         py::arg("invstd"), py::arg("gamma"), py::arg("relu"), py::arg("with_res"),
         py::arg("affine_grads"), py::arg("ext_part") = py::none(), py::arg("ext_rpb") = 0,
-        py::arg("acc_b") = py::none(), py::arg("zero_f") = py::none());
+        py::arg("acc_b") = py::none(), py::arg("zero_f") = py::none(),
+        py::arg("acc_ready") = false);
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("variant"), py::arg("with_stats"), py::arg("addend") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
         py::arg("bn_mean") = py::none(), py::arg("addmask") = py::none(),
-        py::arg("stats_final") = false);
+        py::arg("stats_final") = false, py::arg("bn_acc") = py::none());
   m.def("conv_wgrad", &conv_wgrad);
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);

@@ -1359,11 +1359,14 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
   long long rpb;
   long long nb = reduce_blocks(M, C, &rpb);
   const int ns = chan_slices(C);
-  const bool acc_mode = acc != nullptr && ext_nblk <= 0 && nb * C <= g_acc_max_pairs;
+  // ext_nblk < 0: the producer already summed into acc (fin_dx required): no reduction
+  const bool pre = ext_nblk < 0;
+  if (pre && (acc == nullptr || !fin_dx)) return hipErrorInvalidValue;
+  const bool acc_mode = acc != nullptr && (pre || (ext_nblk == 0 && nb * C <= g_acc_max_pairs));
   double* am = acc_mode ? acc : nullptr;
   if (ext_nblk > 0) {
     nb = ext_nblk;
-  } else {
+  } else if (!pre) {
 #define ARENA_BN_RED(TT, R)                                                                  \
   hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, R>), dim3(nb, ns), dim3(kT), 0, stream,     \
                      static_cast<const TT*>(dy), mask, static_cast<const TT*>(x), M, C, rpb, \

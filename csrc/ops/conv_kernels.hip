@@ -776,8 +776,13 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
               r1 += red[h * 2 * BN + c];
               r2 += red[h * 2 * BN + BN + c];
             }
-            a.part[(size_t)mt * 2 * a.Cout + n0 + c] = r1;
-            a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = r2;
+            if (a.bn_acc != nullptr) {   // acc mode: the BN layer's fp64 backward sums
+              unsafeAtomicAdd(a.bn_acc + n0 + c, (double)r1);
+              unsafeAtomicAdd(a.bn_acc + a.Cout + n0 + c, (double)r2);
+            } else {
+              a.part[(size_t)mt * 2 * a.Cout + n0 + c] = r1;
+              a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = r2;
+            }
           }
       }
     }
@@ -1040,8 +1045,10 @@ hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
 // statistics (EPI 1) as column sums over the tile's valid rows -- per-tile partials (mean, M2) or
 // fp64 acc-mode atomics, the formats the v1 kernel emits. Tiles that do not fit LDS at once are
 // processed in bands of one wave-row (EH = WM rows), statistics merged across bands (Chan).
-// Mapped outputs (strided dgrad phases, incl. fill_sib) are stored by the plain epilogue.
-// Not covered (v1 handles them): c16, split-K, persistent tiles, EPI 2.
+// Mapped outputs (strided dgrad phases, incl. fill_sib) are stored by the plain epilogue. EPI 2
+// (BN-backward partials of a dgrad output) rides on the coalesced store loop: each thread owns one
+// 8-channel column chunk, so g and g * (x - mean) accumulate in registers across its rows/bands.
+// Not covered (v1 handles them): c16, split-K, persistent tiles.
 // ================================================================================================
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 
@@ -1255,6 +1262,19 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
         }
   }
   float st_n = 0.f, st_mean = 0.f, st_m2 = 0.f;   // running statistics of channel tid (< BN)
+  // EPI 2: this thread's 8 channels (n0 + (tid % CPR) * 8 + e: the store loop below keeps a
+  // thread on one 16-byte column chunk) -- sum g and sum g * (x - mean) over its rows
+  float e1[EPI == 2 ? 8 : 1], e2[EPI == 2 ? 8 : 1], emu[EPI == 2 ? 8 : 1];
+  if constexpr (EPI == 2) {
+    static_assert(NT % CPR == 0, "EPI 2: a thread's column chunk is fixed");
+    const float* mp = a.bnmean + n0 + (tid % CPR) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      e1[e] = 0.f;
+      e2[e] = 0.f;
+      emu[e] = mp[e];
+    }
+  }
 #pragma unroll
   for (int band = 0; band < BM / EH; ++band) {
     if (band > 0) lds_barrier();   // every reader of the previous band is done
@@ -1294,7 +1314,13 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
         pix = ((size_t)n * a.Hy + ho * a.osh + a.ooh) * a.Wy + wo * a.osw + a.oow;
       }
       const size_t off = pix * a.Cout + n0 + cc * 8;
-      if (EPI == 0 && a.add != nullptr) {
+      uint4 bxq;
+      uint32_t bmk = 0xffu;
+      if constexpr (EPI == 2) {   // the BN layer's input and ReLU bits at the same pixel/channels
+        bxq = *reinterpret_cast<const uint4*>(a.bnx + off);
+        if (a.bnmask) bmk = a.bnmask[(size_t)(rbase + row) * (a.Cout >> 3) + (n0 >> 3) + cc];
+      }
+      if (EPI != 1 && a.add != nullptr) {
         const uint4 qa = masked_add8(a.add, a.addmask, off);
         const uint32_t u[4] = {qa.x, qa.y, qa.z, qa.w};
 #pragma unroll
@@ -1303,9 +1329,23 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
           v[2 * e + 1] += __uint_as_float(u[e] & 0xffff0000u);
         }
       }
-      *reinterpret_cast<uint4*>(a.y + off) =
-          make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]), pack_bf16x2(v[4], v[5]),
-                     pack_bf16x2(v[6], v[7]));
+      const uint4 yq = make_uint4(pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3]),
+                                  pack_bf16x2(v[4], v[5]), pack_bf16x2(v[6], v[7]));
+      *reinterpret_cast<uint4*>(a.y + off) = yq;
+      if constexpr (EPI == 2) {
+        // g = the stored dY (bf16) where the BN output's ReLU passed it
+        const uint32_t yu[4] = {yq.x, yq.y, yq.z, yq.w}, xu[4] = {bxq.x, bxq.y, bxq.z, bxq.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float glo = (bmk >> (2 * e)) & 1u ? __uint_as_float(yu[e] << 16) : 0.f;
+          const float ghi = (bmk >> (2 * e + 1)) & 1u ? __uint_as_float(yu[e] & 0xffff0000u) : 0.f;
+          e1[2 * e] += glo;
+          e1[2 * e + 1] += ghi;
+          e2[2 * e] = fmaf(glo, __uint_as_float(xu[e] << 16) - emu[2 * e], e2[2 * e]);
+          e2[2 * e + 1] =
+              fmaf(ghi, __uint_as_float(xu[e] & 0xffff0000u) - emu[2 * e + 1], e2[2 * e + 1]);
+        }
+      }
       if (EPI == 0 && a.fill_sib) {   // 1x1 stride-2 dgrad: the tapless pixels get add (or 0)
         for (int da = 0; da < a.osh; ++da) {
           const int hy = ho * a.osh + da;
@@ -1362,6 +1402,31 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
       }
     }
   }
+  if constexpr (EPI == 2) {
+    // per-tile BN-backward partials (bn_bwd_reduce's format, rpb = BM): the RG2 row groups'
+    // sums reduced through the (free) epilogue tile, one quantity at a time
+    constexpr int RG2 = NT / CPR;
+    static_assert(EH >= RG2, "EPI 2 reduction fits the epilogue tile");
+    const int cc = tid % CPR, rg = tid / CPR;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      lds_barrier();   // every reader of the last band (or of the previous quantity) is done
+      float* dst = tile + rg * BN + cc * 8;
+      const float* src = q == 0 ? e1 : e2;
+      *reinterpret_cast<f32x4v*>(dst) = f32x4v{src[0], src[1], src[2], src[3]};
+      *reinterpret_cast<f32x4v*>(dst + 4) = f32x4v{src[4], src[5], src[6], src[7]};
+      lds_barrier();
+      if (tid < BN) {
+        float sum = 0.f;
+#pragma unroll
+        for (int g2 = 0; g2 < RG2; ++g2) sum += tile[g2 * BN + tid];
+        if (a.bn_acc != nullptr)   // acc mode: the BN layer's fp64 backward sums
+          unsafeAtomicAdd(a.bn_acc + q * a.Cout + n0 + tid, (double)sum);
+        else
+          a.part[(size_t)mt * 2 * a.Cout + q * a.Cout + n0 + tid] = sum;
+      }
+    }
+  }
   if constexpr (EPI == 1) {
     if (tid < BN) {
       const int c = n0 + tid;
@@ -1386,8 +1451,10 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv2_kernel(ConvArgs a) {
 
 // serial, wave-row epilogue bands, <= 128 VGPRs: four waves per SIMD (up to four 4-wave blocks
 // per CU by LDS), the structure that wins the streaming-bound layers in v1 (variants 8..11)
+// (EPI 2 on the 128x128 tile: three waves per SIMD -- its 24 extra live registers spill at four)
 template <int BM, int BN, int EPI>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
+__global__ __launch_bounds__(256)
+__attribute__((amdgpu_waves_per_eu(EPI == 2 && BM * BN >= 128 * 128 ? 3 : 4)))
 void conv2_kernel_occ4(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
   conv2_body<BM, BN, 2, 2, 1, EPI, true>(a);
@@ -1397,19 +1464,24 @@ void conv2_kernel_occ4(ConvArgs a) {
 template <int BM, int BN, int NWM, int NWN, int NBUF, bool OCC4 = false>
 hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
-  if (a.c16 || a.bnx != nullptr || a.ksplit != 1 || a.tpb != 1 || a.Cout % BN)
-    return hipErrorInvalidValue;
-  if ((a.part != nullptr || a.bn_acc != nullptr) && (a.add != nullptr || a.mapped))
+  if (a.c16 || a.ksplit != 1 || a.tpb != 1 || a.Cout % BN) return hipErrorInvalidValue;
+  const bool bwd_bn = a.bnx != nullptr;   // EPI 2 (the caller checked part / bnmean / no map)
+  if (!bwd_bn && (a.part != nullptr || a.bn_acc != nullptr) && (a.add != nullptr || a.mapped))
     return hipErrorInvalidValue;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
   const bool stats = a.part != nullptr || a.bn_acc != nullptr;
   if constexpr (OCC4) {
-    if (stats)
+    if (bwd_bn)
+      hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 2>), dim3(nwg), dim3(256), 0, st, a);
+    else if (stats)
       hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 1>), dim3(nwg), dim3(256), 0, st, a);
     else
       hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 0>), dim3(nwg), dim3(256), 0, st, a);
+  } else if (bwd_bn) {
+    hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 2>), dim3(nwg),
+                       dim3(64 * NWM * NWN), 0, st, a);
   } else if (stats) {
     hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 1>), dim3(nwg),
                        dim3(64 * NWM * NWN), 0, st, a);
@@ -1502,12 +1574,13 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.bnx = (const uint16_t*)bnx;
   a.bnmask = bnmask;
   a.bnmean = bnmean;
-  if (bnx != nullptr && (part == nullptr || bnmean == nullptr || y_map != nullptr))
+  if (bnx != nullptr &&
+      ((part == nullptr) == (bn_acc == nullptr) || bnmean == nullptr || y_map != nullptr))
     return hipErrorInvalidValue;
   // forward statistics are taken from the accumulators before the epilogue adds an addend
   if (part != nullptr && bnx == nullptr && add != nullptr) return hipErrorInvalidValue;
-  if (bn_acc != nullptr) {
-    if (part != nullptr || bnx != nullptr || add != nullptr) return hipErrorInvalidValue;
+  if (bn_acc != nullptr) {   // forward statistics without an addend, or the EPI 2 sums
+    if (part != nullptr || (bnx == nullptr && add != nullptr)) return hipErrorInvalidValue;
     a.bn_acc = bn_acc;
   }
   a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.R = R; a.S = S;

@@ -577,7 +577,8 @@ def test_grad_join_matches_autograd_sum(mode, monkeypatch):
 @pytest.mark.gpu
 def test_dgrad_epilogue_bn_backward_partials():
     """conv2d_bwd_data(..., bn=(x, mask, mean)): per-tile sum g and sum g (x - mean) of the
-    stored dX (g = dX * mask bit), the bn_bwd_reduce partial format, tail tile included."""
+    stored dX (g = dX * mask bit), the bn_bwd_reduce partial format, tail tile included, on every
+    v1 and v2 tile, with and without an addend."""
     n, cin, h, w, cout, k = 3, 128, 9, 11, 64, 3
     x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=5)
     dy = torch.randn(n, cout, h, w, device="cuda").to(torch.bfloat16).contiguous(
@@ -589,44 +590,70 @@ def test_dgrad_epilogue_bn_backward_partials():
     mean = torch.randn(cin, device="cuda") * 0.3
     bits = ((mask.view(m, cin // 8, 1).int() >> torch.arange(8, device="cuda").view(1, 1, 8)) & 1)
     bits = bits.view(m, cin).float()
-    for v in conv.variants_for(cin):
+    addend = torch.randn(n, cin, h, w, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    vs2 = conv.v2_variants_for(cin)
+    assert vs2
+    xc = bnx.permute(0, 2, 3, 1).reshape(m, cin).float() - mean
+    for v in conv.variants_for(cin) + vs2:   # v1 tiles and the v2 coalesced-epilogue form
         dx0 = conv.conv2d_bwd_data(dy, wt, 1, v)
         dx, (part, rpb) = conv.conv2d_bwd_data(dy, wt, 1, v, bn=(bnx, mask, mean))
-        assert torch.equal(dx, dx0)
-        g = dx.permute(0, 2, 3, 1).reshape(m, cin).float() * bits
-        xc = bnx.permute(0, 2, 3, 1).reshape(m, cin).float() - mean
-        nt = -(-m // rpb)
-        assert part.numel() == nt * 2 * cin
-        p = part.view(nt, 2, cin)
-        for t in range(nt):
-            sl = slice(t * rpb, min(m, (t + 1) * rpb))
-            torch.testing.assert_close(p[t, 0], g[sl].sum(0), rtol=1e-4, atol=1e-3)
-            torch.testing.assert_close(p[t, 1], (g[sl] * xc[sl]).sum(0), rtol=1e-4, atol=1e-3)
+        assert torch.equal(dx, dx0), v
+        assert rpb == conv.TILES[v][0]
+        for add in (None, addend):   # with an addend, g is the stored dX + addend
+            if add is not None:
+                dx, (part, rpb) = conv.conv2d_bwd_data(dy, wt, 1, v, addend=add,
+                                                       bn=(bnx, mask, mean))
+                assert torch.equal(dx, conv.conv2d_bwd_data(dy, wt, 1, v, addend=add)), v
+            g = dx.permute(0, 2, 3, 1).reshape(m, cin).float() * bits
+            nt = -(-m // rpb)
+            assert part.numel() == nt * 2 * cin
+            p = part.view(nt, 2, cin)
+            for t in range(nt):
+                sl = slice(t * rpb, min(m, (t + 1) * rpb))
+                torch.testing.assert_close(p[t, 0], g[sl].sum(0), rtol=1e-4, atol=1e-3)
+                torch.testing.assert_close(p[t, 1], (g[sl] * xc[sl]).sum(0), rtol=1e-4,
+                                           atol=1e-3)
+        # acc form: the same sums added into an fp64 [2, C] set (twice: it accumulates)
+        acc = torch.zeros(2 * cin, dtype=torch.float64, device="cuda")
+        for rep_ in range(2):
+            dxs, none = conv.conv2d_bwd_data(dy, wt, 1, v, bn=(bnx, mask, mean), bn_acc=acc)
+            assert none is None and torch.equal(dxs, dx0), v
+        g0 = dx0.permute(0, 2, 3, 1).reshape(m, cin).float() * bits
+        torch.testing.assert_close(acc[:cin].float(), 2 * g0.sum(0), rtol=1e-4, atol=2e-3)
+        torch.testing.assert_close(acc[cin:].float(), 2 * (g0 * xc).sum(0), rtol=1e-4, atol=2e-3)
         # no ReLU: every bit set
         _, (part1, _) = conv.conv2d_bwd_data(dy, wt, 1, v, bn=(bnx, None, mean))
         torch.testing.assert_close(part1.view(nt, 2, cin)[:, 0].sum(0),
-                                   dx.permute(0, 2, 3, 1).reshape(m, cin).float().sum(0),
+                                   dx0.permute(0, 2, 3, 1).reshape(m, cin).float().sum(0),
                                    rtol=1e-4, atol=1e-3)
 
 
 @pytest.mark.gpu
-def test_bn_grad_links_match_plain_backward(monkeypatch):
+@pytest.mark.parametrize("form", ["partials", "acc"])
+def test_bn_grad_links_match_plain_backward(monkeypatch, form):
     """Two ResNet blocks with the BN backward partials computed in the convs' backward-data
-    epilogues (BNGradLink) give the gradients of the plain BN reduction path."""
+    epilogues (BNGradLink) give the gradients of the plain BN reduction path -- as per-tile
+    partials (BN finalize + dx) and as fp64 sums in the BN's own set (dx only)."""
     from arena_amd.models import resnet as R
     conv.set_mode("ours")
+    links0, pairs0 = conv._BN_LINKS, conv._LINK_ACC_MAX_PAIRS
     conv.set_bn_links(True)
+    conv.set_link_acc_max_pairs(1 << 30 if form == "acc" else 0)
 
     class NoLink(conv.BNGradLink):
-        def set_bn(self, x, mask, mean):
+        def set_bn(self, *a, **k):
             pass   # never ready: every BN runs its own reduction
 
     class Counting(conv.BNGradLink):
         hits = 0
+        kinds = set()
 
         def take(self, dy):
             r = super().take(dy)
             Counting.hits += r is not None
+            if r is not None:
+                Counting.kinds.add("acc" if isinstance(r[0], str) else "partials")
             return r
 
     try:
@@ -655,12 +682,14 @@ def test_bn_grad_links_match_plain_backward(monkeypatch):
                                           for n, p in net.named_parameters()})
         # bn1, bn2 of both blocks and block 0's bn3 (joined through block 1's conv1)
         assert Counting.hits == 5, Counting.hits
+        assert Counting.kinds == {form}, Counting.kinds
         assert _rel(out["link"][0], out["plain"][0]) < 2e-2
         for n, gp in out["plain"][1].items():
             assert _rel(out["link"][1][n], gp) < 2e-2, n
     finally:
         conv.set_mode(None)
-        conv.set_bn_links(False)
+        conv.set_bn_links(links0)
+        conv.set_link_acc_max_pairs(pairs0)
 
 
 @pytest.mark.gpu

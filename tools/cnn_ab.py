@@ -6,7 +6,8 @@ Builds one model + optimizer + synthetic batch per variant (same seed), warms ea
 ``--chunk`` timed replays of each variant for ``--rounds`` rounds, so clock/thermal drift hits
 every variant alike (cdna_hip_programming.md §5.4 rule 24). Variants are conv modes
 (ARENA_CONV values), optionally suffixed ``:async`` (weight gradients on a side stream) and/or
-``:link`` (BN-backward partials in the dgrad epilogues), ``:torchstem`` (the stem's
+``:link`` / ``:nolink`` (BN-backward partials in the dgrad epilogues; on by default) and/or
+``:laccP<n>`` (their fp64-sum form up to n tile-channel pairs), ``:torchstem`` (the stem's
 input/weight casts and weight transform as torch ops) and/or ``:nomask`` (the last BN writes
 dy * mask for the residual join instead of parking (dy, bits)) and/or ``:finP<n>`` (at most n
 level-1 blocks per channel group in the BN finalize kernels) and/or ``:redG<b>x<r>`` (BN reduction grid) and/or ``:accP<n>`` (conv-epilogue
@@ -50,11 +51,14 @@ def main():
     args = cnn_bench.parse(["--model", a.model, "--batch_size", str(a.batch)])
     variants = {}
     conv_acc_default = conv._ACC_MAX_PAIRS
+    link_acc_default = conv._LINK_ACC_MAX_PAIRS
     for i, name in enumerate(a.modes.split(",")):
         mode, _, opt_s = name.partition(":")
         conv.set_mode(mode)
         conv.set_async_wgrad("async" in opt_s.split("+"))
-        conv.set_bn_links("link" in opt_s.split("+"))
+        opts = opt_s.split("+")
+        # BN-backward partials in the dgrad epilogue: on by default, "nolink" turns them off
+        conv.set_bn_links("nolink" not in opts if "link" not in opts else True)
         conv.set_stem_fused("torchstem" not in opt_s.split("+"))
         conv.set_masked_join("nomask" not in opt_s.split("+"))
         # finP<n>: at most n level-1 blocks per channel group in the BN finalize kernels (the
@@ -73,6 +77,9 @@ def main():
         # accP<n>: conv-epilogue BN statistics as fp64 sums up to n (tile, channel) pairs
         accp = [int(o[4:]) for o in opt_s.split("+") if o.startswith("accP")]
         conv.set_acc_max_pairs(accp[0] if accp else conv_acc_default)
+        # laccP<n>: the same for the linked dgrad epilogue's BN-backward sums
+        laccp = [int(o[5:]) for o in opt_s.split("+") if o.startswith("laccP")]
+        conv.set_link_acc_max_pairs(laccp[0] if laccp else link_acc_default)
         # finbwd0: BN backward sums from the pool + a finalize launch (not the layer's own set)
         from arena_amd.ops import batchnorm as _bn
         _bn.set_fin_bwd("finbwd0" not in opt_s.split("+"))
