@@ -49,6 +49,11 @@ V2_TILES = {V2 + 0: (256, 128), V2 + 1: (256, 256), V2 + 2: (128, 128), V2 + 3: 
             V2 + 4: (128, 256), V2 + 5: (128, 64), V2 + 6: (64, 64), V2 + 7: (64, 128),
             # serial single-buffer forms with wave-row epilogue bands: 4 waves per SIMD
             V2 + 8: (128, 128), V2 + 9: (128, 64), V2 + 10: (64, 128), V2 + 11: (64, 64)}
+# 3x3 / stride 1 / pad 1 halo forms (width <= 63): the tile's input window is staged once per
+# 64-channel chunk and the nine taps read it shifted (conv_kernels.hip Conv2Geo::HALO)
+V2_HALO = {V2 + 12: (128, 128), V2 + 13: (128, 64)}
+HALO_MAX_W = 63
+V2_TILES.update(V2_HALO)
 TILES.update(V2_TILES)
 _V2_ON = os.environ.get("ARENA_CONV_V2", "1") != "0"
 _CUS = 256
@@ -75,8 +80,16 @@ def set_v2(on: bool) -> None:
 
 def v2_variants_for(cout: int):
     """v2 tile variants for ``cout`` output channels (forward / backward-data, incl. the strided
-    phases)."""
-    return [v for v, (_, bn) in V2_TILES.items() if cout % bn == 0] if _V2_ON else []
+    phases); the halo forms come from ``halo_variants_for``."""
+    return [v for v, (_, bn) in V2_TILES.items()
+            if cout % bn == 0 and v not in V2_HALO] if _V2_ON else []
+
+
+def halo_variants_for(cout: int, k, stride: int, pad: int, width: int):
+    """The 3x3 halo forms, for a 3x3 / stride 1 / pad 1 convolution of a <= 63-wide image."""
+    if not _V2_ON or tuple(k) != (3, 3) or stride != 1 or pad != 1 or width > HALO_MAX_W:
+        return []
+    return [v for v, (_, bn) in V2_HALO.items() if cout % bn == 0]
 
 
 _PERSIST_ON = os.environ.get("ARENA_CONV_PERSIST", "1") != "0"
@@ -736,12 +749,13 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
             return us if fin else us + _FIN_PENALTY_US
 
         fns = {}
-        for v in (variants_for(cout) + v2_variants_for(cout)
+        halo = lambda c: halo_variants_for(c, k, stride, pad, x.shape[3])  # noqa: E731
+        for v in (variants_for(cout) + v2_variants_for(cout) + halo(cout)
                   + split_variants_for(m_out, cout, cin * k[0] * k[1])):
             fns[("fwd", v)] = (lambda v=v: fwd_time(v))
         if stride == 1:
             m_in = x.shape[0] * x.shape[2] * x.shape[3]
-            for v in (variants_for(cin) + v2_variants_for(cin)
+            for v in (variants_for(cin) + v2_variants_for(cin) + halo(cin)
                       + split_variants_for(m_in, cin, cout * k[0] * k[1])):
                 fns[("bwd", v)] = (lambda v=v: _time(lambda: conv2d_bwd_data(dy, w, pad, v)))
             if _BN_LINKS:   # the linked form: a BN input, ReLU bits and mean of x's shape
@@ -749,7 +763,7 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                 bmask = torch.randint(0, 256, (m_in * cin // 8,), device=x.device,
                                       dtype=torch.uint8)
                 bmean = torch.zeros(cin, device=x.device)
-                for v in variants_for(cin) + v2_variants_for(cin):
+                for v in variants_for(cin) + v2_variants_for(cin) + halo(cin):
                     fns[("bwdbn", v)] = (lambda v=v: _time(lambda: conv2d_bwd_data(
                         dy, w, pad, v, bn=(bnx, bmask, bmean))))
         else:   # phase decomposition: per-phase heuristic (-1) or one tile for every phase

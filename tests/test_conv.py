@@ -110,6 +110,9 @@ V2_SHAPES = [  # n, cin, h, w, cout, k, stride
     (2, 192, 6, 5, 256, 3, 1),
     (8, 64, 28, 28, 64, 3, 1),      # 6272 rows: tail tile of 128 rows
     (2, 256, 14, 14, 512, 1, 1),    # BN = 256 tiles, two row bands in the 256x256 epilogue
+    (2, 64, 56, 56, 128, 3, 1),     # halo window of 242 rows
+    (4, 128, 7, 7, 128, 3, 1),      # halo windows spanning several images
+    (1, 64, 5, 63, 64, 3, 1),       # the widest halo image
 ]
 
 
@@ -126,7 +129,9 @@ def test_conv_v2_matches_fp32(shape):
     pad = k // 2
     x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=5)
     ref = F.conv2d(x.float(), wt.float(), stride=st, padding=pad)
-    vs = conv.v2_variants_for(cout)
+    halo = conv.halo_variants_for(cout, (k, k), st, pad, w)
+    assert bool(halo) == (k == 3 and st == 1)
+    vs = conv.v2_variants_for(cout) + halo
     assert vs
     for v in vs:
         y = conv.conv2d_fwd(x, wt, st, pad, v)
@@ -166,7 +171,7 @@ def test_conv_v2_matches_fp32(shape):
         memory_format=torch.channels_last)
     bits = torch.randint(0, 256, (addend.numel() // 8,), device="cuda", dtype=torch.uint8)
     dense = conv.MaskedGrad(addend, bits).materialize()
-    for v in conv.v2_variants_for(cin):
+    for v in conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, pad, w):
         dx = conv.conv2d_bwd_data(dy, wt, pad, v)
         assert _rel(dx, dx_ref) < 1e-2, (v, _rel(dx, dx_ref))
         dxa = conv.conv2d_bwd_data(dy, wt, pad, v, addend=addend)
@@ -208,7 +213,12 @@ def test_conv_wgrad_v2_matches_fp32(shape):
 
 def test_v2_variants_are_forward_and_dgrad_only():
     assert set(conv.v2_variants_for(64)) == {conv.V2 + v for v in (3, 5, 6, 9, 11)}
-    assert set(conv.v2_variants_for(256)) == set(conv.V2_TILES)
+    assert set(conv.v2_variants_for(256)) == set(conv.V2_TILES) - set(conv.V2_HALO)
+    assert set(conv.halo_variants_for(256, (3, 3), 1, 1, 14)) == set(conv.V2_HALO)
+    assert conv.halo_variants_for(64, (3, 3), 1, 1, 56) == [conv.V2 + 13]
+    assert not conv.halo_variants_for(256, (3, 3), 2, 1, 14)
+    assert not conv.halo_variants_for(256, (3, 3), 1, 1, 64)
+    assert not conv.halo_variants_for(256, (1, 1), 1, 0, 14)
     assert all(conv.tiles_per_block(v) == 1 and conv.split_of(v) == 1 for v in conv.V2_TILES)
     assert not set(conv.variants_for(256)) & set(conv.V2_TILES)   # disjoint code ranges
     assert conv.persist_variants_for(128 * 56 * 56, 256, list(conv.V2_TILES)) == []
@@ -592,8 +602,8 @@ def test_dgrad_epilogue_bn_backward_partials():
     bits = bits.view(m, cin).float()
     addend = torch.randn(n, cin, h, w, device="cuda").to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
-    vs2 = conv.v2_variants_for(cin)
-    assert vs2
+    vs2 = conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, 1, w)
+    assert vs2 and set(conv.V2_HALO) <= set(vs2)
     xc = bnx.permute(0, 2, 3, 1).reshape(m, cin).float() - mean
     for v in conv.variants_for(cin) + vs2:   # v1 tiles and the v2 coalesced-epilogue form
         dx0 = conv.conv2d_bwd_data(dy, wt, 1, v)
