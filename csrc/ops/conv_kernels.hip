@@ -1063,6 +1063,7 @@ constexpr int kHaloMaxW = 63;
 template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false,
           bool HALO = false>
 struct Conv2Geo {
+  static constexpr int kBM = BM, kBN = BN;
   static constexpr int NT = 64 * NWM * NWN;
   static constexpr int WM = BM / NWM, WN = BN / NWN;
   static constexpr int MI = WM / 32, NI = WN / 32;
@@ -1071,7 +1072,8 @@ struct Conv2Geo {
   static constexpr int kHaloRows = BM + 2 * kHaloMaxW + 2;   // window rows (max W)
   static constexpr int AIH = (kHaloRows * 8 + NT - 1) / NT;  // window loads per thread
   static constexpr int kWinBytes = AIH * NT / 8 * kRowBytes;
-  static constexpr int kStage = HALO ? kWinBytes + 2 * BN * kRowBytes : NBUF * kBufBytes;
+  // HALO: the window + a ring of NBUF per-tap weight buffers (NBUF - 1 taps in flight)
+  static constexpr int kStage = HALO ? kWinBytes + NBUF * BN * kRowBytes : NBUF * kBufBytes;
   static constexpr int SL = BN / 4;       // float4 slots per tile row
   static constexpr int RG = NT / SL;      // row groups of the statistics passes
   static constexpr int kRed = EPI == 1 ? (RG * BN + BN) * 4 : 0;
@@ -1086,276 +1088,19 @@ struct Conv2Geo {
   static_assert(kLds <= kLdsMax, "LDS budget");
 };
 
-template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false,
-          bool HALO = false>
-__device__ __forceinline__ void conv2_body(const ConvArgs& a) {
-  using G = Conv2Geo<BM, BN, NWM, NWN, NBUF, EPI, BAND, HALO>;
-  constexpr int NT = G::NT, WM = G::WM, WN = G::WN, MI = G::MI, NI = G::NI;
-  constexpr int AI = G::AI, BI = G::BI, kBufBytes = G::kBufBytes;
-  constexpr int SL = G::SL, RG = G::RG, EH = G::EH;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[G::kLds];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // XCD-aware order (as v1): each XCD gets a contiguous range of tiles, column tiles of one row
-  // tile consecutive (their A rows stay in that XCD's L2)
-  const int nwg = a.m_tiles * a.n_tiles;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int nt = lin % a.n_tiles, mt = lin / a.n_tiles;
-  const int n0 = nt * BN, m0 = mt * BM;
-
-  f32x16v acc[MI][NI];
-#pragma unroll
-  for (int i = 0; i < MI; ++i)
-#pragma unroll
-    for (int j = 0; j < NI; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int wm = wave / NWN, wn = wave % NWN;
-  const int fr = lane & 31, hh = lane >> 5;
-
-  // ---- staging descriptors (v1's descriptor form): slot s = (wave*AI + i)*64 + lane -> LDS row
-  // s / 8, chunk position s % 8 = lane % 8 ----
-  const int pos = lane & 7;
-  constexpr uint32_t kOOB = 0x80000000u;
-  const __amdgpu_buffer_rsrc_t xrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
-  const __amdgpu_buffer_rsrc_t wrsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
-  if constexpr (HALO) {
-    // ---- window staging: row j of the window = input pixel org + j (zero outside [0, M)) ----
-    constexpr int AIH = G::AIH, kWin = G::kWinBytes;
-    const int Wd = a.W;
-    const int WR = BM + 2 * Wd + 2;
-    const int org = m0 - Wd - 1;
-    uint32_t w_off[AIH];
-#pragma unroll
-    for (int i = 0; i < AIH; ++i) {
-      const int j = (wave * AIH + i) * 8 + (lane >> 3);
-      const int pix = org + j;
-      w_off[i] = (j < WR && pix >= 0 && pix < a.M)
-                     ? (uint32_t)(((size_t)pix * a.C + (pos ^ swz(j)) * 8) * 2)
-                     : kOOB;
-    }
-    uint32_t b_voff[BI];
-#pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const int row = (wave * BI + i) * 8 + (lane >> 3);
-      b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
-    }
-    // in-image taps of this lane's fragment rows: bit r*3 + s
-    uint32_t tmask[MI];
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int m = m0 + wm * WM + i * 32 + fr;
-      uint32_t mk = 0u;
-      if (m < a.M) {
-        const int hw = a.Ho * a.Wo;
-        const int n = m / hw, rem = m - n * hw;
-        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-#pragma unroll
-        for (int r = 0; r < 3; ++r)
-#pragma unroll
-          for (int s2 = 0; s2 < 3; ++s2)
-            if ((unsigned)(ho + r - 1) < (unsigned)a.H && (unsigned)(wo + s2 - 1) < (unsigned)Wd)
-              mk |= 1u << (r * 3 + s2);
-      }
-      tmask[i] = mk;
-    }
-    auto stage_win = [&](int cb) {
-#pragma unroll
-      for (int i = 0; i < AIH; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_ptr_t)(lds + (wave * AIH + i) * 64 * 16),
-                                                 16, w_off[i], cb * kRowBytes, 0, 0);
-    };
-    auto stage_b = [&](int tap, int cb, int buf) {
-      uint8_t* bb = lds + kWin + buf * BN * kRowBytes;
-#pragma unroll
-      for (int i = 0; i < BI; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
-                                                 16, b_voff[i], (tap * a.C + cb * kBK) * 2, 0, 0);
-    };
-    auto compute_tap = [&](int tap, int buf) {
-      const int r = tap / 3, s2 = tap - 3 * r;
-      const int shift = r * Wd + s2;
-      const uint8_t* bbuf = lds + kWin + buf * BN * kRowBytes;
-      bool ok[MI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) ok[i] = (tmask[i] >> tap) & 1u;
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        bf16x8 af[MI], bfr[NI];
-        const int c = kk * 2 + hh;
-#pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int j = wm * WM + i * 32 + fr + shift;
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + j * kRowBytes + ((c ^ swz(j)) << 4));
-          af[i] = ok[i] ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-        }
-#pragma unroll
-        for (int jn = 0; jn < NI; ++jn) {
-          const int row = wn * WN + jn * 32 + fr;
-          bfr[jn] = *reinterpret_cast<const bf16x8*>(bbuf + row * kRowBytes + ((c ^ swz(row)) << 4));
-        }
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int jn = 0; jn < NI; ++jn)
-            acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
-      }
-    };
-    // ---- K loop: per channel chunk, the window + tap 0's weights, then taps 1..8 double-buffered
-    const int CB = a.C / kBK;
-    for (int cb = 0; cb < CB; ++cb) {
-      stage_win(cb);   // the previous chunk's last tap ended on a barrier: the window is free
-      stage_b(0, cb, 0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      for (int t = 0; t < 9; ++t) {
-        if (t < 8) stage_b(t + 1, cb, (t + 1) & 1);   // its buffer's readers (tap t - 1) are done
-        compute_tap(t, t & 1);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
-    }
-  } else {
-    int a_lane[AI];
-    uint32_t a_mask[AI], a_cur[AI], b_voff[BI];
-  #pragma unroll
-    for (int i = 0; i < AI; ++i) {
-      const int row = (wave * AI + i) * 8 + (lane >> 3);
-      const int m = m0 + row;
-      uint32_t mk = 0u;
-      int off = 0;
-      if (m < a.M) {
-        const int hw = a.Ho * a.Wo;
-        const int n = m / hw, rem = m - n * hw;
-        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
-        const int hb = ho * a.stride - a.pad, wb = wo * a.stride - a.pad_w;
-        for (int r = 0; r < a.R; ++r) {
-          if ((unsigned)(hb + r) >= (unsigned)a.H) continue;
-          for (int s2 = 0; s2 < a.S; ++s2)
-            if ((unsigned)(wb + s2) < (unsigned)a.W) mk |= 1u << (r * a.S + s2);
-        }
-        off = (((n * a.H + hb) * a.W + wb) * a.C + (pos ^ swz(row)) * 8) * 2;
-      }
-      a_lane[i] = off;
-      a_mask[i] = mk;
-    }
-  #pragma unroll
-    for (int i = 0; i < BI; ++i) {
-      const int row = (wave * BI + i) * 8 + (lane >> 3);
-      b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
-    }
-    const int CB = a.C / kBK;
-    const int T = a.Ktot / kBK;
-    int s_tap = 0, s_cb = 0, s_s = 0, s_tapoff = 0, s_t = 0;
-  #pragma unroll
-    for (int i = 0; i < AI; ++i) a_cur[i] = (a_mask[i] & 1u) ? (uint32_t)a_lane[i] : kOOB;
-
-    auto stage = [&](int buf) {
-      uint8_t* base = lds + buf * kBufBytes;
-      const int coff = s_cb * kRowBytes;
-  #pragma unroll
-      for (int i = 0; i < AI; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_ptr_t)(base + (wave * AI + i) * 64 * 16),
-                                                 16, a_cur[i], coff, 0, 0);
-      uint8_t* bb = base + BM * kRowBytes;
-  #pragma unroll
-      for (int i = 0; i < BI; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
-                                                 16, b_voff[i], s_t * kRowBytes, 0, 0);
-      ++s_t;
-      if (++s_cb == CB) {
-        s_cb = 0;
-        ++s_tap;
-        s_tapoff += a.C * 2;
-        if (++s_s == a.S) {
-          s_s = 0;
-          s_tapoff += (a.W - a.S) * a.C * 2;
-        }
-  #pragma unroll
-        for (int i = 0; i < AI; ++i)
-          a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
-      }
-    };
-
-
-    auto compute = [&](int buf) {
-      const uint8_t* abuf = lds + buf * kBufBytes;
-      const uint8_t* bbuf = abuf + BM * kRowBytes;
-  #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        bf16x8 af[MI], bfr[NI];
-        const int c = kk * 2 + hh;   // 16-byte chunk of this lane's 8 k values
-  #pragma unroll
-        for (int i = 0; i < MI; ++i) {
-          const int row = wm * WM + i * 32 + fr;
-          af[i] = *reinterpret_cast<const bf16x8*>(abuf + row * kRowBytes + ((c ^ swz(row)) << 4));
-        }
-  #pragma unroll
-        for (int j = 0; j < NI; ++j) {
-          const int row = wn * WN + j * 32 + fr;
-          bfr[j] = *reinterpret_cast<const bf16x8*>(bbuf + row * kRowBytes + ((c ^ swz(row)) << 4));
-        }
-  #pragma unroll
-        for (int i = 0; i < MI; ++i)
-  #pragma unroll
-          for (int j = 0; j < NI; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-      }
-    };
-
-    // ---- K loop: S = NBUF - 1 steps in flight ----
-    if constexpr (NBUF == 1) {
-      // serial form (high occupancy: several blocks per CU overlap each other's staging)
-      if (T > 0) stage(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      for (int t = 0; t < T; ++t) {
-        compute(0);
-        if (t + 1 < T) {
-          __syncthreads();   // every wave is done reading the buffer: restage it
-          stage(0);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-      }
-    } else {
-      constexpr int S = NBUF - 1;
-      constexpr int kLps = AI + BI;   // LDS-DMA instructions per thread per stage
-  #pragma unroll
-      for (int i = 0; i < S; ++i)
-        if (i < T) stage(i);
-      if (T >= S)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * kLps) : "memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-      int cur = 0;
-      for (int t = 0; t < T; ++t) {
-        // RAW: stage t + 1 was retired by the vmcnt before the last barrier. WAR: stage t + S
-        // overwrites buffer (t - 1) % NBUF, whose reads completed before that barrier.
-        if (t + S < T) stage(cur == 0 ? NBUF - 1 : cur - 1);
-        compute(cur);
-        if (t + S < T)
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((S - 1) * kLps) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-        cur = cur == NBUF - 1 ? 0 : cur + 1;
-      }
-    }
-  }
-
+// The v2 epilogue: the accumulators through an fp32 LDS tile at `lds` (EH x BN floats, bands of
+// EH rows), coalesced bf16 stores (+ addend, mapped placement, fill_sib), and the EPI 1 / EPI 2
+// BatchNorm sums (`red`: [RG + 1][BN] floats of EPI 1 scratch, may follow the tile).
+template <class G, int EPI>
+__device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
+                                               f32x16v (&acc)[G::MI][G::NI], uint8_t* lds,
+                                               float* red, int m0, int n0, int mt, int tid,
+                                               int wm, int wn, int fr, int hh) {
+  constexpr int BM = G::kBM, BN = G::kBN, NT = G::NT, WM = G::WM, WN = G::WN;
+  constexpr int MI = G::MI, NI = G::NI, SL = G::SL, RG = G::RG, EH = G::EH;
   // ---- epilogue through the fp32 LDS tile (the stage buffers are free: the loop ended on a
   // barrier after every wave's last read) ----
   float* tile = reinterpret_cast<float*>(lds);
-  float* red = tile + EH * BN;          // [RG][BN] partial column sums (EPI 1)
   float* cmean = red + RG * BN;         // [BN] band mean (EPI 1)
   constexpr int CPR = BN / 8;           // 16-byte bf16 output chunks per row
   if constexpr (EPI == 1) {
@@ -1552,6 +1297,288 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
   }
 }
 
+template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false,
+          bool HALO = false>
+__device__ __forceinline__ void conv2_body(const ConvArgs& a) {
+  using G = Conv2Geo<BM, BN, NWM, NWN, NBUF, EPI, BAND, HALO>;
+  constexpr int NT = G::NT, WM = G::WM, WN = G::WN, MI = G::MI, NI = G::NI;
+  constexpr int AI = G::AI, BI = G::BI, kBufBytes = G::kBufBytes;
+  constexpr int SL = G::SL, RG = G::RG, EH = G::EH;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G::kLds];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // XCD-aware order (as v1): each XCD gets a contiguous range of tiles, column tiles of one row
+  // tile consecutive (their A rows stay in that XCD's L2)
+  const int nwg = a.m_tiles * a.n_tiles;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int nt = lin % a.n_tiles, mt = lin / a.n_tiles;
+  const int n0 = nt * BN, m0 = mt * BM;
+
+  f32x16v acc[MI][NI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NI; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int wm = wave / NWN, wn = wave % NWN;
+  const int fr = lane & 31, hh = lane >> 5;
+
+  // ---- staging descriptors (v1's descriptor form): slot s = (wave*AI + i)*64 + lane -> LDS row
+  // s / 8, chunk position s % 8 = lane % 8 ----
+  const int pos = lane & 7;
+  constexpr uint32_t kOOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t xrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.x, (short)0, a.xbytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wrsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.w, (short)0, a.wbytes, 0x00020000);
+  if constexpr (HALO) {
+    // ---- window staging: row j of the window = input pixel org + j (zero outside [0, M)) ----
+    constexpr int AIH = G::AIH, kWin = G::kWinBytes;
+    const int Wd = a.W;
+    const int WR = BM + 2 * Wd + 2;
+    const int org = m0 - Wd - 1;
+    uint32_t w_off[AIH];
+#pragma unroll
+    for (int i = 0; i < AIH; ++i) {
+      const int j = (wave * AIH + i) * 8 + (lane >> 3);
+      const int pix = org + j;
+      w_off[i] = (j < WR && pix >= 0 && pix < a.M)
+                     ? (uint32_t)(((size_t)pix * a.C + (pos ^ swz(j)) * 8) * 2)
+                     : kOOB;
+    }
+    uint32_t b_voff[BI];
+#pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = (wave * BI + i) * 8 + (lane >> 3);
+      b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
+    }
+    // in-image taps of this lane's fragment rows: bit r*3 + s
+    uint32_t tmask[MI];
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * WM + i * 32 + fr;
+      uint32_t mk = 0u;
+      if (m < a.M) {
+        const int hw = a.Ho * a.Wo;
+        const int n = m / hw, rem = m - n * hw;
+        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+#pragma unroll
+          for (int s2 = 0; s2 < 3; ++s2)
+            if ((unsigned)(ho + r - 1) < (unsigned)a.H && (unsigned)(wo + s2 - 1) < (unsigned)Wd)
+              mk |= 1u << (r * 3 + s2);
+      }
+      tmask[i] = mk;
+    }
+    auto stage_win = [&](int cb) {
+#pragma unroll
+      for (int i = 0; i < AIH; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_ptr_t)(lds + (wave * AIH + i) * 64 * 16),
+                                                 16, w_off[i], cb * kRowBytes, 0, 0);
+    };
+    auto stage_b = [&](int tap, int cb, int buf) {
+      uint8_t* bb = lds + kWin + buf * BN * kRowBytes;
+#pragma unroll
+      for (int i = 0; i < BI; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
+                                                 16, b_voff[i], (tap * a.C + cb * kBK) * 2, 0, 0);
+    };
+    auto compute_tap = [&](int tap, int buf) {
+      const int r = tap / 3, s2 = tap - 3 * r;
+      const int shift = r * Wd + s2;
+      const uint8_t* bbuf = lds + kWin + buf * BN * kRowBytes;
+      bool ok[MI];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) ok[i] = (tmask[i] >> tap) & 1u;
+#pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        bf16x8 af[MI], bfr[NI];
+        const int c = kk * 2 + hh;
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int j = wm * WM + i * 32 + fr + shift;
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + j * kRowBytes + ((c ^ swz(j)) << 4));
+          af[i] = ok[i] ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int jn = 0; jn < NI; ++jn) {
+          const int row = wn * WN + jn * 32 + fr;
+          bfr[jn] = *reinterpret_cast<const bf16x8*>(bbuf + row * kRowBytes + ((c ^ swz(row)) << 4));
+        }
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int jn = 0; jn < NI; ++jn)
+            acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
+      }
+    };
+    // ---- K loop: per channel chunk, the window + the first D = NBUF - 1 taps' weights, then
+    // one tap's weights issued per tap, D ahead (a ring of NBUF buffers; only loads in flight,
+    // so the counted vmcnt waits are exact)
+    constexpr int D = NBUF - 1;
+    static_assert(D >= 1 && D < 9, "weight ring depth");
+    const int CB = a.C / kBK;
+    for (int cb = 0; cb < CB; ++cb) {
+      stage_win(cb);   // the previous chunk's last tap ended on a barrier: the window is free
+#pragma unroll
+      for (int t = 0; t < D; ++t) stage_b(t, cb, t);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * BI) : "memory");   // window + tap 0
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        // buffer (t + D) % NBUF was last read by tap t - 1, before the barrier that ended it
+        if (t + D < 9) stage_b(t + D, cb, (t + D) % NBUF);
+        compute_tap(t, t % NBUF);
+        if (t + D < 9)   // tap t + 1 landed, D - 1 taps may still be in flight
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((D - 1) * BI) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    }
+  } else {
+    int a_lane[AI];
+    uint32_t a_mask[AI], a_cur[AI], b_voff[BI];
+  #pragma unroll
+    for (int i = 0; i < AI; ++i) {
+      const int row = (wave * AI + i) * 8 + (lane >> 3);
+      const int m = m0 + row;
+      uint32_t mk = 0u;
+      int off = 0;
+      if (m < a.M) {
+        const int hw = a.Ho * a.Wo;
+        const int n = m / hw, rem = m - n * hw;
+        const int ho = rem / a.Wo, wo = rem - ho * a.Wo;
+        const int hb = ho * a.stride - a.pad, wb = wo * a.stride - a.pad_w;
+        for (int r = 0; r < a.R; ++r) {
+          if ((unsigned)(hb + r) >= (unsigned)a.H) continue;
+          for (int s2 = 0; s2 < a.S; ++s2)
+            if ((unsigned)(wb + s2) < (unsigned)a.W) mk |= 1u << (r * a.S + s2);
+        }
+        off = (((n * a.H + hb) * a.W + wb) * a.C + (pos ^ swz(row)) * 8) * 2;
+      }
+      a_lane[i] = off;
+      a_mask[i] = mk;
+    }
+  #pragma unroll
+    for (int i = 0; i < BI; ++i) {
+      const int row = (wave * BI + i) * 8 + (lane >> 3);
+      b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
+    }
+    const int CB = a.C / kBK;
+    const int T = a.Ktot / kBK;
+    int s_tap = 0, s_cb = 0, s_s = 0, s_tapoff = 0, s_t = 0;
+  #pragma unroll
+    for (int i = 0; i < AI; ++i) a_cur[i] = (a_mask[i] & 1u) ? (uint32_t)a_lane[i] : kOOB;
+
+    auto stage = [&](int buf) {
+      uint8_t* base = lds + buf * kBufBytes;
+      const int coff = s_cb * kRowBytes;
+  #pragma unroll
+      for (int i = 0; i < AI; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_ptr_t)(base + (wave * AI + i) * 64 * 16),
+                                                 16, a_cur[i], coff, 0, 0);
+      uint8_t* bb = base + BM * kRowBytes;
+  #pragma unroll
+      for (int i = 0; i < BI; ++i)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
+                                                 16, b_voff[i], s_t * kRowBytes, 0, 0);
+      ++s_t;
+      if (++s_cb == CB) {
+        s_cb = 0;
+        ++s_tap;
+        s_tapoff += a.C * 2;
+        if (++s_s == a.S) {
+          s_s = 0;
+          s_tapoff += (a.W - a.S) * a.C * 2;
+        }
+  #pragma unroll
+        for (int i = 0; i < AI; ++i)
+          a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
+      }
+    };
+
+
+    auto compute = [&](int buf) {
+      const uint8_t* abuf = lds + buf * kBufBytes;
+      const uint8_t* bbuf = abuf + BM * kRowBytes;
+  #pragma unroll
+      for (int kk = 0; kk < 4; ++kk) {
+        bf16x8 af[MI], bfr[NI];
+        const int c = kk * 2 + hh;   // 16-byte chunk of this lane's 8 k values
+  #pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int row = wm * WM + i * 32 + fr;
+          af[i] = *reinterpret_cast<const bf16x8*>(abuf + row * kRowBytes + ((c ^ swz(row)) << 4));
+        }
+  #pragma unroll
+        for (int j = 0; j < NI; ++j) {
+          const int row = wn * WN + j * 32 + fr;
+          bfr[j] = *reinterpret_cast<const bf16x8*>(bbuf + row * kRowBytes + ((c ^ swz(row)) << 4));
+        }
+  #pragma unroll
+        for (int i = 0; i < MI; ++i)
+  #pragma unroll
+          for (int j = 0; j < NI; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      }
+    };
+
+    // ---- K loop: S = NBUF - 1 steps in flight ----
+    if constexpr (NBUF == 1) {
+      // serial form (high occupancy: several blocks per CU overlap each other's staging)
+      if (T > 0) stage(0);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      for (int t = 0; t < T; ++t) {
+        compute(0);
+        if (t + 1 < T) {
+          __syncthreads();   // every wave is done reading the buffer: restage it
+          stage(0);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+    } else {
+      constexpr int S = NBUF - 1;
+      constexpr int kLps = AI + BI;   // LDS-DMA instructions per thread per stage
+  #pragma unroll
+      for (int i = 0; i < S; ++i)
+        if (i < T) stage(i);
+      if (T >= S)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((S - 1) * kLps) : "memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      int cur = 0;
+      for (int t = 0; t < T; ++t) {
+        // RAW: stage t + 1 was retired by the vmcnt before the last barrier. WAR: stage t + S
+        // overwrites buffer (t - 1) % NBUF, whose reads completed before that barrier.
+        if (t + S < T) stage(cur == 0 ? NBUF - 1 : cur - 1);
+        compute(cur);
+        if (t + S < T)
+          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((S - 1) * kLps) : "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        cur = cur == NBUF - 1 ? 0 : cur + 1;
+      }
+    }
+  }
+
+  conv2_epilogue<G, EPI>(a, acc, lds, reinterpret_cast<float*>(lds) + EH * BN, m0, n0, mt, tid,
+                         wm, wn, fr, hh);
+}
+
 template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI>
 __global__ __launch_bounds__(64 * NWM * NWN) void conv2_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
@@ -1571,11 +1598,12 @@ void conv2_kernel_occ4(ConvArgs a) {
 #endif
 }
 
-// the 3x3 halo form (see Conv2Geo::HALO): 4 waves, two blocks per CU by LDS
+// the 3x3 halo form (see Conv2Geo::HALO): 4 waves, a ring of NBR per-tap weight buffers --
+// 128x128: three (80 KB, two blocks per CU); 128x64: two (48 KB, three blocks per CU)
 template <int BM, int BN, int EPI>
 __global__ __launch_bounds__(256) void conv2_kernel_halo(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv2_body<BM, BN, 2, 2, 2, EPI, false, true>(a);
+  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, true>(a);
 #endif
 }
 
