@@ -18,8 +18,10 @@ def category(n: str) -> str:
         return "conv wgrad"
     if "igemm_bwd" in n or "bwd_data" in n:
         return "conv dgrad"
-    if "conv_fwd" in n or "igemm_fwd" in n:
-        return "conv fwd"
+    if "conv_fwd" in n or "igemm_fwd" in n or "conv2_kernel" in n:
+        return "conv fwd / dgrad (implicit GEMM)"
+    if "conv_phase_weights" in n or "flip_weight" in n:
+        return "conv weight transforms"
     if "Cijk" in n or "gemm" in n.lower():
         return "gemm"
     if "elementwise" in n or "Functor" in n:
