@@ -101,14 +101,27 @@ def build(args, dev, world):
                 raise SystemExit("--master_weights on with several ranks needs the xGMI "
                                  "collective (single node, --comm auto|xgmi)")
             master = False   # fp32 weights + DistributedOptimizer (RCCL) instead
+    opt = None
     if master and world > 1:
+        from ..parallel.xgmi import XgmiUnavailable
         from ..parallel.zero import ShardedMasterSGD
         # every parameter on one registered communicator: bf16 conv/fc weights with fp32
         # masters, and the fp32 BN scales/shifts + biases (no decay) as fp32 tail buckets
-        opt = ShardedMasterSGD(
-            [{"params": decay, "weight_decay": args.weight_decay},
-             {"params": no_decay, "weight_decay": 0.0, "weights": "fp32"}],
-            lr=args.learning_rate, momentum=args.momentum, bucket_mb=args.bucket_mb)
+        try:
+            opt = ShardedMasterSGD(
+                [{"params": decay, "weight_decay": args.weight_decay},
+                 {"params": no_decay, "weight_decay": 0.0, "weights": "fp32"}],
+                lr=args.learning_rate, momentum=args.momentum, bucket_mb=args.bucket_mb)
+        except XgmiUnavailable as e:
+            # the peer mappings or the self-test failed on some rank (all ranks learn it
+            # together): the parameters were not re-bound yet, so the RCCL path can take over
+            if mw == "on":
+                raise
+            print(f"[rank {hvd.rank()}] xGMI communicator unavailable ({e}); "
+                  f"fp32 weights + DistributedOptimizer instead", file=sys.stderr, flush=True)
+            master = False
+    if opt is not None:
+        pass
     elif master:
         # conv/fc weights live in bf16 (fp32 masters inside MasterSGD): no per-step casts
         from ..ops.optim import MasterSGD, OptimizerGroup
