@@ -324,7 +324,8 @@ def conv2d_bwd_data_strided(dy: Tensor, w: Tensor, x_hw: Tuple[int, int], stride
     mapped output). All phase weights come from one ``conv_phase_weights`` launch. ``addend`` (the
     residual join's other gradient) is added in the epilogue. Phases without taps (1x1 stride 2:
     three of four) are the addend or zero: when phase (0, 0) is the only one with taps its
-    epilogue writes them too (fill_sib), so dX is written in one pass."""
+    epilogue writes them too (fill_sib), so dX is written in one pass. With a v2 tile variant
+    the phases run as one launch (``conv_dgrad_phases``)."""
     N, Cout, Ho, Wo = dy.shape
     Cin, R, S = w.shape[1], w.shape[2], w.shape[3]
     H, W = x_hw
@@ -353,14 +354,21 @@ def conv2d_bwd_data_strided(dy: Tensor, w: Tensor, x_hw: Tuple[int, int], stride
         else:
             dx.zero_()
         addend = dx
+    geo = []
     for (a, b, r0, c0), wp in zip(phases, wps):
         Rp, Sp = wp.shape[2], wp.shape[3]
         ca, cb = (a + pad - r0) // stride, (b + pad - c0) // stride
         Hp, Wp = (H - a + stride - 1) // stride, (W - b + stride - 1) // stride
-        if Hp <= 0 or Wp <= 0:
-            continue
+        if Hp > 0 and Wp > 0:
+            geo.append((wp, [Rp - 1 - ca, Sp - 1 - cb, Hp, Wp, a, b]))
+    if V2 <= variant and variant not in V2_HALO and len(geo) > 1:
+        # v2 tiles: every phase in one launch (the phases' tiles fill the chip together)
+        ext.conv_dgrad_phases(dy, [g[0] for g in geo], [g[1] for g in geo], dx, addend, stride,
+                              int(variant))
+        return dx
+    for wp, (ph_, pw_, Hp, Wp, a, b) in geo:
         v = variant if variant >= 0 else pick_variant(N * Hp * Wp, Cin)
-        ext.conv_fwd_ex(dy, wp, 1, Rp - 1 - ca, Sp - 1 - cb, Hp, Wp, int(v), False, addend, dx,
+        ext.conv_fwd_ex(dy, wp, 1, ph_, pw_, Hp, Wp, int(v), False, addend, dx,
                         [stride, stride, a, b] + ([1] if sib else []), False)
     return dx
 

@@ -69,6 +69,10 @@ hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void
                              const void*, const uint8_t*, const float*, int, int, int, int, int,
                              int, int, int, int, int, int, int, const int*, int, int, double*,
                              int, void*, unsigned*, int, hipStream_t);
+hipError_t arena_conv_fwd_phases(const void*, void*, const void*, int, int, int, int, int, int,
+                                 int, int, int, int, const void* const*, const int*, const int*,
+                                 const int*, const int*, const int*, const int*, const int*,
+                                 const int*, int, hipStream_t);
 long long arena_conv_fwd_ksplit_floats(long long, int, int, int);
 void arena_conv_set_stats_one_pass(int);
 long long arena_conv_fwd_tiles(long long, int, int);
@@ -1482,6 +1486,57 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
   return {y};
 }
 
+// Every phase convolution of a stride-`stride` backward-data pass in one launch (v2 tile
+// `variant`): dy [N, C, H, W] (channels_last bf16), phase weights wps[p] [Cout, C, R_p, S_p]
+// (conv_phase_weights' views), geometry[p] = {pad_h, pad_w, Ho, Wo, ooh, oow}; phase p writes
+// pixel (ho, wo) of its grid to (ho*stride + ooh, wo*stride + oow) of dx_out [N, Cout, Hy, Wy]
+// (+ addend shaped like dx_out, which may alias it).
+void conv_dgrad_phases(Tensor dy, std::vector<Tensor> wps, std::vector<std::vector<int64_t>> geom,
+                       Tensor dx_out, OptT addend, int64_t stride, int64_t variant) {
+  TORCH_CHECK(dy.is_cuda() && dy.dim() == 4 && dy.scalar_type() == torch::kBFloat16 &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad_phases: dy must be a channels_last bf16 GPU tensor");
+  const int64_t np = (int64_t)wps.size();
+  TORCH_CHECK(np >= 1 && np <= 4 && (int64_t)geom.size() == np, "conv_dgrad_phases: 1..4 phases");
+  const int64_t N = dy.size(0), C = dy.size(1), H = dy.size(2), W = dy.size(3);
+  TORCH_CHECK(dx_out.is_cuda() && dx_out.device() == dy.device() && dx_out.dim() == 4 &&
+                  dx_out.scalar_type() == torch::kBFloat16 && dx_out.size(0) == N &&
+                  dx_out.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad_phases: dx_out must be a channels_last bf16 [N, Cout, Hy, Wy] tensor");
+  const int64_t Cout = dx_out.size(1);
+  if (addend.has_value()) {
+    TORCH_CHECK(addend->sizes() == dx_out.sizes() && addend->scalar_type() == torch::kBFloat16 &&
+                    addend->device() == dx_out.device() &&
+                    addend->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_dgrad_phases: addend must be shaped like dx_out");
+  }
+  std::vector<const void*> wp(np);
+  std::vector<int> R(np), S(np), ph(np), pw(np), Ho(np), Wo(np), oh(np), ow(np);
+  for (int64_t p = 0; p < np; ++p) {
+    const Tensor& w = wps[p];
+    TORCH_CHECK(w.is_cuda() && w.device() == dy.device() && w.dim() == 4 &&
+                    w.scalar_type() == torch::kBFloat16 && w.size(0) == Cout && w.size(1) == C &&
+                    w.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "conv_dgrad_phases: phase weights must be channels_last bf16 [Cout, C, R, S]");
+    TORCH_CHECK(geom[p].size() == 6, "conv_dgrad_phases: geometry is {pad_h, pad_w, Ho, Wo, ooh, oow}");
+    wp[p] = w.data_ptr();
+    R[p] = (int)w.size(2); S[p] = (int)w.size(3);
+    ph[p] = (int)geom[p][0]; pw[p] = (int)geom[p][1]; Ho[p] = (int)geom[p][2];
+    Wo[p] = (int)geom[p][3]; oh[p] = (int)geom[p][4]; ow[p] = (int)geom[p][5];
+    TORCH_CHECK(ph[p] >= 0 && pw[p] >= 0 && ph[p] < R[p] && pw[p] < S[p] &&
+                    (Ho[p] - 1) * stride + oh[p] < dx_out.size(2) &&
+                    (Wo[p] - 1) * stride + ow[p] < dx_out.size(3),
+                "conv_dgrad_phases: phase ", p, " geometry outside dx_out");
+  }
+  check_hip(arena_conv_fwd_phases(dy.data_ptr(), dx_out.data_ptr(),
+                                  addend.has_value() ? addend->data_ptr() : nullptr, (int)N, (int)H,
+                                  (int)W, (int)C, (int)Cout, (int)dx_out.size(2),
+                                  (int)dx_out.size(3), (int)stride, (int)stride, (int)np, wp.data(),
+                                  R.data(), S.data(), ph.data(), pw.data(), Ho.data(), Wo.data(),
+                                  oh.data(), ow.data(), (int)variant, cur_stream()),
+            "conv_dgrad_phases");
+}
+
 // dW [Cout, C, R, S] (channels_last) of a convolution with top/left padding and an explicit
 // output size (dy's), c16 mode as conv_fwd_ex.
 // wgrad tile (Cout x R*S*C) of a variant: 0..3 (+4 serial) v1, 8..11 the v2 32x32x16 kernel
@@ -1820,6 +1875,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("with_stats"), py::arg("addend"), py::arg("y_out"), py::arg("y_map"),
         py::arg("c16"), py::arg("stats_final") = false);
   m.def("conv_wgrad_ex", &conv_wgrad_ex);
+  m.def("conv_dgrad_phases", &conv_dgrad_phases, py::arg("dy"), py::arg("wps"), py::arg("geom"),
+        py::arg("dx_out"), py::arg("addend"), py::arg("stride"), py::arg("variant"));
   m.def("s2d_stem", &s2d_stem);
   m.def("stem_weight", &stem_weight);
   m.def("stem_weight_grad", &stem_weight_grad);

@@ -104,6 +104,15 @@ struct ConvArgs {
   int xbytes, wbytes;  // buffer-descriptor ranges of x and w (both < 2^31 bytes, host-checked)
   int tpb;             // output tiles per block (persistent form, see conv_fwd_body); 1 = one
   int st1p;            // EPI 1 statistics in one pass (sum, sum of squares) instead of two
+  // Several phase convolutions of a strided backward-data pass in ONE launch (v2 tiles, plain
+  // mapped epilogue): phase p owns blocks [ph[p].blk0, ph[p + 1].blk0) (starts on multiples of 8,
+  // so the XCD-aware tile order holds within each phase) and overrides the per-phase fields.
+  struct Phase {
+    const uint16_t* w;
+    int R, S, pad, pad_w, Ho, Wo, ooh, oow, wbytes, blk0;
+  };
+  int nph;             // 0: a single convolution
+  Phase ph[4];
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -1299,7 +1308,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
 
 template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false,
           bool HALO = false>
-__device__ __forceinline__ void conv2_body(const ConvArgs& a) {
+__device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
   using G = Conv2Geo<BM, BN, NWM, NWN, NBUF, EPI, BAND, HALO>;
   constexpr int NT = G::NT, WM = G::WM, WN = G::WN, MI = G::MI, NI = G::NI;
   constexpr int AI = G::AI, BI = G::BI, kBufBytes = G::kBufBytes;
@@ -1310,7 +1319,6 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
   // XCD-aware order (as v1): each XCD gets a contiguous range of tiles, column tiles of one row
   // tile consecutive (their A rows stay in that XCD's L2)
   const int nwg = a.m_tiles * a.n_tiles;
-  const int bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int nt = lin % a.n_tiles, mt = lin / a.n_tiles;
@@ -1579,10 +1587,36 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a) {
                          wm, wn, fr, hh);
 }
 
+// The multi-phase launch: this block's phase, its arguments and its block index within it
+// (false: a padding block past the phase's tiles, which exits before any barrier).
+template <int BM>
+__device__ __forceinline__ bool conv2_phase(const ConvArgs& a, ConvArgs& b, int& bid) {
+  int p = 0;
+  while (p + 1 < a.nph && (int)blockIdx.x >= a.ph[p + 1].blk0) ++p;
+  const ConvArgs::Phase& ph = a.ph[p];
+  b = a;
+  b.w = ph.w;
+  b.R = ph.R; b.S = ph.S; b.pad = ph.pad; b.pad_w = ph.pad_w;
+  b.Ho = ph.Ho; b.Wo = ph.Wo; b.ooh = ph.ooh; b.oow = ph.oow; b.wbytes = ph.wbytes;
+  b.M = a.N * ph.Ho * ph.Wo;
+  b.Ktot = ph.R * ph.S * a.C;
+  b.m_tiles = (b.M + BM - 1) / BM;
+  bid = (int)blockIdx.x - ph.blk0;
+  return bid < b.m_tiles * b.n_tiles;
+}
+
 template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI>
 __global__ __launch_bounds__(64 * NWM * NWN) void conv2_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
-  conv2_body<BM, BN, NWM, NWN, NBUF, EPI>(a);
+  if constexpr (EPI == 0) {
+    if (a.nph > 0) {
+      ConvArgs b;
+      int bid;
+      if (conv2_phase<BM>(a, b, bid)) conv2_body<BM, BN, NWM, NWN, NBUF, EPI>(b, bid);
+      return;
+    }
+  }
+  conv2_body<BM, BN, NWM, NWN, NBUF, EPI>(a, blockIdx.x);
 #endif
 }
 
@@ -1594,7 +1628,15 @@ __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(EPI == 2 && BM * BN >= 128 * 128 ? 3 : 4)))
 void conv2_kernel_occ4(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv2_body<BM, BN, 2, 2, 1, EPI, true>(a);
+  if constexpr (EPI == 0) {
+    if (a.nph > 0) {
+      ConvArgs b;
+      int bid;
+      if (conv2_phase<BM>(a, b, bid)) conv2_body<BM, BN, 2, 2, 1, EPI, true>(b, bid);
+      return;
+    }
+  }
+  conv2_body<BM, BN, 2, 2, 1, EPI, true>(a, blockIdx.x);
 #endif
 }
 
@@ -1603,7 +1645,7 @@ void conv2_kernel_occ4(ConvArgs a) {
 template <int BM, int BN, int EPI>
 __global__ __launch_bounds__(256) void conv2_kernel_halo(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, true>(a);
+  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, true>(a, blockIdx.x);
 #endif
 }
 
@@ -1637,8 +1679,18 @@ hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
     return hipErrorInvalidValue;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  const int nwg = a.m_tiles * a.n_tiles;
+  int nwg = a.m_tiles * a.n_tiles;
   const bool stats = a.part != nullptr || a.bn_acc != nullptr;
+  if (a.nph > 0) {   // phases back to back, each starting on a multiple of 8 blocks
+    if (stats || bwd_bn) return hipErrorInvalidValue;
+    int b0 = 0;
+    for (int p = 0; p < a.nph; ++p) {
+      a.ph[p].blk0 = b0;
+      const long long mp = (long long)a.N * a.ph[p].Ho * a.ph[p].Wo;
+      b0 += ((int)((mp + BM - 1) / BM) * a.n_tiles + 7) / 8 * 8;
+    }
+    nwg = b0;
+  }
   if constexpr (OCC4) {
     if (bwd_bn)
       hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 2>), dim3(nwg), dim3(256), 0, st, a);
@@ -1816,6 +1868,53 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
     case 3: return launch<64, 64>(a, pipe, st);
     default: return hipErrorInvalidValue;
   }
+}
+
+// All phase convolutions of a strided backward-data pass in one launch of v2 tile `variant`
+// (kV2Base + i, not the halo forms): x = dY [N][H][W][C], phase p's weights w[p]
+// [Cout][R[p]][S[p]][C] with top/left padding pad_h/pad_w[p] over a Ho[p] x Wo[p] phase grid,
+// stored at (ho*osh + ooh[p], wo*osw + oow[p]) of y [N][Hy][Wy][Cout] (+ add, same shape; add may
+// alias y). nph <= 4.
+hipError_t arena_conv_fwd_phases(const void* x, void* y, const void* add, int N, int H, int W,
+                                 int C, int Cout, int Hy, int Wy, int osh, int osw, int nph,
+                                 const void* const* w, const int* R, const int* S,
+                                 const int* pad_h, const int* pad_w, const int* Ho, const int* Wo,
+                                 const int* ooh, const int* oow, int variant, hipStream_t st) {
+  const int idx = variant - kV2Base;
+  if (idx < 0 || idx >= 12 || nph < 1 || nph > 4 || C % kBK || Cout % 64 || N <= 0)
+    return hipErrorInvalidValue;
+  ConvArgs a{};
+  a.x = (const uint16_t*)x;
+  a.y = (uint16_t*)y;
+  a.add = (const uint16_t*)add;
+  a.N = N; a.H = H; a.W = W; a.C = C; a.Cout = Cout; a.stride = 1;
+  a.mapped = 1; a.Hy = Hy; a.Wy = Wy; a.osh = osh; a.osw = osw;
+  a.coal = 1;
+  a.ksplit = 1;
+  a.tpb = 1;
+  const long long xb = (long long)N * H * W * C * 2;
+  if (xb >= (1LL << 31) || osh <= 0 || osw <= 0) return hipErrorInvalidValue;
+  a.xbytes = (int)xb;
+  a.nph = nph;
+  for (int p = 0; p < nph; ++p) {
+    ConvArgs::Phase& ph = a.ph[p];
+    ph.w = (const uint16_t*)w[p];
+    ph.R = R[p]; ph.S = S[p]; ph.pad = pad_h[p]; ph.pad_w = pad_w[p];
+    ph.Ho = Ho[p]; ph.Wo = Wo[p]; ph.ooh = ooh[p]; ph.oow = oow[p];
+    const long long wb = (long long)Cout * R[p] * S[p] * C * 2;
+    if (wb >= (1LL << 31) || R[p] * S[p] > 32 || R[p] <= 0 || S[p] <= 0 || Ho[p] <= 0 ||
+        Wo[p] <= 0 || ooh[p] < 0 || oow[p] < 0 || (Ho[p] - 1) * osh + ooh[p] >= Hy ||
+        (Wo[p] - 1) * osw + oow[p] >= Wy || (long long)N * Ho[p] * Wo[p] >= (1LL << 31))
+      return hipErrorInvalidValue;
+    ph.wbytes = (int)wb;
+  }
+  // the single-convolution fields stay consistent with phase 0 (launch2_t's checks read them)
+  a.w = a.ph[0].w; a.R = R[0]; a.S = S[0]; a.pad = pad_h[0]; a.pad_w = pad_w[0];
+  a.Ho = Ho[0]; a.Wo = Wo[0]; a.ooh = ooh[0]; a.oow = oow[0]; a.wbytes = a.ph[0].wbytes;
+  a.M = N * Ho[0] * Wo[0];
+  a.Ktot = R[0] * S[0] * C;
+  a.st1p = g_conv_st1p;
+  return launch2(a, idx, st);
 }
 
 hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, const void* add,
