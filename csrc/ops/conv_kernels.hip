@@ -1085,7 +1085,7 @@ struct Conv2Geo {
   static constexpr int kStage = HALO ? kWinBytes + NBUF * BN * kRowBytes : NBUF * kBufBytes;
   static constexpr int SL = BN / 4;       // float4 slots per tile row
   static constexpr int RG = NT / SL;      // row groups of the statistics passes
-  static constexpr int kRed = EPI == 1 ? (RG * BN + BN) * 4 : 0;
+  static constexpr int kRed = 0;   // EPI 1's partials reuse the band's tile (2 RG rows)
   // rows per epilogue band: the whole tile when it fits, else one wave-row; BAND forces the
   // wave-row bands to keep the block's LDS small (the high-occupancy serial variants)
   static constexpr int EH = !BAND && BM * BN * 4 + kRed <= kLdsMax - 1024 ? BM : WM;
@@ -1094,23 +1094,23 @@ struct Conv2Geo {
   static_assert(MI >= 1 && NI >= 1 && AI >= 1 && BI >= 1, "tile too small for the wave grid");
   static_assert(AI * NT == BM * 8 && BI * NT == BN * 8, "staging slots must cover the tile");
   static_assert(SL >= 8 && NT % SL == 0, "epilogue layout");
+  static_assert(EPI != 1 || 2 * RG <= EH, "EPI 1 partials fit the band's tile");
   static_assert(kLds <= kLdsMax, "LDS budget");
 };
 
 // The v2 epilogue: the accumulators through an fp32 LDS tile at `lds` (EH x BN floats, bands of
 // EH rows), coalesced bf16 stores (+ addend, mapped placement, fill_sib), and the EPI 1 / EPI 2
-// BatchNorm sums (`red`: [RG + 1][BN] floats of EPI 1 scratch, may follow the tile).
+// BatchNorm sums (their partials reuse the tile).
 template <class G, int EPI>
 __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
                                                f32x16v (&acc)[G::MI][G::NI], uint8_t* lds,
-                                               float* red, int m0, int n0, int mt, int tid,
-                                               int wm, int wn, int fr, int hh) {
+                                               int m0, int n0, int mt, int tid, int wm, int wn,
+                                               int fr, int hh) {
   constexpr int BM = G::kBM, BN = G::kBN, NT = G::NT, WM = G::WM, WN = G::WN;
   constexpr int MI = G::MI, NI = G::NI, SL = G::SL, RG = G::RG, EH = G::EH;
   // ---- epilogue through the fp32 LDS tile (the stage buffers are free: the loop ended on a
   // barrier after every wave's last read) ----
   float* tile = reinterpret_cast<float*>(lds);
-  float* cmean = red + RG * BN;         // [BN] band mean (EPI 1)
   constexpr int CPR = BN / 8;           // 16-byte bf16 output chunks per row
   if constexpr (EPI == 1) {
     // statistics of the stored (bf16-rounded) values: round once, the stores re-round exactly
@@ -1226,34 +1226,33 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
     }
     if constexpr (EPI == 1) {
       if (nvalid > 0) {
-        // two-pass column statistics over the band's valid rows: thread = (row group, slot)
+        // one pass over the band's valid rows, shifted by the band's first row k (the same shift
+        // for every thread of a channel): thread = (row group, slot) sums d = x - k and d^2; the
+        // band's mean is k + s / n and its M2 = q - s^2 / n. The partials then overwrite the
+        // tile (every read of it is done), so EPI 1 needs no LDS of its own.
         const int sl = tid % SL, rg = tid / SL;
-        f32x4v s4 = {0.f, 0.f, 0.f, 0.f};
-        for (int row = rg; row < nvalid; row += RG)
-          s4 += *reinterpret_cast<const f32x4v*>(tile + (row * SL + (sl ^ (row & 7))) * 4);
-        *reinterpret_cast<f32x4v*>(red + rg * BN + sl * 4) = s4;
-        lds_barrier();
-        if (tid < BN) {
-          float sum = 0.f;
-#pragma unroll 8
-          for (int g2 = 0; g2 < RG; ++g2) sum += red[g2 * BN + tid];
-          cmean[tid] = sum / (float)nvalid;
-        }
-        lds_barrier();
-        const f32x4v mu = *reinterpret_cast<const f32x4v*>(cmean + sl * 4);
-        f32x4v q4 = {0.f, 0.f, 0.f, 0.f};
+        const f32x4v k4 = *reinterpret_cast<const f32x4v*>(tile + sl * 4);   // row 0, slot sl
+        const float kc = tid < BN ? tile[tid] : 0.f;                         // channel tid's k
+        f32x4v s4 = {0.f, 0.f, 0.f, 0.f}, q4 = {0.f, 0.f, 0.f, 0.f};
         for (int row = rg; row < nvalid; row += RG) {
-          const f32x4v d = *reinterpret_cast<const f32x4v*>(tile + (row * SL + (sl ^ (row & 7))) * 4) - mu;
+          const f32x4v d = *reinterpret_cast<const f32x4v*>(tile + (row * SL + (sl ^ (row & 7))) * 4) - k4;
+          s4 += d;
           q4 += d * d;
         }
-        lds_barrier();   // every thread has read cmean's band sums (red is rewritten below)
-        *reinterpret_cast<f32x4v*>(red + rg * BN + sl * 4) = q4;
+        lds_barrier();   // every thread is done reading the band: its tile takes the partials
+        *reinterpret_cast<f32x4v*>(tile + rg * BN + sl * 4) = s4;
+        *reinterpret_cast<f32x4v*>(tile + (RG + rg) * BN + sl * 4) = q4;
         lds_barrier();
         if (tid < BN) {
-          float m2 = 0.f;
+          float sd = 0.f, m2 = 0.f;
 #pragma unroll 8
-          for (int g2 = 0; g2 < RG; ++g2) m2 += red[g2 * BN + tid];
-          const float bmean = cmean[tid], nb = (float)nvalid;
+          for (int g2 = 0; g2 < RG; ++g2) {
+            sd += tile[g2 * BN + tid];
+            m2 += tile[(RG + g2) * BN + tid];
+          }
+          const float nb = (float)nvalid;
+          const float bmean = kc + sd / nb;
+          m2 = fmaxf(m2 - sd * sd / nb, 0.f);
           if (st_n == 0.f) {
             st_n = nb; st_mean = bmean; st_m2 = m2;
           } else {   // Chan's merge of two bands
@@ -1583,8 +1582,7 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
     }
   }
 
-  conv2_epilogue<G, EPI>(a, acc, lds, reinterpret_cast<float*>(lds) + EH * BN, m0, n0, mt, tid,
-                         wm, wn, fr, hh);
+  conv2_epilogue<G, EPI>(a, acc, lds, m0, n0, mt, tid, wm, wn, fr, hh);
 }
 
 // The multi-phase launch: this block's phase, its arguments and its block index within it
