@@ -51,8 +51,10 @@ V2_TILES = {V2 + 0: (256, 128), V2 + 1: (256, 256), V2 + 2: (128, 128), V2 + 3: 
             V2 + 8: (128, 128), V2 + 9: (128, 64), V2 + 10: (64, 128), V2 + 11: (64, 64)}
 # 3x3 / stride 1 / pad 1 halo forms (width <= 63): the tile's input window is staged once per
 # 64-channel chunk and the nine taps read it shifted (conv_kernels.hip Conv2Geo::HALO)
-V2_HALO = {V2 + 12: (128, 128), V2 + 13: (128, 64)}
+V2_HALO = {V2 + 12: (128, 128), V2 + 13: (128, 64),
+           V2 + 14: (128, 64)}   # 14: the window of <= 31-wide images (four blocks per CU)
 HALO_MAX_W = 63
+HALO_SMALL = {V2 + 14: 31}
 V2_TILES.update(V2_HALO)
 TILES.update(V2_TILES)
 _V2_ON = os.environ.get("ARENA_CONV_V2", "1") != "0"
@@ -89,7 +91,8 @@ def halo_variants_for(cout: int, k, stride: int, pad: int, width: int):
     """The 3x3 halo forms, for a 3x3 / stride 1 / pad 1 convolution of a <= 63-wide image."""
     if not _V2_ON or tuple(k) != (3, 3) or stride != 1 or pad != 1 or width > HALO_MAX_W:
         return []
-    return [v for v, (_, bn) in V2_HALO.items() if cout % bn == 0]
+    return [v for v, (_, bn) in V2_HALO.items()
+            if cout % bn == 0 and width <= HALO_SMALL.get(v, HALO_MAX_W)]
 
 
 _PERSIST_ON = os.environ.get("ARENA_CONV_PERSIST", "1") != "0"

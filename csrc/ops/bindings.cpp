@@ -842,7 +842,7 @@ ConvSplit conv_split(const Tensor& x, int64_t variant, int64_t M, int64_t Cout, 
   ConvSplit s;
   TORCH_CHECK(variant >= 0, "conv: bad variant ", variant);
   if (variant >= 4096) {   // v2 tile kernel (conv_kernels.hip conv2_body): never split/persistent
-    TORCH_CHECK(variant < 4096 + 14, "conv: unknown v2 variant ", variant);
+    TORCH_CHECK(variant < 4096 + 15, "conv: unknown v2 variant ", variant);
     s.base = (int)variant;
     return s;
   }

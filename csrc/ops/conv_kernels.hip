@@ -1068,9 +1068,10 @@ constexpr int kLdsMax = 160 * 1024;
 // taps read it at row offsets r*W + s, and taps that fall outside the image (row/column padding or
 // a neighbouring image) are zeroed on the fragment. A is staged once instead of nine times.
 constexpr int kHaloMaxW = 63;
+constexpr int kHaloSmallW = 31;   // HALO == 2: a window sized for <= 31-wide images
 
 template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false,
-          bool HALO = false>
+          int HALO = 0>
 struct Conv2Geo {
   static constexpr int kBM = BM, kBN = BN;
   static constexpr int NT = 64 * NWM * NWN;
@@ -1078,7 +1079,8 @@ struct Conv2Geo {
   static constexpr int MI = WM / 32, NI = WN / 32;
   static constexpr int AI = BM * 8 / NT, BI = BN * 8 / NT;
   static constexpr int kBufBytes = (BM + BN) * kRowBytes;
-  static constexpr int kHaloRows = BM + 2 * kHaloMaxW + 2;   // window rows (max W)
+  // window rows (max W: kHaloMaxW, or kHaloSmallW for HALO == 2)
+  static constexpr int kHaloRows = BM + 2 * (HALO == 2 ? kHaloSmallW : kHaloMaxW) + 2;
   static constexpr int AIH = (kHaloRows * 8 + NT - 1) / NT;  // window loads per thread
   static constexpr int kWinBytes = AIH * NT / 8 * kRowBytes;
   // HALO: the window + a ring of NBUF per-tap weight buffers (NBUF - 1 taps in flight)
@@ -1306,7 +1308,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
 }
 
 template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false,
-          bool HALO = false>
+          int HALO = 0>
 __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
   using G = Conv2Geo<BM, BN, NWM, NWN, NBUF, EPI, BAND, HALO>;
   constexpr int NT = G::NT, WM = G::WM, WN = G::WN, MI = G::MI, NI = G::NI;
@@ -1639,20 +1641,21 @@ void conv2_kernel_occ4(ConvArgs a) {
 }
 
 // the 3x3 halo form (see Conv2Geo::HALO): 4 waves, a ring of NBR per-tap weight buffers --
-// 128x128: three (80 KB, two blocks per CU); 128x64: two (48 KB, three blocks per CU)
-template <int BM, int BN, int EPI>
+// 128x128: three (80 KB, two blocks per CU); 128x64: two (48 KB, three blocks per CU; with the
+// small window of <= 31-wide images 40 KB, four blocks per CU)
+template <int BM, int BN, int EPI, int HW>
 __global__ __launch_bounds__(256) void conv2_kernel_halo(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, true>(a, blockIdx.x);
+  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, HW>(a, blockIdx.x);
 #endif
 }
 
-template <int BM, int BN>
+template <int BM, int BN, int HW = 1>
 hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   if (a.c16 || a.ksplit != 1 || a.tpb != 1 || a.Cout % BN || a.R != 3 || a.S != 3 ||
       a.stride != 1 || a.pad != 1 || a.pad_w != 1 || a.Ho != a.H || a.Wo != a.W ||
-      a.W > kHaloMaxW || a.mapped)
+      a.W > (HW == 2 ? kHaloSmallW : kHaloMaxW) || a.mapped)
     return hipErrorInvalidValue;
   if (a.bnx == nullptr && (a.part != nullptr || a.bn_acc != nullptr) && a.add != nullptr)
     return hipErrorInvalidValue;
@@ -1660,11 +1663,11 @@ hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
   if (a.bnx != nullptr)
-    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2>), dim3(nwg), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW>), dim3(nwg), dim3(256), 0, st, a);
   else if (a.part != nullptr || a.bn_acc != nullptr)
-    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1>), dim3(nwg), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1, HW>), dim3(nwg), dim3(256), 0, st, a);
   else
-    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 0>), dim3(nwg), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 0, HW>), dim3(nwg), dim3(256), 0, st, a);
   return hipGetLastError();
 }
 
@@ -1711,11 +1714,11 @@ hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
 
 // v2 variant table (code 1024 + index): BM x BN tile, waves NWM x NWN, stage buffers
 constexpr int kV2Base = 4096;   // above every v1 code (split + 16 k, persistent + 256 p <= 1039)
-constexpr int kV2Count = 14;
+constexpr int kV2Count = 15;
 constexpr int kV2Tiles[kV2Count][2] = {{256, 128}, {256, 256}, {128, 128}, {256, 64}, {128, 256},
                                        {128, 64}, {64, 64}, {64, 128},
                                        {128, 128}, {128, 64}, {64, 128}, {64, 64},
-                                       {128, 128}, {128, 64}};
+                                       {128, 128}, {128, 64}, {128, 64}};
 
 hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
   switch (idx) {
@@ -1737,6 +1740,7 @@ hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
     // 3x3 / stride 1 / pad 1 halo forms (conv2_kernel_halo)
     case 12: return launch2_halo<128, 128>(a, st);
     case 13: return launch2_halo<128, 64>(a, st);
+    case 14: return launch2_halo<128, 64, 2>(a, st);   // <= 31-wide images: 4 blocks per CU
     default: return hipErrorInvalidValue;
   }
 }

@@ -215,7 +215,9 @@ def test_v2_variants_are_forward_and_dgrad_only():
     assert set(conv.v2_variants_for(64)) == {conv.V2 + v for v in (3, 5, 6, 9, 11)}
     assert set(conv.v2_variants_for(256)) == set(conv.V2_TILES) - set(conv.V2_HALO)
     assert set(conv.halo_variants_for(256, (3, 3), 1, 1, 14)) == set(conv.V2_HALO)
-    assert conv.halo_variants_for(64, (3, 3), 1, 1, 56) == [conv.V2 + 13]
+    assert conv.halo_variants_for(64, (3, 3), 1, 1, 56) == [conv.V2 + 13]   # no small window
+    assert conv.V2 + 14 in conv.halo_variants_for(64, (3, 3), 1, 1, 31)
+    assert conv.V2 + 14 not in conv.halo_variants_for(64, (3, 3), 1, 1, 32)
     assert not conv.halo_variants_for(256, (3, 3), 2, 1, 14)
     assert not conv.halo_variants_for(256, (3, 3), 1, 1, 64)
     assert not conv.halo_variants_for(256, (1, 1), 1, 0, 14)
