@@ -22,7 +22,7 @@ from typing import Tuple
 
 import torch
 
-from . import _ext
+from . import _ext, planstore
 
 Tensor = torch.Tensor
 TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}
@@ -739,84 +739,101 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
         plan.bwd_bn = plan.bwd if stride == 1 else MIOPEN
         plan.tuned = mode == "ours"
     else:
-        # Only the MFMA kernels are candidates: a captured step with MIOpen convolutions in it
-        # returned wrong gradients on replays that followed other GPU/host work, while the same
-        # step on these kernels alone stayed bit-identical run to run (tools/graph_mem_*.py,
-        # docs/perf.md "MIOpen inside a captured step"). ARENA_CONV=miopen keeps the library
-        # path for comparisons.
-        # (a random output gradient of the conv's output shape; no library call: F.conv2d here
-        # ran MIOpen's Find -- its naive and CK kernels -- once per shape, ~0.5 s of startup)
-        dy = torch.randn(x.shape[0], cout, ho, wo, device=x.device, dtype=x.dtype).contiguous(
-            memory_format=torch.channels_last)
-        t = {}
-        m_out = x.shape[0] * ho * wo
+        def tune() -> dict:
+            # Only the MFMA kernels are candidates: a captured step with MIOpen convolutions in it
+            # returned wrong gradients on replays that followed other GPU/host work, while the same
+            # step on these kernels alone stayed bit-identical run to run (tools/graph_mem_*.py,
+            # docs/perf.md "MIOpen inside a captured step"). ARENA_CONV=miopen keeps the library
+            # path for comparisons.
+            # (a random output gradient of the conv's output shape; no library call: F.conv2d here
+            # ran MIOpen's Find -- its naive and CK kernels -- once per shape, ~0.5 s of startup)
+            dy = torch.randn(x.shape[0], cout, ho, wo, device=x.device, dtype=x.dtype).contiguous(
+                memory_format=torch.channels_last)
+            t = {}
+            m_out = x.shape[0] * ho * wo
 
-        def fwd_time(v):
-            # timed the way the step runs it: statistics summed in the epilogue where _use_acc
-            # says so (into a scratch set), else per-tile partials plus the BN finalize launch
-            # that consumes them (charged as _FIN_PENALTY_US)
-            fin = _use_acc(m_out, v, cout)
-            us = _time(lambda: conv2d_fwd(x, w, stride, pad, v, with_stats=True, final=fin))
-            return us if fin else us + _FIN_PENALTY_US
+            def fwd_time(v):
+                # timed the way the step runs it: statistics summed in the epilogue where _use_acc
+                # says so (into a scratch set), else per-tile partials plus the BN finalize launch
+                # that consumes them (charged as _FIN_PENALTY_US)
+                fin = _use_acc(m_out, v, cout)
+                us = _time(lambda: conv2d_fwd(x, w, stride, pad, v, with_stats=True, final=fin))
+                return us if fin else us + _FIN_PENALTY_US
 
-        fns = {}
-        halo = lambda c: halo_variants_for(c, k, stride, pad, x.shape[3])  # noqa: E731
-        for v in (variants_for(cout) + v2_variants_for(cout) + halo(cout)
-                  + split_variants_for(m_out, cout, cin * k[0] * k[1])):
-            fns[("fwd", v)] = (lambda v=v: fwd_time(v))
-        if stride == 1:
-            m_in = x.shape[0] * x.shape[2] * x.shape[3]
-            for v in (variants_for(cin) + v2_variants_for(cin) + halo(cin)
-                      + split_variants_for(m_in, cin, cout * k[0] * k[1])):
-                fns[("bwd", v)] = (lambda v=v: _time(lambda: conv2d_bwd_data(dy, w, pad, v)))
-            if _BN_LINKS:   # the linked form: a BN input, ReLU bits and mean of x's shape
-                bnx = torch.randn_like(x)
-                bmask = torch.randint(0, 256, (m_in * cin // 8,), device=x.device,
-                                      dtype=torch.uint8)
-                bmean = torch.zeros(cin, device=x.device)
-                for v in variants_for(cin) + v2_variants_for(cin) + halo(cin):
-                    fns[("bwdbn", v)] = (lambda v=v: _time(lambda: conv2d_bwd_data(
-                        dy, w, pad, v, bn=(bnx, bmask, bmean))))
-        else:   # phase decomposition: per-phase heuristic (-1) or one tile for every phase
-            hw = (x.shape[2], x.shape[3])
-            for v in [-1] + variants_for(cin) + v2_variants_for(cin):
-                fns[("bwd", v)] = (lambda v=v: _time(
-                    lambda: conv2d_bwd_data_strided(dy, w, hw, stride, pad, v)))
-        for c in wg:
-            fns[("wgrad", c)] = (lambda c=c: _time(
-                lambda: conv2d_wgrad(x, dy, k, stride, pad, c[0], c[1])))
-        ext = _ext.load()
-        ext.bn_acc_scratch(True)
-        try:
-            for key_, fn in fns.items():
-                t[key_] = fn()
-            # persistent forms of the fastest base variants
-            for v in persist_variants_for(m_out, cout, _best(t, "fwd", 3)):
+            fns = {}
+            halo = lambda c: halo_variants_for(c, k, stride, pad, x.shape[3])  # noqa: E731
+            for v in (variants_for(cout) + v2_variants_for(cout) + halo(cout)
+                      + split_variants_for(m_out, cout, cin * k[0] * k[1])):
                 fns[("fwd", v)] = (lambda v=v: fwd_time(v))
-                t[("fwd", v)] = fns[("fwd", v)]()
             if stride == 1:
-                for v in persist_variants_for(m_in, cin, _best(t, "bwd", 3)):
-                    fns[("bwd", v)] = (lambda v=v: _time(lambda: conv2d_bwd_data(dy, w, pad, v)))
-                    t[("bwd", v)] = fns[("bwd", v)]()
-            # One timing per candidate picks the lucky one among near-equal variants (the
-            # choices moved run to run by ~1 % of the step): the 3 fastest of each direction are
-            # timed twice more, interleaved, and ranked by their median.
-            kinds = ("fwd", "bwd", "wgrad") + (
-                ("bwdbn",) if any(k[0] == "bwdbn" for k in fns) else ())
-            finals = {kind: _best(t, kind, 3) for kind in kinds}
-            reps = {(kind, c): [t[(kind, c)]] for kind, cs in finals.items() for c in cs}
-            for _ in range(2):
-                for key_ in reps:
-                    reps[key_].append(fns[key_]())
-            for key_, vs in reps.items():
-                t[key_] = sorted(vs)[1]
-        finally:
-            ext.bn_acc_scratch(False)
-        for kind in kinds:
-            best = min(t[(kind, c)] for c in finals[kind])
-            choice = next(c for c in finals[kind] if t[(kind, c)] == best)
-            setattr(plan, "bwd_bn" if kind == "bwdbn" else kind, choice)
-        plan.times = {f"{kd}:{c}": round(v, 1) for (kd, c), v in t.items()}
+                m_in = x.shape[0] * x.shape[2] * x.shape[3]
+                for v in (variants_for(cin) + v2_variants_for(cin) + halo(cin)
+                          + split_variants_for(m_in, cin, cout * k[0] * k[1])):
+                    fns[("bwd", v)] = (lambda v=v: _time(
+                        lambda: conv2d_bwd_data(dy, w, pad, v)))
+                if _BN_LINKS:   # the linked form: a BN input, ReLU bits and mean of x's shape
+                    bnx = torch.randn_like(x)
+                    bmask = torch.randint(0, 256, (m_in * cin // 8,), device=x.device,
+                                          dtype=torch.uint8)
+                    bmean = torch.zeros(cin, device=x.device)
+                    bsums = torch.zeros(2 * cin, dtype=torch.float64, device=x.device)
+                    for v in variants_for(cin) + v2_variants_for(cin) + halo(cin):
+                        # timed in the epilogue form the step will run: fp64 sums into the BN's
+                        # backward set where _use_link_acc picks it, else per-tile partials
+                        acc = bsums if _use_link_acc(m_in, v, cin) else None
+                        fns[("bwdbn", v)] = (lambda v=v, acc=acc: _time(lambda: conv2d_bwd_data(
+                            dy, w, pad, v, bn=(bnx, bmask, bmean), bn_acc=acc)))
+            else:   # phase decomposition: per-phase heuristic (-1) or one tile for every phase
+                hw = (x.shape[2], x.shape[3])
+                for v in [-1] + variants_for(cin) + v2_variants_for(cin):
+                    fns[("bwd", v)] = (lambda v=v: _time(
+                        lambda: conv2d_bwd_data_strided(dy, w, hw, stride, pad, v)))
+            for c in wg:
+                fns[("wgrad", c)] = (lambda c=c: _time(
+                    lambda: conv2d_wgrad(x, dy, k, stride, pad, c[0], c[1])))
+            ext = _ext.load()
+            ext.bn_acc_scratch(True)
+            try:
+                for key_, fn in fns.items():
+                    t[key_] = fn()
+                # persistent forms of the fastest base variants
+                for v in persist_variants_for(m_out, cout, _best(t, "fwd", 3)):
+                    fns[("fwd", v)] = (lambda v=v: fwd_time(v))
+                    t[("fwd", v)] = fns[("fwd", v)]()
+                if stride == 1:
+                    for v in persist_variants_for(m_in, cin, _best(t, "bwd", 3)):
+                        fns[("bwd", v)] = (lambda v=v: _time(
+                            lambda: conv2d_bwd_data(dy, w, pad, v)))
+                        t[("bwd", v)] = fns[("bwd", v)]()
+                # One timing per candidate picks the lucky one among near-equal variants (the
+                # choices moved run to run by ~1 % of the step): the 3 fastest of each direction are
+                # timed twice more, interleaved, and ranked by their median.
+                kinds = ("fwd", "bwd", "wgrad") + (
+                    ("bwdbn",) if any(k[0] == "bwdbn" for k in fns) else ())
+                finals = {kind: _best(t, kind, 3) for kind in kinds}
+                reps = {(kind, c): [t[(kind, c)]] for kind, cs in finals.items() for c in cs}
+                for _ in range(2):
+                    for key_ in reps:
+                        reps[key_].append(fns[key_]())
+                for key_, vs in reps.items():
+                    t[key_] = sorted(vs)[1]
+            finally:
+                ext.bn_acc_scratch(False)
+            out = {}
+            for kind in kinds:
+                best = min(t[(kind, c)] for c in finals[kind])
+                choice = next(c for c in finals[kind] if t[(kind, c)] == best)
+                out["bwd_bn" if kind == "bwdbn" else kind] = choice
+            out["times"] = {f"{kd}:{c}": round(v, 1) for (kd, c), v in t.items()}
+            return out
+
+        # one decision per job: rank 0 times, every rank adopts (or the ARENA_CONV_PLAN file)
+        got = planstore.decide("conv", key[:4] + key[5:], x.device, tune)
+        for f in ("fwd", "bwd", "wgrad", "bwd_bn"):
+            if f in got:
+                v = got[f]
+                setattr(plan, f, tuple(v) if isinstance(v, list) else v)
+        plan.times = dict(got.get("times", {}))
         plan.tuned = True
     _PLANS[key] = plan
     return plan
@@ -1169,14 +1186,19 @@ def _stem_plan(z: Tensor, w16: Tensor) -> Tuple[int, Tuple[int, int]]:
         if _mode() == "ours":
             _STEM_PLANS[key] = plan
         return plan
-    tf = {v: _time(lambda: ext.conv_fwd_ex(z, w16, 1, 2, 2, ho, wo, v, True, None, None, [],
-                                            True)) for v in fvs}
-    dy = torch.randn(z.shape[0], w16.shape[0], ho, wo, device=z.device, dtype=z.dtype).contiguous(
-        memory_format=torch.channels_last)
-    tw = {c: _time(lambda: ext.conv_wgrad_ex(z, dy, 4, 4, 1, 2, 2, c[0], c[1], False, 1.0, True))
-          for c in wcs}
-    plan = (min(tf, key=tf.get), min(tw, key=tw.get))
+
+    def tune() -> dict:
+        tf = {v: _time(lambda: ext.conv_fwd_ex(z, w16, 1, 2, 2, ho, wo, v, True, None, None, [],
+                                                True)) for v in fvs}
+        dy = torch.randn(z.shape[0], w16.shape[0], ho, wo, device=z.device,
+                         dtype=z.dtype).contiguous(memory_format=torch.channels_last)
+        tw = {c: _time(lambda: ext.conv_wgrad_ex(z, dy, 4, 4, 1, 2, 2, c[0], c[1], False, 1.0,
+                                                 True)) for c in wcs}
+        if os.environ.get("ARENA_CONV_LOG") == "1":
+            print(f"stem {tuple(z.shape)}: {tf} {tw}", flush=True)
+        return {"fwd": min(tf, key=tf.get), "wgrad": list(min(tw, key=tw.get))}
+
+    got = planstore.decide("stem", (key[0], key[1], key[3]), z.device, tune)
+    plan = (int(got["fwd"]), tuple(got["wgrad"]))
     _STEM_PLANS[key] = plan
-    if os.environ.get("ARENA_CONV_LOG") == "1":
-        print(f"stem {tuple(z.shape)}: fwd={plan[0]} wgrad={plan[1]} {tf} {tw}", flush=True)
     return plan

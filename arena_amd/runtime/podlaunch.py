@@ -14,7 +14,9 @@ imports torch or HIP), gives each the torch.distributed environment, and supervi
   ``GROUP_RANK`` / ``GROUP_WORLD_SIZE`` = pod index / pod count (torchrun's names);
 * the first rank that exits non-zero takes the others down (SIGTERM, then SIGKILL after a grace
   period) and the launcher exits with that code -- a crashed rank must not leave its peers
-  blocked in a collective until the RCCL timeout;
+  blocked in a collective until the RCCL timeout. Every rank runs in its own process session and
+  is signalled as a process GROUP, so the real rank behind a compound command
+  (``cd /w && python train.py``: a grandchild of the launcher) goes down with its shell;
 * SIGTERM/SIGINT to the launcher (pod deletion, ``arena delete``) is forwarded to every rank;
 * the ranks' stdout/stderr are forwarded line by line (one pod log, never two ranks' output
   spliced into one line); ``ARENA_RANK_TAG_OUTPUT=1`` prefixes every line with ``[<rank>]``, like
@@ -113,8 +115,9 @@ class _Gang:
         self.stopping = False
 
     def start(self, argv: List[str], env: Dict[str, str]) -> None:
+        # own session: the rank and everything it starts form one process group (pgid == pid)
         p = subprocess.Popen(argv, env=env, stdin=subprocess.DEVNULL, stdout=subprocess.PIPE,
-                             stderr=subprocess.PIPE)
+                             stderr=subprocess.PIPE, start_new_session=True)
         self.procs.append(p)
         prefix = f"[{env['RANK']}] ".encode() if self.tag else b""
         for src, dst in ((p.stdout, sys.stdout.buffer), (p.stderr, sys.stderr.buffer)):
@@ -128,19 +131,35 @@ class _Gang:
             t.join(max(0.0, deadline - time.time()))
 
     def signal_all(self, sig: int) -> None:
+        """Signal every rank's process group -- also of a rank whose shell already exited, since
+        a grandchild it started may still hold the group (and a GPU)."""
         for p in self.procs:
-            if p.poll() is None:
-                try:
-                    p.send_signal(sig)
-                except OSError:
-                    pass
+            try:
+                os.killpg(p.pid, sig)
+            except (ProcessLookupError, PermissionError):
+                pass
+            except OSError:
+                if p.poll() is None:
+                    try:
+                        p.send_signal(sig)
+                    except OSError:
+                        pass
+
+    def _group_alive(self, p: subprocess.Popen) -> bool:
+        if p.poll() is None:
+            return True
+        try:
+            os.killpg(p.pid, 0)
+            return True
+        except OSError:
+            return False
 
     def stop(self) -> None:
         """SIGTERM every live rank, SIGKILL what is left after the grace period."""
         self.stopping = True
         self.signal_all(signal.SIGTERM)
         deadline = time.time() + self.grace_s
-        while time.time() < deadline and any(p.poll() is None for p in self.procs):
+        while time.time() < deadline and any(self._group_alive(p) for p in self.procs):
             time.sleep(0.05)
         self.signal_all(signal.SIGKILL)
         for p in self.procs:
@@ -165,6 +184,57 @@ class _Gang:
             time.sleep(0.05)
 
 
+def run_gang(argvs: List[List[str]], envs: List[Dict[str, str]], grace_s: float = 10.0,
+             tag: bool = False) -> int:
+    """Start one process per (argv, env), supervise them as a gang (first failure takes the rest
+    down), forward SIGTERM/SIGINT, relay their output line by line; the gang's exit code."""
+    gang = _Gang(grace_s, tag=tag)
+    prev = {}
+
+    def forward(sig, _frame):
+        gang.stop()
+        gang.drain(1.0)
+        sys.exit(128 + sig)
+
+    for s in (signal.SIGTERM, signal.SIGINT):
+        prev[s] = signal.signal(s, forward)
+    try:
+        for a, e in zip(argvs, envs):
+            gang.start(a, e)
+        rc = gang.wait()
+        gang.drain()
+        return rc
+    finally:
+        if any(p.poll() is None for p in gang.procs):
+            gang.stop()
+        for s, h in prev.items():
+            signal.signal(s, h)
+
+
+def local_world_envs(nproc: int, env: Optional[Dict[str, str]] = None,
+                     master_port: Optional[int] = None) -> List[Dict[str, str]]:
+    """torch.distributed environments of a one-node world of ``nproc`` ranks on this host (what
+    ``torchrun --standalone --nproc-per-node nproc`` would set), for a launcher that starts the
+    ranks itself: RANK = LOCAL_RANK = i, WORLD_SIZE = LOCAL_WORLD_SIZE = nproc, rendezvous at
+    127.0.0.1 on a free port."""
+    base = dict(os.environ if env is None else env)
+    if master_port is None:
+        import socket
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            master_port = s.getsockname()[1]
+    base.update(ARENA_RANKS_PER_POD=str(nproc), ARENA_PODS="1", ARENA_POD_INDEX="0")
+    base.pop("ARENA_RANK_LOCAL_IDS", None)
+    base.pop("ARENA_NODE_RANKS", None)
+    out = []
+    for e in rank_envs(base):
+        e.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(master_port))
+        for k in ("ARENA_RANKS_PER_POD", "ARENA_PODS", "ARENA_POD_INDEX"):
+            e.pop(k, None)
+        out.append(e)
+    return out
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     env = dict(os.environ)
     command = env.get("ARENA_RANK_COMMAND", "")
@@ -177,21 +247,9 @@ def main(argv: Optional[List[str]] = None) -> int:
         print("podlaunch: no command (ARENA_RANK_COMMAND or arguments after --)", file=sys.stderr)
         return 2
     envs = rank_envs(env)
-    gang = _Gang(float(env.get("ARENA_RANK_GRACE_S", "10")),
-                 tag=env.get("ARENA_RANK_TAG_OUTPUT", "0") == "1")
-
-    def forward(sig, _frame):
-        gang.stop()
-        gang.drain(1.0)
-        sys.exit(128 + sig)
-
-    signal.signal(signal.SIGTERM, forward)
-    signal.signal(signal.SIGINT, forward)
-    for e in envs:
-        gang.start(rank_argv(command, e), e)
-    rc = gang.wait()
-    gang.drain()
-    return rc
+    return run_gang([rank_argv(command, e) for e in envs], envs,
+                    float(env.get("ARENA_RANK_GRACE_S", "10")),
+                    tag=env.get("ARENA_RANK_TAG_OUTPUT", "0") == "1")
 
 
 if __name__ == "__main__":

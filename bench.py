@@ -11,6 +11,21 @@ gradient all-reduce when N>1, Adam update, device-side data gather + epoch reshu
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
+``--gpus N`` is honoured either way. Under torchrun (``WORLD_SIZE`` set) every rank is already a
+process. Without it and N > 1, this process becomes the launcher before it imports torch or touches
+a GPU: it starts N copies of itself, one per GPU, with RANK / LOCAL_RANK / WORLD_SIZE /
+LOCAL_WORLD_SIZE / MASTER_ADDR=127.0.0.1 / a free MASTER_PORT (``runtime.podlaunch``'s gang: the
+first failing rank takes the others down, the launcher exits with its code; never exec), and relays
+their output -- rank 0's JSON line is the launcher's stdout. That is the reference's launcher role
+(``mpirun`` over the hostfile, charts/tf-horovod/templates/config.yaml:67-84,
+charts/tf-horovod/README.md:66-69 ``hvd-distribute.sh <hosts> <gpus>``).
+
+``--same-gpu`` (or ``ARENA_BENCH_SAME_GPU=1``) emulates an N-GPU node on one GPU: all ranks on
+device 0, a gloo process group (RCCL refuses two ranks per device), the xGMI collectives over
+same-device hipIpc mappings. It exercises the whole N > 1 path (sharded optimizers at W = N,
+hipGraph-captured collectives, replica verification); its throughput is N ranks time-sharing one
+GPU, so the line says ``"emulated"`` and is NOT a scaling number.
+
 The MNIST steps run as replays of one hipGraph whose length divides the warmup, the timed step
 count and the epoch; ``config.exec`` reports how many timed steps were replayed vs run eagerly.
 The same line also carries ``resnet50_images_per_s`` (all ranks) / ``resnet50_ms_per_step``
@@ -30,7 +45,13 @@ import time
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); started by this script unless under torchrun")
+    ap.add_argument("--same-gpu", action="store_true",
+                    default=os.environ.get("ARENA_BENCH_SAME_GPU", "0") == "1",
+                    help="emulate --gpus N on one GPU (all ranks on device 0, gloo + xGMI "
+                         "same-device mappings): a correctness run of the N>1 path, not a "
+                         "scaling number")
     ap.add_argument("--steps", type=int, default=3000)
     ap.add_argument("--warmup", type=int, default=300)
     ap.add_argument("--impl", choices=["fused", "torch"], default="fused",
@@ -55,6 +76,26 @@ def parse():
     ap.add_argument("--resnet-verify-every", type=int, default=10,
                     help="N>1: replica bit-identity check every K timed ResNet steps (untimed)")
     return ap.parse_args()
+
+
+def max_over_ranks(x: float, dev) -> float:
+    """MAX of a host float over all ranks (the slowest rank sets a synchronous step). gloo (the
+    same-GPU emulation) reduces on the host, RCCL on the device."""
+    import torch
+    import torch.distributed as dist
+    on_dev = dist.get_backend() == "nccl"
+    e = torch.tensor([x], dtype=torch.float64, device=dev if on_dev else "cpu")
+    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    return float(e.item())
+
+
+def _plan_stats() -> dict:
+    """How the conv plans were decided (tuned here / received from rank 0 / from the plan file)
+    and the seconds spent timing candidates."""
+    from arena_amd.ops import planstore
+    st = planstore.stats()
+    st["tune_s"] = round(st["tune_s"], 2)
+    return st
 
 
 def bench_resnet50(dev, steps: int, batch: int, world: int = 1, verify_every: int = 10) -> dict:
@@ -113,9 +154,7 @@ def bench_resnet50(dev, steps: int, batch: int, world: int = 1, verify_every: in
         if check is not None:
             check.maybe(done)
     if world > 1:
-        e = torch.tensor([dt], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        dt = float(e.item())
+        dt = max_over_ranks(dt, dev)
         check.verify(steps)
     loss = float(g_loss)
     if not loss == loss:
@@ -127,28 +166,61 @@ def bench_resnet50(dev, steps: int, batch: int, world: int = 1, verify_every: in
                                "optimizer": "momentum-sgd fp32 masters", "timed_steps": steps,
                                "comm": cnn_bench.comm_name(opt) if world > 1 else "none",
                                "exec": f"hipgraph[whole step] {steps}/{steps} replays",
-                               "final_loss": round(loss, 4)}}
+                               "final_loss": round(loss, 4),
+                               "conv_plan": _plan_stats()}}
     if check is not None:
         out["resnet50_config"]["replicas_verified"] = check.checks
     return out
 
 
+def launch_ranks(args, argv=None) -> int:
+    """Launcher mode (``--gpus N > 1`` and no ``WORLD_SIZE``): start N ranks of this script and
+    supervise them as a gang. Runs before torch is imported (no GPU call in this process)."""
+    from arena_amd.runtime.podlaunch import local_world_envs, run_gang
+    envs = local_world_envs(args.gpus)
+    for e in envs:
+        e["ARENA_BENCH_LAUNCHED"] = "1"
+        if args.same_gpu:
+            e["ARENA_BENCH_SAME_GPU"] = "1"
+    argv = [sys.executable, os.path.abspath(__file__)] + list(sys.argv[1:] if argv is None
+                                                               else argv)
+    print(f"[bench] launching {args.gpus} ranks (127.0.0.1:{envs[0]['MASTER_PORT']}"
+          f"{', same GPU' if args.same_gpu else ''})", file=sys.stderr, flush=True)
+    return run_gang([argv] * args.gpus, envs, grace_s=15.0)
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    if os.environ.get("ARENA_BENCH_ENV_PROBE") == "1":
+        # test hook (tests/test_bench_launch.py): report the rank environment, touch no GPU
+        keys = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+                "MASTER_PORT", "ARENA_BENCH_SAME_GPU", "ARENA_BENCH_LAUNCHED")
+        print(json.dumps({k: os.environ.get(k) for k in keys}), flush=True)
+        if os.environ.get("ARENA_BENCH_PROBE_FAIL_RANK") == os.environ.get("RANK"):
+            sys.exit(3)
+        time.sleep(float(os.environ.get("ARENA_BENCH_PROBE_SLEEP", "0")))
+        return
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    same_gpu = args.same_gpu and world > 1
     if world != args.gpus and rank == 0:
         print(f"[bench] note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE",
               file=sys.stderr)
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = 0 if same_gpu else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     pg = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if same_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
         pg = dist.group.WORLD
 
     from arena_amd.data.mnist import load_mnist
@@ -210,9 +282,7 @@ def main():
     torch.cuda.synchronize()
     elapsed = t1 - t0
     if world > 1:
-        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        elapsed = max_over_ranks(elapsed, dev)
 
     extra = {}
     if check is not None:
@@ -256,9 +326,14 @@ def main():
             "data": f"synthetic ({data.source} MNIST-shaped uint8 60k/10k, device-resident)",
             "config": {"model": f"mnist_mlp_784-{args.hidden}-10 (relu, dropout 0.9, adam 1e-3)",
                        "global_batch": world * cfg.batch, "seq_len": None,
-                       "parallelism": f"dp{world}", "impl": args.impl, "exec": mode},
+                       "parallelism": f"dp{world}", "impl": args.impl, "exec": mode,
+                       "launch": "bench.py" if os.environ.get("ARENA_BENCH_LAUNCHED") else
+                       ("torchrun" if world > 1 else "single")},
             **extra,
         }
+        if same_gpu:
+            out["emulated"] = (f"{world} ranks time-sharing ONE GPU (gloo + same-device xGMI "
+                               f"mappings): checks the N>1 path, not a scaling number")
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -201,6 +201,48 @@ def test_podlaunch_failing_rank_takes_the_gang_down(tmp_path):
     assert {e["WORLD_SIZE"] for e in envs} == {"12"} and envs[0]["GROUP_RANK"] == "2"
 
 
+def _pid_alive(pid: int) -> bool:
+    try:
+        with open(f"/proc/{pid}/status") as f:
+            return "\nState:\tZ" not in f.read()      # a zombie has exited
+    except OSError:
+        return False
+
+
+def test_podlaunch_takes_down_grandchildren_of_compound_commands(tmp_path):
+    """A compound rank command (``cd dir && python ...`` inside a subshell) runs the real rank as
+    a grandchild of the launcher; when a peer rank fails, the whole rank's process group must be
+    signalled, not just its shell (podlaunch.py:116)."""
+    import subprocess
+    prog = ("import os, time; open(os.path.join(%r, 'pid' + os.environ['RANK']), 'w')"
+            ".write(str(os.getpid())); time.sleep(120)") % str(tmp_path)
+    cmd = (f'if [ "$RANK" = 1 ]; then sleep 2; exit 5; fi; cd {tmp_path} && '
+           f'( {PY} -c "{prog}" ); true')
+    env = dict(os.environ, ARENA_RANKS_PER_POD="3", ARENA_PODS="1", ARENA_POD_INDEX="0",
+               ARENA_RANK_GRACE_S="2", PYTHONPATH=REPO, ARENA_RANK_COMMAND=cmd)
+    r = subprocess.run([PY, "-m", "arena_amd.runtime.podlaunch"], env=env, timeout=60)
+    assert r.returncode == 5
+    pids = [int((tmp_path / f"pid{k}").read_text()) for k in (0, 2)]
+    deadline = time.time() + 10
+    while time.time() < deadline and any(_pid_alive(p) for p in pids):
+        time.sleep(0.1)
+    assert not any(_pid_alive(p) for p in pids), pids
+
+
+def test_local_world_envs_for_self_launching_bench():
+    """bench.py --gpus N without torchrun: the environments it gives its N ranks."""
+    from arena_amd.runtime import podlaunch
+    envs = podlaunch.local_world_envs(4, {"PATH": "/bin", "ARENA_RANK_LOCAL_IDS": "5,6"},
+                                      master_port=29123)
+    assert [e["RANK"] for e in envs] == ["0", "1", "2", "3"]
+    assert [e["LOCAL_RANK"] for e in envs] == ["0", "1", "2", "3"]
+    for e in envs:
+        assert e["WORLD_SIZE"] == "4" and e["LOCAL_WORLD_SIZE"] == "4"
+        assert e["MASTER_ADDR"] == "127.0.0.1" and e["MASTER_PORT"] == "29123"
+        assert e["GROUP_RANK"] == "0" and e["GROUP_WORLD_SIZE"] == "1" and e["PATH"] == "/bin"
+        assert "ARENA_RANK_LOCAL_IDS" not in e and "ARENA_PODS" not in e
+
+
 def test_allreduce_worker_fault_fails_job_and_reaps(env, monkeypatch):
     monkeypatch.setenv("ARENA_FAULT_POD", "fi-tf-horovod-0")
     monkeypatch.setenv("ARENA_FAULT_AFTER_MS", "300")
