@@ -91,37 +91,23 @@ def build(args, dev, world):
     if master and (getattr(args, "dtype", "bf16") != "bf16" or dev.type != "cuda"):
         raise SystemExit("--master_weights on needs --dtype bf16 on a GPU (the weights become "
                          "bf16 and the update runs in the HIP multi-tensor kernel)")
-    if master and world > 1:
-        # data parallel keeps the bf16-weight design through the sharded xGMI optimizer; it
-        # needs every rank's GPU mapped into every rank (one node): decided collectively
-        from ..parallel import xgmi
-        ok = getattr(args, "comm", "auto") != "rccl" and xgmi.usable()
-        if not ok:
-            if mw == "on":
-                raise SystemExit("--master_weights on with several ranks needs the xGMI "
-                                 "collective (single node, --comm auto|xgmi)")
-            master = False   # fp32 weights + DistributedOptimizer (RCCL) instead
     opt = None
     if master and world > 1:
-        from ..parallel.xgmi import XgmiUnavailable
+        # data parallel keeps the bf16-weight design: ShardedMasterSGD over the xGMI kernels
+        # where every rank's GPU is mapped into every rank (one node), else over RCCL
+        # reduce-scatter / shard update / all-gather (decided collectively: all ranks agree)
         from ..parallel.zero import ShardedMasterSGD
-        # every parameter on one registered communicator: bf16 conv/fc weights with fp32
-        # masters, and the fp32 BN scales/shifts + biases (no decay) as fp32 tail buckets
-        try:
-            opt = ShardedMasterSGD(
-                [{"params": decay, "weight_decay": args.weight_decay},
-                 {"params": no_decay, "weight_decay": 0.0, "weights": "fp32"}],
-                lr=args.learning_rate, momentum=args.momentum, bucket_mb=args.bucket_mb)
-        except XgmiUnavailable as e:
-            # the peer mappings or the self-test failed on some rank (all ranks learn it
-            # together): the parameters were not re-bound yet, so the RCCL path can take over
-            if mw == "on":
-                raise
-            print(f"[rank {hvd.rank()}] xGMI communicator unavailable ({e}); "
-                  f"fp32 weights + DistributedOptimizer instead", file=sys.stderr, flush=True)
-            master = False
+        comm = getattr(args, "comm", "auto")
+        opt = ShardedMasterSGD(
+            [{"params": decay, "weight_decay": args.weight_decay},
+             {"params": no_decay, "weight_decay": 0.0, "weights": "fp32"}],
+            lr=args.learning_rate, momentum=args.momentum, bucket_mb=args.bucket_mb,
+            backend="rccl" if comm == "rccl" else comm, order=list(model.parameters()))
+        if hvd.rank() == 0 and opt.backend != "xgmi" and comm == "auto":
+            print("[rank 0] ShardedMasterSGD over RCCL (ranks cannot map each other's GPUs)",
+                  file=sys.stderr, flush=True)
     if opt is not None:
-        pass
+        pass                   # data parallel, sharded
     elif master:
         # conv/fc weights live in bf16 (fp32 masters inside MasterSGD): no per-step casts
         from ..ops.optim import MasterSGD, OptimizerGroup
@@ -150,7 +136,7 @@ def comm_name(opt) -> str:
     """How the optimizer moves gradients (for logs and the JSON line)."""
     from ..parallel.zero import ShardedMasterSGD
     if isinstance(opt, ShardedMasterSGD):
-        return f"xgmi-sharded-sgd[{len(opt.buckets)} buckets]"
+        return f"{opt.backend}-sharded-sgd[{len(opt.buckets)} buckets]"
     c = getattr(opt, "comm", None)
     return c if isinstance(c, str) else "none"
 
@@ -159,7 +145,7 @@ def comms_of(opt) -> list:
     """The xGMI communicators an optimizer owns (for ReplicaCheck's barrier-timeout check)."""
     from ..parallel.zero import ShardedMasterSGD
     if isinstance(opt, ShardedMasterSGD):
-        return [opt.comm]
+        return [opt.comm]       # None on the RCCL backend (ReplicaCheck skips it)
     return [getattr(opt, "xgmi", None)]
 
 

@@ -143,3 +143,12 @@ def mt_sgd_master(grads: Sequence[Tensor], offsets: Sequence[int], master: Tenso
     also writes the rounded bf16 weights into ``wbf`` (see ``mt_sgd_master_kernel``)."""
     _impl(master).mt_sgd_master(list(grads), [int(o) for o in offsets], master, mom, wbf,
                                 float(lr), float(momentum), float(weight_decay))
+
+
+def shard_sgd(grad: Tensor, w32: Tensor, mom: Tensor, wbf: Optional[Tensor] = None, *, lr: float,
+              momentum: float, weight_decay: float, scale: float) -> None:
+    """Momentum SGD over one flat range (a rank's shard of a reduce-scattered bucket):
+    d = grad * scale + wd * w32; mom = momentum * mom + d; w32 -= lr * mom; with bf16 ``grad``
+    the fp32 ``w32`` are masters and ``wbf`` receives the rounded bf16 weights."""
+    _impl(w32).shard_sgd(grad, w32, mom, wbf, float(lr), float(momentum), float(weight_decay),
+                         float(scale))

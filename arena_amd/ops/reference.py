@@ -282,3 +282,12 @@ def mt_sgd_master(grads, offsets, master, mom, wbf, lr, momentum, weight_decay):
         m.mul_(momentum).add_(_storage_flat(g).float() + weight_decay * w)
         w.sub_(lr * m)
         wbf[off:off + n].copy_(w)
+
+
+def shard_sgd(grad, w32, mom, wbf, lr, momentum, weight_decay, scale):
+    """CPU reference of the HIP ``shard_sgd`` kernel (same operation order)."""
+    d = grad.float() * scale + weight_decay * w32
+    mom.mul_(momentum).add_(d)
+    w32.sub_(lr * mom)
+    if wbf is not None:
+        wbf.copy_(w32)

@@ -1,24 +1,35 @@
-"""Sharded mixed-precision momentum SGD for data-parallel CNN training over xGMI.
+"""Sharded mixed-precision momentum SGD for data-parallel CNN training (xGMI or RCCL).
 
 The single-GPU ResNet path keeps conv/linear weights in bf16 with fp32 masters updated by one
 multi-tensor kernel (:class:`arena_amd.ops.optim.MasterSGD`). Data parallel used to give that up:
 Horovod's ``DistributedOptimizer`` moves fp32 gradients of fp32 weights, so every step cast the
-weights to bf16, the gradients back to fp32, and pushed twice the bytes over xGMI.
+weights to bf16, the gradients back to fp32, and pushed twice the bytes over the links.
 
 :class:`ShardedMasterSGD` keeps the single-GPU design across ranks (ZeRO-1 style), for every
-parameter of the model on ONE registered communicator:
+parameter of the model:
 
-* bf16 parameters (conv/fc weights) live in that rank's registered xGMI weight buffer (the
-  model's parameters are views into it); fp32 parameters (BatchNorm scales/shifts, biases) live in
-  an fp32 tail region of the same buffer;
-* gradient buckets (reverse registration order, ~``bucket_mb`` each, never mixing dtypes or
-  param groups) are packed into the registered staging buffer as soon as their last gradient is
-  produced (post-accumulate hooks, on a comm stream, overlapped with the rest of backward);
-* one kernel per bucket then reduce-scatters the gradients (fp32 sums in a fixed rank order),
-  applies momentum SGD with weight decay to the rank's chunk (``xgmi_sgd_bf16``: fp32 masters,
-  rounded bf16 weights all-gathered; ``xgmi_sgd_f32``: the fp32 weights are the masters) and
-  all-gathers the result into every rank's weight buffer -- the bytes of one allreduce, no
-  separate optimizer pass;
+* bf16 parameters (conv/fc weights) live in one flat bf16 weight buffer (the model's parameters
+  are views into it); fp32 parameters (BatchNorm scales/shifts, biases) live in an fp32 region
+  behind it;
+* gradient buckets of ~``bucket_mb`` are formed in gradient-readiness order (reverse model
+  order, ``order=``). A bucket may hold a bf16 and an fp32 sub-range side by side, so a block's
+  BN parameters travel with the conv weights whose gradients become ready at the same time
+  instead of in one fp32 tail bucket that can only launch after the whole backward. The
+  input-side bucket -- the last one ready, whose update nothing can overlap -- is capped at
+  ``last_bucket_mb``;
+* each bucket is packed as soon as its last gradient is produced (post-accumulate hooks, on a
+  comm stream, overlapped with the rest of backward) and updated by a reduce-scatter -> fp32
+  shard update -> all-gather, the bytes of one allreduce and no separate optimizer pass:
+
+  - ``backend="xgmi"`` (one node, every rank's GPU mapped into every rank): one kernel per
+    sub-range over hipIpc peer memory (``xgmi_sgd_bf16`` / ``xgmi_sgd_f32``: fp32 sums in a fixed
+    rank order, the rank's chunk updated, rounded weights written to every rank's buffer);
+  - ``backend="rccl"`` (ranks that cannot map each other: multi-pod, multi-node):
+    ``reduce_scatter_tensor`` of the bucket's bf16 (or fp32) range, the ``shard_sgd`` HIP kernel
+    on the owned equal-size shard, ``all_gather_into_tensor`` of the updated weights. bf16 buckets
+    reduce in bf16 by default (the bytes the xGMI path moves); ``rccl_reduce_fp32=True`` reduces
+    fp32 copies instead (exact sums, twice the bytes);
+  - ``"auto"``: xgmi when ``xgmi.usable`` and the communicator comes up on every rank, else rccl;
 * every rank ends each step with bit-identical weights (``--verify_every`` checks it).
 
 Update timing. With ``overlap=True`` (default) a bucket's update runs during ``backward()`` as
@@ -35,13 +46,12 @@ arrived (unused parameters: zero gradient, as Horovod) and joins the comm stream
   a captured hipGraph bakes the values in at capture).
 
 Masters and momentum are full-length arrays of which each rank updates only the chunks it
-owns; :meth:`state_dict` reassembles them. Requires the xGMI collective (``xgmi.usable``); the CNN
-bench falls back to fp32 weights + ``DistributedOptimizer`` (RCCL) elsewhere.
+owns; :meth:`state_dict` reassembles them.
 """
 from __future__ import annotations
 
 import contextlib
-from typing import Iterable, List
+from typing import Iterable, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -51,34 +61,55 @@ from ..runtime import heartbeat
 
 Tensor = torch.Tensor
 _BF16, _F32 = torch.bfloat16, torch.float32
+_ALIGN = {_BF16: 8, _F32: 4}          # 16-byte slots
 
 
 def _pad(n: int, a: int) -> int:
     return (n + a - 1) // a * a
 
 
-class _Bucket:
+class _Range:
+    """One dtype's part of a bucket: its parameters' slots in that dtype's region."""
+
     def __init__(self, dtype, gi, params, offsets, start, end):
         self.dtype, self.gi = dtype, gi            # element dtype and param-group index
         self.params, self.offsets = params, offsets
         self.start, self.end = start, end          # region-relative, element units of `dtype`
-        self.pending = set(id(p) for p in params)
+
+
+class _Bucket:
+    def __init__(self, ranges: List[_Range]):
+        self.ranges = ranges                        # bf16 first, then fp32 (each optional)
+        self.params = [p for r in ranges for p in r.params]
+        self.pending = set(id(p) for p in self.params)
         self.launched = False
+
+    @property
+    def dtypes(self):
+        return {r.dtype for r in self.ranges}
+
+    @property
+    def dtype(self):
+        """The bucket's element dtype if it has one sub-range (else "mixed")."""
+        return self.ranges[0].dtype if len(self.ranges) == 1 else "mixed"
 
 
 class ShardedMasterSGD:
-    """Momentum SGD (torch.optim.SGD semantics, dampening 0) sharded over the xGMI ranks.
+    """Momentum SGD (torch.optim.SGD semantics, dampening 0) sharded over the data-parallel ranks.
 
     ``params``: tensors, or torch-style param-group dicts (``{"params": [...], "weight_decay":
     0.0, "weights": "fp32"}``) whose ``lr`` / ``momentum`` / ``weight_decay`` override the
     defaults. ``weights`` (default ``"bf16"``) is the dtype the group's parameters are kept in:
     bf16 weights with fp32 masters (the parameters are converted in place), or fp32 weights that
-    are their own masters. Parameters must be CUDA tensors, contiguous or channels_last."""
+    are their own masters. Parameters must be contiguous or channels_last; CUDA tensors (CPU
+    tensors with ``backend="rccl"`` over gloo, for tests). ``order``: the parameters in model
+    (registration) order, which decides the buckets (default: the param groups' order)."""
 
     def __init__(self, params: Iterable, lr: float, momentum: float = 0.0,
                  weight_decay: float = 0.0, bucket_mb: float = 16.0, group=None,
-                 timeout_s: float = 60.0, overlap: bool = True):
-        from .xgmi import XgmiComm
+                 timeout_s: float = 60.0, overlap: bool = True, backend: str = "auto",
+                 order: Optional[Iterable[Tensor]] = None, last_bucket_mb: Optional[float] = None,
+                 rccl_reduce_fp32: bool = False):
         plist = list(params)
         if plist and isinstance(plist[0], dict):
             raw_groups = plist
@@ -95,6 +126,8 @@ class ShardedMasterSGD:
             raise ValueError("ShardedMasterSGD needs at least one parameter")
         if len({id(p) for p in self.params}) != len(self.params):
             raise ValueError("a parameter appears in more than one param group")
+        if backend not in ("auto", "xgmi", "rccl"):
+            raise ValueError(f"backend must be auto, xgmi or rccl (got {backend!r})")
         self.state: dict = {}   # Horovod's broadcast_optimizer_state finds nothing to send: the
         #                         masters are derived from the (already broadcast) weights
         self.group = group
@@ -102,6 +135,8 @@ class ShardedMasterSGD:
         self._no_sync = False
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        dev = self.params[0].device
+        self.device = dev
         kind_of = {}
         for gi, g in enumerate(self.param_groups):
             kind = {"bf16": _BF16, "fp32": _F32}.get(raw_groups[gi].get("weights", "bf16"))
@@ -110,51 +145,47 @@ class ShardedMasterSGD:
             g["weights"] = "bf16" if kind == _BF16 else "fp32"
             for p in g["params"]:
                 kind_of[id(p)] = (kind, gi)
-                if not p.is_cuda:
-                    raise ValueError("ShardedMasterSGD runs on GPU parameters")
+                if p.device != dev:
+                    raise ValueError("ShardedMasterSGD parameters must share one device")
                 if not p.is_floating_point():
                     raise TypeError(f"ShardedMasterSGD takes floating-point parameters, got "
                                     f"{p.dtype}")
                 if not (p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last)):
                     raise ValueError("parameters must be contiguous or channels_last")
-        # Layout: gradient-readiness order (reverse registration). bf16 region [0, T16) in bf16
-        # elements (16-byte aligned slots), fp32 region [F0, F0 + T32) in floats behind it. One
-        # open bucket per weight dtype; it closes once it holds ~bucket_mb, or when the next
-        # parameter of that dtype belongs to another param group (a bucket's range is contiguous
-        # and its hyperparameters are one group's).
-        cap = {_BF16: max(8, int(bucket_mb * 2**20 / 2)), _F32: max(4, int(bucket_mb * 2**20 / 4))}
-        align = {_BF16: 8, _F32: 4}
-        self.offsets = {}
-        self.buckets: List[_Bucket] = []
-        size = {_BF16: 0, _F32: 0}
-        open_ = {}
-
-        def close(dt):
-            gi, ps, offs, start = open_.pop(dt)
-            self.buckets.append(_Bucket(dt, gi, ps, offs, start, size[dt]))
-
-        for p in reversed(self.params):
-            dt, gi = kind_of[id(p)]
-            if dt in open_ and open_[dt][0] != gi:
-                close(dt)
-            if dt not in open_:
-                open_[dt] = (gi, [], [], size[dt])
-            off = size[dt]
-            self.offsets[id(p)] = off
-            open_[dt][1].append(p)
-            open_[dt][2].append(off)
-            size[dt] = off + _pad(p.numel(), align[dt])
-            if size[dt] - open_[dt][3] >= cap[dt]:
-                close(dt)
-        for dt in list(open_):
-            close(dt)
-        self.t16, self.t32 = size[_BF16], size[_F32]
-        self.f0 = _pad((self.t16 + 1) // 2, 4)            # fp32 region start (floats)
-        floats = self.f0 + self.t32
-        self.comm = XgmiComm(group, staging_elems=floats, param_elems=floats,
-                             timeout_s=timeout_s)
-        dev = self.params[0].device
-        buf, wbuf = self.comm.buffer(), self.comm.params()
+        if dev.type != "cuda" and backend != "rccl":
+            raise ValueError("ShardedMasterSGD on CPU tensors needs backend='rccl' (gloo)")
+        requested = backend
+        if backend == "auto":
+            from . import xgmi
+            backend = "xgmi" if xgmi.usable(group) else "rccl"
+        self.rccl_reduce_fp32 = bool(rccl_reduce_fp32)
+        model_order = self._model_order(order)
+        last_mb = bucket_mb / 4 if last_bucket_mb is None else last_bucket_mb
+        self.comm = None
+        if backend == "xgmi":
+            from .xgmi import XgmiComm, XgmiUnavailable
+            self._form_buckets(model_order, kind_of, bucket_mb, last_mb, pad_to=1)
+            floats = self.f0 + self.t32
+            try:
+                # collective: every rank learns together whether the peer mappings came up
+                self.comm = XgmiComm(group, staging_elems=floats, param_elems=floats,
+                                     timeout_s=timeout_s)
+            except XgmiUnavailable:
+                if requested == "xgmi":
+                    raise
+                backend = "rccl"
+        self.backend = backend
+        if self.comm is None:
+            # RCCL layout: sub-ranges padded to world x 16-byte slots (equal, aligned shards)
+            self._form_buckets(model_order, kind_of, bucket_mb, last_mb, pad_to=self.world)
+            floats = self.f0 + self.t32
+            wbuf = torch.zeros(floats, dtype=_F32, device=dev)
+            buf = torch.zeros(floats, dtype=_F32, device=dev)
+            self._rs_out = torch.zeros(self._max_shard_words(), dtype=_F32, device=dev)
+            self._rs_wide = (torch.zeros(self._max_range_elems(_BF16), dtype=_F32, device=dev)
+                             if self.rccl_reduce_fp32 else None)
+        else:
+            buf, wbuf = self.comm.buffer(), self.comm.params()
         self.wbf = wbuf.view(_BF16)[: self.t16]
         self.stage = buf.view(_BF16)[: self.t16]
         self.w32 = wbuf[self.f0: self.f0 + self.t32]
@@ -178,46 +209,162 @@ class ShardedMasterSGD:
                     v = self._view(self.w32, p, o)
                 v.copy_(p)
                 p.data = v          # bf16 group: the parameter becomes bf16 (weights in the
-                p.grad = None       # registered buffer, fp32 master in self.master)
-        self.stream = torch.cuda.Stream(device=dev)
+                p.grad = None       # flat buffer, fp32 master in self.master)
+        self.stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
+
+    # ------------------------------------------------------------------------------- layout
+    def _model_order(self, order) -> List[Tensor]:
+        if order is None:
+            return list(self.params)
+        mine = {id(p) for p in self.params}
+        seen, out = set(), []
+        for p in order:
+            if id(p) in mine and id(p) not in seen:
+                out.append(p)
+                seen.add(id(p))
+        out += [p for p in self.params if id(p) not in seen]   # not in `order`: appended
+        return out
+
+    def _form_buckets(self, model_order, kind_of, bucket_mb, last_mb, pad_to):
+        """Buckets in readiness order. Built from the INPUT side (model order): the first group
+        closes at ``last_mb`` (it is ready last and nothing overlaps its update), the others at
+        ``bucket_mb``; a group also closes when a parameter's param group differs from the one
+        its dtype's sub-range already has (one set of hyperparameters per sub-range). With
+        ``pad_to`` > 1 every sub-range is padded to a multiple of pad_to slots, so RCCL's
+        reduce-scatter splits it into equal, aligned shards."""
+        cap = max(1, int(bucket_mb * 2**20))
+        first_cap = max(1, int(last_mb * 2**20))
+        groups, cur, cur_bytes, cur_gi = [], [], 0, {}
+        for p in model_order:
+            dt, gi = kind_of[id(p)]
+            if cur and cur_gi.get(dt, gi) != gi:
+                groups.append(cur)
+                cur, cur_bytes, cur_gi = [], 0, {}
+            cur.append(p)
+            cur_gi[dt] = gi
+            cur_bytes += p.numel() * (2 if dt == _BF16 else 4)
+            if cur_bytes >= (first_cap if not groups else cap):
+                groups.append(cur)
+                cur, cur_bytes, cur_gi = [], 0, {}
+        if cur:
+            groups.append(cur)
+        self.offsets = {}
+        self.buckets: List[_Bucket] = []
+        size = {_BF16: 0, _F32: 0}
+        for grp in reversed(groups):                 # readiness order
+            ranges = []
+            for dt in (_BF16, _F32):
+                ps = [p for p in reversed(grp) if kind_of[id(p)][0] == dt]
+                if not ps:
+                    continue
+                start, offs = size[dt], []
+                for p in ps:
+                    offs.append(size[dt])
+                    self.offsets[id(p)] = size[dt]
+                    size[dt] += _pad(p.numel(), _ALIGN[dt])
+                size[dt] = start + _pad(size[dt] - start, _ALIGN[dt] * pad_to)
+                ranges.append(_Range(dt, kind_of[id(ps[0])][1], ps, offs, start, size[dt]))
+            self.buckets.append(_Bucket(ranges))
+        self.t16, self.t32 = size[_BF16], size[_F32]
+        self.f0 = _pad((self.t16 + 1) // 2, 4)            # fp32 region start (floats)
+
+    def _max_range_elems(self, dtype) -> int:
+        return max([r.end - r.start for b in self.buckets for r in b.ranges if r.dtype == dtype]
+                   + [0])
+
+    def _max_shard_words(self) -> int:
+        """fp32 words of the largest reduce-scatter output (a bf16 shard fits in half)."""
+        m16 = self._max_range_elems(_BF16) // max(1, self.world)
+        m32 = self._max_range_elems(_F32) // max(1, self.world)
+        return max(4, m16 if self.rccl_reduce_fp32 else (m16 + 1) // 2, m32)
 
     # ----------------------------------------------------------------------------------------
     @staticmethod
     def _view(flat: Tensor, p: Tensor, off: int) -> Tensor:
         return torch.as_strided(flat, p.shape, p.stride(), flat.storage_offset() + off)
 
+    def _stream_ctx(self):
+        return torch.cuda.stream(self.stream) if self.stream is not None else \
+            contextlib.nullcontext()
+
     def _launch(self, b: _Bucket) -> None:
-        main = torch.cuda.current_stream()
-        self.stream.wait_stream(main)
-        g = self.param_groups[b.gi]
-        stage = self.stage if b.dtype == _BF16 else self.stage32
-        with torch.cuda.stream(self.stream):
+        if self.stream is not None:
+            self.stream.wait_stream(torch.cuda.current_stream())
+        with self._stream_ctx():
             dst, src = [], []
-            for p, o in zip(b.params, b.offsets):
-                v = self._view(stage, p, o)
-                if p.grad is None:
-                    v.zero_()          # unused parameter this step: zero gradient (Horovod)
-                    continue
-                gr = p.grad
-                if gr.dtype != p.dtype or not _same_memory_order(gr, p):
-                    raise RuntimeError("ShardedMasterSGD: gradients must have the parameter's "
-                                       f"dtype and memory order (param {p.dtype} "
-                                       f"{tuple(p.shape)} {p.stride()}, grad {gr.dtype} "
-                                       f"{gr.stride()})")
-                gr.record_stream(self.stream)
-                dst.append(v)
-                src.append(gr)
+            for r in b.ranges:
+                stage = self.stage if r.dtype == _BF16 else self.stage32
+                for p, o in zip(r.params, r.offsets):
+                    v = self._view(stage, p, o)
+                    if p.grad is None:
+                        v.zero_()          # unused parameter this step: zero gradient (Horovod)
+                        continue
+                    gr = p.grad
+                    if gr.dtype != p.dtype or not _same_memory_order(gr, p):
+                        raise RuntimeError(
+                            "ShardedMasterSGD: gradients must have the parameter's dtype and "
+                            f"memory order (param {p.dtype} {tuple(p.shape)} {p.stride()}, grad "
+                            f"{gr.dtype} {gr.stride()})")
+                    if self.stream is not None:
+                        gr.record_stream(self.stream)
+                    dst.append(v)
+                    src.append(gr)
             if dst:
                 torch._foreach_copy_(dst, src)
-            lr, mu, wd = float(g["lr"]), float(g["momentum"]), float(g["weight_decay"])
-            if b.dtype == _BF16:
-                self.comm.peers.sgd_bf16(self.master, self.mom, b.start, b.end - b.start, lr, mu,
-                                         wd, 1.0 / self.world)
-            else:
-                self.comm.peers.sgd_f32(self.mom32[b.start:b.end], self.f0 + b.start,
-                                        b.end - b.start, lr, mu, wd, 1.0 / self.world)
+            for r in b.ranges:
+                g = self.param_groups[r.gi]
+                lr, mu, wd = float(g["lr"]), float(g["momentum"]), float(g["weight_decay"])
+                if self.comm is not None:
+                    self._update_xgmi(r, lr, mu, wd)
+                else:
+                    self._update_rccl(r, lr, mu, wd)
         b.launched = True
+
+    def _update_xgmi(self, r: _Range, lr, mu, wd) -> None:
+        if r.dtype == _BF16:
+            self.comm.peers.sgd_bf16(self.master, self.mom, r.start, r.end - r.start, lr, mu, wd,
+                                     1.0 / self.world)
+        else:
+            self.comm.peers.sgd_f32(self.mom32[r.start:r.end], self.f0 + r.start,
+                                    r.end - r.start, lr, mu, wd, 1.0 / self.world)
+
+    def _update_rccl(self, r: _Range, lr, mu, wd) -> None:
+        """reduce-scatter -> shard_sgd on the owned shard -> all-gather, on the current (comm)
+        stream. Sub-ranges are padded to world x 16-byte slots: equal, aligned shards."""
+        from ..ops import fused
+        n = r.end - r.start
+        sl = n // self.world
+        lo = r.start + self.rank * sl
+        scale = 1.0 / self.world
+        if r.dtype == _BF16:
+            if self.rccl_reduce_fp32:
+                wide = self._rs_wide[:n]
+                wide.copy_(self.stage[r.start:r.end])
+                out = self._rs_out[:sl]
+                self._reduce_scatter(out, wide)
+            else:
+                out = self._rs_out.view(_BF16)[:sl]
+                self._reduce_scatter(out, self.stage[r.start:r.end])
+            fused.shard_sgd(out, self.master[lo:lo + sl], self.mom[lo:lo + sl],
+                            self.wbf[lo:lo + sl], lr=lr, momentum=mu, weight_decay=wd,
+                            scale=scale)
+            self._all_gather(self.wbf[r.start:r.end], self.wbf[lo:lo + sl])
+        else:
+            out = self._rs_out[:sl]
+            self._reduce_scatter(out, self.stage32[r.start:r.end])
+            fused.shard_sgd(out, self.w32[lo:lo + sl], self.mom32[lo:lo + sl], None, lr=lr,
+                            momentum=mu, weight_decay=wd, scale=scale)
+            self._all_gather(self.w32[r.start:r.end], self.w32[lo:lo + sl])
+
+    def _reduce_scatter(self, out: Tensor, inp: Tensor) -> None:
+        dist.reduce_scatter_tensor(out, inp, group=self.group)
+
+    def _all_gather(self, out: Tensor, mine: Tensor) -> None:
+        # in place on RCCL (the send buffer is this rank's slot of the receive buffer); gloo
+        # gets a copy
+        dist.all_gather_into_tensor(out, mine.clone() if out.device.type == "cpu" else mine,
+                                    group=self.group)
 
     def _on_grad(self, p) -> None:
         if self._no_sync:
@@ -232,11 +379,15 @@ class ShardedMasterSGD:
         if not b.pending and self.overlap:
             self._launch(b)
 
+    def _join(self) -> None:
+        if self.stream is not None:
+            torch.cuda.current_stream().wait_stream(self.stream)
+
     def _reset(self) -> None:
         if any(b.launched for b in self.buckets):
             # updates already issued on the comm stream: later work on the main stream (the
             # next forward reads the weights) must be ordered after them
-            torch.cuda.current_stream().wait_stream(self.stream)
+            self._join()
         for b in self.buckets:
             b.launched = False
             b.pending = set(id(p) for p in b.params)
@@ -264,7 +415,7 @@ class ShardedMasterSGD:
         for b in self.buckets:   # same launch order on every rank: bucket order
             if not b.launched:
                 self._launch(b)
-        torch.cuda.current_stream().wait_stream(self.stream)
+        self._join()
         for b in self.buckets:
             b.launched = False
             b.pending = set(id(p) for p in b.params)
@@ -273,30 +424,37 @@ class ShardedMasterSGD:
 
     # ----------------------------------------------------------------------- state / sharding
     def shard_ranges(self, rank: int | None = None, dtype=_BF16):
-        """Region-relative [lo, hi) element ranges this rank owns, one per bucket of ``dtype``."""
+        """Region-relative [lo, hi) element ranges this rank owns, one per sub-range of
+        ``dtype``."""
         r = self.rank if rank is None else rank
         out = []
         for b in self.buckets:
-            if b.dtype != dtype:
-                continue
-            if dtype == _BF16:
-                out.append(tuple(self.comm.ext.ccl_sgd_shard(b.start, b.end - b.start,
-                                                             self.world, r)))
-            else:
-                lo, hi = self.comm.ext.ccl_sgd_f32_shard(self.f0 + b.start, b.end - b.start,
-                                                         self.world, r)
-                out.append((lo - self.f0, hi - self.f0))
+            for rg in b.ranges:
+                if rg.dtype != dtype:
+                    continue
+                n = rg.end - rg.start
+                if self.comm is None:
+                    sl = n // self.world
+                    out.append((rg.start + r * sl, rg.start + (r + 1) * sl))
+                elif dtype == _BF16:
+                    out.append(tuple(self.comm.ext.ccl_sgd_shard(rg.start, n, self.world, r)))
+                else:
+                    lo, hi = self.comm.ext.ccl_sgd_f32_shard(self.f0 + rg.start, n, self.world, r)
+                    out.append((lo - self.f0, hi - self.f0))
         return out
 
     @torch.no_grad()
     def _gathered(self, flat: Tensor, dtype) -> Tensor:
         """Full-length copy of a sharded fp32 array: owned chunks from every rank (sum of the
-        rank-masked arrays over xGMI; collective)."""
+        rank-masked arrays; collective)."""
         mine = torch.zeros_like(flat)
         for lo, hi in self.shard_ranges(dtype=dtype):
             mine[lo:hi] = flat[lo:hi]
         if mine.numel():
-            self.comm.all_reduce_(mine)
+            if self.comm is not None:
+                self.comm.all_reduce_(mine)
+            elif self.world > 1:
+                dist.all_reduce(mine, group=self.group)
         return mine
 
     def _logical(self, flat: Tensor, p: Tensor) -> Tensor:
@@ -305,7 +463,7 @@ class ShardedMasterSGD:
     def state_dict(self) -> dict:
         """fp32 masters + momentum per parameter in logical layout, and the param groups'
         hyperparameters (collective: every rank must call it)."""
-        torch.cuda.current_stream().wait_stream(self.stream)
+        self._join()
         master = self._gathered(self.master, _BF16) if self.t16 else self.master
         mom = self._gathered(self.mom, _BF16) if self.t16 else self.mom
         mom32 = self._gathered(self.mom32, _F32) if self.t32 else self.mom32
@@ -339,7 +497,7 @@ class ShardedMasterSGD:
         if groups is not None and len(groups) != len(self.param_groups):
             raise ValueError(f"ShardedMasterSGD state has {len(groups)} param groups, the "
                              f"optimizer {len(self.param_groups)}")
-        torch.cuda.current_stream().wait_stream(self.stream)
+        self._join()
         for p, a, b in zip(self.params, masters, moms):
             o = self.offsets[id(p)]
             if p.dtype == _BF16:
@@ -357,7 +515,7 @@ class ShardedMasterSGD:
 
     @torch.no_grad()
     def _rebind(self) -> None:
-        """Make every parameter a view into the registered weight buffer again (after a
+        """Make every parameter a view into the flat weight buffer again (after a
         ``p.data = t`` re-binding), keeping the buffer's values."""
         for p in self.params:
             o = self.offsets[id(p)]
@@ -370,9 +528,9 @@ class ShardedMasterSGD:
         """Re-derive the masters from the current parameter values (call after
         ``model.load_state_dict(...)`` on a model whose optimizer already exists; otherwise the
         next update overwrites the loaded weights with stale masters). A parameter whose data
-        was re-bound (``p.data = t``) is copied back into the registered buffer and re-bound to
+        was re-bound (``p.data = t``) is copied back into the flat buffer and re-bound to
         it, so the all-gathered weights reach the model again. Momentum is kept."""
-        torch.cuda.current_stream().wait_stream(self.stream)
+        self._join()
         for p in self.params:
             o = self.offsets[id(p)]
             v = self._view(self.wbf if p.dtype == _BF16 else self.w32, p, o)
@@ -386,5 +544,7 @@ class ShardedMasterSGD:
         for h in self._hooks:
             h.remove()
         self._hooks = []
-        torch.cuda.synchronize()
-        self.comm.close()
+        if self.device.type == "cuda":
+            torch.cuda.synchronize()
+        if self.comm is not None:
+            self.comm.close()

@@ -32,6 +32,8 @@ hipError_t arena_mt_copy_scale(float* const*, const long long*, const long long*
                                int, hipStream_t);
 hipError_t arena_mt_sgd_master(const void* const*, const long long*, const long long*, int,
                                float*, float*, void*, float, float, float, hipStream_t);
+hipError_t arena_shard_sgd(const void*, int, float*, float*, void*, long long, float, float, float,
+                           float, hipStream_t);
 // csrc/ccl/xgmi_ccl.hip
 hipError_t arena_ccl_malloc(void**, size_t, int);
 hipError_t arena_ccl_free(void*);
@@ -630,6 +632,40 @@ void mt_sgd_master(std::vector<Tensor> grads, std::vector<int64_t> offsets, Tens
                                 master.data_ptr<float>(), mom.data_ptr<float>(), wbf.data_ptr(),
                                 (float)lr, (float)momentum, (float)weight_decay, cur_stream()),
             "mt_sgd_master");
+}
+
+void shard_sgd(Tensor grad, Tensor w32, Tensor mom, c10::optional<Tensor> wbf, double lr,
+               double momentum, double weight_decay, double scale) {
+  check_f32(w32, "w32");
+  check_f32(mom, "mom");
+  check_dev(grad, "grad");
+  const bool bf = grad.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf || grad.scalar_type() == torch::kFloat32, "shard_sgd: grad must be bf16 or fp32");
+  TORCH_CHECK(grad.is_contiguous() && w32.is_contiguous() && mom.is_contiguous() &&
+                  grad.device() == w32.device() && mom.device() == w32.device(),
+              "shard_sgd: contiguous tensors on one GPU");
+  const int64_t n = w32.numel();
+  TORCH_CHECK(grad.numel() == n && mom.numel() == n && n % 4 == 0,
+              "shard_sgd: equal sizes, a multiple of 4");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w32.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(mom.data_ptr()) % 16 == 0 &&
+                  reinterpret_cast<uintptr_t>(grad.data_ptr()) % (bf ? 8 : 16) == 0,
+              "shard_sgd: misaligned range");
+  void* wp = nullptr;
+  if (bf) {
+    TORCH_CHECK(wbf.has_value(), "shard_sgd: bf16 gradients need the bf16 weight range");
+    check_dev(*wbf, "wbf");
+    TORCH_CHECK(wbf->scalar_type() == torch::kBFloat16 && wbf->is_contiguous() &&
+                    wbf->numel() == n && reinterpret_cast<uintptr_t>(wbf->data_ptr()) % 8 == 0,
+                "shard_sgd: wbf must be a dense, 8-byte aligned bf16 range of the same size");
+    wp = wbf->data_ptr();
+  } else {
+    TORCH_CHECK(!wbf.has_value(), "shard_sgd: fp32 weights are their own masters (no wbf)");
+  }
+  check_hip(arena_shard_sgd(grad.data_ptr(), bf ? 1 : 0, w32.data_ptr<float>(),
+                            mom.data_ptr<float>(), wp, n, (float)lr, (float)momentum,
+                            (float)weight_decay, (float)scale, cur_stream()),
+            "shard_sgd");
 }
 
 // ------------------------------------------------------------------------------ xGMI collective
@@ -1912,6 +1948,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("softmax_xent", &softmax_xent);
   m.def("mt_copy_scale", &mt_copy_scale);
   m.def("mt_sgd_master", &mt_sgd_master);
+  m.def("shard_sgd", &shard_sgd, py::arg("grad"), py::arg("w32"), py::arg("mom"),
+        py::arg("wbf") = py::none(), py::arg("lr"), py::arg("momentum"),
+        py::arg("weight_decay"), py::arg("scale"));
   m.def("ccl_malloc", &ccl_malloc);
   m.def("ccl_free", &ccl_free);
   m.def("ccl_memset", &ccl_memset);

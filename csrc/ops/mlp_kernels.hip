@@ -1185,6 +1185,54 @@ __global__ __launch_bounds__(256) void mt_sgd_master_kernel(MtArgs a, float* __r
   *reinterpret_cast<uint2*>(wbf + o) = make_uint2(r[0] | (r[1] << 16), r[2] | (r[3] << 16));
 }
 
+// Momentum SGD over ONE flat range: a data-parallel rank's shard of a gradient bucket after the
+// RCCL reduce-scatter (ShardedMasterSGD's off-node backend). Same arithmetic, in the same order,
+// as the xGMI kernels' shard update (csrc/ccl/xgmi_ccl.hip xgmi_sgd_*): d = g * scale + wd * w,
+// m = mu * m + d, w = w - lr * m. BF16: bf16 summed gradient, fp32 master, rounded bf16 weight
+// written to wbf; else fp32 gradient and the fp32 weights are their own masters. n % 4 == 0 and
+// 16-byte aligned fp32 pointers (host-checked): one thread owns 4 elements per grid-stride step.
+template <bool BF16>
+__global__ __launch_bounds__(256) void shard_sgd_kernel(const void* __restrict__ grad,
+                                                        float* __restrict__ w32,
+                                                        float* __restrict__ mom,
+                                                        uint16_t* __restrict__ wbf, long long n,
+                                                        float lr, float mu, float wd,
+                                                        float scale) {
+  const long long stride = (long long)gridDim.x * 1024;
+  for (long long j = ((long long)blockIdx.x * 256 + threadIdx.x) * 4; j < n; j += stride) {
+    float g[4];
+    if constexpr (BF16) {
+      const uint2 g2 = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(grad) + j);
+      g[0] = bf16_to_f32(g2.x & 0xffffu);
+      g[1] = bf16_to_f32(g2.x >> 16);
+      g[2] = bf16_to_f32(g2.y & 0xffffu);
+      g[3] = bf16_to_f32(g2.y >> 16);
+    } else {
+      const float4 g4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(grad) + j);
+      g[0] = g4.x;
+      g[1] = g4.y;
+      g[2] = g4.z;
+      g[3] = g4.w;
+    }
+    float4 w4 = *reinterpret_cast<const float4*>(w32 + j);
+    float4 m4 = *reinterpret_cast<const float4*>(mom + j);
+    float* w = &w4.x;
+    float* m = &m4.x;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d = g[k] * scale + wd * w[k];
+      m[k] = mu * m[k] + d;
+      w[k] = w[k] - lr * m[k];
+    }
+    *reinterpret_cast<float4*>(w32 + j) = w4;
+    *reinterpret_cast<float4*>(mom + j) = m4;
+    if constexpr (BF16) {
+      *reinterpret_cast<uint2*>(wbf + j) = make_uint2(f32_to_bf16(w[0]) | (f32_to_bf16(w[1]) << 16),
+                                                      f32_to_bf16(w[2]) | (f32_to_bf16(w[3]) << 16));
+    }
+  }
+}
+
 }  // namespace
 
 // =============================================================================================
@@ -1411,6 +1459,21 @@ hipError_t arena_mt_sgd_master(const void* const* grads, const long long* offs, 
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
+}
+
+hipError_t arena_shard_sgd(const void* grad, int grad_bf16, float* w32, float* mom, void* wbf,
+                           long long n, float lr, float mu, float wd, float scale,
+                           hipStream_t stream) {
+  if (n % 4 || (grad_bf16 && !wbf)) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  const long long blocks = std::min<long long>((n + 1023) / 1024, 4096);
+  if (grad_bf16)
+    hipLaunchKernelGGL(shard_sgd_kernel<true>, dim3((unsigned)blocks), dim3(256), 0, stream, grad,
+                       w32, mom, reinterpret_cast<uint16_t*>(wbf), n, lr, mu, wd, scale);
+  else
+    hipLaunchKernelGGL(shard_sgd_kernel<false>, dim3((unsigned)blocks), dim3(256), 0, stream, grad,
+                       w32, mom, nullptr, n, lr, mu, wd, scale);
+  return hipGetLastError();
 }
 
 }  // extern "C"

@@ -161,3 +161,34 @@ def test_master_sgd_kernel_matches_torch_sgd_gpu():
     from arena_amd.ops import _ext
     _ext.load()
     _run("cuda")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_shard_sgd_kernel_matches_reference(dtype):
+    """The RCCL backend's shard update (``shard_sgd`` HIP kernel) against its fp32 torch
+    reference: bit-exact with exact hyperparameters (lr 2^-4, momentum 1/2, wd 2^-10, scale 1/4:
+    every product exact, each result rounds once whatever FMAs the compiler forms), and within
+    fp32 / bf16 rounding with real ones."""
+    from arena_amd.ops import fused
+    n = 4096 + 12
+    for lr, mu, wd, sc, exact in ((2.0 ** -4, 0.5, 2.0 ** -10, 0.25, True),
+                                  (0.05, 0.9, 1e-3, 1.0 / 3, False)):
+        g = torch.Generator().manual_seed(5)
+        grad = (torch.randn(n, generator=g) * 0.1).to(dtype)
+        w = torch.randn(n, generator=g)
+        m = torch.randn(n, generator=g) * 0.01
+        wr, mr = w.clone(), m.clone()
+        wbr = torch.empty(n, dtype=torch.bfloat16) if dtype == torch.bfloat16 else None
+        fused.shard_sgd(grad, wr, mr, wbr, lr=lr, momentum=mu, weight_decay=wd, scale=sc)
+        wg, mg = w.cuda(), m.cuda()
+        wbg = torch.empty(n, dtype=torch.bfloat16, device="cuda") if wbr is not None else None
+        fused.shard_sgd(grad.cuda(), wg, mg, wbg, lr=lr, momentum=mu, weight_decay=wd, scale=sc)
+        torch.cuda.synchronize()
+        if exact:
+            assert torch.equal(wg.cpu(), wr) and torch.equal(mg.cpu(), mr)
+        else:
+            assert float((wg.cpu() - wr).abs().max()) <= 4 * 2.0 ** -23 * float(wr.abs().max())
+            assert float((mg.cpu() - mr).abs().max()) <= 4 * 2.0 ** -23 * float(mr.abs().max())
+        if wbr is not None:
+            assert torch.equal(wbg.cpu(), wg.cpu().to(torch.bfloat16))   # RNE of the master

@@ -352,7 +352,7 @@ def _sharded_sgd_kernel(rank, world, port, q):
                        "weight_decay": 0.0, "weights": "fp32"}]
             opt = ShardedMasterSGD(groups, lr=lr, momentum=mu, bucket_mb=0.005, timeout_s=30.0)
             assert len(opt.buckets) >= 4, len(opt.buckets)
-            assert {b.dtype for b in opt.buckets} == {bf, f32}
+            assert set().union(*(b.dtypes for b in opt.buckets)) == {bf, f32}
             for step in range(3):
                 if step == 2:
                     lr = lr * 2
@@ -495,7 +495,7 @@ def _zero_sgd(rank, world, port, q):
         # ---- (1) one step vs a single broadcast reference
         model, opt, x, y = cnn_bench.build(args, dev, world)
         assert isinstance(opt, ShardedMasterSGD) and len(opt.buckets) > 2, type(opt)
-        assert {b.dtype for b in opt.buckets} == {bf, torch.float32}
+        assert set().union(*(b.dtypes for b in opt.buckets)) == {bf, torch.float32}
         params = list(model.parameters())
         decay = {id(p) for p in opt.param_groups[0]["params"]}
         w0 = [p.detach().float().clone() for p in params]
@@ -756,3 +756,69 @@ def test_dp_resnet_step_as_hipgraph_matches_eager():
     for r, res in out.items():
         assert res["graph_vs_eager"] <= 1e-4 * max(1.0, res["scale"]), (r, res)
     assert out[0]["digest"] == out[1]["digest"], out  # replicas bit-identical
+
+
+def _rccl_sharded(rank, world, port, q):
+    """ShardedMasterSGD's RCCL backend on the GPU (a world-1 NCCL group: the reduce-scatter /
+    shard_sgd / all-gather sequence runs through RCCL and the HIP kernel, on the comm stream,
+    eager and captured in a hipGraph) against the fp32 torch SGD formula."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0",
+                          WORLD_SIZE="1", LOCAL_RANK="0")
+        torch.cuda.set_device(0)
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+        from arena_amd.parallel.zero import ShardedMasterSGD
+        lr, mu, wd = 2.0 ** -4, 0.5, 2.0 ** -10
+        g0 = torch.Generator(device="cuda").manual_seed(3)
+        shapes = [((64, 32, 3, 3), torch.bfloat16), ((64,), torch.float32),
+                  ((128, 64), torch.bfloat16), ((128,), torch.float32)]
+        params = [torch.nn.Parameter(torch.randn(s, device="cuda", generator=g0).to(dt))
+                  for s, dt in shapes]
+        master = [p.detach().float().clone() for p in params]
+        mom = [torch.zeros_like(m) for m in master]
+        opt = ShardedMasterSGD([{"params": [params[0], params[2]], "weight_decay": wd},
+                                {"params": [params[1], params[3]], "weight_decay": 0.0,
+                                 "weights": "fp32"}], lr=lr, momentum=mu, bucket_mb=0.02,
+                               backend="rccl", order=params)
+        grads = [(torch.randn(p.shape, device="cuda", generator=g0) * 0.1).to(p.dtype)
+                 for p in params]
+        graph = None
+        for step in range(5):
+            if step == 2:           # capture the update (hooks fire in step()) and replay it
+                for p, gr in zip(params, grads):
+                    p.grad = gr
+                graph = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                    opt.step()
+            if graph is not None:
+                graph.replay()
+            else:
+                for p, gr in zip(params, grads):
+                    p.grad = gr
+                opt.step()
+                opt.zero_grad()
+            for i, (p, gr) in enumerate(zip(params, grads)):
+                d = gr.float() + (wd if p.dtype == torch.bfloat16 else 0.0) * master[i]
+                mom[i] = mu * mom[i] + d
+                master[i] = master[i] - lr * mom[i]
+        torch.cuda.synchronize()
+        res = {"backend": opt.backend,
+               "w_bits": sum(int((p.detach() != m.to(p.dtype)).sum())
+                             for p, m in zip(params, master))}
+        sd = opt.state_dict()
+        pos = {id(p): i for i, p in enumerate(opt.params)}
+        res["master_bits"] = sum(int((sd["master"][pos[id(p)]] != m).sum())
+                                 for p, m in zip(params, master))
+        opt.close()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
+def test_sharded_sgd_rccl_backend_on_gpu():
+    out = _run(_rccl_sharded, 1)
+    res = out[0]
+    assert res["backend"] == "rccl", res
+    assert res["w_bits"] == 0 and res["master_bits"] == 0, res   # exact hyperparameters
