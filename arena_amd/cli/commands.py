@@ -165,7 +165,15 @@ def cmd_submit_mpi(ctx, ns) -> int:
     a.ranks_per_pod = ns.ranksPerPod
     a.jupyter = ns.jupyter
     _fill_sync_tb(a, ns)
-    return _submit(ctx, a, _command_args(ns))
+    rc = _submit(ctx, a, _command_args(ns))
+    rpp = a.effective_ranks_per_pod()
+    if rpp > 1 and getattr(ctx.backend, "name", "") != "local":
+        # the pods' entry point is now the in-pod launcher, which runs inside the user's image
+        log.warning(f"each pod starts {rpp} ranks (one per GPU) through `python3 -m "
+                    f"arena_amd.runtime.podlaunch`: the image {a.image!r} must have arena_amd "
+                    f"installed (pods exit 127 with a message otherwise); --ranksPerPod 1 runs "
+                    f"the command once per pod as given")
+    return rc
 
 
 def cmd_submit_sj(ctx, ns) -> int:

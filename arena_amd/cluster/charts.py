@@ -365,7 +365,16 @@ def _jobmon(release: str, ns: str, values: dict, app: str, env: Dict[str, str]) 
                                                "env": _env_list(full_env)}]}}}}
 
 
-POD_LAUNCHER = "exec python3 -m arena_amd.runtime.podlaunch"
+# The in-pod launcher runs inside the user's training image, so that image must have arena_amd
+# importable under python3. Check first and fail with a message that names the fix, instead of a
+# bare ModuleNotFoundError in the pod log (exit 127, "command not found" class).
+POD_LAUNCHER = (
+    "if ! python3 -c 'import arena_amd.runtime.podlaunch' >/dev/null 2>&1; then "
+    "echo \"arena: --ranksPerPod > 1 starts the pod's ranks with python3 -m "
+    "arena_amd.runtime.podlaunch, but arena_amd is not importable in this image. Install it "
+    "in the image (pip install arena_amd) or submit with --ranksPerPod 1 (one rank per pod, "
+    "the command runs as given).\" >&2; exit 127; fi; "
+    "exec python3 -m arena_amd.runtime.podlaunch")
 
 
 def jupyter_command(values: dict) -> List[str]:
@@ -391,7 +400,11 @@ def render_tf_horovod(release: str, ns: str, values: dict) -> List[dict]:
     in-pod launcher (``arena_amd.runtime.podlaunch``), which starts ``ranksPerPod`` children with
     ``RANK = pod_index * ranksPerPod + LOCAL_RANK``, ``LOCAL_WORLD_SIZE = ranksPerPod`` and
     ``WORLD_SIZE = pods * ranksPerPod`` before any GPU call. A one-pod job with 8 GPUs is then 8
-    ranks that all see all 8 devices, so the xGMI collectives apply.
+    ranks that all see all 8 devices, so the xGMI collectives apply. The launcher runs inside the
+    user's image: the pod first checks that ``arena_amd`` is importable there and otherwise exits
+    127 with a message naming the two fixes (install it, or ``--ranksPerPod 1``, which keeps the
+    launcher-free one-rank-per-pod form for any image). ``arena submit mpijob`` prints the same
+    requirement when it renders the launcher form.
 
     The ordinal comes from the pod's own name through the downward API (``POD_NAME`` =
     ``metadata.name`` = ``<fullname>-<i>``), never from ``$HOSTNAME``: under ``hostNetwork`` (the

@@ -313,3 +313,33 @@ def test_tfjob_eight_workers_fit_one_node():
     # pod networking: every pod has its own IP, the base ports are kept
     v = dict(a.values(), useHostNetwork=False)
     assert set(charts.task_ports(v)["worker"]) == {22222}
+
+
+def test_mpijob_default_ranks_per_pod_with_8_gpus_renders_launcher():
+    """The default for ``--gpus 8``: 8 ranks per pod through the in-pod launcher (ADVICE r4:
+    the behaviour change is explicit). The pod command checks that arena_amd is importable in
+    the user's image and names the fixes (install it, or --ranksPerPod 1) before exec."""
+    import subprocess
+    a = S.MPIJobArgs()
+    a.name, a.image, a.gpu_count, a.workers = "big", "rocm/pytorch:latest", 8, 2
+    a.prepare(["python", "train.py"])
+    assert a.values()["ranksPerPod"] == 8
+    docs = {(d["kind"], d["metadata"]["name"]): d
+            for d in charts.render(a.chart, "big", "default", a.values())}
+    job, ss = docs[("Job", "big-tf-horovod-job")], docs[("StatefulSet", "big-tf-horovod")]
+    for d in (job, ss):
+        c = _containers(d)[0]
+        env = _env(c)
+        assert env["WORLD_SIZE"] == "16" and env["ARENA_RANKS_PER_POD"] == "8"
+        assert c["resources"]["limits"]["amd.com/gpu"] == 8
+        cmd = c["command"]
+        assert cmd[:2] == ["sh", "-c"] and "import arena_amd.runtime.podlaunch" in cmd[2]
+        assert "--ranksPerPod 1" in cmd[2] and cmd[2].rstrip().endswith(
+            "exec python3 -m arena_amd.runtime.podlaunch")
+    # an image without arena_amd: the pod command exits 127 with the message (run it here with a
+    # python3 that cannot import it)
+    cmd = _containers(ss)[0]["command"][2]
+    r = subprocess.run(["sh", "-c", cmd], env={"PATH": os.environ["PATH"], "HOME": "/tmp",
+                                               "PYTHONPATH": "/nonexistent", "PYTHONNOUSERSITE": "1"},
+                       capture_output=True, text=True, timeout=60, cwd="/tmp")
+    assert r.returncode == 127 and "--ranksPerPod 1" in r.stderr, (r.returncode, r.stderr)
