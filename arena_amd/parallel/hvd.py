@@ -178,15 +178,26 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
             by_dtype.setdefault((t.dtype, t.device), []).append(t)
     flats = {k: torch.cat([t.detach().reshape(-1) for t in ts]) for k, ts in by_dtype.items()}
     comm, temp = _STATE["xgmi"] or None, False
-    if _STATE["xgmi"] is None and any(dev.type == "cuda" for _, dev in flats):
-        words = max(((f.numel() * f.element_size() + 15) // 16 * 4) for (_, dev), f in
-                    flats.items() if dev.type == "cuda")
-        comm, temp = _new_comm(min(words, _XGMI_STAGING)), True
+    if _STATE["xgmi"] is None:
+        # whether to build a temporary xGMI communicator is decided COLLECTIVELY: building it is
+        # a collective (xgmi.usable, XgmiComm), so a rank whose list happens to hold no GPU
+        # tensor must still take part, or the ranks that do would wait for it forever
+        words = max([((f.numel() * f.element_size() + 15) // 16 * 4) for (_, dev), f in
+                     flats.items() if dev.type == "cuda"] + [0])
+        allw: List[Optional[int]] = [None] * size()
+        dist.all_gather_object(allw, words)
+        if max(allw) > 0:
+            comm, temp = _new_comm(min(max(allw), _XGMI_STAGING)), True
     try:
         for (dt, dev), ts in by_dtype.items():
             flat = flats[(dt, dev)]
             if comm is not None and flat.is_cuda:
                 comm.broadcast_(flat, root_rank)   # xGMI direct pull / scatter + all-gather
+            elif not flat.is_cuda and dist.get_backend() == "nccl":
+                # host tensors (e.g. torch Adam's CPU "step") through the device for RCCL
+                dflat = flat.cuda()
+                dist.broadcast(dflat, root_rank)
+                flat.copy_(dflat.cpu())
             else:
                 dist.broadcast(flat, root_rank)
             off = 0
@@ -200,30 +211,83 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
             comm.close()
 
 
-def _optimizer_state_tensors(optimizer) -> List[torch.Tensor]:
+def _leaf_optimizers(optimizer) -> list:
+    """The torch-style optimizers inside ``optimizer`` (OptimizerGroup members, the one a
+    DistributedOptimizer wraps), in a fixed order."""
     subs = getattr(optimizer, "opts", None)          # OptimizerGroup: its members, in order
     if subs is not None:
-        return [t for o in subs for t in _optimizer_state_tensors(o)]
+        return [o for s in subs for o in _leaf_optimizers(s)]
     inner = getattr(optimizer, "opt", None)          # DistributedOptimizer wraps one
     if inner is not None and not hasattr(optimizer, "param_groups"):
-        return _optimizer_state_tensors(inner)
-    state = getattr(optimizer, "state", None)
-    if not state:        # nothing to send (e.g. ShardedMasterSGD: masters derive from weights)
+        return _leaf_optimizers(inner)
+    return [optimizer]
+
+
+def _state_layout(opt) -> list:
+    """[(group, param, key, kind, meta)] of a torch-style optimizer's per-parameter state: kind
+    "t" for tensors (meta = shape, dtype name), "v" for plain values (meta = the value)."""
+    state = getattr(opt, "state", None)
+    if not state or not hasattr(opt, "param_groups"):
         return []
     out = []
-    for group in optimizer.param_groups:
-        for p in group["params"]:
-            for v in state.get(p, {}).values():
+    for gi, group in enumerate(opt.param_groups):
+        for pi, p in enumerate(group["params"]):
+            st = state.get(p, {})
+            for k in sorted(st, key=str):
+                v = st[k]
                 if torch.is_tensor(v):
-                    out.append(v)
+                    out.append((gi, pi, k, "t", (tuple(v.shape), str(v.dtype).split(".")[-1])))
+                else:
+                    out.append((gi, pi, k, "v", v))
+    return out
+
+
+def _optimizer_state_tensors(optimizer) -> List[torch.Tensor]:
+    out = []
+    for opt in _leaf_optimizers(optimizer):
+        state = getattr(opt, "state", None)
+        if not state:        # nothing to send (e.g. ShardedMasterSGD: masters derive from weights)
+            continue
+        for group in opt.param_groups:
+            for p in group["params"]:
+                st = state.get(p, {})
+                for k in sorted(st, key=str):
+                    if torch.is_tensor(st[k]):
+                        out.append(st[k])
     return out
 
 
 def broadcast_optimizer_state(optimizer, root_rank: int = 0) -> None:
-    """Broadcast the root's optimizer state tensors (momentum buffers, Adam moments) in place.
-    Recurses into ``OptimizerGroup`` members; optimizers without per-parameter state are
-    skipped. Every rank must hold the same state structure (call after a first step or on
-    freshly built optimizers)."""
+    """Broadcast the root's optimizer state (momentum buffers, Adam moments, step counts) in
+    place. Recurses into ``OptimizerGroup`` members; optimizers without per-parameter state are
+    skipped. The usual Horovod pattern works -- a checkpoint loaded on the root only: the root's
+    state LAYOUT is broadcast first, and every other rank creates whatever state it lacks (zeros
+    of the root's shape and dtype, the root's plain values) before the tensors move, so every
+    rank enters the same collectives."""
+    if size() == 1:
+        return
+    leaves = _leaf_optimizers(optimizer)
+    box = [[_state_layout(o) for o in leaves] if rank() == root_rank else None]
+    dist.broadcast_object_list(box, src=root_rank)
+    layouts = box[0]
+    if len(layouts) != len(leaves):
+        raise RuntimeError(f"broadcast_optimizer_state: root has {len(layouts)} optimizers, "
+                           f"rank {rank()} has {len(leaves)}")
+    for opt, layout in zip(leaves, layouts):
+        for gi, pi, k, kind, meta in layout:
+            p = opt.param_groups[gi]["params"][pi]
+            st = opt.state[p]          # torch optimizers' state is a defaultdict(dict)
+            if kind == "v":
+                st[k] = meta
+                continue
+            shape, dtname = meta
+            have = st.get(k)
+            dt = getattr(torch, dtname)
+            if not (torch.is_tensor(have) and tuple(have.shape) == shape and have.dtype == dt):
+                # torch keeps Adam's scalar "step" on the CPU unless capturable/fused
+                dev = have.device if torch.is_tensor(have) else (
+                    torch.device("cpu") if (k == "step" and shape == ()) else p.device)
+                st[k] = torch.zeros(shape, dtype=dt, device=dev)
     broadcast_parameters(_optimizer_state_tensors(optimizer), root_rank)
 
 

@@ -142,6 +142,54 @@ def test_hvd_broadcast_optimizer_state_recurses_groups():
     assert res[0][0] == 4.0
 
 
+def _hvd_root_only_state_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    torch.set_num_threads(1)
+    from torch import nn
+    from arena_amd.parallel import hvd
+    hvd.init("gloo")
+    try:
+        torch.manual_seed(3)
+        m = nn.Linear(3, 5)
+        o = torch.optim.Adam(m.parameters(), lr=0.1)
+        if rank == 0:       # "checkpoint loaded on the root only": only rank 0 has state
+            m(torch.ones(2, 3)).sum().backward()
+            o.step()
+            o.step()
+        hvd.broadcast_optimizer_state(o, root_rank=0)
+        st = [o.state[p] for p in m.parameters()]
+        q.put((rank, {"m": torch.cat([s["exp_avg"].reshape(-1) for s in st]).numpy(),
+                      "v": torch.cat([s["exp_avg_sq"].reshape(-1) for s in st]).numpy(),
+                      "step": [float(s["step"]) for s in st]}))
+        # the optimizer keeps working on every rank afterwards
+        m(torch.ones(2, 3)).sum().backward()
+        o.step()
+    finally:
+        hvd.shutdown()
+
+
+@pytest.mark.timeout(120)
+def test_hvd_broadcast_optimizer_state_root_only_state():
+    """ADVICE r4 (hvd.py:211): the Horovod pattern of restoring a checkpoint on rank 0 and
+    broadcasting the optimizer state. Rank 1 has NO state; it must not skip the collectives
+    (that hung the job): the root's state layout is broadcast first and rank 1 creates it."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hvd_root_only_state_worker, args=(r, world, port, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0]["m"], res[1]["m"])
+    np.testing.assert_array_equal(res[0]["v"], res[1]["v"])
+    assert res[1]["step"] == [2.0, 2.0] and np.abs(res[1]["m"]).sum() > 0
+
+
 def test_cluster_spec_parsing():
     env = {"TF_CONFIG": '{"cluster":{"ps":["h:1"],"worker":["a:2","b:3"]},'
                         '"task":{"type":"worker","index":1}}'}
