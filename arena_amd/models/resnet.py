@@ -71,9 +71,13 @@ class Bottleneck(nn.Module):
         if self.down_conv is not None:
             y, st = self.down_conv.forward_stats(x, join=join, bn_link=link)
             idt = self.down_bn(y, stats=st, res_in=rmask)
+        # bn1 / bn2 feed one conv each: folded into it where the kernels allow (the conv
+        # normalises its staged operand; the BN output is never written, see BNFold)
         y, st = self.conv1.forward_stats(x, join=join, bn_link=link)
-        y, st = self.conv2.forward_stats(self.bn1(y, stats=st, link=lk1), bn_link=lk1)
-        y, st = self.conv3.forward_stats(self.bn2(y, stats=st, link=lk2), bn_link=lk2)
+        a, fold = self.bn1.forward_fold(y, self.conv2, stats=st, link=lk1)
+        y, st = self.conv2.forward_stats(a, bn_link=lk1, fold=fold)
+        a, fold = self.bn2.forward_fold(y, self.conv3, stats=st, link=lk2)
+        y, st = self.conv3.forward_stats(a, bn_link=lk2, fold=fold)
         return self.bn3(y, residual=idt, stats=st, join=join if self.down_conv is None else None,
                         link=link_out, res_out=rmask)
 

@@ -179,7 +179,7 @@ def pick_variant(m: int, cout: int) -> int:
 def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int = -1,
                with_stats: bool = False, addend: Tensor | None = None, bn=None,
                addmask: Tensor | None = None, final: bool = False,
-               bn_acc: Tensor | None = None):
+               bn_acc: Tensor | None = None, pre: Tensor | None = None):
     """y = conv2d(x, w) (+ addend) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S].
 
     with_stats: returns (y, (part, rpb)) where part holds per-tile BatchNorm partials of y
@@ -194,7 +194,11 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
     (that BN's fp64 [2, C] backward sums) the epilogue adds them there instead and returns
     (y, None).
     final (with with_stats): the statistics come back finished, ``(y, FinishedStats)`` -- the
-    epilogue's fp64 atomics + last-tile ticket replace the BN's finalize launch."""
+    epilogue's fp64 atomics + last-tile ticket replace the BN's finalize launch.
+    pre: the BatchNorm-apply fold (``BNFold``, v2 / halo variants): with with_stats, x is the raw
+    input of a ReLU BN and ``pre`` its fp32 [3, C] (mean, scale, shift) -- the kernel convolves
+    relu(bn(x)) without it ever being stored; with ``bn`` (backward data), ``pre`` is that BN's
+    table and its ReLU bits are recomputed from bn_x (bn_mask unused)."""
     x = x.contiguous(memory_format=torch.channels_last)
     w = w.contiguous(memory_format=torch.channels_last)
     if variant < 0:
@@ -209,7 +213,8 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
     fin = bool(final and with_stats and bn is None and addend is None)
     out = _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant), bool(with_stats),
                                addend, bx, bm, bmu, addmask if addend is not None else None,
-                               stats_final=fin, bn_acc=bn_acc if bn is not None else None)
+                               stats_final=fin, bn_acc=bn_acc if bn is not None else None,
+                               pre=pre)
     if bn is not None and bn_acc is not None:
         return out[0], None          # the sums went into the caller's bn_acc
     if fin:
@@ -230,7 +235,8 @@ def flip_weight(w: Tensor) -> Tensor:
 
 def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1,
                     addend: Tensor | None = None, bn=None, wflip: Tensor | None = None,
-                    addmask: Tensor | None = None, bn_acc: Tensor | None = None):
+                    addmask: Tensor | None = None, bn_acc: Tensor | None = None,
+                    pre: Tensor | None = None):
     """dX (+ addend) of a stride-1 convolution (same spatial size when pad = (R-1)/2).
     With ``bn`` (see conv2d_fwd) returns (dX, (part, rpb)): the backward partials of the
     BatchNorm layer whose output is this convolution's input. ``wflip``: ``flip_weight(w)``
@@ -238,7 +244,7 @@ def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1,
     r = w.shape[2]
     wf = wflip if wflip is not None else flip_weight(w)
     return conv2d_fwd(dy, wf, 1, r - 1 - pad, variant, addend=addend, bn=bn, addmask=addmask,
-                      bn_acc=bn_acc)
+                      bn_acc=bn_acc, pre=pre)
 
 
 # On by default since the v2 tiles carry the partials in their coalesced store loop and the plan
@@ -462,16 +468,19 @@ class BNGradLink:
     With the BN's own backward-sum set (``bacc``, batchnorm._BwdAcc) and few enough (tile,
     channel) pairs (``_use_acc``), the epilogue adds fp64 sums into that set instead of writing
     per-tile partials, and the BN's dx pass reads them directly: no reduction, no finalize."""
-    __slots__ = ("x", "mask", "mean", "bacc", "part", "rpb", "acc", "dy_ptr")
+    __slots__ = ("x", "mask", "mean", "bacc", "part", "rpb", "acc", "dy_ptr", "coef")
 
     def __init__(self):
-        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = None
+        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = self.coef = None
         self.rpb = 0
         self.dy_ptr = 0
 
-    def set_bn(self, x: Tensor, mask: Tensor | None, mean: Tensor, bacc=None) -> None:
+    def set_bn(self, x: Tensor, mask: Tensor | None, mean: Tensor, bacc=None,
+               coef: Tensor | None = None) -> None:
+        """``coef``: a folded BN (no output, no mask stored): its [3, C] table, from which the
+        linked epilogue recomputes the ReLU bits."""
         if _BN_LINKS:
-            self.x, self.mask, self.mean, self.bacc = x, mask, mean, bacc
+            self.x, self.mask, self.mean, self.bacc, self.coef = x, mask, mean, bacc, coef
 
     def ready(self) -> bool:
         return self.x is not None
@@ -491,7 +500,7 @@ class BNGradLink:
                 out = ("acc", self.acc)
             elif self.part is not None:
                 out = (self.part, self.rpb)
-        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = None
+        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = self.coef = None
         self.dy_ptr = 0
         return out
 
@@ -595,16 +604,17 @@ def wgrad_variants_for(cin: int, cout: int):
 
 def conv2d_wgrad(x: Tensor, dy: Tensor, kernel: Tuple[int, int], stride: int = 1, pad: int = 0,
                  variant: int = -1, splits: int = 0, out_dtype=torch.bfloat16,
-                 scale: float = 1.0) -> Tensor:
+                 scale: float = 1.0, pre: Tensor | None = None) -> Tensor:
     """dW [Cout, C, R, S] (channels_last) of y = conv2d(x, w): split-K MFMA kernel + a
-    fixed-order slab reduction (bit-reproducible)."""
+    fixed-order slab reduction (bit-reproducible). ``pre`` (the BN fold): x is the raw input of
+    the ReLU BN with coefficient table ``pre`` and the kernel uses relu(bn(x)) as its X operand."""
     x = x.contiguous(memory_format=torch.channels_last)
     dy = dy.contiguous(memory_format=torch.channels_last)
     if variant < 0:
         variant = wgrad_variants_for(x.shape[1], dy.shape[1])[0]
     return _ext.load().conv_wgrad(x, dy, int(kernel[0]), int(kernel[1]), int(stride), int(pad),
                                   int(variant), int(splits), out_dtype == torch.float32,
-                                  float(scale))
+                                  float(scale), pre=pre)
 
 
 # ------------------------------------------------------------------------------------------------
@@ -646,8 +656,50 @@ class ConvPlan:
     # in that form, since the extra epilogue reorders the tiles (v1's 128x128 form drops to one
     # wave per SIMD, 196 VGPRs + 72 AGPRs)
     bwd_bn: object = MIOPEN
+    # the BatchNorm-apply fold (BNFold: x is a ReLU BN's raw input, normalised in the kernels'
+    # staged operands): forward with statistics, weight gradient, and the linked backward-data
+    # form with the ReLU bits recomputed -- v2 / halo variants only, timed in those forms. MIOPEN:
+    # no fold for this shape.
+    fwd_fold: object = MIOPEN
+    wgrad_fold: object = MIOPEN
+    bwd_bn_fold: object = MIOPEN
     tuned: bool = False
     times: Dict[str, float] = field(default_factory=dict)
+
+    def fold_ok(self) -> bool:
+        return self.fwd_fold != MIOPEN and self.wgrad_fold != MIOPEN
+
+
+# BatchNorm-apply fold (ARENA_BN_FOLD; see batchnorm.BatchNormAct2d.forward_fold): a ReLU BN whose
+# output only feeds one convolution is never materialised -- the conv stages the BN's input and
+# applies relu(fma(x - mean, scale, shift)) to each staged chunk in LDS (forward A operand, weight-
+# gradient X operand); the BN backward and the linked dgrad epilogue recompute the ReLU bits from
+# x. Geometry: 1x1 / stride 1 / unpadded (the generic v2 tiles) or 3x3 / stride 1 / pad 1 at
+# <= 63 wide (the halo tiles), C <= 512.
+_BN_FOLD = os.environ.get("ARENA_BN_FOLD", "1") == "1"
+_FOLD_MAX_C = 512
+
+
+def set_bn_fold(on: bool) -> None:
+    global _BN_FOLD
+    _BN_FOLD = bool(on)
+
+
+def bn_fold_enabled() -> bool:
+    return _BN_FOLD
+
+
+def fold_geometry_ok(cin: int, k, stride: int, pad: int, width: int) -> bool:
+    k = tuple(k)
+    return cin <= _FOLD_MAX_C and _V2_ON and (
+        (k == (1, 1) and stride == 1 and pad == 0)
+        or (k == (3, 3) and stride == 1 and pad == 1 and width <= HALO_MAX_W))
+
+
+def _fold_fwd_variants(cout: int, k, stride: int, pad: int, width: int):
+    if tuple(k) == (1, 1):
+        return v2_variants_for(cout)
+    return halo_variants_for(cout, k, stride, pad, width)
 
 
 _PLANS: Dict[tuple, ConvPlan] = {}
@@ -717,7 +769,7 @@ def _best(t: dict, kind: str, n: int):
 
 def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
     key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _PERSIST_ON,
-           _V2_ON, _BN_LINKS)
+           _V2_ON, _BN_LINKS, _BN_FOLD)
     plan = _PLANS.get(key)
     if plan is not None and (plan.tuned or torch.cuda.is_current_stream_capturing()):
         return plan
@@ -737,6 +789,14 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                      else -1) if "bwd" in dirs else MIOPEN)
         plan.wgrad = wg[len(wg) // 2] if (wg and "wgrad" in dirs) else MIOPEN
         plan.bwd_bn = plan.bwd if stride == 1 else MIOPEN
+        if _BN_FOLD and fold_geometry_ok(cin, k, stride, pad, x.shape[3]) and \
+                "fwd" in dirs and "wgrad" in dirs and wg:
+            fv = _fold_fwd_variants(cout, k, stride, pad, x.shape[3])
+            bv = v2_variants_for(cin) + halo_variants_for(cin, k, stride, pad, x.shape[3])
+            # the serial four-wave v2 tiles (V2 + 8 / 9) / the widest halo form
+            pick = lambda vs: next((v for v in (V2 + 8, V2 + 9, V2 + 14, V2 + 13)  # noqa: E731
+                                    if v in vs), MIOPEN)
+            plan.fwd_fold, plan.bwd_bn_fold, plan.wgrad_fold = pick(fv), pick(bv), plan.wgrad
         plan.tuned = mode == "ours"
     else:
         def tune() -> dict:
@@ -791,6 +851,22 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
             for c in wg:
                 fns[("wgrad", c)] = (lambda c=c: _time(
                     lambda: conv2d_wgrad(x, dy, k, stride, pad, c[0], c[1])))
+            # the BN fold's forms (BNFold): identity coefficients (relu(x)) -- the timing does not
+            # depend on the values
+            fold = _BN_FOLD and fold_geometry_ok(cin, k, stride, pad, x.shape[3])
+            coef = None
+            if fold:
+                coef = torch.stack([torch.zeros(cin), torch.ones(cin), torch.zeros(cin)]).to(
+                    device=x.device, dtype=torch.float32).contiguous()
+
+                def fwdpre_time(v):
+                    fin = _use_acc(m_out, v, cout)
+                    us = _time(lambda: conv2d_fwd(x, w, stride, pad, v, with_stats=True,
+                                                  final=fin, pre=coef))
+                    return us if fin else us + _FIN_PENALTY_US
+
+                for v in _fold_fwd_variants(cout, k, stride, pad, x.shape[3]):
+                    fns[("fwdpre", v)] = (lambda v=v: fwdpre_time(v))
             ext = _ext.load()
             ext.bn_acc_scratch(True)
             try:
@@ -805,11 +881,27 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                         fns[("bwd", v)] = (lambda v=v: _time(
                             lambda: conv2d_bwd_data(dy, w, pad, v)))
                         t[("bwd", v)] = fns[("bwd", v)]()
+                if fold:
+                    # the fold's weight gradient: the 3 fastest plain candidates in the pre form
+                    for c in _best(t, "wgrad", 3):
+                        fns[("wgradpre", c)] = (lambda c=c: _time(lambda: conv2d_wgrad(
+                            x, dy, k, stride, pad, c[0], c[1], pre=coef)))
+                        t[("wgradpre", c)] = fns[("wgradpre", c)]()
+                    # the linked backward-data form with the ReLU bits recomputed (v2 / halo)
+                    if _BN_LINKS and stride == 1:
+                        v2bn = [c for c in _best(t, "bwdbn", 64) if c >= V2][:3]
+                        for v in v2bn:
+                            acc = bsums if _use_link_acc(m_in, v, cin) else None
+                            fns[("bwdbnpre", v)] = (lambda v=v, acc=acc: _time(
+                                lambda: conv2d_bwd_data(dy, w, pad, v, bn=(bnx, None, bmean),
+                                                        bn_acc=acc, pre=coef)))
+                            t[("bwdbnpre", v)] = fns[("bwdbnpre", v)]()
                 # One timing per candidate picks the lucky one among near-equal variants (the
                 # choices moved run to run by ~1 % of the step): the 3 fastest of each direction are
                 # timed twice more, interleaved, and ranked by their median.
-                kinds = ("fwd", "bwd", "wgrad") + (
-                    ("bwdbn",) if any(k[0] == "bwdbn" for k in fns) else ())
+                kinds = ("fwd", "bwd", "wgrad") + tuple(
+                    kd for kd in ("bwdbn", "fwdpre", "wgradpre", "bwdbnpre")
+                    if any(k_[0] == kd for k_ in fns))
                 finals = {kind: _best(t, kind, 3) for kind in kinds}
                 reps = {(kind, c): [t[(kind, c)]] for kind, cs in finals.items() for c in cs}
                 for _ in range(2):
@@ -820,16 +912,18 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
             finally:
                 ext.bn_acc_scratch(False)
             out = {}
+            names = {"bwdbn": "bwd_bn", "fwdpre": "fwd_fold", "wgradpre": "wgrad_fold",
+                     "bwdbnpre": "bwd_bn_fold"}
             for kind in kinds:
                 best = min(t[(kind, c)] for c in finals[kind])
                 choice = next(c for c in finals[kind] if t[(kind, c)] == best)
-                out["bwd_bn" if kind == "bwdbn" else kind] = choice
+                out[names.get(kind, kind)] = choice
             out["times"] = {f"{kd}:{c}": round(v, 1) for (kd, c), v in t.items()}
             return out
 
         # one decision per job: rank 0 times, every rank adopts (or the ARENA_CONV_PLAN file)
         got = planstore.decide("conv", key[:4] + key[5:], x.device, tune)
-        for f in ("fwd", "bwd", "wgrad", "bwd_bn"):
+        for f in ("fwd", "bwd", "wgrad", "bwd_bn", "fwd_fold", "wgrad_fold", "bwd_bn_fold"):
             if f in got:
                 v = got[f]
                 setattr(plan, f, tuple(v) if isinstance(v, list) else v)
@@ -989,11 +1083,32 @@ class _nullctx:
         return False
 
 
+class BNFold:
+    """A ReLU BatchNorm folded into the convolution that consumes its output (see ``_BN_FOLD``):
+    the BN's forward (``BatchNormAct2d.forward_fold``) fills ``x`` (its raw input) and ``coef``
+    (its [3, C] mean / scale / shift) and returns a zero-stride placeholder of the output's shape
+    that only carries autograd; the conv reads ``x`` and normalises its staged operands with
+    ``coef``, and its backward-data result is the BN output's gradient, which flows back into the
+    BN's backward as usual."""
+    __slots__ = ("x", "coef")
+
+    def __init__(self):
+        self.x = self.coef = None
+
+
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, plan, want_stats, join=None, bn_link=None):
+    def forward(ctx, x, w, stride, pad, plan, want_stats, join=None, bn_link=None, fold=None):
         part = x.new_empty(0, dtype=torch.float32)
-        if plan.fwd == MIOPEN:
+        ctx.pre = None
+        if fold is not None:
+            # x is the folded BN's placeholder: convolve relu(bn(fold.x)) in the kernel
+            x, ctx.pre = fold.x, fold.coef
+            fin = _use_acc(_out_pixels(x, w, stride, pad), plan.fwd_fold, w.shape[0])
+            y, st = conv2d_fwd(x, w, stride, pad, plan.fwd_fold, with_stats=True, final=fin,
+                               pre=ctx.pre)
+            part = st.fin if fin else st[0]
+        elif plan.fwd == MIOPEN:
             y = F.conv2d(x, w, stride=stride, padding=pad)
         elif want_stats and _use_acc(_out_pixels(x, w, stride, pad), plan.fwd,
                                      w.shape[0]):
@@ -1003,7 +1118,7 @@ class _ConvFn(torch.autograd.Function):
             y, (part, _) = conv2d_fwd(x, w, stride, pad, plan.fwd, with_stats=True)
         else:
             y = conv2d_fwd(x, w, stride, pad, plan.fwd)
-        ctx.save_for_backward(x, w)
+        ctx.save_for_backward(x, w, ctx.pre)
         ctx.conf = (stride, pad, plan)
         ctx.w_leaf = w.is_leaf
         # W' of a WeightFlipper scope (flipped this step, before this forward)
@@ -1020,8 +1135,8 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dpart):
         if dy is None:
-            return None, None, None, None, None, None, None, None
-        x, w = ctx.saved_tensors
+            return None, None, None, None, None, None, None, None, None
+        x, w, pre = ctx.saved_tensors
         stride, pad, plan = ctx.conf
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
@@ -1040,7 +1155,8 @@ class _ConvFn(torch.autograd.Function):
             # the BN partials need the COMPLETE gradient of x: not from a join's first arriver
             use_bn = (lk is not None and plan.bwd != MIOPEN and stride == 1
                       and lk.x.shape == x.shape
-                      and (join is None or other is not None))
+                      and (join is None or other is not None)
+                      and (lk.coef is None or plan.bwd_bn_fold != MIOPEN))
             if plan.bwd == MIOPEN:
                 dx = _miopen_bwd(dy, x, w, stride, pad, [True, False, False])[0]
                 if other is not None:
@@ -1049,18 +1165,22 @@ class _ConvFn(torch.autograd.Function):
                 dx = conv2d_bwd_data_strided(dy, w, (x.shape[2], x.shape[3]), stride, pad,
                                              plan.bwd, addend=other)
             elif use_bn:
-                vb = plan.bwd if plan.bwd_bn == MIOPEN else plan.bwd_bn
+                if lk.coef is not None:   # a folded BN: v2 / halo form, bits from its table
+                    vb = plan.bwd_bn_fold
+                else:
+                    vb = plan.bwd if plan.bwd_bn == MIOPEN else plan.bwd_bn
                 m_in = x.shape[0] * x.shape[2] * x.shape[3]
                 if lk.bacc is not None and _use_link_acc(m_in, vb, x.shape[1]):
                     acc = lk.bacc.for_backward(x, x.shape[1])
                     dx, _ = conv2d_bwd_data(dy, w, pad, vb, addend=other,
                                             bn=(lk.x, lk.mask, lk.mean), wflip=ctx.wflip,
-                                            addmask=omask, bn_acc=acc)
+                                            addmask=omask, bn_acc=acc, pre=lk.coef)
                     lk.publish_acc(acc, dx)
                 else:
                     dx, (part, rpb) = conv2d_bwd_data(dy, w, pad, vb, addend=other,
                                                       bn=(lk.x, lk.mask, lk.mean),
-                                                      wflip=ctx.wflip, addmask=omask)
+                                                      wflip=ctx.wflip, addmask=omask,
+                                                      pre=lk.coef)
                     lk.publish(part, rpb, dx)
             else:
                 dx = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other, wflip=ctx.wflip,
@@ -1074,7 +1194,11 @@ class _ConvFn(torch.autograd.Function):
                 side = _side_stream(dy.device)
                 side.wait_stream(main)   # dy, x (and w) are complete on the main stream
             with torch.cuda.stream(side) if side is not None else _nullctx():
-                if plan.wgrad == MIOPEN:
+                if pre is not None:        # the folded BN's output as the X operand
+                    v, sp = plan.wgrad_fold
+                    dw = conv2d_wgrad(x, dy, (w.shape[2], w.shape[3]), stride, pad, v, sp,
+                                      out_dtype=w.dtype, pre=pre)
+                elif plan.wgrad == MIOPEN:
                     dw = _miopen_bwd(dy, x, w, stride, pad, [False, True, False])[1]
                 else:
                     v, sp = plan.wgrad
@@ -1085,7 +1209,7 @@ class _ConvFn(torch.autograd.Function):
                 x.record_stream(side)
                 dy.record_stream(side)
                 dw.record_stream(main)
-        return dx, dw, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None, None
 
 
 class Conv2dNHWC(nn.Conv2d):
@@ -1104,12 +1228,43 @@ class Conv2dNHWC(nn.Conv2d):
     def forward(self, x: Tensor) -> Tensor:
         return self.forward_stats(x, want_stats=False)[0]
 
+    def fold_plan(self, x: Tensor):
+        """The plan for input ``x`` (the raw input of a ReLU BN about to be folded into this
+        conv) when the fold applies to this conv and shape, else None. Tunes on first use."""
+        if not (_BN_FOLD and x.is_cuda and _mode() != "off" and x.dtype == torch.bfloat16
+                and self.training and torch.is_grad_enabled()):
+            return None
+        w = self.weight
+        if w.dtype != torch.bfloat16:
+            if not (torch.is_autocast_enabled("cuda")
+                    and torch.get_autocast_dtype("cuda") == torch.bfloat16):
+                return None
+            w = w.to(torch.bfloat16)
+        s, p = self.stride[0], self.padding[0]
+        if not fold_geometry_ok(x.shape[1], (w.shape[2], w.shape[3]), s, p, x.shape[3]):
+            return None
+        plan = plan_for(x.contiguous(memory_format=torch.channels_last),
+                        w.contiguous(memory_format=torch.channels_last), s, p)
+        return plan if plan.fold_ok() else None
+
     def forward_stats(self, x: Tensor, want_stats: bool = True, join: GradJoin | None = None,
-                      bn_link: BNGradLink | None = None):
+                      bn_link: BNGradLink | None = None, fold: BNFold | None = None):
         """(y, stats): ``stats`` are the BatchNorm partials of y for ``BatchNormAct2d(y,
         stats=stats)`` when the kernel produced y (else None: the BN computes them itself).
         ``join``: x has a second consumer registered on the same GradJoin (see there).
-        ``bn_link``: x is the output of the BatchNorm layer that filled this link."""
+        ``bn_link``: x is the output of the BatchNorm layer that filled this link.
+        ``fold``: x is the placeholder of a folded BN's output (``BatchNormAct2d.forward_fold``
+        after ``fold_plan`` accepted it): the kernels convolve relu(bn(fold.x))."""
+        if fold is not None:
+            w = self.weight
+            if w.dtype != torch.bfloat16:
+                w = w.to(torch.bfloat16)
+            w = w.contiguous(memory_format=torch.channels_last)
+            s, p = self.stride[0], self.padding[0]
+            plan = plan_for(fold.x, w, s, p)
+            with torch.autocast("cuda", enabled=False):
+                y, part = _ConvFn.apply(x, w, s, p, plan, True, join, bn_link, fold)
+            return y, _stats_out(want_stats, part, TILES[plan.fwd_fold][0])
         if not x.is_cuda or _mode() == "off":
             return super().forward(x), None
         amp = torch.is_autocast_enabled("cuda") and \

@@ -14,8 +14,8 @@ slowest rank sets a synchronous step) and different fp32 accumulation orders. So
   inside :func:`rank_local`, or the job sets ``ARENA_CONV_PLAN_SHARE=0``;
 * **persisted plans**: ``ARENA_CONV_PLAN=<path>`` names a JSON file of plans keyed by
   (kind, GPU arch, kernel-source hash, shape, stride, pad, mode flags). A plan found there is used
-  without timing anything; plans tuned in this run are merged into it by rank 0. A file written
-  by a different build of the kernels (source hash) is ignored with a warning;
+  without timing anything; plans decided in this run are merged into it by global rank 0. Plans
+  of a different build of the kernels (another source hash) never match;
 * the time spent tuning is accumulated (:func:`stats`) and printed by the benchmarks.
 """
 from __future__ import annotations
@@ -160,12 +160,23 @@ def decide(kind: str, key: tuple, device, tune: Callable[[], dict]) -> dict:
         dist.broadcast_object_list(box, src=0)
         value = box[0]
         _STATS["shared" if sw[0] == 0 else "received"] += 1
-    if sw is None or sw[0] == 0:
+    if _writer():
         try:
             _save(fkey, value)
         except OSError as e:
             print(f"[conv-plan] could not write {_path()}: {e}", file=sys.stderr)
     return value
+
+
+def _writer() -> bool:
+    """Only global rank 0 writes the plan file (one writer per job, no clobbering)."""
+    try:
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank() == 0
+    except Exception:  # noqa: BLE001
+        pass
+    return True
 
 
 def reset() -> None:

@@ -113,6 +113,14 @@ struct ConvArgs {
   };
   int nph;             // 0: a single convolution
   Phase ph[4];
+  // BatchNorm-apply fold (v2 / halo tiles only): x is the RAW input of a ReLU BatchNorm layer
+  // whose output this convolution consumes, and pre = [3][C] floats (batch mean, scale, shift)
+  // of that layer. EPI 1 (forward): the A operand becomes relu(fma(x - mean, scale, shift))
+  // rounded to bf16 -- bn_apply_kernel's arithmetic and rounding, so the products equal the
+  // unfused path's bit for bit -- transformed once per staged chunk in LDS (the BN output is never
+  // written). EPI 2 (backward-data with BN-backward sums): the ReLU bits of that BN's output are
+  // recomputed from bnx with the same arithmetic instead of read from bnmask (pre = [3][Cout]).
+  const float* pre;
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -174,6 +182,65 @@ __device__ __forceinline__ uint32_t pack_bf16x2(float a, float b) {
 
 __device__ __forceinline__ float bf16_round(float f) {
   return __uint_as_float(pack_bf16x2(f, 0.f) << 16);
+}
+
+// ---- BatchNorm-apply fold (ConvArgs::pre, WgradArgs::pre) ----
+constexpr int kPreMaxC = 512;   // widest folded BN (the bottleneck mid widths 64..512)
+
+struct PreCoef {   // 8 channels' (mean, scale, shift)
+  f32x4v mu0, mu1, sc0, sc1, sh0, sh1;
+};
+
+// coefficients of channels c..c+7 from a [3][ld] float table (global or LDS)
+__device__ __forceinline__ PreCoef pre_coef(const float* t, int ld, int c) {
+  PreCoef k;
+  k.mu0 = *reinterpret_cast<const f32x4v*>(t + c);
+  k.mu1 = *reinterpret_cast<const f32x4v*>(t + c + 4);
+  k.sc0 = *reinterpret_cast<const f32x4v*>(t + ld + c);
+  k.sc1 = *reinterpret_cast<const f32x4v*>(t + ld + c + 4);
+  k.sh0 = *reinterpret_cast<const f32x4v*>(t + 2 * ld + c);
+  k.sh1 = *reinterpret_cast<const f32x4v*>(t + 2 * ld + c + 4);
+  return k;
+}
+
+__device__ __forceinline__ float pre_val(float x, float mu, float sc, float sh) {
+  return fmaxf(fmaf(x - mu, sc, sh), 0.f);
+}
+
+// 8 bf16 (one 16-byte chunk) -> relu(fma(x - mean, scale, shift)), rounded to bf16
+__device__ __forceinline__ uint4 pre_chunk(uint4 q, const PreCoef& k) {
+  const uint32_t u[4] = {q.x, q.y, q.z, q.w};
+  uint32_t o[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const f32x4v& mu = e < 2 ? k.mu0 : k.mu1;
+    const f32x4v& sc = e < 2 ? k.sc0 : k.sc1;
+    const f32x4v& sh = e < 2 ? k.sh0 : k.sh1;
+    const int i = (2 * e) & 3;
+    o[e] = pack_bf16x2(pre_val(__uint_as_float(u[e] << 16), mu[i], sc[i], sh[i]),
+                       pre_val(__uint_as_float(u[e] & 0xffff0000u), mu[i + 1], sc[i + 1],
+                               sh[i + 1]));
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+// the ReLU bits of that BN output at 8 channels (bn_apply's store_pos rule: the stored bf16 > 0)
+__device__ __forceinline__ uint32_t pre_bits(uint4 q, const PreCoef& k) {
+  const uint4 r = pre_chunk(q, k);
+  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
+  uint32_t b = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const uint32_t h = (i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xffffu);
+    const bool pos = (h & 0x8000u) == 0 && (h & 0x7fffu) != 0 && (h & 0x7fffu) <= 0x7f80u;
+    b |= (pos ? 1u : 0u) << i;
+  }
+  return b;
+}
+
+// in place on a staged chunk in LDS
+__device__ __forceinline__ void pre_lds(uint8_t* p, const PreCoef& k) {
+  *reinterpret_cast<uint4*>(p) = pre_chunk(*reinterpret_cast<const uint4*>(p), k);
 }
 
 // sum over the 16 lanes of a DPP row (lane bits 0..3); every lane of the row gets the sum
@@ -1103,7 +1170,7 @@ struct Conv2Geo {
 // The v2 epilogue: the accumulators through an fp32 LDS tile at `lds` (EH x BN floats, bands of
 // EH rows), coalesced bf16 stores (+ addend, mapped placement, fill_sib), and the EPI 1 / EPI 2
 // BatchNorm sums (their partials reuse the tile).
-template <class G, int EPI>
+template <class G, int EPI, bool PRE = false>
 __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
                                                f32x16v (&acc)[G::MI][G::NI], uint8_t* lds,
                                                int m0, int n0, int mt, int tid, int wm, int wn,
@@ -1131,6 +1198,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
   // EPI 2: this thread's 8 channels (n0 + (tid % CPR) * 8 + e: the store loop below keeps a
   // thread on one 16-byte column chunk) -- sum g and sum g * (x - mean) over its rows
   float e1[EPI == 2 ? 8 : 1], e2[EPI == 2 ? 8 : 1], emu[EPI == 2 ? 8 : 1];
+  PreCoef epk;   // EPI 2 + PRE: the folded BN's coefficients of this thread's 8 channels
   if constexpr (EPI == 2) {
     static_assert(NT % CPR == 0, "EPI 2: a thread's column chunk is fixed");
     const float* mp = a.bnmean + n0 + (tid % CPR) * 8;
@@ -1140,6 +1208,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
       e2[e] = 0.f;
       emu[e] = mp[e];
     }
+    if constexpr (PRE) epk = pre_coef(a.pre, a.Cout, n0 + (tid % CPR) * 8);
   }
 #pragma unroll
   for (int band = 0; band < BM / EH; ++band) {
@@ -1184,7 +1253,10 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
       uint32_t bmk = 0xffu;
       if constexpr (EPI == 2) {   // the BN layer's input and ReLU bits at the same pixel/channels
         bxq = *reinterpret_cast<const uint4*>(a.bnx + off);
-        if (a.bnmask) bmk = a.bnmask[(size_t)(rbase + row) * (a.Cout >> 3) + (n0 >> 3) + cc];
+        if constexpr (PRE)          // folded BN: its output was never stored, recompute the bits
+          bmk = pre_bits(bxq, epk);
+        else if (a.bnmask)
+          bmk = a.bnmask[(size_t)(rbase + row) * (a.Cout >> 3) + (n0 >> 3) + cc];
       }
       if (EPI != 1 && a.add != nullptr) {
         const uint4 qa = masked_add8(a.add, a.addmask, off);
@@ -1308,13 +1380,24 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
 }
 
 template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false,
-          int HALO = 0>
+          int HALO = 0, bool PRE = false>
 __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
   using G = Conv2Geo<BM, BN, NWM, NWN, NBUF, EPI, BAND, HALO>;
   constexpr int NT = G::NT, WM = G::WM, WN = G::WN, MI = G::MI, NI = G::NI;
   constexpr int AI = G::AI, BI = G::BI, kBufBytes = G::kBufBytes;
   constexpr int SL = G::SL, RG = G::RG, EH = G::EH;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[G::kLds];
+  static_assert(!PRE || EPI != 0, "the BN fold rides on the statistics / BN-backward epilogues");
+  // BN fold, forward, generic tiles: the folded BN's [3][C] coefficient table sits behind the stage
+  // buffers (the epilogue may overwrite it: the K loop is done with it). The halo form keeps its
+  // one chunk of coefficients per thread in registers instead (its LDS is sized to the block).
+  constexpr bool kPreA = PRE && EPI == 1;
+  constexpr int kPreTab = (kPreA && !HALO) ? 3 * kPreMaxC * 4 : 0;
+  constexpr int kLdsAll = G::kStage + kPreTab > G::kLds ? G::kStage + kPreTab : G::kLds;
+  static_assert(kLdsAll <= kLdsMax, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsAll];
+  // the fold's transform assignment: thread = (logical 16-byte chunk lc, first row) of the staged
+  // A rows; every thread transforms one chunk position, so it needs one chunk's coefficients
+  const int pre_lc = threadIdx.x & 7, pre_r0 = threadIdx.x >> 3;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // XCD-aware order (as v1): each XCD gets a contiguous range of tiles, column tiles of one row
@@ -1433,12 +1516,23 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
     static_assert(D >= 1 && D < 9, "weight ring depth");
     const int CB = a.C / kBK;
     for (int cb = 0; cb < CB; ++cb) {
+      PreCoef pk;
+      if constexpr (kPreA) pk = pre_coef(a.pre, a.C, cb * kBK + pre_lc * 8);
       stage_win(cb);   // the previous chunk's last tap ended on a barrier: the window is free
 #pragma unroll
       for (int t = 0; t < D; ++t) stage_b(t, cb, t);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * BI) : "memory");   // window + tap 0
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      if constexpr (kPreA) {
+        // BN fold: every in-image window row through relu(fma(x - mean, scale, shift)) once
+        // (rows outside [0, M) only feed masked taps and stay zero)
+        for (int j = pre_r0; j < WR; j += NT / 8) {
+          const int pix = org + j;
+          if (pix >= 0 && pix < a.M) pre_lds(lds + j * kRowBytes + ((pre_lc ^ swz(j)) << 4), pk);
+        }
+        lds_barrier();
+      }
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         // buffer (t + D) % NBUF was last read by tap t - 1, before the barrier that ended it
@@ -1484,6 +1578,23 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
     const int CB = a.C / kBK;
     const int T = a.Ktot / kBK;
     int s_tap = 0, s_cb = 0, s_s = 0, s_tapoff = 0, s_t = 0;
+    if constexpr (kPreA) {   // the folded BN's coefficients, once per block
+      float* tab = reinterpret_cast<float*>(lds + G::kStage);
+      for (int i = threadIdx.x; i < 3 * a.C; i += NT) tab[i] = a.pre[i];
+      lds_barrier();
+    }
+    // BN fold (1x1 / stride 1 / unpadded, host-checked): step t's A tile (chunk t % CB) in buffer
+    // `buf` through relu(fma(x - mean, scale, shift)); rows past M stay as they are (never stored)
+    auto pre_tile = [&](int buf, int t) {
+      if constexpr (kPreA) {
+        const float* tab = reinterpret_cast<const float*>(lds + G::kStage);
+        const PreCoef pk = pre_coef(tab, a.C, (t % CB) * kBK + pre_lc * 8);
+        uint8_t* abuf = lds + buf * kBufBytes;
+        for (int r = pre_r0; r < BM; r += NT / 8)
+          if (m0 + r < a.M) pre_lds(abuf + r * kRowBytes + ((pre_lc ^ swz(r)) << 4), pk);
+        lds_barrier();
+      }
+    };
   #pragma unroll
     for (int i = 0; i < AI; ++i) a_cur[i] = (a_mask[i] & 1u) ? (uint32_t)a_lane[i] : kOOB;
 
@@ -1546,6 +1657,7 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
       if (T > 0) stage(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (T > 0) pre_tile(0, 0);
       for (int t = 0; t < T; ++t) {
         compute(0);
         if (t + 1 < T) {
@@ -1554,6 +1666,7 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
+        if (t + 1 < T) pre_tile(0, t + 1);
       }
     } else {
       constexpr int S = NBUF - 1;
@@ -1567,6 +1680,7 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      if (T > 0) pre_tile(0, 0);
       int cur = 0;
       for (int t = 0; t < T; ++t) {
         // RAW: stage t + 1 was retired by the vmcnt before the last barrier. WAR: stage t + S
@@ -1580,11 +1694,13 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         cur = cur == NBUF - 1 ? 0 : cur + 1;
+        // the fold of stage t + 1 (buffer cur): every wave is past compute(t) and its data landed
+        if (t + 1 < T) pre_tile(cur, t + 1);
       }
     }
   }
 
-  conv2_epilogue<G, EPI>(a, acc, lds, m0, n0, mt, tid, wm, wn, fr, hh);
+  conv2_epilogue<G, EPI, PRE>(a, acc, lds, m0, n0, mt, tid, wm, wn, fr, hh);
 }
 
 // The multi-phase launch: this block's phase, its arguments and its block index within it
@@ -1605,7 +1721,7 @@ __device__ __forceinline__ bool conv2_phase(const ConvArgs& a, ConvArgs& b, int&
   return bid < b.m_tiles * b.n_tiles;
 }
 
-template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI>
+template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool PRE = false>
 __global__ __launch_bounds__(64 * NWM * NWN) void conv2_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
   if constexpr (EPI == 0) {
@@ -1616,14 +1732,14 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv2_kernel(ConvArgs a) {
       return;
     }
   }
-  conv2_body<BM, BN, NWM, NWN, NBUF, EPI>(a, blockIdx.x);
+  conv2_body<BM, BN, NWM, NWN, NBUF, EPI, false, 0, PRE>(a, blockIdx.x);
 #endif
 }
 
 // serial, wave-row epilogue bands, <= 128 VGPRs: four waves per SIMD (up to four 4-wave blocks
 // per CU by LDS), the structure that wins the streaming-bound layers in v1 (variants 8..11)
 // (EPI 2 on the 128x128 tile: three waves per SIMD -- its 24 extra live registers spill at four)
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, bool PRE = false>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(EPI == 2 && BM * BN >= 128 * 128 ? 3 : 4)))
 void conv2_kernel_occ4(ConvArgs a) {
@@ -1636,17 +1752,17 @@ void conv2_kernel_occ4(ConvArgs a) {
       return;
     }
   }
-  conv2_body<BM, BN, 2, 2, 1, EPI, true>(a, blockIdx.x);
+  conv2_body<BM, BN, 2, 2, 1, EPI, true, 0, PRE>(a, blockIdx.x);
 #endif
 }
 
 // the 3x3 halo form (see Conv2Geo::HALO): 4 waves, a ring of NBR per-tap weight buffers --
 // 128x128: three (80 KB, two blocks per CU); 128x64: two (48 KB, three blocks per CU; with the
 // small window of <= 31-wide images 40 KB, four blocks per CU)
-template <int BM, int BN, int EPI, int HW>
+template <int BM, int BN, int EPI, int HW, bool PRE = false>
 __global__ __launch_bounds__(256) void conv2_kernel_halo(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, HW>(a, blockIdx.x);
+  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, HW, PRE>(a, blockIdx.x);
 #endif
 }
 
@@ -1662,7 +1778,14 @@ hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
-  if (a.bnx != nullptr)
+  if (a.pre != nullptr) {   // BN fold: forward with statistics, or the linked backward-data form
+    if (a.bnx != nullptr)
+      hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW, true>), dim3(nwg), dim3(256), 0, st, a);
+    else if ((a.part != nullptr || a.bn_acc != nullptr) && a.C <= kPreMaxC)
+      hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1, HW, true>), dim3(nwg), dim3(256), 0, st, a);
+    else
+      return hipErrorInvalidValue;
+  } else if (a.bnx != nullptr)
     hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW>), dim3(nwg), dim3(256), 0, st, a);
   else if (a.part != nullptr || a.bn_acc != nullptr)
     hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1, HW>), dim3(nwg), dim3(256), 0, st, a);
@@ -1691,6 +1814,26 @@ hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
       b0 += ((int)((mp + BM - 1) / BM) * a.n_tiles + 7) / 8 * 8;
     }
     nwg = b0;
+  }
+  if (a.pre != nullptr) {
+    // BN fold: the forward with statistics of a 1x1 / stride 1 / unpadded conv (the A tile is a
+    // plain pixel block), or the linked backward-data form (ReLU bits from the coefficients)
+    const bool fwd_ok = stats && !bwd_bn && a.R == 1 && a.S == 1 && a.stride == 1 &&
+                        a.pad == 0 && a.pad_w == 0 && a.C <= kPreMaxC && !a.mapped && a.nph == 0;
+    if (!(bwd_bn || fwd_ok)) return hipErrorInvalidValue;
+    if constexpr (OCC4) {
+      if (bwd_bn)
+        hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 2, true>), dim3(nwg), dim3(256), 0, st, a);
+      else
+        hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 1, true>), dim3(nwg), dim3(256), 0, st, a);
+    } else if (bwd_bn) {
+      hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 2, true>), dim3(nwg),
+                         dim3(64 * NWM * NWN), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 1, true>), dim3(nwg),
+                         dim3(64 * NWM * NWN), 0, st, a);
+    }
+    return hipGetLastError();
   }
   if constexpr (OCC4) {
     if (bwd_bn)
@@ -1784,7 +1927,7 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
                              int H, int W, int C, int Cout, int R, int S, int stride, int pad_h,
                              int pad_w, int Ho, int Wo, const int* y_map, int c16, int variant,
                              double* bn_acc, int ksplit, void* kws, unsigned* kcnt, int tpb,
-                             hipStream_t st) {
+                             const float* pre, hipStream_t st) {
   if (Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0) return hipErrorInvalidValue;
   if (tpb < 1 || (tpb > 1 && ksplit != 1)) return hipErrorInvalidValue;
   if (c16 ? (C != 16 || S % 4) : (C % kBK)) return hipErrorInvalidValue;
@@ -1852,10 +1995,12 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.kcnt = kcnt;
   a.tpb = tpb;
   a.st1p = g_conv_st1p;
+  a.pre = pre;
   if (v2) {
     if (c16) return hipErrorInvalidValue;
     return launch2(a, variant - kV2Base, st);
   }
+  if (pre != nullptr) return hipErrorInvalidValue;   // the BN fold runs on the v2 / halo tiles
   if (variant >= 12) {   // 256-row tiles, 8 waves: 12/13 two stage buffers, 14/15 three
     const int nb = variant >= 14 ? 3 : 2;
     if ((variant & 1) == 0)
@@ -1925,7 +2070,7 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
                           int variant, hipStream_t st) {
   return arena_conv_fwd_ex(x, w, y, part, add, nullptr, bnx, bnmask, bnmean, N, H, W, C, Cout, R, S,
                            stride, pad, pad, 0, 0, nullptr, 0, variant, nullptr, 1, nullptr, nullptr,
-                           1, st);
+                           1, nullptr, st);
 }
 
 // Split-K workspace of one launch, in floats (0 when ksplit == 1), and its ticket count (tiles).
@@ -2327,6 +2472,10 @@ struct WgradArgs {
   int c16;             // C == 16, a BN = 64 column tile = one filter row x 4 columns x 16 channels
   int xbytes, dybytes; // buffer-descriptor ranges (both < 2^31 bytes, host-checked)
   int aff;             // 1x1, stride 1, no padding: X pixel m is output pixel m (affine staging)
+  // BatchNorm-apply fold (see ConvArgs::pre): x is the raw input of the ReLU BN whose output the
+  // convolution consumed, pre = its [3][C] (mean, scale, shift); the X image is normalised in LDS
+  // once per staged step (padded taps stay zero)
+  const float* pre;
 };
 
 // chunk permutation of a pixel row of RB bytes (bit 0 of the chunk index is kept: 32-B pairs)
@@ -2338,7 +2487,7 @@ __device__ __forceinline__ int wswz(int row) {
 
 // NBUF 2: double-buffered pixel steps; NBUF 1 (variants 4..7): one buffer, serial steps, four
 // waves per SIMD -- more blocks per CU hide the staging latency instead (see conv_fwd_kernel_occ4).
-template <int BM, int BN, int NBUF>
+template <int BM, int BN, int NBUF, bool PRE = false>
 __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
   constexpr int RA = BM * 2, RBB = BN * 2;        // row bytes of the A (dY) and B (X) images
   constexpr int CA = RA / 16, CB = RBB / 16;       // 16-byte chunks per row
@@ -2346,7 +2495,8 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
   constexpr int AI = kPix * CA / kThreads, BI = kPix * CB / kThreads;
   constexpr int kBuf = kPix * (RA + RBB);
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
-  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf];
+  // PRE: the folded BN's coefficients of this block's BN input channels behind the stage buffers
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf + (PRE ? 3 * BN * 4 : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = a.m_tiles * a.n_tiles;
@@ -2453,10 +2603,41 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
   const int wm = wave >> 1, wn = wave & 1;
   const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
 
+  // BN fold: the X image of step `step` in buffer `buf` through relu(fma(x - mean, scale, shift));
+  // thread = one logical chunk of rows tid / CB + k * kThreads / CB (one chunk's coefficients)
+  auto pre_x = [&](int buf, int step) {
+    if constexpr (PRE) {
+      const int lc = tid % CB;
+      const PreCoef pk = pre_coef(reinterpret_cast<const float*>(lds + NBUF * kBuf), BN, lc * 8);
+      uint8_t* bb = lds + buf * kBuf + kPix * RA;
+      const int p0 = (step0 + step) * kPix;
+      for (int row = tid / CB; row < kPix; row += kThreads / CB) {
+        const int m = p0 + row;
+        bool ok = m < a.M;
+        if (ok && !a.aff) {   // a padded tap stays zero (the BN output's zero padding)
+          const int n = (int)fdiv((uint32_t)m, a.div_hw);
+          const int rem = m - n * a.Ho * a.Wo;
+          const int ho = (int)fdiv((uint32_t)rem, a.div_w);
+          const int wo = rem - ho * a.Wo;
+          ok = (unsigned)(ho * a.stride - a.pad + rr) < (unsigned)a.H &&
+               (unsigned)(wo * a.stride - a.pad_w + ss) < (unsigned)a.W;
+        }
+        if (ok) pre_lds(bb + row * RBB + ((lc ^ wswz<RBB>(row)) << 4), pk);
+      }
+      lds_barrier();
+    }
+  };
+  if constexpr (PRE) {
+    float* tab = reinterpret_cast<float*>(lds + NBUF * kBuf);
+    for (int i = tid; i < 3 * BN; i += kThreads) tab[i] = a.pre[(i / BN) * a.C + ci0 + i % BN];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // visible after the first barrier
+  }
+
   if (nsteps > 0) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    pre_x(0, 0);
   }
   for (int t = 0; t < nsteps; ++t) {
     const int cur = NBUF == 1 ? 0 : (t & 1);
@@ -2498,6 +2679,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (t + 1 < nsteps) pre_x(NBUF == 1 ? 0 : (cur ^ 1), t + 1);
   }
 
   // lane holds D[co = .. + 4*g + reg][kk = .. + (lane & 15)]
@@ -2515,18 +2697,18 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
     }
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool PRE = false>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
-  conv_wgrad_body<BM, BN, 2>(a);
+  conv_wgrad_body<BM, BN, 2, PRE>(a);
 #endif
 }
 
-template <int BM, int BN>
+template <int BM, int BN, bool PRE = false>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 void conv_wgrad_kernel_occ4(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv_wgrad_body<BM, BN, 1>(a);
+  conv_wgrad_body<BM, BN, 1, PRE>(a);
 #endif
 }
 
@@ -2609,7 +2791,7 @@ FastDiv make_fastdiv(uint32_t d) {
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int wswz2(int row) { return 4 * (row & 3); }
 
-template <int BM, int BN, int NWM, int NWN, int NBUF>
+template <int BM, int BN, int NWM, int NWN, int NBUF, bool PRE = false>
 __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int RA = BM * 2, RBB = BN * 2;        // row bytes of the dY and X images
@@ -2621,7 +2803,8 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
   static_assert(CA >= 16 && CB >= 16, "the 64-byte granule permutation needs >= 256-byte rows");
   static_assert(AI >= 1 && BI >= 1 && MI >= 1 && NI >= 1, "tile too small for the wave grid");
   static_assert(AI * NT == kPix * CA && BI * NT == kPix * CB, "staging slots must cover the tile");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf];
+  // PRE: the folded BN's coefficients of this block's BN input channels behind the stage buffers
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf + (PRE ? 3 * BN * 4 : 0)];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = a.m_tiles * a.n_tiles;
@@ -2711,6 +2894,35 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
   const int wm = wave / NWN, wn = wave % NWN;
   const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
 
+  // BN fold (see conv_wgrad_body's pre_x), granule permutation wswz2
+  auto pre_x = [&](int buf, int step) {
+    if constexpr (PRE) {
+      const int lc = tid % CB;
+      const PreCoef pk = pre_coef(reinterpret_cast<const float*>(lds + NBUF * kBuf), BN, lc * 8);
+      uint8_t* bb = lds + buf * kBuf + kPix * RA;
+      const int p0 = (step0 + step) * kPix;
+      for (int row = tid / CB; row < kPix; row += NT / CB) {
+        const int m = p0 + row;
+        bool ok = m < a.M;
+        if (ok && !a.aff) {
+          const int n = (int)fdiv((uint32_t)m, a.div_hw);
+          const int rem = m - n * a.Ho * a.Wo;
+          const int ho = (int)fdiv((uint32_t)rem, a.div_w);
+          const int wo = rem - ho * a.Wo;
+          ok = (unsigned)(ho * a.stride - a.pad + rr) < (unsigned)a.H &&
+               (unsigned)(wo * a.stride - a.pad_w + ss) < (unsigned)a.W;
+        }
+        if (ok) pre_lds(bb + row * RBB + ((lc ^ wswz2(row)) << 4), pk);
+      }
+      lds_barrier();
+    }
+  };
+  if constexpr (PRE) {
+    float* tab = reinterpret_cast<float*>(lds + NBUF * kBuf);
+    for (int i = tid; i < 3 * BN; i += NT) tab[i] = a.pre[(i / BN) * a.C + ci0 + i % BN];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // visible after the first barrier
+  }
+
   auto compute = [&](int buf) {
     const uint8_t* abuf = lds + buf * kBuf;
     const uint8_t* bbuf = abuf + kPix * RA;
@@ -2750,6 +2962,7 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    pre_x(0, 0);
     for (int t = 0; t < nsteps; ++t) {
       compute(0);
       if (t + 1 < nsteps) {
@@ -2758,6 +2971,7 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (t + 1 < nsteps) pre_x(0, t + 1);
     }
   } else if (nsteps > 0) {
     constexpr int S = NBUF > 1 ? NBUF - 1 : 1;
@@ -2771,6 +2985,7 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    pre_x(0, 0);
     int cur = 0;
     for (int t = 0; t < nsteps; ++t) {
       if (t + S < nsteps) stage(t + S, cur == 0 ? NBUF - 1 : cur - 1);
@@ -2782,6 +2997,7 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       cur = cur == NBUF - 1 ? 0 : cur + 1;
+      if (t + 1 < nsteps) pre_x(cur, t + 1);
     }
   }
 
@@ -2802,19 +3018,19 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
     }
 }
 
-template <int BM, int BN, int NWM, int NWN, int NBUF>
+template <int BM, int BN, int NWM, int NWN, int NBUF, bool PRE = false>
 __global__ __launch_bounds__(64 * NWM * NWN) void conv_wgrad2_kernel(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv_wgrad2_body<BM, BN, NWM, NWN, NBUF>(a);
+  conv_wgrad2_body<BM, BN, NWM, NWN, NBUF, PRE>(a);
 #endif
 }
 
 // serial single-buffer form, <= 128 VGPRs: four waves per SIMD (v1's variants 4..7 structure)
-template <int BM, int BN>
+template <int BM, int BN, bool PRE = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 void conv_wgrad2_kernel_occ4(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv_wgrad2_body<BM, BN, 2, 2, 1>(a);
+  conv_wgrad2_body<BM, BN, 2, 2, 1, PRE>(a);
 #endif
 }
 
@@ -2831,12 +3047,20 @@ hipError_t launch_wgrad2(WgradArgs a, int splits_hint, hipStream_t st) {
   splits = std::min(splits, total);
   a.sps = (total + splits - 1) / splits;
   a.splits = (total + a.sps - 1) / a.sps;
-  if constexpr (OCC4)
-    hipLaunchKernelGGL((conv_wgrad2_kernel_occ4<BM, BN>), dim3(tiles * a.splits), dim3(256), 0, st,
-                       a);
-  else
+  if constexpr (OCC4) {
+    if (a.pre)
+      hipLaunchKernelGGL((conv_wgrad2_kernel_occ4<BM, BN, true>), dim3(tiles * a.splits),
+                         dim3(256), 0, st, a);
+    else
+      hipLaunchKernelGGL((conv_wgrad2_kernel_occ4<BM, BN>), dim3(tiles * a.splits), dim3(256),
+                         0, st, a);
+  } else if (a.pre) {
+    hipLaunchKernelGGL((conv_wgrad2_kernel<BM, BN, NWM, NWN, NBUF, true>), dim3(tiles * a.splits),
+                       dim3(64 * NWM * NWN), 0, st, a);
+  } else {
     hipLaunchKernelGGL((conv_wgrad2_kernel<BM, BN, NWM, NWN, NBUF>), dim3(tiles * a.splits),
                        dim3(64 * NWM * NWN), 0, st, a);
+  }
   return hipGetLastError();
 }
 
@@ -2850,9 +3074,15 @@ hipError_t launch_wgrad(WgradArgs a, int splits_hint, bool serial, hipStream_t s
   splits = std::min(splits, total);
   a.sps = (total + splits - 1) / splits;
   a.splits = (total + a.sps - 1) / a.sps;
-  if (serial)
+  if (serial && a.pre)
+    hipLaunchKernelGGL((conv_wgrad_kernel_occ4<BM, BN, true>), dim3(tiles * a.splits),
+                       dim3(kThreads), 0, st, a);
+  else if (serial)
     hipLaunchKernelGGL((conv_wgrad_kernel_occ4<BM, BN>), dim3(tiles * a.splits), dim3(kThreads), 0,
                        st, a);
+  else if (a.pre)
+    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, true>), dim3(tiles * a.splits), dim3(kThreads),
+                       0, st, a);
   else
     hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN>), dim3(tiles * a.splits), dim3(kThreads), 0, st,
                        a);
@@ -2888,7 +3118,8 @@ int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int varia
 hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* dw_bf16,
                                float* dw_f32, int N, int H, int W, int C, int Cout, int R, int S,
                                int stride, int pad_h, int pad_w, int Ho, int Wo, int c16,
-                               int variant, int splits_hint, float scale, hipStream_t st) {
+                               int variant, int splits_hint, float scale, const float* pre,
+                               hipStream_t st) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
   if (variant < 0 || variant > 12) return hipErrorInvalidValue;
   const bool v2 = variant >= 8;
@@ -2899,7 +3130,9 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
   if (v2 && c16) return hipErrorInvalidValue;
   if (c16 ? (C != 16 || S % 4 || tbn != 64) : (C % tbn != 0)) return hipErrorInvalidValue;
   if (Cout % tbm || N <= 0 || stride <= 0) return hipErrorInvalidValue;
+  if (pre != nullptr && c16) return hipErrorInvalidValue;
   WgradArgs a{};
+  a.pre = pre;
   a.x = (const uint16_t*)x;
   a.dy = (const uint16_t*)dy;
   a.ws = ws;
@@ -2959,7 +3192,16 @@ hipError_t arena_conv_wgrad(const void* x, const void* dy, float* ws, void* dw_b
                             int N, int H, int W, int C, int Cout, int R, int S, int stride,
                             int pad, int variant, int splits_hint, float scale, hipStream_t st) {
   return arena_conv_wgrad_ex(x, dy, ws, dw_bf16, dw_f32, N, H, W, C, Cout, R, S, stride, pad, pad,
-                             0, 0, 0, variant, splits_hint, scale, st);
+                             0, 0, 0, variant, splits_hint, scale, nullptr, st);
+}
+
+// the BN-fold form (WgradArgs::pre: x is the raw input of the BN whose output the conv consumed)
+hipError_t arena_conv_wgrad_pre(const void* x, const void* dy, float* ws, void* dw_bf16,
+                                float* dw_f32, int N, int H, int W, int C, int Cout, int R, int S,
+                                int stride, int pad, int variant, int splits_hint, float scale,
+                                const float* pre, hipStream_t st) {
+  return arena_conv_wgrad_ex(x, dy, ws, dw_bf16, dw_f32, N, H, W, C, Cout, R, S, stride, pad, pad,
+                             0, 0, 0, variant, splits_hint, scale, pre, st);
 }
 
 }  // extern "C"

@@ -5,9 +5,10 @@ setup (RCCL refuses two ranks on one device). Default: bf16 weights with the sha
 
 What it checks:
 
-* gradient buckets (12 MB default: 5 buckets for ResNet-50's bf16 weights + an fp32 BN/bias
-  tail bucket) through the registered xGMI staging buffer, issued on the comm stream while
-  backward is still running;
+* gradient buckets (12 MB default, in model order: each bucket's bf16 conv weights travel with
+  the fp32 BN/bias parameters of the same blocks; the input-side bucket is a quarter size)
+  through the registered xGMI staging buffer, issued on the comm stream while backward is
+  still running;
 * fused BN kernels under bf16 autocast in every rank;
 * that all replicas stay bit-identical after the steps (same averaged gradient everywhere).
 
@@ -49,7 +50,8 @@ def trace_overlap(model, opt, x, y, path):
         orig(b)
         e = torch.cuda.Event(enable_timing=True)
         e.record(opt.stream)
-        marks.append((len(marks), b.dtype, b.end - b.start, e))
+        marks.append((len(marks), str(b.dtype).replace("torch.", ""),
+                      {str(r.dtype).replace("torch.", ""): r.end - r.start for r in b.ranges}, e))
 
     opt._launch = launch
     torch.cuda.synchronize()
@@ -67,7 +69,7 @@ def trace_overlap(model, opt, x, y, path):
     torch.cuda.synchronize()
     opt._launch = orig
     t_bwd = start.elapsed_time(bwd_end)
-    rows = [{"bucket": i, "dtype": str(dt), "elems": n, "done_ms": round(start.elapsed_time(e), 3)}
+    rows = [{"bucket": i, "dtype": dt, "elems": n, "done_ms": round(start.elapsed_time(e), 3)}
             for i, dt, n, e in marks]
     with open(path, "w") as f:
         for r in rows:
