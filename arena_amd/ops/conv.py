@@ -670,13 +670,17 @@ class ConvPlan:
         return self.fwd_fold != MIOPEN and self.wgrad_fold != MIOPEN
 
 
-# BatchNorm-apply fold (ARENA_BN_FOLD; see batchnorm.BatchNormAct2d.forward_fold): a ReLU BN whose
-# output only feeds one convolution is never materialised -- the conv stages the BN's input and
-# applies relu(fma(x - mean, scale, shift)) to each staged chunk in LDS (forward A operand, weight-
-# gradient X operand); the BN backward and the linked dgrad epilogue recompute the ReLU bits from
-# x. Geometry: 1x1 / stride 1 / unpadded (the generic v2 tiles) or 3x3 / stride 1 / pad 1 at
-# <= 63 wide (the halo tiles), C <= 512.
-_BN_FOLD = os.environ.get("ARENA_BN_FOLD", "1") == "1"
+# BatchNorm-apply fold (ARENA_BN_FOLD=1; see batchnorm.BatchNormAct2d.forward_fold): a ReLU BN
+# whose output only feeds one convolution is never materialised -- the conv stages the BN's input
+# and applies relu(fma(x - mean, scale, shift)) to each staged chunk in LDS (forward A operand,
+# weight-gradient X operand); the BN backward and the linked dgrad epilogue recompute the ReLU
+# bits from x. Geometry: 1x1 / stride 1 / unpadded (the generic v2 tiles) or 3x3 / stride 1 /
+# pad 1 at <= 63 wide (the halo tiles), C <= 512. OFF by default: measured slower on ResNet-50
+# (12.305 vs 11.867 ms per step, profiles/r5_fold_ab.jsonl). Each staged chunk is transformed by
+# every tile that stages it -- Cout/BN times in a 1x1 forward, once per tap and column tile in the
+# weight gradient -- where the apply pass transforms each element once; per layer the fold forms
+# cost more than the apply pass they remove (docs/perf.md, round 5).
+_BN_FOLD = os.environ.get("ARENA_BN_FOLD", "0") == "1"
 _FOLD_MAX_C = 512
 
 
