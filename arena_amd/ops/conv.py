@@ -43,7 +43,7 @@ TILES.update({v + 256 * p: TILES[v] for v in range(16) for p in PERSIST})
 # 4096 + i: the v2 tile kernel (conv_kernels.hip conv2_body): 32x32x16 MFMAs, 8-wave 256-row
 # tiles (4-wave 128x128), two K steps in flight, epilogue through an fp32 LDS tile. Forward and
 # backward-data (incl. the strided phases): plain, masked addend, BatchNorm statistics, BatchNorm-
-# backward partials or sums (BNGradLink); never split or persistent.
+# backward partials or sums (BNGradLink); never persistent (split-K forms: V2_KSPLITS below).
 V2 = 4096
 V2_TILES = {V2 + 0: (256, 128), V2 + 1: (256, 256), V2 + 2: (128, 128), V2 + 3: (256, 64),
             V2 + 4: (128, 256), V2 + 5: (128, 64), V2 + 6: (64, 64), V2 + 7: (64, 128),
@@ -57,8 +57,21 @@ HALO_MAX_W = 63
 HALO_SMALL = {V2 + 14: 31}
 V2_TILES.update(V2_HALO)
 TILES.update(V2_TILES)
+# + 16 * (k - 1) on a v2 code: the same tile with its K steps (halo forms: its 64-channel chunks)
+# split over k blocks; each slice writes an fp32 slab, the last to arrive (ticket per tile) sums
+# them in slice order and runs the epilogue -- bit-reproducible. For the layers whose tiles leave
+# CUs idle: the 14x14 / 7x7 stages at batch 128, where one 128x128 tile's K loop of 16-72 steps is
+# the whole launch (conv_kernels.hip conv2_body, split-K hand-off).
+V2_KSPLITS = (2, 3, 4, 6, 8)
+TILES.update({v + 16 * (k - 1): TILES[v] for v in V2_TILES for k in V2_KSPLITS})
 _V2_ON = os.environ.get("ARENA_CONV_V2", "1") != "0"
+_V2_SPLIT_ON = os.environ.get("ARENA_CONV_V2SPLIT", "1") != "0"
 _CUS = 256
+
+
+def v2_base(v: int) -> int:
+    """The unsplit v2 code of a v2 variant (``v`` itself for v1 codes)."""
+    return V2 + (v - V2) % 16 if v >= V2 else v
 
 
 def kvariant(v: int, ks: int) -> int:
@@ -72,6 +85,12 @@ def split_of(v: int) -> int:
 
 def tiles_per_block(v: int) -> int:
     return 1 if v >= V2 else 1 << (v // 256)
+
+
+def set_v2_split(on: bool) -> None:
+    """A/B switch: offer the v2 split-K forms to the autotuner (part of the plan key)."""
+    global _V2_SPLIT_ON
+    _V2_SPLIT_ON = bool(on)
 
 
 def set_v2(on: bool) -> None:
@@ -158,6 +177,34 @@ def split_variants_for(m: int, cout: int, ktot: int):
             if steps // ks >= 4:
                 ks_set.add(ks)
         out += [kvariant(v, k) for k in sorted(ks_set)]
+    return out
+
+
+def v2_split_variants_for(m: int, cout: int, ktot: int, bases):
+    """Split-K forms of the v2 tile variants ``bases`` whose grid gives fewer than two blocks per
+    CU: the splits that bring the launch to about 1, 2 or 4 blocks per CU, with at least 4 K steps
+    per slice (halo forms: at least one 64-channel chunk, ``ktot`` = 9 C)."""
+    out = []
+    if not (_V2_ON and _V2_SPLIT_ON) or os.environ.get("ARENA_CONV_KSPLIT", "1") == "0":
+        return out
+    for v in bases:
+        if v < V2 or v != v2_base(v):
+            continue
+        bm, bn = TILES[v]
+        if cout % bn:
+            continue
+        tiles = -(-m // bm) * (cout // bn)
+        if tiles >= 2 * _CUS:
+            continue
+        cap = ktot // (9 * 64) if v in V2_HALO else ktot // 64 // 4
+        ks_set = set()
+        for want in (_CUS, 2 * _CUS, 4 * _CUS):
+            need = -(-want // tiles)
+            fits = [k for k in V2_KSPLITS if k <= cap]
+            ks = next((k for k in fits if k >= need), fits[-1] if fits else 1)
+            if ks > 1:
+                ks_set.add(ks)
+        out += [v + 16 * (k - 1) for k in sorted(ks_set)]
     return out
 
 
@@ -773,7 +820,7 @@ def _best(t: dict, kind: str, n: int):
 
 def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
     key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _PERSIST_ON,
-           _V2_ON, _BN_LINKS, _BN_FOLD)
+           _V2_ON, _BN_LINKS, _BN_FOLD, _V2_SPLIT_ON)
     plan = _PLANS.get(key)
     if plan is not None and (plan.tuned or torch.cuda.is_current_stream_capturing()):
         return plan
@@ -885,6 +932,27 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                         fns[("bwd", v)] = (lambda v=v: _time(
                             lambda: conv2d_bwd_data(dy, w, pad, v)))
                         t[("bwd", v)] = fns[("bwd", v)]()
+                # split-K forms of the 3 fastest v2 tiles (+ the 256x128 tile: the most FLOPs
+                # per staged byte) where their grid under-fills the chip
+                def v2_top(kind):
+                    return [c for c in _best(t, kind, 64) if c >= V2][:3] + [V2]
+
+                for v in v2_split_variants_for(m_out, cout, cin * k[0] * k[1], v2_top("fwd")):
+                    fns[("fwd", v)] = (lambda v=v: fwd_time(v))
+                    t[("fwd", v)] = fns[("fwd", v)]()
+                if stride == 1:
+                    ktot_b = cout * k[0] * k[1]
+                    for v in v2_split_variants_for(m_in, cin, ktot_b, v2_top("bwd")):
+                        fns[("bwd", v)] = (lambda v=v: _time(
+                            lambda: conv2d_bwd_data(dy, w, pad, v)))
+                        t[("bwd", v)] = fns[("bwd", v)]()
+                    if _BN_LINKS:
+                        for v in v2_split_variants_for(m_in, cin, ktot_b, v2_top("bwdbn")):
+                            acc = bsums if _use_link_acc(m_in, v, cin) else None
+                            fns[("bwdbn", v)] = (lambda v=v, acc=acc: _time(
+                                lambda: conv2d_bwd_data(dy, w, pad, v, bn=(bnx, bmask, bmean),
+                                                        bn_acc=acc)))
+                            t[("bwdbn", v)] = fns[("bwdbn", v)]()
                 if fold:
                     # the fold's weight gradient: the 3 fastest plain candidates in the pre form
                     for c in _best(t, "wgrad", 3):
@@ -893,7 +961,8 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                         t[("wgradpre", c)] = fns[("wgradpre", c)]()
                     # the linked backward-data form with the ReLU bits recomputed (v2 / halo)
                     if _BN_LINKS and stride == 1:
-                        v2bn = [c for c in _best(t, "bwdbn", 64) if c >= V2][:3]
+                        v2bn = [c for c in _best(t, "bwdbn", 64)
+                                if c >= V2 and c == v2_base(c)][:3]   # the fold never splits
                         for v in v2bn:
                             acc = bsums if _use_link_acc(m_in, v, cin) else None
                             fns[("bwdbnpre", v)] = (lambda v=v, acc=acc: _time(

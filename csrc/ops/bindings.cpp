@@ -872,7 +872,7 @@ unsigned* conv_tickets(const Tensor& like, int64_t tiles) {
 
 // conv variant code: tile/pipeline variant (0..15) + 16 * (ksplit - 1) + 256 * p, where p > 0
 // selects the persistent form with 2^p output tiles per block (not with split-K); 4096 + i: the v2
-// tile kernel's variant i
+// tile kernel's variant i, + 16 * (ksplit - 1) for its split-K form
 struct ConvSplit {
   int base = 0, ks = 1, tpb = 1;
   Tensor ws;
@@ -882,19 +882,21 @@ struct ConvSplit {
 ConvSplit conv_split(const Tensor& x, int64_t variant, int64_t M, int64_t Cout, int64_t Ktot) {
   ConvSplit s;
   TORCH_CHECK(variant >= 0, "conv: bad variant ", variant);
-  if (variant >= 4096) {   // v2 tile kernel (conv_kernels.hip conv2_body): never split/persistent
-    TORCH_CHECK(variant < 4096 + 15, "conv: unknown v2 variant ", variant);
-    s.base = (int)variant;
-    return s;
+  if (variant >= 4096) {   // v2 tile kernel (conv_kernels.hip conv2_body): 4096 + i + 16 (ks - 1)
+    const int64_t r = variant - 4096;
+    TORCH_CHECK(r % 16 < 15 && r / 16 < 8, "conv: unknown v2 variant ", variant);
+    s.base = 4096 + (int)(r % 16);
+    s.ks = (int)(r / 16) + 1;
+  } else {
+    s.base = (int)(variant % 16);
+    s.ks = (int)(variant % 256 / 16) + 1;
+    const int p = (int)(variant / 256);
+    TORCH_CHECK(p <= 4 && (p == 0 || s.ks == 1), "conv: bad persistent variant ", variant);
+    s.tpb = 1 << p;
+    TORCH_CHECK(s.base <= 15, "conv: variant ", variant, " is not a tile variant");
+    TORCH_CHECK((s.base & 1) || Cout % 128 == 0, "conv: variant ", variant,
+                " needs Cout % 128 == 0 (Cout = ", Cout, ")");
   }
-  s.base = (int)(variant % 16);
-  s.ks = (int)(variant % 256 / 16) + 1;
-  const int p = (int)(variant / 256);
-  TORCH_CHECK(p <= 4 && (p == 0 || s.ks == 1), "conv: bad persistent variant ", variant);
-  s.tpb = 1 << p;
-  TORCH_CHECK(s.base <= 15, "conv: variant ", variant, " is not a tile variant");
-  TORCH_CHECK((s.base & 1) || Cout % 128 == 0, "conv: variant ", variant,
-              " needs Cout % 128 == 0 (Cout = ", Cout, ")");
   if (s.ks > 1) {
     TORCH_CHECK(s.ks <= Ktot / 64, "conv: split-K ", s.ks, " exceeds the ", Ktot / 64,
                 " K steps");

@@ -134,6 +134,41 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
+// ---- split-K slab hand-off inside a launch (cdna_hip_programming.md §6 Guideline 16, form R1) --
+// The slabs are stored write-through (sc1) and drained by every storing wave before the block's
+// barrier; one lane then takes a relaxed agent-scope ticket. No release fence: an agent-scope
+// release writes back the whole XCD L2 (buffer_wbl2), and with every split block of a launch
+// doing one, the v2 split tiles ran ~2x slower than unsplit (profiles/r5_split_plan_fenced.log).
+// The reducer reads every slab with sc1 loads, so it needs no acquire either.
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void slab_store(__amdgpu_buffer_rsrc_t r, int off, float4 v) {
+  __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, v), r, off, 0, 16);
+}
+
+__device__ __forceinline__ float4 slab_load(__amdgpu_buffer_rsrc_t r, int off) {
+  return __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 16));
+}
+
+// After this block's slab stores: true (in every thread) for the block that drew the last of
+// ks tickets on *cnt, which it resets for the next launch. `flag_lds`: 4 bytes of the block's LDS
+// that no wave reads or writes at this point (the stage buffers after the K loop's last barrier).
+__device__ __forceinline__ bool slab_ticket(unsigned* cnt, int ks, uint8_t* flag_lds) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every storing wave: its slab is out
+  __syncthreads();
+  volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(flag_lds);
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned last = old == (unsigned)(ks - 1) ? 1u : 0u;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    flag[0] = last;
+  }
+  __syncthreads();
+  const bool last = flag[0] != 0u;
+  __syncthreads();   // every wave has read the flag before the epilogue reuses the LDS
+  return last;
+}
+
 __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, (lds_ptr_t)lds_wave_base, 16, 0, 0);
 }
@@ -588,50 +623,33 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     }
 
     if (ks > 1) {
-      // ---- split-K hand-off (cdna_hip_programming.md §5 "In-launch split-K reduction") ----
+      // ---- split-K hand-off (slab_store / slab_ticket: write-through slabs, relaxed ticket,
+      // sc1 reads; the flag travels through the stage LDS, free after the K loop's barrier -- a
+      // second __shared__ object would perturb the K loop's waits, cdna_hip_programming.md §5
+      // item 4a) ----
       constexpr int NA = MI * NI;
-      float4* slab = a.kws + (size_t)tile * ks * NA * NT;
+      const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+          (void*)(a.kws + (size_t)tile * ks * NA * NT), (short)0, ks * NA * NT * 16, 0x00020000);
 #pragma unroll
       for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < NI; ++j)
-          slab[((size_t)slice * NA + i * NI + j) * NT + tid] =
-              make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      // the flag travels through the stage LDS (free: the K loop ended on a barrier); a second
-      // __shared__ object would perturb the K loop's waits (cdna_hip_programming.md §5 item 4a)
-      volatile unsigned* flag = reinterpret_cast<volatile unsigned*>(lds);
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned old =
-            __hip_atomic_fetch_add(a.kcnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const unsigned last = old == (unsigned)(ks - 1) ? 1u : 0u;
-        if (last) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          a.kcnt[tile] = 0u;   // ready for the next launch (kernel boundary orders it)
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        flag[0] = last;
-      }
-      __syncthreads();
-      const unsigned last = flag[0];
-      __syncthreads();   // every wave has read the flag before the epilogue reuses the LDS
-      if (!last) return;
+          slab_store(srs, ((slice * NA + i * NI + j) * NT + tid) * 16,
+                     make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]));
+      if (!slab_ticket(a.kcnt + tile, ks, lds)) return;
       // sum the slices in slice order (this block's own slab re-read from memory: the order, and
       // so the rounding, is independent of which block arrived last)
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
 #pragma unroll
         for (int j = 0; j < NI; ++j) {
-          const float4 v = slab[(size_t)(i * NI + j) * NT + tid];
+          const float4 v = slab_load(srs, ((i * NI + j) * NT + tid) * 16);
           acc[i][j] = f32x4v{v.x, v.y, v.z, v.w};
         }
         for (int s = 1; s < ks; ++s) {
           float4 v[NI];
 #pragma unroll
-          for (int j = 0; j < NI; ++j) v[j] = slab[((size_t)s * NA + i * NI + j) * NT + tid];
+          for (int j = 0; j < NI; ++j) v[j] = slab_load(srs, ((s * NA + i * NI + j) * NT + tid) * 16);
 #pragma unroll
           for (int j = 0; j < NI; ++j) acc[i][j] += f32x4v{v[j].x, v[j].y, v[j].z, v[j].w};
         }
@@ -1401,11 +1419,16 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // XCD-aware order (as v1): each XCD gets a contiguous range of tiles, column tiles of one row
-  // tile consecutive (their A rows stay in that XCD's L2)
-  const int nwg = a.m_tiles * a.n_tiles;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  // tile consecutive (their A rows stay in that XCD's L2). Split-K (ksplit > 1): the ksplit blocks
+  // of one output tile are consecutive in that order too, so a tile's slices (and the reducer
+  // that reads their slabs) share an XCD except at range edges.
+  const int ks = a.ksplit;
+  const int nblk = a.m_tiles * a.n_tiles * ks;
+  const int xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
   const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int nt = lin % a.n_tiles, mt = lin / a.n_tiles;
+  const int tile = ks > 1 ? lin / ks : lin;
+  const int slice = lin - tile * ks;
+  const int nt = tile % a.n_tiles, mt = tile / a.n_tiles;
   const int n0 = nt * BN, m0 = mt * BM;
 
   f32x16v acc[MI][NI];
@@ -1515,7 +1538,9 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
     constexpr int D = NBUF - 1;
     static_assert(D >= 1 && D < 9, "weight ring depth");
     const int CB = a.C / kBK;
-    for (int cb = 0; cb < CB; ++cb) {
+    // split-K: slice s owns channel chunks [s*CB/ks, (s+1)*CB/ks) (host-checked ks <= CB)
+    const int cb_end = (slice + 1) * CB / ks;
+    for (int cb = slice * CB / ks; cb < cb_end; ++cb) {
       PreCoef pk;
       if constexpr (kPreA) pk = pre_coef(a.pre, a.C, cb * kBK + pre_lc * 8);
       stage_win(cb);   // the previous chunk's last tap ended on a barrier: the window is free
@@ -1576,8 +1601,13 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
       b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
     }
     const int CB = a.C / kBK;
-    const int T = a.Ktot / kBK;
-    int s_tap = 0, s_cb = 0, s_s = 0, s_tapoff = 0, s_t = 0;
+    // split-K: slice s owns K steps [s*Tall/ks, (s+1)*Tall/ks); the staging cursor starts at the
+    // first one (tap = t0 / CB, chunk = t0 % CB; tap (r, s) sits (r*W + s)*C elements from tap 0)
+    const int Tall = a.Ktot / kBK;
+    const int t0 = slice * Tall / ks;
+    const int T = (slice + 1) * Tall / ks - t0;
+    int s_tap = t0 / CB, s_cb = t0 - (t0 / CB) * CB, s_s = s_tap % a.S, s_t = t0;
+    int s_tapoff = ((s_tap / a.S) * a.W + s_s) * a.C * 2;
     if constexpr (kPreA) {   // the folded BN's coefficients, once per block
       float* tab = reinterpret_cast<float*>(lds + G::kStage);
       for (int i = threadIdx.x; i < 3 * a.C; i += NT) tab[i] = a.pre[i];
@@ -1596,7 +1626,8 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
       }
     };
   #pragma unroll
-    for (int i = 0; i < AI; ++i) a_cur[i] = (a_mask[i] & 1u) ? (uint32_t)a_lane[i] : kOOB;
+    for (int i = 0; i < AI; ++i)
+      a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
 
     auto stage = [&](int buf) {
       uint8_t* base = lds + buf * kBufBytes;
@@ -1700,6 +1731,52 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
     }
   }
 
+  if (ks > 1) {
+    // ---- split-K hand-off (see slab_store / slab_ticket): every slice writes its fp32
+    // accumulators to kws [tile][slice][group][thread] write-through, takes a ticket on
+    // kcnt[tile]; the block drawing the last one sums the slices in slice order -- its own slab
+    // re-read too, so the rounding does not depend on which block arrived last -- and runs the
+    // epilogue (statistics / BN-backward sums included) ----
+    constexpr int NA = MI * NI * 4;
+    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(a.kws + (size_t)tile * ks * NA * NT), (short)0, ks * NA * NT * 16, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NI; ++j)
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          slab_store(srs, ((slice * NA + (i * NI + j) * 4 + g) * NT + tid) * 16,
+                     make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
+                                 acc[i][j][4 * g + 3]));
+    if (!slab_ticket(a.kcnt + tile, ks, lds)) return;
+    // one row of fragments (NI * 4 loads in flight) per slice, slices in order
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int base = (i * NI * 4 * NT + tid) * 16;
+#pragma unroll
+      for (int jg = 0; jg < NI * 4; ++jg) {
+        const float4 v = slab_load(srs, base + jg * NT * 16);
+        acc[i][jg >> 2][4 * (jg & 3)] = v.x;
+        acc[i][jg >> 2][4 * (jg & 3) + 1] = v.y;
+        acc[i][jg >> 2][4 * (jg & 3) + 2] = v.z;
+        acc[i][jg >> 2][4 * (jg & 3) + 3] = v.w;
+      }
+      for (int q = 1; q < ks; ++q) {
+        float4 v[NI * 4];
+#pragma unroll
+        for (int jg = 0; jg < NI * 4; ++jg) v[jg] = slab_load(srs, base + (q * NA + jg) * NT * 16);
+#pragma unroll
+        for (int jg = 0; jg < NI * 4; ++jg) {
+          acc[i][jg >> 2][4 * (jg & 3)] += v[jg].x;
+          acc[i][jg >> 2][4 * (jg & 3) + 1] += v[jg].y;
+          acc[i][jg >> 2][4 * (jg & 3) + 2] += v[jg].z;
+          acc[i][jg >> 2][4 * (jg & 3) + 3] += v[jg].w;
+        }
+      }
+    }
+  }
+
   conv2_epilogue<G, EPI, PRE>(a, acc, lds, m0, n0, mt, tid, wm, wn, fr, hh);
 }
 
@@ -1769,15 +1846,18 @@ __global__ __launch_bounds__(256) void conv2_kernel_halo(ConvArgs a) {
 template <int BM, int BN, int HW = 1>
 hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
-  if (a.c16 || a.ksplit != 1 || a.tpb != 1 || a.Cout % BN || a.R != 3 || a.S != 3 ||
+  if (a.c16 || a.tpb != 1 || a.Cout % BN || a.R != 3 || a.S != 3 ||
       a.stride != 1 || a.pad != 1 || a.pad_w != 1 || a.Ho != a.H || a.Wo != a.W ||
       a.W > (HW == 2 ? kHaloSmallW : kHaloMaxW) || a.mapped)
+    return hipErrorInvalidValue;
+  // split-K over the 64-channel chunks (every slice stages whole windows)
+  if (a.ksplit < 1 || a.ksplit > a.C / kBK || (a.ksplit > 1 && a.pre != nullptr))
     return hipErrorInvalidValue;
   if (a.bnx == nullptr && (a.part != nullptr || a.bn_acc != nullptr) && a.add != nullptr)
     return hipErrorInvalidValue;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  const int nwg = a.m_tiles * a.n_tiles;
+  const int nwg = a.m_tiles * a.n_tiles * a.ksplit;
   if (a.pre != nullptr) {   // BN fold: forward with statistics, or the linked backward-data form
     if (a.bnx != nullptr)
       hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW, true>), dim3(nwg), dim3(256), 0, st, a);
@@ -1797,13 +1877,17 @@ hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
 template <int BM, int BN, int NWM, int NWN, int NBUF, bool OCC4 = false>
 hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
-  if (a.c16 || a.ksplit != 1 || a.tpb != 1 || a.Cout % BN) return hipErrorInvalidValue;
+  if (a.c16 || a.tpb != 1 || a.Cout % BN) return hipErrorInvalidValue;
+  // split-K: single convolutions only (not the phase launch, the mapped epilogue or the fold)
+  if (a.ksplit < 1 || a.ksplit > a.Ktot / kBK ||
+      (a.ksplit > 1 && (a.nph > 0 || a.mapped || a.pre != nullptr)))
+    return hipErrorInvalidValue;
   const bool bwd_bn = a.bnx != nullptr;   // EPI 2 (the caller checked part / bnmean / no map)
   if (!bwd_bn && (a.part != nullptr || a.bn_acc != nullptr) && (a.add != nullptr || a.mapped))
     return hipErrorInvalidValue;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  int nwg = a.m_tiles * a.n_tiles;
+  int nwg = a.m_tiles * a.n_tiles * a.ksplit;
   const bool stats = a.part != nullptr || a.bn_acc != nullptr;
   if (a.nph > 0) {   // phases back to back, each starting on a multiple of 8 blocks
     if (stats || bwd_bn) return hipErrorInvalidValue;
@@ -2089,7 +2173,9 @@ static void conv_tile(int variant, int* bm, int* bn) {
 }
 
 long long arena_conv_fwd_ksplit_floats(long long M, int Cout, int variant, int ksplit) {
-  if (ksplit <= 1 || variant < 0 || variant > 15) return 0;   // v2 tiles never split
+  if (ksplit <= 1 || variant < 0 ||
+      (variant > 15 && !(variant >= kV2Base && variant < kV2Base + kV2Count)))
+    return 0;
   int bm, bn;
   conv_tile(variant, &bm, &bn);
   return ((M + bm - 1) / bm) * (Cout / bn) * ksplit * bm * bn;

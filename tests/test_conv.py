@@ -113,6 +113,8 @@ V2_SHAPES = [  # n, cin, h, w, cout, k, stride
     (2, 64, 56, 56, 128, 3, 1),     # halo window of 242 rows
     (4, 128, 7, 7, 128, 3, 1),      # halo windows spanning several images
     (1, 64, 5, 63, 64, 3, 1),       # the widest halo image
+    (2, 128, 9, 31, 128, 3, 1),     # the small window's widest image (V2+14 at its limit)
+    (1, 128, 5, 63, 128, 3, 1),     # the big window at W = 63 with the 128-wide tile (V2+12)
 ]
 
 
@@ -179,6 +181,23 @@ def test_conv_v2_matches_fp32(shape):
         a = conv.conv2d_bwd_data(dy, wt, pad, v, addend=addend, addmask=bits)
         b = conv.conv2d_bwd_data(dy, wt, pad, v, addend=dense)
         assert torch.equal(a, b), v
+    # the linked (BN-backward partials) form at these shapes -- incl. the halo windows at their
+    # widest images -- against fp32 sums of the stored dX
+    bnx = torch.randn(x.shape, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    m = x.shape[0] * x.shape[2] * x.shape[3]
+    mean = torch.randn(cin, device="cuda") * 0.3
+    xc = bnx.permute(0, 2, 3, 1).reshape(m, cin).float() - mean
+    for v in conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, pad, w):
+        dx0 = conv.conv2d_bwd_data(dy, wt, pad, v)
+        dx, (part, rpb) = conv.conv2d_bwd_data(dy, wt, pad, v, bn=(bnx, bits, mean))
+        assert torch.equal(dx, dx0), v
+        assert _rel(dx, dx_ref) < 1e-2, (v, _rel(dx, dx_ref))
+        g = dx.permute(0, 2, 3, 1).reshape(m, cin).float() * \
+            conv._unpack_bits(bits, dx).permute(0, 2, 3, 1).reshape(m, cin).float()
+        p = part.view(-1, 2, cin)
+        torch.testing.assert_close(p[:, 0].sum(0), g.sum(0), rtol=1e-3, atol=1e-2)
+        torch.testing.assert_close(p[:, 1].sum(0), (g * xc).sum(0), rtol=1e-3, atol=1e-2)
 
 
 @pytest.mark.gpu
@@ -273,6 +292,89 @@ def test_conv_split_k_matches_unsplit(shape):
             kv = conv.kvariant(v, 2)
             dxa = conv.conv2d_bwd_data(dy, wt, pad, kv, addend=addend)
             assert _rel(dxa, dx_ref + addend.float()) < 1e-2, (v, _rel(dxa, dx_ref + addend.float()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape", [(2, 256, 7, 7, 128, 3, 1), (3, 128, 6, 5, 256, 1, 1),
+                                   (2, 512, 7, 7, 256, 1, 1), (1, 192, 5, 9, 128, 3, 1)])
+def test_conv_v2_split_k_matches_fp32(shape):
+    """v2 / halo split-K forms (slabs + ticket, last block sums slices in order and runs the
+    epilogue): forward, statistics (partials and finished sums), backward-data with the masked
+    addend and the linked BN-backward partials, against fp32 references -- bit-identical run to
+    run. Uneven slices (3 over 9 K steps, 3 over 3 channel chunks) included."""
+    from arena_amd.ops import _ext
+    from arena_amd.ops.batchnorm import BatchNormAct2d
+    _ext.load()
+    n, cin, h, w, cout, k, st = shape
+    pad = k // 2
+    x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=9)
+    ref = F.conv2d(x.float(), wt.float(), stride=st, padding=pad)
+
+    def splits(v, ktot):
+        cap = ktot // (9 * 64) if v in conv.V2_HALO else ktot // 64
+        return [v + 16 * (s - 1) for s in (2, 3, 4) if s <= cap]
+
+    bases = conv.v2_variants_for(cout) + conv.halo_variants_for(cout, (k, k), st, pad, w)
+    for v in bases:
+        for kv in splits(v, cin * k * k):
+            assert conv.v2_base(kv) == v and conv.TILES[kv] == conv.TILES[v]
+            y = conv.conv2d_fwd(x, wt, st, pad, kv)
+            assert _rel(y, ref) < 1e-2, (kv, _rel(y, ref))
+            assert torch.equal(conv.conv2d_fwd(x, wt, st, pad, kv), y), kv
+            yp, stats = conv.conv2d_fwd(x, wt, st, pad, kv, with_stats=True)
+            yf, fin = conv.conv2d_fwd(x, wt, st, pad, kv, with_stats=True, final=True)
+            assert torch.equal(yp, y) and torch.equal(yf, y) and stats[1] == conv.TILES[v][0]
+            bns = [BatchNormAct2d(cout).cuda() for _ in range(3)]
+            r = bns[0](y)
+            assert _rel(bns[1](y, stats=stats), r) < 1e-2, kv
+            assert _rel(bns[2](y, stats=fin), r) < 1e-2, kv
+            torch.testing.assert_close(bns[2].running_var, bns[0].running_var, rtol=1e-3,
+                                       atol=1e-5)
+    dy = torch.randn(ref.shape, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    dx_ref = torch.ops.aten.convolution_backward(
+        dy.float(), x.float(), wt.float(), None, [1, 1], [pad, pad], [1, 1], False, [0, 0], 1,
+        [True, False, False])[0]
+    addend = torch.randn(x.shape, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    bits = torch.randint(0, 256, (addend.numel() // 8,), device="cuda", dtype=torch.uint8)
+    dense = conv.MaskedGrad(addend, bits).materialize()
+    bnx = torch.randn(x.shape, device="cuda").to(torch.bfloat16).contiguous(
+        memory_format=torch.channels_last)
+    m = x.shape[0] * x.shape[2] * x.shape[3]
+    mean = torch.randn(cin, device="cuda") * 0.3
+    xc = bnx.permute(0, 2, 3, 1).reshape(m, cin).float() - mean
+    bases = conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, pad, w)
+    for v in bases:
+        for kv in splits(v, cout * k * k):
+            dx = conv.conv2d_bwd_data(dy, wt, pad, kv)
+            assert _rel(dx, dx_ref) < 1e-2, (kv, _rel(dx, dx_ref))
+            a = conv.conv2d_bwd_data(dy, wt, pad, kv, addend=addend, addmask=bits)
+            assert torch.equal(a, conv.conv2d_bwd_data(dy, wt, pad, kv, addend=dense)), kv
+            assert _rel(a, dx_ref + dense.float()) < 1e-2, kv
+            dxl, (part, rpb) = conv.conv2d_bwd_data(dy, wt, pad, kv, bn=(bnx, bits, mean))
+            assert torch.equal(dxl, dx), kv
+            g = dx.permute(0, 2, 3, 1).reshape(m, cin).float() * \
+                conv._unpack_bits(bits, dx).permute(0, 2, 3, 1).reshape(m, cin).float()
+            p = part.view(-1, 2, cin)
+            torch.testing.assert_close(p[:, 0].sum(0), g.sum(0), rtol=1e-3, atol=1e-2)
+            torch.testing.assert_close(p[:, 1].sum(0), (g * xc).sum(0), rtol=1e-3, atol=1e-2)
+
+
+def test_v2_split_variants_only_for_underfilled_grids():
+    V2 = conv.V2
+    # 56x56 x 256 at batch 128: 3136 row tiles, never split
+    assert conv.v2_split_variants_for(128 * 56 * 56, 256, 256, [V2 + 2, V2 + 8]) == []
+    # 7x7 x 512, K = 2048 (196 tiles of 128x128): splits toward 1, 2 and 4 blocks per CU
+    sv = conv.v2_split_variants_for(128 * 7 * 7, 512, 2048, [V2 + 2, V2 + 0])
+    assert sv and all(conv.split_of(v) > 1 and conv.v2_base(v) in (V2 + 2, V2 + 0) for v in sv)
+    assert all(2048 // 64 // conv.split_of(v) >= 4 for v in sv)
+    # halo forms split over 64-channel chunks: 3x3 x 128 input channels has two
+    hv = conv.v2_split_variants_for(128 * 7 * 7, 128, 9 * 128, [V2 + 12, V2 + 13])
+    assert hv and all(conv.split_of(v) == 2 for v in hv)
+    # split codes are never bases, and bases of other codes are themselves
+    assert conv.v2_split_variants_for(128 * 7 * 7, 512, 2048, [V2 + 2 + 16]) == []
+    assert conv.v2_base(V2 + 2 + 48) == V2 + 2 and conv.v2_base(5) == 5
 
 
 @pytest.mark.gpu
