@@ -65,7 +65,13 @@ TILES.update(V2_TILES)
 V2_KSPLITS = (2, 3, 4, 6, 8)
 TILES.update({v + 16 * (k - 1): TILES[v] for v in V2_TILES for k in V2_KSPLITS})
 _V2_ON = os.environ.get("ARENA_CONV_V2", "1") != "0"
-_V2_SPLIT_ON = os.environ.get("ARENA_CONV_V2SPLIT", "1") != "0"
+# Not offered to the autotuner by default (ARENA_CONV_V2SPLIT=1 does): on every ResNet-50 layer at
+# batch 128 the split forms lost to the unsplit tiles -- 2048->512 @7 forward 37.2 vs 28.1 us,
+# 3x3 512 @7 43.6 vs 41.4, the rest by 1.3-2.5x (profiles/r5_split_plan_sc1.log; step 12.276 vs
+# 12.200 ms, r5_split_ab_sc1.jsonl). These layers are bound by each CU's L2->LDS rate over its
+# tiles, which a split does not change (docs/perf.md, round 5), and the hand-off adds a slab
+# round trip to every tile's tail.
+_V2_SPLIT_ON = os.environ.get("ARENA_CONV_V2SPLIT", "0") == "1"
 _CUS = 256
 
 

@@ -237,7 +237,13 @@ class XgmiComm:
                 pass
         self._own = []
 
-    def close(self) -> None:
+    def close(self, collective: bool = True) -> None:
+        """Unmap the peers' buffers, then free this rank's. Collective by default: every rank
+        unmaps before any rank frees, so no buffer is freed while a peer still maps it. (Freed
+        under a live peer mapping, the next allocation could land on the same addresses, and
+        exporting it then failed with ``hipIpcGetMemHandle: invalid argument`` -- seen with 8
+        ranks on one GPU, where a temporary broadcast communicator is closed right before the
+        optimizer's is created.)"""
         torch.cuda.synchronize()
         for p in self._opened:
             try:
@@ -246,6 +252,8 @@ class XgmiComm:
                 pass
         self._opened = []
         self.peers = None
+        if collective and dist.is_initialized():
+            dist.barrier(group=self.group)
         self._free()
 
     # ------------------------------------------------------------------------------- buffers

@@ -361,8 +361,11 @@ def test_conv_v2_split_k_matches_fp32(shape):
             torch.testing.assert_close(p[:, 1].sum(0), (g * xc).sum(0), rtol=1e-3, atol=1e-2)
 
 
-def test_v2_split_variants_only_for_underfilled_grids():
+def test_v2_split_variants_only_for_underfilled_grids(monkeypatch):
     V2 = conv.V2
+    monkeypatch.setattr(conv, "_V2_SPLIT_ON", False)
+    assert conv.v2_split_variants_for(128 * 7 * 7, 512, 2048, [V2 + 2]) == []   # off by default
+    monkeypatch.setattr(conv, "_V2_SPLIT_ON", True)
     # 56x56 x 256 at batch 128: 3136 row tiles, never split
     assert conv.v2_split_variants_for(128 * 56 * 56, 256, 256, [V2 + 2, V2 + 8]) == []
     # 7x7 x 512, K = 2048 (196 tiles of 128x128): splits toward 1, 2 and 4 blocks per CU

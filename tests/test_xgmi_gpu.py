@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import os
 import socket
+import sys
 import traceback
 
 import pytest
@@ -485,10 +486,17 @@ def _zero_sgd(rank, world, port, q):
         from arena_amd.parallel.zero import ShardedMasterSGD
         hvd.init()
         conv.set_mode("ours")
+        # W = 8 ranks time-share one GPU: every bucket is a rendezvous of 8 processes whose
+        # kernels the GPU schedules in turn, so W = 8 uses a few 4 MB buckets (the model is
+        # 15 MB) instead of one per tensor
         args = types.SimpleNamespace(model="resnet_tiny", data_format="NHWC", batch_size=8,
                                      image_size=32, num_classes=10, width=64, learning_rate=0.05,
-                                     momentum=0.9, weight_decay=1e-3, bucket_mb=0.05, comm="xgmi",
+                                     momentum=0.9, weight_decay=1e-3,
+                                     bucket_mb=0.05 if world <= 2 else 4.0, comm="xgmi",
                                      master_weights="auto", dtype="bf16")
+
+        def progress(what):   # one line per stage (a slow shared-GPU run is visibly alive)
+            print(f"[zero_sgd w{world} r{rank}] {what}", file=sys.stderr, flush=True)
         dev = torch.device("cuda", 0)
         bf = torch.bfloat16
         res = {}
@@ -520,9 +528,11 @@ def _zero_sgd(rank, world, port, q):
                 refs.append((w0[i] - args.learning_rate * gavg).reshape(-1))   # momentum 0
             flat_ref.copy_(torch.cat(refs).cpu())
         dist.broadcast(flat_ref, 0)
+        progress("reference broadcast")
         cnn_bench.train_step(model, opt, x, y, bf)
         torch.cuda.synchronize()
         opt.comm.check()
+        progress("one DP step")
         off, worst_ulp, worst_f32 = 0, 0.0, 0.0
         for i, p in enumerate(params):
             n = p.numel()
@@ -558,6 +568,7 @@ def _zero_sgd(rank, world, port, q):
                 cnn_bench.train_step(model, opt, x, y, bf)
             torch.cuda.synchronize()
             opt.comm.check()
+            progress(f"4 steps, graph={graph}")
             flats.append(torch.cat([p.detach().float().reshape(-1) for p in model.parameters()]))
             opt.close()
             dist.barrier()

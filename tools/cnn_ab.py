@@ -14,8 +14,8 @@ level-1 blocks per channel group in the BN finalize kernels) and/or ``:redG<b>x<
 BN statistics as fp64 sums up to n tile-channel pairs) and/or ``:finbwd0`` (BN backward sums
 from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv forms) and/or
 ``:nostempool`` (stem BN and max pool unfused) and/or ``:fold`` (bn1 / bn2 folded into the
-consuming convs instead of applied by their own pass) and/or ``:nov2split`` (no split-K forms of
-the v2 tiles), joined with ``+``.
+consuming convs instead of applied by their own pass) and/or ``:v2split`` (split-K forms of the
+v2 tiles among the candidates), joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
     python tools/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
@@ -91,8 +91,8 @@ def main():
         _bn.set_stem_pool_fused("nostempool" not in opt_s.split("+"))
         # fold: bn1 / bn2 folded into the consuming convs (off by default, ARENA_BN_FOLD)
         conv.set_bn_fold("fold" in opt_s.split("+"))
-        # nov2split: no v2 split-K forms among the autotuner's candidates
-        conv.set_v2_split("nov2split" not in opt_s.split("+"))
+        # v2split: the v2 split-K forms among the autotuner's candidates (off by default)
+        conv.set_v2_split("v2split" in opt_s.split("+"))
         # st1p: conv-epilogue BN statistics in one pass (the launch args bake the switch)
         _e.load().conv_set_stats_one_pass("st1p" in opt_s.split("+"))
         model, opt, x, y = cnn_bench.build(args, dev, 1)
