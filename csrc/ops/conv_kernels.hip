@@ -1147,10 +1147,6 @@ hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 
 constexpr int kLdsMax = 160 * 1024;
-#ifndef ARENA_CONV_PF
-#define ARENA_CONV_PF 1
-#endif
-constexpr bool kConvPF = ARENA_CONV_PF != 0;
 
 // HALO (3x3, stride 1, pad 1, W <= kHaloMaxW): the A operand of a BM-pixel tile is the window of
 // input pixels [m0 - W - 1, m0 + BM + W] (NHW-linear), staged ONCE per 64-channel chunk; the nine
@@ -1413,9 +1409,6 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
   // buffers (the epilogue may overwrite it: the K loop is done with it). The halo form keeps its
   // one chunk of coefficients per thread in registers instead (its LDS is sized to the block).
   constexpr bool kPreA = PRE && EPI == 1;
-  // pipelined / halo tiles: the next 16-deep K slice's fragments are read from LDS into a second
-  // register set while the current slice's MFMAs run (ARENA_CONV_PF build switch, default on)
-  constexpr bool kPF = kConvPF && !BAND;
   constexpr int kPreTab = (kPreA && !HALO) ? 3 * kPreMaxC * 4 : 0;
   constexpr int kLdsAll = G::kStage + kPreTab > G::kLds ? G::kStage + kPreTab : G::kLds;
   static_assert(kLdsAll <= kLdsMax, "LDS budget");
@@ -1510,42 +1503,6 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
         __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
                                                  16, b_voff[i], (tap * a.C + cb * kBK) * 2, 0, 0);
     };
-    // fragments of 16-deep K slice kk of tap `shift` (taps outside the image zeroed)
-    auto tap_frags = [&](const uint8_t* bbuf, int shift, const bool (&ok)[MI], int kk,
-                         bf16x8 (&af)[MI], bf16x8 (&bfr)[NI]) {
-      const int c = kk * 2 + hh;
-#pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int j = wm * WM + i * 32 + fr + shift;
-        const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + j * kRowBytes + ((c ^ swz(j)) << 4));
-        af[i] = ok[i] ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
-      }
-#pragma unroll
-      for (int jn = 0; jn < NI; ++jn) {
-        const int row = wn * WN + jn * 32 + fr;
-        bfr[jn] = *reinterpret_cast<const bf16x8*>(bbuf + row * kRowBytes + ((c ^ swz(row)) << 4));
-      }
-    };
-    auto compute_tap_pf = [&](int tap, int buf) {
-      const int r = tap / 3, s2 = tap - 3 * r;
-      const int shift = r * Wd + s2;
-      const uint8_t* bbuf = lds + kWin + buf * BN * kRowBytes;
-      bool ok[MI];
-#pragma unroll
-      for (int i = 0; i < MI; ++i) ok[i] = (tmask[i] >> tap) & 1u;
-      bf16x8 af[2][MI], bfr[2][NI];
-      tap_frags(bbuf, shift, ok, 0, af[0], bfr[0]);
-#pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        if (kk + 1 < 4) tap_frags(bbuf, shift, ok, kk + 1, af[(kk + 1) & 1], bfr[(kk + 1) & 1]);
-#pragma unroll
-        for (int i = 0; i < MI; ++i)
-#pragma unroll
-          for (int jn = 0; jn < NI; ++jn)
-            acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[kk & 1][jn], af[kk & 1][i],
-                                                                 acc[i][jn], 0, 0, 0);
-      }
-    };
     auto compute_tap = [&](int tap, int buf) {
       const int r = tap / 3, s2 = tap - 3 * r;
       const int shift = r * Wd + s2;
@@ -1605,10 +1562,7 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
       for (int t = 0; t < 9; ++t) {
         // buffer (t + D) % NBUF was last read by tap t - 1, before the barrier that ended it
         if (t + D < 9) stage_b(t + D, cb, (t + D) % NBUF);
-        if constexpr (kPF)
-          compute_tap_pf(t, t % NBUF);
-        else
-          compute_tap(t, t % NBUF);
+        compute_tap(t, t % NBUF);
         if (t + D < 9)   // tap t + 1 landed, D - 1 taps may still be in flight
           asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((D - 1) * BI) : "memory");
         else
@@ -1703,36 +1657,6 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
     };
 
 
-    auto frags = [&](const uint8_t* abuf, const uint8_t* bbuf, int kk, bf16x8 (&af)[MI],
-                     bf16x8 (&bfr)[NI]) {
-      const int c = kk * 2 + hh;
-  #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int row = wm * WM + i * 32 + fr;
-        af[i] = *reinterpret_cast<const bf16x8*>(abuf + row * kRowBytes + ((c ^ swz(row)) << 4));
-      }
-  #pragma unroll
-      for (int j = 0; j < NI; ++j) {
-        const int row = wn * WN + j * 32 + fr;
-        bfr[j] = *reinterpret_cast<const bf16x8*>(bbuf + row * kRowBytes + ((c ^ swz(row)) << 4));
-      }
-    };
-    auto compute_pf = [&](int buf) {
-      const uint8_t* abuf = lds + buf * kBufBytes;
-      const uint8_t* bbuf = abuf + BM * kRowBytes;
-      bf16x8 af[2][MI], bfr[2][NI];
-      frags(abuf, bbuf, 0, af[0], bfr[0]);
-  #pragma unroll
-      for (int kk = 0; kk < 4; ++kk) {
-        if (kk + 1 < 4) frags(abuf, bbuf, kk + 1, af[(kk + 1) & 1], bfr[(kk + 1) & 1]);
-  #pragma unroll
-        for (int i = 0; i < MI; ++i)
-  #pragma unroll
-          for (int j = 0; j < NI; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[kk & 1][j], af[kk & 1][i],
-                                                                acc[i][j], 0, 0, 0);
-      }
-    };
     auto compute = [&](int buf) {
       const uint8_t* abuf = lds + buf * kBufBytes;
       const uint8_t* bbuf = abuf + BM * kRowBytes;
@@ -1793,10 +1717,7 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
         // RAW: stage t + 1 was retired by the vmcnt before the last barrier. WAR: stage t + S
         // overwrites buffer (t - 1) % NBUF, whose reads completed before that barrier.
         if (t + S < T) stage(cur == 0 ? NBUF - 1 : cur - 1);
-        if constexpr (kPF)
-          compute_pf(cur);
-        else
-          compute(cur);
+        compute(cur);
         if (t + S < T)
           asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((S - 1) * kLps) : "memory");
         else
