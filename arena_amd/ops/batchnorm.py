@@ -59,17 +59,33 @@ def reference(x, residual, weight, bias, running_mean, running_var, training, mo
     return F.relu(y) if relu else y
 
 
+def acc_rep() -> int:
+    """Replicas per fp64 accumulator set (csrc/ops/abi.h ARENA_ACC_REP): a set is [rep, 2, C];
+    producers with many blocks (the conv epilogues) spread their same-address atomics over the
+    replicas and every reader sums them."""
+    return int(getattr(_ext.load(), "acc_rep", 1))
+
+
+def acc_totals(t: torch.Tensor) -> torch.Tensor:
+    """The [2, C] totals of an accumulator set (its replicas summed)."""
+    return t.reshape(-1, 2, t.shape[-1]).sum(0)
+
+
 class FinishedStats:
-    """Batch statistics of a conv output accumulated inside the conv kernel: the fp64 [2, C]
-    accumulator set (sum y, sum y^2) its epilogue added into with memory-side atomics
-    (``conv2d_fwd(..., with_stats=True, final=True)``). The BN layer consuming it skips its
-    statistics pass; its apply pass derives the coefficients from the sums, and its backward dx
-    pass zeroes the set, which returns to a rotating pool (a set whose backward never ran is
-    zeroed on the stream before the pool hands it out again)."""
+    """Batch statistics of a conv output accumulated inside the conv kernel: the fp64 [rep, 2, C]
+    accumulator set (sum y, sum y^2, spread over ``acc_rep()`` replicas) its epilogue added into
+    with memory-side atomics (``conv2d_fwd(..., with_stats=True, final=True)``). The BN layer
+    consuming it skips its statistics pass; its apply pass derives the coefficients from the
+    sums, and its backward dx pass zeroes the set, which returns to a rotating pool (a set whose
+    backward never ran is zeroed on the stream before the pool hands it out again)."""
     __slots__ = ("fin",)
 
     def __init__(self, fin: torch.Tensor):
         self.fin = fin
+
+    def sums(self) -> torch.Tensor:
+        """[2, C]: (sum y, sum y^2)."""
+        return acc_totals(self.fin)
 
     def discard(self) -> None:
         self.fin.zero_()
@@ -107,8 +123,9 @@ def set_fin_bwd(on: bool) -> None:
 
 
 class _BwdAcc:
-    """A BN layer's own fp64 [2, C] backward sums (``bn_bwd(acc_b=...)``). The backward's dx pass
-    leaves them in place; the layer's next forward apply pass zeroes them (``bn_fwd(zero_b=...)``).
+    """A BN layer's own fp64 [rep, 2, C] backward sums (``bn_bwd(acc_b=...)``, ``acc_rep()``
+    replicas). The backward's dx pass leaves them in place; the layer's next forward apply pass
+    zeroes them (``bn_fwd(zero_b=...)``).
     ``dirty`` tracks that on the host: a backward that finds the set still dirty (no forward ran in
     between) zeroes it first. One set per module keeps captured graphs valid: every replay's
     forward zeroes the set its previous replay's backward filled."""
@@ -125,8 +142,9 @@ class _BwdAcc:
         return self.t
 
     def for_backward(self, like: torch.Tensor, c: int) -> torch.Tensor:
-        if self.t is None or self.t.device != like.device or self.t.numel() != 2 * c:
-            self.t = torch.zeros(2 * c, dtype=torch.float64, device=like.device)
+        n = acc_rep() * 2 * c
+        if self.t is None or self.t.device != like.device or self.t.numel() != n:
+            self.t = torch.zeros(n, dtype=torch.float64, device=like.device)
         elif self.dirty:
             self.t.zero_()
         self.dirty = True

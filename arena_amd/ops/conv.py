@@ -313,15 +313,19 @@ def set_bn_links(on: bool) -> None:
     _BN_LINKS = bool(on)
 
 
-# BatchNorm statistics summed inside the conv kernel (fp64 fire-and-forget atomics into an [2, C]
-# set the BN apply pass derives its coefficients from) instead of per-tile partials plus a
-# finalize launch in the BN layer (on by default; ARENA_BN_FINAL=0 for A/Bs). Also switches the BN
-# kernels' own statistics/backward reductions to the same acc mode.
+# BatchNorm statistics summed inside the conv kernel (fp64 fire-and-forget atomics into an
+# [rep, 2, C] set the BN apply pass derives its coefficients from) instead of per-tile partials
+# plus a finalize launch in the BN layer (on by default; ARENA_BN_FINAL=0 for A/Bs). Also switches
+# the BN kernels' own statistics/backward reductions to the same acc mode.
 _BN_FINAL = os.environ.get("ARENA_BN_FINAL", "1") == "1"
-# Above this many (tile, channel) pairs the epilogue's atomics (16 B each, at the ~1.3 TB/s
-# memory-side atomic rate, competing with the tile's output stores) cost more than the partial
-# merge + finalize launch they replace (profiles/r3_bn_acc_ab.jsonl, r3_bn_fin_ab.jsonl).
-_ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_ACC_MAX_PAIRS", str(128 << 10)))
+# Up to this many (tile, channel) pairs per layer the epilogue sums; above it, per-tile partials
+# and the BN finalize launch. With one accumulator replica, the same-address atomics of the 56x56
+# layers (3136 tiles per channel) serialized and 128 k was the best cap
+# (profiles/r4_acc_threshold_ab.jsonl); with the row tiles spread over 4 replicas (csrc/ops/abi.h ARENA_ACC_REP) every layer
+# takes the sums: 10,852 / 10,832 / 10,891 vs 10,678 / 10,664 / 10,706 images/s, alternating
+# runs on one box (profiles/r5_acc_rep_ab.txt; 16 replicas cost the consumers more than they
+# save, r5_accrep16_ab.jsonl).
+_ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_ACC_MAX_PAIRS", str(4 << 20)))
 
 
 # the same rule for the dgrad epilogue's BN-backward sums (BNGradLink acc form), separately
@@ -366,11 +370,11 @@ def set_bn_final(on: bool) -> None:
 
 
 def _stats_out(want: bool, part: Tensor, rpb: int):
-    """What ``forward_stats`` hands the BN layer: finished statistics ([2, C]: mean, variance)
-    or the flat per-tile partials."""
+    """What ``forward_stats`` hands the BN layer: finished statistics (the fp64 [rep, 2, C] sums
+    of the conv epilogue) or the flat fp32 per-tile partials."""
     if not want:
         return None
-    if part.dim() == 2:
+    if part.dtype == torch.float64:
         from .batchnorm import FinishedStats
         return FinishedStats(part)
     return (part, rpb)
@@ -893,7 +897,9 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                     bmask = torch.randint(0, 256, (m_in * cin // 8,), device=x.device,
                                           dtype=torch.uint8)
                     bmean = torch.zeros(cin, device=x.device)
-                    bsums = torch.zeros(2 * cin, dtype=torch.float64, device=x.device)
+                    from .batchnorm import acc_rep
+                    bsums = torch.zeros(acc_rep() * 2 * cin, dtype=torch.float64,
+                                        device=x.device)
                     for v in variants_for(cin) + v2_variants_for(cin) + halo(cin):
                         # timed in the epilogue form the step will run: fp64 sums into the BN's
                         # backward set where _use_link_acc picks it, else per-tile partials

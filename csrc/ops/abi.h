@@ -2,6 +2,13 @@
 #pragma once
 #include <stdint.h>
 
+// BatchNorm statistics accumulators ("acc mode", bn_kernels.hip / conv_kernels.hip): every fp64
+// set is ARENA_ACC_REP consecutive [2][C] replicas; a consumer sums all of them, in replica order.
+// The conv epilogues (up to 3136 tiles per channel at batch 128) add row tile mt's sums into
+// replica mt % ARENA_ACC_REP, so their same-address fp64 atomics do not serialize; the BN passes'
+// reductions (at most 512 block sums per channel) add into replica 0.
+#define ARENA_ACC_REP 4
+
 // ----------------------------------------------------------------------------------------------
 // Host-visible plain-C ABI structs shared with the torch binding TU (bindings.cpp).
 // ----------------------------------------------------------------------------------------------

@@ -778,13 +778,14 @@ unsigned* bn_tickets(const Tensor& like) {
 }
 
 // Statistics accumulators of acc mode (conv_kernels.hip ConvArgs::bn_acc, bn_kernels.hip): a
-// rotating pool of fp64 [2][C] sets, zero when handed out. A forward set (conv epilogue or
-// statistics pass -> apply pass) is zeroed by its layer's backward dx pass (bn_bwd zero_f); a
-// backward set from the pool by its finalize. The host tracks which sets may still hold sums (a
+// rotating pool of fp64 [kRep][2][C] sets (abi.h ARENA_ACC_REP replicas), zero when handed out.
+// A forward set (conv epilogue or statistics pass -> apply pass) is zeroed by its layer's
+// backward dx pass (bn_bwd zero_f); a backward set from the pool by its finalize. The host tracks which sets may still hold sums (a
 // training forward whose backward never ran): such a set is zeroed on the stream before it is
 // handed out again. Graph replays stay valid because every captured step zeroes the sets it
 // dirtied (forward and backward are captured together).
 constexpr int kAccSets = 128, kAccC = 2048;
+constexpr int64_t kRep = ARENA_ACC_REP;   // replicas per set (abi.h): a set is [kRep][2][C]
 struct AccPool {
   Tensor t;
   unsigned next = 0;
@@ -809,8 +810,8 @@ Tensor bn_acc_set(const Tensor& like, int64_t C) {
     static std::vector<Tensor> scratch;
     if ((int)scratch.size() <= dev) scratch.resize(dev + 1);
     if (!scratch[dev].defined())
-      scratch[dev] = torch::zeros({2 * kAccC}, like.options().dtype(torch::kFloat64));
-    return scratch[dev].narrow(0, 0, 2 * C).view({2, C});
+      scratch[dev] = torch::zeros({kRep * 2 * kAccC}, like.options().dtype(torch::kFloat64));
+    return scratch[dev].narrow(0, 0, kRep * 2 * C).view({kRep, 2, C});
   }
   if (!p.t.defined()) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
@@ -818,7 +819,7 @@ Tensor bn_acc_set(const Tensor& like, int64_t C) {
     TORCH_CHECK(cs == hipStreamCaptureStatusNone,
                 "arena BatchNorm: run one eager step before capturing a graph (its statistics "
                 "accumulators are allocated and zeroed on first use)");
-    p.t = torch::zeros({kAccSets, 2 * kAccC}, like.options().dtype(torch::kFloat64));
+    p.t = torch::zeros({kAccSets, kRep * 2 * kAccC}, like.options().dtype(torch::kFloat64));
     p.dirty.assign(kAccSets, 0);
     check_hip(hipStreamSynchronize(cur_stream()), "bn_acc_set zero");
   }
@@ -826,7 +827,7 @@ Tensor bn_acc_set(const Tensor& like, int64_t C) {
   Tensor row = p.t[set];
   if (p.dirty[set]) row.zero_();
   p.dirty[set] = 1;
-  return row.narrow(0, 0, 2 * C).view({2, C});
+  return row.narrow(0, 0, kRep * 2 * C).view({kRep, 2, C});
 }
 
 // A kernel that zeroes `t` (a pool set) has been enqueued: the set is clean for its next user.
@@ -836,8 +837,8 @@ void bn_acc_clean(const Tensor& t) {
   if (dev < 0 || (int)pools.size() <= dev || !pools[dev].t.defined()) return;
   const AccPool& p = pools[dev];
   const int64_t off = (const double*)t.data_ptr() - (const double*)p.t.data_ptr();
-  if (off < 0 || off >= (int64_t)kAccSets * 2 * kAccC) return;
-  pools[dev].dirty[off / (2 * kAccC)] = 0;
+  if (off < 0 || off >= (int64_t)kAccSets * kRep * 2 * kAccC) return;
+  pools[dev].dirty[off / (kRep * 2 * kAccC)] = 0;
 }
 
 // Split-K tickets of the conv kernel (ConvArgs::kcnt): one ring of zeroed counters per device;
@@ -960,8 +961,8 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
     if (stats_fin.has_value()) {
       TORCH_CHECK(stats_fin->is_cuda() && stats_fin->device() == x.device() &&
                       stats_fin->scalar_type() == torch::kFloat64 && stats_fin->is_contiguous() &&
-                      stats_fin->numel() == 2 * g.C && !stats_part.has_value(),
-                  "stats_fin must be a contiguous fp64 [2, C] tensor (and excludes stats_part)");
+                      stats_fin->numel() == kRep * 2 * g.C && !stats_part.has_value(),
+                  "stats_fin must be a contiguous fp64 [kRep, 2, C] set (and excludes stats_part)");
     } else if (stats_part.has_value()) {
       check_f32(*stats_part, "stats_part");
       TORCH_CHECK(stats_rpb > 0 && stats_part->is_contiguous(), "stats_part: bad layout");
@@ -1068,8 +1069,8 @@ std::vector<Tensor> bn_fold_fwd(Tensor x, OptT gamma, OptT beta, OptT running_me
   if (fin) {
     TORCH_CHECK(stats_fin->is_cuda() && stats_fin->device() == x.device() &&
                     stats_fin->scalar_type() == torch::kFloat64 && stats_fin->is_contiguous() &&
-                    stats_fin->numel() == 2 * g.C,
-                "bn_fold_fwd: stats_fin must be a contiguous fp64 [2, C] tensor");
+                    stats_fin->numel() == kRep * 2 * g.C,
+                "bn_fold_fwd: stats_fin must be a contiguous fp64 [kRep, 2, C] set");
   } else {
     check_f32(*stats_part, "stats_part");
     TORCH_CHECK(stats_rpb > 0 && stats_part->is_contiguous(), "stats_part: bad layout");
@@ -1165,7 +1166,7 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
   if (acc_ready) {
     TORCH_CHECK(acc_b->is_cuda() && acc_b->device() == x.device() &&
                     acc_b->scalar_type() == torch::kFloat64 && acc_b->is_contiguous() &&
-                    acc_b->numel() == 2 * g.C,
+                    acc_b->numel() == kRep * 2 * g.C,
                 "acc_b must be a contiguous fp64 tensor of 2*C elements on x's device");
     acc = *acc_b;
     fin_dx = 1;
@@ -1174,7 +1175,7 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
     if (acc_b.has_value()) {
       TORCH_CHECK(acc_b->is_cuda() && acc_b->device() == x.device() &&
                       acc_b->scalar_type() == torch::kFloat64 && acc_b->is_contiguous() &&
-                      acc_b->numel() == 2 * g.C,
+                      acc_b->numel() == kRep * 2 * g.C,
                   "acc_b must be a contiguous fp64 tensor of 2*C elements on x's device");
       acc = *acc_b;
       fin_dx = 1;
@@ -1222,8 +1223,8 @@ std::vector<Tensor> bn_pool_fwd(Tensor x, OptT gamma, OptT beta, OptT running_me
   if (fin.has_value())
     TORCH_CHECK(fin->is_cuda() && fin->device() == x.device() &&
                     fin->scalar_type() == torch::kFloat64 && fin->is_contiguous() &&
-                    fin->numel() == 2 * g.C,
-                "bn_pool_fwd: fin must be the fp64 [2, C] statistics sums");
+                    fin->numel() == kRep * 2 * g.C,
+                "bn_pool_fwd: fin must be the fp64 [kRep, 2, C] statistics sums");
   int ext_nblk = 0;
   Tensor lvl2;
   unsigned* tickets = nullptr;
@@ -1302,7 +1303,7 @@ std::vector<Tensor> bn_pool_bwd(Tensor dy, Tensor pos, Tensor x, Tensor mean, Te
               "bn_pool_bwd: pos must be the forward's argmax bytes");
   TORCH_CHECK(acc_b.is_cuda() && acc_b.device() == x.device() &&
                   acc_b.scalar_type() == torch::kFloat64 && acc_b.is_contiguous() &&
-                  acc_b.numel() == 2 * g.C,
+                  acc_b.numel() == kRep * 2 * g.C,
               "acc_b must be a contiguous fp64 tensor of 2*C elements on x's device");
   auto f32 = x.options().dtype(torch::kFloat32);
   ArenaBNBwd b{};
@@ -1398,8 +1399,8 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
     TORCH_CHECK(bn_x.has_value() && with_stats && !fin, "conv_fwd: bn_acc is the bn_x form's");
     TORCH_CHECK(bn_acc->is_cuda() && bn_acc->device() == x.device() &&
                     bn_acc->scalar_type() == torch::kFloat64 && bn_acc->is_contiguous() &&
-                    bn_acc->numel() == 2 * Cout,
-                "conv_fwd: bn_acc must be a contiguous fp64 tensor of 2*Cout elements");
+                    bn_acc->numel() == kRep * 2 * Cout,
+                "conv_fwd: bn_acc must be a contiguous fp64 [kRep, 2, Cout] set");
   }
   Tensor part = with_stats && !fin && !bacc
                     ? torch::empty({m_tiles * 2 * Cout}, x.options().dtype(torch::kFloat32))
@@ -2054,6 +2055,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_set_acc", [](bool on) { g_bn_acc = on; });
   m.def("bn_acc_scratch", [](bool on) { g_acc_scratch = on; });
   m.def("bn_pool_fwd", &bn_pool_fwd);
+  m.attr("acc_rep") = (int)ARENA_ACC_REP;   // replicas per BatchNorm accumulator set
   m.def("conv_set_stats_one_pass", [](bool on) { arena_conv_set_stats_one_pass(on ? 1 : 0); });
   m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {

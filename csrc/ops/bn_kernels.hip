@@ -137,6 +137,22 @@ __device__ __forceinline__ void load8f(const float* p, float v[kVec]) {
 // plain stores: its last reader has finished by stream order). That replaces the two-level merge
 // of per-block partials (up to 3136 per channel) in the partial-based finalize kernels below.
 
+// Replicated sets (abi.h ARENA_ACC_REP): the BN passes' reductions emit at most 512 block sums
+// per channel and add into replica 0; the conv epilogues spread over all replicas. Readers sum
+// every replica in replica order.
+constexpr int kAccRep = ARENA_ACC_REP;
+
+__device__ __forceinline__ void acc_sums(const double* __restrict__ acc, int C, int c, double& s1,
+                                         double& s2) {
+  s1 = acc[c];
+  s2 = acc[C + c];
+#pragma unroll
+  for (int r = 1; r < kAccRep; ++r) {
+    s1 += acc[(size_t)r * 2 * C + c];
+    s2 += acc[(size_t)r * 2 * C + C + c];
+  }
+}
+
 // Reduction geometry. A block covers `cg` channel groups (all C / 8 of them, or a 32-group slice
 // for C > 256: blockIdx.y picks the slice) and kT / cg row slots. The channel split keeps the
 // number of (row block, channel) pairs -- the per-block sums a reduction emits -- at <= 512 x 256
@@ -435,7 +451,8 @@ __device__ __forceinline__ void apply_coefs(int C, long long M, const double* fi
       sc = st.scale[c];
       sh = st.shift[c];
     } else {
-      const double s1 = fin[c], s2 = fin[C + c];
+      double s1, s2;
+      acc_sums(fin, C, c, s1, s2);
       const double mean = s1 * inv_m;
       const double d = s2 - s1 * mean;
       const double m2 = d > 0.0 ? d : 0.0;
@@ -540,7 +557,8 @@ __global__ __launch_bounds__(kT) void bn_fold_coef_kernel(ArenaBNStats st,
     const int c = blockIdx.x * kT + threadIdx.x;
     if (c >= C) return;
     const double inv_m = 1.0 / (double)M;
-    const double s1 = fin[c], s2 = fin[C + c];
+    double s1, s2;
+    acc_sums(fin, C, c, s1, s2);
     const double mean = s1 * inv_m;
     const double d = s2 - s1 * mean;
     const double m2 = d > 0.0 ? d : 0.0;
@@ -700,9 +718,14 @@ __global__ __launch_bounds__(kT) void bn_bwd_acc_finalize_kernel(double* __restr
                                                                  ArenaBNBwd out) {
   const int c = blockIdx.x * kT + threadIdx.x;
   if (c >= C) return;
-  const double a = __hip_atomic_exchange(acc + c, 0.0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const double b = __hip_atomic_exchange(acc + C + c, 0.0, __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT);
+  double a = 0.0, b = 0.0;
+#pragma unroll
+  for (int r = 0; r < kAccRep; ++r) {
+    a += __hip_atomic_exchange(acc + (size_t)r * 2 * C + c, 0.0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    b += __hip_atomic_exchange(acc + (size_t)r * 2 * C + C + c, 0.0, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+  }
   bn_bwd_finish(out, c, a, b, M);
 }
 
@@ -762,7 +785,8 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
   for (int c = threadIdx.x; c < C; c += kT) {   // one thread per channel (see lds8)
     float a_, b_, c_;
     if constexpr (FIN) {
-      const double a = acc[c], b = acc[C + c];
+      double a, b;
+      acc_sums(acc, C, c, a, b);
       const float invstd = co.invstd[c];
       const float gam = co.gamma ? co.gamma[c] : 1.f;
       a_ = gam * invstd;
@@ -1034,7 +1058,8 @@ __global__ __launch_bounds__(kT) void bn_pool_bwd_dx_kernel(const T* __restrict_
   const int c8 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1));
   const double inv_m = 1.0 / (double)M;
   for (int c = threadIdx.x; c < C; c += kT) {
-    const double a = acc[c], b = acc[C + c];
+    double a, b;
+    acc_sums(acc, C, c, a, b);
     const float invstd = co.invstd[c];
     const float gam = co.gamma ? co.gamma[c] : 1.f;
     s_co[c] = gam * invstd;
@@ -1215,7 +1240,8 @@ __global__ __launch_bounds__(kT) void bn_pool_bwd_dx_q_kernel(const T* __restric
   const int c8 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1));
   const double inv_m = 1.0 / (double)M;
   for (int c = threadIdx.x; c < C; c += kT) {
-    const double a = acc[c], b = acc[C + c];
+    double a, b;
+    acc_sums(acc, C, c, a, b);
     const float invstd = co.invstd[c];
     const float gam = co.gamma ? co.gamma[c] : 1.f;
     s_co[c] = gam * invstd;

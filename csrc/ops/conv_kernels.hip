@@ -87,7 +87,7 @@ struct ConvArgs {
   int c16;
   // EPI 1, accumulated statistics (bn_acc != null, part unused): every tile adds its moment
   // sums (n*mean = sum y, M2 + n*mean^2 = sum y^2 over its rows) into fp64 accumulators
-  // bn_acc [2][Cout] with memory-side atomics, fire-and-forget (the persistent form: once per
+  // bn_acc [ARENA_ACC_REP][2][Cout] (replica mt % ARENA_ACC_REP) with memory-side atomics, fire-and-forget (the persistent form: once per
   // block). The consuming BN apply pass derives its coefficients from the sums (bn_kernels.hip
   // apply_coefs) and the layer's backward zeroes them: no finalize launch, where per-tile
   // partials (3136 per channel for a 56x56 layer at batch 128) need a two-level merge.
@@ -287,6 +287,13 @@ __device__ __forceinline__ float row16_sum(float v) {
   return v;
 }
 
+// The accumulator replica (abi.h ARENA_ACC_REP) that row tile `mt` adds its BatchNorm sums into:
+// tiles of one column range differ in mt, so the same-address fp64 atomics of up to 3136 tiles per
+// channel spread over every replica.
+__device__ __forceinline__ double* acc_replica(const ConvArgs& a, int mt) {
+  return a.bn_acc + (size_t)(mt % ARENA_ACC_REP) * 2 * a.Cout;
+}
+
 // EPI 1 accumulated-statistics tail (see ConvArgs::bn_acc). `emit(add)` calls add(c, mean, m2)
 // for the block's channels c in [0, BN) whose tile statistics this thread holds. The values are
 // restaged in LDS so that consecutive lanes add to consecutive channels: 64 fp64 adds = 512
@@ -301,7 +308,7 @@ __device__ __forceinline__ double* bn_lacc_storage() {
 // lacc != null (persistent tiles): the sums are added into the block's LDS set lacc [2][BN] by
 // the same owner thread per channel instead, and flushed once after the last tile.
 template <int BM, int BN, int NT, typename Emit>
-__device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int n0, int nrows,
+__device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int mt, int n0, int nrows,
                                                 double* lacc, Emit&& emit) {
   __shared__ float s_st[2][BN];
   emit([&](int c, float mean, float m2) {
@@ -311,7 +318,7 @@ __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int n0, int n
   // LDS-only barrier: __syncthreads() would also wait for the tile's output stores (vmcnt(0)),
   // holding the CU slot for their whole latency (measured +16 us on a 56x56 1x1 layer)
   lds_barrier();
-  double* acc = a.bn_acc + n0;
+  double* acc = acc_replica(a, mt) + n0;
   const double n = (double)nrows;
   for (int c = threadIdx.x; c < BN; c += NT) {
     const double mu = (double)s_st[0][c];
@@ -871,8 +878,9 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
               r2 += red[h * 2 * BN + BN + c];
             }
             if (a.bn_acc != nullptr) {   // acc mode: the BN layer's fp64 backward sums
-              unsafeAtomicAdd(a.bn_acc + n0 + c, (double)r1);
-              unsafeAtomicAdd(a.bn_acc + a.Cout + n0 + c, (double)r2);
+              double* acc = acc_replica(a, mt) + n0;
+              unsafeAtomicAdd(acc + c, (double)r1);
+              unsafeAtomicAdd(acc + a.Cout + c, (double)r2);
             } else {
               a.part[(size_t)mt * 2 * a.Cout + n0 + c] = r1;
               a.part[(size_t)mt * 2 * a.Cout + a.Cout + n0 + c] = r2;
@@ -1011,7 +1019,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
             }
         }
       } else {
-        bn_acc_epilogue<BM, BN, NT>(a, n0, nrows, lacc, [&](auto&& add) {
+        bn_acc_epilogue<BM, BN, NT>(a, mt, n0, nrows, lacc, [&](auto&& add) {
           if (wm == 0 && fr == 0) {
 #pragma unroll
             for (int j = 0; j < NI; ++j)
@@ -1023,7 +1031,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
     }
   }   // tile loop
   if (lacc != nullptr) {   // the block's sums, once (each channel by the thread that summed it)
-    double* acc = a.bn_acc + n0;
+    double* acc = acc_replica(a, (int)blockIdx.x) + n0;
     for (int c = threadIdx.x; c < BN; c += NT) {
       unsafeAtomicAdd(acc + c, lacc[c]);
       unsafeAtomicAdd(acc + a.Cout + c, lacc[BN + c]);
@@ -1376,7 +1384,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
 #pragma unroll
         for (int g2 = 0; g2 < RG2; ++g2) sum += tile[g2 * BN + tid];
         if (a.bn_acc != nullptr)   // acc mode: the BN layer's fp64 backward sums
-          unsafeAtomicAdd(a.bn_acc + q * a.Cout + n0 + tid, (double)sum);
+          unsafeAtomicAdd(acc_replica(a, mt) + q * a.Cout + n0 + tid, (double)sum);
         else
           a.part[(size_t)mt * 2 * a.Cout + q * a.Cout + n0 + tid] = sum;
       }
@@ -1390,8 +1398,9 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
         a.part[(size_t)mt * 2 * a.Cout + a.Cout + c] = st_m2;
       } else {
         const double n = (double)st_n, mu = (double)st_mean;
-        unsafeAtomicAdd(a.bn_acc + c, n * mu);                                 // sum y
-        unsafeAtomicAdd(a.bn_acc + a.Cout + c, (double)st_m2 + n * mu * mu);   // sum y^2
+        double* acc = acc_replica(a, mt);
+        unsafeAtomicAdd(acc + c, n * mu);                                 // sum y
+        unsafeAtomicAdd(acc + a.Cout + c, (double)st_m2 + n * mu * mu);   // sum y^2
       }
     }
   }

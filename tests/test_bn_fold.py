@@ -47,7 +47,10 @@ def _bn_parts(y1, seed):
     beta = torch.randn(c, device="cuda", generator=g) * 0.5
     m = y1.shape[0] * y1.shape[2] * y1.shape[3]
     yf = y1.permute(0, 2, 3, 1).reshape(m, c).double()
-    fin = torch.stack([yf.sum(0), (yf * yf).sum(0)]).contiguous()   # what the conv epilogue sums
+    # what the conv epilogue sums, in replica 0 of a [rep, 2, C] set
+    from arena_amd.ops.batchnorm import acc_rep
+    fin = torch.zeros(acc_rep(), 2, c, dtype=torch.float64, device="cuda")
+    fin[0] = torch.stack([yf.sum(0), (yf * yf).sum(0)])
     rm0, rv0 = torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")
     out, mean, invstd, mask, _ = ext.bn_fwd(y1, None, gamma, beta, rm0.clone(), rv0.clone(), True,
                                             0.1, 1e-5, True, None, None, 0, fin)
@@ -81,8 +84,8 @@ def test_fold_kernels_bit_identical_to_unfused(shape):
             yu = conv.conv2d_fwd(out, wt, 1, pad, v, with_stats=True, final=fin)
             yp = conv.conv2d_fwd(y1, wt, 1, pad, v, with_stats=True, final=fin, pre=coef)
             assert torch.equal(yp[0], yu[0]), (v, fin)
-            su = yu[1].fin if fin else yu[1][0]
-            sp = yp[1].fin if fin else yp[1][0]
+            su = yu[1].sums() if fin else yu[1][0]
+            sp = yp[1].sums() if fin else yp[1][0]
             if fin:
                 torch.testing.assert_close(sp, su, rtol=1e-9, atol=1e-6)   # fp64 atomics order
             else:

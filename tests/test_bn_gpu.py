@@ -159,12 +159,13 @@ def test_conv_finished_stats_feed_bn(shape):
     w = _nhwc((torch.randn(C, 64, 3, 3, device="cuda") * 0.05).to(torch.bfloat16))
     for rep in range(130):   # more uses than the pool has sets (128)
         y, st = conv.conv2d_fwd(x, w, 1, 1, with_stats=True, final=True)
-        assert isinstance(st, FinishedStats) and st.fin.shape == (2, C)
+        assert isinstance(st, FinishedStats) and st.fin.shape[-2:] == (2, C)
         assert st.fin.dtype == torch.float64
         yf = y.double()
         Mrows = N * H * W
-        assert torch.allclose(st.fin[0] / Mrows, yf.mean(dim=(0, 2, 3)), rtol=1e-5, atol=1e-6)
-        assert torch.allclose(st.fin[1] / Mrows, (yf * yf).mean(dim=(0, 2, 3)), rtol=1e-5,
+        tot = st.sums()
+        assert torch.allclose(tot[0] / Mrows, yf.mean(dim=(0, 2, 3)), rtol=1e-5, atol=1e-6)
+        assert torch.allclose(tot[1] / Mrows, (yf * yf).mean(dim=(0, 2, 3)), rtol=1e-5,
                               atol=1e-6)
         if rep < 129:
             st.discard()      # what a BN layer's finalize does: the set is zero again
@@ -295,10 +296,11 @@ def test_bn_relu_maxpool_fused_matches_modules(dtype, partials, pad):
                 if dtype != torch.bfloat16:     # fp32 BN input: a statistics pass, not the sums
                     st.discard()
                     st = batchnorm.FinishedStats(st.fin)
-                    with torch.no_grad():
+                    with torch.no_grad():   # replica 0 holds the sums, the others stay zero
                         yf = y.double()
-                        st.fin[0].copy_(yf.sum(dim=(0, 2, 3)))
-                        st.fin[1].copy_((yf * yf).sum(dim=(0, 2, 3)))
+                        f = st.fin.view(-1, 2, C)
+                        f[0, 0].copy_(yf.sum(dim=(0, 2, 3)))
+                        f[0, 1].copy_((yf * yf).sum(dim=(0, 2, 3)))
                 out = batchnorm.bn_relu_maxpool(bn, pool, y, st)
                 if g is None:
                     g = _nhwc(torch.randn(out.shape, device="cuda").to(out.dtype))

@@ -394,7 +394,7 @@ def test_conv_persistent_tiles_match_one_tile_per_block(shape):
     for v in conv.variants_for(cout):
         y, (part, rpb) = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True)
         _, fin = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True, final=True)
-        ref_sums = fin.fin.clone()
+        ref_sums = fin.sums()
         fin.discard()
         for p in (1, 2, 3):
             pv = v + 256 * p
@@ -403,7 +403,7 @@ def test_conv_persistent_tiles_match_one_tile_per_block(shape):
             assert torch.equal(y2, y) and rpb2 == rpb and torch.equal(part2, part), (v, p)
             y3, fin3 = conv.conv2d_fwd(x, wt, st, pad, pv, with_stats=True, final=True)
             assert torch.equal(y3, y)
-            torch.testing.assert_close(fin3.fin, ref_sums, rtol=1e-9, atol=1e-6)
+            torch.testing.assert_close(fin3.sums(), ref_sums, rtol=1e-9, atol=1e-6)
             fin3.discard()
     if st == 1:
         dy = torch.randn(n, cout, h, w, device="cuda").to(torch.bfloat16).contiguous(
@@ -731,11 +731,13 @@ def test_dgrad_epilogue_bn_backward_partials():
                 torch.testing.assert_close(p[t, 0], g[sl].sum(0), rtol=1e-4, atol=1e-3)
                 torch.testing.assert_close(p[t, 1], (g[sl] * xc[sl]).sum(0), rtol=1e-4,
                                            atol=1e-3)
-        # acc form: the same sums added into an fp64 [2, C] set (twice: it accumulates)
-        acc = torch.zeros(2 * cin, dtype=torch.float64, device="cuda")
+        # acc form: the same sums added into an fp64 [rep, 2, C] set (twice: it accumulates)
+        from arena_amd.ops.batchnorm import acc_rep, acc_totals
+        acc_set = torch.zeros(acc_rep() * 2 * cin, dtype=torch.float64, device="cuda")
         for rep_ in range(2):
-            dxs, none = conv.conv2d_bwd_data(dy, wt, 1, v, bn=(bnx, mask, mean), bn_acc=acc)
+            dxs, none = conv.conv2d_bwd_data(dy, wt, 1, v, bn=(bnx, mask, mean), bn_acc=acc_set)
             assert none is None and torch.equal(dxs, dx0), v
+        acc = acc_totals(acc_set.view(-1, 2, cin)).reshape(-1)
         g0 = dx0.permute(0, 2, 3, 1).reshape(m, cin).float() * bits
         torch.testing.assert_close(acc[:cin].float(), 2 * g0.sum(0), rtol=1e-4, atol=2e-3)
         torch.testing.assert_close(acc[cin:].float(), 2 * (g0 * xc).sum(0), rtol=1e-4, atol=2e-3)
