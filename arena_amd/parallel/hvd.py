@@ -206,6 +206,10 @@ def broadcast_parameters(params, root_rank: int = 0) -> None:
                     n = t.numel()
                     t.copy_(flat[off:off + n].view_as(t))
                     off += n
+        if comm is not None:
+            # a barrier that timed out leaves the copies incomplete: fail here, before training
+            # starts from weights that silently differ between ranks
+            comm.check()
     finally:
         if temp and comm is not None:
             comm.close()

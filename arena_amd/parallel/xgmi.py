@@ -145,6 +145,15 @@ class XgmiComm:
         ext = _ext.load()
         self.ext = ext
         self.device = torch.cuda.current_device()
+        # ranks sharing one GPU (same-device rehearsals): their launches must fit on it together,
+        # so each collective launch gets at most 128 / W blocks (csrc/ccl/xgmi_ccl.hip
+        # g_max_blocks; the same cap on every rank, so the block geometries still match)
+        devs: List[Optional[str]] = [None] * self.world
+        dist.all_gather_object(devs, _device_id(self.device), group=group)
+        self.shared_gpu = len(set(devs)) < self.world and all(devs)
+        if hasattr(ext, "ccl_set_max_blocks"):
+            ext.ccl_set_max_blocks(max(4, 128 // self.world) if self.shared_gpu
+                                   else ext.ccl_max_blocks)
         self.staging_elems = _round4(staging_elems)
         self.param_elems = _round4(param_elems) if param_elems else 0
         self._own, self._opened = [], []

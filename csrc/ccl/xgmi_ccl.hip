@@ -547,6 +547,13 @@ __global__ __launch_bounds__(kThreads) void xgmi_sgd_f32_kernel(ArenaXgmiPeers P
 // Floats of a chunk per block. Every block pays two cross-rank barriers (one L2 writeback + one
 // invalidate each), so blocks are made fat rather than numerous; tunable for sweeps.
 long long g_block_elems = 4096;
+// Blocks per collective launch (<= kMaxB, the flag slots). Every block of a launch meets the
+// blocks of the same index on every rank at its barriers, so all ranks' blocks must be able to
+// run at once. With one rank per GPU that is each GPU's own launch; when several ranks share a
+// GPU (same-device rehearsals of a W-GPU node) their launches must fit on it TOGETHER: XgmiComm
+// lowers the cap to 128 / W there (8 ranks x 256 blocks starved each other until the barrier
+// timeouts -- a 32 MB broadcast at W = 8 hung for minutes and returned partial copies).
+int g_max_blocks = kMaxB;
 // Crossover measured on 1x MI355X, 2 ranks (profiles/r1_ccl_oneshot_ab.jsonl): one-shot 3.0 vs
 // 3.7 us at 4 KB, 3.56 vs 3.97 us at 16 KB, but 4.5 vs 4.26 us at 64 KB. One-shot also moves
 // (W-1) x n bytes per rank over the links instead of 2 (W-1)/W x n, so the default stays at 32 KB.
@@ -559,7 +566,7 @@ long long g_bcast_direct_max = 128 << 10;
 
 void range_geometry(long long n, long long* S, int* nb) {
   int blocks = (int)std::min<long long>(
-      kMaxB, std::max<long long>(1, (n + g_block_elems - 1) / g_block_elems));
+      g_max_blocks, std::max<long long>(1, (n + g_block_elems - 1) / g_block_elems));
   long long s = (n + blocks - 1) / blocks;
   s = (s + 3) / 4 * 4;
   *S = s;
@@ -570,7 +577,7 @@ void geometry(long long n, int W, long long* L, long long* S, int* nb) {
   long long l = (n + W - 1) / W;
   l = (l + 3) / 4 * 4;
   int blocks = (int)std::min<long long>(
-      kMaxB, std::max<long long>(1, (l + g_block_elems - 1) / g_block_elems));
+      g_max_blocks, std::max<long long>(1, (l + g_block_elems - 1) / g_block_elems));
   long long s = (l + blocks - 1) / blocks;
   s = (s + 3) / 4 * 4;
   *L = l;
@@ -657,6 +664,7 @@ hipError_t arena_ccl_adam(const ArenaXgmiPeers* P, float* M, float* V, long long
 }
 
 void arena_ccl_set_block_elems(long long e) { g_block_elems = e < 256 ? 256 : e; }
+void arena_ccl_set_max_blocks(int b) { g_max_blocks = b < 1 ? 1 : (b > kMaxB ? kMaxB : b); }
 
 // Broadcast n floats (n % 4 == 0, n <= buf_elems) from `root`: in = the root's source, out =
 // every rank's destination (in == out is allowed; non-roots ignore in).
@@ -688,7 +696,8 @@ void sgd_geometry(long long n, int W, long long* L, long long* S, int* nb) {
   long long l = (n + W - 1) / W;
   l = (l + 7) / 8 * 8;
   const long long per_block = std::max<long long>(8, g_block_elems * 2);  // bytes as the fp32 path
-  int blocks = (int)std::min<long long>(kMaxB, std::max<long long>(1, (l + per_block - 1) / per_block));
+  int blocks = (int)std::min<long long>(g_max_blocks,
+                                        std::max<long long>(1, (l + per_block - 1) / per_block));
   long long s = (l + blocks - 1) / blocks;
   s = (s + 7) / 8 * 8;
   *L = l;

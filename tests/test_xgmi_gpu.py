@@ -7,6 +7,7 @@ and torch.optim.Adam / the flat Adam kernel.
 """
 from __future__ import annotations
 
+import functools
 import os
 import socket
 import sys
@@ -457,7 +458,7 @@ def _sharded_sgd_semantics(rank, world, port, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-def _zero_sgd(rank, world, port, q):
+def _zero_sgd(rank, world, port, q, bucket_mb=None):
     """Data-parallel ResNet with bf16 weights: ShardedMasterSGD (reduce-scatter grads -> fp32
     master SGD on the owned chunk -> all-gather weights, one xGMI kernel per bucket, BN/bias in
     fp32 tail buckets of the same communicator).
@@ -492,7 +493,8 @@ def _zero_sgd(rank, world, port, q):
         args = types.SimpleNamespace(model="resnet_tiny", data_format="NHWC", batch_size=8,
                                      image_size=32, num_classes=10, width=64, learning_rate=0.05,
                                      momentum=0.9, weight_decay=1e-3,
-                                     bucket_mb=0.05 if world <= 2 else 4.0, comm="xgmi",
+                                     bucket_mb=bucket_mb or (0.05 if world <= 2 else 4.0),
+                                     comm="xgmi",
                                      master_weights="auto", dtype="bf16")
 
         def progress(what):   # one line per stage (a slow shared-GPU run is visibly alive)
@@ -507,6 +509,12 @@ def _zero_sgd(rank, world, port, q):
         params = list(model.parameters())
         decay = {id(p) for p in opt.param_groups[0]["params"]}
         w0 = [p.detach().float().clone() for p in params]
+        # diagnostics: identical starting weights on every rank (the build's broadcast)
+        dig = [None] * world
+        dist.all_gather_object(dig, float(torch.cat([w.reshape(-1) for w in w0]).double().sum()))
+        res["init_identical"] = len(set(dig)) == 1
+        bucket_of = {id(q): k for k, b in enumerate(opt.buckets) for r_ in b.ranges
+                     for q in r_.params}
         flat_ref = torch.zeros(sum(p.numel() for p in params), dtype=torch.float32)
         if rank == 0:
             grads = []
@@ -534,11 +542,14 @@ def _zero_sgd(rank, world, port, q):
         opt.comm.check()
         progress("one DP step")
         off, worst_ulp, worst_f32 = 0, 0.0, 0.0
+        per_param = []
         for i, p in enumerate(params):
             n = p.numel()
             ref = flat_ref[off:off + n].to(dev).view(p.shape)
             off += n
             got = p.detach().float()
+            per_param.append((float((got - ref).abs().max()), i, str(p.dtype)[6:],
+                              bucket_of.get(id(p), -1), tuple(p.shape)))
             if p.dtype == bf:
                 # one bf16 rounding of w0 - lr * g (its ulp at the operands' scale, so a
                 # cancelling update is not measured in ulps of a near-zero result) + 1 % of the
@@ -552,6 +563,8 @@ def _zero_sgd(rank, world, port, q):
                 worst_f32 = max(worst_f32, float(((got - ref).abs() / tol).max()))
         res["one_step_bf16_ulps"] = worst_ulp
         res["one_step_f32_rel"] = worst_f32
+        res["worst_params"] = sorted(per_param, reverse=True)[:6]
+        res["n_buckets"] = len(opt.buckets)
         opt.close()
         dist.barrier()
         # ---- (2) eager vs hipGraph replay, replicas bit-identical
@@ -581,6 +594,52 @@ def _zero_sgd(rank, world, port, q):
         q.put((rank, res, None))
     except Exception:  # noqa: BLE001
         q.put((rank, None, traceback.format_exc()))
+
+
+def _bcast_big(rank, world, port, q):
+    """A model-sized broadcast the way a job's build runs it: (a) a 32 MB vector through a comm
+    whose staging holds it whole (the zero-copy two-shot path), (b) hvd.broadcast_parameters of a
+    resnet_tiny state_dict through the temporary communicator, every non-root rank starting from
+    different weights."""
+    try:
+        dist = _init(rank, world, port)
+        from arena_amd.models.resnet import resnet
+        from arena_amd.parallel import hvd
+        from arena_amd.parallel.xgmi import XgmiComm
+        hvd.init()
+        res = {}
+        n = 8 << 20
+        want = torch.randn(n, device="cuda", generator=torch.Generator(device="cuda").manual_seed(7))
+        x = want.clone() if rank == 0 else torch.randn(n, device="cuda")
+        comm = XgmiComm(staging_elems=n, timeout_s=60.0)
+        comm.broadcast_(x, 0)
+        torch.cuda.synchronize()
+        res["vec"] = bool(torch.equal(x, want))
+        comm.check()
+        comm.close()
+        print(f"[bcast_big w{world} r{rank}] 32 MB broadcast done", file=sys.stderr, flush=True)
+        torch.manual_seed(1234 + (rank > 0) * (rank + 1))
+        model = resnet("resnet_tiny", num_classes=10, width=64).cuda().to(
+            memory_format=torch.channels_last)
+        hvd.broadcast_parameters(model.state_dict(), root_rank=0)
+        torch.cuda.synchronize()
+        dig = float(torch.cat([t.detach().double().reshape(-1) for t in
+                               model.state_dict().values()]).sum())
+        digs = [None] * world
+        dist.all_gather_object(digs, dig)
+        res["params"] = len(set(digs)) == 1
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_xgmi_model_sized_broadcast(world):
+    out = _run(_bcast_big, world, timeout=300)
+    for r, res in out.items():
+        assert res["vec"] and res["params"], (r, res)
 
 
 def _bcast_gather(rank, world, port, q):
@@ -703,11 +762,12 @@ def test_sharded_sgd_update_timing_semantics():
         assert res["no_sync_b"] < 1e-5 and res["no_sync_a"] == 0, (r, res)
 
 
-@pytest.mark.parametrize("world", [2, 8])
-def test_dp_resnet_sharded_bf16_sgd(world):
+@pytest.mark.parametrize("world,bucket_mb", [(2, None), (2, 4.0), (8, None)])
+def test_dp_resnet_sharded_bf16_sgd(world, bucket_mb):
     """W = 8: the 8-GPU node's data-parallel configuration (ShardedMasterSGD over 8 ranks, eager
-    and hipGraph-captured), here with 8 ranks time-sharing one GPU."""
-    out = _run(_zero_sgd, world, timeout=420)
+    and hipGraph-captured), here with 8 ranks time-sharing one GPU. (2, 4.0): W = 2 with the
+    few large mixed-dtype buckets W = 8 uses."""
+    out = _run(functools.partial(_zero_sgd, bucket_mb=bucket_mb), world, timeout=420)
     for r, res in out.items():
         assert res["one_step_bf16_ulps"] <= 1.0, (r, res)
         assert res["one_step_f32_rel"] <= 1.0, (r, res)
