@@ -59,6 +59,7 @@ hipError_t arena_ccl_sgd_f32(const ArenaXgmiPeers*, float*, long long, long long
 void arena_ccl_sgd_f32_shard(long long, long long, int, int, long long*, long long*);
 void arena_ccl_set_block_elems(long long);
 void arena_ccl_set_max_blocks(int);
+void arena_bn_set_elem_max_blocks(int);
 void arena_ccl_set_oneshot_max(long long);
 long long arena_ccl_get_oneshot_max();
 // csrc/ops/conv_kernels.hip
@@ -2083,6 +2084,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ccl_shard", &ccl_shard);
   m.def("ccl_set_block_elems", [](int64_t e) { arena_ccl_set_block_elems(e); });
   m.def("ccl_set_max_blocks", [](int64_t b) { arena_ccl_set_max_blocks((int)b); });
+  m.def("bn_set_elem_max_blocks", [](int64_t b) { arena_bn_set_elem_max_blocks((int)b); });
   m.def("ccl_set_oneshot_max", [](int64_t e) { arena_ccl_set_oneshot_max(e); });
   m.def("ccl_get_oneshot_max", []() { return (int64_t)arena_ccl_get_oneshot_max(); });
   m.def("ccl_set_bcast_direct_max", [](int64_t e) { arena_ccl_set_bcast_direct_max(e); });

@@ -1327,9 +1327,14 @@ long long reduce_blocks(long long M, int C, long long* rpb) {
   return (M + r - 1) / r;
 }
 
+// Grid of the streaming passes (apply, dx): at most g_elem_max_blocks blocks, each thread then
+// loops over its vectors. Every block derives its per-channel coefficients in its prologue (from
+// the fp64 sums: ARENA_ACC_REP replicas x 2 x C loads), so fewer, fatter blocks pay that less often.
+int g_elem_max_blocks = 4096;
+
 int elementwise_blocks(long long nvec) {
   long long b = (nvec + 2LL * kT - 1) / (2LL * kT);
-  return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+  return (int)(b < 1 ? 1 : (b > g_elem_max_blocks ? g_elem_max_blocks : b));
 }
 
 bool bad_shape(long long M, int C) {
@@ -1343,6 +1348,8 @@ extern "C" {
 void arena_bn_set_fin_max_blocks(int p) { g_fin_max_p = p < 1 ? 1 : (p > 64 ? 64 : p); }
 
 void arena_bn_set_nt(int on) { g_bn_nt = on ? 1 : 0; }
+
+void arena_bn_set_elem_max_blocks(int b) { g_elem_max_blocks = b < 64 ? 64 : (b > 65536 ? 65536 : b); }
 
 void arena_bn_set_pool_quad_mult(int m) { g_pool_quad_mult = m < 1 ? 1 : (m > 16 ? 16 : m); }
 

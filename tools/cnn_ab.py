@@ -15,7 +15,8 @@ BN statistics as fp64 sums up to n tile-channel pairs) and/or ``:finbwd0`` (BN b
 from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv forms) and/or
 ``:nostempool`` (stem BN and max pool unfused) and/or ``:fold`` (bn1 / bn2 folded into the
 consuming convs instead of applied by their own pass) and/or ``:v2split`` (split-K forms of the
-v2 tiles among the candidates), joined with ``+``.
+v2 tiles among the candidates) and/or ``:ebk<n>`` (at most n blocks per BN apply / dx pass),
+joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
     python tools/cnn_ab.py --modes miopen,auto --batch 128 > gpurun_out/cnn_ab.jsonl
@@ -93,6 +94,9 @@ def main():
         conv.set_bn_fold("fold" in opt_s.split("+"))
         # v2split: the v2 split-K forms among the autotuner's candidates (off by default)
         conv.set_v2_split("v2split" in opt_s.split("+"))
+        # ebk<n>: at most n blocks per BN apply / dx pass (grid baked into the captured graph)
+        ebk = [int(o[3:]) for o in opt_s.split("+") if o.startswith("ebk")]
+        _e.load().bn_set_elem_max_blocks(ebk[0] if ebk else 4096)
         # st1p: conv-epilogue BN statistics in one pass (the launch args bake the switch)
         _e.load().conv_set_stats_one_pass("st1p" in opt_s.split("+"))
         model, opt, x, y = cnn_bench.build(args, dev, 1)
