@@ -1329,8 +1329,10 @@ long long reduce_blocks(long long M, int C, long long* rpb) {
 
 // Grid of the streaming passes (apply, dx): at most g_elem_max_blocks blocks, each thread then
 // loops over its vectors. Every block derives its per-channel coefficients in its prologue (from
-// the fp64 sums: ARENA_ACC_REP replicas x 2 x C loads), so fewer, fatter blocks pay that less often.
-int g_elem_max_blocks = 4096;
+// the fp64 sums: ARENA_ACC_REP replicas x 2 x C loads), so fewer, fatter blocks pay that less
+// often: ResNet-50 step 11.718 / 11.677 / 11.578 / 11.811 ms at 4096 / 2048 / 1024 / 512
+// (profiles/r5_ebk_ab.jsonl, same process).
+int g_elem_max_blocks = 1024;
 
 int elementwise_blocks(long long nvec) {
   long long b = (nvec + 2LL * kT - 1) / (2LL * kT);

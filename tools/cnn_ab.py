@@ -96,7 +96,7 @@ def main():
         conv.set_v2_split("v2split" in opt_s.split("+"))
         # ebk<n>: at most n blocks per BN apply / dx pass (grid baked into the captured graph)
         ebk = [int(o[3:]) for o in opt_s.split("+") if o.startswith("ebk")]
-        _e.load().bn_set_elem_max_blocks(ebk[0] if ebk else 4096)
+        _e.load().bn_set_elem_max_blocks(ebk[0] if ebk else 1024)
         # st1p: conv-epilogue BN statistics in one pass (the launch args bake the switch)
         _e.load().conv_set_stats_one_pass("st1p" in opt_s.split("+"))
         model, opt, x, y = cnn_bench.build(args, dev, 1)
