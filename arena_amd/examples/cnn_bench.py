@@ -49,7 +49,9 @@ def parse(argv=None):
                     help="gradient bucket size (Horovod fusion buffer). 12 MB splits ResNet-50's "
                          "51 MB of bf16 gradients into 5 buckets, so the first buckets' "
                          "collectives run while backward is still producing the rest")
-    ap.add_argument("--comm", choices=["auto", "xgmi", "rccl"], default="auto")
+    ap.add_argument("--comm", choices=["auto", "xgmi", "rccl", "hier"], default="auto",
+                    help="DP gradient path: xgmi kernels (one node), rccl (flat), hier (node-level "
+                         "then inter-node RCCL on 1/local_size of the bytes); auto picks")
     ap.add_argument("--device", default="auto")
     ap.add_argument("--graph", type=int, default=1,
                     help="1: capture the whole training step (fwd, bwd, optimizer) in one hipGraph "
@@ -102,10 +104,10 @@ def build(args, dev, world):
             [{"params": decay, "weight_decay": args.weight_decay},
              {"params": no_decay, "weight_decay": 0.0, "weights": "fp32"}],
             lr=args.learning_rate, momentum=args.momentum, bucket_mb=args.bucket_mb,
-            backend="rccl" if comm == "rccl" else comm, order=list(model.parameters()))
+            backend=comm, order=list(model.parameters()))
         if hvd.rank() == 0 and opt.backend != "xgmi" and comm == "auto":
-            print("[rank 0] ShardedMasterSGD over RCCL (ranks cannot map each other's GPUs)",
-                  file=sys.stderr, flush=True)
+            print(f"[rank 0] ShardedMasterSGD over RCCL, {opt.backend} (ranks cannot map each "
+                  "other's GPUs)", file=sys.stderr, flush=True)
     if opt is not None:
         pass                   # data parallel, sharded
     elif master:

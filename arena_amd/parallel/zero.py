@@ -29,7 +29,14 @@ parameter of the model:
     on the owned equal-size shard, ``all_gather_into_tensor`` of the updated weights. bf16 buckets
     reduce in bf16 by default (the bytes the xGMI path moves); ``rccl_reduce_fp32=True`` reduces
     fp32 copies instead (exact sums, twice the bytes);
-  - ``"auto"``: xgmi when ``xgmi.usable`` and the communicator comes up on every rank, else rccl;
+  - ``backend="hier"`` (several nodes of ``local_size`` ranks each, consecutive ranks per node):
+    the same three steps in two levels -- reduce-scatter inside the node (RCCL rides xGMI there),
+    reduce-scatter of that 1/L chunk between nodes, ``shard_sgd`` on the 1/W shard, all-gather
+    between nodes, all-gather inside the node. Each rank sends 1/L of the bucket over the
+    inter-node network instead of all of it (Horovod's hierarchical allreduce, sharded);
+  - ``"auto"``: xgmi when ``xgmi.usable`` and the communicator comes up on every rank; else hier
+    when the job spans several nodes of more than one rank each (``local_size`` or
+    ``LOCAL_WORLD_SIZE``); else rccl;
 * every rank ends each step with bit-identical weights (``--verify_every`` checks it).
 
 Update timing. With ``overlap=True`` (default) a bucket's update runs during ``backward()`` as
@@ -51,6 +58,7 @@ owns; :meth:`state_dict` reassembles them.
 from __future__ import annotations
 
 import contextlib
+import os
 from typing import Iterable, List, Optional
 
 import torch
@@ -109,7 +117,7 @@ class ShardedMasterSGD:
                  weight_decay: float = 0.0, bucket_mb: float = 16.0, group=None,
                  timeout_s: float = 60.0, overlap: bool = True, backend: str = "auto",
                  order: Optional[Iterable[Tensor]] = None, last_bucket_mb: Optional[float] = None,
-                 rccl_reduce_fp32: bool = False):
+                 rccl_reduce_fp32: bool = False, local_size: Optional[int] = None):
         plist = list(params)
         if plist and isinstance(plist[0], dict):
             raw_groups = plist
@@ -126,8 +134,8 @@ class ShardedMasterSGD:
             raise ValueError("ShardedMasterSGD needs at least one parameter")
         if len({id(p) for p in self.params}) != len(self.params):
             raise ValueError("a parameter appears in more than one param group")
-        if backend not in ("auto", "xgmi", "rccl"):
-            raise ValueError(f"backend must be auto, xgmi or rccl (got {backend!r})")
+        if backend not in ("auto", "xgmi", "rccl", "hier"):
+            raise ValueError(f"backend must be auto, xgmi, rccl or hier (got {backend!r})")
         self.state: dict = {}   # Horovod's broadcast_optimizer_state finds nothing to send: the
         #                         masters are derived from the (already broadcast) weights
         self.group = group
@@ -152,12 +160,19 @@ class ShardedMasterSGD:
                                     f"{p.dtype}")
                 if not (p.is_contiguous() or p.is_contiguous(memory_format=torch.channels_last)):
                     raise ValueError("parameters must be contiguous or channels_last")
-        if dev.type != "cuda" and backend != "rccl":
-            raise ValueError("ShardedMasterSGD on CPU tensors needs backend='rccl' (gloo)")
+        if dev.type != "cuda" and backend == "xgmi":
+            raise ValueError("ShardedMasterSGD on CPU tensors runs over gloo: backend 'rccl', "
+                             "'hier' or 'auto'")
         requested = backend
+        self.local_size = self._local_size(local_size)
         if backend == "auto":
             from . import xgmi
-            backend = "xgmi" if xgmi.usable(group) else "rccl"
+            backend = "xgmi" if dev.type == "cuda" and xgmi.usable(group) else "rccl"
+        if backend == "rccl" and requested == "auto" and 1 < self.local_size < self.world:
+            backend = "hier"
+        self._intra = self._inter = None
+        if backend == "hier":
+            self._make_level_groups()
         self.rccl_reduce_fp32 = bool(rccl_reduce_fp32)
         model_order = self._model_order(order)
         last_mb = bucket_mb / 4 if last_bucket_mb is None else last_bucket_mb
@@ -184,6 +199,8 @@ class ShardedMasterSGD:
             self._rs_out = torch.zeros(self._max_shard_words(), dtype=_F32, device=dev)
             self._rs_wide = (torch.zeros(self._max_range_elems(_BF16), dtype=_F32, device=dev)
                              if self.rccl_reduce_fp32 else None)
+            self._rs_mid = (torch.zeros(self._max_chunk_words(), dtype=_F32, device=dev)
+                            if self._intra is not None else None)
         else:
             buf, wbuf = self.comm.buffer(), self.comm.params()
         self.wbf = wbuf.view(_BF16)[: self.t16]
@@ -269,6 +286,51 @@ class ShardedMasterSGD:
         self.t16, self.t32 = size[_BF16], size[_F32]
         self.f0 = _pad((self.t16 + 1) // 2, 4)            # fp32 region start (floats)
 
+    def _local_size(self, local_size) -> int:
+        """Ranks per node for the hierarchical backend (``LOCAL_WORLD_SIZE`` by default: torchrun
+        numbers a node's ranks consecutively); must divide the world."""
+        if local_size is None:
+            local_size = int(os.environ.get("LOCAL_WORLD_SIZE", self.world))
+        local_size = int(local_size)
+        if local_size < 1 or self.world % local_size:
+            raise ValueError(f"local_size {local_size} must divide the world size {self.world}")
+        return local_size
+
+    def _make_level_groups(self) -> None:
+        """One group per node (its L consecutive ranks) and one per local rank (the same local
+        rank on every node). Collective: every rank creates every group, in the same order."""
+        L, W = self.local_size, self.world
+        if not 1 < L < W:
+            raise ValueError(f"backend='hier' needs 1 < local_size < world (got local_size {L}, "
+                             f"world {W})")
+        granks = (dist.get_process_group_ranks(self.group) if self.group is not None
+                  else list(range(W)))
+        self.nodes = W // L
+        self.node, self.lrank = self.rank // L, self.rank % L
+        for k in range(self.nodes):
+            g = dist.new_group([granks[k * L + l] for l in range(L)])
+            if k == self.node:
+                self._intra = g
+        for l in range(L):
+            g = dist.new_group([granks[k * L + l] for k in range(self.nodes)])
+            if l == self.lrank:
+                self._inter = g
+
+    def _shard_index(self, rank: int) -> int:
+        """Which 1/W slice of every sub-range ``rank`` owns: the flat backend slices in rank
+        order; the hierarchical one gives local rank l the node-level chunk l, of which node k
+        owns slice k."""
+        if self._intra is None:
+            return rank
+        return (rank % self.local_size) * self.nodes + rank // self.local_size
+
+    def _max_chunk_words(self) -> int:
+        """fp32 words of the largest node-level (1/L) reduce-scatter output."""
+        L = self.local_size
+        m16 = self._max_range_elems(_BF16) // L
+        m32 = self._max_range_elems(_F32) // L
+        return max(4, m16 if self.rccl_reduce_fp32 else (m16 + 1) // 2, m32)
+
     def _max_range_elems(self, dtype) -> int:
         return max([r.end - r.start for b in self.buckets for r in b.ranges if r.dtype == dtype]
                    + [0])
@@ -331,11 +393,12 @@ class ShardedMasterSGD:
 
     def _update_rccl(self, r: _Range, lr, mu, wd) -> None:
         """reduce-scatter -> shard_sgd on the owned shard -> all-gather, on the current (comm)
-        stream. Sub-ranges are padded to world x 16-byte slots: equal, aligned shards."""
+        stream. Sub-ranges are padded to world x 16-byte slots: equal, aligned shards. The
+        hierarchical backend does each collective in two levels (node, then between nodes)."""
         from ..ops import fused
         n = r.end - r.start
         sl = n // self.world
-        lo = r.start + self.rank * sl
+        lo = r.start + self._shard_index(self.rank) * sl
         scale = 1.0 / self.world
         if r.dtype == _BF16:
             if self.rccl_reduce_fp32:
@@ -349,22 +412,38 @@ class ShardedMasterSGD:
             fused.shard_sgd(out, self.master[lo:lo + sl], self.mom[lo:lo + sl],
                             self.wbf[lo:lo + sl], lr=lr, momentum=mu, weight_decay=wd,
                             scale=scale)
-            self._all_gather(self.wbf[r.start:r.end], self.wbf[lo:lo + sl])
+            self._all_gather(self.wbf, r.start, n, lo, sl)
         else:
             out = self._rs_out[:sl]
             self._reduce_scatter(out, self.stage32[r.start:r.end])
             fused.shard_sgd(out, self.w32[lo:lo + sl], self.mom32[lo:lo + sl], None, lr=lr,
                             momentum=mu, weight_decay=wd, scale=scale)
-            self._all_gather(self.w32[r.start:r.end], self.w32[lo:lo + sl])
+            self._all_gather(self.w32, r.start, n, lo, sl)
 
     def _reduce_scatter(self, out: Tensor, inp: Tensor) -> None:
-        dist.reduce_scatter_tensor(out, inp, group=self.group)
+        if self._intra is None:
+            dist.reduce_scatter_tensor(out, inp, group=self.group)
+            return
+        # node level: local rank l gets chunk l (summed over the node); then the nodes
+        # reduce-scatter that chunk, node k keeping slice k of it
+        mid = self._rs_mid.view(inp.dtype)[: inp.numel() // self.local_size]
+        dist.reduce_scatter_tensor(mid, inp, group=self._intra)
+        dist.reduce_scatter_tensor(out, mid, group=self._inter)
 
-    def _all_gather(self, out: Tensor, mine: Tensor) -> None:
-        # in place on RCCL (the send buffer is this rank's slot of the receive buffer); gloo
-        # gets a copy
-        dist.all_gather_into_tensor(out, mine.clone() if out.device.type == "cpu" else mine,
-                                    group=self.group)
+    def _all_gather(self, flat: Tensor, start: int, n: int, lo: int, sl: int) -> None:
+        """Every rank's updated slice [lo, lo + sl) into ``flat[start:start + n]``."""
+        def gather(out, mine, group):
+            # in place on RCCL (the send buffer is this rank's slot of the receive buffer);
+            # gloo gets a copy
+            dist.all_gather_into_tensor(out, mine.clone() if out.device.type == "cpu" else mine,
+                                        group=group)
+        if self._intra is None:
+            gather(flat[start:start + n], flat[lo:lo + sl], self.group)
+            return
+        chunk = n // self.local_size
+        c0 = start + self.lrank * chunk
+        gather(flat[c0:c0 + chunk], flat[lo:lo + sl], self._inter)
+        gather(flat[start:start + n], flat[c0:c0 + chunk], self._intra)
 
     def _on_grad(self, p) -> None:
         if self._no_sync:
@@ -435,7 +514,8 @@ class ShardedMasterSGD:
                 n = rg.end - rg.start
                 if self.comm is None:
                     sl = n // self.world
-                    out.append((rg.start + r * sl, rg.start + (r + 1) * sl))
+                    s = self._shard_index(r)
+                    out.append((rg.start + s * sl, rg.start + (s + 1) * sl))
                 elif dtype == _BF16:
                     out.append(tuple(self.comm.ext.ccl_sgd_shard(rg.start, n, self.world, r)))
                 else:

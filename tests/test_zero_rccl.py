@@ -51,7 +51,7 @@ def _grads(step, rank, params):
     return out
 
 
-def _worker(rank, world, port, reduce_fp32, q):
+def _worker(rank, world, port, reduce_fp32, q, backend="rccl", local_size=None):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                           WORLD_SIZE=str(world))
@@ -71,8 +71,11 @@ def _worker(rank, world, port, reduce_fp32, q):
                                 {"params": [p for p, k in params if k == "fp32"],
                                  "weight_decay": 0.0, "weights": "fp32"}],
                                lr=lr, momentum=mu, bucket_mb=0.004, last_bucket_mb=0.001,
-                               backend="rccl", order=order, rccl_reduce_fp32=reduce_fp32)
+                               backend=backend, order=order, rccl_reduce_fp32=reduce_fp32,
+                               local_size=local_size)
         res = {"backend": opt.backend, "nbuckets": len(opt.buckets),
+               "shards": {str(dt): [opt.shard_ranges(r, dt) for r in range(world)]
+                          for dt in (torch.bfloat16, torch.float32)},
                "mixed": sum(1 for b in opt.buckets if len(b.ranges) == 2)}
         # layout: each sub-range splits into equal 16-byte-aligned shards
         res["padded"] = all((r.end - r.start) % (world * (8 if r.dtype == torch.bfloat16 else 4))
@@ -120,11 +123,12 @@ def _worker(rank, world, port, reduce_fp32, q):
         q.put((rank, None, traceback.format_exc()))
 
 
-def _run(world, reduce_fp32):
+def _run(world, reduce_fp32, backend="rccl", local_size=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, reduce_fp32, q))
+    procs = [ctx.Process(target=_worker, args=(r, world, port, reduce_fp32, q, backend,
+                                                local_size))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -156,3 +160,45 @@ def test_rccl_sharded_sgd_matches_torch_sgd(world, reduce_fp32):
         assert res["master_rel"] < tol, (r, res)
         assert res["w_vs_master"] == 0.0, (r, res)
     assert len({res["digest"] for res in out.values()}) == 1, out     # replicas identical
+
+
+def _check_shards_partition(res, world):
+    """Every sub-range's W shards are disjoint, equal and cover it exactly."""
+    for dt, per_rank in res["shards"].items():
+        for j in range(len(per_rank[0])):
+            spans = sorted(per_rank[r][j] for r in range(world))
+            for (a, b), (c, _) in zip(spans, spans[1:]):
+                assert b == c, (dt, j, spans)
+            assert len({b - a for a, b in spans}) == 1, (dt, j, spans)
+
+
+@pytest.mark.parametrize("world,local_size", [(4, 2), (6, 2)])
+@pytest.mark.parametrize("reduce_fp32", [True, False])
+def test_hier_sharded_sgd_matches_torch_sgd(world, local_size, reduce_fp32):
+    """Hierarchical backend (Horovod's hierarchical allreduce, sharded): node-level
+    reduce-scatter, then between nodes on the 1/L chunk; shard update; all-gathers in reverse.
+    Here 2 and 3 'nodes' of 2 ranks each on gloo."""
+    out = _run(world, reduce_fp32, backend="hier", local_size=local_size)
+    for r, res in out.items():
+        assert res["backend"] == "hier" and res["padded"], res
+        _check_shards_partition(res, world)
+        tol = 1e-5 if reduce_fp32 else 2e-2
+        assert res["master_rel"] < tol, (r, res)
+        assert res["w_vs_master"] == 0.0, (r, res)
+    assert len({res["digest"] for res in out.values()}) == 1, out
+    # the hierarchical slice order differs from the flat one: local rank l, node k owns
+    # slice l * nodes + k
+    nodes = world // local_size
+    sh = out[0]["shards"][str(torch.bfloat16)]
+    base = sh[0][0][0]
+    sl = sh[0][0][1] - base
+    for r in range(world):
+        assert sh[r][0][0] == base + ((r % local_size) * nodes + r // local_size) * sl
+
+
+def test_auto_picks_hier_across_nodes():
+    """auto -> hier when the job spans several nodes of more than one rank each (ranks that
+    cannot map each other); an explicit rccl stays flat; one node -> flat rccl."""
+    assert all(res["backend"] == "hier" for res in _run(4, False, "auto", 2).values())
+    assert all(res["backend"] == "rccl" for res in _run(4, False, "rccl", 2).values())
+    assert all(res["backend"] == "rccl" for res in _run(2, False, "auto", 2).values())
