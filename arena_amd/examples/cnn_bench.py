@@ -286,7 +286,7 @@ def main(argv=None) -> int:
         from ..ops import conv
         for key, plan in conv.plans().items():
             print(f"conv {key[0]} w{key[1]} s{key[2]} p{key[3]}: fwd={plan.fwd} bwd={plan.bwd} "
-                  f"wgrad={plan.wgrad} {plan.times}", file=sys.stderr)
+                  f"bwd_bn={plan.bwd_bn} link={plan.link} wgrad={plan.wgrad} {plan.times}", file=sys.stderr)
     hvd.shutdown()
     return 0
 

@@ -28,6 +28,7 @@ Semantics match ``nn.BatchNorm2d`` in training and eval mode:
 """
 from __future__ import annotations
 
+import os
 from typing import Optional
 
 import torch
@@ -373,14 +374,25 @@ def set_stem_pool_fused(on: bool) -> None:
     _STEM_POOL_FUSED = bool(on)
 
 
+# The forward also saves x at each window's argmax (pooled size): the backward's sums then come
+# from (dy, xsel), two pooled-size streams, instead of x (4x larger) plus the argmax gather
+# (ARENA_STEM_XSEL=0: the per-pixel reduction over x).
+_STEM_XSEL = os.environ.get("ARENA_STEM_XSEL", "1") == "1"
+
+
+def set_stem_xsel(on: bool) -> None:
+    global _STEM_XSEL
+    _STEM_XSEL = bool(on)
+
+
 class _BNPoolFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, num_batches,
                 fin, part, rpb, bacc, k, s, p):
-        y, pos, mean, invstd, scale, shift = _ext.load().bn_pool_fwd(
+        y, pos, mean, invstd, scale, shift, xsel = _ext.load().bn_pool_fwd(
             x, weight, bias, running_mean, running_var, momentum, eps, num_batches, fin, part,
-            rpb, k, s, p, bacc.take_zero())
-        ctx.save_for_backward(x, pos, mean, invstd, scale, shift, weight)
+            rpb, k, s, p, bacc.take_zero(), _STEM_XSEL)
+        ctx.save_for_backward(x, pos, mean, invstd, scale, shift, weight, xsel)
         ctx.fin, ctx.bacc, ctx.geom = fin, bacc, (k, s, p)
         ctx.affine = weight is not None
         ctx.mark_non_differentiable(pos)
@@ -388,11 +400,11 @@ class _BNPoolFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x, pos, mean, invstd, scale, shift, weight = ctx.saved_tensors
+        x, pos, mean, invstd, scale, shift, weight, xsel = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx, dgamma, dbeta = _ext.load().bn_pool_bwd(
             dy, pos, x, mean, invstd, scale, shift, weight, ctx.affine, *ctx.geom,
-            ctx.bacc.for_backward(x, x.shape[1]), ctx.fin)
+            ctx.bacc.for_backward(x, x.shape[1]), ctx.fin, xsel)
         return (dx, dgamma if ctx.affine else None, dbeta if ctx.affine else None, None, None,
                 None, None, None, None, None, None, None, None, None, None)
 

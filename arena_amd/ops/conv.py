@@ -333,6 +333,35 @@ _ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_ACC_MAX_PAIRS", str(4 << 20)))
 _LINK_ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_LINK_ACC_MAX_PAIRS", str(_ACC_MAX_PAIRS)))
 
 
+# ARENA_BN_LINK_CHOICE=1: per layer, the tuner prices the link -- the linked dgrad's extra
+# epilogue time against the BN backward's own reduction pass over (dy, x) (``_bn_reduce_us``) --
+# and links only where the epilogue is cheaper. Measured, off: the reduction pass costs more than
+# the epilogue on all but one ResNet-50 layer (256-channel input @56: 57 us of epilogue vs a 93 us
+# pass), the one it unlinked (1024 ch @14, 17.1 vs 16.2 us) made the step slower, 11.947 vs 11.869
+# ms (profiles/r5_link_ab.jsonl, interleaved replays).
+_LINK_CHOICE = os.environ.get("ARENA_BN_LINK_CHOICE", "0") == "1"
+
+
+def set_link_choice(on: bool) -> None:
+    global _LINK_CHOICE
+    _LINK_CHOICE = bool(on)
+
+
+def _bn_reduce_us(x: Tensor, mask: Tensor, mean: Tensor) -> float:
+    """GPU time of the BN backward's reduction pass for an input of ``x``'s shape: the fused
+    backward with its own reduction minus the same backward fed ready sums (a linked conv's)."""
+    from .batchnorm import acc_rep
+    ext = _ext.load()
+    c = x.shape[1]
+    ones = torch.ones(c, device=x.device)
+    acc = torch.zeros(acc_rep() * 2 * c, dtype=torch.float64, device=x.device)
+    dy = torch.randn_like(x)
+    own = _time(lambda: ext.bn_bwd(dy, mask, x, mean, ones, ones, True, False, True, acc_b=acc))
+    fed = _time(lambda: ext.bn_bwd(dy, mask, x, mean, ones, ones, True, False, True, acc_b=acc,
+                                   acc_ready=True))
+    return max(0.0, own - fed)
+
+
 def set_link_acc_max_pairs(n: int) -> None:
     global _LINK_ACC_MAX_PAIRS
     _LINK_ACC_MAX_PAIRS = int(n)
@@ -720,6 +749,9 @@ class ConvPlan:
     fwd_fold: object = MIOPEN
     wgrad_fold: object = MIOPEN
     bwd_bn_fold: object = MIOPEN
+    # whether the backward-data pass takes the BN-backward sums at all (BNGradLink): False where
+    # the tuner found the BN's own reduction pass cheaper than the linked epilogue
+    link: bool = True
     tuned: bool = False
     times: Dict[str, float] = field(default_factory=dict)
 
@@ -830,7 +862,7 @@ def _best(t: dict, kind: str, n: int):
 
 def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
     key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _PERSIST_ON,
-           _V2_ON, _BN_LINKS, _BN_FOLD, _V2_SPLIT_ON)
+           _V2_ON, _BN_LINKS, _BN_FOLD, _V2_SPLIT_ON, _LINK_CHOICE)
     plan = _PLANS.get(key)
     if plan is not None and (plan.tuned or torch.cuda.is_current_stream_capturing()):
         return plan
@@ -994,6 +1026,8 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                         reps[key_].append(fns[key_]())
                 for key_, vs in reps.items():
                     t[key_] = sorted(vs)[1]
+                if _LINK_CHOICE and "bwdbn" in kinds and "bwd" in kinds:
+                    t[("reduce", "bn")] = _bn_reduce_us(bnx, bmask, bmean)
             finally:
                 ext.bn_acc_scratch(False)
             out = {}
@@ -1003,12 +1037,17 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                 best = min(t[(kind, c)] for c in finals[kind])
                 choice = next(c for c in finals[kind] if t[(kind, c)] == best)
                 out[names.get(kind, kind)] = choice
+            if ("reduce", "bn") in t:
+                linked = t[("bwdbn", out["bwd_bn"])]
+                plain = t[("bwd", out["bwd"])] + t[("reduce", "bn")]
+                out["link"] = bool(linked <= plain)
             out["times"] = {f"{kd}:{c}": round(v, 1) for (kd, c), v in t.items()}
             return out
 
         # one decision per job: rank 0 times, every rank adopts (or the ARENA_CONV_PLAN file)
         got = planstore.decide("conv", key[:4] + key[5:], x.device, tune)
-        for f in ("fwd", "bwd", "wgrad", "bwd_bn", "fwd_fold", "wgrad_fold", "bwd_bn_fold"):
+        for f in ("fwd", "bwd", "wgrad", "bwd_bn", "fwd_fold", "wgrad_fold", "bwd_bn_fold",
+                  "link"):
             if f in got:
                 v = got[f]
                 setattr(plan, f, tuple(v) if isinstance(v, list) else v)
@@ -1239,6 +1278,7 @@ class _ConvFn(torch.autograd.Function):
             lk = ctx.bn_link
             # the BN partials need the COMPLETE gradient of x: not from a join's first arriver
             use_bn = (lk is not None and plan.bwd != MIOPEN and stride == 1
+                      and (plan.link or lk.coef is not None)
                       and lk.x.shape == x.shape
                       and (join is None or other is not None)
                       and (lk.coef is None or plan.bwd_bn_fold != MIOPEN))

@@ -118,11 +118,12 @@ hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, vo
 hipError_t arena_bn_fold_fwd(long long, int, const double*, float*, int, long long, double*,
                              unsigned*, ArenaBNStats, double*, int, hipStream_t);
 int arena_bn_acc_ok(long long, int);
-hipError_t arena_bn_pool_fwd(int, const void*, void*, uint8_t*, int, int, int, int, int, int, int,
-                             ArenaBNStats, const double*, const float*, int, long long, double*,
-                             unsigned*, double*, int, hipStream_t);
-hipError_t arena_bn_pool_bwd(int, const void*, const uint8_t*, const void*, void*, int, int, int,
-                             int, int, int, int, ArenaBNBwd, double*, double*, int, hipStream_t);
+hipError_t arena_bn_pool_fwd(int, const void*, void*, uint8_t*, void*, int, int, int, int, int, int,
+                             int, ArenaBNStats, const double*, const float*, int, long long,
+                             double*, unsigned*, double*, int, hipStream_t);
+hipError_t arena_bn_pool_bwd(int, const void*, const uint8_t*, const void*, const void*, void*, int,
+                             int, int, int, int, int, int, ArenaBNBwd, double*, double*, int,
+                             hipStream_t);
 #ifdef ARENA_TIMELINE
 hipError_t arena_timeline_read(long long*, int);
 #endif
@@ -1212,13 +1213,14 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
 // Fused stem BatchNorm + ReLU + k x k / s max pool (training; bn_kernels.hip arena_bn_pool_fwd):
 // x is the BN input with its statistics from the producing conv: summed (fin, fp64 [2][C]) or as
 // per-tile partials (stats_part, stats_rpb rows per partial; fin then empty).
-// Returns (y, pos, mean, invstd, scale, shift): the pooled output, its uint8 in-window argmax,
-// and the saved statistics. fin stays in place until bn_pool_bwd(zero_f=fin) zeroes it; zero_b:
-// as in bn_fwd.
+// Returns (y, pos, mean, invstd, scale, shift, xsel): the pooled output, its uint8 in-window
+// argmax, the saved statistics, and (with_xsel; else empty) x at each window's argmax, from which
+// the backward takes its sums. fin stays in place until bn_pool_bwd(zero_f=fin) zeroes it;
+// zero_b: as in bn_fwd.
 std::vector<Tensor> bn_pool_fwd(Tensor x, OptT gamma, OptT beta, OptT running_mean,
                                 OptT running_var, double momentum, double eps, OptT num_batches,
                                 OptT fin, OptT stats_part, int64_t stats_rpb, int64_t k, int64_t s,
-                                int64_t p, OptT zero_b) {
+                                int64_t p, OptT zero_b, bool with_xsel) {
   const BNGeom g = bn_geom(x, "x");
   TORCH_CHECK(fin.has_value() != stats_part.has_value(),
               "bn_pool_fwd: give the statistics as fin sums or as stats_part partials");
@@ -1267,6 +1269,7 @@ std::vector<Tensor> bn_pool_fwd(Tensor x, OptT gamma, OptT beta, OptT running_me
   TORCH_CHECK(OH > 0 && OW > 0, "bn_pool_fwd: bad pool geometry");
   Tensor y = torch::empty({N, g.C, OH, OW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor pos = torch::empty({N * OH * OW * g.C}, x.options().dtype(torch::kUInt8));
+  Tensor xsel = with_xsel ? torch::empty_like(y) : Tensor();
   double* zb = nullptr;
   int nzb = 0;
   if (zero_b.has_value()) {
@@ -1276,23 +1279,26 @@ std::vector<Tensor> bn_pool_fwd(Tensor x, OptT gamma, OptT beta, OptT running_me
     zb = zero_b->data_ptr<double>();
     nzb = (int)zero_b->numel();
   }
-  check_hip(arena_bn_pool_fwd(g.dtype, x.data_ptr(), y.data_ptr(), pos.data_ptr<uint8_t>(), (int)N,
-                              (int)H, (int)W, (int)g.C, (int)k, (int)s, (int)p, st,
+  check_hip(arena_bn_pool_fwd(g.dtype, x.data_ptr(), y.data_ptr(), pos.data_ptr<uint8_t>(),
+                              with_xsel ? xsel.data_ptr() : nullptr, (int)N, (int)H, (int)W,
+                              (int)g.C, (int)k, (int)s, (int)p, st,
                               fin.has_value() ? fin->data_ptr<double>() : nullptr,
                               stats_part.has_value() ? stats_part->data_ptr<float>() : nullptr,
                               ext_nblk, (long long)stats_rpb,
                               lvl2.defined() ? lvl2.data_ptr<double>() : nullptr, tickets, zb, nzb,
                               cur_stream()),
             "bn_pool_fwd");
-  return {y, pos, mean, invstd, scale, shift};
+  return {y, pos, mean, invstd, scale, shift, xsel};
 }
 
 // Backward of bn_pool_fwd: returns (dx, dgamma or empty, dbeta or empty). acc_b: the layer's own
 // fp64 [2, C] backward sums (zero on entry, left for the next forward's zero_b); zero_f: the
-// forward's fin, zeroed by the dx pass.
+// forward's fin, zeroed by the dx pass; xsel: the forward's selected inputs (the reduction then
+// reads them and dy instead of x).
 std::vector<Tensor> bn_pool_bwd(Tensor dy, Tensor pos, Tensor x, Tensor mean, Tensor invstd,
                                 Tensor scale, Tensor shift, OptT gamma, bool affine_grads,
-                                int64_t k, int64_t s, int64_t p, Tensor acc_b, OptT zero_f) {
+                                int64_t k, int64_t s, int64_t p, Tensor acc_b, OptT zero_f,
+                                OptT xsel) {
   const BNGeom g = bn_geom(x, "x");
   for (const Tensor* t : {&mean, &invstd, &scale, &shift}) {
     check_f32(*t, "saved statistics");
@@ -1303,6 +1309,12 @@ std::vector<Tensor> bn_pool_bwd(Tensor dy, Tensor pos, Tensor x, Tensor mean, Te
               "bn_pool_bwd: dy must be a channels_last tensor like the pooled output");
   TORCH_CHECK(pos.scalar_type() == torch::kUInt8 && pos.numel() == dy.numel() && pos.is_contiguous(),
               "bn_pool_bwd: pos must be the forward's argmax bytes");
+  const bool has_xsel = xsel.has_value() && xsel->defined();
+  if (has_xsel)
+    TORCH_CHECK(xsel->is_cuda() && xsel->device() == x.device() &&
+                    xsel->scalar_type() == x.scalar_type() && xsel->sizes() == dy.sizes() &&
+                    xsel->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "bn_pool_bwd: xsel must be the forward's selected inputs (dy's shape and layout)");
   TORCH_CHECK(acc_b.is_cuda() && acc_b.device() == x.device() &&
                   acc_b.scalar_type() == torch::kFloat64 && acc_b.is_contiguous() &&
                   acc_b.numel() == kRep * 2 * g.C,
@@ -1332,7 +1344,7 @@ std::vector<Tensor> bn_pool_bwd(Tensor dy, Tensor pos, Tensor x, Tensor mean, Te
   }
   Tensor dx = torch::empty_like(x);
   check_hip(arena_bn_pool_bwd(g.dtype, dy.data_ptr(), pos.data_ptr<uint8_t>(), x.data_ptr(),
-                              dx.data_ptr(), (int)x.size(0), (int)x.size(2), (int)x.size(3),
+                              has_xsel ? xsel->data_ptr() : nullptr, dx.data_ptr(), (int)x.size(0), (int)x.size(2), (int)x.size(3),
                               (int)g.C, (int)k, (int)s, (int)p, b, acc_b.data_ptr<double>(), zf,
                               nzf, cur_stream()),
             "bn_pool_bwd");

@@ -862,6 +862,7 @@ template <typename T, bool FIN>
 __global__ __launch_bounds__(kT) void bn_pool_fwd_kernel(const T* __restrict__ x,
                                                          T* __restrict__ y,
                                                          uint8_t* __restrict__ pos,
+                                                         T* __restrict__ xsel,
                                                          ArenaBNStats st,
                                                          const double* __restrict__ fin,
                                                          long long M, PoolG g,
@@ -881,10 +882,10 @@ __global__ __launch_bounds__(kT) void bn_pool_fwd_kernel(const T* __restrict__ x
   const int n32 = row / g.OH, oh = row - n32 * g.OH;
   const long long n = n32;
   const int h0 = oh * g.s - g.p, w0 = ow * g.s - g.p;
-  float m[kVec];
+  float m[kVec], xb[kVec];
   int best[kVec];
 #pragma unroll
-  for (int i = 0; i < kVec; ++i) { m[i] = -INFINITY; best[i] = -1; }
+  for (int i = 0; i < kVec; ++i) { m[i] = -INFINITY; best[i] = -1; xb[i] = 0.f; }
   for (int kh = 0; kh < g.k; ++kh) {
     const int h = h0 + kh;
     if (h < 0 || h >= g.H) continue;
@@ -897,7 +898,7 @@ __global__ __launch_bounds__(kT) void bn_pool_fwd_kernel(const T* __restrict__ x
 #pragma unroll
       for (int i = 0; i < kVec; ++i) {
         const float v = stored_val<T>(fmaxf(fmaf(a[i] - mu[i], sc[i], sh[i]), 0.f));
-        if (v > m[i] || __builtin_isnan(v) || best[i] < 0) { m[i] = v; best[i] = q; }
+        if (v > m[i] || __builtin_isnan(v) || best[i] < 0) { m[i] = v; best[i] = q; xb[i] = a[i]; }
       }
     }
   }
@@ -909,6 +910,7 @@ __global__ __launch_bounds__(kT) void bn_pool_fwd_kernel(const T* __restrict__ x
   pk.y = (uint32_t)(best[4] & 0xff) | ((uint32_t)(best[5] & 0xff) << 8) |
          ((uint32_t)(best[6] & 0xff) << 16) | ((uint32_t)(best[7] & 0xff) << 24);
   *reinterpret_cast<uint2*>(pos + v * kVec) = pk;
+  if (xsel != nullptr) V8<T>::store(xsel + v * kVec, xb);   // x at the argmax (exact: x is T)
 }
 
 // The pool's gradient at input pixel r (row-major n, h, w), channels 8 c8 .. 8 c8 + 7: the sum of
@@ -1199,6 +1201,78 @@ __global__ __launch_bounds__(kT) void bn_pool_bwd_reduce_q_kernel(const T* __res
           const float gg = on ? gq.g[px][e] : 0.f;
           sg[e] += gg;
           sgx[e] = fmaf(gg, v[e] - mu[e], sgx[e]);
+        }
+      }
+    }
+  }
+  __shared__ float s_g[kT * kVec], s_gx[kT * kVec];
+  if (q.slot < q.rip) {
+#pragma unroll
+    for (int e = 0; e < kVec; ++e) {
+      s_g[q.slot * q.cw + q.gl * kVec + e] = sg[e];
+      s_gx[q.slot * q.cw + q.gl * kVec + e] = sgx[e];
+    }
+  }
+  __syncthreads();
+  for (int cl = threadIdx.x; cl < q.cw; cl += kT) {
+    float a = 0.f, b = 0.f;
+    for (int s2 = 0; s2 < q.rip; ++s2) {
+      a += s_g[s2 * q.cw + cl];
+      b += s_gx[s2 * q.cw + cl];
+    }
+    unsafeAtomicAdd(acc + q.cb + cl, (double)a);
+    unsafeAtomicAdd(acc + C + q.cb + cl, (double)b);
+  }
+}
+
+// Backward reduction from the forward's selected inputs. Window o's gradient reaches only its
+// argmax pixel, whose x the forward saved as xsel[o] (and whose ReLU bit follows from it), so
+//   sum g = sum_o dy[o] on(xsel[o]),   sum g (x - mean) = sum_o dy[o] on(xsel[o]) (xsel[o] - mean)
+// -- the per-pixel sums of bn_pool_bwd_reduce_q_kernel regrouped by window: two pooled-size
+// streams (dy, xsel) instead of x (4x the pooled size) plus the argmax gather. Rows: pooled pixels.
+template <typename T>
+__global__ __launch_bounds__(kT) void bn_pool_bwd_reduce_sel_kernel(const T* __restrict__ dy,
+                                                                    const T* __restrict__ xsel,
+                                                                    long long MO, long long rpb,
+                                                                    int C, ArenaBNBwd co,
+                                                                    double* __restrict__ acc) {
+  __shared__ __attribute__((aligned(16))) float s_c[3 * 256];
+  for (int c = threadIdx.x; c < C; c += kT) {
+    s_c[c] = co.mean[c];
+    s_c[C + c] = co.scale[c];
+    s_c[2 * C + c] = co.shift[c];
+  }
+  __syncthreads();
+  const Geo q = geo(C);
+  long long r0, r1;
+  block_rows(MO, rpb, &r0, &r1);
+  float sg[kVec], sgx[kVec], mu[kVec], sc[kVec], sh[kVec];
+#pragma unroll
+  for (int e = 0; e < kVec; ++e) sg[e] = sgx[e] = 0.f;
+  lds8(s_c + q.g * kVec, mu);
+  lds8(s_c + C + q.g * kVec, sc);
+  lds8(s_c + 2 * C + q.g * kVec, sh);
+  if (q.slot < q.rip) {
+    constexpr int U = 4;   // rows in flight per thread
+    for (long long r = r0 + q.slot; r < r1; r += U * q.rip) {
+      float d[U][kVec], v[U][kVec];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const long long ru = r + u * q.rip;
+        const long long rc = ru < r1 ? ru : r;   // clamped: branch-free loads
+        V8<T>::load(dy + rc * C + (long long)q.g * kVec, d[u]);
+        V8<T>::load(xsel + rc * C + (long long)q.g * kVec, v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const bool row_ok = r + u * q.rip < r1;
+#pragma unroll
+        for (int e = 0; e < kVec; ++e) {
+          const bool on = row_ok &&
+                          stored_val<T>(fmaxf(fmaf(v[u][e] - mu[e], sc[e], sh[e]), 0.f)) > 0.f;
+          const float gg = on ? d[u][e] : 0.f;
+          sg[e] += gg;
+          sgx[e] = fmaf(gg, v[u][e] - mu[e], sgx[e]);
         }
       }
     }
@@ -1583,7 +1657,8 @@ hipError_t arena_bn_fold_fwd(long long M, int C, const double* fin, float* part,
 // `part` [ext_nblk][2][C] (ext_rpb rows each), merged first by the finalize kernel (lvl2 /
 // tickets as in arena_bn_fwd). Only the 3x3 / 2 style pools whose inputs have <= 2 x 2 candidate
 // windows, C % 8 == 0, C <= 256. zero / nzero: see arena_bn_fwd.
-hipError_t arena_bn_pool_fwd(int dtype, const void* x, void* y, uint8_t* pos, int N, int H, int W,
+hipError_t arena_bn_pool_fwd(int dtype, const void* x, void* y, uint8_t* pos, void* xsel, int N,
+                             int H, int W,
                              int C, int k, int s, int p, ArenaBNStats st, const double* fin,
                              const float* part, int ext_nblk, long long ext_rpb, double* lvl2,
                              unsigned* tickets, double* zero, int nzero, hipStream_t stream) {
@@ -1602,8 +1677,8 @@ hipError_t arena_bn_pool_fwd(int dtype, const void* x, void* y, uint8_t* pos, in
   const dim3 grid((unsigned)(N * g.OH), (unsigned)((g.OW * cg + kT - 1) / kT));
 #define ARENA_BN_POOL(TT, F)                                                                   \
   hipLaunchKernelGGL((bn_pool_fwd_kernel<TT, F>), grid, dim3(kT), 3 * C * 4, stream,          \
-                     static_cast<const TT*>(x), static_cast<TT*>(y), pos, st, fin, M, g, zero, \
-                     nzero)
+                     static_cast<const TT*>(x), static_cast<TT*>(y), pos,                     \
+                     static_cast<TT*>(xsel), st, fin, M, g, zero, nzero)
   if (dtype == 1) {
     if (fin) ARENA_BN_POOL(uint16_t, true); else ARENA_BN_POOL(uint16_t, false);
   } else {
@@ -1617,9 +1692,10 @@ hipError_t arena_bn_pool_fwd(int dtype, const void* x, void* y, uint8_t* pos, in
 // reduction adds into acc (fp64 [2][C], zero on entry: the layer's own backward set, left in
 // place for its next forward to zero) and the dx pass derives its coefficients from it.
 // co.scale / co.shift: the forward's (ReLU mask recomputed from x). zero / nzero: see arena_bn_bwd.
-hipError_t arena_bn_pool_bwd(int dtype, const void* dy, const uint8_t* pos, const void* x, void* dx,
-                             int N, int H, int W, int C, int k, int s, int p, ArenaBNBwd co,
-                             double* acc, double* zero, int nzero, hipStream_t stream) {
+hipError_t arena_bn_pool_bwd(int dtype, const void* dy, const uint8_t* pos, const void* x,
+                             const void* xsel, void* dx, int N, int H, int W, int C, int k, int s,
+                             int p, ArenaBNBwd co, double* acc, double* zero, int nzero,
+                             hipStream_t stream) {
   PoolG g{N, H, W, C, (H + 2 * p - k) / s + 1, (W + 2 * p - k) / s + 1, k, s, p};
   const long long M = (long long)N * H * W;
   if (bad_shape(M, C) || C > 256 || M >= (1LL << 31) || acc == nullptr || co.scale == nullptr ||
@@ -1635,6 +1711,19 @@ hipError_t arena_bn_pool_bwd(int dtype, const void* dy, const uint8_t* pos, cons
   const long long nvec = M * (C / kVec);
   long long ne = (nvec + kT - 1) / kT;
   ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);
+  if (xsel != nullptr) {   // the sums from the forward's selected inputs (pooled-size streams)
+    const long long MO = (long long)N * g.OH * g.OW;
+    long long orpb;
+    const long long onb = reduce_blocks(MO, C, &orpb);
+    if (dtype == 1)
+      hipLaunchKernelGGL(bn_pool_bwd_reduce_sel_kernel<uint16_t>, dim3(onb, 1), dim3(kT), 0,
+                         stream, static_cast<const uint16_t*>(dy),
+                         static_cast<const uint16_t*>(xsel), MO, orpb, C, co, acc);
+    else
+      hipLaunchKernelGGL(bn_pool_bwd_reduce_sel_kernel<float>, dim3(onb, 1), dim3(kT), 0, stream,
+                         static_cast<const float*>(dy), static_cast<const float*>(xsel), MO, orpb,
+                         C, co, acc);
+  }
   if (k == 3 && s == 2 && p == 1) {   // the ResNet stem pool: 2x2 input quads per gather
     const long long NQ = (long long)N * ((H + 1) / 2) * ((W + 1) / 2);
     g_max_reduce_blocks = saved_max * g_pool_quad_mult;
@@ -1645,9 +1734,10 @@ hipError_t arena_bn_pool_bwd(int dtype, const void* dy, const uint8_t* pos, cons
     long long qne = (nqv + kT - 1) / kT;
     qne = qne < 1 ? 1 : (qne > 4096 ? 4096 : qne);
 #define ARENA_BN_POOL_Q(TT)                                                                     \
-    hipLaunchKernelGGL(bn_pool_bwd_reduce_q_kernel<TT>, dim3(qnb, 1), dim3(kT), 0, stream,     \
-                       static_cast<const TT*>(dy), pos, static_cast<const TT*>(x), NQ, qrpb, g, \
-                       co, acc);                                                                \
+    if (xsel == nullptr)                                                                        \
+      hipLaunchKernelGGL(bn_pool_bwd_reduce_q_kernel<TT>, dim3(qnb, 1), dim3(kT), 0, stream,   \
+                         static_cast<const TT*>(dy), pos, static_cast<const TT*>(x), NQ, qrpb, \
+                         g, co, acc);                                                           \
     hipLaunchKernelGGL(bn_pool_bwd_dx_q_kernel<TT>, dim3(qne), dim3(kT), 6 * C * 4, stream,    \
                        static_cast<const TT*>(dy), pos, static_cast<const TT*>(x),              \
                        static_cast<TT*>(dx), nqv, g, co, acc, M, zero, nzero)
@@ -1656,16 +1746,18 @@ hipError_t arena_bn_pool_bwd(int dtype, const void* dy, const uint8_t* pos, cons
     return hipGetLastError();
   }
   if (dtype == 1) {
-    hipLaunchKernelGGL(bn_pool_bwd_reduce_kernel<uint16_t>, dim3(nb, 1), dim3(kT), 0, stream,
-                       static_cast<const uint16_t*>(dy), pos, static_cast<const uint16_t*>(x), M,
-                       rpb, g, co, acc);
+    if (xsel == nullptr)
+      hipLaunchKernelGGL(bn_pool_bwd_reduce_kernel<uint16_t>, dim3(nb, 1), dim3(kT), 0, stream,
+                         static_cast<const uint16_t*>(dy), pos, static_cast<const uint16_t*>(x),
+                         M, rpb, g, co, acc);
     hipLaunchKernelGGL(bn_pool_bwd_dx_kernel<uint16_t>, dim3(ne), dim3(kT), 6 * C * 4, stream,
                        static_cast<const uint16_t*>(dy), pos, static_cast<const uint16_t*>(x),
                        static_cast<uint16_t*>(dx), nvec, g, co, acc, M, zero, nzero);
   } else {
-    hipLaunchKernelGGL(bn_pool_bwd_reduce_kernel<float>, dim3(nb, 1), dim3(kT), 0, stream,
-                       static_cast<const float*>(dy), pos, static_cast<const float*>(x), M, rpb,
-                       g, co, acc);
+    if (xsel == nullptr)
+      hipLaunchKernelGGL(bn_pool_bwd_reduce_kernel<float>, dim3(nb, 1), dim3(kT), 0, stream,
+                         static_cast<const float*>(dy), pos, static_cast<const float*>(x), M, rpb,
+                         g, co, acc);
     hipLaunchKernelGGL(bn_pool_bwd_dx_kernel<float>, dim3(ne), dim3(kT), 6 * C * 4, stream,
                        static_cast<const float*>(dy), pos, static_cast<const float*>(x),
                        static_cast<float*>(dx), nvec, g, co, acc, M, zero, nzero);

@@ -266,13 +266,16 @@ def test_bn_accumulators_rezeroed_across_steps(C):
 
 @pytest.mark.parametrize("dtype,partials,pad", [(torch.bfloat16, False, 1), (torch.float32, False, 1),
                                                 (torch.bfloat16, True, 1), (torch.bfloat16, False, 0)])
-def test_bn_relu_maxpool_fused_matches_modules(dtype, partials, pad):
+@pytest.mark.parametrize("xsel", [True, False])
+def test_bn_relu_maxpool_fused_matches_modules(dtype, partials, pad, xsel):
     """The fused stem (BN + ReLU + 3x3/2 max pool, statistics summed by the conv epilogue):
     pooled output bit-identical to BatchNormAct2d + MaxPool2dNHWC, same running statistics,
     gradients equal to rounding (the fused backward does not round the pooled gradient to the
-    activation dtype before the BN reduction), over repeated steps (accumulator re-zeroing)."""
+    activation dtype before the BN reduction), over repeated steps (accumulator re-zeroing).
+    xsel: the backward's sums from the forward's saved argmax inputs (default) or per pixel."""
     from arena_amd.ops import batchnorm, conv
     from arena_amd.ops.pool import MaxPool2dNHWC
+    batchnorm.set_stem_xsel(xsel)
     torch.manual_seed(4)
     N, Cin, C, H, W = 4, 64, 64, 18, 17
     mods = []
@@ -321,3 +324,4 @@ def test_bn_relu_maxpool_fused_matches_modules(dtype, partials, pad):
             assert int(mods[0][0].num_batches_tracked) == step + 1
     finally:
         batchnorm.set_stem_pool_fused(True)
+        batchnorm.set_stem_xsel(True)

@@ -13,9 +13,10 @@ dy * mask for the residual join instead of parking (dy, bits)) and/or ``:finP<n>
 level-1 blocks per channel group in the BN finalize kernels) and/or ``:redG<b>x<r>`` (BN reduction grid) and/or ``:accP<n>`` (conv-epilogue
 BN statistics as fp64 sums up to n tile-channel pairs) and/or ``:finbwd0`` (BN backward sums
 from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv forms) and/or
-``:nostempool`` (stem BN and max pool unfused) and/or ``:fold`` (bn1 / bn2 folded into the
+``:nostempool`` (stem BN and max pool unfused) and/or ``:noxsel`` (stem backward sums per pixel
+over x instead of from the saved argmax inputs) and/or ``:fold`` (bn1 / bn2 folded into the
 consuming convs instead of applied by their own pass) and/or ``:v2split`` (split-K forms of the
-v2 tiles among the candidates) and/or ``:ebk<n>`` (at most n blocks per BN apply / dx pass),
+v2 tiles among the candidates) and/or ``:linkprice`` (per-layer link pricing) and/or ``:ebk<n>`` (at most n blocks per BN apply / dx pass),
 joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
@@ -62,6 +63,8 @@ def main():
         opts = opt_s.split("+")
         # BN-backward partials in the dgrad epilogue: on by default, "nolink" turns them off
         conv.set_bn_links("nolink" not in opts if "link" not in opts else True)
+        # linkprice: the tuner prices each layer's link against the BN's own reduction pass
+        conv.set_link_choice("linkprice" in opts)
         conv.set_stem_fused("torchstem" not in opt_s.split("+"))
         conv.set_masked_join("nomask" not in opt_s.split("+"))
         # finP<n>: at most n level-1 blocks per channel group in the BN finalize kernels (the
@@ -90,6 +93,7 @@ def main():
         conv.set_persist("nopersist" not in opt_s.split("+"))
         # nostempool: stem BN apply + max pool kernels instead of the fused pass
         _bn.set_stem_pool_fused("nostempool" not in opt_s.split("+"))
+        _bn.set_stem_xsel("noxsel" not in opt_s.split("+"))   # stem sums per pixel over x
         # fold: bn1 / bn2 folded into the consuming convs (off by default, ARENA_BN_FOLD)
         conv.set_bn_fold("fold" in opt_s.split("+"))
         # v2split: the v2 split-K forms among the autotuner's candidates (off by default)
