@@ -60,6 +60,8 @@ void arena_ccl_sgd_f32_shard(long long, long long, int, int, long long*, long lo
 void arena_ccl_set_block_elems(long long);
 void arena_ccl_set_max_blocks(int);
 void arena_bn_set_elem_max_blocks(int);
+void arena_bn_set_dx_max_blocks(int);
+void arena_bn_set_slice(int);
 void arena_ccl_set_oneshot_max(long long);
 long long arena_ccl_get_oneshot_max();
 // csrc/ops/conv_kernels.hip
@@ -2097,6 +2099,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("ccl_set_block_elems", [](int64_t e) { arena_ccl_set_block_elems(e); });
   m.def("ccl_set_max_blocks", [](int64_t b) { arena_ccl_set_max_blocks((int)b); });
   m.def("bn_set_elem_max_blocks", [](int64_t b) { arena_bn_set_elem_max_blocks((int)b); });
+  m.def("bn_set_dx_max_blocks", [](int64_t b) { arena_bn_set_dx_max_blocks((int)b); });
+  m.def("bn_set_slice", [](int64_t on) { arena_bn_set_slice((int)on); });
   m.def("ccl_set_oneshot_max", [](int64_t e) { arena_ccl_set_oneshot_max(e); });
   m.def("ccl_get_oneshot_max", []() { return (int64_t)arena_ccl_get_oneshot_max(); });
   m.def("ccl_set_bcast_direct_max", [](int64_t e) { arena_ccl_set_bcast_direct_max(e); });

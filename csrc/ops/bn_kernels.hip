@@ -440,11 +440,16 @@ __device__ __forceinline__ void lds8(const float* p, float v[kVec]) {
 // also writes st's outputs (mean / invstd for the backward, scale / shift, running statistics,
 // the batch counter). The sums stay in place: the backward's dx pass of this layer zeroes them
 // (arena_bn_bwd `zero`), after their last reader here has finished.
+// [c_lo, c_lo + cs): the channels this block covers (all C, or one 256-channel slice of a
+// channel-sliced grid, see Slice); s_co holds them at local indices [k][cs].
+// writer: this block writes st's outputs for its channels (one block per channel).
 template <bool FIN>
 __device__ __forceinline__ void apply_coefs(int C, long long M, const double* fin,
-                                            const ArenaBNStats& st, float* s_co) {
+                                            const ArenaBNStats& st, float* s_co, int c_lo,
+                                            int cs, bool writer) {
   const double inv_m = 1.0 / (double)M;
-  for (int c = threadIdx.x; c < C; c += kT) {
+  for (int cl = threadIdx.x; cl < cs; cl += kT) {
+    const int c = c_lo + cl;
     float mu, sc, sh;
     if constexpr (!FIN) {
       mu = st.mean[c];
@@ -460,7 +465,7 @@ __device__ __forceinline__ void apply_coefs(int C, long long M, const double* fi
       mu = (float)mean;
       sc = (st.gamma ? st.gamma[c] : 1.f) * inv;
       sh = st.beta ? st.beta[c] : 0.f;
-      if (blockIdx.x == 0 && blockIdx.y == 0) {
+      if (writer) {
         st.mean[c] = mu;
         st.invstd[c] = inv;
         st.scale[c] = sc;
@@ -474,11 +479,45 @@ __device__ __forceinline__ void apply_coefs(int C, long long M, const double* fi
         if (c == 0 && st.batches != nullptr) *st.batches += 1;
       }
     }
-    s_co[c] = mu;
-    s_co[C + c] = sc;
-    s_co[2 * C + c] = sh;
+    s_co[cl] = mu;
+    s_co[cs + cl] = sc;
+    s_co[2 * cs + cl] = sh;
   }
   __syncthreads();
+}
+
+// Thread -> vector mapping of the streaming passes (apply, dx). Every vector a thread touches has
+// the same channel group, so its coefficients load once. Flat grid (gridDim.y == 1): vector
+// blockIdx.x * kT + tid, stride gridDim.x * kT (cg | kT, host-checked). Channel-sliced grid
+// (gridDim.y = cg / 32 slices of 256 channels, for C > 256): a block covers 32 groups x 8 rows of
+// its slice, so its coefficient prologue derives 256 channels instead of all C -- with C = 2048
+// and ~6 vectors per thread that prologue was most of the pass (the 7x7 dx ran at 1.9 TB/s).
+struct Slice {
+  long long v0, stride;   // first vector, vector stride
+  int c_lo, cs;           // channel range of the block (coefficients)
+  int c0;                 // the thread's first channel, local to [c_lo, c_lo + cs)
+};
+constexpr int kSliceG = 32;   // channel groups per slice
+
+__device__ __forceinline__ Slice slice_of(int cg) {
+  Slice q;
+  if (gridDim.y == 1) {
+    q.v0 = (long long)blockIdx.x * kT + threadIdx.x;
+    q.stride = (long long)gridDim.x * kT;
+    q.c_lo = 0;
+    q.cs = cg * kVec;
+    q.c0 = (int)(q.v0 & (cg - 1)) * kVec;
+  } else {
+    constexpr int kRows = kT / kSliceG;
+    const int gl = threadIdx.x & (kSliceG - 1);
+    const long long row0 = (long long)blockIdx.x * kRows + threadIdx.x / kSliceG;
+    q.v0 = row0 * cg + (long long)blockIdx.y * kSliceG + gl;
+    q.stride = (long long)gridDim.x * kRows * cg;
+    q.c_lo = blockIdx.y * kSliceG * kVec;
+    q.cs = kSliceG * kVec;
+    q.c0 = gl * kVec;
+  }
+  return q;
 }
 
 // NT: non-temporal loads of x (and res) -- their last read before the backward pass
@@ -493,18 +532,16 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
                                                       long long M, long long nvec, int cg,
                                                       double* __restrict__ zero, int nzero) {
   extern __shared__ __attribute__((aligned(16))) float s_co[];
-  const long long stride = (long long)gridDim.x * kT;
-  // every vector this thread touches has the same channel group: the grid stride is a multiple
-  // of kT, and cg divides kT (host-checked), so the per-channel coefficients load once
-  const int c0 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1)) * kVec;
+  const Slice q = slice_of(cg);
+  const long long stride = q.stride;
   const int C = cg * kVec;
-  apply_coefs<FIN>(C, M, fin, st, s_co);
+  apply_coefs<FIN>(C, M, fin, st, s_co, q.c_lo, q.cs, blockIdx.x == 0);   // one per slice
   float mu[kVec], sc[kVec], sh[kVec];
-  lds8(s_co + c0, mu);
-  lds8(s_co + C + c0, sc);
-  lds8(s_co + 2 * C + c0, sh);
+  lds8(s_co + q.c0, mu);
+  lds8(s_co + q.cs + q.c0, sc);
+  lds8(s_co + 2 * q.cs + q.c0, sh);
   zero_duty(zero, nzero);
-  for (long long v0 = (long long)blockIdx.x * kT + threadIdx.x; v0 < nvec; v0 += 2 * stride) {
+  for (long long v0 = q.v0; v0 < nvec; v0 += 2 * stride) {
     float a[2][kVec], b[2][kVec];
     bool ok[2];
     long long vv[2];
@@ -777,12 +814,13 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
                                                        const double* __restrict__ acc, long long M,
                                                        double* __restrict__ zero, int nzero) {
   extern __shared__ __attribute__((aligned(16))) float s_co[];
-  const long long stride = (long long)gridDim.x * kT;
-  // fixed channel group per thread (grid stride = multiple of kT, cg | kT): coefficients once
-  const int c0 = (int)(((long long)blockIdx.x * kT + threadIdx.x) & (cg - 1)) * kVec;
+  const Slice q = slice_of(cg);   // fixed channel group per thread: coefficients once
+  const long long stride = q.stride;
+  const int c0 = q.c0, cs = q.cs;
   const int C = cg * kVec;
   const double inv_m = 1.0 / (double)M;
-  for (int c = threadIdx.x; c < C; c += kT) {   // one thread per channel (see lds8)
+  for (int cl = threadIdx.x; cl < cs; cl += kT) {   // one thread per channel (see lds8)
+    const int c = q.c_lo + cl;
     float a_, b_, c_;
     if constexpr (FIN) {
       double a, b;
@@ -801,27 +839,27 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
       b_ = co.cb[c];
       c_ = co.cc[c];
     }
-    s_co[c] = a_;
-    s_co[C + c] = b_;
-    s_co[2 * C + c] = c_;
-    s_co[3 * C + c] = co.mean[c];
+    s_co[cl] = a_;
+    s_co[cs + cl] = b_;
+    s_co[2 * cs + cl] = c_;
+    s_co[3 * cs + cl] = co.mean[c];
     if constexpr (MX) {
-      s_co[4 * C + c] = co.scale[c];
-      s_co[5 * C + c] = co.shift[c];
+      s_co[4 * cs + cl] = co.scale[c];
+      s_co[5 * cs + cl] = co.shift[c];
     }
   }
   __syncthreads();
   float ca[kVec], cb[kVec], cc[kVec], mu[kVec], fsc[MX ? kVec : 1], fsh[MX ? kVec : 1];
   lds8(s_co + c0, ca);
-  lds8(s_co + C + c0, cb);
-  lds8(s_co + 2 * C + c0, cc);
-  lds8(s_co + 3 * C + c0, mu);
+  lds8(s_co + cs + c0, cb);
+  lds8(s_co + 2 * cs + c0, cc);
+  lds8(s_co + 3 * cs + c0, mu);
   if constexpr (MX) {
-    lds8(s_co + 4 * C + c0, fsc);
-    lds8(s_co + 5 * C + c0, fsh);
+    lds8(s_co + 4 * cs + c0, fsc);
+    lds8(s_co + 5 * cs + c0, fsh);
   }
   zero_duty(zero, nzero);
-  for (long long v = (long long)blockIdx.x * kT + threadIdx.x; v < nvec; v += stride) {
+  for (long long v = q.v0; v < nvec; v += stride) {
     float d[kVec], xv[kVec];
     if (NT) V8<T>::loadnt(dy + v * kVec, d); else V8<T>::load(dy + v * kVec, d);
     uint32_t mb = (RELU && !MX) ? (uint32_t)mask[v] : 0xffu;
@@ -869,7 +907,7 @@ __global__ __launch_bounds__(kT) void bn_pool_fwd_kernel(const T* __restrict__ x
                                                          double* __restrict__ zero, int nzero) {
   extern __shared__ __attribute__((aligned(16))) float s_co[];
   const int C = g.C, cg = C / kVec;
-  apply_coefs<FIN>(C, M, fin, st, s_co);
+  apply_coefs<FIN>(C, M, fin, st, s_co, 0, C, blockIdx.x == 0 && blockIdx.y == 0);
   zero_duty(zero, nzero);
   const int row = blockIdx.x;
   const int t = blockIdx.y * kT + threadIdx.x;
@@ -1413,6 +1451,25 @@ int elementwise_blocks(long long nvec) {
   return (int)(b < 1 ? 1 : (b > g_elem_max_blocks ? g_elem_max_blocks : b));
 }
 
+// The dx pass's grid (one vector per thread per iteration): at most g_dx_max_blocks blocks.
+// Channel-sliced grids (Slice) for the apply / dx passes of layers with C > 256. ResNet-50 step,
+// interleaved replays (profiles/r5_slice_ab.jsonl): flat grids with 4096 dx blocks 11.990 ms,
+// sliced 11.651, sliced + 1024 dx blocks 11.502 (flat + 1024: 11.723).
+int g_dx_max_blocks = 1024;
+int g_bn_slice = 1;
+
+// (x, y) grid of a streaming pass with `total` blocks wanted: flat, or row blocks x channel
+// slices when slicing is on and C > 256 (the same number of blocks in all).
+dim3 stream_grid(long long total, int C) {
+  const int cg = C / kVec;
+  if (!g_bn_slice || cg <= kSliceG) return dim3((unsigned)total);
+  const int ns = cg / kSliceG;
+  const long long bx = total / ns;
+  return dim3((unsigned)(bx < 1 ? 1 : bx), (unsigned)ns);
+}
+
+int stream_lds_channels(int C) { return (g_bn_slice && C / kVec > kSliceG) ? kSliceG * kVec : C; }
+
 bool bad_shape(long long M, int C) {
   return M <= 0 || C <= 0 || C % kVec != 0 || C > kMaxC || (kT % (C / kVec)) != 0;
 }
@@ -1426,6 +1483,10 @@ void arena_bn_set_fin_max_blocks(int p) { g_fin_max_p = p < 1 ? 1 : (p > 64 ? 64
 void arena_bn_set_nt(int on) { g_bn_nt = on ? 1 : 0; }
 
 void arena_bn_set_elem_max_blocks(int b) { g_elem_max_blocks = b < 64 ? 64 : (b > 65536 ? 65536 : b); }
+
+void arena_bn_set_dx_max_blocks(int b) { g_dx_max_blocks = b < 64 ? 64 : (b > 65536 ? 65536 : b); }
+
+void arena_bn_set_slice(int on) { g_bn_slice = on ? 1 : 0; }
 
 void arena_bn_set_pool_quad_mult(int m) { g_pool_quad_mult = m < 1 ? 1 : (m > 16 ? 16 : m); }
 
@@ -1508,10 +1569,11 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
                        dim3(kT), 0, stream, part, (int)nb, M, C, rpb, lvl2, tickets, st);
   }
   const long long nvec = M * (C / kVec);
-  const int nb = elementwise_blocks(nvec);
+  const dim3 agrid = stream_grid(elementwise_blocks(nvec), C);
+  const int acs = stream_lds_channels(C);
   const int cg = C / kVec;
 #define ARENA_BN_APPLY_NT(TT, R, S, NT, F)                                                   \
-  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S, NT, F>), dim3(nb), dim3(kT), 3 * C * 4, stream, \
+  hipLaunchKernelGGL((bn_apply_kernel<TT, R, S, NT, F>), agrid, dim3(kT), 3 * acs * 4, stream, \
                      static_cast<const TT*>(x), static_cast<const TT*>(res), static_cast<TT*>(y), \
                      mask, st, acc, M, nvec, cg, zero, nzero)
 #define ARENA_BN_APPLY_F(TT, R, S, F)                                                        \
@@ -1592,11 +1654,13 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
                        dim3(kT), 0, stream, part, (int)nb, M, C, lvl2, tickets, co);
   const long long nvec = M * (C / kVec);
   long long ne = (nvec + kT - 1) / kT;
-  ne = ne < 1 ? 1 : (ne > 4096 ? 4096 : ne);
+  ne = ne < 1 ? 1 : (ne > g_dx_max_blocks ? g_dx_max_blocks : ne);
+  const dim3 dgrid = stream_grid(ne, C);
+  const int dcs = stream_lds_channels(C);
   const int cg = C / kVec;
 #define ARENA_BN_DX_NTX(TT, R, S, NT, F, X)                                                  \
-  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S, NT, F, X>), dim3(ne), dim3(kT),             \
-                     (X ? 6 : 4) * C * 4, stream,                                           \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S, NT, F, X>), dgrid, dim3(kT),                \
+                     (X ? 6 : 4) * dcs * 4, stream,                                         \
                      static_cast<const TT*>(dy), mask, static_cast<const TT*>(x),            \
                      static_cast<TT*>(dx), static_cast<TT*>(dres), nvec, cg, co, acc, M,     \
                      zero, nzero)

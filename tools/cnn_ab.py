@@ -16,7 +16,8 @@ from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv 
 ``:nostempool`` (stem BN and max pool unfused) and/or ``:noxsel`` (stem backward sums per pixel
 over x instead of from the saved argmax inputs) and/or ``:fold`` (bn1 / bn2 folded into the
 consuming convs instead of applied by their own pass) and/or ``:v2split`` (split-K forms of the
-v2 tiles among the candidates) and/or ``:linkprice`` (per-layer link pricing) and/or ``:ebk<n>`` (at most n blocks per BN apply / dx pass),
+v2 tiles among the candidates) and/or ``:linkprice`` (per-layer link pricing) and/or ``:ebk<n>`` (at most n blocks per BN apply pass), ``:dxb<n>`` (per dx pass), ``:noslice`` (flat
+grids for C > 256 instead of 256-channel slices),
 joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
 
@@ -98,9 +99,14 @@ def main():
         conv.set_bn_fold("fold" in opt_s.split("+"))
         # v2split: the v2 split-K forms among the autotuner's candidates (off by default)
         conv.set_v2_split("v2split" in opt_s.split("+"))
-        # ebk<n>: at most n blocks per BN apply / dx pass (grid baked into the captured graph)
+        # ebk<n>: at most n blocks per BN apply pass (grid baked into the captured graph)
         ebk = [int(o[3:]) for o in opt_s.split("+") if o.startswith("ebk")]
         _e.load().bn_set_elem_max_blocks(ebk[0] if ebk else 1024)
+        # dxb<n>: at most n blocks per BN dx pass; noslice: flat grids for C > 256 (no channel
+        # slices in the apply / dx passes)
+        dxb = [int(o[3:]) for o in opt_s.split("+") if o.startswith("dxb")]
+        _e.load().bn_set_dx_max_blocks(dxb[0] if dxb else 1024)
+        _e.load().bn_set_slice(0 if "noslice" in opt_s.split("+") else 1)
         # st1p: conv-epilogue BN statistics in one pass (the launch args bake the switch)
         _e.load().conv_set_stats_one_pass("st1p" in opt_s.split("+"))
         model, opt, x, y = cnn_bench.build(args, dev, 1)
