@@ -202,3 +202,24 @@ def test_auto_picks_hier_across_nodes():
     assert all(res["backend"] == "hier" for res in _run(4, False, "auto", 2).values())
     assert all(res["backend"] == "rccl" for res in _run(4, False, "rccl", 2).values())
     assert all(res["backend"] == "rccl" for res in _run(2, False, "auto", 2).values())
+
+
+def test_hier_rejects_bad_local_size():
+    """local_size must divide the world and leave more than one node of more than one rank."""
+    import torch.distributed as dist
+    from arena_amd.parallel.zero import ShardedMasterSGD
+    store = dist.HashStore()
+    dist.init_process_group("gloo", store=store, rank=0, world_size=1)
+    try:
+        p = torch.nn.Parameter(torch.randn(8, 8).to(torch.bfloat16))
+        with pytest.raises(ValueError, match="1 < local_size < world"):
+            ShardedMasterSGD([p], lr=0.1, backend="hier", local_size=1)
+        with pytest.raises(ValueError, match="must divide"):
+            ShardedMasterSGD([p], lr=0.1, backend="rccl", local_size=3)
+        with pytest.raises(ValueError, match="backend must be"):
+            ShardedMasterSGD([p], lr=0.1, backend="ring")
+        opt = ShardedMasterSGD([p], lr=0.1, backend="auto")   # one rank: flat, no level groups
+        assert opt.backend == "rccl" and opt._intra is None
+        opt.close()
+    finally:
+        dist.destroy_process_group()
