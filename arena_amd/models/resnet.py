@@ -18,6 +18,7 @@ Parameters stay fp32 (master weights) for the data-parallel buckets and the opti
 """
 from __future__ import annotations
 
+import os
 from typing import List
 
 import torch
@@ -26,6 +27,16 @@ from torch import nn
 from ..ops.batchnorm import BatchNormAct2d, ResidualMask, bn_relu_maxpool
 from ..ops.conv import BNGradLink, Conv2dNHWC, GradJoin, StemConv2d, WeightFlipper
 from ..ops.pool import MaxPool2dNHWC
+
+# Downsample blocks build their shortcut after the main path (see Bottleneck.forward; A/B switch,
+# ARENA_DOWN_LAST=0 builds it first).
+_DOWN_LAST = os.environ.get("ARENA_DOWN_LAST", "1") == "1"
+
+
+def set_downsample_last(on: bool) -> None:
+    global _DOWN_LAST
+    _DOWN_LAST = bool(on)
+
 
 DEPTHS = {"resnet50": [3, 4, 6, 3], "resnet101": [3, 4, 23, 3],
           "resnet152": [3, 8, 36, 3], "resnet_tiny": [1, 1, 1, 1]}
@@ -68,9 +79,13 @@ class Bottleneck(nn.Module):
         idt = x
         # downsample block: bn3's residual gradient reaches down_bn as (dy, bn3's ReLU mask)
         rmask = ResidualMask() if (train and self.down_conv is not None) else None
-        if self.down_conv is not None:
-            y, st = self.down_conv.forward_stats(x, join=join, bn_link=link)
-            idt = self.down_bn(y, stats=st, res_in=rmask)
+
+        def shortcut():
+            y_, st_ = self.down_conv.forward_stats(x, join=join, bn_link=link)
+            return self.down_bn(y_, stats=st_, res_in=rmask)
+
+        if self.down_conv is not None and not _DOWN_LAST:
+            idt = shortcut()
         # bn1 / bn2 feed one conv each: folded into it where the kernels allow (the conv
         # normalises its staged operand; the BN output is never written, see BNFold)
         y, st = self.conv1.forward_stats(x, join=join, bn_link=link)
@@ -78,6 +93,12 @@ class Bottleneck(nn.Module):
         y, st = self.conv2.forward_stats(a, bn_link=lk1, fold=fold)
         a, fold = self.bn2.forward_fold(y, self.conv3, stats=st, link=lk2)
         y, st = self.conv3.forward_stats(a, bn_link=lk2, fold=fold)
+        if self.down_conv is not None and _DOWN_LAST:
+            # created after the main path, the shortcut's backward runs first (autograd takes
+            # the ready node with the highest sequence number): its strided dgrad parks at the
+            # join and conv1's stride-1 dgrad completes it -- so conv1's epilogue can take the
+            # previous BN's backward sums (BNGradLink), which a strided dgrad cannot
+            idt = shortcut()
         return self.bn3(y, residual=idt, stats=st, join=join if self.down_conv is None else None,
                         link=link_out, res_out=rmask)
 
