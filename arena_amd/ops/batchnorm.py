@@ -99,18 +99,37 @@ class ResidualMask:
     and dx passes already read a mask, so dy * mask is never written. The gradient down_bn
     receives is the unmasked dy whenever bn3 published, so ``take`` always returns the mask then.
     bn3 only publishes when down_bn ran on the fused kernels (``armed`` by its forward), the only
-    path whose backward takes the mask."""
-    __slots__ = ("armed", "mask")
+    path whose backward takes the mask.
+
+    down_bn's forward also leaves its input, batch mean and backward-sum set here (``x2``,
+    ``mean2``, ``bacc2``): bn3's dx pass, which holds the masked dy anyway, then adds down_bn's
+    backward sums as it streams (``bn_bwd(x2=...)``) and publishes them, and down_bn's backward
+    skips its reduction pass (ARENA_RES_SUMS=0: down_bn reduces itself)."""
+    __slots__ = ("armed", "mask", "x2", "mean2", "bacc2", "sums")
 
     def __init__(self):
         self.armed, self.mask = False, None
+        self.x2 = self.mean2 = self.bacc2 = self.sums = None
 
-    def publish(self, mask: torch.Tensor) -> None:
-        self.mask = mask
+    def publish(self, mask: torch.Tensor, sums: Optional[torch.Tensor] = None) -> None:
+        self.mask, self.sums = mask, sums
 
     def take(self):
         m, self.mask = self.mask, None
         return m
+
+    def take_sums(self):
+        s, self.sums = self.sums, None
+        self.x2 = self.mean2 = self.bacc2 = None
+        return s
+
+
+_RES_SUMS = os.environ.get("ARENA_RES_SUMS", "1") == "1"
+
+
+def set_res_sums(on: bool) -> None:
+    global _RES_SUMS
+    _RES_SUMS = bool(on)
 
 
 _FIN_BWD = True
@@ -188,6 +207,9 @@ class _BNActFn(torch.autograd.Function):
         ctx.res_in = res_in if training else None
         if res_in is not None:
             res_in.armed = training
+            if (training and _RES_SUMS and bacc is not None and _FIN_BWD
+                    and x.dtype == torch.bfloat16):
+                res_in.x2, res_in.mean2, res_in.bacc2 = x, mean, bacc
         return y
 
     @staticmethod
@@ -199,10 +221,12 @@ class _BNActFn(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         ext = ctx.link.take(dy) if ctx.link is not None else None
         relu = ctx.relu
+        sums2 = None
         if ctx.res_in is not None:   # the consumer BN handed over its ReLU mask for this dy
             m = ctx.res_in.take()
             if m is not None:
                 relu, mask = True, m
+                sums2 = ctx.res_in.take_sums()   # and maybe summed this layer's sums too
         # the residual gradient is dy * ReLU mask; when this BN reaches the residual join first
         # and the other consumer's dgrad epilogue takes a masked addend, park (dy, mask) instead
         # of writing that product (one full write of the block input's size saved)
@@ -214,16 +238,25 @@ class _BNActFn(torch.autograd.Function):
         ready = bool(ext) and isinstance(ext[0], str)   # ("acc", sums): the conv summed
         if ready:
             acc_b, ext = ext[1], None
+        elif sums2 is not None:                         # bn3's dx pass summed them
+            acc_b, ext, ready = sums2, None, True
         else:
             acc_b = ctx.bacc.for_backward(x, x.shape[1]) \
                 if (ctx.bacc is not None and not ext and _FIN_BWD) else None
-        dx, dres, dgamma, dbeta = _ext.load().bn_bwd(dy, mask, x, mean, invstd, weight, relu,
-                                                     ctx.has_res and not masked and not to_res,
-                                                     ctx.affine, ext[0] if ext else None,
-                                                     ext[1] if ext else 0, acc_b=acc_b,
-                                                     zero_f=ctx.facc, acc_ready=ready)
+        # to_res: the residual BN's backward sums ride along in this dx pass where they can
+        ro = ctx.res_out if to_res else None
+        s2 = (ro is not None and ro.x2 is not None and acc_b is not None and relu
+              and ro.x2.shape == x.shape and ro.x2.dtype == x.dtype)
+        acc2 = ro.bacc2.for_backward(ro.x2, x.shape[1]) if s2 else None
+        dx, dres, dgamma, dbeta, sums2_out = _ext.load().bn_bwd(
+            dy, mask, x, mean, invstd, weight, relu, ctx.has_res and not masked and not to_res,
+            ctx.affine, ext[0] if ext else None, ext[1] if ext else 0, acc_b=acc_b,
+            zero_f=ctx.facc, acc_ready=ready, x2=ro.x2 if s2 else None,
+            mean2=ro.mean2 if s2 else None, acc2=acc2)
         if to_res:
-            ctx.res_out.publish(mask)
+            # sums2_out: the set filled for the residual BN (None: it reduces itself; its set,
+            # marked dirty above, is zeroed again by its own backward's for_backward)
+            ctx.res_out.publish(mask, sums2_out)
             dres = dy
         elif masked:
             parked = ctx.join.park_or_take(conv.MaskedGrad(dy, mask))
@@ -280,7 +313,7 @@ class _BNFoldFn(torch.autograd.Function):
         else:
             acc_b = ctx.bacc.for_backward(x, x.shape[1]) \
                 if (ctx.bacc is not None and not ext and _FIN_BWD) else None
-        dx, _, dgamma, dbeta = _ext.load().bn_bwd(dy, None, x, coef[0], invstd, weight, True,
+        dx, _, dgamma, dbeta, _ = _ext.load().bn_bwd(dy, None, x, coef[0], invstd, weight, True,
                                                   False, ctx.affine, ext[0] if ext else None,
                                                   ext[1] if ext else 0, acc_b=acc_b,
                                                   zero_f=ctx.facc, acc_ready=ready, coef=coef)

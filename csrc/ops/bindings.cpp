@@ -116,7 +116,7 @@ hipError_t arena_bn_fwd(int, const void*, const void*, void*, uint8_t*, long lon
                         double*, int, hipStream_t);
 hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, void*, long long, int,
                         int, float*, int, double*, unsigned*, ArenaBNBwd, double*, int, double*,
-                        int, int, hipStream_t);
+                        int, int, const void*, const float*, double*, hipStream_t);
 hipError_t arena_bn_fold_fwd(long long, int, const double*, float*, int, long long, double*,
                              unsigned*, ArenaBNStats, double*, int, hipStream_t);
 int arena_bn_acc_ok(long long, int);
@@ -1105,11 +1105,27 @@ std::vector<Tensor> bn_fold_fwd(Tensor x, OptT gamma, OptT beta, OptT running_me
 
 // coef (optional, a folded layer: bn_fold_fwd's [3, C] mean / scale / shift): the ReLU bits are
 // recomputed from x with the forward's arithmetic instead of read from mask.
+// x2 / mean2 / acc2 (optional): the dx pass also adds the backward sums of a second BN whose input
+// is x2 and whose gradient is this layer's masked dy (a downsample block's down_bn) into acc2,
+// that layer's own [kRep, 2, C] set -- where the pass derives its coefficients from sums, with
+// ReLU and no residual output. Returns (dx, dres, dgamma, dbeta, acc2 if it was filled).
 std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor invstd, OptT gamma,
                            bool relu, bool with_res, bool affine_grads, OptT ext_part,
-                           int64_t ext_rpb, OptT acc_b, OptT zero_f, bool acc_ready, OptT coef) {
+                           int64_t ext_rpb, OptT acc_b, OptT zero_f, bool acc_ready, OptT coef,
+                           OptT x2, OptT mean2, OptT acc2) {
   const BNGeom g = bn_geom(x, "x");
   bn_same(x, dy, "grad_output");
+  const bool sum2 = x2.has_value() && x2->defined();
+  if (sum2) {
+    bn_same(x, *x2, "x2");
+    TORCH_CHECK(mean2.has_value() && acc2.has_value(), "bn_bwd: x2 needs mean2 and acc2");
+    check_f32(*mean2, "mean2");
+    TORCH_CHECK(mean2->numel() == g.C, "bn_bwd: mean2 must have C elements");
+    TORCH_CHECK(acc2->is_cuda() && acc2->device() == x.device() &&
+                    acc2->scalar_type() == torch::kFloat64 && acc2->is_contiguous() &&
+                    acc2->numel() == kRep * 2 * g.C,
+                "bn_bwd: acc2 must be a contiguous fp64 [kRep, 2, C] set on x's device");
+  }
   const bool mask_x = relu && coef.has_value() && coef->defined();
   if (mask_x) {
     check_f32(*coef, "coef");
@@ -1199,17 +1215,22 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
   }
   Tensor dx = torch::empty_like(x);
   Tensor dres = with_res ? torch::empty_like(x) : Tensor();
+  // the second BN's sums ride along only where the dx pass derives its coefficients from sums
+  // (fin_dx) on the plain ReLU path; else the caller's second BN reduces itself
+  const bool use2 = sum2 && fin_dx == 1 && relu && !with_res && !mask_x;
   check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(),
                          relu && !mask_x ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(),
                          dx.data_ptr(), with_res ? dres.data_ptr() : nullptr, g.M, g.C,
                          relu ? 1 : 0, part.defined() ? part.data_ptr<float>() : nullptr, ext_nblk,
                          lvl2.defined() ? lvl2.data_ptr<double>() : nullptr, tickets, b,
                          acc.defined() ? acc.data_ptr<double>() : nullptr, fin_dx, zf, nzf,
-                         mask_x ? 1 : 0, cur_stream()),
+                         mask_x ? 1 : 0, use2 ? x2->data_ptr() : nullptr,
+                         use2 ? mean2->data_ptr<float>() : nullptr,
+                         use2 ? acc2->data_ptr<double>() : nullptr, cur_stream()),
             "bn_bwd");
   if (acc.defined() && !fin_dx) bn_acc_clean(acc);   // the finalize zeroed the pool set
   if (zf != nullptr) bn_acc_clean(*zero_f);
-  return {dx, dres, dgamma, dbeta};
+  return {dx, dres, dgamma, dbeta, use2 ? *acc2 : Tensor()};
 }
 
 // Fused stem BatchNorm + ReLU + k x k / s max pool (training; bn_kernels.hip arena_bn_pool_fwd):
@@ -2049,7 +2070,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("invstd"), py::arg("gamma"), py::arg("relu"), py::arg("with_res"),
         py::arg("affine_grads"), py::arg("ext_part") = py::none(), py::arg("ext_rpb") = 0,
         py::arg("acc_b") = py::none(), py::arg("zero_f") = py::none(),
-        py::arg("acc_ready") = false, py::arg("coef") = py::none());
+        py::arg("acc_ready") = false, py::arg("coef") = py::none(), py::arg("x2") = py::none(),
+        py::arg("mean2") = py::none(), py::arg("acc2") = py::none());
   m.def("bn_fold_fwd", &bn_fold_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"),
         py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
         py::arg("num_batches"), py::arg("stats_part") = py::none(), py::arg("stats_rpb") = 0,

@@ -805,14 +805,21 @@ __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const float* __rest
 // dynamic shared memory: 4 * C floats
 // MX (with RELU): ReLU bits from x and the forward's coefficients (folded layer, see the reduction)
 // dynamic shared memory: 6 * C floats with MX
-template <typename T, bool RELU, bool RES, bool NT, bool FIN, bool MX = false>
+// S2 (RELU, FIN, no RES / MX): the same pass also sums (g, g (x2 - mean2)) per channel into acc2
+// [ARENA_ACC_REP][2][C] -- the backward sums of a second BN whose gradient is this layer's masked
+// dy g: a downsample block's down_bn, the residual of this bn3 (see batchnorm.ResidualMask). Its
+// own reduction pass (dy, mask and x2 read again) then does not run.
+template <typename T, bool RELU, bool RES, bool NT, bool FIN, bool MX = false, bool S2 = false>
 __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
                                                        const uint8_t* __restrict__ mask,
                                                        const T* __restrict__ x,
                                                        T* __restrict__ dx, T* __restrict__ dres,
                                                        long long nvec, int cg, ArenaBNBwd co,
                                                        const double* __restrict__ acc, long long M,
-                                                       double* __restrict__ zero, int nzero) {
+                                                       double* __restrict__ zero, int nzero,
+                                                       const T* __restrict__ x2,
+                                                       const float* __restrict__ mean2,
+                                                       double* __restrict__ acc2) {
   extern __shared__ __attribute__((aligned(16))) float s_co[];
   const Slice q = slice_of(cg);   // fixed channel group per thread: coefficients once
   const long long stride = q.stride;
@@ -859,11 +866,22 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
     lds8(s_co + 5 * cs + c0, fsh);
   }
   zero_duty(zero, nzero);
+  float mu2[S2 ? kVec : 1], sa2[S2 ? kVec : 1], sb2[S2 ? kVec : 1];
+  if constexpr (S2) {
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      mu2[i] = mean2[q.c_lo + c0 + i];
+      sa2[i] = sb2[i] = 0.f;
+    }
+  }
   for (long long v = q.v0; v < nvec; v += stride) {
-    float d[kVec], xv[kVec];
+    float d[kVec], xv[kVec], x2v[S2 ? kVec : 1];
     if (NT) V8<T>::loadnt(dy + v * kVec, d); else V8<T>::load(dy + v * kVec, d);
     uint32_t mb = (RELU && !MX) ? (uint32_t)mask[v] : 0xffu;
     if (NT) V8<T>::loadnt(x + v * kVec, xv); else V8<T>::load(x + v * kVec, xv);
+    if constexpr (S2) {
+      if (NT) V8<T>::loadnt(x2 + v * kVec, x2v); else V8<T>::load(x2 + v * kVec, x2v);
+    }
     if constexpr (RELU && MX) mb = relu_bits_from_x<T>(xv, mu, fsc, fsh);
     float g[kVec], o[kVec];
 #pragma unroll
@@ -871,8 +889,39 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
       g[i] = ((mb >> i) & 1u) ? d[i] : 0.f;
       o[i] = ca[i] * (g[i] - cb[i] - (xv[i] - mu[i]) * cc[i]);
     }
+    if constexpr (S2) {
+#pragma unroll
+      for (int i = 0; i < kVec; ++i) {
+        sa2[i] += g[i];
+        sb2[i] = fmaf(g[i], x2v[i] - mu2[i], sb2[i]);
+      }
+    }
     V8<T>::store(dx + v * kVec, o);
     if (RES) V8<T>::store(dres + v * kVec, g);
+  }
+  if constexpr (S2) {
+    // the block's partial sums per channel: thread t holds channel group t % cgl of row t / cgl
+    // (flat grid: cgl = cg, cg | kT; sliced: 32), summed over the rows in LDS, then one fp64
+    // atomic per (channel, sum) into replica blockIdx.x % ARENA_ACC_REP
+    __shared__ float s_a2[kT * kVec], s_b2[kT * kVec];
+#pragma unroll
+    for (int i = 0; i < kVec; ++i) {
+      s_a2[threadIdx.x * kVec + i] = sa2[i];
+      s_b2[threadIdx.x * kVec + i] = sb2[i];
+    }
+    __syncthreads();
+    const int cgl = cs / kVec;
+    if ((int)threadIdx.x < cs) {
+      const int gq = threadIdx.x / kVec, i = threadIdx.x % kVec;
+      float a = 0.f, b = 0.f;
+      for (int r = 0; r < kT / cgl; ++r) {
+        a += s_a2[(r * cgl + gq) * kVec + i];
+        b += s_b2[(r * cgl + gq) * kVec + i];
+      }
+      double* dst = acc2 + (size_t)(blockIdx.x % kAccRep) * 2 * C;
+      unsafeAtomicAdd(dst + q.c_lo + threadIdx.x, (double)a);
+      unsafeAtomicAdd(dst + C + q.c_lo + threadIdx.x, (double)b);
+    }
   }
 }
 
@@ -1611,10 +1660,13 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
 // of this layer, whose last reader -- the apply pass -- has finished).
 // mask_x (relu, a folded layer): no mask; the ReLU bits are recomputed from x with co.mean /
 // co.scale / co.shift (the forward's coefficients)
+// x2 / mean2 / acc2 (optional): the second BN's input, batch mean and backward sums (S2 in
+// bn_bwd_dx_kernel); only with relu, no dres, no mask_x and sums fed or summed here (fin_dx).
 hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const void* x, void* dx,
                         void* dres, long long M, int C, int relu, float* part, int ext_nblk,
                         double* lvl2, unsigned* tickets, ArenaBNBwd co, double* acc, int fin_dx,
-                        double* zero, int nzero, int mask_x, hipStream_t stream) {
+                        double* zero, int nzero, int mask_x, const void* x2, const float* mean2,
+                        double* acc2, hipStream_t stream) {
   if (bad_shape(M, C)) return hipErrorInvalidValue;
   const bool mx = relu && mask_x;
   if (relu && !mx && mask == nullptr) return hipErrorInvalidValue;
@@ -1663,7 +1715,7 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
                      (X ? 6 : 4) * dcs * 4, stream,                                         \
                      static_cast<const TT*>(dy), mask, static_cast<const TT*>(x),            \
                      static_cast<TT*>(dx), static_cast<TT*>(dres), nvec, cg, co, acc, M,     \
-                     zero, nzero)
+                     zero, nzero, nullptr, nullptr, nullptr)
 #define ARENA_BN_DX_NT(TT, R, S, NT, F)                                                      \
   do { if (R && mx) ARENA_BN_DX_NTX(TT, R, S, NT, F, R);                                     \
        else ARENA_BN_DX_NTX(TT, R, S, NT, F, false); } while (0)
@@ -1674,7 +1726,21 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
   do { if (fin) ARENA_BN_DX_F(TT, R, S, true); else ARENA_BN_DX_F(TT, R, S, false); }        \
   while (0)
   const bool r = relu != 0, s = dres != nullptr;
-  if (dtype == 1) {
+  if (x2 != nullptr) {
+    if (!(fin && r && !s && !mx) || mean2 == nullptr || acc2 == nullptr)
+      return hipErrorInvalidValue;
+#define ARENA_BN_DX_S2(TT, NT)                                                                 \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, true, false, NT, true, false, true>), dgrid,        \
+                     dim3(kT), 4 * dcs * 4, stream, static_cast<const TT*>(dy), mask,           \
+                     static_cast<const TT*>(x), static_cast<TT*>(dx), nullptr, nvec, cg, co,    \
+                     acc, M, zero, nzero, static_cast<const TT*>(x2), mean2, acc2)
+    if (dtype == 1) {
+      if (g_bn_nt) ARENA_BN_DX_S2(uint16_t, true); else ARENA_BN_DX_S2(uint16_t, false);
+    } else {
+      if (g_bn_nt) ARENA_BN_DX_S2(float, true); else ARENA_BN_DX_S2(float, false);
+    }
+#undef ARENA_BN_DX_S2
+  } else if (dtype == 1) {
     if (r && s) ARENA_BN_DX(uint16_t, true, true);
     else if (r) ARENA_BN_DX(uint16_t, true, false);
     else if (s) ARENA_BN_DX(uint16_t, false, true);

@@ -1061,10 +1061,13 @@ def test_conv_masked_addend_matches_torch():
 @pytest.mark.parametrize("cin,stride", [(128, 2), (64, 1)])
 def test_residual_mask_handoff_matches_materialized(cin, stride):
     """A downsample block whose bn3 hands (dy, ReLU bits) to down_bn (ResidualMask) gives the same
-    gradients, bit for bit, as bn3 writing dy * mask for down_bn; the handoff is taken."""
+    gradients, bit for bit, as bn3 writing dy * mask for down_bn; the handoff is taken. (down_bn
+    reduces its own sums here in both arms: with them summed in bn3's dx pass the order differs,
+    see test_residual_bn_sums_in_bn3_dx_pass.)"""
     from arena_amd.models import resnet as R
     from arena_amd.ops import batchnorm as B
     conv.set_mode("ours")
+    B.set_res_sums(False)
     taken = []
     orig = B.ResidualMask.take
 
@@ -1100,7 +1103,59 @@ def test_residual_mask_handoff_matches_materialized(cin, stride):
             assert torch.equal(out[True][1][n], gp), n
     finally:
         B.ResidualMask.take = orig
+        B.set_res_sums(True)
         conv.set_masked_join(True)
+        conv.set_mode(None)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("cin,stride", [(128, 2), (64, 1), (512, 2)])
+def test_residual_bn_sums_in_bn3_dx_pass(cin, stride):
+    """down_bn's backward sums added by bn3's dx pass (bn_bwd x2=...) instead of down_bn's own
+    reduction: the path is taken, and every gradient matches the self-reducing path to bf16
+    rounding (the fp32 / fp64 summation order differs)."""
+    from arena_amd.models import resnet as R
+    from arena_amd.ops import batchnorm as B
+    conv.set_mode("ours")
+    got = []
+    orig = B.ResidualMask.take_sums
+
+    def spy(self):
+        s_ = orig(self)
+        got.append(s_ is not None)
+        return s_
+
+    try:
+        torch.manual_seed(0)
+        mid = 64 if cin <= 128 else 128
+        blk = R.Bottleneck(cin, mid, stride).cuda().to(memory_format=torch.channels_last)
+        with torch.no_grad():
+            blk.bn3.weight.uniform_(0.5, 1.5)
+        x0 = torch.randn(4, cin, 14, 14, device="cuda").to(torch.bfloat16).contiguous(
+            memory_format=torch.channels_last)
+        g = torch.randn(4, mid * 4, 14 // stride, 14 // stride, device="cuda").to(
+            torch.bfloat16).contiguous(memory_format=torch.channels_last)
+        B.ResidualMask.take_sums = spy
+        out = {}
+        for on in (True, False):
+            B.set_res_sums(on)
+            got.clear()
+            blk.zero_grad(set_to_none=True)
+            x = x0.clone().requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                y = blk(x)
+            y.backward(g)
+            out[on] = (x.grad.float(), {n: p.grad.float() for n, p in blk.named_parameters()},
+                       list(got))
+        assert out[True][2] == [True] and out[False][2] == [False], (out[True][2], out[False][2])
+        torch.testing.assert_close(out[True][0], out[False][0], rtol=2e-2, atol=2e-2)
+        for n, gp in out[False][1].items():
+            scale = max(1.0, float(gp.abs().max()))
+            torch.testing.assert_close(out[True][1][n] / scale, gp / scale, rtol=2e-2,
+                                       atol=2e-2, msg=n)
+    finally:
+        B.ResidualMask.take_sums = orig
+        B.set_res_sums(True)
         conv.set_mode(None)
 
 

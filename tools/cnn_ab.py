@@ -14,7 +14,8 @@ level-1 blocks per channel group in the BN finalize kernels) and/or ``:redG<b>x<
 BN statistics as fp64 sums up to n tile-channel pairs) and/or ``:finbwd0`` (BN backward sums
 from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv forms) and/or
 ``:nostempool`` (stem BN and max pool unfused) and/or ``:noxsel`` (stem backward sums per pixel
-over x instead of from the saved argmax inputs) and/or ``:downfirst`` (downsample shortcut built
+over x instead of from the saved argmax inputs) and/or ``:noressums`` (down_bn's backward sums
+by its own reduction, not in bn3's dx pass) and/or ``:downfirst`` (downsample shortcut built
 before the main path: its strided dgrad completes the join, no BN link there) and/or ``:fold`` (bn1 / bn2 folded into the
 consuming convs instead of applied by their own pass) and/or ``:v2split`` (split-K forms of the
 v2 tiles among the candidates) and/or ``:linkprice`` (per-layer link pricing) and/or ``:ebk<n>`` (at most n blocks per BN apply pass), ``:dxb<n>`` (per dx pass), ``:noslice`` (flat
@@ -96,6 +97,7 @@ def main():
         # nostempool: stem BN apply + max pool kernels instead of the fused pass
         _bn.set_stem_pool_fused("nostempool" not in opt_s.split("+"))
         _bn.set_stem_xsel("noxsel" not in opt_s.split("+"))   # stem sums per pixel over x
+        _bn.set_res_sums("noressums" not in opt_s.split("+"))   # down_bn reduces itself
         from arena_amd.models import resnet as _rn
         _rn.set_downsample_last("downfirst" not in opt_s.split("+"))   # shortcut built first
         # fold: bn1 / bn2 folded into the consuming convs (off by default, ARENA_BN_FOLD)
