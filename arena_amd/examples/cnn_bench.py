@@ -138,7 +138,10 @@ def comm_name(opt) -> str:
     """How the optimizer moves gradients (for logs and the JSON line)."""
     from ..parallel.zero import ShardedMasterSGD
     if isinstance(opt, ShardedMasterSGD):
-        return f"{opt.backend}-sharded-sgd[{len(opt.buckets)} buckets]"
+        red = ""
+        if opt.backend in ("rccl", "hier"):
+            red = ",fp32-reduce" if opt.rccl_reduce_fp32 else ",bf16-ring-reduce"
+        return f"{opt.backend}-sharded-sgd[{len(opt.buckets)} buckets{red}]"
     c = getattr(opt, "comm", None)
     return c if isinstance(c, str) else "none"
 
@@ -286,7 +289,7 @@ def main(argv=None) -> int:
         from ..ops import conv
         for key, plan in conv.plans().items():
             print(f"conv {key[0]} w{key[1]} s{key[2]} p{key[3]}: fwd={plan.fwd} bwd={plan.bwd} "
-                  f"bwd_bn={plan.bwd_bn} link={plan.link} wgrad={plan.wgrad} {plan.times}", file=sys.stderr)
+                  f"bwd_bn={plan.bwd_bn} wgrad={plan.wgrad} {plan.times}", file=sys.stderr)
     hvd.shutdown()
     return 0
 

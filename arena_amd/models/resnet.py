@@ -86,13 +86,11 @@ class Bottleneck(nn.Module):
 
         if self.down_conv is not None and not _DOWN_LAST:
             idt = shortcut()
-        # bn1 / bn2 feed one conv each: folded into it where the kernels allow (the conv
-        # normalises its staged operand; the BN output is never written, see BNFold)
         y, st = self.conv1.forward_stats(x, join=join, bn_link=link)
-        a, fold = self.bn1.forward_fold(y, self.conv2, stats=st, link=lk1)
-        y, st = self.conv2.forward_stats(a, bn_link=lk1, fold=fold)
-        a, fold = self.bn2.forward_fold(y, self.conv3, stats=st, link=lk2)
-        y, st = self.conv3.forward_stats(a, bn_link=lk2, fold=fold)
+        a = self.bn1(y, stats=st, link=lk1)
+        y, st = self.conv2.forward_stats(a, bn_link=lk1)
+        a = self.bn2(y, stats=st, link=lk2)
+        y, st = self.conv3.forward_stats(a, bn_link=lk2)
         if self.down_conv is not None and _DOWN_LAST:
             # created after the main path, the shortcut's backward runs first (autograd takes
             # the ready node with the highest sequence number): its strided dgrad parks at the

@@ -275,52 +275,6 @@ class _BNActFn(torch.autograd.Function):
                 None, None, None, None, None)
 
 
-class _BNFoldFn(torch.autograd.Function):
-    """The BatchNorm-apply fold (``conv.BNFold``): statistics -> coefficients only; the output is
-    a zero-stride placeholder (autograd's edge to the consuming conv), the conv normalises its
-    staged operands itself. Backward: the regular fused BN backward with the ReLU bits recomputed
-    from x (``bn_bwd(coef=...)``), its sums from the consuming conv's linked dgrad epilogue when
-    that ran (BNGradLink with ``coef``)."""
-
-    @staticmethod
-    def forward(ctx, x, weight, bias, running_mean, running_var, momentum, eps, num_batches,
-                stats, link, bacc, fold):
-        fin, part, rpb = (stats.fin, None, 0) if isinstance(stats, FinishedStats) else \
-            (None, stats[0], int(stats[1]))
-        coef, invstd = _ext.load().bn_fold_fwd(
-            x, weight, bias, running_mean, running_var, momentum, eps, num_batches, part, rpb,
-            fin, zero_b=bacc.take_zero() if bacc is not None else None)
-        ctx.facc = fin
-        ctx.bacc = bacc
-        ctx.save_for_backward(x, coef, invstd, weight)
-        ctx.affine = weight is not None
-        fold.x, fold.coef = x, coef
-        ctx.link = None
-        if link is not None:
-            link.set_bn(x, None, coef[0], bacc if _FIN_BWD else None, coef=coef)
-            ctx.link = link
-        # the output's metadata only (shape, dtype, device): nothing is stored
-        return torch.empty((), dtype=x.dtype, device=x.device).expand(x.shape)
-
-    @staticmethod
-    def backward(ctx, dy):
-        x, coef, invstd, weight = ctx.saved_tensors
-        dy = dy.contiguous(memory_format=torch.channels_last)
-        ext = ctx.link.take(dy) if ctx.link is not None else None
-        ready = bool(ext) and isinstance(ext[0], str)   # ("acc", sums): the conv summed
-        if ready:
-            acc_b, ext = ext[1], None
-        else:
-            acc_b = ctx.bacc.for_backward(x, x.shape[1]) \
-                if (ctx.bacc is not None and not ext and _FIN_BWD) else None
-        dx, _, dgamma, dbeta, _ = _ext.load().bn_bwd(dy, None, x, coef[0], invstd, weight, True,
-                                                  False, ctx.affine, ext[0] if ext else None,
-                                                  ext[1] if ext else 0, acc_b=acc_b,
-                                                  zero_f=ctx.facc, acc_ready=ready, coef=coef)
-        return (dx, dgamma if ctx.affine else None, dbeta if ctx.affine else None, None, None,
-                None, None, None, None, None, None, None)
-
-
 def bn_act(x, residual=None, weight=None, bias=None, running_mean=None, running_var=None,
            training=True, momentum=0.1, eps=1e-5, relu=True):
     """Functional form of :class:`BatchNormAct2d`."""
@@ -372,25 +326,6 @@ class BatchNormAct2d(nn.BatchNorm2d):
         return _BNActFn.apply(x, residual, self.weight, self.bias, rm, rv, training, mom,
                               self.eps, self.relu, None, None, join, link, res_out, res_in,
                               self._bacc)
-
-    def forward_fold(self, x: torch.Tensor, consumer, stats=None, link=None):
-        """``(out, fold)`` for a ReLU BN whose output only feeds ``consumer`` (a
-        ``Conv2dNHWC``): when the BatchNorm-apply fold applies (training, statistics from the
-        producing conv, the consumer's shape has fold-capable kernels), ``out`` is a placeholder
-        and ``fold`` the ``conv.BNFold`` to hand to ``consumer.forward_stats(out, fold=fold)``:
-        the output is never written, the conv normalises its staged operands. Otherwise the
-        regular forward: ``(self(x, stats=stats, link=link), None)``."""
-        ok = (self.relu and self.training and self.track_running_stats
-              and self.momentum is not None and stats is not None and kernel_ok(x)
-              and x.dtype == torch.bfloat16 and x.shape[1] <= conv._FOLD_MAX_C
-              and torch.is_grad_enabled() and consumer.fold_plan(x) is not None)
-        if not ok:
-            return self(x, stats=stats, link=link), None
-        fold = conv.BNFold()
-        out = _BNFoldFn.apply(x, self.weight, self.bias, self.running_mean, self.running_var,
-                              self.momentum, self.eps, self.num_batches_tracked, stats, link,
-                              self._bacc, fold)
-        return out, fold
 
 
 # ------------------------------------------------------------------------------------------------

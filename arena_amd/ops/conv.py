@@ -35,15 +35,10 @@ TILES.update({12: (256, 128), 13: (256, 64), 14: (256, 128), 15: (256, 64)})
 # bit-reproducible): for the layers whose tile count leaves CUs idle (14x14 / 7x7 at batch 128)
 KSPLITS = (2, 3, 4, 6, 8)
 TILES.update({v + 16 * (k - 1): TILES[v] for v in range(16) for k in KSPLITS})
-# + 256 * p (p = 1..4, unsplit tiles only): the persistent form, 2^p output tiles of one column
-# tile per block -- the block's BatchNorm sums are merged in LDS and flushed once (see
-# conv_kernels.hip conv_fwd_body), and the per-block prologue is paid once per 2^p tiles
-PERSIST = (1, 2, 3, 4)
-TILES.update({v + 256 * p: TILES[v] for v in range(16) for p in PERSIST})
 # 4096 + i: the v2 tile kernel (conv_kernels.hip conv2_body): 32x32x16 MFMAs, 8-wave 256-row
 # tiles (4-wave 128x128), two K steps in flight, epilogue through an fp32 LDS tile. Forward and
 # backward-data (incl. the strided phases): plain, masked addend, BatchNorm statistics, BatchNorm-
-# backward partials or sums (BNGradLink); never persistent (split-K forms: V2_KSPLITS below).
+# backward partials or sums (BNGradLink).
 V2 = 4096
 V2_TILES = {V2 + 0: (256, 128), V2 + 1: (256, 256), V2 + 2: (128, 128), V2 + 3: (256, 64),
             V2 + 4: (128, 256), V2 + 5: (128, 64), V2 + 6: (64, 64), V2 + 7: (64, 128),
@@ -57,27 +52,8 @@ HALO_MAX_W = 63
 HALO_SMALL = {V2 + 14: 31}
 V2_TILES.update(V2_HALO)
 TILES.update(V2_TILES)
-# + 16 * (k - 1) on a v2 code: the same tile with its K steps (halo forms: its 64-channel chunks)
-# split over k blocks; each slice writes an fp32 slab, the last to arrive (ticket per tile) sums
-# them in slice order and runs the epilogue -- bit-reproducible. For the layers whose tiles leave
-# CUs idle: the 14x14 / 7x7 stages at batch 128, where one 128x128 tile's K loop of 16-72 steps is
-# the whole launch (conv_kernels.hip conv2_body, split-K hand-off).
-V2_KSPLITS = (2, 3, 4, 6, 8)
-TILES.update({v + 16 * (k - 1): TILES[v] for v in V2_TILES for k in V2_KSPLITS})
 _V2_ON = os.environ.get("ARENA_CONV_V2", "1") != "0"
-# Not offered to the autotuner by default (ARENA_CONV_V2SPLIT=1 does): on every ResNet-50 layer at
-# batch 128 the split forms lost to the unsplit tiles -- 2048->512 @7 forward 37.2 vs 28.1 us,
-# 3x3 512 @7 43.6 vs 41.4, the rest by 1.3-2.5x (profiles/r5_split_plan_sc1.log; step 12.276 vs
-# 12.200 ms, r5_split_ab_sc1.jsonl). These layers are bound by each CU's L2->LDS rate over its
-# tiles, which a split does not change (docs/perf.md, round 5), and the hand-off adds a slab
-# round trip to every tile's tail.
-_V2_SPLIT_ON = os.environ.get("ARENA_CONV_V2SPLIT", "0") == "1"
 _CUS = 256
-
-
-def v2_base(v: int) -> int:
-    """The unsplit v2 code of a v2 variant (``v`` itself for v1 codes)."""
-    return V2 + (v - V2) % 16 if v >= V2 else v
 
 
 def kvariant(v: int, ks: int) -> int:
@@ -86,17 +62,7 @@ def kvariant(v: int, ks: int) -> int:
 
 
 def split_of(v: int) -> int:
-    return v % 256 // 16 + 1
-
-
-def tiles_per_block(v: int) -> int:
-    return 1 if v >= V2 else 1 << (v // 256)
-
-
-def set_v2_split(on: bool) -> None:
-    """A/B switch: offer the v2 split-K forms to the autotuner (part of the plan key)."""
-    global _V2_SPLIT_ON
-    _V2_SPLIT_ON = bool(on)
+    return 1 if v >= V2 else v // 16 + 1
 
 
 def set_v2(on: bool) -> None:
@@ -118,29 +84,6 @@ def halo_variants_for(cout: int, k, stride: int, pad: int, width: int):
         return []
     return [v for v, (_, bn) in V2_HALO.items()
             if cout % bn == 0 and width <= HALO_SMALL.get(v, HALO_MAX_W)]
-
-
-_PERSIST_ON = os.environ.get("ARENA_CONV_PERSIST", "1") != "0"
-
-
-def set_persist(on: bool) -> None:
-    """A/B switch: offer the persistent forms to the autotuner (part of the plan key)."""
-    global _PERSIST_ON
-    _PERSIST_ON = bool(on)
-
-
-def persist_variants_for(m: int, cout: int, bases):
-    """Persistent forms of the tile variants ``bases`` that keep at least one block per CU."""
-    out = []
-    if not _PERSIST_ON:
-        return out
-    for v in bases:
-        if v >= 16:
-            continue
-        bm, bn = TILES[v]
-        tiles = -(-m // bm) * (cout // bn)
-        out += [v + 256 * p for p in PERSIST if tiles >> p >= _CUS]
-    return out
 
 
 def out_hw(h: int, w: int, r: int, s: int, stride: int, pad: int) -> Tuple[int, int]:
@@ -186,34 +129,6 @@ def split_variants_for(m: int, cout: int, ktot: int):
     return out
 
 
-def v2_split_variants_for(m: int, cout: int, ktot: int, bases):
-    """Split-K forms of the v2 tile variants ``bases`` whose grid gives fewer than two blocks per
-    CU: the splits that bring the launch to about 1, 2 or 4 blocks per CU, with at least 4 K steps
-    per slice (halo forms: at least one 64-channel chunk, ``ktot`` = 9 C)."""
-    out = []
-    if not (_V2_ON and _V2_SPLIT_ON) or os.environ.get("ARENA_CONV_KSPLIT", "1") == "0":
-        return out
-    for v in bases:
-        if v < V2 or v != v2_base(v):
-            continue
-        bm, bn = TILES[v]
-        if cout % bn:
-            continue
-        tiles = -(-m // bm) * (cout // bn)
-        if tiles >= 2 * _CUS:
-            continue
-        cap = ktot // (9 * 64) if v in V2_HALO else ktot // 64 // 4
-        ks_set = set()
-        for want in (_CUS, 2 * _CUS, 4 * _CUS):
-            need = -(-want // tiles)
-            fits = [k for k in V2_KSPLITS if k <= cap]
-            ks = next((k for k in fits if k >= need), fits[-1] if fits else 1)
-            if ks > 1:
-                ks_set.add(ks)
-        out += [v + 16 * (k - 1) for k in sorted(ks_set)]
-    return out
-
-
 def pick_variant(m: int, cout: int) -> int:
     """Largest tile that still gives every CU at least two blocks; else the most blocks."""
     best, best_blocks = None, 0
@@ -232,7 +147,7 @@ def pick_variant(m: int, cout: int) -> int:
 def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int = -1,
                with_stats: bool = False, addend: Tensor | None = None, bn=None,
                addmask: Tensor | None = None, final: bool = False,
-               bn_acc: Tensor | None = None, pre: Tensor | None = None):
+               bn_acc: Tensor | None = None):
     """y = conv2d(x, w) (+ addend) for channels_last bf16 x [N,C,H,W] and w [Cout,C,R,S].
 
     with_stats: returns (y, (part, rpb)) where part holds per-tile BatchNorm partials of y
@@ -247,11 +162,7 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
     (that BN's fp64 [2, C] backward sums) the epilogue adds them there instead and returns
     (y, None).
     final (with with_stats): the statistics come back finished, ``(y, FinishedStats)`` -- the
-    epilogue's fp64 atomics + last-tile ticket replace the BN's finalize launch.
-    pre: the BatchNorm-apply fold (``BNFold``, v2 / halo variants): with with_stats, x is the raw
-    input of a ReLU BN and ``pre`` its fp32 [3, C] (mean, scale, shift) -- the kernel convolves
-    relu(bn(x)) without it ever being stored; with ``bn`` (backward data), ``pre`` is that BN's
-    table and its ReLU bits are recomputed from bn_x (bn_mask unused)."""
+    epilogue's fp64 atomics + last-tile ticket replace the BN's finalize launch."""
     x = x.contiguous(memory_format=torch.channels_last)
     w = w.contiguous(memory_format=torch.channels_last)
     if variant < 0:
@@ -266,8 +177,7 @@ def conv2d_fwd(x: Tensor, w: Tensor, stride: int = 1, pad: int = 0, variant: int
     fin = bool(final and with_stats and bn is None and addend is None)
     out = _ext.load().conv_fwd(x, w, int(stride), int(pad), int(variant), bool(with_stats),
                                addend, bx, bm, bmu, addmask if addend is not None else None,
-                               stats_final=fin, bn_acc=bn_acc if bn is not None else None,
-                               pre=pre)
+                               stats_final=fin, bn_acc=bn_acc if bn is not None else None)
     if bn is not None and bn_acc is not None:
         return out[0], None          # the sums went into the caller's bn_acc
     if fin:
@@ -288,8 +198,7 @@ def flip_weight(w: Tensor) -> Tensor:
 
 def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1,
                     addend: Tensor | None = None, bn=None, wflip: Tensor | None = None,
-                    addmask: Tensor | None = None, bn_acc: Tensor | None = None,
-                    pre: Tensor | None = None):
+                    addmask: Tensor | None = None, bn_acc: Tensor | None = None):
     """dX (+ addend) of a stride-1 convolution (same spatial size when pad = (R-1)/2).
     With ``bn`` (see conv2d_fwd) returns (dX, (part, rpb)): the backward partials of the
     BatchNorm layer whose output is this convolution's input. ``wflip``: ``flip_weight(w)``
@@ -297,7 +206,7 @@ def conv2d_bwd_data(dy: Tensor, w: Tensor, pad: int, variant: int = -1,
     r = w.shape[2]
     wf = wflip if wflip is not None else flip_weight(w)
     return conv2d_fwd(dy, wf, 1, r - 1 - pad, variant, addend=addend, bn=bn, addmask=addmask,
-                      bn_acc=bn_acc, pre=pre)
+                      bn_acc=bn_acc)
 
 
 # On by default since the v2 tiles carry the partials in their coalesced store loop and the plan
@@ -333,43 +242,13 @@ _ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_ACC_MAX_PAIRS", str(4 << 20)))
 _LINK_ACC_MAX_PAIRS = int(os.environ.get("ARENA_BN_LINK_ACC_MAX_PAIRS", str(_ACC_MAX_PAIRS)))
 
 
-# ARENA_BN_LINK_CHOICE=1: per layer, the tuner prices the link -- the linked dgrad's extra
-# epilogue time against the BN backward's own reduction pass over (dy, x) (``_bn_reduce_us``) --
-# and links only where the epilogue is cheaper. Measured, off: the reduction pass costs more than
-# the epilogue on all but one ResNet-50 layer (256-channel input @56: 57 us of epilogue vs a 93 us
-# pass), the one it unlinked (1024 ch @14, 17.1 vs 16.2 us) made the step slower, 11.947 vs 11.869
-# ms (profiles/r5_link_ab.jsonl, interleaved replays).
-_LINK_CHOICE = os.environ.get("ARENA_BN_LINK_CHOICE", "0") == "1"
-
-
-def set_link_choice(on: bool) -> None:
-    global _LINK_CHOICE
-    _LINK_CHOICE = bool(on)
-
-
-def _bn_reduce_us(x: Tensor, mask: Tensor, mean: Tensor) -> float:
-    """GPU time of the BN backward's reduction pass for an input of ``x``'s shape: the fused
-    backward with its own reduction minus the same backward fed ready sums (a linked conv's)."""
-    from .batchnorm import acc_rep
-    ext = _ext.load()
-    c = x.shape[1]
-    ones = torch.ones(c, device=x.device)
-    acc = torch.zeros(acc_rep() * 2 * c, dtype=torch.float64, device=x.device)
-    dy = torch.randn_like(x)
-    own = _time(lambda: ext.bn_bwd(dy, mask, x, mean, ones, ones, True, False, True, acc_b=acc))
-    fed = _time(lambda: ext.bn_bwd(dy, mask, x, mean, ones, ones, True, False, True, acc_b=acc,
-                                   acc_ready=True))
-    return max(0.0, own - fed)
-
-
 def set_link_acc_max_pairs(n: int) -> None:
     global _LINK_ACC_MAX_PAIRS
     _LINK_ACC_MAX_PAIRS = int(n)
 
 
 def _use_link_acc(m: int, variant: int, c: int) -> bool:
-    bm, tpb = TILES[variant][0], tiles_per_block(variant)
-    return -(-(-(-m // bm)) // tpb) * c <= _LINK_ACC_MAX_PAIRS
+    return -(-m // TILES[variant][0]) * c <= _LINK_ACC_MAX_PAIRS
 
 
 def set_acc_max_pairs(n: int) -> None:
@@ -382,8 +261,7 @@ def set_acc_max_pairs(n: int) -> None:
 def _use_acc(m: int, variant: int, cout: int) -> bool:
     """Whether a forward of ``m`` output pixels on tile variant ``variant`` sums its BatchNorm
     statistics in the epilogue (fp64 atomics, one set per block) instead of per-tile partials."""
-    bm, tpb = TILES[variant][0], tiles_per_block(variant)
-    return _BN_FINAL and -(-(-(-m // bm)) // tpb) * cout <= _ACC_MAX_PAIRS
+    return _BN_FINAL and -(-m // TILES[variant][0]) * cout <= _ACC_MAX_PAIRS
 
 
 def _out_pixels(x: Tensor, w: Tensor, stride: int, pad: int) -> int:
@@ -554,19 +432,16 @@ class BNGradLink:
     With the BN's own backward-sum set (``bacc``, batchnorm._BwdAcc) and few enough (tile,
     channel) pairs (``_use_acc``), the epilogue adds fp64 sums into that set instead of writing
     per-tile partials, and the BN's dx pass reads them directly: no reduction, no finalize."""
-    __slots__ = ("x", "mask", "mean", "bacc", "part", "rpb", "acc", "dy_ptr", "coef")
+    __slots__ = ("x", "mask", "mean", "bacc", "part", "rpb", "acc", "dy_ptr")
 
     def __init__(self):
-        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = self.coef = None
+        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = None
         self.rpb = 0
         self.dy_ptr = 0
 
-    def set_bn(self, x: Tensor, mask: Tensor | None, mean: Tensor, bacc=None,
-               coef: Tensor | None = None) -> None:
-        """``coef``: a folded BN (no output, no mask stored): its [3, C] table, from which the
-        linked epilogue recomputes the ReLU bits."""
+    def set_bn(self, x: Tensor, mask: Tensor | None, mean: Tensor, bacc=None) -> None:
         if _BN_LINKS:
-            self.x, self.mask, self.mean, self.bacc, self.coef = x, mask, mean, bacc, coef
+            self.x, self.mask, self.mean, self.bacc = x, mask, mean, bacc
 
     def ready(self) -> bool:
         return self.x is not None
@@ -586,7 +461,7 @@ class BNGradLink:
                 out = ("acc", self.acc)
             elif self.part is not None:
                 out = (self.part, self.rpb)
-        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = self.coef = None
+        self.x = self.mask = self.mean = self.bacc = self.part = self.acc = None
         self.dy_ptr = 0
         return out
 
@@ -690,17 +565,16 @@ def wgrad_variants_for(cin: int, cout: int):
 
 def conv2d_wgrad(x: Tensor, dy: Tensor, kernel: Tuple[int, int], stride: int = 1, pad: int = 0,
                  variant: int = -1, splits: int = 0, out_dtype=torch.bfloat16,
-                 scale: float = 1.0, pre: Tensor | None = None) -> Tensor:
+                 scale: float = 1.0) -> Tensor:
     """dW [Cout, C, R, S] (channels_last) of y = conv2d(x, w): split-K MFMA kernel + a
-    fixed-order slab reduction (bit-reproducible). ``pre`` (the BN fold): x is the raw input of
-    the ReLU BN with coefficient table ``pre`` and the kernel uses relu(bn(x)) as its X operand."""
+    fixed-order slab reduction (bit-reproducible)."""
     x = x.contiguous(memory_format=torch.channels_last)
     dy = dy.contiguous(memory_format=torch.channels_last)
     if variant < 0:
         variant = wgrad_variants_for(x.shape[1], dy.shape[1])[0]
     return _ext.load().conv_wgrad(x, dy, int(kernel[0]), int(kernel[1]), int(stride), int(pad),
                                   int(variant), int(splits), out_dtype == torch.float32,
-                                  float(scale), pre=pre)
+                                  float(scale))
 
 
 # ------------------------------------------------------------------------------------------------
@@ -742,57 +616,8 @@ class ConvPlan:
     # in that form, since the extra epilogue reorders the tiles (v1's 128x128 form drops to one
     # wave per SIMD, 196 VGPRs + 72 AGPRs)
     bwd_bn: object = MIOPEN
-    # the BatchNorm-apply fold (BNFold: x is a ReLU BN's raw input, normalised in the kernels'
-    # staged operands): forward with statistics, weight gradient, and the linked backward-data
-    # form with the ReLU bits recomputed -- v2 / halo variants only, timed in those forms. MIOPEN:
-    # no fold for this shape.
-    fwd_fold: object = MIOPEN
-    wgrad_fold: object = MIOPEN
-    bwd_bn_fold: object = MIOPEN
-    # whether the backward-data pass takes the BN-backward sums at all (BNGradLink): False where
-    # the tuner found the BN's own reduction pass cheaper than the linked epilogue
-    link: bool = True
     tuned: bool = False
     times: Dict[str, float] = field(default_factory=dict)
-
-    def fold_ok(self) -> bool:
-        return self.fwd_fold != MIOPEN and self.wgrad_fold != MIOPEN
-
-
-# BatchNorm-apply fold (ARENA_BN_FOLD=1; see batchnorm.BatchNormAct2d.forward_fold): a ReLU BN
-# whose output only feeds one convolution is never materialised -- the conv stages the BN's input
-# and applies relu(fma(x - mean, scale, shift)) to each staged chunk in LDS (forward A operand,
-# weight-gradient X operand); the BN backward and the linked dgrad epilogue recompute the ReLU
-# bits from x. Geometry: 1x1 / stride 1 / unpadded (the generic v2 tiles) or 3x3 / stride 1 /
-# pad 1 at <= 63 wide (the halo tiles), C <= 512. OFF by default: measured slower on ResNet-50
-# (12.305 vs 11.867 ms per step, profiles/r5_fold_ab.jsonl). Each staged chunk is transformed by
-# every tile that stages it -- Cout/BN times in a 1x1 forward, once per tap and column tile in the
-# weight gradient -- where the apply pass transforms each element once; per layer the fold forms
-# cost more than the apply pass they remove (docs/perf.md, round 5).
-_BN_FOLD = os.environ.get("ARENA_BN_FOLD", "0") == "1"
-_FOLD_MAX_C = 512
-
-
-def set_bn_fold(on: bool) -> None:
-    global _BN_FOLD
-    _BN_FOLD = bool(on)
-
-
-def bn_fold_enabled() -> bool:
-    return _BN_FOLD
-
-
-def fold_geometry_ok(cin: int, k, stride: int, pad: int, width: int) -> bool:
-    k = tuple(k)
-    return cin <= _FOLD_MAX_C and _V2_ON and (
-        (k == (1, 1) and stride == 1 and pad == 0)
-        or (k == (3, 3) and stride == 1 and pad == 1 and width <= HALO_MAX_W))
-
-
-def _fold_fwd_variants(cout: int, k, stride: int, pad: int, width: int):
-    if tuple(k) == (1, 1):
-        return v2_variants_for(cout)
-    return halo_variants_for(cout, k, stride, pad, width)
 
 
 _PLANS: Dict[tuple, ConvPlan] = {}
@@ -861,8 +686,8 @@ def _best(t: dict, kind: str, n: int):
 
 
 def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
-    key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _PERSIST_ON,
-           _V2_ON, _BN_LINKS, _BN_FOLD, _V2_SPLIT_ON, _LINK_CHOICE)
+    key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _V2_ON,
+           _BN_LINKS)
     plan = _PLANS.get(key)
     if plan is not None and (plan.tuned or torch.cuda.is_current_stream_capturing()):
         return plan
@@ -882,14 +707,6 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                      else -1) if "bwd" in dirs else MIOPEN)
         plan.wgrad = wg[len(wg) // 2] if (wg and "wgrad" in dirs) else MIOPEN
         plan.bwd_bn = plan.bwd if stride == 1 else MIOPEN
-        if _BN_FOLD and fold_geometry_ok(cin, k, stride, pad, x.shape[3]) and \
-                "fwd" in dirs and "wgrad" in dirs and wg:
-            fv = _fold_fwd_variants(cout, k, stride, pad, x.shape[3])
-            bv = v2_variants_for(cin) + halo_variants_for(cin, k, stride, pad, x.shape[3])
-            # the serial four-wave v2 tiles (V2 + 8 / 9) / the widest halo form
-            pick = lambda vs: next((v for v in (V2 + 8, V2 + 9, V2 + 14, V2 + 13)  # noqa: E731
-                                    if v in vs), MIOPEN)
-            plan.fwd_fold, plan.bwd_bn_fold, plan.wgrad_fold = pick(fv), pick(bv), plan.wgrad
         plan.tuned = mode == "ours"
     else:
         def tune() -> dict:
@@ -946,79 +763,16 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
             for c in wg:
                 fns[("wgrad", c)] = (lambda c=c: _time(
                     lambda: conv2d_wgrad(x, dy, k, stride, pad, c[0], c[1])))
-            # the BN fold's forms (BNFold): identity coefficients (relu(x)) -- the timing does not
-            # depend on the values
-            fold = _BN_FOLD and fold_geometry_ok(cin, k, stride, pad, x.shape[3])
-            coef = None
-            if fold:
-                coef = torch.stack([torch.zeros(cin), torch.ones(cin), torch.zeros(cin)]).to(
-                    device=x.device, dtype=torch.float32).contiguous()
-
-                def fwdpre_time(v):
-                    fin = _use_acc(m_out, v, cout)
-                    us = _time(lambda: conv2d_fwd(x, w, stride, pad, v, with_stats=True,
-                                                  final=fin, pre=coef))
-                    return us if fin else us + _FIN_PENALTY_US
-
-                for v in _fold_fwd_variants(cout, k, stride, pad, x.shape[3]):
-                    fns[("fwdpre", v)] = (lambda v=v: fwdpre_time(v))
             ext = _ext.load()
             ext.bn_acc_scratch(True)
             try:
                 for key_, fn in fns.items():
                     t[key_] = fn()
-                # persistent forms of the fastest base variants
-                for v in persist_variants_for(m_out, cout, _best(t, "fwd", 3)):
-                    fns[("fwd", v)] = (lambda v=v: fwd_time(v))
-                    t[("fwd", v)] = fns[("fwd", v)]()
-                if stride == 1:
-                    for v in persist_variants_for(m_in, cin, _best(t, "bwd", 3)):
-                        fns[("bwd", v)] = (lambda v=v: _time(
-                            lambda: conv2d_bwd_data(dy, w, pad, v)))
-                        t[("bwd", v)] = fns[("bwd", v)]()
-                # split-K forms of the 3 fastest v2 tiles (+ the 256x128 tile: the most FLOPs
-                # per staged byte) where their grid under-fills the chip
-                def v2_top(kind):
-                    return [c for c in _best(t, kind, 64) if c >= V2][:3] + [V2]
-
-                for v in v2_split_variants_for(m_out, cout, cin * k[0] * k[1], v2_top("fwd")):
-                    fns[("fwd", v)] = (lambda v=v: fwd_time(v))
-                    t[("fwd", v)] = fns[("fwd", v)]()
-                if stride == 1:
-                    ktot_b = cout * k[0] * k[1]
-                    for v in v2_split_variants_for(m_in, cin, ktot_b, v2_top("bwd")):
-                        fns[("bwd", v)] = (lambda v=v: _time(
-                            lambda: conv2d_bwd_data(dy, w, pad, v)))
-                        t[("bwd", v)] = fns[("bwd", v)]()
-                    if _BN_LINKS:
-                        for v in v2_split_variants_for(m_in, cin, ktot_b, v2_top("bwdbn")):
-                            acc = bsums if _use_link_acc(m_in, v, cin) else None
-                            fns[("bwdbn", v)] = (lambda v=v, acc=acc: _time(
-                                lambda: conv2d_bwd_data(dy, w, pad, v, bn=(bnx, bmask, bmean),
-                                                        bn_acc=acc)))
-                            t[("bwdbn", v)] = fns[("bwdbn", v)]()
-                if fold:
-                    # the fold's weight gradient: the 3 fastest plain candidates in the pre form
-                    for c in _best(t, "wgrad", 3):
-                        fns[("wgradpre", c)] = (lambda c=c: _time(lambda: conv2d_wgrad(
-                            x, dy, k, stride, pad, c[0], c[1], pre=coef)))
-                        t[("wgradpre", c)] = fns[("wgradpre", c)]()
-                    # the linked backward-data form with the ReLU bits recomputed (v2 / halo)
-                    if _BN_LINKS and stride == 1:
-                        v2bn = [c for c in _best(t, "bwdbn", 64)
-                                if c >= V2 and c == v2_base(c)][:3]   # the fold never splits
-                        for v in v2bn:
-                            acc = bsums if _use_link_acc(m_in, v, cin) else None
-                            fns[("bwdbnpre", v)] = (lambda v=v, acc=acc: _time(
-                                lambda: conv2d_bwd_data(dy, w, pad, v, bn=(bnx, None, bmean),
-                                                        bn_acc=acc, pre=coef)))
-                            t[("bwdbnpre", v)] = fns[("bwdbnpre", v)]()
                 # One timing per candidate picks the lucky one among near-equal variants (the
                 # choices moved run to run by ~1 % of the step): the 3 fastest of each direction are
                 # timed twice more, interleaved, and ranked by their median.
-                kinds = ("fwd", "bwd", "wgrad") + tuple(
-                    kd for kd in ("bwdbn", "fwdpre", "wgradpre", "bwdbnpre")
-                    if any(k_[0] == kd for k_ in fns))
+                kinds = ("fwd", "bwd", "wgrad") + (("bwdbn",) if any(k_[0] == "bwdbn" for k_ in fns)
+                                                   else ())
                 finals = {kind: _best(t, kind, 3) for kind in kinds}
                 reps = {(kind, c): [t[(kind, c)]] for kind, cs in finals.items() for c in cs}
                 for _ in range(2):
@@ -1026,28 +780,20 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                         reps[key_].append(fns[key_]())
                 for key_, vs in reps.items():
                     t[key_] = sorted(vs)[1]
-                if _LINK_CHOICE and "bwdbn" in kinds and "bwd" in kinds:
-                    t[("reduce", "bn")] = _bn_reduce_us(bnx, bmask, bmean)
             finally:
                 ext.bn_acc_scratch(False)
             out = {}
-            names = {"bwdbn": "bwd_bn", "fwdpre": "fwd_fold", "wgradpre": "wgrad_fold",
-                     "bwdbnpre": "bwd_bn_fold"}
+            names = {"bwdbn": "bwd_bn"}
             for kind in kinds:
                 best = min(t[(kind, c)] for c in finals[kind])
                 choice = next(c for c in finals[kind] if t[(kind, c)] == best)
                 out[names.get(kind, kind)] = choice
-            if ("reduce", "bn") in t:
-                linked = t[("bwdbn", out["bwd_bn"])]
-                plain = t[("bwd", out["bwd"])] + t[("reduce", "bn")]
-                out["link"] = bool(linked <= plain)
             out["times"] = {f"{kd}:{c}": round(v, 1) for (kd, c), v in t.items()}
             return out
 
         # one decision per job: rank 0 times, every rank adopts (or the ARENA_CONV_PLAN file)
         got = planstore.decide("conv", key[:4] + key[5:], x.device, tune)
-        for f in ("fwd", "bwd", "wgrad", "bwd_bn", "fwd_fold", "wgrad_fold", "bwd_bn_fold",
-                  "link"):
+        for f in ("fwd", "bwd", "wgrad", "bwd_bn"):
             if f in got:
                 v = got[f]
                 setattr(plan, f, tuple(v) if isinstance(v, list) else v)
@@ -1207,32 +953,11 @@ class _nullctx:
         return False
 
 
-class BNFold:
-    """A ReLU BatchNorm folded into the convolution that consumes its output (see ``_BN_FOLD``):
-    the BN's forward (``BatchNormAct2d.forward_fold``) fills ``x`` (its raw input) and ``coef``
-    (its [3, C] mean / scale / shift) and returns a zero-stride placeholder of the output's shape
-    that only carries autograd; the conv reads ``x`` and normalises its staged operands with
-    ``coef``, and its backward-data result is the BN output's gradient, which flows back into the
-    BN's backward as usual."""
-    __slots__ = ("x", "coef")
-
-    def __init__(self):
-        self.x = self.coef = None
-
-
 class _ConvFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, w, stride, pad, plan, want_stats, join=None, bn_link=None, fold=None):
+    def forward(ctx, x, w, stride, pad, plan, want_stats, join=None, bn_link=None):
         part = x.new_empty(0, dtype=torch.float32)
-        ctx.pre = None
-        if fold is not None:
-            # x is the folded BN's placeholder: convolve relu(bn(fold.x)) in the kernel
-            x, ctx.pre = fold.x, fold.coef
-            fin = _use_acc(_out_pixels(x, w, stride, pad), plan.fwd_fold, w.shape[0])
-            y, st = conv2d_fwd(x, w, stride, pad, plan.fwd_fold, with_stats=True, final=fin,
-                               pre=ctx.pre)
-            part = st.fin if fin else st[0]
-        elif plan.fwd == MIOPEN:
+        if plan.fwd == MIOPEN:
             y = F.conv2d(x, w, stride=stride, padding=pad)
         elif want_stats and _use_acc(_out_pixels(x, w, stride, pad), plan.fwd,
                                      w.shape[0]):
@@ -1242,7 +967,7 @@ class _ConvFn(torch.autograd.Function):
             y, (part, _) = conv2d_fwd(x, w, stride, pad, plan.fwd, with_stats=True)
         else:
             y = conv2d_fwd(x, w, stride, pad, plan.fwd)
-        ctx.save_for_backward(x, w, ctx.pre)
+        ctx.save_for_backward(x, w)
         ctx.conf = (stride, pad, plan)
         ctx.w_leaf = w.is_leaf
         # W' of a WeightFlipper scope (flipped this step, before this forward)
@@ -1259,8 +984,8 @@ class _ConvFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy, _dpart):
         if dy is None:
-            return None, None, None, None, None, None, None, None, None
-        x, w, pre = ctx.saved_tensors
+            return None, None, None, None, None, None, None, None
+        x, w = ctx.saved_tensors
         stride, pad, plan = ctx.conf
         dy = dy.contiguous(memory_format=torch.channels_last)
         dx = dw = None
@@ -1278,10 +1003,8 @@ class _ConvFn(torch.autograd.Function):
             lk = ctx.bn_link
             # the BN partials need the COMPLETE gradient of x: not from a join's first arriver
             use_bn = (lk is not None and plan.bwd != MIOPEN and stride == 1
-                      and (plan.link or lk.coef is not None)
                       and lk.x.shape == x.shape
-                      and (join is None or other is not None)
-                      and (lk.coef is None or plan.bwd_bn_fold != MIOPEN))
+                      and (join is None or other is not None))
             if plan.bwd == MIOPEN:
                 dx = _miopen_bwd(dy, x, w, stride, pad, [True, False, False])[0]
                 if other is not None:
@@ -1290,22 +1013,18 @@ class _ConvFn(torch.autograd.Function):
                 dx = conv2d_bwd_data_strided(dy, w, (x.shape[2], x.shape[3]), stride, pad,
                                              plan.bwd, addend=other)
             elif use_bn:
-                if lk.coef is not None:   # a folded BN: v2 / halo form, bits from its table
-                    vb = plan.bwd_bn_fold
-                else:
-                    vb = plan.bwd if plan.bwd_bn == MIOPEN else plan.bwd_bn
+                vb = plan.bwd if plan.bwd_bn == MIOPEN else plan.bwd_bn
                 m_in = x.shape[0] * x.shape[2] * x.shape[3]
                 if lk.bacc is not None and _use_link_acc(m_in, vb, x.shape[1]):
                     acc = lk.bacc.for_backward(x, x.shape[1])
                     dx, _ = conv2d_bwd_data(dy, w, pad, vb, addend=other,
                                             bn=(lk.x, lk.mask, lk.mean), wflip=ctx.wflip,
-                                            addmask=omask, bn_acc=acc, pre=lk.coef)
+                                            addmask=omask, bn_acc=acc)
                     lk.publish_acc(acc, dx)
                 else:
                     dx, (part, rpb) = conv2d_bwd_data(dy, w, pad, vb, addend=other,
                                                       bn=(lk.x, lk.mask, lk.mean),
-                                                      wflip=ctx.wflip, addmask=omask,
-                                                      pre=lk.coef)
+                                                      wflip=ctx.wflip, addmask=omask)
                     lk.publish(part, rpb, dx)
             else:
                 dx = conv2d_bwd_data(dy, w, pad, plan.bwd, addend=other, wflip=ctx.wflip,
@@ -1319,11 +1038,7 @@ class _ConvFn(torch.autograd.Function):
                 side = _side_stream(dy.device)
                 side.wait_stream(main)   # dy, x (and w) are complete on the main stream
             with torch.cuda.stream(side) if side is not None else _nullctx():
-                if pre is not None:        # the folded BN's output as the X operand
-                    v, sp = plan.wgrad_fold
-                    dw = conv2d_wgrad(x, dy, (w.shape[2], w.shape[3]), stride, pad, v, sp,
-                                      out_dtype=w.dtype, pre=pre)
-                elif plan.wgrad == MIOPEN:
+                if plan.wgrad == MIOPEN:
                     dw = _miopen_bwd(dy, x, w, stride, pad, [False, True, False])[1]
                 else:
                     v, sp = plan.wgrad
@@ -1334,7 +1049,7 @@ class _ConvFn(torch.autograd.Function):
                 x.record_stream(side)
                 dy.record_stream(side)
                 dw.record_stream(main)
-        return dx, dw, None, None, None, None, None, None, None
+        return dx, dw, None, None, None, None, None, None
 
 
 class Conv2dNHWC(nn.Conv2d):
@@ -1353,43 +1068,12 @@ class Conv2dNHWC(nn.Conv2d):
     def forward(self, x: Tensor) -> Tensor:
         return self.forward_stats(x, want_stats=False)[0]
 
-    def fold_plan(self, x: Tensor):
-        """The plan for input ``x`` (the raw input of a ReLU BN about to be folded into this
-        conv) when the fold applies to this conv and shape, else None. Tunes on first use."""
-        if not (_BN_FOLD and x.is_cuda and _mode() != "off" and x.dtype == torch.bfloat16
-                and self.training and torch.is_grad_enabled()):
-            return None
-        w = self.weight
-        if w.dtype != torch.bfloat16:
-            if not (torch.is_autocast_enabled("cuda")
-                    and torch.get_autocast_dtype("cuda") == torch.bfloat16):
-                return None
-            w = w.to(torch.bfloat16)
-        s, p = self.stride[0], self.padding[0]
-        if not fold_geometry_ok(x.shape[1], (w.shape[2], w.shape[3]), s, p, x.shape[3]):
-            return None
-        plan = plan_for(x.contiguous(memory_format=torch.channels_last),
-                        w.contiguous(memory_format=torch.channels_last), s, p)
-        return plan if plan.fold_ok() else None
-
     def forward_stats(self, x: Tensor, want_stats: bool = True, join: GradJoin | None = None,
-                      bn_link: BNGradLink | None = None, fold: BNFold | None = None):
+                      bn_link: BNGradLink | None = None):
         """(y, stats): ``stats`` are the BatchNorm partials of y for ``BatchNormAct2d(y,
         stats=stats)`` when the kernel produced y (else None: the BN computes them itself).
         ``join``: x has a second consumer registered on the same GradJoin (see there).
-        ``bn_link``: x is the output of the BatchNorm layer that filled this link.
-        ``fold``: x is the placeholder of a folded BN's output (``BatchNormAct2d.forward_fold``
-        after ``fold_plan`` accepted it): the kernels convolve relu(bn(fold.x))."""
-        if fold is not None:
-            w = self.weight
-            if w.dtype != torch.bfloat16:
-                w = w.to(torch.bfloat16)
-            w = w.contiguous(memory_format=torch.channels_last)
-            s, p = self.stride[0], self.padding[0]
-            plan = plan_for(fold.x, w, s, p)
-            with torch.autocast("cuda", enabled=False):
-                y, part = _ConvFn.apply(x, w, s, p, plan, True, join, bn_link, fold)
-            return y, _stats_out(want_stats, part, TILES[plan.fwd_fold][0])
+        ``bn_link``: x is the output of the BatchNorm layer that filled this link."""
         if not x.is_cuda or _mode() == "off":
             return super().forward(x), None
         amp = torch.is_autocast_enabled("cuda") and \

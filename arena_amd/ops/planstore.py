@@ -14,7 +14,8 @@ slowest rank sets a synchronous step) and different fp32 accumulation orders. So
   inside :func:`rank_local`, or the job sets ``ARENA_CONV_PLAN_SHARE=0``;
 * **persisted plans**: ``ARENA_CONV_PLAN=<path>`` names a JSON file of plans keyed by
   (kind, GPU arch, kernel-source hash, shape, stride, pad, mode flags). A plan found there is used
-  without timing anything; plans decided in this run are merged into it by global rank 0. Plans
+  without timing anything; plans decided in this run are merged into it by global rank 0. In a
+  shared world only rank 0 consults the file and every decision is broadcast, hit or miss. Plans
   of a different build of the kernels (another source hash) never match;
 * the time spent tuning is accumulated (:func:`stats`) and printed by the benchmarks.
 """
@@ -139,28 +140,32 @@ def _shared_world():
 
 
 def decide(kind: str, key: tuple, device, tune: Callable[[], dict]) -> dict:
-    """The plan (a JSON-able dict) for ``key``: from the plan file, else tuned by rank 0 and
-    broadcast to every rank (or tuned locally in a world of one / inside :func:`rank_local`)."""
-    _load_file()
+    """The plan (a JSON-able dict) for ``key``: from the plan file, else tuned -- in a shared world
+    by rank 0 ALONE, which then broadcasts ``(from_file, plan)`` to every rank. Only rank 0 reads
+    the file there, and every call is a broadcast, so the collective sequence is the same on every
+    rank whatever each rank's copy of the file holds (a node-local file on a multi-node job, or a
+    file rank 0 is still writing while a slow rank loads it, cannot desynchronise the ranks)."""
     fkey = file_key(kind, key, device)
-    hit = _FILE.get(fkey)
-    if hit is not None:
-        _STATS["file_hits"] += 1
-        return hit
     sw = _shared_world()
-    value = None
+    value, from_file = None, False
     if sw is None or sw[0] == 0:
-        t0 = time.perf_counter()
-        value = tune()
-        _STATS["tune_s"] += time.perf_counter() - t0
-        _STATS["tuned"] += 1
+        _load_file()
+        value = _FILE.get(fkey)
+        from_file = value is not None
+        if not from_file:
+            t0 = time.perf_counter()
+            value = tune()
+            _STATS["tune_s"] += time.perf_counter() - t0
+            _STATS["tuned"] += 1
     if sw is not None:
         import torch.distributed as dist
-        box = [value]
+        box = [(from_file, value)]
         dist.broadcast_object_list(box, src=0)
-        value = box[0]
+        from_file, value = box[0]
         _STATS["shared" if sw[0] == 0 else "received"] += 1
-    if _writer():
+    if from_file:
+        _STATS["file_hits"] += 1
+    elif _writer():
         try:
             _save(fkey, value)
         except OSError as e:

@@ -240,7 +240,8 @@ def _state_layout(opt) -> list:
             for k in sorted(st, key=str):
                 v = st[k]
                 if torch.is_tensor(v):
-                    out.append((gi, pi, k, "t", (tuple(v.shape), str(v.dtype).split(".")[-1])))
+                    out.append((gi, pi, k, "t", (tuple(v.shape), str(v.dtype).split(".")[-1],
+                                                 v.device.type)))
                 else:
                     out.append((gi, pi, k, "v", v))
     return out
@@ -284,14 +285,19 @@ def broadcast_optimizer_state(optimizer, root_rank: int = 0) -> None:
             if kind == "v":
                 st[k] = meta
                 continue
-            shape, dtname = meta
+            shape, dtname, devtype = meta
             have = st.get(k)
             dt = getattr(torch, dtname)
-            if not (torch.is_tensor(have) and tuple(have.shape) == shape and have.dtype == dt):
-                # torch keeps Adam's scalar "step" on the CPU unless capturable/fused
-                dev = have.device if torch.is_tensor(have) else (
-                    torch.device("cpu") if (k == "step" and shape == ()) else p.device)
-                st[k] = torch.zeros(shape, dtype=dt, device=dev)
+            # the ROOT's device type decides where the tensor lives (torch keeps Adam's scalar
+            # "step" on the CPU unless fused/capturable, then on the parameter's device): the
+            # broadcast groups tensors by (dtype, device), so a rank whose copy lives elsewhere
+            # would enter collectives of different sizes than the root
+            dev = torch.device("cpu") if devtype == "cpu" else (
+                p.device if p.device.type == devtype else torch.device(devtype))
+            if not (torch.is_tensor(have) and tuple(have.shape) == shape and have.dtype == dt
+                    and have.device.type == devtype):
+                st[k] = (have.to(dev) if torch.is_tensor(have) and tuple(have.shape) == shape
+                         and have.dtype == dt else torch.zeros(shape, dtype=dt, device=dev))
     broadcast_parameters(_optimizer_state_tensors(optimizer), root_rank)
 
 

@@ -198,6 +198,9 @@ class XgmiComm:
             ok, err_msg = 0, repr(e)
         self._epoch = torch.zeros(ext.ccl_max_blocks, dtype=torch.int32, device="cuda")
         self._err = torch.zeros(1, dtype=torch.int32, device="cuda")
+        self._ptrs = ptrs
+        self.selftest_result: dict = {}
+        self.form = "pull"
         if ok:
             self.peers = ext.XgmiPeers(ptrs["buf"], ptrs.get("buf2", []), ptrs["sig"], self._epoch,
                                        self._err, self.staging_elems, self.param_elems, self.rank,
@@ -208,7 +211,7 @@ class XgmiComm:
         torch.cuda.synchronize()
         self._agree(ok, f"hipIpc mapping failed: {err_msg}")
         if selftest:
-            self._selftest()
+            self._selftest_all()
 
     # --------------------------------------------------------------------------------- setup
     def _agree(self, ok: int, why: str) -> None:
@@ -219,24 +222,212 @@ class XgmiComm:
             self.close()
             raise XgmiUnavailable(why if not ok else "a peer rank failed")
 
-    def _selftest(self) -> None:
-        ok, why = 1, ""
-        try:
-            tot = sum(range(1, self.world + 1))
-            for n in (4, 1000, min(self.staging_elems, 300004)):
-                base = (torch.arange(n, device="cuda", dtype=torch.float32) % 977)
-                x = base * (self.rank + 1)
-                out = torch.empty_like(x)
-                self.all_reduce_(x, out=out)
+    def _selftest_all(self) -> None:
+        """Run every kernel kind this communicator will serve on known data and agree on the
+        outcome collectively. The pull form (the default: no kernel stores into a peer's buffer) is
+        tested unless ``ARENA_XGMI_PUSH=1`` asks for the push form, which is kept only if ITS test
+        passes on every rank (otherwise the pull form is tested and used). Any pull failure raises
+        :class:`XgmiUnavailable` on every rank, so callers fall back to RCCL at construction
+        instead of meeting a bad kernel mid-run. Result: ``selftest_result`` {kernel: "ok" or the
+        failure}, ``form`` ("pull" / "push")."""
+        forms = ["push", "pull"] if os.environ.get("ARENA_XGMI_PUSH", "0") == "1" else ["pull"]
+        for form in forms:
+            self.peers.push = form == "push"
+            res = self._selftest()
+            everyone = [None] * self.world
+            dist.all_gather_object(everyone, res, group=self.group)
+            merged = {}
+            for r, d in enumerate(everyone):
+                for k, v in d.items():
+                    if v != "ok" and k not in merged:
+                        merged[k] = f"rank {r}: {v}"
+                    merged.setdefault(k, "ok")
+            self.selftest_result = merged
+            bad = [k for k, v in merged.items() if v != "ok"]
+            if not bad:
+                self.form = form
+                log.info("xGMI self-test passed (%s form): %s", form, ", ".join(merged))
+                return
+            log.warning("xGMI self-test of the %s form failed: %s", form,
+                        "; ".join(f"{k}: {merged[k]}" for k in bad))
+            if "timeout" in bad:
+                break       # a barrier timed out: the flag protocol itself is broken
+        self.peers.push = False
+        self.close()
+        raise XgmiUnavailable("xGMI self-test failed: " + "; ".join(
+            f"{k}: {v}" for k, v in self.selftest_result.items() if v != "ok"))
+
+    def _peer_view(self, key: str, r: int, n: int) -> torch.Tensor:
+        return self.ext.ccl_tensor(self._ptrs[key][r], n, self.device)
+
+    def _prewarm(self) -> None:
+        """Read every rank's registered buffers through this rank's mappings, so any line that
+        could go stale (a peer's data cached in this GPU's L2, or this rank's own lines) is
+        resident before the kernel under test runs."""
+        acc = torch.zeros((), device="cuda")
+        for key, n in (("buf", self.staging_elems), ("buf2", self.param_elems)):
+            if key in self._ptrs and n:
+                for r in range(self.world):
+                    acc += self._peer_view(key, r, n).sum()
+        torch.cuda.synchronize()
+
+    def _selftest(self) -> dict:
+        """One pass over every kernel kind; returns {kernel: "ok" | reason}. Inputs are small
+        integers (sums exact in fp32 whatever the order) and the optimizer steps use
+        power-of-two coefficients, so the expected results are bit-exact."""
+        res = {}
+        W, rk = self.world, self.rank
+        tot = W * (W + 1) // 2
+
+        def run(name, fn):
+            try:
+                self._prewarm()
+                ok = fn()
                 torch.cuda.synchronize()
-                if not torch.equal(out, base * tot):
-                    ok, why = 0, f"self-test mismatch at n={n}"
-                    break
-            if ok and int(self._err.item()):
-                ok, why = 0, "barrier timeout during self-test"
-        except Exception as e:  # noqa: BLE001
-            ok, why = 0, repr(e)
-        self._agree(ok, why)
+                res[name] = "ok" if ok else "mismatch"
+            except Exception as e:  # noqa: BLE001
+                res[name] = repr(e)[:200]
+
+        cap = self.staging_elems
+        big = min(cap, 300004) // 4 * 4
+        oneshot_max = self.ext.ccl_get_oneshot_max()
+
+        def allreduce(n):
+            base = torch.arange(n, device="cuda", dtype=torch.float32) % 977
+            for it in range(2):                      # second call reads lines the first cached
+                out = torch.empty(n, device="cuda")
+                self.all_reduce_(base * (rk + 1 + it), out=out)
+                if not torch.equal(out, base * (tot + W * it)):
+                    return False
+            stage = self._buf[:n]                    # zero-copy, in place on the staging buffer
+            stage.copy_(base * (rk + 1))
+            self.all_reduce_(stage)
+            return bool(torch.equal(stage, base * tot))
+
+        run("allreduce_oneshot", lambda: allreduce(min(1000, cap) // 4 * 4 or 4))
+        if big > oneshot_max:
+            run("allreduce_twoshot", lambda: allreduce(big))
+
+        def bcast(n):
+            for root in (0, W - 1):
+                t = (torch.arange(n, device="cuda", dtype=torch.float32) % 101) * (root + 3)
+                x = t.clone() if rk == root else torch.full((n,), -1.0, device="cuda")
+                self.broadcast_(x, root=root)
+                if not torch.equal(x, t):
+                    return False
+            return True
+
+        run("broadcast_direct", lambda: bcast(min(1000, cap) // 4 * 4 or 4))
+        if W > 2 and big > (128 << 10):
+            run("broadcast_twoshot", lambda: bcast(big))
+
+        def allgather():
+            m = min(4096, cap)
+            x = torch.arange(m, device="cuda", dtype=torch.float32) + 10000 * rk
+            got = self.all_gather(x)
+            want = torch.stack([torch.arange(m, device="cuda", dtype=torch.float32) + 10000 * q
+                                for q in range(W)])
+            return bool(torch.equal(got, want))
+
+        run("allgather", allgather)
+        if self.param_elems:
+            run("adam", self._selftest_adam)
+            run("sgd_bf16", self._selftest_sgd_bf16)
+            run("sgd_f32", self._selftest_sgd_f32)
+        if int(self._err.item()):
+            res["timeout"] = "a barrier wait timed out during the self-test"
+            self._err.zero_()
+        # leave the registered buffers as construction made them
+        self._buf.zero_()
+        if self._buf2 is not None:
+            self._buf2.zero_()
+        torch.cuda.synchronize()
+        return res
+
+    def _grad_rows(self, n: int, step: int, scale: float = 1.0):
+        """Every rank's gradient for ``step`` (deterministic, identical on all ranks)."""
+        i = torch.arange(n, device="cuda", dtype=torch.float32)
+        return [((i * (q + 3) + 7 * step) % 17 - 8) * scale for q in range(self.world)]
+
+    def _selftest_adam(self) -> bool:
+        from ..ops import fused
+        n = min(self.staging_elems, self.param_elems, 1 << 16) // 4 * 4
+        P0 = (torch.arange(n, device="cuda", dtype=torch.float32) % 31) + 100.0
+        Pref, Mref, Vref = P0.clone(), torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+        M, V = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+        self._buf2[:n].copy_(P0)
+        for step in range(1, 3):
+            g = self._grad_rows(n, step)
+            gsum = g[0].clone()
+            for x in g[1:]:
+                gsum += x
+            t = torch.full((1,), float(step), device="cuda")
+            self._buf[:n].copy_(g[self.rank])
+            self._prewarm()
+            self.adam_(M, V, n, lr=0.25, t_step=t)
+            fused.adam_flat(Pref, Mref, Vref, gsum, lr=0.25, t_step=t)
+            torch.cuda.synchronize()
+            if not torch.allclose(self._buf2[:n], Pref, rtol=1e-6, atol=0):
+                return False
+        return True
+
+    def _selftest_sgd_bf16(self) -> bool:
+        bf = torch.bfloat16
+        words = min(self.staging_elems, self.param_elems)
+        off = 8 * 3                                      # a bucket that does not start at 0
+        n = (min(2 * words - off, 1 << 17) // 8) * 8
+        if n <= 0:
+            return True
+        wbf = self._buf2.view(bf)
+        stage = self._buf.view(bf)
+        w0 = ((torch.arange(n, device="cuda", dtype=torch.float32) % 64) - 32) * 0.125
+        master = torch.zeros(off + n, device="cuda")
+        mom = torch.zeros(off + n, device="cuda")
+        master[off:] = w0
+        wbf[off:off + n].copy_(w0.to(bf))
+        ref_w, ref_m = w0.clone(), torch.zeros(n, device="cuda")
+        lr, mu, wd = 2.0 ** -4, 0.5, 2.0 ** -10
+        for step in range(2):
+            g = self._grad_rows(n, step, 0.25)
+            stage[off:off + n].copy_(g[self.rank].to(bf))
+            gsum = g[0].clone()
+            for x in g[1:]:
+                gsum += x
+            ref_m = mu * ref_m + (gsum + wd * ref_w)
+            ref_w = ref_w - lr * ref_m
+            self._prewarm()
+            self.peers.sgd_bf16(master, mom, off, n, lr, mu, wd, 1.0)
+            torch.cuda.synchronize()
+            if not torch.equal(wbf[off:off + n], ref_w.to(bf)):
+                return False
+        lo, hi = self.ext.ccl_sgd_shard(off, n, self.world, self.rank)
+        return bool(torch.equal(master[lo:hi], ref_w[lo - off:hi - off]))
+
+    def _selftest_sgd_f32(self) -> bool:
+        words = min(self.staging_elems, self.param_elems)
+        off = 4 * 5
+        n = (min(words - off, 1 << 16) // 4) * 4
+        if n <= 0:
+            return True
+        w0 = ((torch.arange(n, device="cuda", dtype=torch.float32) % 64) - 32) * 0.125
+        self._buf2[off:off + n].copy_(w0)
+        mom = torch.zeros(n, device="cuda")
+        ref_w, ref_m = w0.clone(), torch.zeros(n, device="cuda")
+        lr, mu, wd = 2.0 ** -4, 0.5, 2.0 ** -10
+        for step in range(2):
+            g = self._grad_rows(n, step, 0.25)
+            self._buf[off:off + n].copy_(g[self.rank])
+            gsum = g[0].clone()
+            for x in g[1:]:
+                gsum += x
+            ref_m = mu * ref_m + (gsum + wd * ref_w)
+            ref_w = ref_w - lr * ref_m
+            self._prewarm()
+            self.peers.sgd_f32(mom, off, n, lr, mu, wd, 1.0)
+            torch.cuda.synchronize()
+            if not torch.equal(self._buf2[off:off + n], ref_w):
+                return False
+        return True
 
     def _free(self):
         for p in self._own:

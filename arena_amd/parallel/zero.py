@@ -23,12 +23,15 @@ parameter of the model:
 
   - ``backend="xgmi"`` (one node, every rank's GPU mapped into every rank): one kernel per
     sub-range over hipIpc peer memory (``xgmi_sgd_bf16`` / ``xgmi_sgd_f32``: fp32 sums in a fixed
-    rank order, the rank's chunk updated, rounded weights written to every rank's buffer);
+    rank order, the rank's chunk updated in its own buffer, every rank then pulling the other
+    ranks' rounded weights -- no kernel stores into a peer's memory);
   - ``backend="rccl"`` (ranks that cannot map each other: multi-pod, multi-node):
     ``reduce_scatter_tensor`` of the bucket's bf16 (or fp32) range, the ``shard_sgd`` HIP kernel
     on the owned equal-size shard, ``all_gather_into_tensor`` of the updated weights. bf16 buckets
     reduce in bf16 by default (the bytes the xGMI path moves); ``rccl_reduce_fp32=True`` reduces
-    fp32 copies instead (exact sums, twice the bytes);
+    fp32 copies instead (exact sums, twice the bytes; the default on ``hier``, whose two levels
+    would round a bf16 sum twice). Buckets launch strictly in index order on every rank, even
+    when a rank's gradients become ready in another order;
   - ``backend="hier"`` (several nodes of ``local_size`` ranks each, consecutive ranks per node):
     the same three steps in two levels -- reduce-scatter inside the node (RCCL rides xGMI there),
     reduce-scatter of that 1/L chunk between nodes, ``shard_sgd`` on the 1/W shard, all-gather
@@ -117,7 +120,7 @@ class ShardedMasterSGD:
                  weight_decay: float = 0.0, bucket_mb: float = 16.0, group=None,
                  timeout_s: float = 60.0, overlap: bool = True, backend: str = "auto",
                  order: Optional[Iterable[Tensor]] = None, last_bucket_mb: Optional[float] = None,
-                 rccl_reduce_fp32: bool = False, local_size: Optional[int] = None):
+                 rccl_reduce_fp32: Optional[bool] = None, local_size: Optional[int] = None):
         plist = list(params)
         if plist and isinstance(plist[0], dict):
             raw_groups = plist
@@ -164,16 +167,13 @@ class ShardedMasterSGD:
             raise ValueError("ShardedMasterSGD on CPU tensors runs over gloo: backend 'rccl', "
                              "'hier' or 'auto'")
         requested = backend
-        self.local_size = self._local_size(local_size)
+        self.local_size = self._local_size(local_size, strict=backend == "hier")
         if backend == "auto":
             from . import xgmi
-            backend = "xgmi" if dev.type == "cuda" and xgmi.usable(group) else "rccl"
-        if backend == "rccl" and requested == "auto" and 1 < self.local_size < self.world:
-            backend = "hier"
+            backend = "xgmi" if dev.type == "cuda" and xgmi.usable(group) else self._flat_or_hier()
         self._intra = self._inter = None
         if backend == "hier":
             self._make_level_groups()
-        self.rccl_reduce_fp32 = bool(rccl_reduce_fp32)
         model_order = self._model_order(order)
         last_mb = bucket_mb / 4 if last_bucket_mb is None else last_bucket_mb
         self.comm = None
@@ -188,8 +188,14 @@ class ShardedMasterSGD:
             except XgmiUnavailable:
                 if requested == "xgmi":
                     raise
-                backend = "rccl"
+                backend = self._flat_or_hier()
+                if backend == "hier":
+                    self._make_level_groups()
         self.backend = backend
+        # default: bf16 ring sums on the flat RCCL backend (the bytes xGMI moves), fp32 on the
+        # hierarchical one, whose two levels would otherwise round the sum twice
+        self.rccl_reduce_fp32 = (backend == "hier") if rccl_reduce_fp32 is None \
+            else bool(rccl_reduce_fp32)
         if self.comm is None:
             # RCCL layout: sub-ranges padded to world x 16-byte slots (equal, aligned shards)
             self._form_buckets(model_order, kind_of, bucket_mb, last_mb, pad_to=self.world)
@@ -227,6 +233,7 @@ class ShardedMasterSGD:
                 v.copy_(p)
                 p.data = v          # bf16 group: the parameter becomes bf16 (weights in the
                 p.grad = None       # flat buffer, fp32 master in self.master)
+        self._next = 0          # index of the next bucket to launch (strict bucket order)
         self.stream = torch.cuda.Stream(device=dev) if dev.type == "cuda" else None
         self._hooks = [p.register_post_accumulate_grad_hook(self._on_grad) for p in self.params]
 
@@ -286,15 +293,23 @@ class ShardedMasterSGD:
         self.t16, self.t32 = size[_BF16], size[_F32]
         self.f0 = _pad((self.t16 + 1) // 2, 4)            # fp32 region start (floats)
 
-    def _local_size(self, local_size) -> int:
+    def _local_size(self, local_size, strict: bool) -> int:
         """Ranks per node for the hierarchical backend (``LOCAL_WORLD_SIZE`` by default: torchrun
-        numbers a node's ranks consecutively); must divide the world."""
+        numbers a node's ranks consecutively). Only ``backend='hier'`` requires it to divide the
+        world; otherwise a non-dividing value (uneven nodes) just rules the hierarchy out."""
         if local_size is None:
             local_size = int(os.environ.get("LOCAL_WORLD_SIZE", self.world))
         local_size = int(local_size)
         if local_size < 1 or self.world % local_size:
-            raise ValueError(f"local_size {local_size} must divide the world size {self.world}")
+            if strict:
+                raise ValueError(f"local_size {local_size} must divide the world size "
+                                 f"{self.world}")
+            return self.world
         return local_size
+
+    def _flat_or_hier(self) -> str:
+        """The RCCL form ``auto`` picks: two-level when the job spans several equal nodes."""
+        return "hier" if 1 < self.local_size < self.world else "rccl"
 
     def _make_level_groups(self) -> None:
         """One group per node (its L consecutive ranks) and one per local rank (the same local
@@ -456,7 +471,22 @@ class ShardedMasterSGD:
                 "extra backwards inside `with opt.no_sync():`")
         b.pending.discard(id(p))
         if not b.pending and self.overlap:
+            self._launch_ready_prefix()
+
+    def _launch_ready_prefix(self) -> None:
+        """Launch buckets strictly in index order: bucket i only once 0..i-1 have launched. The
+        RCCL / hier backends need every rank to issue its collectives in the same order, and a
+        rank whose gradients arrive in another order (data-dependent control flow, an unused
+        parameter) would otherwise reduce one bucket against a peer's different one."""
+        while self._next < len(self.buckets):
+            b = self.buckets[self._next]
+            if b.pending or b.launched:
+                if b.launched:
+                    self._next += 1
+                    continue
+                return
             self._launch(b)
+            self._next += 1
 
     def _join(self) -> None:
         if self.stream is not None:
@@ -470,6 +500,7 @@ class ShardedMasterSGD:
         for b in self.buckets:
             b.launched = False
             b.pending = set(id(p) for p in b.params)
+        self._next = 0
 
     # ------------------------------------------------------------------------- optimizer API
     @contextlib.contextmanager
@@ -498,6 +529,7 @@ class ShardedMasterSGD:
         for b in self.buckets:
             b.launched = False
             b.pending = set(id(p) for p in b.params)
+        self._next = 0
         heartbeat.beat()
         return None
 

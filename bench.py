@@ -30,7 +30,10 @@ The MNIST steps run as replays of one hipGraph whose length divides the warmup, 
 count and the epoch; ``config.exec`` reports how many timed steps were replayed vs run eagerly.
 The same line also carries ``resnet50_images_per_s`` (all ranks) / ``resnet50_ms_per_step``
 (ResNet-50 bs128 per GPU, bf16, whole training step in one hipGraph, data parallel over the
-sharded xGMI optimizer at N>1; ``--resnet 0`` skips it).
+sharded xGMI optimizer at N>1; ``--resnet 0`` skips it). At N>1 it also carries ``ccl``: xGMI vs
+RCCL time and bus bandwidth per collective and size, the xGMI self-test outcome per kernel and the
+protocol form in use (``--ccl 0`` skips it). A failed ResNet or collective run at N>1 is reported
+in the line (``failed``) and the process exits 3.
 
 Rank 0 prints ONE JSON line.
 """
@@ -73,6 +76,9 @@ def parse():
                          "of the same JSON line")
     ap.add_argument("--resnet-steps", type=int, default=20)
     ap.add_argument("--resnet-batch", type=int, default=128)
+    ap.add_argument("--ccl", type=int, default=1,
+                    help="N>1: also time allreduce 4 KB..256 MB, all-gather, broadcast and one "
+                         "ResNet-sized sharded-SGD bucket through xGMI and RCCL (key 'ccl')")
     ap.add_argument("--resnet-verify-every", type=int, default=10,
                     help="N>1: replica bit-identity check every K timed ResNet steps (untimed)")
     return ap.parse_args()
@@ -116,6 +122,9 @@ def bench_resnet50(dev, steps: int, batch: int, world: int = 1, verify_every: in
     import torch.distributed as dist
     from arena_amd.examples import cnn_bench
     from arena_amd.parallel import hvd
+    if os.environ.get("ARENA_BENCH_FAIL_RESNET") == "1":
+        # test hook (tests/test_bench_gpu.py): a failed N > 1 ResNet run must fail the process
+        raise RuntimeError("injected ResNet-50 failure (ARENA_BENCH_FAIL_RESNET=1)")
     args = cnn_bench.parse(["--model", "resnet50", "--batch_size", str(batch), "--dtype", "bf16"])
     torch.backends.cudnn.benchmark = True
     if world > 1:
@@ -298,15 +307,27 @@ def main():
         extra["test_loss"] = round(tl, 5)
         extra["test_acc"] = round(ta, 5)
 
+    failed = []
     if args.resnet and args.impl == "fused":
         del tr
         torch.cuda.empty_cache()
         try:
             extra.update(bench_resnet50(dev, args.resnet_steps, args.resnet_batch, world,
                                         args.resnet_verify_every))
-        except Exception as e:   # the headline (already measured) is still reported
-            print(f"[bench] ResNet-50 extra keys failed: {e!r}", file=sys.stderr)
+        except Exception as e:   # reported in the line, then the run fails (exit 3)
+            print(f"[bench] ResNet-50 failed: {e!r}", file=sys.stderr)
             extra["resnet50_error"] = repr(e)[:300]
+            failed.append("resnet50")
+    if world > 1 and args.ccl:
+        # north-star #2: xGMI vs RCCL collective bandwidth on this node
+        from arena_amd.parallel import cclbench
+        torch.cuda.empty_cache()
+        try:
+            extra["ccl"] = cclbench.north_star(world)
+        except Exception as e:
+            print(f"[bench] collective benchmark failed: {e!r}", file=sys.stderr)
+            extra["ccl_error"] = repr(e)[:300]
+            failed.append("ccl")
 
     samples = world * cfg.batch * args.steps
     value = samples / elapsed
@@ -334,9 +355,15 @@ def main():
         if same_gpu:
             out["emulated"] = (f"{world} ranks time-sharing ONE GPU (gloo + same-device xGMI "
                                f"mappings): checks the N>1 path, not a scaling number")
+        if failed:
+            out["failed"] = failed
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    if failed:
+        # the line above still reports what was measured, but a diverged or broken N > 1 run
+        # must not look like a success to whoever checks the exit code
+        sys.exit(3)
 
 
 if __name__ == "__main__":

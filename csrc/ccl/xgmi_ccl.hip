@@ -3,25 +3,39 @@
 // The reference's allreduce jobs rely on Horovod + NCCL inside the user image (SURVEY §2.10,
 // §2.12: DistributedOptimizer gradient allreduce every step). On an 8x MI355X node every GPU has a
 // direct xGMI link to every other GPU, so instead of a ring (one link busy per hop) each rank
-// reads its 1/W chunk from ALL peers at once and writes the reduced chunk back to all of them:
-// a "two-shot" allreduce (reduce-scatter + all-gather) in ONE kernel, using all W-1 links in
-// both directions, with no host involvement (graph-capturable).
+// reads its 1/W chunk from ALL peers at once, reduces it, and then every rank reads every reduced
+// chunk from its owner: a "two-shot" allreduce (reduce-scatter + all-gather) in ONE kernel, using
+// all W-1 links in both directions, with no host involvement (graph-capturable).
 //
 // Buffers are plain hipMalloc allocations shared through hipIpc handles; the barrier flags live
 // in uncached memory (hipDeviceMallocUncached). Block b of every rank owns sub-range b of every
-// chunk, and synchronises only with block b of the other ranks:
+// chunk, and synchronises only with block b of the other ranks.
 //
-//   copy-in (own sub-range b of every chunk)    -> barrier 0 -> reduce chunk[rank] sub-range b
-//   from all ranks, write the sum to all ranks   -> barrier 1 -> copy-out sub-range b
+// PULL ONLY (default): no kernel stores into a peer's buffer. Data crosses xGMI only as loads of
+// a peer's memory issued after a barrier whose release side (buffer_wbl2 + flag store at system
+// scope) the owner passed after writing it, and whose acquire side (buffer_inv at system scope)
+// the reader passed before loading it. A remote GPU's write into a cacheable allocation that the
+// owner's XCD L2 may already hold is therefore never relied on -- that case cannot be exercised
+// by same-GPU rehearsals, so the design avoids it instead of testing it:
+//
+//   copy-in (own sub-range b of every chunk) -> barrier 0 -> reduce chunk[rank] sub-range b from
+//   all ranks into MY buffer -> barrier 1 -> pull chunk[q] sub-range b from rank q for every q
+//   -> barrier 2 (peers finished reading my chunk before my next copy-in overwrites it)
+//
+// The fused optimizer kernels (Adam, sharded SGD) need no third barrier: an owner next writes its
+// chunk of buf2 after barrier 0 of a LATER call, which no peer reaches before finishing this one.
+// The push form (owner stores its chunk into every peer's buffer, two barriers) is kept behind
+// ArenaXgmiPeers::push and used only when the communicator's self-test of it passed.
 //
 // Why that is race-free: every remote access to a rank's buffer by block b of another rank
-// happens between that rank's block b arriving at barrier 0 and at barrier 1 of the same call,
-// and the accessed ranges (chunk[rank] sub-range b) are disjoint between ranks. Flag values are
+// happens between barriers that rank's block b also takes part in, and within a phase the
+// accessed ranges (chunk[owner] sub-range b) are disjoint between ranks. Flag values are
 // per-block call counters (no reset between calls).
 //
 // xgmi_adam fuses the gradient reduce-scatter, a sharded Adam step and the parameter all-gather:
 // rank r sums chunk r of every rank's gradient, applies Adam to that chunk only (its optimizer
-// state shard), and pushes the updated parameters into every rank's parameter buffer. Bytes on
+// state shard), writes the updated parameters into its own parameter buffer, and every rank pulls
+// the other ranks' updated chunks after barrier 1 (push form: the owner stores them). Bytes on
 // the wire equal one two-shot allreduce, but the optimizer pass runs on 1/W of the vector and
 // the separate all-reduce + Adam launches disappear.
 //
@@ -125,6 +139,53 @@ __device__ __forceinline__ void copy_chunks(float* __restrict__ dst, const float
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Copies between registered buffers: U float4 slots per thread, all loads before any store.
+template <int NSRC>
+__device__ __forceinline__ void pull_range(float* const* dst, const float* const* src,
+                                           const long long* dst_off, const long long* src_off,
+                                           long long lo, long long hi, const long long* lim) {
+  constexpr int U = kU;
+  for (long long o0 = lo + threadIdx.x * 4; o0 < hi; o0 += (long long)kThreads * 4 * U) {
+    float4 v[U][NSRC];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long o = o0 + (long long)u * kThreads * 4;
+#pragma unroll
+      for (int q = 0; q < NSRC; ++q)
+        if (o < hi && o < lim[q]) v[u][q] = ld4(src[q] + src_off[q] + o);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long o = o0 + (long long)u * kThreads * 4;
+#pragma unroll
+      for (int q = 0; q < NSRC; ++q)
+        if (o < hi && o < lim[q]) st4(dst[q] + dst_off[q] + o, v[u][q]);
+    }
+  }
+}
+
+// Phase 2 of the pull protocol: after barrier 1 every owner q holds its finished chunk q in its
+// OWN buffer `src[q] + base`; this rank copies chunk q (sub-range [lo, hi) of it) from rank q
+// into `dst + base` for every q, skipping its own chunk when dst is its own buffer. Chunks are L
+// units long; elements at or past n do not exist. One load per link in flight per slot.
+template <int W>
+__device__ __forceinline__ void pull_chunks(float* dst, float* const* src, long long base,
+                                            long long n, long long L, long long lo, long long hi,
+                                            int rank, bool skip_own) {
+  float* d[W];
+  const float* sp[W];
+  long long off[W], lim[W];
+#pragma unroll
+  for (int q = 0; q < W; ++q) {
+    d[q] = dst;
+    sp[q] = src[q];
+    off[q] = base + (long long)q * L;
+    lim[q] = (skip_own && q == rank) ? 0 : n - (long long)q * L;
+  }
+  pull_range<W>(d, sp, off, off, lo, hi, lim);
+}
+
 template <int W>
 __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(ArenaXgmiPeers P,
                                                                    const float* __restrict__ in,
@@ -162,13 +223,23 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(ArenaXgmiPeers
       for (int q = 1; q < W; ++q) acc = add4(acc, v[u][q]);  // fixed order: same on all ranks
       acc.x *= scale; acc.y *= scale; acc.z *= scale; acc.w *= scale;
       if (ok[u]) {
+        if (P.push) {
 #pragma unroll
-        for (int q = 0; q < W; ++q) st4(P.buf[q] + idx[u], acc);
+          for (int q = 0; q < W; ++q) st4(P.buf[q] + idx[u], acc);
+        } else {
+          st4(mine + idx[u], acc);  // the owner's chunk stays home; peers pull it below
+        }
       }
     }
   }
   xbarrier<W>(P, 1, b, e);
-  if (out != mine) copy_chunks<W>(out, mine, n, L, lo, hi);
+  if (P.push) {
+    if (out != mine) copy_chunks<W>(out, mine, n, L, lo, hi);
+  } else {
+    pull_chunks<W>(out, P.buf, 0, n, L, lo, hi, P.rank, out == mine);
+    // peers read my chunk until here: the next call's copy-in must not overwrite it earlier
+    xbarrier<W>(P, 2, b, e);
+  }
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
@@ -250,40 +321,21 @@ __global__ __launch_bounds__(kThreads) void xgmi_adam_kernel(ArenaXgmiPeers P, f
       if (ok[u]) {
         st4(M + idx[u], m[u]);
         st4(V + idx[u], s[u]);
+        if (P.push) {
 #pragma unroll
-        for (int q = 0; q < W; ++q) st4(P.buf2[q] + idx[u], p[u]);
+          for (int q = 0; q < W; ++q) st4(P.buf2[q] + idx[u], p[u]);
+        } else {
+          st4(Pm + idx[u], p[u]);
+        }
       }
     }
   }
   xbarrier<W>(P, 1, b, e);
+  // pull: every other chunk from its owner. No third barrier: an owner next writes its chunk of
+  // buf2 after barrier 0 of a later call, which no peer reaches before this kernel has ended.
+  if (!P.push) pull_chunks<W>(Pm, P.buf2, 0, n, L, lo, hi, P.rank, true);
   counter_op(ctr);
   if (threadIdx.x == 0) P.epoch[b] = e;
-}
-
-// ---------------------------------------------------------------------------------------------
-// Copies between registered buffers: U float4 slots per thread, all loads before any store.
-template <int NSRC>
-__device__ __forceinline__ void pull_range(float* const* dst, const float* const* src,
-                                           const long long* dst_off, const long long* src_off,
-                                           long long lo, long long hi, const long long* lim) {
-  constexpr int U = kU;
-  for (long long o0 = lo + threadIdx.x * 4; o0 < hi; o0 += (long long)kThreads * 4 * U) {
-    float4 v[U][NSRC];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long o = o0 + (long long)u * kThreads * 4;
-#pragma unroll
-      for (int q = 0; q < NSRC; ++q)
-        if (o < hi && o < lim[q]) v[u][q] = ld4(src[q] + src_off[q] + o);
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long o = o0 + (long long)u * kThreads * 4;
-#pragma unroll
-      for (int q = 0; q < NSRC; ++q)
-        if (o < hi && o < lim[q]) st4(dst[q] + dst_off[q] + o, v[u][q]);
-    }
-  }
 }
 
 // Direct-pull broadcast: block b moves floats [b*S, b*S+S) of the vector.
@@ -481,13 +533,20 @@ __global__ __launch_bounds__(kThreads) void xgmi_sgd_bf16_kernel(ArenaXgmiPeers 
         st4(master + idx[u] + 4, w[u][1]);
         st4(mom + idx[u], m[u][0]);
         st4(mom + idx[u] + 4, m[u][1]);
+        if (P.push) {
 #pragma unroll
-        for (int q = 0; q < W; ++q)
-          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(P.buf2[q]) + idx[u]) = packed;
+          for (int q = 0; q < W; ++q)
+            *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(P.buf2[q]) + idx[u]) = packed;
+        } else {
+          *reinterpret_cast<uint4*>(reinterpret_cast<uint16_t*>(P.buf2[P.rank]) + idx[u]) = packed;
+        }
       }
     }
   }
   xbarrier<W>(P, 1, b, e);
+  // pull the other chunks in float units (off, n, L, S are multiples of 8 bf16 = 4 floats)
+  if (!P.push)
+    pull_chunks<W>(P.buf2[P.rank], P.buf2, off / 2, n / 2, L / 2, lo / 2, hi / 2, P.rank, true);
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
@@ -535,12 +594,17 @@ __global__ __launch_bounds__(kThreads) void xgmi_sgd_f32_kernel(ArenaXgmiPeers P
       sgd1(c, g.w, w[u].w, m[u].w);
       if (ok[u]) {
         st4(mom + idx[u], m[u]);
+        if (P.push) {
 #pragma unroll
-        for (int q = 0; q < W; ++q) st4(P.buf2[q] + off + idx[u], w[u]);
+          for (int q = 0; q < W; ++q) st4(P.buf2[q] + off + idx[u], w[u]);
+        } else {
+          st4(P.buf2[P.rank] + off + idx[u], w[u]);
+        }
       }
     }
   }
   xbarrier<W>(P, 1, b, e);
+  if (!P.push) pull_chunks<W>(P.buf2[P.rank], P.buf2, off, n, L, lo, hi, P.rank, true);
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 

@@ -130,6 +130,10 @@ struct ArenaXgmiPeers {
   long long buf_elems;                // capacity of buf[] (floats)
   long long buf2_elems;
   int rank, world;
+  // 0 (default): every kernel stores only into this rank's own buffers and peers PULL the owner's
+  // chunk after a barrier; 1: the owner pushes its chunk into every peer's buffer (one barrier
+  // less for the two-shot allreduce; used only when its own construction-time self-test passed)
+  int push;
   long long timeout_cycles;           // barrier wait bound in s_memrealtime ticks (100 MHz)
 };
 }  // extern "C"

@@ -74,7 +74,7 @@ hipError_t arena_conv_flip_multi(int, const void* const*, void* const*, const in
 hipError_t arena_conv_fwd_ex(const void*, const void*, void*, float*, const void*, const uint8_t*,
                              const void*, const uint8_t*, const float*, int, int, int, int, int,
                              int, int, int, int, int, int, int, const int*, int, int, double*,
-                             int, void*, unsigned*, int, const float*, hipStream_t);
+                             int, void*, unsigned*, hipStream_t);
 hipError_t arena_conv_fwd_phases(const void*, void*, const void*, int, int, int, int, int, int,
                                  int, int, int, int, const void* const*, const int*, const int*,
                                  const int*, const int*, const int*, const int*, const int*,
@@ -85,10 +85,7 @@ long long arena_conv_fwd_tiles(long long, int, int);
 int arena_conv_fwd_tile_rows(int);
 hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
                                int, int, int, int, int, int, int, int, int, int, int, float,
-                               const float*, hipStream_t);
-hipError_t arena_conv_wgrad_pre(const void*, const void*, float*, void*, float*, int, int, int, int,
-                                int, int, int, int, int, int, int, float, const float*,
-                                hipStream_t);
+                               hipStream_t);
 hipError_t arena_s2d_stem(const void*, void*, int, int, int, int, int, hipStream_t);
 hipError_t arena_stem_weight(const void*, void*, int, int, long long, long long, long long,
                              long long, int, hipStream_t);
@@ -116,9 +113,7 @@ hipError_t arena_bn_fwd(int, const void*, const void*, void*, uint8_t*, long lon
                         double*, int, hipStream_t);
 hipError_t arena_bn_bwd(int, const void*, const uint8_t*, const void*, void*, void*, long long, int,
                         int, float*, int, double*, unsigned*, ArenaBNBwd, double*, int, double*,
-                        int, int, const void*, const float*, double*, hipStream_t);
-hipError_t arena_bn_fold_fwd(long long, int, const double*, float*, int, long long, double*,
-                             unsigned*, ArenaBNStats, double*, int, hipStream_t);
+                        int, const void*, const float*, double*, hipStream_t);
 int arena_bn_acc_ok(long long, int);
 hipError_t arena_bn_pool_fwd(int, const void*, void*, uint8_t*, void*, int, int, int, int, int, int,
                              int, ArenaBNStats, const double*, const float*, int, long long,
@@ -876,11 +871,10 @@ unsigned* conv_tickets(const Tensor& like, int64_t tiles) {
   return p;
 }
 
-// conv variant code: tile/pipeline variant (0..15) + 16 * (ksplit - 1) + 256 * p, where p > 0
-// selects the persistent form with 2^p output tiles per block (not with split-K); 4096 + i: the v2
-// tile kernel's variant i, + 16 * (ksplit - 1) for its split-K form
+// conv variant code: v1 tile/pipeline variant (0..15) + 16 * (ksplit - 1); 4096 + i: the v2 tile
+// kernel's variant i (never split)
 struct ConvSplit {
-  int base = 0, ks = 1, tpb = 1;
+  int base = 0, ks = 1;
   Tensor ws;
   unsigned* cnt = nullptr;
 };
@@ -888,18 +882,13 @@ struct ConvSplit {
 ConvSplit conv_split(const Tensor& x, int64_t variant, int64_t M, int64_t Cout, int64_t Ktot) {
   ConvSplit s;
   TORCH_CHECK(variant >= 0, "conv: bad variant ", variant);
-  if (variant >= 4096) {   // v2 tile kernel (conv_kernels.hip conv2_body): 4096 + i + 16 (ks - 1)
-    const int64_t r = variant - 4096;
-    TORCH_CHECK(r % 16 < 15 && r / 16 < 8, "conv: unknown v2 variant ", variant);
-    s.base = 4096 + (int)(r % 16);
-    s.ks = (int)(r / 16) + 1;
-  } else {
+  if (variant >= 4096) {   // v2 tile kernel (conv_kernels.hip conv2_body): 4096 + i
+    TORCH_CHECK(variant - 4096 < 15, "conv: unknown v2 variant ", variant);
+    s.base = (int)variant;
+  } else {   // v1 tile i (0..15), its K steps split over ks blocks: i + 16 (ks - 1)
+    TORCH_CHECK(variant < 256, "conv: unknown variant ", variant);
     s.base = (int)(variant % 16);
-    s.ks = (int)(variant % 256 / 16) + 1;
-    const int p = (int)(variant / 256);
-    TORCH_CHECK(p <= 4 && (p == 0 || s.ks == 1), "conv: bad persistent variant ", variant);
-    s.tpb = 1 << p;
-    TORCH_CHECK(s.base <= 15, "conv: variant ", variant, " is not a tile variant");
+    s.ks = (int)(variant / 16) + 1;
     TORCH_CHECK((s.base & 1) || Cout % 128 == 0, "conv: variant ", variant,
                 " needs Cout % 128 == 0 (Cout = ", Cout, ")");
   }
@@ -1033,86 +1022,14 @@ std::vector<Tensor> bn_fwd(Tensor x, OptT res, OptT gamma, OptT beta, OptT runni
 // into it and the dx pass derives its coefficients from it (no finalize launch); the sums stay in
 // place until the layer's next bn_fwd(zero_b=acc_b). Without it a pool set and a finalize are used.
 // zero_f (optional): the forward's statistics sums (bn_fwd's acc output), zeroed by the dx pass.
-// BatchNorm-apply fold, forward (training): the statistics of x from the producing conv (stats_fin
-// fp64 [2, C] sums, or stats_part per-tile partials of stats_rpb rows), and ONLY the coefficients:
-// returns (coef [3, C] = mean, scale, shift -- the consuming conv's `pre` table --, invstd). The
-// running statistics and num_batches are updated; zero_b (optional): this layer's backward sums,
-// cleared; stats_fin stays in place until bn_bwd(zero_f=stats_fin).
-std::vector<Tensor> bn_fold_fwd(Tensor x, OptT gamma, OptT beta, OptT running_mean,
-                                OptT running_var, double momentum, double eps, OptT num_batches,
-                                OptT stats_part, int64_t stats_rpb, OptT stats_fin, OptT zero_b) {
-  const BNGeom g = bn_geom(x, "x");
-  auto f32 = x.options().dtype(torch::kFloat32);
-  Tensor coef = torch::empty({3, g.C}, f32), invstd = torch::empty({g.C}, f32);
-  ArenaBNStats st{};
-  st.eps = (float)eps;
-  st.momentum = (float)momentum;
-  st.gamma = bn_vec(gamma, g.C, "weight");
-  st.beta = bn_vec(beta, g.C, "bias");
-  st.mean = coef.data_ptr<float>();
-  st.scale = st.mean + g.C;
-  st.shift = st.mean + 2 * g.C;
-  st.invstd = invstd.data_ptr<float>();
-  if (running_mean.has_value() || running_var.has_value()) {
-    TORCH_CHECK(running_mean.has_value() && running_var.has_value(),
-                "running_mean and running_var go together");
-    st.running_mean = const_cast<float*>(bn_vec(running_mean, g.C, "running_mean"));
-    st.running_var = const_cast<float*>(bn_vec(running_var, g.C, "running_var"));
-  }
-  if (num_batches.has_value()) {
-    check_dev(*num_batches, "num_batches_tracked");
-    TORCH_CHECK(num_batches->scalar_type() == torch::kInt64 && num_batches->numel() == 1,
-                "num_batches_tracked must be an int64 scalar tensor");
-    st.batches = reinterpret_cast<long long*>(num_batches->data_ptr<int64_t>());
-  }
-  const bool fin = stats_fin.has_value() && stats_fin->defined();
-  TORCH_CHECK(fin != (stats_part.has_value() && stats_part->defined()),
-              "bn_fold_fwd: give the statistics as stats_fin sums or as stats_part partials");
-  Tensor lvl2;
-  unsigned* tickets = nullptr;
-  int nblk = 0;
-  if (fin) {
-    TORCH_CHECK(stats_fin->is_cuda() && stats_fin->device() == x.device() &&
-                    stats_fin->scalar_type() == torch::kFloat64 && stats_fin->is_contiguous() &&
-                    stats_fin->numel() == kRep * 2 * g.C,
-                "bn_fold_fwd: stats_fin must be a contiguous fp64 [kRep, 2, C] set");
-  } else {
-    check_f32(*stats_part, "stats_part");
-    TORCH_CHECK(stats_rpb > 0 && stats_part->is_contiguous(), "stats_part: bad layout");
-    nblk = (int)((g.M + stats_rpb - 1) / stats_rpb);
-    TORCH_CHECK(stats_part->numel() == (int64_t)nblk * 2 * g.C, "stats_part has ",
-                stats_part->numel(), " floats, expected ", (int64_t)nblk * 2 * g.C);
-    lvl2 = bn_lvl2(nblk, g.C, x);
-    tickets = bn_tickets(x);
-  }
-  double* zb = nullptr;
-  int nzb = 0;
-  if (zero_b.has_value() && zero_b->defined()) {
-    TORCH_CHECK(zero_b->is_cuda() && zero_b->device() == x.device() &&
-                    zero_b->scalar_type() == torch::kFloat64 && zero_b->is_contiguous(),
-                "zero_b must be a contiguous fp64 tensor on x's device");
-    zb = zero_b->data_ptr<double>();
-    nzb = (int)zero_b->numel();
-  }
-  check_hip(arena_bn_fold_fwd(g.M, (int)g.C, fin ? stats_fin->data_ptr<double>() : nullptr,
-                              fin ? nullptr : stats_part->data_ptr<float>(), nblk,
-                              (long long)stats_rpb,
-                              lvl2.defined() ? lvl2.data_ptr<double>() : nullptr, tickets, st, zb,
-                              nzb, cur_stream()),
-            "bn_fold_fwd");
-  return {coef, invstd};
-}
-
-// coef (optional, a folded layer: bn_fold_fwd's [3, C] mean / scale / shift): the ReLU bits are
-// recomputed from x with the forward's arithmetic instead of read from mask.
 // x2 / mean2 / acc2 (optional): the dx pass also adds the backward sums of a second BN whose input
 // is x2 and whose gradient is this layer's masked dy (a downsample block's down_bn) into acc2,
 // that layer's own [kRep, 2, C] set -- where the pass derives its coefficients from sums, with
 // ReLU and no residual output. Returns (dx, dres, dgamma, dbeta, acc2 if it was filled).
 std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor invstd, OptT gamma,
                            bool relu, bool with_res, bool affine_grads, OptT ext_part,
-                           int64_t ext_rpb, OptT acc_b, OptT zero_f, bool acc_ready, OptT coef,
-                           OptT x2, OptT mean2, OptT acc2) {
+                           int64_t ext_rpb, OptT acc_b, OptT zero_f, bool acc_ready, OptT x2,
+                           OptT mean2, OptT acc2) {
   const BNGeom g = bn_geom(x, "x");
   bn_same(x, dy, "grad_output");
   const bool sum2 = x2.has_value() && x2->defined();
@@ -1126,12 +1043,7 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
                     acc2->numel() == kRep * 2 * g.C,
                 "bn_bwd: acc2 must be a contiguous fp64 [kRep, 2, C] set on x's device");
   }
-  const bool mask_x = relu && coef.has_value() && coef->defined();
-  if (mask_x) {
-    check_f32(*coef, "coef");
-    TORCH_CHECK(coef->is_contiguous() && coef->numel() == 3 * g.C,
-                "bn_bwd: coef must be a contiguous fp32 [3, C] table");
-  } else if (relu) {
+  if (relu) {
     TORCH_CHECK(mask.has_value() && mask->is_cuda() && mask->scalar_type() == torch::kUInt8 &&
                     mask->is_contiguous() && mask->numel() == g.M * g.C / 8 &&
                     mask->device() == x.device(),
@@ -1156,10 +1068,6 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
   b.ca = co.data_ptr<float>();
   b.cb = b.ca + g.C;
   b.cc = b.cb + g.C;
-  if (mask_x) {
-    b.scale = coef->data_ptr<float>() + g.C;
-    b.shift = coef->data_ptr<float>() + 2 * g.C;
-  }
   Tensor part;
   int ext_nblk = 0;
   if (ext_part.has_value()) {
@@ -1217,14 +1125,14 @@ std::vector<Tensor> bn_bwd(Tensor dy, OptT mask, Tensor x, Tensor mean, Tensor i
   Tensor dres = with_res ? torch::empty_like(x) : Tensor();
   // the second BN's sums ride along only where the dx pass derives its coefficients from sums
   // (fin_dx) on the plain ReLU path; else the caller's second BN reduces itself
-  const bool use2 = sum2 && fin_dx == 1 && relu && !with_res && !mask_x;
+  const bool use2 = sum2 && fin_dx == 1 && relu && !with_res;
   check_hip(arena_bn_bwd(g.dtype, dy.data_ptr(),
-                         relu && !mask_x ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(),
+                         relu ? mask->data_ptr<uint8_t>() : nullptr, x.data_ptr(),
                          dx.data_ptr(), with_res ? dres.data_ptr() : nullptr, g.M, g.C,
                          relu ? 1 : 0, part.defined() ? part.data_ptr<float>() : nullptr, ext_nblk,
                          lvl2.defined() ? lvl2.data_ptr<double>() : nullptr, tickets, b,
                          acc.defined() ? acc.data_ptr<double>() : nullptr, fin_dx, zf, nzf,
-                         mask_x ? 1 : 0, use2 ? x2->data_ptr() : nullptr,
+                         use2 ? x2->data_ptr() : nullptr,
                          use2 ? mean2->data_ptr<float>() : nullptr,
                          use2 ? acc2->data_ptr<double>() : nullptr, cur_stream()),
             "bn_bwd");
@@ -1398,14 +1306,9 @@ void pool_check(const Tensor& t, const char* name) {
 // stats_final (with with_stats, forward statistics only): the second output is the fp64 [2][Cout]
 // accumulator set (sum y, sum y^2) the epilogue added into, for bn_fwd(stats_fin=...), instead of
 // the per-tile partials.
-// pre (optional, the BatchNorm-apply fold; v2 / halo variants): x is the raw input of a ReLU BN
-// layer whose output the conv consumes, pre = that layer's fp32 [3, C] (mean, scale, shift); the
-// kernel normalises its staged A operand (forward with statistics of a 1x1 / stride 1 / unpadded or
-// a 3x3 halo conv). With bn_x (the backward-data form): pre = [3, Cout] of the BN whose output
-// gradient y is, and its ReLU bits are recomputed from bn_x (bn_mask unused).
 std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, int64_t variant,
                              bool with_stats, OptT addend, OptT bn_x, OptT bn_mask,
-                             OptT bn_mean, OptT addmask, bool stats_final, OptT bn_acc, OptT pre) {
+                             OptT bn_mean, OptT addmask, bool stats_final, OptT bn_acc) {
   TORCH_CHECK(x.is_cuda() && w.is_cuda() && x.dim() == 4 && w.dim() == 4,
               "conv_fwd: x and w must be 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && w.scalar_type() == torch::kBFloat16,
@@ -1469,16 +1372,6 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                     addmask->numel() == y.numel() / 8,
                 "conv_fwd: addmask needs an addend and numel(y) / 8 uint8 bytes");
   }
-  const bool has_pre = pre.has_value() && pre->defined();
-  if (has_pre) {
-    check_f32(*pre, "pre");
-    const int64_t pc = bn_x.has_value() ? Cout : C;
-    TORCH_CHECK(pre->is_contiguous() && pre->numel() == 3 * pc && variant >= 4096 && with_stats &&
-                    !addend.has_value(),
-                "conv_fwd: pre must be a contiguous fp32 [3, ", pc, "] table, with a v2 / halo "
-                "variant and with_stats, no addend");
-    TORCH_CHECK(bn_x.has_value() || C <= 512, "conv_fwd: the BN fold takes C <= 512");
-  }
   check_hip(arena_conv_fwd_ex(x.data_ptr(), w.data_ptr(), y.data_ptr(),
                               part.defined() ? part.data_ptr<float>() : nullptr,
                               addend.has_value() ? addend->data_ptr() : nullptr,
@@ -1491,8 +1384,7 @@ std::vector<Tensor> conv_fwd(Tensor x, Tensor w, int64_t stride, int64_t pad, in
                               (int)N, (int)H, (int)W, (int)C, (int)Cout, (int)R, (int)S,
                               (int)stride, (int)pad, (int)pad, 0, 0, nullptr, 0, ks.base,
                               acc_t.defined() ? acc_t.data_ptr<double>() : nullptr, ks.ks,
-                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, ks.tpb,
-                              has_pre ? pre->data_ptr<float>() : nullptr, cur_stream()),
+                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, cur_stream()),
             "conv_fwd");
   if (acc_t.defined()) return {y, acc_t};
   if (with_stats) return {y, part};
@@ -1655,8 +1547,7 @@ std::vector<Tensor> conv_fwd_ex(Tensor x, Tensor w, int64_t stride, int64_t pad_
                               (int)stride, (int)pad_h, (int)pad_w, (int)Ho, (int)Wo,
                               y_out.has_value() ? map6.data() : nullptr, c16 ? 1 : 0,
                               ks.base, fin ? acc_t.data_ptr<double>() : nullptr, ks.ks,
-                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, ks.tpb, nullptr,
-                              cur_stream()),
+                              ks.ks > 1 ? ks.ws.data_ptr() : nullptr, ks.cnt, cur_stream()),
             "conv_fwd_ex");
   if (fin) return {y, acc_t};
   if (with_stats) return {y, part};
@@ -1764,7 +1655,7 @@ Tensor conv_wgrad_ex(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, 
                                 out_fp32 ? dw.data_ptr<float>() : nullptr, (int)N, (int)H, (int)W,
                                 (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad_h,
                                 (int)pad_w, (int)Ho, (int)Wo, c16 ? 1 : 0, (int)variant,
-                                (int)splits_hint, (float)scale, nullptr, cur_stream()),
+                                (int)splits_hint, (float)scale, cur_stream()),
             "conv_wgrad_ex");
   return dw;
 }
@@ -1826,10 +1717,8 @@ Tensor stem_weight_grad(Tensor dw16, Tensor w) {
 }
 
 // dW of an NHWC convolution: [Cout, C, R, S] channels_last, bf16 (for MasterSGD) or fp32.
-// pre (optional, the BN fold): x is the raw input of the ReLU BN layer whose output the conv
-// consumed, pre its fp32 [3, C] (mean, scale, shift); X = relu(fma(x - mean, scale, shift)).
 Tensor conv_wgrad(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int64_t pad,
-                  int64_t variant, int64_t splits_hint, bool out_fp32, double scale, OptT pre) {
+                  int64_t variant, int64_t splits_hint, bool out_fp32, double scale) {
   TORCH_CHECK(x.is_cuda() && dy.is_cuda() && x.dim() == 4 && dy.dim() == 4,
               "conv_wgrad: x and dy must be 4-D GPU tensors");
   TORCH_CHECK(x.scalar_type() == torch::kBFloat16 && dy.scalar_type() == torch::kBFloat16,
@@ -1858,18 +1747,12 @@ Tensor conv_wgrad(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int
   Tensor dw = torch::empty({Cout, C, R, S}, x.options()
                                                 .dtype(out_fp32 ? torch::kFloat32 : torch::kBFloat16)
                                                 .memory_format(at::MemoryFormat::ChannelsLast));
-  const bool has_pre = pre.has_value() && pre->defined();
-  if (has_pre) {
-    check_f32(*pre, "pre");
-    TORCH_CHECK(pre->is_contiguous() && pre->numel() == 3 * C,
-                "conv_wgrad: pre must be a contiguous fp32 [3, C] table");
-  }
-  check_hip(arena_conv_wgrad_pre(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(),
-                                 out_fp32 ? nullptr : dw.data_ptr(),
-                                 out_fp32 ? dw.data_ptr<float>() : nullptr, (int)N, (int)H, (int)W,
-                                 (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad,
-                                 (int)variant, (int)splits_hint, (float)scale,
-                                 has_pre ? pre->data_ptr<float>() : nullptr, cur_stream()),
+  check_hip(arena_conv_wgrad_ex(x.data_ptr(), dy.data_ptr(), ws.data_ptr<float>(),
+                                out_fp32 ? nullptr : dw.data_ptr(),
+                                out_fp32 ? dw.data_ptr<float>() : nullptr, (int)N, (int)H, (int)W,
+                                (int)C, (int)Cout, (int)R, (int)S, (int)stride, (int)pad, (int)pad,
+                                0, 0, 0, (int)variant, (int)splits_hint, (float)scale,
+                                cur_stream()),
             "conv_wgrad");
   return dw;
 }
@@ -2037,6 +1920,8 @@ class XgmiPeers {
   }
 
   int64_t world() const { return p_.world; }
+  bool push() const { return p_.push != 0; }
+  void set_push(bool on) { p_.push = on ? 1 : 0; }
 
  private:
   ArenaXgmiPeers p_;
@@ -2070,21 +1955,16 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("invstd"), py::arg("gamma"), py::arg("relu"), py::arg("with_res"),
         py::arg("affine_grads"), py::arg("ext_part") = py::none(), py::arg("ext_rpb") = 0,
         py::arg("acc_b") = py::none(), py::arg("zero_f") = py::none(),
-        py::arg("acc_ready") = false, py::arg("coef") = py::none(), py::arg("x2") = py::none(),
+        py::arg("acc_ready") = false, py::arg("x2") = py::none(),
         py::arg("mean2") = py::none(), py::arg("acc2") = py::none());
-  m.def("bn_fold_fwd", &bn_fold_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"),
-        py::arg("running_mean"), py::arg("running_var"), py::arg("momentum"), py::arg("eps"),
-        py::arg("num_batches"), py::arg("stats_part") = py::none(), py::arg("stats_rpb") = 0,
-        py::arg("stats_fin") = py::none(), py::arg("zero_b") = py::none());
   m.def("conv_fwd", &conv_fwd, py::arg("x"), py::arg("w"), py::arg("stride"), py::arg("pad"),
         py::arg("variant"), py::arg("with_stats"), py::arg("addend") = py::none(),
         py::arg("bn_x") = py::none(), py::arg("bn_mask") = py::none(),
         py::arg("bn_mean") = py::none(), py::arg("addmask") = py::none(),
-        py::arg("stats_final") = false, py::arg("bn_acc") = py::none(),
-        py::arg("pre") = py::none());
+        py::arg("stats_final") = false, py::arg("bn_acc") = py::none());
   m.def("conv_wgrad", &conv_wgrad, py::arg("x"), py::arg("dy"), py::arg("R"), py::arg("S"),
         py::arg("stride"), py::arg("pad"), py::arg("variant"), py::arg("splits_hint"),
-        py::arg("out_fp32"), py::arg("scale"), py::arg("pre") = py::none());
+        py::arg("out_fp32"), py::arg("scale"));
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_set_fin_max_blocks", [](int64_t p) { arena_bn_set_fin_max_blocks((int)p); });
@@ -2145,7 +2025,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
       .def("allgather", &XgmiPeers::allgather)
       .def("sgd_bf16", &XgmiPeers::sgd_bf16)
       .def("sgd_f32", &XgmiPeers::sgd_f32)
-      .def_property_readonly("world", &XgmiPeers::world);
+      .def_property_readonly("world", &XgmiPeers::world)
+      .def_property("push", &XgmiPeers::push, &XgmiPeers::set_push);
 #ifdef ARENA_TIMELINE
   m.def("timeline_read", [](bool clear) {
     auto t = torch::empty({4, 1024, 16}, torch::TensorOptions().dtype(torch::kInt64));

@@ -577,69 +577,6 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
   }
 }
 
-// ------------------------------------------------------------------------- BN-apply fold
-// The layer's output is never written: the consuming convolution normalises its staged operand
-// (conv_kernels.hip ConvArgs::pre) from st.mean / st.scale / st.shift, which the binding places
-// back to back as one [3][C] table. This pass only produces them. FIN: from the fp64 sums, with
-// apply_coefs' arithmetic (so the conv's operand equals the unfused apply's output bit for bit),
-// plus the running statistics and the batch counter; else the partial-merge finalize kernel
-// already wrote them. Block 0 also clears `zero` (the layer's backward sums of the last step).
-template <bool FIN>
-__global__ __launch_bounds__(kT) void bn_fold_coef_kernel(ArenaBNStats st,
-                                                          const double* __restrict__ fin,
-                                                          long long M, int C,
-                                                          double* __restrict__ zero, int nzero) {
-  zero_duty(zero, nzero);
-  if constexpr (FIN) {
-    const int c = blockIdx.x * kT + threadIdx.x;
-    if (c >= C) return;
-    const double inv_m = 1.0 / (double)M;
-    double s1, s2;
-    acc_sums(fin, C, c, s1, s2);
-    const double mean = s1 * inv_m;
-    const double d = s2 - s1 * mean;
-    const double m2 = d > 0.0 ? d : 0.0;
-    const float inv = (float)(1.0 / sqrt(m2 * inv_m + (double)st.eps));
-    const float mu = (float)mean;
-    st.mean[c] = mu;
-    st.invstd[c] = inv;
-    st.scale[c] = (st.gamma ? st.gamma[c] : 1.f) * inv;
-    st.shift[c] = st.beta ? st.beta[c] : 0.f;
-    if (st.running_mean) {
-      const float mom = st.momentum;
-      const double unbiased = M > 1 ? m2 / (double)(M - 1) : m2 * inv_m;
-      st.running_mean[c] = (1.f - mom) * st.running_mean[c] + mom * mu;
-      st.running_var[c] = (1.f - mom) * st.running_var[c] + mom * (float)unbiased;
-    }
-    if (c == 0 && st.batches != nullptr) *st.batches += 1;
-  }
-}
-
-// ReLU bits of a folded layer's output, recomputed from its input x with the forward's arithmetic
-// and rounding (the bits bn_apply's store_pos would have stored)
-template <typename T>
-__device__ __forceinline__ uint32_t relu_bits_from_x(const float xv[kVec], const float mu[kVec],
-                                                     const float sc[kVec], const float sh[kVec]) {
-  float o[kVec];
-#pragma unroll
-  for (int i = 0; i < kVec; ++i) o[i] = fmaxf(fmaf(xv[i] - mu[i], sc[i], sh[i]), 0.f);
-  uint32_t b = 0;
-  if constexpr (sizeof(T) == 2) {
-#pragma unroll
-    for (int i = 0; i < kVec; i += 2) {
-      const uint32_t w = V8<uint16_t>::pack2(o[i], o[i + 1]);
-      const uint32_t lo = w & 0xffffu, hi = w >> 16;
-      b |= ((lo & 0x8000u) == 0 && (lo & 0x7fffu) != 0 && (lo & 0x7fffu) <= 0x7f80u ? 1u : 0u) << i;
-      b |= ((hi & 0x8000u) == 0 && (hi & 0x7fffu) != 0 && (hi & 0x7fffu) <= 0x7f80u ? 1u : 0u)
-           << (i + 1);
-    }
-  } else {
-#pragma unroll
-    for (int i = 0; i < kVec; ++i) b |= (o[i] > 0.f ? 1u : 0u) << i;
-  }
-  return b;
-}
-
 // ---------------------------------------------------------------------------- backward sums
 // g = RELU ? dy * mask : dy;  per channel: sum g, sum g * (x - mean).  part: [nblk][2][C]
 // bn_bwd_finish: the backward finalize of channel c from its sums (sum g, sum g (x - mean)).
@@ -656,9 +593,7 @@ __device__ __forceinline__ void bn_bwd_finish(const ArenaBNBwd& out, int c, doub
 }
 
 // acc != null (acc mode): the block sums go to acc [2][C]; else the per-block partials to part.
-// MX (with RELU): the ReLU bits come from x and the forward's coefficients (a folded layer, whose
-// output and mask were never stored) instead of `mask`
-template <typename T, bool RELU, bool MX = false>
+template <typename T, bool RELU>
 __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__ dy,
                                                            const uint8_t* __restrict__ mask,
                                                            const T* __restrict__ x, long long M,
@@ -669,19 +604,12 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
   const Geo q = geo(C);
   long long r0, r1;
   block_rows(M, rpb, &r0, &r1);
-  float sg[kVec], sgx[kVec], mu[kVec], fsc[MX ? kVec : 1], fsh[MX ? kVec : 1];
+  float sg[kVec], sgx[kVec], mu[kVec];
 #pragma unroll
   for (int i = 0; i < kVec; ++i) sg[i] = sgx[i] = 0.f;
   if (q.slot < q.rip) {
 #pragma unroll
     for (int i = 0; i < kVec; ++i) mu[i] = out.mean[q.g * kVec + i];
-    if constexpr (MX) {
-#pragma unroll
-      for (int i = 0; i < kVec; ++i) {
-        fsc[i] = out.scale[q.g * kVec + i];
-        fsh[i] = out.shift[q.g * kVec + i];
-      }
-    }
     const long long off = (long long)q.g * kVec;
     long long r = r0 + q.slot;
     for (; r + q.rip < r1; r += 2LL * q.rip) {  // 2 rows per step: all loads in flight
@@ -692,12 +620,8 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
         const long long rr = r + (long long)u * q.rip;
         const long long p = rr * C + off;
         V8<T>::load(dy + p, d[u]);
-        if (RELU && !MX) mb[u] = mask[rr * (C / kVec) + q.g];
+        if (RELU) mb[u] = mask[rr * (C / kVec) + q.g];
         V8<T>::load(x + p, v[u]);
-      }
-      if constexpr (RELU && MX) {
-#pragma unroll
-        for (int u = 0; u < 2; ++u) mb[u] = relu_bits_from_x<T>(v[u], mu, fsc, fsh);
       }
 #pragma unroll
       for (int u = 0; u < 2; ++u)
@@ -712,9 +636,8 @@ __global__ __launch_bounds__(kT) void bn_bwd_reduce_kernel(const T* __restrict__
       float d[kVec], v[kVec];
       const long long p = r * C + off;
       V8<T>::load(dy + p, d);
-      uint32_t mb = (RELU && !MX) ? (uint32_t)mask[r * (C / kVec) + q.g] : 0xffu;
+      const uint32_t mb = RELU ? (uint32_t)mask[r * (C / kVec) + q.g] : 0xffu;
       V8<T>::load(x + p, v);
-      if constexpr (RELU && MX) mb = relu_bits_from_x<T>(v, mu, fsc, fsh);
 #pragma unroll
       for (int i = 0; i < kVec; ++i) {
         const float g = ((mb >> i) & 1u) ? d[i] : 0.f;
@@ -803,13 +726,11 @@ __global__ __launch_bounds__(kT) void bn_bwd_finalize_kernel(const float* __rest
 // multiplied instead of divided); block 0 writes dgamma / dbeta. The sums are left in place: the layer's
 // next forward apply pass zeroes them (arena_bn_fwd `zero`).
 // dynamic shared memory: 4 * C floats
-// MX (with RELU): ReLU bits from x and the forward's coefficients (folded layer, see the reduction)
-// dynamic shared memory: 6 * C floats with MX
-// S2 (RELU, FIN, no RES / MX): the same pass also sums (g, g (x2 - mean2)) per channel into acc2
+// S2 (RELU, FIN, no RES): the same pass also sums (g, g (x2 - mean2)) per channel into acc2
 // [ARENA_ACC_REP][2][C] -- the backward sums of a second BN whose gradient is this layer's masked
 // dy g: a downsample block's down_bn, the residual of this bn3 (see batchnorm.ResidualMask). Its
 // own reduction pass (dy, mask and x2 read again) then does not run.
-template <typename T, bool RELU, bool RES, bool NT, bool FIN, bool MX = false, bool S2 = false>
+template <typename T, bool RELU, bool RES, bool NT, bool FIN, bool S2 = false>
 __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
                                                        const uint8_t* __restrict__ mask,
                                                        const T* __restrict__ x,
@@ -850,21 +771,13 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
     s_co[cs + cl] = b_;
     s_co[2 * cs + cl] = c_;
     s_co[3 * cs + cl] = co.mean[c];
-    if constexpr (MX) {
-      s_co[4 * cs + cl] = co.scale[c];
-      s_co[5 * cs + cl] = co.shift[c];
-    }
   }
   __syncthreads();
-  float ca[kVec], cb[kVec], cc[kVec], mu[kVec], fsc[MX ? kVec : 1], fsh[MX ? kVec : 1];
+  float ca[kVec], cb[kVec], cc[kVec], mu[kVec];
   lds8(s_co + c0, ca);
   lds8(s_co + cs + c0, cb);
   lds8(s_co + 2 * cs + c0, cc);
   lds8(s_co + 3 * cs + c0, mu);
-  if constexpr (MX) {
-    lds8(s_co + 4 * cs + c0, fsc);
-    lds8(s_co + 5 * cs + c0, fsh);
-  }
   zero_duty(zero, nzero);
   float mu2[S2 ? kVec : 1], sa2[S2 ? kVec : 1], sb2[S2 ? kVec : 1];
   if constexpr (S2) {
@@ -877,12 +790,11 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
   for (long long v = q.v0; v < nvec; v += stride) {
     float d[kVec], xv[kVec], x2v[S2 ? kVec : 1];
     if (NT) V8<T>::loadnt(dy + v * kVec, d); else V8<T>::load(dy + v * kVec, d);
-    uint32_t mb = (RELU && !MX) ? (uint32_t)mask[v] : 0xffu;
+    const uint32_t mb = RELU ? (uint32_t)mask[v] : 0xffu;
     if (NT) V8<T>::loadnt(x + v * kVec, xv); else V8<T>::load(x + v * kVec, xv);
     if constexpr (S2) {
       if (NT) V8<T>::loadnt(x2 + v * kVec, x2v); else V8<T>::load(x2 + v * kVec, x2v);
     }
-    if constexpr (RELU && MX) mb = relu_bits_from_x<T>(xv, mu, fsc, fsh);
     float g[kVec], o[kVec];
 #pragma unroll
     for (int i = 0; i < kVec; ++i) {
@@ -1658,19 +1570,15 @@ hipError_t arena_bn_fwd(int dtype, const void* x, const void* res, void* y, uint
 // else a one-thread-per-channel finalize writes the coefficients and zeroes `acc`.
 // zero / nzero (optional): doubles block 0 of the dx pass clears (the forward's statistics sums
 // of this layer, whose last reader -- the apply pass -- has finished).
-// mask_x (relu, a folded layer): no mask; the ReLU bits are recomputed from x with co.mean /
-// co.scale / co.shift (the forward's coefficients)
 // x2 / mean2 / acc2 (optional): the second BN's input, batch mean and backward sums (S2 in
-// bn_bwd_dx_kernel); only with relu, no dres, no mask_x and sums fed or summed here (fin_dx).
+// bn_bwd_dx_kernel); only with relu, no dres and sums fed or summed here (fin_dx).
 hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const void* x, void* dx,
                         void* dres, long long M, int C, int relu, float* part, int ext_nblk,
                         double* lvl2, unsigned* tickets, ArenaBNBwd co, double* acc, int fin_dx,
-                        double* zero, int nzero, int mask_x, const void* x2, const float* mean2,
+                        double* zero, int nzero, const void* x2, const float* mean2,
                         double* acc2, hipStream_t stream) {
   if (bad_shape(M, C)) return hipErrorInvalidValue;
-  const bool mx = relu && mask_x;
-  if (relu && !mx && mask == nullptr) return hipErrorInvalidValue;
-  if (mx && (co.scale == nullptr || co.shift == nullptr)) return hipErrorInvalidValue;
+  if (relu && mask == nullptr) return hipErrorInvalidValue;
   long long rpb;
   long long nb = reduce_blocks(M, C, &rpb);
   const int ns = chan_slices(C);
@@ -1682,18 +1590,16 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
   if (ext_nblk > 0) {
     nb = ext_nblk;
   } else if (!pre) {
-#define ARENA_BN_RED(TT, R, X)                                                               \
-  hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, R, X>), dim3(nb, ns), dim3(kT), 0, stream,  \
+#define ARENA_BN_RED(TT, R)                                                                  \
+  hipLaunchKernelGGL((bn_bwd_reduce_kernel<TT, R>), dim3(nb, ns), dim3(kT), 0, stream,     \
                      static_cast<const TT*>(dy), mask, static_cast<const TT*>(x), M, C, rpb, \
                      part, co, am)
     if (dtype == 1) {
-      if (mx) ARENA_BN_RED(uint16_t, true, true);
-      else if (relu) ARENA_BN_RED(uint16_t, true, false);
-      else ARENA_BN_RED(uint16_t, false, false);
+      if (relu) ARENA_BN_RED(uint16_t, true);
+      else ARENA_BN_RED(uint16_t, false);
     } else {
-      if (mx) ARENA_BN_RED(float, true, true);
-      else if (relu) ARENA_BN_RED(float, true, false);
-      else ARENA_BN_RED(float, false, false);
+      if (relu) ARENA_BN_RED(float, true);
+      else ARENA_BN_RED(float, false);
     }
 #undef ARENA_BN_RED
   }
@@ -1710,15 +1616,11 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
   const dim3 dgrid = stream_grid(ne, C);
   const int dcs = stream_lds_channels(C);
   const int cg = C / kVec;
-#define ARENA_BN_DX_NTX(TT, R, S, NT, F, X)                                                  \
-  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S, NT, F, X>), dgrid, dim3(kT),                \
-                     (X ? 6 : 4) * dcs * 4, stream,                                         \
-                     static_cast<const TT*>(dy), mask, static_cast<const TT*>(x),            \
+#define ARENA_BN_DX_NT(TT, R, S, NT, F)                                                      \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, R, S, NT, F>), dgrid, dim3(kT), 4 * dcs * 4,     \
+                     stream, static_cast<const TT*>(dy), mask, static_cast<const TT*>(x),    \
                      static_cast<TT*>(dx), static_cast<TT*>(dres), nvec, cg, co, acc, M,     \
                      zero, nzero, nullptr, nullptr, nullptr)
-#define ARENA_BN_DX_NT(TT, R, S, NT, F)                                                      \
-  do { if (R && mx) ARENA_BN_DX_NTX(TT, R, S, NT, F, R);                                     \
-       else ARENA_BN_DX_NTX(TT, R, S, NT, F, false); } while (0)
 #define ARENA_BN_DX_F(TT, R, S, F)                                                           \
   do { if (g_bn_nt) ARENA_BN_DX_NT(TT, R, S, true, F);                                       \
        else ARENA_BN_DX_NT(TT, R, S, false, F); } while (0)
@@ -1727,10 +1629,10 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
   while (0)
   const bool r = relu != 0, s = dres != nullptr;
   if (x2 != nullptr) {
-    if (!(fin && r && !s && !mx) || mean2 == nullptr || acc2 == nullptr)
+    if (!(fin && r && !s) || mean2 == nullptr || acc2 == nullptr)
       return hipErrorInvalidValue;
 #define ARENA_BN_DX_S2(TT, NT)                                                                 \
-  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, true, false, NT, true, false, true>), dgrid,        \
+  hipLaunchKernelGGL((bn_bwd_dx_kernel<TT, true, false, NT, true, true>), dgrid,              \
                      dim3(kT), 4 * dcs * 4, stream, static_cast<const TT*>(dy), mask,           \
                      static_cast<const TT*>(x), static_cast<TT*>(dx), nullptr, nvec, cg, co,    \
                      acc, M, zero, nzero, static_cast<const TT*>(x2), mean2, acc2)
@@ -1754,31 +1656,6 @@ hipError_t arena_bn_bwd(int dtype, const void* dy, const uint8_t* mask, const vo
 #undef ARENA_BN_DX
 #undef ARENA_BN_DX_F
 #undef ARENA_BN_DX_NT
-#undef ARENA_BN_DX_NTX
-  return hipGetLastError();
-}
-
-// The BN-apply fold's forward (training): the statistics as in arena_bn_fwd (acc-mode sums from
-// the producing conv -- FIN --, or its per-tile partials merged by the finalize kernel), then only
-// the coefficients: st.mean / st.scale / st.shift (the caller passes them as one [3][C] table for
-// the consuming convolution), st.invstd, the running statistics and the batch counter. No output,
-// no mask. fin: the fp64 [2][C] sums (left in place for the backward dx pass to zero).
-hipError_t arena_bn_fold_fwd(long long M, int C, const double* fin, float* part, int ext_nblk,
-                             long long ext_rpb, double* lvl2, unsigned* tickets, ArenaBNStats st,
-                             double* zero, int nzero, hipStream_t stream) {
-  if (bad_shape(M, C)) return hipErrorInvalidValue;
-  if (fin != nullptr) {
-    hipLaunchKernelGGL(bn_fold_coef_kernel<true>, dim3((C + kT - 1) / kT), dim3(kT), 0, stream,
-                       st, fin, M, C, zero, nzero);
-    return hipGetLastError();
-  }
-  if (ext_nblk <= 0 || ext_rpb <= 0 || (long long)ext_nblk * ext_rpb < M)
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL(bn_stats_finalize_kernel, dim3((C + 63) / 64, fin_blocks_per_group(ext_nblk)),
-                     dim3(kT), 0, stream, part, ext_nblk, M, C, ext_rpb, lvl2, tickets, st);
-  if (zero != nullptr)
-    hipLaunchKernelGGL(bn_fold_coef_kernel<false>, dim3(1), dim3(kT), 0, stream, st, nullptr, M,
-                       C, zero, nzero);
   return hipGetLastError();
 }
 

@@ -102,7 +102,6 @@ struct ConvArgs {
   float4* kws;
   unsigned* kcnt;
   int xbytes, wbytes;  // buffer-descriptor ranges of x and w (both < 2^31 bytes, host-checked)
-  int tpb;             // output tiles per block (persistent form, see conv_fwd_body); 1 = one
   int st1p;            // EPI 1 statistics in one pass (sum, sum of squares) instead of two
   // Several phase convolutions of a strided backward-data pass in ONE launch (v2 tiles, plain
   // mapped epilogue): phase p owns blocks [ph[p].blk0, ph[p + 1].blk0) (starts on multiples of 8,
@@ -113,14 +112,6 @@ struct ConvArgs {
   };
   int nph;             // 0: a single convolution
   Phase ph[4];
-  // BatchNorm-apply fold (v2 / halo tiles only): x is the RAW input of a ReLU BatchNorm layer
-  // whose output this convolution consumes, and pre = [3][C] floats (batch mean, scale, shift)
-  // of that layer. EPI 1 (forward): the A operand becomes relu(fma(x - mean, scale, shift))
-  // rounded to bf16 -- bn_apply_kernel's arithmetic and rounding, so the products equal the
-  // unfused path's bit for bit -- transformed once per staged chunk in LDS (the BN output is never
-  // written). EPI 2 (backward-data with BN-backward sums): the ReLU bits of that BN's output are
-  // recomputed from bnx with the same arithmetic instead of read from bnmask (pre = [3][Cout]).
-  const float* pre;
 };
 
 __device__ __forceinline__ int swz(int row) { return (row >> 1) & 7; }
@@ -219,65 +210,6 @@ __device__ __forceinline__ float bf16_round(float f) {
   return __uint_as_float(pack_bf16x2(f, 0.f) << 16);
 }
 
-// ---- BatchNorm-apply fold (ConvArgs::pre, WgradArgs::pre) ----
-constexpr int kPreMaxC = 512;   // widest folded BN (the bottleneck mid widths 64..512)
-
-struct PreCoef {   // 8 channels' (mean, scale, shift)
-  f32x4v mu0, mu1, sc0, sc1, sh0, sh1;
-};
-
-// coefficients of channels c..c+7 from a [3][ld] float table (global or LDS)
-__device__ __forceinline__ PreCoef pre_coef(const float* t, int ld, int c) {
-  PreCoef k;
-  k.mu0 = *reinterpret_cast<const f32x4v*>(t + c);
-  k.mu1 = *reinterpret_cast<const f32x4v*>(t + c + 4);
-  k.sc0 = *reinterpret_cast<const f32x4v*>(t + ld + c);
-  k.sc1 = *reinterpret_cast<const f32x4v*>(t + ld + c + 4);
-  k.sh0 = *reinterpret_cast<const f32x4v*>(t + 2 * ld + c);
-  k.sh1 = *reinterpret_cast<const f32x4v*>(t + 2 * ld + c + 4);
-  return k;
-}
-
-__device__ __forceinline__ float pre_val(float x, float mu, float sc, float sh) {
-  return fmaxf(fmaf(x - mu, sc, sh), 0.f);
-}
-
-// 8 bf16 (one 16-byte chunk) -> relu(fma(x - mean, scale, shift)), rounded to bf16
-__device__ __forceinline__ uint4 pre_chunk(uint4 q, const PreCoef& k) {
-  const uint32_t u[4] = {q.x, q.y, q.z, q.w};
-  uint32_t o[4];
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const f32x4v& mu = e < 2 ? k.mu0 : k.mu1;
-    const f32x4v& sc = e < 2 ? k.sc0 : k.sc1;
-    const f32x4v& sh = e < 2 ? k.sh0 : k.sh1;
-    const int i = (2 * e) & 3;
-    o[e] = pack_bf16x2(pre_val(__uint_as_float(u[e] << 16), mu[i], sc[i], sh[i]),
-                       pre_val(__uint_as_float(u[e] & 0xffff0000u), mu[i + 1], sc[i + 1],
-                               sh[i + 1]));
-  }
-  return make_uint4(o[0], o[1], o[2], o[3]);
-}
-
-// the ReLU bits of that BN output at 8 channels (bn_apply's store_pos rule: the stored bf16 > 0)
-__device__ __forceinline__ uint32_t pre_bits(uint4 q, const PreCoef& k) {
-  const uint4 r = pre_chunk(q, k);
-  const uint32_t w[4] = {r.x, r.y, r.z, r.w};
-  uint32_t b = 0;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t h = (i & 1) ? (w[i >> 1] >> 16) : (w[i >> 1] & 0xffffu);
-    const bool pos = (h & 0x8000u) == 0 && (h & 0x7fffu) != 0 && (h & 0x7fffu) <= 0x7f80u;
-    b |= (pos ? 1u : 0u) << i;
-  }
-  return b;
-}
-
-// in place on a staged chunk in LDS
-__device__ __forceinline__ void pre_lds(uint8_t* p, const PreCoef& k) {
-  *reinterpret_cast<uint4*>(p) = pre_chunk(*reinterpret_cast<const uint4*>(p), k);
-}
-
 // sum over the 16 lanes of a DPP row (lane bits 0..3); every lane of the row gets the sum
 __device__ __forceinline__ float row16_sum(float v) {
   v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
@@ -299,17 +231,9 @@ __device__ __forceinline__ double* acc_replica(const ConvArgs& a, int mt) {
 // restaged in LDS so that consecutive lanes add to consecutive channels: 64 fp64 adds = 512
 // contiguous bytes per wave instruction (scattered few-lane atomics cost one 64-B memory-side
 // request each). No wait and no fence: the kernel's end makes the sums visible to the finalize.
-template <int BN>
-__device__ __forceinline__ double* bn_lacc_storage() {
-  __shared__ double s[2 * BN];
-  return s;
-}
-
-// lacc != null (persistent tiles): the sums are added into the block's LDS set lacc [2][BN] by
-// the same owner thread per channel instead, and flushed once after the last tile.
 template <int BM, int BN, int NT, typename Emit>
 __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int mt, int n0, int nrows,
-                                                double* lacc, Emit&& emit) {
+                                                Emit&& emit) {
   __shared__ float s_st[2][BN];
   emit([&](int c, float mean, float m2) {
     s_st[0][c] = mean;
@@ -323,13 +247,8 @@ __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int mt, int n
   for (int c = threadIdx.x; c < BN; c += NT) {
     const double mu = (double)s_st[0][c];
     const double s1 = n * mu, s2 = (double)s_st[1][c] + n * mu * mu;
-    if (lacc != nullptr) {
-      lacc[c] += s1;
-      lacc[BN + c] += s2;
-    } else {
-      unsafeAtomicAdd(acc + c, s1);             // sum y
-      unsafeAtomicAdd(acc + a.Cout + c, s2);    // sum y^2
-    }
+    unsafeAtomicAdd(acc + c, s1);             // sum y
+    unsafeAtomicAdd(acc + a.Cout + c, s2);    // sum y^2
   }
 }
 
@@ -349,11 +268,7 @@ __device__ __forceinline__ void bn_acc_epilogue(const ConvArgs& a, int mt, int n
 // arithmetic of the flat form (a tap division, bounds checks and 64-bit addresses per slot per
 // step) issued ~115 VALU and ~140 SALU per K step against 16 MFMAs (the kernels were
 // issue-bound, not load-bound). C16 = true is the stem's space-to-depth form on flat loads.
-// PT: the persistent form (a.tpb output tiles per block); a separate instantiation, because the
-// tile loop costs 30-60 VGPRs even when it runs once (hipcc keeps the per-tile staging state live
-// across the back edge), which spilled the high-occupancy variants.
-template <int BM, int BN, int EPI, int NBUF = 2, int NWM = 2, int NWN = 2, bool C16 = false,
-          bool PT = false>
+template <int BM, int BN, int EPI, int NBUF = 2, int NWM = 2, int NWN = 2, bool C16 = false>
 __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int WM = BM / NWM, WN = BN / NWN;    // per-wave output tile
@@ -369,37 +284,19 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
   // XCD-aware tile order: blocks b and b+8 share an XCD (round-robin dispatch), so give each XCD
   // a contiguous range of tiles (bijective for any grid size).
   const int ks = a.ksplit;
-  // Persistent tiles (a.tpb > 1, never with split-K): block `lin` computes the output tiles
-  // (mt0 + i, nt), i < tpb, of one column tile, so its BatchNorm sums (acc mode) are merged in LDS
-  // across them and reach memory once per block: 1/tpb of the fp64 atomics onto the [2][Cout]
-  // set, which per-tile flushing made too slow for the 56x56 / 28x28 layers (~800 k pairs). The
-  // lin order keeps a row chunk's column tiles consecutive (one XCD: the A rows hit its L2).
-  const int tpb = PT ? a.tpb : 1;
-  const int nwg = tpb > 1 ? (a.m_tiles + tpb - 1) / tpb * a.n_tiles : a.m_tiles * a.n_tiles * ks;
+  const int nwg = a.m_tiles * a.n_tiles * ks;
   const int bid = blockIdx.x;
   const int xcd = bid & 7, q = nwg >> 3, r8 = nwg & 7;
   const int lin = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + (bid >> 3);
   // a tile's K slices are consecutive in the XCD order: the last arriver reads same-XCD slabs
-  const int tile0 = tpb > 1 ? lin : (ks > 1 ? lin / ks : lin);
-  const int slice = (tpb == 1 && ks > 1) ? lin - tile0 * ks : 0;
+  const int tile0 = ks > 1 ? lin / ks : lin;
+  const int slice = ks > 1 ? lin - tile0 * ks : 0;
   const int nt = tile0 % a.n_tiles;
-  const int mt0 = tpb > 1 ? tile0 / a.n_tiles * tpb : tile0 / a.n_tiles;
+  const int mt0 = tile0 / a.n_tiles;
   const int n0 = nt * BN;
-  // block-level BatchNorm sums of the persistent form (EPI 1, acc mode): [2][BN], one owner
-  // thread per channel (the same thread in every tile's epilogue, so no barrier between them)
-  double* lacc = nullptr;
-  if constexpr (EPI == 1) {
-    if (tpb > 1 && a.bn_acc != nullptr) {
-      lacc = bn_lacc_storage<BN>();
-      for (int c = threadIdx.x; c < BN; c += NT) lacc[c] = lacc[BN + c] = 0.0;
-    }
-  }
 
-#pragma unroll 1
-  for (int it = 0; it < tpb; ++it) {
-    const int mt = mt0 + it;
-    if (mt >= a.m_tiles) break;
-    if (it > 0) lds_barrier();   // the previous tile's epilogue is done with the stage LDS
+  {
+    const int mt = mt0;
     const int tile = mt * a.n_tiles + nt;
     const int m0 = mt * BM;
 
@@ -1019,7 +916,7 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
             }
         }
       } else {
-        bn_acc_epilogue<BM, BN, NT>(a, mt, n0, nrows, lacc, [&](auto&& add) {
+        bn_acc_epilogue<BM, BN, NT>(a, mt, n0, nrows, [&](auto&& add) {
           if (wm == 0 && fr == 0) {
 #pragma unroll
             for (int j = 0; j < NI; ++j)
@@ -1029,41 +926,34 @@ __device__ __forceinline__ void conv_fwd_body(const ConvArgs& a) {
         });
       }
     }
-  }   // tile loop
-  if (lacc != nullptr) {   // the block's sums, once (each channel by the thread that summed it)
-    double* acc = acc_replica(a, (int)blockIdx.x) + n0;
-    for (int c = threadIdx.x; c < BN; c += NT) {
-      unsafeAtomicAdd(acc + c, lacc[c]);
-      unsafeAtomicAdd(acc + a.Cout + c, lacc[BN + c]);
-    }
   }
 }
 
-template <int BM, int BN, int EPI, int NBUF, bool C16, bool PT = false>
+template <int BM, int BN, int EPI, int NBUF, bool C16>
 __global__ __launch_bounds__(kThreads) void conv_fwd_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
-  conv_fwd_body<BM, BN, EPI, NBUF, 2, 2, C16, PT>(a);
+  conv_fwd_body<BM, BN, EPI, NBUF, 2, 2, C16>(a);
 #endif
 }
 
 // Single stage buffer (one K step -- 1x1 over 64 channels -- or the serial variants 8..11): the
 // shapes that want it are bound by streaming the output, so it trades registers for occupancy --
 // four waves per SIMD (<= 128 VGPRs) instead of two, up to five blocks per CU by LDS.
-template <int BM, int BN, int EPI, bool C16, bool PT = false>
+template <int BM, int BN, int EPI, bool C16>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 void conv_fwd_kernel_occ4(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
-  conv_fwd_body<BM, BN, EPI, 1, 2, 2, C16, PT>(a);
+  conv_fwd_body<BM, BN, EPI, 1, 2, 2, C16>(a);
 #endif
 }
 
 // 256-row tiles on 8 waves (4 x 2, per-wave 64 x BN/2): twice the MFMA work of a 128-row tile per
 // staged weight byte, 2 waves per SIMD at one block per CU (96 KB of LDS double-buffered, 144 KB
 // triple-buffered at BN = 128).
-template <int BM, int BN, int EPI, int NBUF, bool PT = false>
+template <int BM, int BN, int EPI, int NBUF>
 __global__ __launch_bounds__(512) void conv_fwd_kernel_w8(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
-  conv_fwd_body<BM, BN, EPI, NBUF, 4, 2, false, PT>(a);
+  conv_fwd_body<BM, BN, EPI, NBUF, 4, 2, false>(a);
 #endif
 }
 
@@ -1073,21 +963,17 @@ hipError_t launch_w8(const ConvArgs& a0, int nb, hipStream_t st) {
   if (a.c16) return hipErrorInvalidValue;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  const int nwg = a.tpb > 1 ? (a.m_tiles + a.tpb - 1) / a.tpb * a.n_tiles
-                            : a.m_tiles * a.n_tiles * a.ksplit;
+  const int nwg = a.m_tiles * a.n_tiles * a.ksplit;
   if (a.Ktot == kBK) nb = 1;
   const int epi = (a.part == nullptr && a.bn_acc == nullptr) ? 0 : (a.bnx != nullptr ? 2 : 1);
-#define ARENA_CONV_W8P(E, P) \
-  do { if (nb == 1) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 1, P>), dim3(nwg), dim3(512), 0, st, a); \
-       else if (nb == 2) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 2, P>), dim3(nwg), dim3(512), 0, st, a); \
-       else hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 3, P>), dim3(nwg), dim3(512), 0, st, a); } while (0)
 #define ARENA_CONV_W8(E) \
-  do { if (a.tpb > 1) ARENA_CONV_W8P(E, true); else ARENA_CONV_W8P(E, false); } while (0)
+  do { if (nb == 1) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 1>), dim3(nwg), dim3(512), 0, st, a); \
+       else if (nb == 2) hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 2>), dim3(nwg), dim3(512), 0, st, a); \
+       else hipLaunchKernelGGL((conv_fwd_kernel_w8<BM, BN, E, 3>), dim3(nwg), dim3(512), 0, st, a); } while (0)
   if (epi == 0) ARENA_CONV_W8(0);
   else if (epi == 1) ARENA_CONV_W8(1);
   else ARENA_CONV_W8(2);
 #undef ARENA_CONV_W8
-#undef ARENA_CONV_W8P
   return hipGetLastError();
 }
 
@@ -1096,30 +982,24 @@ hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
   ConvArgs a = a0;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  const int nwg = a.tpb > 1 ? (a.m_tiles + a.tpb - 1) / a.tpb * a.n_tiles
-                            : a.m_tiles * a.n_tiles * a.ksplit;
+  const int nwg = a.m_tiles * a.n_tiles * a.ksplit;
   // stage buffers: pipe 0 (variants 0..3) two, pipe 1 (4..7) three, pipe 2 (8..11) one (serial,
   // high occupancy); a single K step always one
   const int nb = a.Ktot == kBK || pipe == 2 ? 1 : (pipe == 1 ? 4 : 2);
   const int epi = (a.part == nullptr && a.bn_acc == nullptr) ? 0 : (a.bnx != nullptr ? 2 : 1);
-#define ARENA_CONV_LAUNCH(E, NB, P) \
-  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, E, NB, C16, P>), dim3(nwg), dim3(kThreads), 0, st, a)
-#define ARENA_CONV_NBP(E, P) \
-  do { if (nb == 1 && (E == 0 || BM * BN < 128 * 128)) /* fits 128 VGPRs without spills */ \
-         hipLaunchKernelGGL((conv_fwd_kernel_occ4<BM, BN, E, C16, P>), dim3(nwg), dim3(kThreads), 0, st, a); \
-       else if (nb == 1) ARENA_CONV_LAUNCH(E, 1, P); \
-       else if (nb == 2) ARENA_CONV_LAUNCH(E, 2, P); \
-       else ARENA_CONV_LAUNCH(E, 4, P); } while (0)
+#define ARENA_CONV_LAUNCH(E, NB) \
+  hipLaunchKernelGGL((conv_fwd_kernel<BM, BN, E, NB, C16>), dim3(nwg), dim3(kThreads), 0, st, a)
 #define ARENA_CONV_NB(E) \
-  do { if constexpr (C16) ARENA_CONV_NBP(E, false); \
-       else if (a.tpb > 1) ARENA_CONV_NBP(E, true); else ARENA_CONV_NBP(E, false); } while (0)
-  if (a.tpb > 1 && C16) return hipErrorInvalidValue;
+  do { if (nb == 1 && (E == 0 || BM * BN < 128 * 128)) /* fits 128 VGPRs without spills */ \
+         hipLaunchKernelGGL((conv_fwd_kernel_occ4<BM, BN, E, C16>), dim3(nwg), dim3(kThreads), 0, st, a); \
+       else if (nb == 1) ARENA_CONV_LAUNCH(E, 1); \
+       else if (nb == 2) ARENA_CONV_LAUNCH(E, 2); \
+       else ARENA_CONV_LAUNCH(E, 4); } while (0)
   if (epi == 0) ARENA_CONV_NB(0);
   else if (epi == 1) ARENA_CONV_NB(1);
   else if constexpr (!C16) ARENA_CONV_NB(2);
   else return hipErrorInvalidValue;
 #undef ARENA_CONV_NB
-#undef ARENA_CONV_NBP
 #undef ARENA_CONV_LAUNCH
   return hipGetLastError();
 }
@@ -1196,7 +1076,7 @@ struct Conv2Geo {
 // The v2 epilogue: the accumulators through an fp32 LDS tile at `lds` (EH x BN floats, bands of
 // EH rows), coalesced bf16 stores (+ addend, mapped placement, fill_sib), and the EPI 1 / EPI 2
 // BatchNorm sums (their partials reuse the tile).
-template <class G, int EPI, bool PRE = false>
+template <class G, int EPI>
 __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
                                                f32x16v (&acc)[G::MI][G::NI], uint8_t* lds,
                                                int m0, int n0, int mt, int tid, int wm, int wn,
@@ -1224,7 +1104,6 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
   // EPI 2: this thread's 8 channels (n0 + (tid % CPR) * 8 + e: the store loop below keeps a
   // thread on one 16-byte column chunk) -- sum g and sum g * (x - mean) over its rows
   float e1[EPI == 2 ? 8 : 1], e2[EPI == 2 ? 8 : 1], emu[EPI == 2 ? 8 : 1];
-  PreCoef epk;   // EPI 2 + PRE: the folded BN's coefficients of this thread's 8 channels
   if constexpr (EPI == 2) {
     static_assert(NT % CPR == 0, "EPI 2: a thread's column chunk is fixed");
     const float* mp = a.bnmean + n0 + (tid % CPR) * 8;
@@ -1234,7 +1113,6 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
       e2[e] = 0.f;
       emu[e] = mp[e];
     }
-    if constexpr (PRE) epk = pre_coef(a.pre, a.Cout, n0 + (tid % CPR) * 8);
   }
 #pragma unroll
   for (int band = 0; band < BM / EH; ++band) {
@@ -1279,9 +1157,7 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
       uint32_t bmk = 0xffu;
       if constexpr (EPI == 2) {   // the BN layer's input and ReLU bits at the same pixel/channels
         bxq = *reinterpret_cast<const uint4*>(a.bnx + off);
-        if constexpr (PRE)          // folded BN: its output was never stored, recompute the bits
-          bmk = pre_bits(bxq, epk);
-        else if (a.bnmask)
+        if (a.bnmask)
           bmk = a.bnmask[(size_t)(rbase + row) * (a.Cout >> 3) + (n0 >> 3) + cc];
       }
       if (EPI != 1 && a.add != nullptr) {
@@ -1407,36 +1283,20 @@ __device__ __forceinline__ void conv2_epilogue(const ConvArgs& a,
 }
 
 template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false,
-          int HALO = 0, bool PRE = false>
+          int HALO = 0>
 __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
   using G = Conv2Geo<BM, BN, NWM, NWN, NBUF, EPI, BAND, HALO>;
   constexpr int NT = G::NT, WM = G::WM, WN = G::WN, MI = G::MI, NI = G::NI;
   constexpr int AI = G::AI, BI = G::BI, kBufBytes = G::kBufBytes;
   constexpr int SL = G::SL, RG = G::RG, EH = G::EH;
-  static_assert(!PRE || EPI != 0, "the BN fold rides on the statistics / BN-backward epilogues");
-  // BN fold, forward, generic tiles: the folded BN's [3][C] coefficient table sits behind the stage
-  // buffers (the epilogue may overwrite it: the K loop is done with it). The halo form keeps its
-  // one chunk of coefficients per thread in registers instead (its LDS is sized to the block).
-  constexpr bool kPreA = PRE && EPI == 1;
-  constexpr int kPreTab = (kPreA && !HALO) ? 3 * kPreMaxC * 4 : 0;
-  constexpr int kLdsAll = G::kStage + kPreTab > G::kLds ? G::kStage + kPreTab : G::kLds;
-  static_assert(kLdsAll <= kLdsMax, "LDS budget");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsAll];
-  // the fold's transform assignment: thread = (logical 16-byte chunk lc, first row) of the staged
-  // A rows; every thread transforms one chunk position, so it needs one chunk's coefficients
-  const int pre_lc = threadIdx.x & 7, pre_r0 = threadIdx.x >> 3;
+  __shared__ __attribute__((aligned(16))) uint8_t lds[G::kLds];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // XCD-aware order (as v1): each XCD gets a contiguous range of tiles, column tiles of one row
-  // tile consecutive (their A rows stay in that XCD's L2). Split-K (ksplit > 1): the ksplit blocks
-  // of one output tile are consecutive in that order too, so a tile's slices (and the reducer
-  // that reads their slabs) share an XCD except at range edges.
-  const int ks = a.ksplit;
-  const int nblk = a.m_tiles * a.n_tiles * ks;
+  // tile consecutive (their A rows stay in that XCD's L2)
+  const int nblk = a.m_tiles * a.n_tiles;
   const int xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
-  const int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tile = ks > 1 ? lin / ks : lin;
-  const int slice = lin - tile * ks;
+  const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int nt = tile % a.n_tiles, mt = tile / a.n_tiles;
   const int n0 = nt * BN, m0 = mt * BM;
 
@@ -1547,26 +1407,13 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
     constexpr int D = NBUF - 1;
     static_assert(D >= 1 && D < 9, "weight ring depth");
     const int CB = a.C / kBK;
-    // split-K: slice s owns channel chunks [s*CB/ks, (s+1)*CB/ks) (host-checked ks <= CB)
-    const int cb_end = (slice + 1) * CB / ks;
-    for (int cb = slice * CB / ks; cb < cb_end; ++cb) {
-      PreCoef pk;
-      if constexpr (kPreA) pk = pre_coef(a.pre, a.C, cb * kBK + pre_lc * 8);
+    for (int cb = 0; cb < CB; ++cb) {
       stage_win(cb);   // the previous chunk's last tap ended on a barrier: the window is free
 #pragma unroll
       for (int t = 0; t < D; ++t) stage_b(t, cb, t);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * BI) : "memory");   // window + tap 0
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if constexpr (kPreA) {
-        // BN fold: every in-image window row through relu(fma(x - mean, scale, shift)) once
-        // (rows outside [0, M) only feed masked taps and stay zero)
-        for (int j = pre_r0; j < WR; j += NT / 8) {
-          const int pix = org + j;
-          if (pix >= 0 && pix < a.M) pre_lds(lds + j * kRowBytes + ((pre_lc ^ swz(j)) << 4), pk);
-        }
-        lds_barrier();
-      }
 #pragma unroll
       for (int t = 0; t < 9; ++t) {
         // buffer (t + D) % NBUF was last read by tap t - 1, before the barrier that ended it
@@ -1610,30 +1457,10 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
       b_voff[i] = (uint32_t)(((n0 + row) * a.Ktot + (pos ^ swz(row)) * 8) * 2);
     }
     const int CB = a.C / kBK;
-    // split-K: slice s owns K steps [s*Tall/ks, (s+1)*Tall/ks); the staging cursor starts at the
-    // first one (tap = t0 / CB, chunk = t0 % CB; tap (r, s) sits (r*W + s)*C elements from tap 0)
-    const int Tall = a.Ktot / kBK;
-    const int t0 = slice * Tall / ks;
-    const int T = (slice + 1) * Tall / ks - t0;
-    int s_tap = t0 / CB, s_cb = t0 - (t0 / CB) * CB, s_s = s_tap % a.S, s_t = t0;
-    int s_tapoff = ((s_tap / a.S) * a.W + s_s) * a.C * 2;
-    if constexpr (kPreA) {   // the folded BN's coefficients, once per block
-      float* tab = reinterpret_cast<float*>(lds + G::kStage);
-      for (int i = threadIdx.x; i < 3 * a.C; i += NT) tab[i] = a.pre[i];
-      lds_barrier();
-    }
-    // BN fold (1x1 / stride 1 / unpadded, host-checked): step t's A tile (chunk t % CB) in buffer
-    // `buf` through relu(fma(x - mean, scale, shift)); rows past M stay as they are (never stored)
-    auto pre_tile = [&](int buf, int t) {
-      if constexpr (kPreA) {
-        const float* tab = reinterpret_cast<const float*>(lds + G::kStage);
-        const PreCoef pk = pre_coef(tab, a.C, (t % CB) * kBK + pre_lc * 8);
-        uint8_t* abuf = lds + buf * kBufBytes;
-        for (int r = pre_r0; r < BM; r += NT / 8)
-          if (m0 + r < a.M) pre_lds(abuf + r * kRowBytes + ((pre_lc ^ swz(r)) << 4), pk);
-        lds_barrier();
-      }
-    };
+    // staging cursor: tap (r, s) sits (r*W + s)*C elements from tap 0
+    const int T = a.Ktot / kBK;
+    int s_tap = 0, s_cb = 0, s_s = 0, s_t = 0;
+    int s_tapoff = 0;
   #pragma unroll
     for (int i = 0; i < AI; ++i)
       a_cur[i] = ((a_mask[i] >> s_tap) & 1u) ? (uint32_t)(a_lane[i] + s_tapoff) : kOOB;
@@ -1697,7 +1524,6 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
       if (T > 0) stage(0);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (T > 0) pre_tile(0, 0);
       for (int t = 0; t < T; ++t) {
         compute(0);
         if (t + 1 < T) {
@@ -1706,7 +1532,6 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
-        if (t + 1 < T) pre_tile(0, t + 1);
       }
     } else {
       constexpr int S = NBUF - 1;
@@ -1720,7 +1545,6 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-      if (T > 0) pre_tile(0, 0);
       int cur = 0;
       for (int t = 0; t < T; ++t) {
         // RAW: stage t + 1 was retired by the vmcnt before the last barrier. WAR: stage t + S
@@ -1734,59 +1558,11 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
         cur = cur == NBUF - 1 ? 0 : cur + 1;
-        // the fold of stage t + 1 (buffer cur): every wave is past compute(t) and its data landed
-        if (t + 1 < T) pre_tile(cur, t + 1);
       }
     }
   }
 
-  if (ks > 1) {
-    // ---- split-K hand-off (see slab_store / slab_ticket): every slice writes its fp32
-    // accumulators to kws [tile][slice][group][thread] write-through, takes a ticket on
-    // kcnt[tile]; the block drawing the last one sums the slices in slice order -- its own slab
-    // re-read too, so the rounding does not depend on which block arrived last -- and runs the
-    // epilogue (statistics / BN-backward sums included) ----
-    constexpr int NA = MI * NI * 4;
-    const __amdgpu_buffer_rsrc_t srs = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.kws + (size_t)tile * ks * NA * NT), (short)0, ks * NA * NT * 16, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < MI; ++i)
-#pragma unroll
-      for (int j = 0; j < NI; ++j)
-#pragma unroll
-        for (int g = 0; g < 4; ++g)
-          slab_store(srs, ((slice * NA + (i * NI + j) * 4 + g) * NT + tid) * 16,
-                     make_float4(acc[i][j][4 * g], acc[i][j][4 * g + 1], acc[i][j][4 * g + 2],
-                                 acc[i][j][4 * g + 3]));
-    if (!slab_ticket(a.kcnt + tile, ks, lds)) return;
-    // one row of fragments (NI * 4 loads in flight) per slice, slices in order
-#pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      const int base = (i * NI * 4 * NT + tid) * 16;
-#pragma unroll
-      for (int jg = 0; jg < NI * 4; ++jg) {
-        const float4 v = slab_load(srs, base + jg * NT * 16);
-        acc[i][jg >> 2][4 * (jg & 3)] = v.x;
-        acc[i][jg >> 2][4 * (jg & 3) + 1] = v.y;
-        acc[i][jg >> 2][4 * (jg & 3) + 2] = v.z;
-        acc[i][jg >> 2][4 * (jg & 3) + 3] = v.w;
-      }
-      for (int q = 1; q < ks; ++q) {
-        float4 v[NI * 4];
-#pragma unroll
-        for (int jg = 0; jg < NI * 4; ++jg) v[jg] = slab_load(srs, base + (q * NA + jg) * NT * 16);
-#pragma unroll
-        for (int jg = 0; jg < NI * 4; ++jg) {
-          acc[i][jg >> 2][4 * (jg & 3)] += v[jg].x;
-          acc[i][jg >> 2][4 * (jg & 3) + 1] += v[jg].y;
-          acc[i][jg >> 2][4 * (jg & 3) + 2] += v[jg].z;
-          acc[i][jg >> 2][4 * (jg & 3) + 3] += v[jg].w;
-        }
-      }
-    }
-  }
-
-  conv2_epilogue<G, EPI, PRE>(a, acc, lds, m0, n0, mt, tid, wm, wn, fr, hh);
+  conv2_epilogue<G, EPI>(a, acc, lds, m0, n0, mt, tid, wm, wn, fr, hh);
 }
 
 // The multi-phase launch: this block's phase, its arguments and its block index within it
@@ -1807,7 +1583,7 @@ __device__ __forceinline__ bool conv2_phase(const ConvArgs& a, ConvArgs& b, int&
   return bid < b.m_tiles * b.n_tiles;
 }
 
-template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool PRE = false>
+template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI>
 __global__ __launch_bounds__(64 * NWM * NWN) void conv2_kernel(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
   if constexpr (EPI == 0) {
@@ -1818,14 +1594,14 @@ __global__ __launch_bounds__(64 * NWM * NWN) void conv2_kernel(ConvArgs a) {
       return;
     }
   }
-  conv2_body<BM, BN, NWM, NWN, NBUF, EPI, false, 0, PRE>(a, blockIdx.x);
+  conv2_body<BM, BN, NWM, NWN, NBUF, EPI>(a, blockIdx.x);
 #endif
 }
 
 // serial, wave-row epilogue bands, <= 128 VGPRs: four waves per SIMD (up to four 4-wave blocks
 // per CU by LDS), the structure that wins the streaming-bound layers in v1 (variants 8..11)
 // (EPI 2 on the 128x128 tile: three waves per SIMD -- its 24 extra live registers spill at four)
-template <int BM, int BN, int EPI, bool PRE = false>
+template <int BM, int BN, int EPI>
 __global__ __launch_bounds__(256)
 __attribute__((amdgpu_waves_per_eu(EPI == 2 && BM * BN >= 128 * 128 ? 3 : 4)))
 void conv2_kernel_occ4(ConvArgs a) {
@@ -1838,43 +1614,34 @@ void conv2_kernel_occ4(ConvArgs a) {
       return;
     }
   }
-  conv2_body<BM, BN, 2, 2, 1, EPI, true, 0, PRE>(a, blockIdx.x);
+  conv2_body<BM, BN, 2, 2, 1, EPI, true>(a, blockIdx.x);
 #endif
 }
 
 // the 3x3 halo form (see Conv2Geo::HALO): 4 waves, a ring of NBR per-tap weight buffers --
 // 128x128: three (80 KB, two blocks per CU); 128x64: two (48 KB, three blocks per CU; with the
 // small window of <= 31-wide images 40 KB, four blocks per CU)
-template <int BM, int BN, int EPI, int HW, bool PRE = false>
+template <int BM, int BN, int EPI, int HW>
 __global__ __launch_bounds__(256) void conv2_kernel_halo(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, HW, PRE>(a, blockIdx.x);
+  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, HW>(a, blockIdx.x);
 #endif
 }
 
 template <int BM, int BN, int HW = 1>
 hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
-  if (a.c16 || a.tpb != 1 || a.Cout % BN || a.R != 3 || a.S != 3 ||
+  if (a.c16 || a.Cout % BN || a.R != 3 || a.S != 3 ||
       a.stride != 1 || a.pad != 1 || a.pad_w != 1 || a.Ho != a.H || a.Wo != a.W ||
       a.W > (HW == 2 ? kHaloSmallW : kHaloMaxW) || a.mapped)
     return hipErrorInvalidValue;
-  // split-K over the 64-channel chunks (every slice stages whole windows)
-  if (a.ksplit < 1 || a.ksplit > a.C / kBK || (a.ksplit > 1 && a.pre != nullptr))
-    return hipErrorInvalidValue;
+  if (a.ksplit != 1) return hipErrorInvalidValue;
   if (a.bnx == nullptr && (a.part != nullptr || a.bn_acc != nullptr) && a.add != nullptr)
     return hipErrorInvalidValue;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  const int nwg = a.m_tiles * a.n_tiles * a.ksplit;
-  if (a.pre != nullptr) {   // BN fold: forward with statistics, or the linked backward-data form
-    if (a.bnx != nullptr)
-      hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW, true>), dim3(nwg), dim3(256), 0, st, a);
-    else if ((a.part != nullptr || a.bn_acc != nullptr) && a.C <= kPreMaxC)
-      hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1, HW, true>), dim3(nwg), dim3(256), 0, st, a);
-    else
-      return hipErrorInvalidValue;
-  } else if (a.bnx != nullptr)
+  const int nwg = a.m_tiles * a.n_tiles;
+  if (a.bnx != nullptr)
     hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW>), dim3(nwg), dim3(256), 0, st, a);
   else if (a.part != nullptr || a.bn_acc != nullptr)
     hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1, HW>), dim3(nwg), dim3(256), 0, st, a);
@@ -1886,17 +1653,14 @@ hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
 template <int BM, int BN, int NWM, int NWN, int NBUF, bool OCC4 = false>
 hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
-  if (a.c16 || a.tpb != 1 || a.Cout % BN) return hipErrorInvalidValue;
-  // split-K: single convolutions only (not the phase launch, the mapped epilogue or the fold)
-  if (a.ksplit < 1 || a.ksplit > a.Ktot / kBK ||
-      (a.ksplit > 1 && (a.nph > 0 || a.mapped || a.pre != nullptr)))
-    return hipErrorInvalidValue;
+  if (a.c16 || a.Cout % BN) return hipErrorInvalidValue;
+  if (a.ksplit != 1) return hipErrorInvalidValue;   // split-K: the v1 tiles only
   const bool bwd_bn = a.bnx != nullptr;   // EPI 2 (the caller checked part / bnmean / no map)
   if (!bwd_bn && (a.part != nullptr || a.bn_acc != nullptr) && (a.add != nullptr || a.mapped))
     return hipErrorInvalidValue;
   a.m_tiles = (a.M + BM - 1) / BM;
   a.n_tiles = a.Cout / BN;
-  int nwg = a.m_tiles * a.n_tiles * a.ksplit;
+  int nwg = a.m_tiles * a.n_tiles;
   const bool stats = a.part != nullptr || a.bn_acc != nullptr;
   if (a.nph > 0) {   // phases back to back, each starting on a multiple of 8 blocks
     if (stats || bwd_bn) return hipErrorInvalidValue;
@@ -1907,26 +1671,6 @@ hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
       b0 += ((int)((mp + BM - 1) / BM) * a.n_tiles + 7) / 8 * 8;
     }
     nwg = b0;
-  }
-  if (a.pre != nullptr) {
-    // BN fold: the forward with statistics of a 1x1 / stride 1 / unpadded conv (the A tile is a
-    // plain pixel block), or the linked backward-data form (ReLU bits from the coefficients)
-    const bool fwd_ok = stats && !bwd_bn && a.R == 1 && a.S == 1 && a.stride == 1 &&
-                        a.pad == 0 && a.pad_w == 0 && a.C <= kPreMaxC && !a.mapped && a.nph == 0;
-    if (!(bwd_bn || fwd_ok)) return hipErrorInvalidValue;
-    if constexpr (OCC4) {
-      if (bwd_bn)
-        hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 2, true>), dim3(nwg), dim3(256), 0, st, a);
-      else
-        hipLaunchKernelGGL((conv2_kernel_occ4<BM, BN, 1, true>), dim3(nwg), dim3(256), 0, st, a);
-    } else if (bwd_bn) {
-      hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 2, true>), dim3(nwg),
-                         dim3(64 * NWM * NWN), 0, st, a);
-    } else {
-      hipLaunchKernelGGL((conv2_kernel<BM, BN, NWM, NWN, NBUF, 1, true>), dim3(nwg),
-                         dim3(64 * NWM * NWN), 0, st, a);
-    }
-    return hipGetLastError();
   }
   if constexpr (OCC4) {
     if (bwd_bn)
@@ -2013,16 +1757,14 @@ void arena_conv_set_stats_one_pass(int on) { g_conv_st1p = on ? 1 : 0; }
 // partials of y instead of forward statistics (see ConvArgs).
 // bn_acc (optional, instead of part): accumulated BatchNorm statistics, see ConvArgs::bn_acc;
 // [2][Cout] doubles, zero on entry (the BN layer that consumes them zeroes them again).
-// tpb: output tiles per block (the persistent form, see conv_fwd_body; 1 with split-K).
 hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part, const void* add,
                              const uint8_t* addmask,
                              const void* bnx, const uint8_t* bnmask, const float* bnmean, int N,
                              int H, int W, int C, int Cout, int R, int S, int stride, int pad_h,
                              int pad_w, int Ho, int Wo, const int* y_map, int c16, int variant,
-                             double* bn_acc, int ksplit, void* kws, unsigned* kcnt, int tpb,
-                             const float* pre, hipStream_t st) {
+                             double* bn_acc, int ksplit, void* kws, unsigned* kcnt,
+                             hipStream_t st) {
   if (Cout % 64 || N <= 0 || R <= 0 || S <= 0 || stride <= 0) return hipErrorInvalidValue;
-  if (tpb < 1 || (tpb > 1 && ksplit != 1)) return hipErrorInvalidValue;
   if (c16 ? (C != 16 || S % 4) : (C % kBK)) return hipErrorInvalidValue;
   ConvArgs a{};
   a.x = (const uint16_t*)x;
@@ -2086,14 +1828,11 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.ksplit = ksplit;
   a.kws = (float4*)kws;
   a.kcnt = kcnt;
-  a.tpb = tpb;
   a.st1p = g_conv_st1p;
-  a.pre = pre;
   if (v2) {
     if (c16) return hipErrorInvalidValue;
     return launch2(a, variant - kV2Base, st);
   }
-  if (pre != nullptr) return hipErrorInvalidValue;   // the BN fold runs on the v2 / halo tiles
   if (variant >= 12) {   // 256-row tiles, 8 waves: 12/13 two stage buffers, 14/15 three
     const int nb = variant >= 14 ? 3 : 2;
     if ((variant & 1) == 0)
@@ -2131,7 +1870,6 @@ hipError_t arena_conv_fwd_phases(const void* x, void* y, const void* add, int N,
   a.mapped = 1; a.Hy = Hy; a.Wy = Wy; a.osh = osh; a.osw = osw;
   a.coal = 1;
   a.ksplit = 1;
-  a.tpb = 1;
   const long long xb = (long long)N * H * W * C * 2;
   if (xb >= (1LL << 31) || osh <= 0 || osw <= 0) return hipErrorInvalidValue;
   a.xbytes = (int)xb;
@@ -2163,7 +1901,7 @@ hipError_t arena_conv_fwd(const void* x, const void* w, void* y, float* part, co
                           int variant, hipStream_t st) {
   return arena_conv_fwd_ex(x, w, y, part, add, nullptr, bnx, bnmask, bnmean, N, H, W, C, Cout, R, S,
                            stride, pad, pad, 0, 0, nullptr, 0, variant, nullptr, 1, nullptr, nullptr,
-                           1, nullptr, st);
+                           st);
 }
 
 // Split-K workspace of one launch, in floats (0 when ksplit == 1), and its ticket count (tiles).
@@ -2182,9 +1920,7 @@ static void conv_tile(int variant, int* bm, int* bn) {
 }
 
 long long arena_conv_fwd_ksplit_floats(long long M, int Cout, int variant, int ksplit) {
-  if (ksplit <= 1 || variant < 0 ||
-      (variant > 15 && !(variant >= kV2Base && variant < kV2Base + kV2Count)))
-    return 0;
+  if (ksplit <= 1 || variant < 0 || variant > 15) return 0;   // split-K: the v1 tiles only
   int bm, bn;
   conv_tile(variant, &bm, &bn);
   return ((M + bm - 1) / bm) * (Cout / bn) * ksplit * bm * bn;
@@ -2567,10 +2303,6 @@ struct WgradArgs {
   int c16;             // C == 16, a BN = 64 column tile = one filter row x 4 columns x 16 channels
   int xbytes, dybytes; // buffer-descriptor ranges (both < 2^31 bytes, host-checked)
   int aff;             // 1x1, stride 1, no padding: X pixel m is output pixel m (affine staging)
-  // BatchNorm-apply fold (see ConvArgs::pre): x is the raw input of the ReLU BN whose output the
-  // convolution consumed, pre = its [3][C] (mean, scale, shift); the X image is normalised in LDS
-  // once per staged step (padded taps stay zero)
-  const float* pre;
 };
 
 // chunk permutation of a pixel row of RB bytes (bit 0 of the chunk index is kept: 32-B pairs)
@@ -2582,7 +2314,7 @@ __device__ __forceinline__ int wswz(int row) {
 
 // NBUF 2: double-buffered pixel steps; NBUF 1 (variants 4..7): one buffer, serial steps, four
 // waves per SIMD -- more blocks per CU hide the staging latency instead (see conv_fwd_kernel_occ4).
-template <int BM, int BN, int NBUF, bool PRE = false>
+template <int BM, int BN, int NBUF>
 __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
   constexpr int RA = BM * 2, RBB = BN * 2;        // row bytes of the A (dY) and B (X) images
   constexpr int CA = RA / 16, CB = RBB / 16;       // 16-byte chunks per row
@@ -2590,8 +2322,7 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
   constexpr int AI = kPix * CA / kThreads, BI = kPix * CB / kThreads;
   constexpr int kBuf = kPix * (RA + RBB);
   constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NI = WN / 16;
-  // PRE: the folded BN's coefficients of this block's BN input channels behind the stage buffers
-  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf + (PRE ? 3 * BN * 4 : 0)];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = a.m_tiles * a.n_tiles;
@@ -2700,39 +2431,11 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
 
   // BN fold: the X image of step `step` in buffer `buf` through relu(fma(x - mean, scale, shift));
   // thread = one logical chunk of rows tid / CB + k * kThreads / CB (one chunk's coefficients)
-  auto pre_x = [&](int buf, int step) {
-    if constexpr (PRE) {
-      const int lc = tid % CB;
-      const PreCoef pk = pre_coef(reinterpret_cast<const float*>(lds + NBUF * kBuf), BN, lc * 8);
-      uint8_t* bb = lds + buf * kBuf + kPix * RA;
-      const int p0 = (step0 + step) * kPix;
-      for (int row = tid / CB; row < kPix; row += kThreads / CB) {
-        const int m = p0 + row;
-        bool ok = m < a.M;
-        if (ok && !a.aff) {   // a padded tap stays zero (the BN output's zero padding)
-          const int n = (int)fdiv((uint32_t)m, a.div_hw);
-          const int rem = m - n * a.Ho * a.Wo;
-          const int ho = (int)fdiv((uint32_t)rem, a.div_w);
-          const int wo = rem - ho * a.Wo;
-          ok = (unsigned)(ho * a.stride - a.pad + rr) < (unsigned)a.H &&
-               (unsigned)(wo * a.stride - a.pad_w + ss) < (unsigned)a.W;
-        }
-        if (ok) pre_lds(bb + row * RBB + ((lc ^ wswz<RBB>(row)) << 4), pk);
-      }
-      lds_barrier();
-    }
-  };
-  if constexpr (PRE) {
-    float* tab = reinterpret_cast<float*>(lds + NBUF * kBuf);
-    for (int i = tid; i < 3 * BN; i += kThreads) tab[i] = a.pre[(i / BN) * a.C + ci0 + i % BN];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // visible after the first barrier
-  }
 
   if (nsteps > 0) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    pre_x(0, 0);
   }
   for (int t = 0; t < nsteps; ++t) {
     const int cur = NBUF == 1 ? 0 : (t & 1);
@@ -2774,7 +2477,6 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (t + 1 < nsteps) pre_x(NBUF == 1 ? 0 : (cur ^ 1), t + 1);
   }
 
   // lane holds D[co = .. + 4*g + reg][kk = .. + (lane & 15)]
@@ -2792,18 +2494,18 @@ __device__ __forceinline__ void conv_wgrad_body(const WgradArgs& a) {
     }
 }
 
-template <int BM, int BN, bool PRE = false>
+template <int BM, int BN>
 __global__ __launch_bounds__(kThreads) void conv_wgrad_kernel(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)   // the body uses device-only builtins
-  conv_wgrad_body<BM, BN, 2, PRE>(a);
+  conv_wgrad_body<BM, BN, 2>(a);
 #endif
 }
 
-template <int BM, int BN, bool PRE = false>
+template <int BM, int BN>
 __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(4)))
 void conv_wgrad_kernel_occ4(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv_wgrad_body<BM, BN, 1, PRE>(a);
+  conv_wgrad_body<BM, BN, 1>(a);
 #endif
 }
 
@@ -2886,7 +2588,7 @@ FastDiv make_fastdiv(uint32_t d) {
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int wswz2(int row) { return 4 * (row & 3); }
 
-template <int BM, int BN, int NWM, int NWN, int NBUF, bool PRE = false>
+template <int BM, int BN, int NWM, int NWN, int NBUF>
 __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int RA = BM * 2, RBB = BN * 2;        // row bytes of the dY and X images
@@ -2898,8 +2600,7 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
   static_assert(CA >= 16 && CB >= 16, "the 64-byte granule permutation needs >= 256-byte rows");
   static_assert(AI >= 1 && BI >= 1 && MI >= 1 && NI >= 1, "tile too small for the wave grid");
   static_assert(AI * NT == kPix * CA && BI * NT == kPix * CB, "staging slots must cover the tile");
-  // PRE: the folded BN's coefficients of this block's BN input channels behind the stage buffers
-  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf + (PRE ? 3 * BN * 4 : 0)];
+  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tiles = a.m_tiles * a.n_tiles;
@@ -2989,34 +2690,6 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
   const int wm = wave / NWN, wn = wave % NWN;
   const int g = lane >> 4, qq = (lane >> 2) & 3, pp = lane & 3;
 
-  // BN fold (see conv_wgrad_body's pre_x), granule permutation wswz2
-  auto pre_x = [&](int buf, int step) {
-    if constexpr (PRE) {
-      const int lc = tid % CB;
-      const PreCoef pk = pre_coef(reinterpret_cast<const float*>(lds + NBUF * kBuf), BN, lc * 8);
-      uint8_t* bb = lds + buf * kBuf + kPix * RA;
-      const int p0 = (step0 + step) * kPix;
-      for (int row = tid / CB; row < kPix; row += NT / CB) {
-        const int m = p0 + row;
-        bool ok = m < a.M;
-        if (ok && !a.aff) {
-          const int n = (int)fdiv((uint32_t)m, a.div_hw);
-          const int rem = m - n * a.Ho * a.Wo;
-          const int ho = (int)fdiv((uint32_t)rem, a.div_w);
-          const int wo = rem - ho * a.Wo;
-          ok = (unsigned)(ho * a.stride - a.pad + rr) < (unsigned)a.H &&
-               (unsigned)(wo * a.stride - a.pad_w + ss) < (unsigned)a.W;
-        }
-        if (ok) pre_lds(bb + row * RBB + ((lc ^ wswz2(row)) << 4), pk);
-      }
-      lds_barrier();
-    }
-  };
-  if constexpr (PRE) {
-    float* tab = reinterpret_cast<float*>(lds + NBUF * kBuf);
-    for (int i = tid; i < 3 * BN; i += NT) tab[i] = a.pre[(i / BN) * a.C + ci0 + i % BN];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // visible after the first barrier
-  }
 
   auto compute = [&](int buf) {
     const uint8_t* abuf = lds + buf * kBuf;
@@ -3057,7 +2730,6 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
     stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    pre_x(0, 0);
     for (int t = 0; t < nsteps; ++t) {
       compute(0);
       if (t + 1 < nsteps) {
@@ -3066,7 +2738,6 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
-      if (t + 1 < nsteps) pre_x(0, t + 1);
     }
   } else if (nsteps > 0) {
     constexpr int S = NBUF > 1 ? NBUF - 1 : 1;
@@ -3080,7 +2751,6 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    pre_x(0, 0);
     int cur = 0;
     for (int t = 0; t < nsteps; ++t) {
       if (t + S < nsteps) stage(t + S, cur == 0 ? NBUF - 1 : cur - 1);
@@ -3092,7 +2762,6 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       cur = cur == NBUF - 1 ? 0 : cur + 1;
-      if (t + 1 < nsteps) pre_x(cur, t + 1);
     }
   }
 
@@ -3113,19 +2782,19 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
     }
 }
 
-template <int BM, int BN, int NWM, int NWN, int NBUF, bool PRE = false>
+template <int BM, int BN, int NWM, int NWN, int NBUF>
 __global__ __launch_bounds__(64 * NWM * NWN) void conv_wgrad2_kernel(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv_wgrad2_body<BM, BN, NWM, NWN, NBUF, PRE>(a);
+  conv_wgrad2_body<BM, BN, NWM, NWN, NBUF>(a);
 #endif
 }
 
 // serial single-buffer form, <= 128 VGPRs: four waves per SIMD (v1's variants 4..7 structure)
-template <int BM, int BN, bool PRE = false>
+template <int BM, int BN>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4)))
 void conv_wgrad2_kernel_occ4(WgradArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv_wgrad2_body<BM, BN, 2, 2, 1, PRE>(a);
+  conv_wgrad2_body<BM, BN, 2, 2, 1>(a);
 #endif
 }
 
@@ -3143,15 +2812,8 @@ hipError_t launch_wgrad2(WgradArgs a, int splits_hint, hipStream_t st) {
   a.sps = (total + splits - 1) / splits;
   a.splits = (total + a.sps - 1) / a.sps;
   if constexpr (OCC4) {
-    if (a.pre)
-      hipLaunchKernelGGL((conv_wgrad2_kernel_occ4<BM, BN, true>), dim3(tiles * a.splits),
-                         dim3(256), 0, st, a);
-    else
-      hipLaunchKernelGGL((conv_wgrad2_kernel_occ4<BM, BN>), dim3(tiles * a.splits), dim3(256),
-                         0, st, a);
-  } else if (a.pre) {
-    hipLaunchKernelGGL((conv_wgrad2_kernel<BM, BN, NWM, NWN, NBUF, true>), dim3(tiles * a.splits),
-                       dim3(64 * NWM * NWN), 0, st, a);
+    hipLaunchKernelGGL((conv_wgrad2_kernel_occ4<BM, BN>), dim3(tiles * a.splits), dim3(256), 0,
+                       st, a);
   } else {
     hipLaunchKernelGGL((conv_wgrad2_kernel<BM, BN, NWM, NWN, NBUF>), dim3(tiles * a.splits),
                        dim3(64 * NWM * NWN), 0, st, a);
@@ -3169,15 +2831,9 @@ hipError_t launch_wgrad(WgradArgs a, int splits_hint, bool serial, hipStream_t s
   splits = std::min(splits, total);
   a.sps = (total + splits - 1) / splits;
   a.splits = (total + a.sps - 1) / a.sps;
-  if (serial && a.pre)
-    hipLaunchKernelGGL((conv_wgrad_kernel_occ4<BM, BN, true>), dim3(tiles * a.splits),
-                       dim3(kThreads), 0, st, a);
-  else if (serial)
+  if (serial)
     hipLaunchKernelGGL((conv_wgrad_kernel_occ4<BM, BN>), dim3(tiles * a.splits), dim3(kThreads), 0,
                        st, a);
-  else if (a.pre)
-    hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN, true>), dim3(tiles * a.splits), dim3(kThreads),
-                       0, st, a);
   else
     hipLaunchKernelGGL((conv_wgrad_kernel<BM, BN>), dim3(tiles * a.splits), dim3(kThreads), 0, st,
                        a);
@@ -3213,8 +2869,7 @@ int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int varia
 hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* dw_bf16,
                                float* dw_f32, int N, int H, int W, int C, int Cout, int R, int S,
                                int stride, int pad_h, int pad_w, int Ho, int Wo, int c16,
-                               int variant, int splits_hint, float scale, const float* pre,
-                               hipStream_t st) {
+                               int variant, int splits_hint, float scale, hipStream_t st) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
   if (variant < 0 || variant > 12) return hipErrorInvalidValue;
   const bool v2 = variant >= 8;
@@ -3225,9 +2880,7 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
   if (v2 && c16) return hipErrorInvalidValue;
   if (c16 ? (C != 16 || S % 4 || tbn != 64) : (C % tbn != 0)) return hipErrorInvalidValue;
   if (Cout % tbm || N <= 0 || stride <= 0) return hipErrorInvalidValue;
-  if (pre != nullptr && c16) return hipErrorInvalidValue;
   WgradArgs a{};
-  a.pre = pre;
   a.x = (const uint16_t*)x;
   a.dy = (const uint16_t*)dy;
   a.ws = ws;
@@ -3287,16 +2940,7 @@ hipError_t arena_conv_wgrad(const void* x, const void* dy, float* ws, void* dw_b
                             int N, int H, int W, int C, int Cout, int R, int S, int stride,
                             int pad, int variant, int splits_hint, float scale, hipStream_t st) {
   return arena_conv_wgrad_ex(x, dy, ws, dw_bf16, dw_f32, N, H, W, C, Cout, R, S, stride, pad, pad,
-                             0, 0, 0, variant, splits_hint, scale, nullptr, st);
-}
-
-// the BN-fold form (WgradArgs::pre: x is the raw input of the BN whose output the conv consumed)
-hipError_t arena_conv_wgrad_pre(const void* x, const void* dy, float* ws, void* dw_bf16,
-                                float* dw_f32, int N, int H, int W, int C, int Cout, int R, int S,
-                                int stride, int pad, int variant, int splits_hint, float scale,
-                                const float* pre, hipStream_t st) {
-  return arena_conv_wgrad_ex(x, dy, ws, dw_bf16, dw_f32, N, H, W, C, Cout, R, S, stride, pad, pad,
-                             0, 0, 0, variant, splits_hint, scale, pre, st);
+                             0, 0, 0, variant, splits_hint, scale, st);
 }
 
 }  // extern "C"

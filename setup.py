@@ -47,6 +47,7 @@ try:
         def build_extensions(self):
             os.makedirs(obj_dir, exist_ok=True)
             hipcc = os.path.join(ROCM, "bin", "hipcc")
+            cmds = []
             for src, obj in zip(HIP_SOURCES, hip_objs):
                 srcp = os.path.join(HERE, src)
                 deps = [srcp] + [os.path.join(HERE, "csrc", "ops", h)
@@ -54,11 +55,18 @@ try:
                 if os.path.exists(obj) and all(os.path.getmtime(obj) >= os.path.getmtime(d)
                                                for d in deps):
                     continue
-                cmd = [hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
-                       "-ffp-contract=fast", "-I", os.path.join(HERE, "csrc", "ops"), "-c", srcp,
-                       "-o", obj] + TIMELINE
+                cmds.append([hipcc, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC",
+                             "-ffp-contract=fast", "-I", os.path.join(HERE, "csrc", "ops"), "-c",
+                             srcp, "-o", obj] + TIMELINE)
+            # independent translation units: compile them concurrently (the conv kernels alone
+            # take minutes; the others finish under it)
+            from concurrent.futures import ThreadPoolExecutor
+            jobs = max(1, min(len(cmds), int(os.environ.get("MAX_JOBS", os.cpu_count() or 1))))
+            for cmd in cmds:
                 print(" ".join(cmd), flush=True)
-                subprocess.run(cmd, check=True)
+            with ThreadPoolExecutor(jobs) as pool:
+                for r in pool.map(lambda c: subprocess.run(c, check=True), cmds):
+                    pass
             super().build_extensions()
 
     ext_modules = [

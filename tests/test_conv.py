@@ -240,9 +240,7 @@ def test_v2_variants_are_forward_and_dgrad_only():
     assert not conv.halo_variants_for(256, (3, 3), 2, 1, 14)
     assert not conv.halo_variants_for(256, (3, 3), 1, 1, 64)
     assert not conv.halo_variants_for(256, (1, 1), 1, 0, 14)
-    assert all(conv.tiles_per_block(v) == 1 and conv.split_of(v) == 1 for v in conv.V2_TILES)
     assert not set(conv.variants_for(256)) & set(conv.V2_TILES)   # disjoint code ranges
-    assert conv.persist_variants_for(128 * 56 * 56, 256, list(conv.V2_TILES)) == []
     # v2 weight gradients need >= 128-channel tiles on both sides
     assert not set(conv.wgrad_variants_for(64, 256)) & set(conv.WGRAD_V2)
     assert set(conv.wgrad_variants_for(256, 256)) >= set(conv.WGRAD_V2)
@@ -292,137 +290,6 @@ def test_conv_split_k_matches_unsplit(shape):
             kv = conv.kvariant(v, 2)
             dxa = conv.conv2d_bwd_data(dy, wt, pad, kv, addend=addend)
             assert _rel(dxa, dx_ref + addend.float()) < 1e-2, (v, _rel(dxa, dx_ref + addend.float()))
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(2, 256, 7, 7, 128, 3, 1), (3, 128, 6, 5, 256, 1, 1),
-                                   (2, 512, 7, 7, 256, 1, 1), (1, 192, 5, 9, 128, 3, 1)])
-def test_conv_v2_split_k_matches_fp32(shape):
-    """v2 / halo split-K forms (slabs + ticket, last block sums slices in order and runs the
-    epilogue): forward, statistics (partials and finished sums), backward-data with the masked
-    addend and the linked BN-backward partials, against fp32 references -- bit-identical run to
-    run. Uneven slices (3 over 9 K steps, 3 over 3 channel chunks) included."""
-    from arena_amd.ops import _ext
-    from arena_amd.ops.batchnorm import BatchNormAct2d
-    _ext.load()
-    n, cin, h, w, cout, k, st = shape
-    pad = k // 2
-    x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=9)
-    ref = F.conv2d(x.float(), wt.float(), stride=st, padding=pad)
-
-    def splits(v, ktot):
-        cap = ktot // (9 * 64) if v in conv.V2_HALO else ktot // 64
-        return [v + 16 * (s - 1) for s in (2, 3, 4) if s <= cap]
-
-    bases = conv.v2_variants_for(cout) + conv.halo_variants_for(cout, (k, k), st, pad, w)
-    for v in bases:
-        for kv in splits(v, cin * k * k):
-            assert conv.v2_base(kv) == v and conv.TILES[kv] == conv.TILES[v]
-            y = conv.conv2d_fwd(x, wt, st, pad, kv)
-            assert _rel(y, ref) < 1e-2, (kv, _rel(y, ref))
-            assert torch.equal(conv.conv2d_fwd(x, wt, st, pad, kv), y), kv
-            yp, stats = conv.conv2d_fwd(x, wt, st, pad, kv, with_stats=True)
-            yf, fin = conv.conv2d_fwd(x, wt, st, pad, kv, with_stats=True, final=True)
-            assert torch.equal(yp, y) and torch.equal(yf, y) and stats[1] == conv.TILES[v][0]
-            bns = [BatchNormAct2d(cout).cuda() for _ in range(3)]
-            r = bns[0](y)
-            assert _rel(bns[1](y, stats=stats), r) < 1e-2, kv
-            assert _rel(bns[2](y, stats=fin), r) < 1e-2, kv
-            torch.testing.assert_close(bns[2].running_var, bns[0].running_var, rtol=1e-3,
-                                       atol=1e-5)
-    dy = torch.randn(ref.shape, device="cuda").to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    dx_ref = torch.ops.aten.convolution_backward(
-        dy.float(), x.float(), wt.float(), None, [1, 1], [pad, pad], [1, 1], False, [0, 0], 1,
-        [True, False, False])[0]
-    addend = torch.randn(x.shape, device="cuda").to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    bits = torch.randint(0, 256, (addend.numel() // 8,), device="cuda", dtype=torch.uint8)
-    dense = conv.MaskedGrad(addend, bits).materialize()
-    bnx = torch.randn(x.shape, device="cuda").to(torch.bfloat16).contiguous(
-        memory_format=torch.channels_last)
-    m = x.shape[0] * x.shape[2] * x.shape[3]
-    mean = torch.randn(cin, device="cuda") * 0.3
-    xc = bnx.permute(0, 2, 3, 1).reshape(m, cin).float() - mean
-    bases = conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, pad, w)
-    for v in bases:
-        for kv in splits(v, cout * k * k):
-            dx = conv.conv2d_bwd_data(dy, wt, pad, kv)
-            assert _rel(dx, dx_ref) < 1e-2, (kv, _rel(dx, dx_ref))
-            a = conv.conv2d_bwd_data(dy, wt, pad, kv, addend=addend, addmask=bits)
-            assert torch.equal(a, conv.conv2d_bwd_data(dy, wt, pad, kv, addend=dense)), kv
-            assert _rel(a, dx_ref + dense.float()) < 1e-2, kv
-            dxl, (part, rpb) = conv.conv2d_bwd_data(dy, wt, pad, kv, bn=(bnx, bits, mean))
-            assert torch.equal(dxl, dx), kv
-            g = dx.permute(0, 2, 3, 1).reshape(m, cin).float() * \
-                conv._unpack_bits(bits, dx).permute(0, 2, 3, 1).reshape(m, cin).float()
-            p = part.view(-1, 2, cin)
-            torch.testing.assert_close(p[:, 0].sum(0), g.sum(0), rtol=1e-3, atol=1e-2)
-            torch.testing.assert_close(p[:, 1].sum(0), (g * xc).sum(0), rtol=1e-3, atol=1e-2)
-
-
-def test_v2_split_variants_only_for_underfilled_grids(monkeypatch):
-    V2 = conv.V2
-    monkeypatch.setattr(conv, "_V2_SPLIT_ON", False)
-    assert conv.v2_split_variants_for(128 * 7 * 7, 512, 2048, [V2 + 2]) == []   # off by default
-    monkeypatch.setattr(conv, "_V2_SPLIT_ON", True)
-    # 56x56 x 256 at batch 128: 3136 row tiles, never split
-    assert conv.v2_split_variants_for(128 * 56 * 56, 256, 256, [V2 + 2, V2 + 8]) == []
-    # 7x7 x 512, K = 2048 (196 tiles of 128x128): splits toward 1, 2 and 4 blocks per CU
-    sv = conv.v2_split_variants_for(128 * 7 * 7, 512, 2048, [V2 + 2, V2 + 0])
-    assert sv and all(conv.split_of(v) > 1 and conv.v2_base(v) in (V2 + 2, V2 + 0) for v in sv)
-    assert all(2048 // 64 // conv.split_of(v) >= 4 for v in sv)
-    # halo forms split over 64-channel chunks: 3x3 x 128 input channels has two
-    hv = conv.v2_split_variants_for(128 * 7 * 7, 128, 9 * 128, [V2 + 12, V2 + 13])
-    assert hv and all(conv.split_of(v) == 2 for v in hv)
-    # split codes are never bases, and bases of other codes are themselves
-    assert conv.v2_split_variants_for(128 * 7 * 7, 512, 2048, [V2 + 2 + 16]) == []
-    assert conv.v2_base(V2 + 2 + 48) == V2 + 2 and conv.v2_base(5) == 5
-
-
-@pytest.mark.gpu
-@pytest.mark.parametrize("shape", [(4, 64, 14, 14, 128, 3, 1), (3, 128, 9, 7, 256, 1, 1),
-                                   (2, 64, 17, 17, 64, 3, 2)])
-def test_conv_persistent_tiles_match_one_tile_per_block(shape):
-    """Persistent variants (2^p output tiles of one column tile per block, BatchNorm sums merged
-    in LDS and flushed once): outputs and per-tile partials bit-identical to the one-tile form,
-    epilogue-summed statistics equal to rounding, ragged last row chunks and tail rows included;
-    the backward-data pass too."""
-    n, cin, h, w, cout, k, st = shape
-    pad = k // 2
-    x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=7)
-    for v in conv.variants_for(cout):
-        y, (part, rpb) = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True)
-        _, fin = conv.conv2d_fwd(x, wt, st, pad, v, with_stats=True, final=True)
-        ref_sums = fin.sums()
-        fin.discard()
-        for p in (1, 2, 3):
-            pv = v + 256 * p
-            assert conv.tiles_per_block(pv) == 1 << p and conv.TILES[pv] == conv.TILES[v]
-            y2, (part2, rpb2) = conv.conv2d_fwd(x, wt, st, pad, pv, with_stats=True)
-            assert torch.equal(y2, y) and rpb2 == rpb and torch.equal(part2, part), (v, p)
-            y3, fin3 = conv.conv2d_fwd(x, wt, st, pad, pv, with_stats=True, final=True)
-            assert torch.equal(y3, y)
-            torch.testing.assert_close(fin3.sums(), ref_sums, rtol=1e-9, atol=1e-6)
-            fin3.discard()
-    if st == 1:
-        dy = torch.randn(n, cout, h, w, device="cuda").to(torch.bfloat16).contiguous(
-            memory_format=torch.channels_last)
-        for v in conv.variants_for(cin):
-            dx = conv.conv2d_bwd_data(dy, wt, pad, v)
-            for p in (1, 2):
-                assert torch.equal(conv.conv2d_bwd_data(dy, wt, pad, v + 256 * p), dx), (v, p)
-
-
-def test_persist_variants_keep_the_chip_filled():
-    # 56x56 x 256 at batch 128 (3136 row tiles of 128): up to 16 tiles per block still fills it
-    pv = conv.persist_variants_for(128 * 56 * 56, 256, [0, 9])
-    assert {conv.tiles_per_block(v) for v in pv} == {2, 4, 8, 16}
-    assert all(-(-128 * 56 * 56 // conv.TILES[v][0]) * (256 // conv.TILES[v][1])
-               // conv.tiles_per_block(v) >= conv._CUS for v in pv)
-    # 7x7 x 512: too few tiles for any
-    assert conv.persist_variants_for(128 * 7 * 7, 512, [0]) == []
-    assert conv.persist_variants_for(128 * 56 * 56, 256, [0 + 16]) == []   # split-K: never
 
 
 def test_wgrad_candidates_aim_at_blocks_per_cu():

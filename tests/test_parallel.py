@@ -142,31 +142,54 @@ def test_hvd_broadcast_optimizer_state_recurses_groups():
     assert res[0][0] == 4.0
 
 
-def _hvd_root_only_state_worker(rank, world, port, q):
+def _hvd_root_only_state_worker(rank, world, port, q, device="cpu", fused=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
     torch.set_num_threads(1)
     from torch import nn
     from arena_amd.parallel import hvd
+    if device == "cuda":
+        torch.cuda.set_device(0)
     hvd.init("gloo")
     try:
         torch.manual_seed(3)
-        m = nn.Linear(3, 5)
-        o = torch.optim.Adam(m.parameters(), lr=0.1)
+        m = nn.Linear(3, 5).to(device)
+        o = torch.optim.Adam(m.parameters(), lr=0.1, fused=fused or None)
         if rank == 0:       # "checkpoint loaded on the root only": only rank 0 has state
-            m(torch.ones(2, 3)).sum().backward()
+            m(torch.ones(2, 3, device=device)).sum().backward()
             o.step()
             o.step()
         hvd.broadcast_optimizer_state(o, root_rank=0)
         st = [o.state[p] for p in m.parameters()]
-        q.put((rank, {"m": torch.cat([s["exp_avg"].reshape(-1) for s in st]).numpy(),
-                      "v": torch.cat([s["exp_avg_sq"].reshape(-1) for s in st]).numpy(),
-                      "step": [float(s["step"]) for s in st]}))
+        q.put((rank, {"m": torch.cat([s["exp_avg"].reshape(-1) for s in st]).cpu().numpy(),
+                      "v": torch.cat([s["exp_avg_sq"].reshape(-1) for s in st]).cpu().numpy(),
+                      "step": [float(s["step"]) for s in st],
+                      "step_dev": [s["step"].device.type for s in st]}))
         # the optimizer keeps working on every rank afterwards
-        m(torch.ones(2, 3)).sum().backward()
+        m(torch.ones(2, 3, device=device)).sum().backward()
         o.step()
     finally:
         hvd.shutdown()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(180)
+def test_hvd_broadcast_optimizer_state_root_only_fused_adam():
+    """ADVICE r5 (hvd.py:328): with Adam(fused=True) the root's "step" lives on the GPU; rank 1
+    (no state) must create it there too, or the (dtype, device)-grouped broadcast sizes differ."""
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_hvd_root_only_state_worker, args=(r, world, port, q, "cuda", True))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=150) for _ in range(world))
+    for p in procs:
+        p.join(30)
+        assert p.exitcode == 0
+    np.testing.assert_array_equal(res[0]["m"], res[1]["m"])
+    assert res[1]["step"] == [2.0, 2.0] and res[1]["step_dev"] == ["cuda", "cuda"], res
 
 
 @pytest.mark.timeout(120)

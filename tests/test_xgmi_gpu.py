@@ -893,3 +893,44 @@ def test_sharded_sgd_rccl_backend_on_gpu():
     res = out[0]
     assert res["backend"] == "rccl", res
     assert res["w_bits"] == 0 and res["master_bits"] == 0, res   # exact hyperparameters
+
+
+def _selftest_forms(rank, world, port, q):
+    """Construction-time self-test: every kernel kind the communicator serves (one-/two-shot
+    allreduce, fused Adam, sharded SGD bf16/f32, both broadcast forms, all-gather) runs on
+    pre-warmed buffers and must be bit-exact; the default form is pull; ARENA_XGMI_PUSH=1 keeps
+    the push form only because its own self-test passed. Then a sharded-SGD step per form."""
+    try:
+        _init(rank, world, port)
+        from arena_amd.parallel.xgmi import XgmiComm
+        res = {}
+        for push in ("0", "1"):
+            os.environ["ARENA_XGMI_PUSH"] = push
+            comm = XgmiComm(staging_elems=400000, param_elems=400000, timeout_s=30.0)
+            res[push] = {"form": comm.form, "selftest": dict(comm.selftest_result),
+                         "push_flag": bool(comm.peers.push)}
+            comm.check()
+            comm.close()
+        os.environ.pop("ARENA_XGMI_PUSH", None)
+        import torch.distributed as dist
+        dist.barrier()
+        dist.destroy_process_group()
+        q.put((rank, res, None))
+    except Exception:  # noqa: BLE001
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_xgmi_selftest_every_kernel_pull_default(world):
+    out = _run(_selftest_forms, world, timeout=300)
+    kinds = {"allreduce_oneshot", "allreduce_twoshot", "adam", "sgd_bf16", "sgd_f32",
+             "broadcast_direct", "allgather"}
+    if world > 2:
+        kinds.add("broadcast_twoshot")
+    for r, res in out.items():
+        pull, push = res["0"], res["1"]
+        assert pull["form"] == "pull" and not pull["push_flag"], (r, res)
+        assert push["form"] == "push" and push["push_flag"], (r, res)
+        for d in (pull, push):
+            assert kinds <= set(d["selftest"]), (r, d)
+            assert all(v == "ok" for v in d["selftest"].values()), (r, d)

@@ -51,7 +51,8 @@ def _grads(step, rank, params):
     return out
 
 
-def _worker(rank, world, port, reduce_fp32, q, backend="rccl", local_size=None):
+def _worker(rank, world, port, reduce_fp32, q, backend="rccl", local_size=None,
+            skew_order=False):
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                           WORLD_SIZE=str(world))
@@ -89,6 +90,13 @@ def _worker(rank, world, port, reduce_fp32, q, backend="rccl", local_size=None):
             unused = 4 if step == 1 else -1          # parameter 4 gets no gradient in step 1
             for i, ((p, _), g) in enumerate(zip(params, grads[rank])):
                 p.grad = None if i == unused else g.clone()
+            if skew_order:
+                # gradients become ready in a rank-dependent order (data-dependent control flow):
+                # rank 0 output side first, the others input side first
+                idx = list(range(len(params)))
+                for i in (idx[::-1] if rank == 0 else idx):
+                    if i != unused:
+                        opt._on_grad(params[i][0])
             opt.step()
             opt.zero_grad()
             for i, r in enumerate(ref):
@@ -123,12 +131,12 @@ def _worker(rank, world, port, reduce_fp32, q, backend="rccl", local_size=None):
         q.put((rank, None, traceback.format_exc()))
 
 
-def _run(world, reduce_fp32, backend="rccl", local_size=None):
+def _run(world, reduce_fp32, backend="rccl", local_size=None, skew_order=False):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _port()
     procs = [ctx.Process(target=_worker, args=(r, world, port, reduce_fp32, q, backend,
-                                                local_size))
+                                                local_size, skew_order))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -215,7 +223,10 @@ def test_hier_rejects_bad_local_size():
         with pytest.raises(ValueError, match="1 < local_size < world"):
             ShardedMasterSGD([p], lr=0.1, backend="hier", local_size=1)
         with pytest.raises(ValueError, match="must divide"):
-            ShardedMasterSGD([p], lr=0.1, backend="rccl", local_size=3)
+            ShardedMasterSGD([p], lr=0.1, backend="hier", local_size=3)
+        # flat RCCL never uses local_size: a non-dividing value is not an error there
+        ShardedMasterSGD([torch.nn.Parameter(torch.randn(8, 8).to(torch.bfloat16))], lr=0.1,
+                         backend="rccl", local_size=3).close()
         with pytest.raises(ValueError, match="backend must be"):
             ShardedMasterSGD([p], lr=0.1, backend="ring")
         opt = ShardedMasterSGD([p], lr=0.1, backend="auto")   # one rank: flat, no level groups
@@ -223,3 +234,31 @@ def test_hier_rejects_bad_local_size():
         opt.close()
     finally:
         dist.destroy_process_group()
+
+
+def test_bucket_launch_order_independent_of_gradient_order():
+    """ADVICE r5 (zero.py:458): with overlap, a bucket used to launch as soon as its gradients
+    were ready on THAT rank, so ranks whose gradients arrive in different orders issued their
+    collectives in different orders (hang, or one bucket reduced against another). Buckets now
+    launch strictly in index order; the result must still match torch SGD on every rank."""
+    out = _run(2, True, skew_order=True)
+    for r, res in out.items():
+        assert res["master_rel"] < 1e-5 and res["w_vs_master"] == 0.0, (r, res)
+    assert len({res["digest"] for res in out.values()}) == 1, out
+
+
+def test_uneven_local_world_size_falls_back_to_flat(monkeypatch):
+    """ADVICE r5 (zero.py:593): a LOCAL_WORLD_SIZE that does not divide the world only rules
+    the hierarchical backend out; it no longer fails flat RCCL."""
+    from arena_amd.parallel.zero import ShardedMasterSGD
+    o = ShardedMasterSGD.__new__(ShardedMasterSGD)
+    o.world = 6
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "4")
+    assert o._local_size(None, strict=False) == 6
+    o.local_size = 6
+    assert o._flat_or_hier() == "rccl"
+    with pytest.raises(ValueError):
+        o._local_size(None, strict=True)
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "2")
+    o.local_size = o._local_size(None, strict=False)
+    assert o._flat_or_hier() == "hier"

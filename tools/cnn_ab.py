@@ -12,13 +12,11 @@ input/weight casts and weight transform as torch ops) and/or ``:nomask`` (the la
 dy * mask for the residual join instead of parking (dy, bits)) and/or ``:finP<n>`` (at most n
 level-1 blocks per channel group in the BN finalize kernels) and/or ``:redG<b>x<r>`` (BN reduction grid) and/or ``:accP<n>`` (conv-epilogue
 BN statistics as fp64 sums up to n tile-channel pairs) and/or ``:finbwd0`` (BN backward sums
-from the pool plus a finalize launch) and/or ``:nopersist`` (no persistent conv forms) and/or
+from the pool plus a finalize launch) and/or
 ``:nostempool`` (stem BN and max pool unfused) and/or ``:noxsel`` (stem backward sums per pixel
 over x instead of from the saved argmax inputs) and/or ``:noressums`` (down_bn's backward sums
 by its own reduction, not in bn3's dx pass) and/or ``:downfirst`` (downsample shortcut built
-before the main path: its strided dgrad completes the join, no BN link there) and/or ``:fold`` (bn1 / bn2 folded into the
-consuming convs instead of applied by their own pass) and/or ``:v2split`` (split-K forms of the
-v2 tiles among the candidates) and/or ``:linkprice`` (per-layer link pricing) and/or ``:ebk<n>`` (at most n blocks per BN apply pass), ``:dxb<n>`` (per dx pass), ``:noslice`` (flat
+before the main path: its strided dgrad completes the join, no BN link there) and/or ``:ebk<n>`` (at most n blocks per BN apply pass), ``:dxb<n>`` (per dx pass), ``:noslice`` (flat
 grids for C > 256 instead of 256-channel slices),
 joined with ``+``.
 Prints one JSON line per variant: median / min ms per step, images/s.
@@ -66,8 +64,6 @@ def main():
         opts = opt_s.split("+")
         # BN-backward partials in the dgrad epilogue: on by default, "nolink" turns them off
         conv.set_bn_links("nolink" not in opts if "link" not in opts else True)
-        # linkprice: the tuner prices each layer's link against the BN's own reduction pass
-        conv.set_link_choice("linkprice" in opts)
         conv.set_stem_fused("torchstem" not in opt_s.split("+"))
         conv.set_masked_join("nomask" not in opt_s.split("+"))
         # finP<n>: at most n level-1 blocks per channel group in the BN finalize kernels (the
@@ -92,18 +88,12 @@ def main():
         # finbwd0: BN backward sums from the pool + a finalize launch (not the layer's own set)
         from arena_amd.ops import batchnorm as _bn
         _bn.set_fin_bwd("finbwd0" not in opt_s.split("+"))
-        # nopersist: no persistent conv forms among the autotuner's candidates
-        conv.set_persist("nopersist" not in opt_s.split("+"))
         # nostempool: stem BN apply + max pool kernels instead of the fused pass
         _bn.set_stem_pool_fused("nostempool" not in opt_s.split("+"))
         _bn.set_stem_xsel("noxsel" not in opt_s.split("+"))   # stem sums per pixel over x
         _bn.set_res_sums("noressums" not in opt_s.split("+"))   # down_bn reduces itself
         from arena_amd.models import resnet as _rn
         _rn.set_downsample_last("downfirst" not in opt_s.split("+"))   # shortcut built first
-        # fold: bn1 / bn2 folded into the consuming convs (off by default, ARENA_BN_FOLD)
-        conv.set_bn_fold("fold" in opt_s.split("+"))
-        # v2split: the v2 split-K forms among the autotuner's candidates (off by default)
-        conv.set_v2_split("v2split" in opt_s.split("+"))
         # ebk<n>: at most n blocks per BN apply pass (grid baked into the captured graph)
         ebk = [int(o[3:]) for o in opt_s.split("+") if o.startswith("ebk")]
         _e.load().bn_set_elem_max_blocks(ebk[0] if ebk else 1024)
