@@ -47,9 +47,13 @@ V2_TILES = {V2 + 0: (256, 128), V2 + 1: (256, 256), V2 + 2: (128, 128), V2 + 3: 
 # 3x3 / stride 1 / pad 1 halo forms (width <= 63): the tile's input window is staged once per
 # 64-channel chunk and the nine taps read it shifted (conv_kernels.hip Conv2Geo::HALO)
 V2_HALO = {V2 + 12: (128, 128), V2 + 13: (128, 64),
-           V2 + 14: (128, 64)}   # 14: the window of <= 31-wide images (four blocks per CU)
+           V2 + 14: (128, 64),   # 14: the window of <= 31-wide images (four blocks per CU)
+           # 15: two groups of four waves split the 64-channel chunks (two waves per SIMD; even
+           # chunk counts only)
+           V2 + 15: (128, 128)}
 HALO_MAX_W = 63
-HALO_SMALL = {V2 + 14: 31}
+HALO_SMALL = {V2 + v: 31 for v in (14, 15)}
+HALO_SPLIT2 = {V2 + 15}
 V2_TILES.update(V2_HALO)
 TILES.update(V2_TILES)
 _V2_ON = os.environ.get("ARENA_CONV_V2", "1") != "0"
@@ -78,12 +82,14 @@ def v2_variants_for(cout: int):
             if cout % bn == 0 and v not in V2_HALO] if _V2_ON else []
 
 
-def halo_variants_for(cout: int, k, stride: int, pad: int, width: int):
-    """The 3x3 halo forms, for a 3x3 / stride 1 / pad 1 convolution of a <= 63-wide image."""
+def halo_variants_for(cout: int, k, stride: int, pad: int, width: int, cin: int | None = None):
+    """The 3x3 halo forms, for a 3x3 / stride 1 / pad 1 convolution of a <= 63-wide image
+    (``cin``: the input channels; the two-group forms need an even number of 64-channel chunks)."""
     if not _V2_ON or tuple(k) != (3, 3) or stride != 1 or pad != 1 or width > HALO_MAX_W:
         return []
     return [v for v, (_, bn) in V2_HALO.items()
-            if cout % bn == 0 and width <= HALO_SMALL.get(v, HALO_MAX_W)]
+            if cout % bn == 0 and width <= HALO_SMALL.get(v, HALO_MAX_W)
+            and (v not in HALO_SPLIT2 or (cin is None or (cin // 64) % 2 == 0))]
 
 
 def out_hw(h: int, w: int, r: int, s: int, stride: int, pad: int) -> Tuple[int, int]:
@@ -554,7 +560,11 @@ WGRAD_TILES = {0: (128, 128), 1: (128, 64), 2: (64, 128), 3: (64, 64)}   # Cout 
 WGRAD_TILES.update({v + 4: t for v, t in list(WGRAD_TILES.items())})   # + 4: serial
 # 8..11: the v2 weight-gradient kernel (32x32x16 MFMAs, 128/256-wide tiles, two steps in flight)
 WGRAD_V2 = {8: (128, 128), 9: (256, 128), 10: (128, 256), 11: (256, 256),
-            12: (128, 128)}   # 12: serial single-buffer, four waves per SIMD
+            12: (128, 128),   # 12: serial single-buffer, four waves per SIMD
+            # 13 / 14: 12 with two / four wave groups per block splitting its pixel steps (the
+            # same waves per CU in 1/2 / 1/4 of the blocks: that many fewer fp32 split slabs)
+            13: (128, 128), 14: (128, 128)}
+WGRAD_GROUPS = {13: 2, 14: 4}
 WGRAD_TILES.update(WGRAD_V2)
 
 
@@ -667,7 +677,9 @@ def _wgrad_candidates(cin, cout, k):
     for v in wgrad_variants_for(cin, cout):
         bm, bn = WGRAD_TILES[v]
         tiles = (cout // bm) * (k[0] * k[1] * cin // bn)
-        for bpc in _WGRAD_BPC:
+        # wave-group forms: a block already holds GRP x 4 waves -- one or two blocks per CU
+        bpcs = (1, 2) if v in WGRAD_GROUPS else _WGRAD_BPC
+        for bpc in bpcs:
             blocks = int(bpc * _CUS)
             out.append((v, max(1, -(-blocks // tiles))))
     return sorted(set(out))
@@ -731,13 +743,13 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                 return us if fin else us + _FIN_PENALTY_US
 
             fns = {}
-            halo = lambda c: halo_variants_for(c, k, stride, pad, x.shape[3])  # noqa: E731
-            for v in (variants_for(cout) + v2_variants_for(cout) + halo(cout)
+            halo = lambda c, kc: halo_variants_for(c, k, stride, pad, x.shape[3], kc)  # noqa: E731
+            for v in (variants_for(cout) + v2_variants_for(cout) + halo(cout, cin)
                       + split_variants_for(m_out, cout, cin * k[0] * k[1])):
                 fns[("fwd", v)] = (lambda v=v: fwd_time(v))
             if stride == 1:
                 m_in = x.shape[0] * x.shape[2] * x.shape[3]
-                for v in (variants_for(cin) + v2_variants_for(cin) + halo(cin)
+                for v in (variants_for(cin) + v2_variants_for(cin) + halo(cin, cout)
                           + split_variants_for(m_in, cin, cout * k[0] * k[1])):
                     fns[("bwd", v)] = (lambda v=v: _time(
                         lambda: conv2d_bwd_data(dy, w, pad, v)))
@@ -749,7 +761,7 @@ def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
                     from .batchnorm import acc_rep
                     bsums = torch.zeros(acc_rep() * 2 * cin, dtype=torch.float64,
                                         device=x.device)
-                    for v in variants_for(cin) + v2_variants_for(cin) + halo(cin):
+                    for v in variants_for(cin) + v2_variants_for(cin) + halo(cin, cout):
                         # timed in the epilogue form the step will run: fp64 sums into the BN's
                         # backward set where _use_link_acc picks it, else per-tile partials
                         acc = bsums if _use_link_acc(m_in, v, cin) else None

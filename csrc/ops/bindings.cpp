@@ -81,6 +81,7 @@ hipError_t arena_conv_fwd_phases(const void*, void*, const void*, int, int, int,
                                  const int*, int, hipStream_t);
 long long arena_conv_fwd_ksplit_floats(long long, int, int, int);
 void arena_conv_set_stats_one_pass(int);
+void arena_conv_set_dbg(int);
 long long arena_conv_fwd_tiles(long long, int, int);
 int arena_conv_fwd_tile_rows(int);
 hipError_t arena_conv_wgrad_ex(const void*, const void*, float*, void*, float*, int, int, int, int,
@@ -883,7 +884,7 @@ ConvSplit conv_split(const Tensor& x, int64_t variant, int64_t M, int64_t Cout, 
   ConvSplit s;
   TORCH_CHECK(variant >= 0, "conv: bad variant ", variant);
   if (variant >= 4096) {   // v2 tile kernel (conv_kernels.hip conv2_body): 4096 + i
-    TORCH_CHECK(variant - 4096 < 15, "conv: unknown v2 variant ", variant);
+    TORCH_CHECK(variant - 4096 < 16, "conv: unknown v2 variant ", variant);
     s.base = (int)variant;
   } else {   // v1 tile i (0..15), its K steps split over ks blocks: i + 16 (ks - 1)
     TORCH_CHECK(variant < 256, "conv: unknown variant ", variant);
@@ -1610,13 +1611,14 @@ void conv_dgrad_phases(Tensor dy, std::vector<Tensor> wps, std::vector<std::vect
 // wgrad tile (Cout x R*S*C) of a variant: 0..3 (+4 serial) v1, 8..11 the v2 32x32x16 kernel
 static bool wgrad_tile(int64_t variant, int* tbm, int* tbn) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  static const int bm2[5] = {128, 256, 128, 256, 128}, bn2[5] = {128, 128, 256, 256, 128};
+  static const int bm2[7] = {128, 256, 128, 256, 128, 128, 128};
+  static const int bn2[7] = {128, 128, 256, 256, 128, 128, 128};
   if (variant >= 0 && variant <= 7) {
     *tbm = bm[variant & 3];
     *tbn = bn[variant & 3];
     return true;
   }
-  if (variant >= 8 && variant <= 12) {
+  if (variant >= 8 && variant <= 14) {
     *tbm = bm2[variant - 8];
     *tbn = bn2[variant - 8];
     return true;
@@ -1735,7 +1737,7 @@ Tensor conv_wgrad(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int
   TORCH_CHECK(dy.size(0) == N && dy.size(2) == Ho && dy.size(3) == Wo,
               "conv_wgrad: dy shape does not match the convolution geometry");
   int tbm = 0, tbn = 0;
-  TORCH_CHECK(wgrad_tile(variant, &tbm, &tbn), "conv_wgrad: variant must be 0..12");
+  TORCH_CHECK(wgrad_tile(variant, &tbm, &tbn), "conv_wgrad: variant must be 0..14");
   TORCH_CHECK(C % tbn == 0 && Cout % tbm == 0, "conv_wgrad: variant ", variant, " needs C % ",
               tbn, " == 0 and Cout % ", tbm, " == 0");
   TORCH_CHECK(N * Ho * Wo < (int64_t(1) << 31), "conv_wgrad: too many output pixels");
@@ -1975,6 +1977,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_pool_fwd", &bn_pool_fwd);
   m.attr("acc_rep") = (int)ARENA_ACC_REP;   // replicas per BatchNorm accumulator set
   m.def("conv_set_stats_one_pass", [](bool on) { arena_conv_set_stats_one_pass(on ? 1 : 0); });
+  m.def("conv_set_dbg", [](int64_t bits) { arena_conv_set_dbg((int)bits); });
   m.def("bn_pool_bwd", &bn_pool_bwd);
   m.def("bn_set_reduce_geometry", [](int64_t max_blocks, int64_t min_rounds) {
     arena_bn_set_reduce_geometry(max_blocks, min_rounds);

@@ -103,6 +103,10 @@ struct ConvArgs {
   unsigned* kcnt;
   int xbytes, wbytes;  // buffer-descriptor ranges of x and w (both < 2^31 bytes, host-checked)
   int st1p;            // EPI 1 statistics in one pass (sum, sum of squares) instead of two
+  // ablation switches of the halo K loop for timing studies only (tools/halo_ablation.py; the
+  // output is garbage with any bit set): 1 no weight loads after the first chunk's prologue,
+  // 2 no window loads after the first chunk, 4 no barriers in the tap loop, 8 no MFMAs
+  int dbg;
   // Several phase convolutions of a strided backward-data pass in ONE launch (v2 tiles, plain
   // mapped epilogue): phase p owns blocks [ph[p].blk0, ph[p + 1].blk0) (starts on multiples of 8,
   // so the XCD-aware tile order holds within each phase) and overrides the per-phase fields.
@@ -1041,7 +1045,16 @@ constexpr int kLdsMax = 160 * 1024;
 // taps read it at row offsets r*W + s, and taps that fall outside the image (row/column padding or
 // a neighbouring image) are zeroed on the fragment. A is staged once instead of nine times.
 constexpr int kHaloMaxW = 63;
-constexpr int kHaloSmallW = 31;   // HALO == 2: a window sized for <= 31-wide images
+constexpr int kHaloSmallW = 31;   // HALO & 3 == 2: a window sized for <= 31-wide images
+// HALO & 4: two window buffers -- chunk cb + 1's window is staged while chunk cb's taps run, and
+// the weight ring runs on across chunk boundaries (no pipeline drain per 64-channel chunk)
+constexpr int kHaloWin2 = 4;
+// HALO & 8: two groups of four waves (512 threads, two waves per SIMD) split the 64-channel chunks
+// by parity, each with its own window and weight ring and the whole BM x BN tile in its
+// accumulators; at the end group 1 hands its sums to group 0 through LDS and exits, and group 0
+// runs the epilogue. With one wave per SIMD the MFMA pipe idles whenever the wave waits on an LDS
+// read or a barrier; the partner wave fills those gaps (needs an even chunk count).
+constexpr int kHaloSplit2 = 8;
 
 template <int BM, int BN, int NWM, int NWN, int NBUF, int EPI, bool BAND = false,
           int HALO = 0>
@@ -1052,12 +1065,16 @@ struct Conv2Geo {
   static constexpr int MI = WM / 32, NI = WN / 32;
   static constexpr int AI = BM * 8 / NT, BI = BN * 8 / NT;
   static constexpr int kBufBytes = (BM + BN) * kRowBytes;
-  // window rows (max W: kHaloMaxW, or kHaloSmallW for HALO == 2)
-  static constexpr int kHaloRows = BM + 2 * (HALO == 2 ? kHaloSmallW : kHaloMaxW) + 2;
+  // window rows (max W: kHaloMaxW, or kHaloSmallW for HALO & 3 == 2)
+  static constexpr int kHaloRows = BM + 2 * ((HALO & 3) == 2 ? kHaloSmallW : kHaloMaxW) + 2;
   static constexpr int AIH = (kHaloRows * 8 + NT - 1) / NT;  // window loads per thread
   static constexpr int kWinBytes = AIH * NT / 8 * kRowBytes;
-  // HALO: the window + a ring of NBUF per-tap weight buffers (NBUF - 1 taps in flight)
-  static constexpr int kStage = HALO ? kWinBytes + NBUF * BN * kRowBytes : NBUF * kBufBytes;
+  static constexpr int kWins = (HALO & kHaloWin2) ? 2 : 1;
+  static constexpr int kGroups = (HALO & kHaloSplit2) ? 2 : 1;
+  // HALO: per wave group the window(s) + a ring of NBUF per-tap weight buffers (NBUF - 1 taps in
+  // flight)
+  static constexpr int kGroupStage = kWins * kWinBytes + NBUF * BN * kRowBytes;
+  static constexpr int kStage = HALO ? kGroups * kGroupStage : NBUF * kBufBytes;
   static constexpr int SL = BN / 4;       // float4 slots per tile row
   static constexpr int RG = NT / SL;      // row groups of the statistics passes
   static constexpr int kRed = 0;   // EPI 1's partials reuse the band's tile (2 RG rows)
@@ -1072,6 +1089,22 @@ struct Conv2Geo {
   static_assert(EPI != 1 || 2 * RG <= EH, "EPI 1 partials fit the band's tile");
   static_assert(kLds <= kLdsMax, "LDS budget");
 };
+
+// s_waitcnt vmcnt(k * BI) lgkmcnt(0) for a k that is a constant after unrolling (the "n" operand
+// needs a constant expression, so the cases are spelled out; the switch folds to one of them)
+template <int BI>
+__device__ __forceinline__ void vm_wait_groups(int k) {
+  switch (k) {
+    case 0: asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory"); break;
+    case 1: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(1 * BI) : "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(2 * BI) : "memory"); break;
+    case 3: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(3 * BI) : "memory"); break;
+    case 4: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(4 * BI) : "memory"); break;
+    case 5: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(5 * BI) : "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(6 * BI) : "memory"); break;
+    default: asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(7 * BI) : "memory"); break;
+  }
+}
 
 // The v2 epilogue: the accumulators through an fp32 LDS tile at `lds` (EH x BN floats, bands of
 // EH rows), coalesced bf16 stores (+ addend, mapped placement, fill_sib), and the EPI 1 / EPI 2
@@ -1291,7 +1324,11 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
   constexpr int SL = G::SL, RG = G::RG, EH = G::EH;
   __shared__ __attribute__((aligned(16))) uint8_t lds[G::kLds];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // kHaloSplit2: wave group grp = threadIdx.x / 256, each group laid out as a 4-wave block
+  constexpr int kGroups = HALO ? G::kGroups : 1;
+  const int grp = kGroups == 2 ? (int)(threadIdx.x >> 8) : 0;
+  const int tid = kGroups == 2 ? (int)(threadIdx.x & 255) : (int)threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
   // XCD-aware order (as v1): each XCD gets a contiguous range of tiles, column tiles of one row
   // tile consecutive (their A rows stay in that XCD's L2)
   const int nblk = a.m_tiles * a.n_tiles;
@@ -1359,23 +1396,31 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
       }
       tmask[i] = mk;
     }
-    auto stage_win = [&](int cb) {
+    constexpr int kWins = G::kWins;
+    uint8_t* const gbase = lds + grp * G::kGroupStage;   // this wave group's buffers
+    uint8_t* const ring = gbase + kWins * kWin;
+    auto stage_win = [&](int cb, int wb) {
 #pragma unroll
       for (int i = 0; i < AIH; ++i)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(xrsrc, (lds_ptr_t)(lds + (wave * AIH + i) * 64 * 16),
-                                                 16, w_off[i], cb * kRowBytes, 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            xrsrc, (lds_ptr_t)(gbase + wb * kWin + (wave * AIH + i) * 64 * 16), 16, w_off[i],
+            cb * kRowBytes, 0, 0);
     };
-    auto stage_b = [&](int tap, int cb, int buf) {
-      uint8_t* bb = lds + kWin + buf * BN * kRowBytes;
+    // the group's chunk sequence: cb = kGroups * j + grp
+    // the weights of the group's global tap g = 9 j + tap into ring buffer g % NBUF
+    auto stage_w = [&](int g) {
+      const int jj = g / 9, tap = g - 9 * jj;
+      const int cb = kGroups * jj + grp;
+      uint8_t* bb = ring + (g % NBUF) * BN * kRowBytes;
 #pragma unroll
       for (int i = 0; i < BI; ++i)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(wrsrc, (lds_ptr_t)(bb + (wave * BI + i) * 64 * 16),
                                                  16, b_voff[i], (tap * a.C + cb * kBK) * 2, 0, 0);
     };
-    auto compute_tap = [&](int tap, int buf) {
+    auto compute_tap = [&](int tap, const uint8_t* win, int buf) {
       const int r = tap / 3, s2 = tap - 3 * r;
       const int shift = r * Wd + s2;
-      const uint8_t* bbuf = lds + kWin + buf * BN * kRowBytes;
+      const uint8_t* bbuf = ring + buf * BN * kRowBytes;
       bool ok[MI];
 #pragma unroll
       for (int i = 0; i < MI; ++i) ok[i] = (tmask[i] >> tap) & 1u;
@@ -1386,7 +1431,7 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int j = wm * WM + i * 32 + fr + shift;
-          const bf16x8 v = *reinterpret_cast<const bf16x8*>(lds + j * kRowBytes + ((c ^ swz(j)) << 4));
+          const bf16x8 v = *reinterpret_cast<const bf16x8*>(win + j * kRowBytes + ((c ^ swz(j)) << 4));
           af[i] = ok[i] ? v : bf16x8{0, 0, 0, 0, 0, 0, 0, 0};
         }
 #pragma unroll
@@ -1401,31 +1446,92 @@ __device__ __forceinline__ void conv2_body(const ConvArgs& a, int bid) {
             acc[i][jn] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(bfr[jn], af[i], acc[i][jn], 0, 0, 0);
       }
     };
-    // ---- K loop: per channel chunk, the window + the first D = NBUF - 1 taps' weights, then
-    // one tap's weights issued per tap, D ahead (a ring of NBUF buffers; only loads in flight,
-    // so the counted vmcnt waits are exact)
+    // ---- K loop over the 9 CB global taps g = 9 cb + tap: the weights run D = NBUF - 1 taps
+    // ahead in a ring of NBUF buffers, across chunk boundaries. Window: one buffer (restaged at
+    // each chunk start, after the barrier that ended the previous chunk's last tap), or two
+    // (kHaloWin2: chunk cb + 1's window issued at chunk cb's first tap, into the buffer chunk
+    // cb - 1 used). Only loads are in flight, in issue order, so every counted vmcnt is exact:
+    // before tap g + 1 the loads younger than its weights W(g + 1) are W(g + 2 .. g + D) and, for
+    // the first D taps of a chunk with two windows, the next chunk's window. ----
     constexpr int D = NBUF - 1;
     static_assert(D >= 1 && D < 9, "weight ring depth");
-    const int CB = a.C / kBK;
+    const int CB = a.C / kBK / kGroups;   // this group's chunks (host-checked: C / 64 divisible)
+    const int T = 9 * CB;
+    const int dbg = a.dbg;
+    stage_win(grp, 0);
+#pragma unroll
+    for (int d = 0; d < D; ++d) stage_w(d);   // T >= 9 > D
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * BI) : "memory");   // window 0 + tap 0
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
     for (int cb = 0; cb < CB; ++cb) {
-      stage_win(cb);   // the previous chunk's last tap ended on a barrier: the window is free
-#pragma unroll
-      for (int t = 0; t < D; ++t) stage_b(t, cb, t);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * BI) : "memory");   // window + tap 0
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int t = 0; t < 9; ++t) {
-        // buffer (t + D) % NBUF was last read by tap t - 1, before the barrier that ended it
-        if (t + D < 9) stage_b(t + D, cb, (t + D) % NBUF);
-        compute_tap(t, t % NBUF);
-        if (t + D < 9)   // tap t + 1 landed, D - 1 taps may still be in flight
-          asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((D - 1) * BI) : "memory");
-        else
-          asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const bool last = cb == CB - 1;
+      const int wb = kWins == 2 ? (cb & 1) : 0;
+      if (kWins == 1 && cb > 0) {
+        // the previous chunk's last tap ended on a barrier: the window is free. Its loads are the
+        // youngest, so waiting for them drains the (older, mostly landed) weights too.
+        if (!(dbg & 2)) stage_win(kGroups * cb + grp, 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();
         asm volatile("" ::: "memory");
       }
+      const uint8_t* win = gbase + wb * kWin;
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        const int g = 9 * cb + t;
+        // buffer (g + D) % NBUF was last read by tap g - 1, before the barrier that ended it
+        if (g + D < T && !(dbg & 1)) stage_w(g + D);
+        if (kWins == 2 && t == 0 && !last && !(dbg & 2))   // (its buffer: chunk cb - 1's, done)
+          stage_win(kGroups * (cb + 1) + grp, wb ^ 1);
+        if (!(dbg & 8)) compute_tap(t, win, g % NBUF);
+        // (t is a constant of the unrolled loop: every branch below folds to one s_waitcnt)
+        if (!last) {
+          // W(g + 1) landed (with two windows and t == 8, the older next-chunk window too)
+          if (kWins == 2 && t + 1 <= D)
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((D - 1) * BI + AIH) : "memory");
+          else
+            asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((D - 1) * BI) : "memory");
+        } else {
+          // last chunk: W(g + 2 .. min(g + D, T - 1)) may stay in flight
+          vm_wait_groups<BI>(t < 8 ? ((D - 1) < (7 - t) ? (D - 1) : (7 - t)) : 0);
+        }
+        if (!(dbg & 4)) __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+    }
+    if constexpr (kGroups == 2) {
+      // group 1 hands its sums to group 0 through LDS (the stage buffers are free: the loop ended
+      // on a barrier after every wave's last read), 16-byte lane-contiguous slots, the same
+      // fragment layout in both groups; fixed order (group 0 + group 1): bit-reproducible
+      float4* xs = reinterpret_cast<float4*>(lds) + (size_t)wave * (MI * NI * 4) * 64 + lane;
+      if (grp == 1) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+              xs[((i * NI + j) * 4 + q) * 64] =
+                  make_float4(acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2],
+                              acc[i][j][4 * q + 3]);
+      }
+      lds_barrier();
+      // group 1 is done; a terminated wave no longer counts toward the workgroup's barriers, so
+      // the epilogue's barriers synchronise group 0 alone
+      if (grp == 1) return;
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NI; ++j)
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float4 v = xs[((i * NI + j) * 4 + q) * 64];
+            acc[i][j][4 * q] += v.x;
+            acc[i][j][4 * q + 1] += v.y;
+            acc[i][j][4 * q + 2] += v.z;
+            acc[i][j][4 * q + 3] += v.w;
+          }
+      lds_barrier();   // every read of the hand-off is done before the epilogue reuses the LDS
     }
   } else {
     int a_lane[AI];
@@ -1621,20 +1727,23 @@ void conv2_kernel_occ4(ConvArgs a) {
 // the 3x3 halo form (see Conv2Geo::HALO): 4 waves, a ring of NBR per-tap weight buffers --
 // 128x128: three (80 KB, two blocks per CU); 128x64: two (48 KB, three blocks per CU; with the
 // small window of <= 31-wide images 40 KB, four blocks per CU)
-template <int BM, int BN, int EPI, int HW>
-__global__ __launch_bounds__(256) void conv2_kernel_halo(ConvArgs a) {
+template <int BM, int BN, int EPI, int HW, int NB>
+__global__ __launch_bounds__((HW & kHaloSplit2) ? 512 : 256) void conv2_kernel_halo(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv2_body<BM, BN, 2, 2, BN >= 128 ? 3 : 2, EPI, false, HW>(a, blockIdx.x);
+  conv2_body<BM, BN, 2, 2, NB, EPI, false, HW>(a, blockIdx.x);
 #endif
 }
 
-template <int BM, int BN, int HW = 1>
+// HW: window size class (1: <= 63 wide, 2: <= 31) | kHaloWin2; NB: weight ring buffers
+template <int BM, int BN, int HW, int NB>
 hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   if (a.c16 || a.Cout % BN || a.R != 3 || a.S != 3 ||
       a.stride != 1 || a.pad != 1 || a.pad_w != 1 || a.Ho != a.H || a.Wo != a.W ||
-      a.W > (HW == 2 ? kHaloSmallW : kHaloMaxW) || a.mapped)
+      a.W > ((HW & 3) == 2 ? kHaloSmallW : kHaloMaxW) || a.mapped ||
+      ((HW & kHaloSplit2) && (a.C / kBK) % 2))
     return hipErrorInvalidValue;
+  const int nthr = (HW & kHaloSplit2) ? 512 : 256;
   if (a.ksplit != 1) return hipErrorInvalidValue;
   if (a.bnx == nullptr && (a.part != nullptr || a.bn_acc != nullptr) && a.add != nullptr)
     return hipErrorInvalidValue;
@@ -1642,11 +1751,11 @@ hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
   if (a.bnx != nullptr)
-    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW>), dim3(nwg), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW, NB>), dim3(nwg), dim3(nthr), 0, st, a);
   else if (a.part != nullptr || a.bn_acc != nullptr)
-    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1, HW>), dim3(nwg), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1, HW, NB>), dim3(nwg), dim3(nthr), 0, st, a);
   else
-    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 0, HW>), dim3(nwg), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 0, HW, NB>), dim3(nwg), dim3(nthr), 0, st, a);
   return hipGetLastError();
 }
 
@@ -1694,11 +1803,12 @@ hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
 
 // v2 variant table (code 1024 + index): BM x BN tile, waves NWM x NWN, stage buffers
 constexpr int kV2Base = 4096;   // above every v1 code (split + 16 k, persistent + 256 p <= 1039)
-constexpr int kV2Count = 15;
+constexpr int kV2Count = 16;
 constexpr int kV2Tiles[kV2Count][2] = {{256, 128}, {256, 256}, {128, 128}, {256, 64}, {128, 256},
                                        {128, 64}, {64, 64}, {64, 128},
                                        {128, 128}, {128, 64}, {64, 128}, {64, 64},
-                                       {128, 128}, {128, 64}, {128, 64}};
+                                       {128, 128}, {128, 64}, {128, 64},
+                                       {128, 128}};
 
 hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
   switch (idx) {
@@ -1717,10 +1827,14 @@ hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
     case 9: return launch2_t<128, 64, 2, 2, 1, true>(a, st);
     case 10: return launch2_t<64, 128, 2, 2, 1, true>(a, st);
     case 11: return launch2_t<64, 64, 2, 2, 1, true>(a, st);
-    // 3x3 / stride 1 / pad 1 halo forms (conv2_kernel_halo)
-    case 12: return launch2_halo<128, 128>(a, st);
-    case 13: return launch2_halo<128, 64>(a, st);
-    case 14: return launch2_halo<128, 64, 2>(a, st);   // <= 31-wide images: 4 blocks per CU
+    // 3x3 / stride 1 / pad 1 halo forms (conv2_kernel_halo); LDS per block in comments
+    case 12: return launch2_halo<128, 128, 1, 3>(a, st);   // 80 KB
+    case 13: return launch2_halo<128, 64, 1, 2>(a, st);    // 48 KB
+    case 14: return launch2_halo<128, 64, 2, 2>(a, st);    // <= 31 wide: 40 KB, 4 blocks per CU
+    // two wave groups splitting the channel chunks (512 threads, two waves per SIMD): 144 KB.
+    // Measured and not kept (profiles/r6_halo_variants.jsonl): 128x128 with two groups and two
+    // ring buffers, 128x64 with two groups, four- and six-deep rings, a second window buffer.
+    case 15: return launch2_halo<128, 128, 2 | kHaloSplit2, 3>(a, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -1742,6 +1856,9 @@ int g_conv_st1p = 0;   // see ConvArgs::st1p (runtime switch: arena_conv_set_sta
 extern "C" {
 
 void arena_conv_set_stats_one_pass(int on) { g_conv_st1p = on ? 1 : 0; }
+
+int g_conv_dbg = 0;   // ConvArgs::dbg (timing ablations only)
+void arena_conv_set_dbg(int bits) { g_conv_dbg = bits; }
 
 // Returns hipErrorInvalidValue for shapes the kernel does not cover (the caller falls back to
 // MIOpen): C % 64 != 0, Cout % 64 != 0, or an unknown tile variant.
@@ -1829,6 +1946,7 @@ hipError_t arena_conv_fwd_ex(const void* x, const void* w, void* y, float* part,
   a.kws = (float4*)kws;
   a.kcnt = kcnt;
   a.st1p = g_conv_st1p;
+  a.dbg = g_conv_dbg;
   if (v2) {
     if (c16) return hipErrorInvalidValue;
     return launch2(a, variant - kV2Base, st);
@@ -1892,6 +2010,7 @@ hipError_t arena_conv_fwd_phases(const void* x, void* y, const void* add, int N,
   a.M = N * Ho[0] * Wo[0];
   a.Ktot = R[0] * S[0] * C;
   a.st1p = g_conv_st1p;
+  a.dbg = g_conv_dbg;
   return launch2(a, idx, st);
 }
 
@@ -2588,7 +2707,14 @@ FastDiv make_fastdiv(uint32_t d) {
 // ------------------------------------------------------------------------------------------------
 __device__ __forceinline__ int wswz2(int row) { return 4 * (row & 3); }
 
-template <int BM, int BN, int NWM, int NWN, int NBUF>
+// GRP > 1: GRP groups of NWM x NWN waves in one block split the block's pixel steps (group g takes
+// steps t = g (mod GRP)) with their own stage buffers and a whole tile of accumulators each; at
+// the end groups 1 .. GRP-1 hand their sums to group 0 through LDS in group order (fixed order:
+// bit-reproducible) and exit, and group 0 writes the slab. A block then covers GRP times the
+// pixels of a one-group block with the same waves per CU, so the launch needs 1 / GRP of the
+// split slabs (fp32 [splits][Cout][Ktot], written here and read back by the reduce pass: 1.8 GB
+// per ResNet-50 step at one group).
+template <int BM, int BN, int NWM, int NWN, int NBUF, int GRP = 1>
 __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
   constexpr int NT = 64 * NWM * NWN;
   constexpr int RA = BM * 2, RBB = BN * 2;        // row bytes of the dY and X images
@@ -2600,9 +2726,15 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
   static_assert(CA >= 16 && CB >= 16, "the 64-byte granule permutation needs >= 256-byte rows");
   static_assert(AI >= 1 && BI >= 1 && MI >= 1 && NI >= 1, "tile too small for the wave grid");
   static_assert(AI * NT == kPix * CA && BI * NT == kPix * CB, "staging slots must cover the tile");
-  __shared__ __attribute__((aligned(16))) uint8_t lds[NBUF * kBuf];
+  constexpr int kHand = GRP > 1 ? NT * MI * NI * 16 * 4 : 0;   // one group's accumulators
+  constexpr int kLdsW = GRP * NBUF * kBuf > kHand ? GRP * NBUF * kBuf : kHand;
+  static_assert(kLdsW <= kLdsMax, "LDS budget");
+  __shared__ __attribute__((aligned(16))) uint8_t lds_all[kLdsW];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int grp = GRP > 1 ? (int)(threadIdx.x / NT) : 0;
+  const int tid = GRP > 1 ? (int)(threadIdx.x % NT) : (int)threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  uint8_t* const lds = lds_all + grp * NBUF * kBuf;   // this group's stage buffers
   const int tiles = a.m_tiles * a.n_tiles;
   const int nwg = tiles * a.splits;
   const int bid = blockIdx.x;
@@ -2613,8 +2745,10 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
   const int co0 = mt * BM, kk0 = nt * BN;
   const int tap = kk0 / a.C, ci0 = kk0 - tap * a.C;
   const int rr = tap / a.S, ss = tap - rr * a.S;
-  const int step0 = split * a.sps;
-  const int nsteps = min(a.sps, (a.M + kPix - 1) / kPix - step0);
+  // this group's steps: step0 + grp, step0 + grp + GRP, ... (a.sps steps per block)
+  const int step0 = split * a.sps + grp;
+  const int nblk_steps = min(a.sps, (a.M + kPix - 1) / kPix - split * a.sps);
+  const int nsteps = nblk_steps > grp ? (nblk_steps - grp + GRP - 1) / GRP : 0;
 
   constexpr int RPI_A = 64 / CA, RPI_B = 64 / CB;   // rows per wave-instruction (1 KB)
   const int a_row_l = lane / CA, a_pos = lane % CA;
@@ -2638,7 +2772,7 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
 
   auto stage = [&](int step, int buf) {
     uint8_t* base = lds + buf * kBuf;
-    const int p0 = (step0 + step) * kPix;
+    const int p0 = (step0 + step * GRP) * kPix;
     const bool full = p0 + kPix <= a.M;
 #pragma unroll
     for (int i = 0; i < AI; ++i) {
@@ -2725,21 +2859,25 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
     }
   };
 
-  if (NBUF == 1 && nsteps > 0) {
+  // every group runs the same trip count (barriers are workgroup-wide); a group past its last
+  // step only takes part in the barriers
+  const int trips = GRP > 1 ? (nblk_steps + GRP - 1) / GRP : nsteps;
+  if (NBUF == 1 && trips > 0) {
     // serial form (high occupancy): stage, wait, compute, restage
-    stage(0, 0);
+    if (nsteps > 0) stage(0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int t = 0; t < nsteps; ++t) {
-      compute(0);
-      if (t + 1 < nsteps) {
+    for (int t = 0; t < trips; ++t) {
+      if (t < nsteps) compute(0);
+      if (t + 1 < trips) {
         __syncthreads();
-        stage(t + 1, 0);
+        if (t + 1 < nsteps) stage(t + 1, 0);
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   } else if (nsteps > 0) {
+    static_assert(GRP == 1 || NBUF == 1, "wave groups: serial form only");
     constexpr int S = NBUF > 1 ? NBUF - 1 : 1;
     constexpr int kLps = AI + BI;
 #pragma unroll
@@ -2765,6 +2903,45 @@ __device__ __forceinline__ void conv_wgrad2_body(const WgradArgs& a) {
     }
   }
 
+  if constexpr (GRP > 1) {
+    // groups 1 .. GRP-1 hand their sums to group 0, one group per round, in group order (the
+    // stage buffers are free: the loop ended on a barrier after every wave's last read)
+    float4* xs = reinterpret_cast<float4*>(lds_all) + (size_t)wave * (MI * NI * 4) * 64 + lane;
+    for (int q = 1; q < GRP; ++q) {
+      if (grp == q) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+              xs[((i * NI + j) * 4 + k) * 64] =
+                  make_float4(acc[i][j][4 * k], acc[i][j][4 * k + 1], acc[i][j][4 * k + 2],
+                              acc[i][j][4 * k + 3]);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (grp == 0) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NI; ++j)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+              const float4 v = xs[((i * NI + j) * 4 + k) * 64];
+              acc[i][j][4 * k] += v.x;
+              acc[i][j][4 * k + 1] += v.y;
+              acc[i][j][4 * k + 2] += v.z;
+              acc[i][j][4 * k + 3] += v.w;
+            }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();   // group 0's reads done before the next group writes
+      asm volatile("" ::: "memory");
+    }
+    if (grp != 0) return;
+  }
   // D[row = co][col = k column]: lane holds column (lane & 31), rows (r & 3) + 8 (r >> 2) +
   // 4 (lane >> 5): 32 consecutive floats per half-wave store
   float* slab = a.ws + (size_t)split * a.Cout * a.Ktot;
@@ -2798,10 +2975,21 @@ void conv_wgrad2_kernel_occ4(WgradArgs a) {
 #endif
 }
 
-// v2 wgrad variant table (variant 8 + i): BM x BN (Cout x R*S*C), waves, stage buffers
-constexpr int kWg2Tiles[5][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256}, {128, 128}};
+// serial single-buffer form with GRP wave groups (2: 512 threads, 4: 1024) splitting the steps
+template <int BM, int BN, int GRP>
+__global__ __launch_bounds__(256 * GRP) void conv_wgrad2_kernel_grp(WgradArgs a) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  conv_wgrad2_body<BM, BN, 2, 2, 1, GRP>(a);
+#endif
+}
 
-template <int BM, int BN, int NWM, int NWN, int NBUF, bool OCC4 = false>
+// v2 wgrad variant table (variant 8 + i): BM x BN (Cout x R*S*C), waves, stage buffers;
+// 13 / 14: the serial 128x128 form with two / four wave groups per block
+constexpr int kWg2Count = 7;
+constexpr int kWg2Tiles[kWg2Count][2] = {{128, 128}, {256, 128}, {128, 256}, {256, 256},
+                                         {128, 128}, {128, 128}, {128, 128}};
+
+template <int BM, int BN, int NWM, int NWN, int NBUF, bool OCC4 = false, int GRP = 1>
 hipError_t launch_wgrad2(WgradArgs a, int splits_hint, hipStream_t st) {
   a.m_tiles = a.Cout / BM;
   a.n_tiles = a.Ktot / BN;
@@ -2811,7 +2999,10 @@ hipError_t launch_wgrad2(WgradArgs a, int splits_hint, hipStream_t st) {
   splits = std::min(splits, total);
   a.sps = (total + splits - 1) / splits;
   a.splits = (total + a.sps - 1) / a.sps;
-  if constexpr (OCC4) {
+  if constexpr (GRP > 1) {
+    hipLaunchKernelGGL((conv_wgrad2_kernel_grp<BM, BN, GRP>), dim3(tiles * a.splits),
+                       dim3(256 * GRP), 0, st, a);
+  } else if constexpr (OCC4) {
     hipLaunchKernelGGL((conv_wgrad2_kernel_occ4<BM, BN>), dim3(tiles * a.splits), dim3(256), 0,
                        st, a);
   } else {
@@ -2850,7 +3041,7 @@ extern "C" {
 int arena_conv_wgrad_splits(int N, int Ho, int Wo, int Cout, int Ktot, int variant,
                             int splits_hint) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (variant < 0 || variant > 12) return -1;
+  if (variant < 0 || variant >= 8 + kWg2Count) return -1;
   const int tbm = variant >= 8 ? kWg2Tiles[variant - 8][0] : bm[variant & 3];
   const int tbn = variant >= 8 ? kWg2Tiles[variant - 8][1] : bn[variant & 3];
   const int tiles = (Cout / tbm) * (Ktot / tbn);
@@ -2871,7 +3062,7 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
                                int stride, int pad_h, int pad_w, int Ho, int Wo, int c16,
                                int variant, int splits_hint, float scale, hipStream_t st) {
   static const int bm[4] = {128, 128, 64, 64}, bn[4] = {128, 64, 128, 64};
-  if (variant < 0 || variant > 12) return hipErrorInvalidValue;
+  if (variant < 0 || variant >= 8 + kWg2Count) return hipErrorInvalidValue;
   const bool v2 = variant >= 8;
   const int tv = variant & 3;
   const bool serial = !v2 && variant >= 4;
@@ -2913,6 +3104,8 @@ hipError_t arena_conv_wgrad_ex(const void* x, const void* dy, float* ws, void* d
       case 1: e = launch_wgrad2<256, 128, 4, 2, 2>(a, splits_hint, st); break;
       case 2: e = launch_wgrad2<128, 256, 2, 4, 2>(a, splits_hint, st); break;
       case 3: e = launch_wgrad2<256, 256, 2, 4, 2>(a, splits_hint, st); break;
+      case 5: e = launch_wgrad2<128, 128, 2, 2, 1, false, 2>(a, splits_hint, st); break;
+      case 6: e = launch_wgrad2<128, 128, 2, 2, 1, false, 4>(a, splits_hint, st); break;
       default: e = launch_wgrad2<128, 128, 2, 2, 1, true>(a, splits_hint, st); break;
     }
   } else switch (tv) {

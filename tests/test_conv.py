@@ -115,6 +115,7 @@ V2_SHAPES = [  # n, cin, h, w, cout, k, stride
     (1, 64, 5, 63, 64, 3, 1),       # the widest halo image
     (2, 128, 9, 31, 128, 3, 1),     # the small window's widest image (V2+14 at its limit)
     (1, 128, 5, 63, 128, 3, 1),     # the big window at W = 63 with the 128-wide tile (V2+12)
+    (2, 320, 7, 9, 128, 3, 1),      # five channel chunks: the ring and the double window wrap
 ]
 
 
@@ -131,7 +132,7 @@ def test_conv_v2_matches_fp32(shape):
     pad = k // 2
     x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=5)
     ref = F.conv2d(x.float(), wt.float(), stride=st, padding=pad)
-    halo = conv.halo_variants_for(cout, (k, k), st, pad, w)
+    halo = conv.halo_variants_for(cout, (k, k), st, pad, w, cin)
     assert bool(halo) == (k == 3 and st == 1)
     vs = conv.v2_variants_for(cout) + halo
     assert vs
@@ -173,7 +174,7 @@ def test_conv_v2_matches_fp32(shape):
         memory_format=torch.channels_last)
     bits = torch.randint(0, 256, (addend.numel() // 8,), device="cuda", dtype=torch.uint8)
     dense = conv.MaskedGrad(addend, bits).materialize()
-    for v in conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, pad, w):
+    for v in conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, pad, w, cout):
         dx = conv.conv2d_bwd_data(dy, wt, pad, v)
         assert _rel(dx, dx_ref) < 1e-2, (v, _rel(dx, dx_ref))
         dxa = conv.conv2d_bwd_data(dy, wt, pad, v, addend=addend)
@@ -188,7 +189,7 @@ def test_conv_v2_matches_fp32(shape):
     m = x.shape[0] * x.shape[2] * x.shape[3]
     mean = torch.randn(cin, device="cuda") * 0.3
     xc = bnx.permute(0, 2, 3, 1).reshape(m, cin).float() - mean
-    for v in conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, pad, w):
+    for v in conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, pad, w, cout):
         dx0 = conv.conv2d_bwd_data(dy, wt, pad, v)
         dx, (part, rpb) = conv.conv2d_bwd_data(dy, wt, pad, v, bn=(bnx, bits, mean))
         assert torch.equal(dx, dx0), v
@@ -234,7 +235,11 @@ def test_v2_variants_are_forward_and_dgrad_only():
     assert set(conv.v2_variants_for(64)) == {conv.V2 + v for v in (3, 5, 6, 9, 11)}
     assert set(conv.v2_variants_for(256)) == set(conv.V2_TILES) - set(conv.V2_HALO)
     assert set(conv.halo_variants_for(256, (3, 3), 1, 1, 14)) == set(conv.V2_HALO)
-    assert conv.halo_variants_for(64, (3, 3), 1, 1, 56) == [conv.V2 + 13]   # no small window
+    # no small window at 56 wide
+    assert conv.halo_variants_for(64, (3, 3), 1, 1, 56) == [conv.V2 + 13]
+    # the two-group forms need an even number of 64-channel chunks
+    assert not set(conv.halo_variants_for(256, (3, 3), 1, 1, 14, 192)) & conv.HALO_SPLIT2
+    assert conv.HALO_SPLIT2 <= set(conv.halo_variants_for(256, (3, 3), 1, 1, 14, 256))
     assert conv.V2 + 14 in conv.halo_variants_for(64, (3, 3), 1, 1, 31)
     assert conv.V2 + 14 not in conv.halo_variants_for(64, (3, 3), 1, 1, 32)
     assert not conv.halo_variants_for(256, (3, 3), 2, 1, 14)
@@ -576,8 +581,8 @@ def test_dgrad_epilogue_bn_backward_partials():
     bits = bits.view(m, cin).float()
     addend = torch.randn(n, cin, h, w, device="cuda").to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)
-    vs2 = conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, 1, w)
-    assert vs2 and set(conv.V2_HALO) <= set(vs2)
+    vs2 = conv.v2_variants_for(cin) + conv.halo_variants_for(cin, (k, k), 1, 1, w, cout)
+    assert vs2 and set(conv.V2_HALO) - conv.HALO_SPLIT2 <= set(vs2)
     xc = bnx.permute(0, 2, 3, 1).reshape(m, cin).float() - mean
     for v in conv.variants_for(cin) + vs2:   # v1 tiles and the v2 coalesced-epilogue form
         dx0 = conv.conv2d_bwd_data(dy, wt, 1, v)

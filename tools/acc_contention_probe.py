@@ -44,8 +44,8 @@ def main():
             memory_format=torch.channels_last)
         m = n * h * w_
         rec = {"layer": f"{ci}->{co} k{k} @{h}", "count": cnt}
-        for direction, c in (("fwd", co), ("bwd", ci)):
-            cands = conv.v2_variants_for(c) + conv.halo_variants_for(c, (k, k), 1, pad, w_)
+        for direction, c, kc in (("fwd", co, ci), ("bwd", ci, co)):
+            cands = conv.v2_variants_for(c) + conv.halo_variants_for(c, (k, k), 1, pad, w_, kc)
             best = {}
             for v in cands:
                 try:

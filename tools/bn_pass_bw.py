@@ -4,7 +4,8 @@
 Per ResNet-50 (batch 128, bf16, NHWC) BN shape: the apply pass with its statistics already summed
 (the conv-epilogue acc form: no reduction, no finalize) and the backward dx pass fed ready sums
 (the linked dgrad's), timed in hipGraphs, bytes counted as the kernels move them. A torch copy of
-the largest tensor is the reference rate.
+the largest tensor is the reference rate; ``x_floor`` is each pass's time over its bytes at the
+4.75 TB/s floor rate (below 1: the MALL serves part of the bytes).
 
     python tools/bn_pass_bw.py --configs slice:4096,flat:4096 > gpurun_out/bn_pass_bw.jsonl
 
@@ -24,6 +25,9 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from arena_amd.ops import _ext  # noqa: E402
 from arena_amd.ops.batchnorm import acc_rep  # noqa: E402
 from arena_amd.ops.conv import _time  # noqa: E402
+
+# the byte floor's rate: the 4.75 TB/s of a large device copy (read + write) on this box, round 5
+FLOOR_BPS = 4.75e12
 
 # (rows M at batch 128, channels C, uses per step, relu, residual)
 SHAPES = [
@@ -92,13 +96,16 @@ def run(ext, dev):
         bd = e * (3 + (1 if res else 0)) + bits
         rec = {"M": m, "C": c, "uses": uses, "res": res,
                "apply_us": round(ta, 1), "apply_TBps": round(ba / ta / 1e6, 2),
-               "dx_us": round(td, 1), "dx_TBps": round(bd / td / 1e6, 2)}
+               "apply_x_floor": round(ta / (ba / FLOOR_BPS * 1e6), 2),
+               "dx_us": round(td, 1), "dx_TBps": round(bd / td / 1e6, 2),
+               "dx_x_floor": round(td / (bd / FLOOR_BPS * 1e6), 2)}
         tot["apply"][0] += uses * ta
         tot["apply"][1] += uses * ba
         tot["dx"][0] += uses * td
         tot["dx"][1] += uses * bd
         print(json.dumps(rec), flush=True)
-    print(json.dumps({k: {"us_per_step": round(v[0], 1), "TBps": round(v[1] / v[0] / 1e6, 2)}
+    print(json.dumps({k: {"us_per_step": round(v[0], 1), "TBps": round(v[1] / v[0] / 1e6, 2),
+                          "x_floor": round(v[0] / (v[1] / FLOOR_BPS * 1e6), 2)}
                       for k, v in tot.items()}), flush=True)
 
 

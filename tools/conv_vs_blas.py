@@ -9,7 +9,12 @@ For every such layer at the given batch this times, on the same box and the same
   in the form the training step runs them (forward with BatchNorm statistics in the epilogue;
   weight gradient including its split-K slab reduction);
 * **blas**: the identical GEMM through ``torch.matmul``, with hipBLASLt and with rocBLAS as the
-  preferred library (the faster of the two is the yardstick), same bf16 inputs and outputs;
+  preferred library (the faster of the two is the yardstick), same bf16 inputs and outputs. The
+  weight gradient dYᵀ·X is a small [Cout, Cin] output over a huge M reduction, which a plain
+  ``g.t() @ a`` hands the library as ONE GEMM with no split-K (679 us for a 64x64 dW at 56x56:
+  not a yardstick). It is timed as a split-K batched GEMM instead: g and a reshaped to [S, M/S, C],
+  ``torch.bmm`` over the S slices, then an fp32 sum over S -- the best S of 4..512 (the plain
+  form stays in the record as ``blas_plain_us``);
 * **floor**: the layer's minimum bytes (inputs read once, output written once) over the copy
   bandwidth measured here with a large device-to-device copy (``--copy-mb``), and its FLOPs over
   2.5 PFLOP/s dense bf16 -- the larger of the two.
@@ -57,6 +62,24 @@ def blas_time(fn, reps: int):
     return out[lib], lib, out
 
 
+def splitk_wgrad(g: torch.Tensor, a: torch.Tensor, reps: int):
+    """(best us, library, S) of dW = g^T a as S batched slice GEMMs + an fp32 sum over S."""
+    m = g.shape[0]
+    best = None
+    for s_ in (4, 8, 16, 32, 64, 128, 256, 512):
+        if m % s_:
+            continue
+        gs = g.reshape(s_, m // s_, g.shape[1])
+        as_ = a.reshape(s_, m // s_, a.shape[1])
+
+        def fn(gs=gs, as_=as_):
+            return torch.bmm(gs.transpose(1, 2), as_).sum(0, dtype=torch.float32)
+        t, lib, _ = blas_time(fn, reps)
+        if best is None or t < best[0]:
+            best = (t, lib, s_)
+    return best
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--batch", type=int, default=128)
@@ -101,6 +124,11 @@ def main():
             t_ours = timeit(ours, args.reps)
             t_step = timeit(ours_step, args.reps) if ours_step is not None else t_ours
             t_blas, lib, libs = blas_time(blas, args.reps)
+            extra = {}
+            if d == "wgrad":
+                extra["blas_plain_us"] = round(t_blas, 1)
+                t_blas, lib, s_ = splitk_wgrad(g, a, args.reps)
+                extra["blas_splitk_S"] = s_
             floor = max(nbytes / bw * 1e6, flop / PEAK_BF16 * 1e6)
             rec = {"layer": layer, "dir": d, "count": cnt, "gflop": round(flop / 1e9, 2),
                    "mb": round(nbytes / 2**20, 1),
@@ -112,7 +140,7 @@ def main():
                    "floor_us": round(floor, 1),
                    "ours_vs_blas": round(t_ours / t_blas, 3),
                    "ours_vs_floor": round(t_ours / floor, 2),
-                   "ours_tbps": round(nbytes / t_ours / 1e6, 2)}
+                   "ours_tbps": round(nbytes / t_ours / 1e6, 2), **extra}
             print(json.dumps(rec), flush=True)
             totals["ours"] += t_ours * cnt
             totals["ours_step"] += t_step * cnt
