@@ -260,6 +260,14 @@ class XgmiComm:
     def _peer_view(self, key: str, r: int, n: int) -> torch.Tensor:
         return self.ext.ccl_tensor(self._ptrs[key][r], n, self.device)
 
+    def _gate(self) -> None:
+        """Every rank's inputs are ready and every rank is here: launch the next self-test
+        kernel together. Without it a rank spins in a kernel's barrier while a peer is still
+        loading code objects for its first torch ops -- with several ranks sharing one GPU, long
+        enough to hit the barrier timeout."""
+        torch.cuda.synchronize()
+        dist.barrier(group=self.group)
+
     def _prewarm(self) -> None:
         """Read every rank's registered buffers through this rank's mappings, so any line that
         could go stale (a peer's data cached in this GPU's L2, or this rank's own lines) is
@@ -285,6 +293,9 @@ class XgmiComm:
                 ok = fn()
                 torch.cuda.synchronize()
                 res[name] = "ok" if ok else "mismatch"
+                if int(self._err.item()):   # attribute a barrier timeout to its kernel
+                    res[name] = "barrier timeout"
+                    self._err.zero_()
             except Exception as e:  # noqa: BLE001
                 res[name] = repr(e)[:200]
 
@@ -296,11 +307,14 @@ class XgmiComm:
             base = torch.arange(n, device="cuda", dtype=torch.float32) % 977
             for it in range(2):                      # second call reads lines the first cached
                 out = torch.empty(n, device="cuda")
-                self.all_reduce_(base * (rk + 1 + it), out=out)
+                inp = base * (rk + 1 + it)
+                self._gate()
+                self.all_reduce_(inp, out=out)
                 if not torch.equal(out, base * (tot + W * it)):
                     return False
             stage = self._buf[:n]                    # zero-copy, in place on the staging buffer
             stage.copy_(base * (rk + 1))
+            self._gate()
             self.all_reduce_(stage)
             return bool(torch.equal(stage, base * tot))
 
@@ -312,6 +326,7 @@ class XgmiComm:
             for root in (0, W - 1):
                 t = (torch.arange(n, device="cuda", dtype=torch.float32) % 101) * (root + 3)
                 x = t.clone() if rk == root else torch.full((n,), -1.0, device="cuda")
+                self._gate()
                 self.broadcast_(x, root=root)
                 if not torch.equal(x, t):
                     return False
@@ -324,6 +339,7 @@ class XgmiComm:
         def allgather():
             m = min(4096, cap)
             x = torch.arange(m, device="cuda", dtype=torch.float32) + 10000 * rk
+            self._gate()
             got = self.all_gather(x)
             want = torch.stack([torch.arange(m, device="cuda", dtype=torch.float32) + 10000 * q
                                 for q in range(W)])
@@ -361,9 +377,10 @@ class XgmiComm:
             gsum = g[0].clone()
             for x in g[1:]:
                 gsum += x
-            t = torch.full((1,), float(step), device="cuda")
+            t = torch.full((1,), step, dtype=torch.int64, device="cuda")
             self._buf[:n].copy_(g[self.rank])
             self._prewarm()
+            self._gate()
             self.adam_(M, V, n, lr=0.25, t_step=t)
             fused.adam_flat(Pref, Mref, Vref, gsum, lr=0.25, t_step=t)
             torch.cuda.synchronize()
@@ -396,6 +413,7 @@ class XgmiComm:
             ref_m = mu * ref_m + (gsum + wd * ref_w)
             ref_w = ref_w - lr * ref_m
             self._prewarm()
+            self._gate()
             self.peers.sgd_bf16(master, mom, off, n, lr, mu, wd, 1.0)
             torch.cuda.synchronize()
             if not torch.equal(wbf[off:off + n], ref_w.to(bf)):
@@ -423,6 +441,7 @@ class XgmiComm:
             ref_m = mu * ref_m + (gsum + wd * ref_w)
             ref_w = ref_w - lr * ref_m
             self._prewarm()
+            self._gate()
             self.peers.sgd_f32(mom, off, n, lr, mu, wd, 1.0)
             torch.cuda.synchronize()
             if not torch.equal(self._buf2[off:off + n], ref_w):

@@ -22,8 +22,9 @@
 //   all ranks into MY buffer -> barrier 1 -> pull chunk[q] sub-range b from rank q for every q
 //   -> barrier 2 (peers finished reading my chunk before my next copy-in overwrites it)
 //
-// The fused optimizer kernels (Adam, sharded SGD) need no third barrier: an owner next writes its
-// chunk of buf2 after barrier 0 of a LATER call, which no peer reaches before finishing this one.
+// The fused optimizer kernels (Adam, sharded SGD) end on the same third barrier: without it a rank
+// could leave the kernel and rewrite its buffer (a host-side copy, a checkpoint load) while a
+// slower peer still pulls from it -- the per-kernel self-test caught exactly that at W = 8.
 // The push form (owner stores its chunk into every peer's buffer, two barriers) is kept behind
 // ArenaXgmiPeers::push and used only when the communicator's self-test of it passed.
 //
@@ -331,9 +332,13 @@ __global__ __launch_bounds__(kThreads) void xgmi_adam_kernel(ArenaXgmiPeers P, f
     }
   }
   xbarrier<W>(P, 1, b, e);
-  // pull: every other chunk from its owner. No third barrier: an owner next writes its chunk of
-  // buf2 after barrier 0 of a later call, which no peer reaches before this kernel has ended.
-  if (!P.push) pull_chunks<W>(Pm, P.buf2, 0, n, L, lo, hi, P.rank, true);
+  // pull: every other chunk from its owner, then a third barrier, so that when this kernel ends on
+  // any rank no peer still reads its buffers (the owner may rewrite them by any means afterwards:
+  // the next step's gradients, a checkpoint load, a host-side copy)
+  if (!P.push) {
+    pull_chunks<W>(Pm, P.buf2, 0, n, L, lo, hi, P.rank, true);
+    xbarrier<W>(P, 2, b, e);
+  }
   counter_op(ctr);
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
@@ -544,9 +549,12 @@ __global__ __launch_bounds__(kThreads) void xgmi_sgd_bf16_kernel(ArenaXgmiPeers 
     }
   }
   xbarrier<W>(P, 1, b, e);
-  // pull the other chunks in float units (off, n, L, S are multiples of 8 bf16 = 4 floats)
-  if (!P.push)
+  // pull the other chunks in float units (off, n, L, S are multiples of 8 bf16 = 4 floats), then
+  // the end barrier (see xgmi_adam_kernel)
+  if (!P.push) {
     pull_chunks<W>(P.buf2[P.rank], P.buf2, off / 2, n / 2, L / 2, lo / 2, hi / 2, P.rank, true);
+    xbarrier<W>(P, 2, b, e);
+  }
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
@@ -604,7 +612,10 @@ __global__ __launch_bounds__(kThreads) void xgmi_sgd_f32_kernel(ArenaXgmiPeers P
     }
   }
   xbarrier<W>(P, 1, b, e);
-  if (!P.push) pull_chunks<W>(P.buf2[P.rank], P.buf2, off, n, L, lo, hi, P.rank, true);
+  if (!P.push) {   // pull, then the end barrier (see xgmi_adam_kernel)
+    pull_chunks<W>(P.buf2[P.rank], P.buf2, off, n, L, lo, hi, P.rank, true);
+    xbarrier<W>(P, 2, b, e);
+  }
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 

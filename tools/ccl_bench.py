@@ -8,6 +8,7 @@ scatter + all-gather) / all-gather / sharded bf16 SGD vs RCCL.
     # local HBM, so this measures the protocol's barrier + launch cost, not link bandwidth)
     python tools/ccl_bench.py --same-gpu 2
 
+``--forms pull,push`` times both xGMI protocol forms (the push form only if its self-test passes).
 Prints one JSON line per (op, size) from rank 0: time per call (graph-replayed, 50 calls per
 graph) and algorithm / bus bandwidth. busbw uses the ring-equivalent factor of each op: allreduce
 2 (W-1)/W, broadcast 1, all-gather (W-1)/W (of the gathered bytes).
@@ -27,49 +28,18 @@ import torch.multiprocessing as mp
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 
-def timed(fn, iters: int = 50, reps: int = 5) -> float:
-    """Seconds per call of fn, captured in a hipGraph of `iters` calls (launch cost excluded)."""
-    s = torch.cuda.Stream()
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        fn()
-    torch.cuda.current_stream().wait_stream(s)
-    torch.cuda.synchronize()
-    g = torch.cuda.CUDAGraph()
-    try:
-        with torch.cuda.graph(g, capture_error_mode="thread_local"):
-            for _ in range(iters):
-                fn()
-        run = g.replay
-    except Exception:  # noqa: BLE001 - e.g. a collective that refuses capture: time eagerly
-        torch.cuda.synchronize()
-
-        def run():
-            for _ in range(iters):
-                fn()
-    run()
-    torch.cuda.synchronize()
-    best = float("inf")
-    for _ in range(reps):
-        if dist.get_world_size() > 1:
-            dist.barrier()
-        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        a.record()
-        run()
-        b.record()
-        b.synchronize()
-        best = min(best, a.elapsed_time(b) / 1e3 / iters)
-    t = torch.tensor([best], dtype=torch.float64,
-                     device="cuda" if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+from arena_amd.parallel.cclbench import timed  # noqa: E402
 
 
 def bench(rank: int, world: int, sizes, rccl: bool,
-          block_sweep=(1024, 2048, 4096, 8192, 16384)) -> None:
+          block_sweep=(1024, 2048, 4096, 8192, 16384), form: str = "pull") -> None:
     from arena_amd.parallel.xgmi import XgmiComm
     maxn = max(sizes) // 4
+    # the push form is requested through the environment and kept only if its self-test passes
+    os.environ["ARENA_XGMI_PUSH"] = "1" if form == "push" else "0"
     comm = XgmiComm(staging_elems=maxn, param_elems=397520, timeout_s=30.0)
+    if comm.form != form:
+        raise RuntimeError(f"asked for the {form} form, the self-test chose {comm.form}")
     rows = []
     comm.all_reduce_(comm.buffer()[:1024])  # first-call warm-up (code object load), untimed
     torch.cuda.synchronize()
@@ -144,18 +114,20 @@ def bench(rank: int, world: int, sizes, rccl: bool,
             algbw = nb / t / 1e9
             f = 1.0 if "broadcast" in op else ((world - 1) / world if "allgather" in op
                                                else 2 * (world - 1) / world)
-            print(json.dumps({"op": op, "bytes": nb, "world": world, "us": round(t * 1e6, 2),
+            print(json.dumps({"op": op, "form": form, "bytes": nb, "world": world,
+                              "us": round(t * 1e6, 2),
                               "algbw_GBs": round(algbw, 2),
                               "busbw_GBs": round(algbw * f, 2)}), flush=True)
     comm.close()
 
 
-def _same_gpu_rank(rank, world, port, sizes):
+def _same_gpu_rank(rank, world, port, sizes, forms):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world), LOCAL_RANK="0")
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
-    bench(rank, world, sizes, rccl=False)
+    for form in forms:
+        bench(rank, world, sizes, rccl=False, form=form)
     dist.destroy_process_group()
 
 
@@ -163,19 +135,23 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--same-gpu", type=int, default=0, help="W ranks sharing GPU 0 (gloo PG)")
     ap.add_argument("--sizes", default="4096,65536,1048576,1590080,8388608,33554432")
+    ap.add_argument("--forms", default="pull",
+                    help="comma list of xGMI protocol forms to time: pull (default), push")
     args = ap.parse_args()
     sizes = [int(s) for s in args.sizes.split(",")]
+    forms = args.forms.split(",")
     if args.same_gpu:
         with socket.socket() as s:
             s.bind(("127.0.0.1", 0))
             port = s.getsockname()[1]
-        mp.start_processes(_same_gpu_rank, args=(args.same_gpu, port, sizes), nprocs=args.same_gpu,
-                           start_method="spawn")
+        mp.start_processes(_same_gpu_rank, args=(args.same_gpu, port, sizes, forms),
+                           nprocs=args.same_gpu, start_method="spawn")
         return
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    bench(dist.get_rank(), dist.get_world_size(), sizes, rccl=True)
+    for form in forms:
+        bench(dist.get_rank(), dist.get_world_size(), sizes, rccl=True, form=form)
     dist.destroy_process_group()
 
 
