@@ -1404,7 +1404,10 @@ long long reduce_blocks(long long M, int C, long long* rpb) {
 // loops over its vectors. Every block derives its per-channel coefficients in its prologue (from
 // the fp64 sums: ARENA_ACC_REP replicas x 2 x C loads), so fewer, fatter blocks pay that less
 // often: ResNet-50 step 11.718 / 11.677 / 11.578 / 11.811 ms at 4096 / 2048 / 1024 / 512
-// (profiles/r5_ebk_ab.jsonl, same process).
+// (profiles/r5_ebk_ab.jsonl, same process). Going further on the small layers -- a floor of 8 or
+// 16 vectors per thread down to 256 blocks -- lost on every shape (25088 x 256 apply 8.3 -> 8.7 /
+// 10.1 us; step 11.411 -> 11.446 / 11.580 ms, profiles/r6_bn_min_vpt_ab.jsonl): those passes are
+// latency-bound by their few µs of issue, not by the coefficient prologue.
 int g_elem_max_blocks = 1024;
 
 int elementwise_blocks(long long nvec) {
