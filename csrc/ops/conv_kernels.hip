@@ -1034,7 +1034,7 @@ hipError_t launch_t(const ConvArgs& a0, int pipe, hipStream_t st) {
 // Mapped outputs (strided dgrad phases, incl. fill_sib) are stored by the plain epilogue. EPI 2
 // (BN-backward partials of a dgrad output) rides on the coalesced store loop: each thread owns one
 // 8-channel column chunk, so g and g * (x - mean) accumulate in registers across its rows/bands.
-// Not covered (v1 handles them): c16, split-K, persistent tiles.
+// Not covered (v1 handles them): c16 and split-K.
 // ================================================================================================
 typedef float f32x16v __attribute__((ext_vector_type(16)));
 
@@ -1802,7 +1802,7 @@ hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
 }
 
 // v2 variant table (code 1024 + index): BM x BN tile, waves NWM x NWN, stage buffers
-constexpr int kV2Base = 4096;   // above every v1 code (split + 16 k, persistent + 256 p <= 1039)
+constexpr int kV2Base = 4096;   // above every v1 code (base + 16 (k - 1), split-K k <= 16)
 constexpr int kV2Count = 16;
 constexpr int kV2Tiles[kV2Count][2] = {{256, 128}, {256, 256}, {128, 128}, {256, 64}, {128, 256},
                                        {128, 64}, {64, 64}, {64, 128},
