@@ -25,6 +25,9 @@
 // The fused optimizer kernels (Adam, sharded SGD) end on the same third barrier: without it a rank
 // could leave the kernel and rewrite its buffer (a host-side copy, a checkpoint load) while a
 // slower peer still pulls from it -- the per-kernel self-test caught exactly that at W = 8.
+// That last barrier of every pull kernel only has to order the peers' finished loads before the
+// owner's later writes, so it runs without the release / acquire fences (xbarrier<W, false>): no
+// L2 write-back or invalidate on the way out of the kernel.
 // The push form (owner stores its chunk into every peer's buffer, two barriers) is kept behind
 // ArenaXgmiPeers::push and used only when the communicator's self-test of it passed.
 //
@@ -81,7 +84,13 @@ __device__ __forceinline__ float4 add4(float4 a, float4 b) {
   return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
 }
 
-template <int W>
+// FENCE = false: a "readers are done" barrier (the last one of a pull kernel). It publishes
+// nothing -- no peer reads anything this rank wrote since the previous barrier before the next
+// call's first barrier, which has its own release -- and acquires nothing, so it skips the L2
+// write-back and invalidate and only orders every peer's completed loads of this rank's buffers
+// before this rank's later writes to them. Its loads have all returned when the flag goes out:
+// each pulled value was stored before the block's s_barrier, which waits for vmcnt(0).
+template <int W, bool FENCE = true>
 __device__ __forceinline__ void xbarrier(const ArenaXgmiPeers& P, int phase, int b, uint32_t e) {
   // every wave's stores have completed (hipcc emits vmcnt(0) before s_barrier)
   __syncthreads();
@@ -89,10 +98,13 @@ __device__ __forceinline__ void xbarrier(const ArenaXgmiPeers& P, int phase, int
     // ONE system-scope release per block (buffer_wbl2: our stores reach memory before the flags),
     // flags written and polled with relaxed system-scope accesses to uncached memory, then ONE
     // acquire (buffer_inv). An acquire per poll would invalidate L2 on every spin iteration.
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    // the write-back must complete before the flag goes out: hipcc drops the vmcnt(0) after
-    // buffer_wbl2 whenever the scoreboard is provably empty (MI355X_MICROARCH.md, compiler hazard)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (FENCE) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      // the write-back must complete before the flag goes out: hipcc drops the vmcnt(0) after
+      // buffer_wbl2 whenever the scoreboard is provably empty (MI355X_MICROARCH.md, compiler
+      // hazard)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     const int t = threadIdx.x;
     if (t < W) {
       const int slot = (phase * kMaxB + b) * kMaxR;
@@ -107,10 +119,12 @@ __device__ __forceinline__ void xbarrier(const ArenaXgmiPeers& P, int phase, int
         __builtin_amdgcn_s_sleep(1);
       }
     }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    // buffer_inv completes asynchronously: hold the barrier until it has, or the block's other
-    // waves could load the peers' data through a not-yet-invalidated L1 (MI355X_MICROARCH.md)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if constexpr (FENCE) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      // buffer_inv completes asynchronously: hold the barrier until it has, or the block's other
+      // waves could load the peers' data through a not-yet-invalidated L1 (MI355X_MICROARCH.md)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
 }
@@ -239,7 +253,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allreduce_kernel(ArenaXgmiPeers
   } else {
     pull_chunks<W>(out, P.buf, 0, n, L, lo, hi, P.rank, out == mine);
     // peers read my chunk until here: the next call's copy-in must not overwrite it earlier
-    xbarrier<W>(P, 2, b, e);
+    xbarrier<W, false>(P, 2, b, e);
   }
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
@@ -337,7 +351,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_adam_kernel(ArenaXgmiPeers P, f
   // the next step's gradients, a checkpoint load, a host-side copy)
   if (!P.push) {
     pull_chunks<W>(Pm, P.buf2, 0, n, L, lo, hi, P.rank, true);
-    xbarrier<W>(P, 2, b, e);
+    xbarrier<W, false>(P, 2, b, e);
   }
   counter_op(ctr);
   if (threadIdx.x == 0) P.epoch[b] = e;
@@ -368,7 +382,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_bcast_direct_kernel(ArenaXgmiPe
   } else if (out != in) {
     pull_range<1>(&dst_out, &src_in, &zero, &zero, lo, hi, &n);
   }
-  xbarrier<W>(P, 1, b, e);
+  xbarrier<W, false>(P, 1, b, e);
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
@@ -411,7 +425,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_bcast_twoshot_kernel(ArenaXgmiP
   } else if (out != in) {
     copy_chunks<W>(out, in, n, L, lo, hi);
   }
-  xbarrier<W>(P, 2, b, e);
+  xbarrier<W, false>(P, 2, b, e);
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
@@ -442,7 +456,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_allgather_kernel(ArenaXgmiPeers
     lim[q] = m;
   }
   pull_range<W>(dst, src, doff, soff, lo, hi, lim);
-  xbarrier<W>(P, 1, b, e);
+  xbarrier<W, false>(P, 1, b, e);
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
 
@@ -553,7 +567,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_sgd_bf16_kernel(ArenaXgmiPeers 
   // the end barrier (see xgmi_adam_kernel)
   if (!P.push) {
     pull_chunks<W>(P.buf2[P.rank], P.buf2, off / 2, n / 2, L / 2, lo / 2, hi / 2, P.rank, true);
-    xbarrier<W>(P, 2, b, e);
+    xbarrier<W, false>(P, 2, b, e);
   }
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
@@ -614,7 +628,7 @@ __global__ __launch_bounds__(kThreads) void xgmi_sgd_f32_kernel(ArenaXgmiPeers P
   xbarrier<W>(P, 1, b, e);
   if (!P.push) {   // pull, then the end barrier (see xgmi_adam_kernel)
     pull_chunks<W>(P.buf2[P.rank], P.buf2, off, n, L, lo, hi, P.rank, true);
-    xbarrier<W>(P, 2, b, e);
+    xbarrier<W, false>(P, 2, b, e);
   }
   if (threadIdx.x == 0) P.epoch[b] = e;
 }
