@@ -75,9 +75,15 @@ def main():
                 if tb is not None:
                     parts = [(tb, cnt - unlinked[k]), (t, unlinked[k])]
                     row["bwd_linked_us"] = tb
+                    row["bwd_linked_choice"] = str(plan.bwd_bn)
+                    # floor of the linked form: dy in, dx out, the BN input x and its ReLU bits in
+                    lb = (2.0 * n * ho * wo * co + 2.0 * n * h * w * c * 2 + n * h * w * c / 8)
+                    row["bwd_linked_x_floor"] = round(tb / (lb / HBM * 1e6), 2)
             if t is None:
                 continue
-            row[kind] = {"choice": str(choice), "us": t}
+            row[kind] = {"choice": str(choice), "us": t,
+                         "x_floor": round(t / ((io + (2.0 * co * c * r * s if kind != "wgrad" else 0))
+                                              / HBM * 1e6), 2)}
             # the linked dgrad also reads the BN input (bf16) and its ReLU bits
             extra = (2.0 * n * h * w * c + n * h * w * c / 8) if kind == "bwd" else 0.0
             for tt, nn in parts:
