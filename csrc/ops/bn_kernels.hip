@@ -535,6 +535,30 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
   const Slice q = slice_of(cg);
   const long long stride = q.stride;
   const int C = cg * kVec;
+  // the loads of x (and res) do not depend on the coefficients: each thread issues its first two
+  // vectors before the coefficient prologue and the next two before computing the current ones,
+  // so the prologue's round trip to the sums overlaps the first data round trip (most threads of
+  // the 14x14 / 7x7 passes only ever touch two to six vectors)
+  float a[2][kVec], b[2][kVec];
+  bool ok[2];
+  long long vv[2];
+  auto issue = [&](long long v0, float (&ta)[2][kVec], float (&tb)[2][kVec], bool (&tok)[2],
+                   long long (&tvv)[2]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      tvv[u] = v0 + u * stride;
+      tok[u] = tvv[u] < nvec;
+      const long long vc = tok[u] ? tvv[u] : v0;
+      if (NT) {
+        V8<T>::loadnt(x + vc * kVec, ta[u]);
+        if (RES) V8<T>::loadnt(res + vc * kVec, tb[u]);
+      } else {
+        V8<T>::load(x + vc * kVec, ta[u]);
+        if (RES) V8<T>::load(res + vc * kVec, tb[u]);
+      }
+    }
+  };
+  if (q.v0 < nvec) issue(q.v0, a, b, ok, vv);
   apply_coefs<FIN>(C, M, fin, st, s_co, q.c_lo, q.cs, blockIdx.x == 0);   // one per slice
   float mu[kVec], sc[kVec], sh[kVec];
   lds8(s_co + q.c0, mu);
@@ -542,22 +566,11 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
   lds8(s_co + 2 * q.cs + q.c0, sh);
   zero_duty(zero, nzero);
   for (long long v0 = q.v0; v0 < nvec; v0 += 2 * stride) {
-    float a[2][kVec], b[2][kVec];
-    bool ok[2];
-    long long vv[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      vv[u] = v0 + u * stride;
-      ok[u] = vv[u] < nvec;
-      const long long vc = ok[u] ? vv[u] : v0;
-      if (NT) {
-        V8<T>::loadnt(x + vc * kVec, a[u]);
-        if (RES) V8<T>::loadnt(res + vc * kVec, b[u]);
-      } else {
-        V8<T>::load(x + vc * kVec, a[u]);
-        if (RES) V8<T>::load(res + vc * kVec, b[u]);
-      }
-    }
+    float na[2][kVec], nb[2][kVec];
+    bool nok[2] = {false, false};
+    long long nvv[2];
+    const bool more = v0 + 2 * stride < nvec;
+    if (more) issue(v0 + 2 * stride, na, nb, nok, nvv);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       float o[kVec];
@@ -572,6 +585,18 @@ __global__ __launch_bounds__(kT) void bn_apply_kernel(const T* __restrict__ x,
           mask[vv[u]] = (uint8_t)V8<T>::store_pos(y + vv[u] * kVec, o);
         else
           V8<T>::store(y + vv[u] * kVec, o);
+      }
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        ok[u] = nok[u];
+        vv[u] = nvv[u];
+#pragma unroll
+        for (int i = 0; i < kVec; ++i) {
+          a[u][i] = na[u][i];
+          if (RES) b[u][i] = nb[u][i];
+        }
       }
     }
   }
@@ -747,6 +772,20 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
   const int c0 = q.c0, cs = q.cs;
   const int C = cg * kVec;
   const double inv_m = 1.0 / (double)M;
+  // the first vector's loads (dy, mask, x) are issued before the coefficient prologue and each
+  // next vector's before the current one is computed (as in bn_apply_kernel)
+  float d[kVec], xv[kVec], x2v[S2 ? kVec : 1];
+  uint32_t mb = 0xffu;
+  auto issue = [&](long long v, float (&td)[kVec], float (&tx)[kVec], float (&tx2)[S2 ? kVec : 1],
+                   uint32_t& tm) {
+    if (NT) V8<T>::loadnt(dy + v * kVec, td); else V8<T>::load(dy + v * kVec, td);
+    tm = RELU ? (uint32_t)mask[v] : 0xffu;
+    if (NT) V8<T>::loadnt(x + v * kVec, tx); else V8<T>::load(x + v * kVec, tx);
+    if constexpr (S2) {
+      if (NT) V8<T>::loadnt(x2 + v * kVec, tx2); else V8<T>::load(x2 + v * kVec, tx2);
+    }
+  };
+  if (q.v0 < nvec) issue(q.v0, d, xv, x2v, mb);
   for (int cl = threadIdx.x; cl < cs; cl += kT) {   // one thread per channel (see lds8)
     const int c = q.c_lo + cl;
     float a_, b_, c_;
@@ -788,13 +827,10 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
     }
   }
   for (long long v = q.v0; v < nvec; v += stride) {
-    float d[kVec], xv[kVec], x2v[S2 ? kVec : 1];
-    if (NT) V8<T>::loadnt(dy + v * kVec, d); else V8<T>::load(dy + v * kVec, d);
-    const uint32_t mb = RELU ? (uint32_t)mask[v] : 0xffu;
-    if (NT) V8<T>::loadnt(x + v * kVec, xv); else V8<T>::load(x + v * kVec, xv);
-    if constexpr (S2) {
-      if (NT) V8<T>::loadnt(x2 + v * kVec, x2v); else V8<T>::load(x2 + v * kVec, x2v);
-    }
+    float dn[kVec], xn[kVec], x2n[S2 ? kVec : 1];
+    uint32_t mn = 0xffu;
+    const bool more = v + stride < nvec;
+    if (more) issue(v + stride, dn, xn, x2n, mn);
     float g[kVec], o[kVec];
 #pragma unroll
     for (int i = 0; i < kVec; ++i) {
@@ -810,6 +846,15 @@ __global__ __launch_bounds__(kT) void bn_bwd_dx_kernel(const T* __restrict__ dy,
     }
     V8<T>::store(dx + v * kVec, o);
     if (RES) V8<T>::store(dres + v * kVec, g);
+    if (more) {
+      mb = mn;
+#pragma unroll
+      for (int i = 0; i < kVec; ++i) {
+        d[i] = dn[i];
+        xv[i] = xn[i];
+        if constexpr (S2) x2v[i] = x2n[i];
+      }
+    }
   }
   if constexpr (S2) {
     // the block's partial sums per channel: thread t holds channel group t % cgl of row t / cgl
