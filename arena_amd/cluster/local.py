@@ -465,11 +465,17 @@ class LocalBackend(Backend):
         return out
 
     # ------------------------------------------------------------------------- cluster view
-    def _cluster(self) -> ClusterState:
+    def _cluster(self, only: Optional[str] = None) -> ClusterState:
+        """The cluster view rebuilt from the job store. ``only``: just that release (every
+        object a release renders carries its ``release`` label, and each release's view is built
+        independently), so a label query for one job reads one job's files, not the whole store."""
         full = ClusterState()
         node = self._node()
         full.nodes[node.name] = node
-        for name in self._release_names():
+        names = self._release_names()
+        if only is not None:
+            names = [n for n in names if n == only]
+        for name in names:
             rel = self._read_json(os.path.join(self.job_dir(name), "release.json"))
             if not rel:
                 continue
@@ -529,18 +535,22 @@ class LocalBackend(Backend):
                 full.jobs.pop(tuple(key), None)
         return full
 
+    @staticmethod
+    def _only(selector) -> Optional[str]:
+        return selector.get("release") if selector else None
+
     def list_pods(self, namespace=None, selector=None, active_only=False):
-        return [p for p in self._cluster().pods.values()
+        return [p for p in self._cluster(self._only(selector)).pods.values()
                 if (not namespace or p.namespace == namespace) and matches(p.meta.labels, selector)
                 and not (active_only and p.phase in (POD_SUCCEEDED, POD_FAILED))]
 
     def list_jobs(self, namespace=None, selector=None):
-        return [j for j in self._cluster().jobs.values()
+        return [j for j in self._cluster(self._only(selector)).jobs.values()
                 if (not namespace or j.meta.namespace == namespace)
                 and matches(j.meta.labels, selector)]
 
     def list_tfjobs(self, namespace=None, selector=None):
-        return [t for t in self._cluster().tfjobs.values()
+        return [t for t in self._cluster(self._only(selector)).tfjobs.values()
                 if (not namespace or t.meta.namespace == namespace)
                 and matches(t.meta.labels, selector)]
 
@@ -548,7 +558,7 @@ class LocalBackend(Backend):
         return [self._node()]
 
     def list_services(self, namespace, selector=None):
-        return [s for s in self._cluster().services.values()
+        return [s for s in self._cluster(self._only(selector)).services.values()
                 if s.meta.namespace == namespace and matches(s.meta.labels, selector)]
 
     _DASHBOARDS = ("kubernetes-dashboard", "tf-job-dashboard")

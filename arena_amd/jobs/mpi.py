@@ -6,7 +6,6 @@ are listed too, chief last.
 """
 from __future__ import annotations
 
-from ..cluster.objects import matches
 from .job_info import JobInfo
 from .trainer import Trainer
 
@@ -23,17 +22,14 @@ class MPIJobTrainer(Trainer):
     def is_supported(self, name, namespace) -> bool:
         sel = self._sel(name)
         if self.cache is not None:
-            return any(j.meta.namespace == namespace and matches(j.meta.labels, sel)
-                       for j in self.cache.jobs)
+            return bool(self.cache.select("jobs", namespace, sel))
         return len(self.backend.list_jobs(namespace, sel)) > 0   # Q10: use ns, not a global
 
     def get_training_job(self, name, namespace):
         sel = self._sel(name)
         if self.cache is not None:
-            jobs = [j for j in self.cache.jobs
-                    if j.meta.namespace == namespace and matches(j.meta.labels, sel)]
-            pods = [p for p in self.cache.pods
-                    if p.namespace == namespace and matches(p.meta.labels, sel)]
+            jobs = self.cache.select("jobs", namespace, sel)
+            pods = self.cache.select("pods", namespace, sel)
         else:
             jobs = self.backend.list_jobs(namespace, sel)
             pods = self.backend.list_pods(namespace, sel)

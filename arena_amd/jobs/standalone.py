@@ -2,7 +2,6 @@
 release=<name>, app=training; the chief is the newest pod; the pod list is [chief]."""
 from __future__ import annotations
 
-from ..cluster.objects import matches
 from .job_info import JobInfo
 from .trainer import Trainer
 
@@ -19,17 +18,14 @@ class StandaloneJobTrainer(Trainer):
     def is_supported(self, name, namespace) -> bool:
         sel = self._sel(name)
         if self.cache is not None:
-            return any(j.meta.namespace == namespace and matches(j.meta.labels, sel)
-                       for j in self.cache.jobs)
+            return bool(self.cache.select("jobs", namespace, sel))
         return len(self.backend.list_jobs(namespace, sel)) > 0
 
     def get_training_job(self, name, namespace):
         sel = self._sel(name)
         if self.cache is not None:
-            jobs = [j for j in self.cache.jobs
-                    if j.meta.namespace == namespace and matches(j.meta.labels, sel)]
-            pods = [p for p in self.cache.pods
-                    if p.namespace == namespace and matches(p.meta.labels, sel)]
+            jobs = self.cache.select("jobs", namespace, sel)
+            pods = self.cache.select("pods", namespace, sel)
         else:
             jobs = self.backend.list_jobs(namespace, sel)
             pods = self.backend.list_pods(namespace, sel)

@@ -133,8 +133,7 @@ class TensorFlowJobTrainer(Trainer):
     def _task_jobs(self, name, namespace) -> List[Job]:
         sel = self._sel(name)
         if self.cache is not None:
-            jobs = [j for j in self.cache.jobs
-                    if j.meta.namespace == namespace and matches(j.meta.labels, sel)]
+            jobs = self.cache.select("jobs", namespace, sel)
         else:
             jobs = self.backend.list_jobs(namespace, sel)
         return [j for j in jobs if j.meta.labels.get("tf-replica-type")]
@@ -142,8 +141,7 @@ class TensorFlowJobTrainer(Trainer):
     def _tfjobs(self, name, namespace) -> List[TFJob]:
         sel = self._sel(name)
         if self.cache is not None:
-            return [t for t in self.cache.tfjobs
-                    if t.meta.namespace == namespace and matches(t.meta.labels, sel)]
+            return self.cache.select("tfjobs", namespace, sel)
         try:
             return self.backend.list_tfjobs(namespace, sel)
         except Exception:  # noqa: BLE001 - no TFJob API in this cluster
@@ -155,7 +153,7 @@ class TensorFlowJobTrainer(Trainer):
     def get_training_job(self, name, namespace):
         tfjobs = self._tfjobs(name, namespace)
         if self.cache is not None:
-            pods = self.cache.pods
+            pods = self.cache.of_release("pods", name)
         else:
             pods = self.backend.list_pods(namespace, {"release": name})
         chief, out = None, []

@@ -82,7 +82,10 @@ class Trainer(abc.ABC):
 
 
 class ClusterCache:
-    """All pods / jobs / TFJobs fetched once for list/top (list.go:36-47, pod_helper.go)."""
+    """All pods / jobs / TFJobs fetched once for list/top (list.go:36-47, pod_helper.go), indexed
+    by their ``release`` label: every trainer selector names its release, so a lookup touches only
+    that release's objects and listing N jobs stays linear in N (a scan of every object per job
+    made ``arena list`` quadratic: 100 jobs took 0.12-0.15 s, most of it in label matching)."""
 
     def __init__(self, backend):
         self.pods = backend.list_pods()
@@ -91,6 +94,22 @@ class ClusterCache:
             self.tfjobs = backend.list_tfjobs()
         except Exception:  # noqa: BLE001 - TFJob API absent -> trainer disabled
             self.tfjobs = []
+        self._index = {}
+        for kind in ("pods", "jobs", "tfjobs"):
+            idx = self._index[kind] = {}
+            for o in getattr(self, kind):
+                idx.setdefault(o.meta.labels.get("release"), []).append(o)
+
+    def of_release(self, kind: str, release: str) -> list:
+        """The cached ``kind`` objects labelled ``release=<release>`` (any namespace)."""
+        return self._index[kind].get(release, [])
+
+    def select(self, kind: str, namespace: str, sel: dict) -> list:
+        """The cached ``kind`` objects in ``namespace`` matching the equality selector ``sel``
+        (which must name a release)."""
+        from ..cluster.objects import matches
+        return [o for o in self.of_release(kind, sel["release"])
+                if o.meta.namespace == namespace and matches(o.meta.labels, sel)]
 
 
 def new_trainers(backend, cache=None) -> List[Trainer]:
