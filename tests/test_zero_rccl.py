@@ -154,7 +154,7 @@ def _run(world, reduce_fp32, backend="rccl", local_size=None, skew_order=False):
     return out
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 @pytest.mark.parametrize("reduce_fp32", [True, False])
 def test_rccl_sharded_sgd_matches_torch_sgd(world, reduce_fp32):
     out = _run(world, reduce_fp32)
@@ -180,7 +180,7 @@ def _check_shards_partition(res, world):
             assert len({b - a for a, b in spans}) == 1, (dt, j, spans)
 
 
-@pytest.mark.parametrize("world,local_size", [(4, 2), (6, 2)])
+@pytest.mark.parametrize("world,local_size", [(4, 2), (6, 2), (8, 4)])
 @pytest.mark.parametrize("reduce_fp32", [True, False])
 def test_hier_sharded_sgd_matches_torch_sgd(world, local_size, reduce_fp32):
     """Hierarchical backend (Horovod's hierarchical allreduce, sharded): node-level
