@@ -50,10 +50,15 @@ V2_HALO = {V2 + 12: (128, 128), V2 + 13: (128, 64),
            V2 + 14: (128, 64),   # 14: the window of <= 31-wide images (four blocks per CU)
            # 15: two groups of four waves split the 64-channel chunks (two waves per SIMD; even
            # chunk counts only)
-           V2 + 15: (128, 128)}
+           V2 + 15: (128, 128),
+           # 16..18: eight waves, a 256-pixel or 256-channel tile per block (each weight tap
+           # staged into LDS feeds twice the MFMAs of a 128x128 tile)
+           V2 + 16: (256, 128), V2 + 17: (128, 256), V2 + 18: (256, 64)}
 HALO_MAX_W = 63
 HALO_SMALL = {V2 + v: 31 for v in (14, 15)}
 HALO_SPLIT2 = {V2 + 15}
+HALO_WIDE = {V2 + 16, V2 + 17, V2 + 18}   # the 8-wave forms (set_halo_wide, for A/Bs)
+_HALO_WIDE_ON = True
 V2_TILES.update(V2_HALO)
 TILES.update(V2_TILES)
 _V2_ON = os.environ.get("ARENA_CONV_V2", "1") != "0"
@@ -82,6 +87,12 @@ def v2_variants_for(cout: int):
             if cout % bn == 0 and v not in V2_HALO] if _V2_ON else []
 
 
+def set_halo_wide(on: bool) -> None:
+    """A/B switch: offer the 8-wave halo forms to the autotuner (part of the plan key)."""
+    global _HALO_WIDE_ON
+    _HALO_WIDE_ON = bool(on)
+
+
 def halo_variants_for(cout: int, k, stride: int, pad: int, width: int, cin: int | None = None):
     """The 3x3 halo forms, for a 3x3 / stride 1 / pad 1 convolution of a <= 63-wide image
     (``cin``: the input channels; the two-group forms need an even number of 64-channel chunks)."""
@@ -89,7 +100,8 @@ def halo_variants_for(cout: int, k, stride: int, pad: int, width: int, cin: int 
         return []
     return [v for v, (_, bn) in V2_HALO.items()
             if cout % bn == 0 and width <= HALO_SMALL.get(v, HALO_MAX_W)
-            and (v not in HALO_SPLIT2 or (cin is None or (cin // 64) % 2 == 0))]
+            and (v not in HALO_SPLIT2 or (cin is None or (cin // 64) % 2 == 0))
+            and (_HALO_WIDE_ON or v not in HALO_WIDE)]
 
 
 def out_hw(h: int, w: int, r: int, s: int, stride: int, pad: int) -> Tuple[int, int]:
@@ -699,7 +711,7 @@ def _best(t: dict, kind: str, n: int):
 
 def plan_for(x: Tensor, w: Tensor, stride: int, pad: int) -> ConvPlan:
     key = (tuple(x.shape), tuple(w.shape), stride, pad, x.device.index, _mode(), _V2_ON,
-           _BN_LINKS)
+           _BN_LINKS, _HALO_WIDE_ON)
     plan = _PLANS.get(key)
     if plan is not None and (plan.tuned or torch.cuda.is_current_stream_capturing()):
         return plan

@@ -884,7 +884,7 @@ ConvSplit conv_split(const Tensor& x, int64_t variant, int64_t M, int64_t Cout, 
   ConvSplit s;
   TORCH_CHECK(variant >= 0, "conv: bad variant ", variant);
   if (variant >= 4096) {   // v2 tile kernel (conv_kernels.hip conv2_body): 4096 + i
-    TORCH_CHECK(variant - 4096 < 16, "conv: unknown v2 variant ", variant);
+    TORCH_CHECK(variant - 4096 < 19, "conv: unknown v2 variant ", variant);
     s.base = (int)variant;
   } else {   // v1 tile i (0..15), its K steps split over ks blocks: i + 16 (ks - 1)
     TORCH_CHECK(variant < 256, "conv: unknown variant ", variant);

@@ -1727,15 +1727,18 @@ void conv2_kernel_occ4(ConvArgs a) {
 // the 3x3 halo form (see Conv2Geo::HALO): 4 waves, a ring of NBR per-tap weight buffers --
 // 128x128: three (80 KB, two blocks per CU); 128x64: two (48 KB, three blocks per CU; with the
 // small window of <= 31-wide images 40 KB, four blocks per CU)
-template <int BM, int BN, int EPI, int HW, int NB>
-__global__ __launch_bounds__((HW & kHaloSplit2) ? 512 : 256) void conv2_kernel_halo(ConvArgs a) {
+template <int BM, int BN, int EPI, int HW, int NB, int NWM = 2, int NWN = 2>
+__global__ __launch_bounds__((HW & kHaloSplit2) ? 512 : 64 * NWM * NWN)
+void conv2_kernel_halo(ConvArgs a) {
 #if defined(__HIP_DEVICE_COMPILE__)
-  conv2_body<BM, BN, 2, 2, NB, EPI, false, HW>(a, blockIdx.x);
+  conv2_body<BM, BN, NWM, NWN, NB, EPI, false, HW>(a, blockIdx.x);
 #endif
 }
 
-// HW: window size class (1: <= 63 wide, 2: <= 31) | kHaloWin2; NB: weight ring buffers
-template <int BM, int BN, int HW, int NB>
+// HW: window size class (1: <= 63 wide, 2: <= 31) | kHaloWin2; NB: weight ring buffers; NWM x NWN
+// waves (8-wave forms: a 256-pixel or 256-channel tile per block, so each weight tap staged into
+// LDS feeds twice the MFMAs of a 128x128 tile)
+template <int BM, int BN, int HW, int NB, int NWM = 2, int NWN = 2>
 hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
   ConvArgs a = a0;
   if (a.c16 || a.Cout % BN || a.R != 3 || a.S != 3 ||
@@ -1743,7 +1746,7 @@ hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
       a.W > ((HW & 3) == 2 ? kHaloSmallW : kHaloMaxW) || a.mapped ||
       ((HW & kHaloSplit2) && (a.C / kBK) % 2))
     return hipErrorInvalidValue;
-  const int nthr = (HW & kHaloSplit2) ? 512 : 256;
+  const int nthr = (HW & kHaloSplit2) ? 512 : 64 * NWM * NWN;
   if (a.ksplit != 1) return hipErrorInvalidValue;
   if (a.bnx == nullptr && (a.part != nullptr || a.bn_acc != nullptr) && a.add != nullptr)
     return hipErrorInvalidValue;
@@ -1751,11 +1754,14 @@ hipError_t launch2_halo(const ConvArgs& a0, hipStream_t st) {
   a.n_tiles = a.Cout / BN;
   const int nwg = a.m_tiles * a.n_tiles;
   if (a.bnx != nullptr)
-    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW, NB>), dim3(nwg), dim3(nthr), 0, st, a);
+    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 2, HW, NB, NWM, NWN>), dim3(nwg), dim3(nthr), 0,
+                       st, a);
   else if (a.part != nullptr || a.bn_acc != nullptr)
-    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1, HW, NB>), dim3(nwg), dim3(nthr), 0, st, a);
+    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 1, HW, NB, NWM, NWN>), dim3(nwg), dim3(nthr), 0,
+                       st, a);
   else
-    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 0, HW, NB>), dim3(nwg), dim3(nthr), 0, st, a);
+    hipLaunchKernelGGL((conv2_kernel_halo<BM, BN, 0, HW, NB, NWM, NWN>), dim3(nwg), dim3(nthr), 0,
+                       st, a);
   return hipGetLastError();
 }
 
@@ -1803,12 +1809,13 @@ hipError_t launch2_t(const ConvArgs& a0, hipStream_t st) {
 
 // v2 variant table (code 1024 + index): BM x BN tile, waves NWM x NWN, stage buffers
 constexpr int kV2Base = 4096;   // above every v1 code (base + 16 (k - 1), split-K k <= 16)
-constexpr int kV2Count = 16;
+constexpr int kV2Count = 19;
 constexpr int kV2Tiles[kV2Count][2] = {{256, 128}, {256, 256}, {128, 128}, {256, 64}, {128, 256},
                                        {128, 64}, {64, 64}, {64, 128},
                                        {128, 128}, {128, 64}, {64, 128}, {64, 64},
                                        {128, 128}, {128, 64}, {128, 64},
-                                       {128, 128}};
+                                       {128, 128},
+                                       {256, 128}, {128, 256}, {256, 64}};
 
 hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
   switch (idx) {
@@ -1835,6 +1842,13 @@ hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
     // Measured and not kept (profiles/r6_halo_variants.jsonl): 128x128 with two groups and two
     // ring buffers, 128x64 with two groups, four- and six-deep rings, a second window buffer.
     case 15: return launch2_halo<128, 128, 2 | kHaloSplit2, 3>(a, st);
+    // 8-wave halo forms (one block per CU, two waves per SIMD): the L2 -> LDS weight stream is
+    // what bounds the 4-wave forms (16 KB per tap per 128x128 block ~ 30 B/clk per CU at full MFMA
+    // rate, the measured L2 -> LDS rate; MI355X_MICROARCH.md "gather into LDS"). A 256-pixel or
+    // 256-channel block halves the weight bytes per MFMA.
+    case 16: return launch2_halo<256, 128, 1, 3, 4, 2>(a, st);   // 128 KB (epilogue tile)
+    case 17: return launch2_halo<128, 256, 1, 3, 2, 4>(a, st);   // 128 KB
+    case 18: return launch2_halo<256, 64, 1, 3, 4, 2>(a, st);    // 72 KB, two blocks per CU
     default: return hipErrorInvalidValue;
   }
 }

@@ -236,7 +236,7 @@ def test_v2_variants_are_forward_and_dgrad_only():
     assert set(conv.v2_variants_for(256)) == set(conv.V2_TILES) - set(conv.V2_HALO)
     assert set(conv.halo_variants_for(256, (3, 3), 1, 1, 14)) == set(conv.V2_HALO)
     # no small window at 56 wide
-    assert conv.halo_variants_for(64, (3, 3), 1, 1, 56) == [conv.V2 + 13]
+    assert conv.halo_variants_for(64, (3, 3), 1, 1, 56) == [conv.V2 + 13, conv.V2 + 18]
     # the two-group forms need an even number of 64-channel chunks
     assert not set(conv.halo_variants_for(256, (3, 3), 1, 1, 14, 192)) & conv.HALO_SPLIT2
     assert conv.HALO_SPLIT2 <= set(conv.halo_variants_for(256, (3, 3), 1, 1, 14, 256))
@@ -245,6 +245,12 @@ def test_v2_variants_are_forward_and_dgrad_only():
     assert not conv.halo_variants_for(256, (3, 3), 2, 1, 14)
     assert not conv.halo_variants_for(256, (3, 3), 1, 1, 64)
     assert not conv.halo_variants_for(256, (1, 1), 1, 0, 14)
+    assert conv.HALO_WIDE <= set(conv.halo_variants_for(256, (3, 3), 1, 1, 14))
+    conv.set_halo_wide(False)
+    try:
+        assert not set(conv.halo_variants_for(256, (3, 3), 1, 1, 14)) & conv.HALO_WIDE
+    finally:
+        conv.set_halo_wide(True)
     assert not set(conv.variants_for(256)) & set(conv.V2_TILES)   # disjoint code ranges
     # v2 weight gradients need >= 128-channel tiles on both sides
     assert not set(conv.wgrad_variants_for(64, 256)) & set(conv.WGRAD_V2)
@@ -568,7 +574,7 @@ def test_dgrad_epilogue_bn_backward_partials():
     """conv2d_bwd_data(..., bn=(x, mask, mean)): per-tile sum g and sum g (x - mean) of the
     stored dX (g = dX * mask bit), the bn_bwd_reduce partial format, tail tile included, on every
     v1 and v2 tile, with and without an addend."""
-    n, cin, h, w, cout, k = 3, 128, 9, 11, 64, 3
+    n, cin, h, w, cout, k = 3, 256, 9, 11, 64, 3   # 256 dX channels: every halo tile width
     x, wt = _data(n, cin, h, w, cout, k, "cuda", seed=5)
     dy = torch.randn(n, cout, h, w, device="cuda").to(torch.bfloat16).contiguous(
         memory_format=torch.channels_last)

@@ -7,7 +7,7 @@ Builds one model + optimizer + synthetic batch per variant (same seed), warms ea
 every variant alike (cdna_hip_programming.md §5.4 rule 24). Variants are conv modes
 (ARENA_CONV values), optionally suffixed ``:async`` (weight gradients on a side stream) and/or
 ``:link`` / ``:nolink`` (BN-backward partials in the dgrad epilogues; on by default) and/or
-``:laccP<n>`` (their fp64-sum form up to n tile-channel pairs), ``:torchstem`` (the stem's
+``:laccP<n>`` (their fp64-sum form up to n tile-channel pairs), ``:nohalowide`` (no 8-wave halo forms), ``:torchstem`` (the stem's
 input/weight casts and weight transform as torch ops) and/or ``:nomask`` (the last BN writes
 dy * mask for the residual join instead of parking (dy, bits)) and/or ``:finP<n>`` (at most n
 level-1 blocks per channel group in the BN finalize kernels) and/or ``:redG<b>x<r>`` (BN reduction grid) and/or ``:accP<n>`` (conv-epilogue
@@ -65,6 +65,7 @@ def main():
         # BN-backward partials in the dgrad epilogue: on by default, "nolink" turns them off
         conv.set_bn_links("nolink" not in opts if "link" not in opts else True)
         conv.set_stem_fused("torchstem" not in opt_s.split("+"))
+        conv.set_halo_wide("nohalowide" not in opt_s.split("+"))   # the 8-wave halo forms
         conv.set_masked_join("nomask" not in opt_s.split("+"))
         # finP<n>: at most n level-1 blocks per channel group in the BN finalize kernels (the
         # grid is baked into this variant's captured graph)

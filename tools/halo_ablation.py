@@ -9,6 +9,7 @@ are garbage with any bit set):
 and combinations. One JSON line per (layer, variant, flags): us, TFLOP/s.
 
     python tools/halo_ablation.py > gpurun_out/halo_ablation.jsonl
+    FLAGS=0 python tools/halo_ablation.py     # the variants as they run, no ablation
 """
 from __future__ import annotations
 
@@ -22,7 +23,7 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."
 from arena_amd.ops import _ext, conv  # noqa: E402
 
 LAYERS = [(64, 56), (128, 28), (256, 14), (512, 7)]
-FLAGS = [0, 1, 2, 3, 4, 8, 12, 15]
+FLAGS = [int(f) for f in os.environ.get("FLAGS", "0,1,2,3,4,8,12,15").split(",")]
 
 
 def main():
