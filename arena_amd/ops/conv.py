@@ -57,7 +57,7 @@ V2_HALO = {V2 + 12: (128, 128), V2 + 13: (128, 64),
 HALO_MAX_W = 63
 HALO_SMALL = {V2 + v: 31 for v in (14, 15)}
 HALO_SPLIT2 = {V2 + 15}
-HALO_WIDE = {V2 + 16, V2 + 17, V2 + 18}   # the 8-wave forms (set_halo_wide, for A/Bs)
+HALO_WIDE = {V2 + v for v in range(16, 19)}   # the 8-wave forms (set_halo_wide, for A/Bs)
 _HALO_WIDE_ON = True
 V2_TILES.update(V2_HALO)
 TILES.update(V2_TILES)

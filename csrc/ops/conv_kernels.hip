@@ -1849,6 +1849,8 @@ hipError_t launch2(const ConvArgs& a, int idx, hipStream_t st) {
     case 16: return launch2_halo<256, 128, 1, 3, 4, 2>(a, st);   // 128 KB (epilogue tile)
     case 17: return launch2_halo<128, 256, 1, 3, 2, 4>(a, st);   // 128 KB
     case 18: return launch2_halo<256, 64, 1, 3, 4, 2>(a, st);    // 72 KB, two blocks per CU
+    // (a four-buffer ring on 16 / 18, three taps in flight, measured no faster:
+    // profiles/r6_halo_wide_ring4.jsonl)
     default: return hipErrorInvalidValue;
   }
 }
