@@ -26,7 +26,7 @@ from torch import nn
 
 from ..ops.batchnorm import BatchNormAct2d, ResidualMask, bn_relu_maxpool
 from ..ops.conv import BNGradLink, Conv2dNHWC, GradJoin, StemConv2d, WeightFlipper
-from ..ops.pool import MaxPool2dNHWC
+from ..ops.pool import MaxPool2dNHWC, global_avg_pool
 
 # Downsample blocks build their shortcut after the main path (see Bottleneck.forward; A/B switch,
 # ARENA_DOWN_LAST=0 builds it first).
@@ -132,7 +132,7 @@ class ResNet(nn.Module):
                 out_link = BNGradLink() if torch.is_grad_enabled() else None
                 x = blk(x, link=link, link_out=out_link)
                 link = out_link
-        return self.fc(torch.flatten(nn.functional.adaptive_avg_pool2d(x, 1), 1))
+        return self.fc(global_avg_pool(x))
 
 
 def resnet(name: str = "resnet50", num_classes: int = 1000, width: int = 64) -> ResNet:

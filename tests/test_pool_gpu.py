@@ -58,3 +58,22 @@ def test_resnet_stem_uses_the_kernel():
     from arena_amd.ops.pool import MaxPool2dNHWC
     m = resnet("resnet_tiny", num_classes=10, width=8)
     assert isinstance(m.stem[2], MaxPool2dNHWC)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_global_avg_pool_matches_adaptive_pool(dtype):
+    """ResNet head pool: output and gradient of the channels_last global average pool against
+    F.adaptive_avg_pool2d; the gradient comes back channels_last."""
+    from arena_amd.ops.pool import global_avg_pool
+    x = torch.randn(6, 256, 7, 7, device="cuda").to(dtype).contiguous(
+        memory_format=torch.channels_last).requires_grad_(True)
+    x2 = x.detach().clone().requires_grad_(True)
+    y = global_avg_pool(x)
+    y2 = torch.flatten(torch.nn.functional.adaptive_avg_pool2d(x2, 1), 1)
+    assert y.shape == y2.shape and torch.allclose(y.float(), y2.float(), rtol=1e-2, atol=1e-3)
+    g = torch.randn_like(y)
+    y.backward(g)
+    y2.backward(g)
+    assert x.grad.is_contiguous(memory_format=torch.channels_last)
+    assert torch.allclose(x.grad.float(), x2.grad.float(), rtol=1e-2, atol=1e-4)
