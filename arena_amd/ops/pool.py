@@ -66,7 +66,8 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
     """Mean over H, W of a channels_last activation, [N, C, H, W] -> [N, C]. The backward writes
     the (broadcast) gradient straight into a channels_last tensor: the stock adaptive-pool
     backward materialises it NCHW and the next layer's channels_last conversion then transposes
-    25.7 MB at ResNet-50 bs128 (14 + 45.5 us per step, profiles/r6_kernel_neighbors.txt)."""
+    25.7 MB at ResNet-50 bs128 (14 + 45.5 us per step; this form 5 + 22 us,
+    profiles/r6_kernel_neighbors.txt)."""
 
     @staticmethod
     def forward(ctx, x):
