@@ -116,8 +116,10 @@ def build(args, dev, world):
         opt = OptimizerGroup(
             MasterSGD(decay, lr=args.learning_rate, momentum=args.momentum,
                       weight_decay=args.weight_decay),
+            # BN scales / shifts and biases (fp32): torch's fused multi-tensor SGD, one launch
+            # instead of the five of the foreach form
             torch.optim.SGD(no_decay, lr=args.learning_rate, momentum=args.momentum,
-                            foreach=True))
+                            fused=dev.type == "cuda", foreach=None if dev.type == "cuda" else True))
     else:
         opt = torch.optim.SGD([{"params": decay, "weight_decay": args.weight_decay},
                                {"params": no_decay, "weight_decay": 0.0}],
