@@ -159,7 +159,14 @@ def comms_of(opt) -> list:
 def train_step(model, opt, x, y, amp_dtype, zero_grad=True):
     with torch.autocast(device_type=x.device.type, dtype=amp_dtype, enabled=amp_dtype is not None,
                         cache_enabled=False):
-        loss = F.cross_entropy(model(x), y)
+        logits = model(x)
+    # (outside autocast: the fused loss takes the bf16 logits as they are and sums in fp32, as
+    # autocast's fp32 cross_entropy does after its upcast copy)
+    if x.is_cuda:
+        from ..ops.pool import cross_entropy
+        loss = cross_entropy(logits, y)
+    else:
+        loss = F.cross_entropy(logits.float(), y)
     if zero_grad:
         opt.zero_grad(set_to_none=True)
     loss.backward()

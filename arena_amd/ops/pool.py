@@ -89,3 +89,27 @@ def global_avg_pool(x: torch.Tensor) -> torch.Tensor:
     if x.is_cuda and x.dim() == 4 and x.is_contiguous(memory_format=torch.channels_last):
         return _GlobalAvgPoolFn.apply(x)
     return torch.flatten(F.adaptive_avg_pool2d(x, 1), 1)
+
+
+class _SoftmaxXentFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, labels):
+        loss, lse = _ext.load().xent_fwd(logits, labels)
+        ctx.save_for_backward(logits, labels, lse)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        logits, labels, lse = ctx.saved_tensors
+        return _ext.load().xent_bwd(logits, labels, lse, g.float().reshape(1)), None
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """``F.cross_entropy(logits, labels)`` (mean reduction, fp32 result, no ignore_index / label
+    smoothing) in two HIP launches on the GPU (``pool_kernels.hip`` xent kernels): forward loss +
+    per-row log-sum-exp, backward one elementwise pass in the logits' dtype. Anything else runs
+    the stock op."""
+    if (logits.is_cuda and logits.dim() == 2 and labels.dim() == 1
+            and labels.dtype == torch.int64 and logits.dtype in (torch.bfloat16, torch.float32)):
+        return _SoftmaxXentFn.apply(logits.contiguous(), labels.contiguous())
+    return F.cross_entropy(logits.float(), labels)

@@ -109,6 +109,10 @@ hipError_t arena_maxpool_fwd(int, const void*, void*, uint8_t*, int, int, int, i
                              hipStream_t);
 hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, int, int, int, int,
                              int, hipStream_t);
+hipError_t arena_xent_fwd(int, const void*, const long long*, float*, float*, int, int,
+                          hipStream_t);
+hipError_t arena_xent_bwd(int, const void*, const long long*, const float*, const float*, void*,
+                          int, int, hipStream_t);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, uint8_t*, long long, int, int, int,
                         float*, int, long long, double*, unsigned*, ArenaBNStats, double*, int,
                         double*, int, hipStream_t);
@@ -1759,6 +1763,44 @@ Tensor conv_wgrad(Tensor x, Tensor dy, int64_t R, int64_t S, int64_t stride, int
   return dw;
 }
 
+// Softmax cross-entropy, mean over rows (pool_kernels.hip): (loss, per-row log-sum-exp).
+static void xent_check(const Tensor& x, const Tensor& y) {
+  TORCH_CHECK(x.is_cuda() && y.is_cuda() && x.device() == y.device(), "xent: GPU tensors");
+  TORCH_CHECK(x.dim() == 2 && x.is_contiguous() && x.size(0) > 0 && x.size(1) > 0 &&
+                  (x.scalar_type() == torch::kBFloat16 || x.scalar_type() == torch::kFloat32),
+              "xent: logits must be a contiguous 2-D bf16/fp32 tensor");
+  TORCH_CHECK(y.dim() == 1 && y.is_contiguous() && y.scalar_type() == torch::kInt64 &&
+                  y.size(0) == x.size(0), "xent: labels must be int64 [rows]");
+  TORCH_CHECK(x.numel() < (int64_t(1) << 31), "xent: too many logits");
+}
+
+std::vector<Tensor> xent_fwd(Tensor x, Tensor y) {
+  xent_check(x, y);
+  Tensor loss = torch::empty({}, x.options().dtype(torch::kFloat32));
+  Tensor lse = torch::empty({x.size(0)}, x.options().dtype(torch::kFloat32));
+  check_hip(arena_xent_fwd(x.scalar_type() == torch::kBFloat16 ? 1 : 0, x.data_ptr(),
+                           reinterpret_cast<const long long*>(y.data_ptr<int64_t>()),
+                           loss.data_ptr<float>(), lse.data_ptr<float>(),
+                           (int)x.size(0), (int)x.size(1), cur_stream()),
+            "xent_fwd");
+  return {loss, lse};
+}
+
+Tensor xent_bwd(Tensor x, Tensor y, Tensor lse, Tensor gout) {
+  xent_check(x, y);
+  TORCH_CHECK(lse.is_cuda() && lse.scalar_type() == torch::kFloat32 && lse.numel() == x.size(0) &&
+                  gout.is_cuda() && gout.scalar_type() == torch::kFloat32 && gout.numel() == 1,
+              "xent_bwd: lse fp32 [rows], grad fp32 scalar");
+  Tensor dx = torch::empty_like(x);
+  check_hip(arena_xent_bwd(x.scalar_type() == torch::kBFloat16 ? 1 : 0, x.data_ptr(),
+                           reinterpret_cast<const long long*>(y.data_ptr<int64_t>()),
+                           lse.data_ptr<float>(),
+                           gout.contiguous().data_ptr<float>(), dx.data_ptr(), (int)x.size(0),
+                           (int)x.size(1), cur_stream()),
+            "xent_bwd");
+  return dx;
+}
+
 std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
   pool_check(x, "x");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
@@ -1968,6 +2010,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("stride"), py::arg("pad"), py::arg("variant"), py::arg("splits_hint"),
         py::arg("out_fp32"), py::arg("scale"));
   m.def("maxpool_fwd", &maxpool_fwd);
+  m.def("xent_fwd", &xent_fwd);
+  m.def("xent_bwd", &xent_bwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_set_fin_max_blocks", [](int64_t p) { arena_bn_set_fin_max_blocks((int)p); });
   m.def("bn_set_nt", [](int64_t on) { arena_bn_set_nt((int)on); });

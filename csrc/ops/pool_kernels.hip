@@ -237,3 +237,114 @@ hipError_t arena_maxpool_bwd(int dtype, const void* dy, const uint8_t* pos, void
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------------------------------------------
+// Softmax cross-entropy of the classifier head (mean over rows), fp32 arithmetic on bf16 or fp32
+// logits: F.cross_entropy's result in two launches instead of its seven (upcast copy, log_softmax,
+// nll forward, two fills, nll backward, log_softmax backward, downcast copy: ~45 us per ResNet-50
+// bs128 step, profiles/r6_kernel_neighbors.txt).
+// forward: ONE block, one wave per row at a time (row r -> wave r % 16), every sum in a fixed order
+// (deterministic); writes the mean loss and each row's log-sum-exp. backward: one elementwise pass,
+// dlogits = g * (exp(x - lse) - onehot) / rows, in the logits' dtype.
+// ------------------------------------------------------------------------------------------------
+namespace {
+
+constexpr int kXentWaves = 16;
+
+template <typename T>
+__device__ __forceinline__ float xent_ld(const T* p, long long i) {
+  if constexpr (sizeof(T) == 2) return __uint_as_float((uint32_t)p[i] << 16);
+  else return p[i];
+}
+
+template <typename T>
+__global__ __launch_bounds__(64 * kXentWaves) void xent_fwd_kernel(const T* __restrict__ x,
+                                                                   const long long* __restrict__ y,
+                                                                   float* __restrict__ loss,
+                                                                   float* __restrict__ lse,
+                                                                   int rows, int classes) {
+  __shared__ float part[kXentWaves];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  float acc = 0.f;   // this wave's rows, in row order
+  for (int r = wave; r < rows; r += kXentWaves) {
+    const T* xr = x + (long long)r * classes;
+    float m = -INFINITY;
+    for (int c = lane; c < classes; c += 64) m = fmaxf(m, xent_ld(xr, c));
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float s = 0.f;
+    for (int c = lane; c < classes; c += 64) s += __expf(xent_ld(xr, c) - m);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+    const float l = m + __logf(s);
+    if (lane == 0) {
+      long long t = y[r];
+      t = t < 0 ? 0 : (t >= classes ? classes - 1 : t);
+      lse[r] = l;
+      acc += l - xent_ld(xr, t);
+    }
+  }
+  if (lane == 0) part[wave] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float tot = 0.f;
+    for (int w = 0; w < kXentWaves; ++w) tot += part[w];
+    *loss = tot / (float)rows;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void xent_bwd_kernel(const T* __restrict__ x,
+                                                       const long long* __restrict__ y,
+                                                       const float* __restrict__ lse,
+                                                       const float* __restrict__ gout,
+                                                       T* __restrict__ dx, int rows, int classes) {
+  const long long i = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (long long)rows * classes) return;
+  const int r = (int)(i / classes), c = (int)(i - (long long)r * classes);
+  long long t = y[r];
+  t = t < 0 ? 0 : (t >= classes ? classes - 1 : t);
+  const float p = __expf(xent_ld(x, i) - lse[r]);
+  const float v = (*gout) * (p - (c == t ? 1.f : 0.f)) / (float)rows;
+  if constexpr (sizeof(T) == 2) {
+    const uint32_t u = __float_as_uint(v);
+    dx[i] = (T)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);   // round to nearest even
+  } else {
+    dx[i] = v;
+  }
+}
+
+}  // namespace
+
+extern "C" {
+
+// dtype: 0 = f32, 1 = bf16 logits [rows][classes]; y: int64 [rows]; loss: fp32 scalar; lse: fp32 [rows]
+hipError_t arena_xent_fwd(int dtype, const void* x, const long long* y, float* loss, float* lse,
+                          int rows, int classes, hipStream_t stream) {
+  if (rows <= 0 || classes <= 0) return hipErrorInvalidValue;
+  if (dtype == 1)
+    hipLaunchKernelGGL(xent_fwd_kernel<uint16_t>, dim3(1), dim3(64 * kXentWaves), 0, stream,
+                       static_cast<const uint16_t*>(x), y, loss, lse, rows, classes);
+  else
+    hipLaunchKernelGGL(xent_fwd_kernel<float>, dim3(1), dim3(64 * kXentWaves), 0, stream,
+                       static_cast<const float*>(x), y, loss, lse, rows, classes);
+  return hipGetLastError();
+}
+
+hipError_t arena_xent_bwd(int dtype, const void* x, const long long* y, const float* lse,
+                          const float* gout, void* dx, int rows, int classes, hipStream_t stream) {
+  if (rows <= 0 || classes <= 0) return hipErrorInvalidValue;
+  const long long n = (long long)rows * classes;
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (dtype == 1)
+    hipLaunchKernelGGL(xent_bwd_kernel<uint16_t>, grid, dim3(256), 0, stream,
+                       static_cast<const uint16_t*>(x), y, lse, gout, static_cast<uint16_t*>(dx),
+                       rows, classes);
+  else
+    hipLaunchKernelGGL(xent_bwd_kernel<float>, grid, dim3(256), 0, stream,
+                       static_cast<const float*>(x), y, lse, gout, static_cast<float*>(dx), rows,
+                       classes);
+  return hipGetLastError();
+}
+
+}  // extern "C"

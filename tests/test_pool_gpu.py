@@ -77,3 +77,26 @@ def test_global_avg_pool_matches_adaptive_pool(dtype):
     y2.backward(g)
     assert x.grad.is_contiguous(memory_format=torch.channels_last)
     assert torch.allclose(x.grad.float(), x2.grad.float(), rtol=1e-2, atol=1e-4)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,classes", [(128, 1000), (5, 37), (33, 64)])
+def test_fused_cross_entropy_matches_torch(dtype, rows, classes):
+    """Two-launch softmax cross-entropy (mean) against F.cross_entropy on the fp32-upcast logits:
+    loss and logits gradient (scaled by a non-unit upstream gradient), run-to-run identical."""
+    from arena_amd.ops.pool import cross_entropy
+    g = torch.Generator(device="cuda").manual_seed(rows + classes)
+    x = (torch.randn(rows, classes, device="cuda", generator=g) * 3).to(dtype).requires_grad_(True)
+    y = torch.randint(0, classes, (rows,), device="cuda", generator=g)
+    x2 = x.detach().clone().requires_grad_(True)
+    loss = cross_entropy(x, y)
+    ref = F.cross_entropy(x2.float(), y)
+    assert loss.dtype == torch.float32 and loss.shape == ()
+    assert torch.allclose(loss, ref, rtol=1e-5, atol=1e-5), (float(loss), float(ref))
+    assert torch.equal(loss, cross_entropy(x.detach(), y))
+    (loss * 0.75).backward()
+    (ref * 0.75).backward()
+    assert x.grad.dtype == dtype
+    tol = 1e-2 if dtype == torch.bfloat16 else 1e-5
+    assert torch.allclose(x.grad.float(), x2.grad.float(), rtol=tol, atol=tol * 1e-2)
