@@ -66,8 +66,8 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
     """Mean over H, W of a channels_last activation, [N, C, H, W] -> [N, C]. The backward writes
     the (broadcast) gradient straight into a channels_last tensor: the stock adaptive-pool
     backward materialises it NCHW and the next layer's channels_last conversion then transposes
-    25.7 MB at ResNet-50 bs128 (14 + 45.5 us per step; this form 5 + 22 us,
-    profiles/r6_kernel_neighbors.txt)."""
+    25.7 MB at ResNet-50 bs128 (14 + 45.5 us per step; a broadcast copy into channels_last 5 + 22
+    us, profiles/r6_kernel_neighbors.txt; gap_bwd's single write pass replaces both)."""
 
     @staticmethod
     def forward(ctx, x):
@@ -77,8 +77,8 @@ class _GlobalAvgPoolFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         n, c, h, w = ctx.shape
-        # [N, C, 1, 1] broadcast with strides (C, 1, 0, 0): channel-innermost, so the copy into
-        # an NHWC tensor is one vectorised pass
+        if c % 8 == 0 and g.dtype in (torch.bfloat16, torch.float32):
+            return _ext.load().gap_bwd(g.contiguous(), h, w)   # one write pass (pool_kernels.hip)
         return (g * (1.0 / (h * w)))[:, :, None, None].expand(n, c, h, w).contiguous(
             memory_format=torch.channels_last)
 

@@ -111,6 +111,7 @@ hipError_t arena_maxpool_bwd(int, const void*, const uint8_t*, void*, int, int, 
                              int, hipStream_t);
 hipError_t arena_xent_fwd(int, const void*, const long long*, float*, float*, int, int,
                           hipStream_t);
+hipError_t arena_gap_bwd(int, const void*, void*, int, int, int, float, hipStream_t);
 hipError_t arena_xent_bwd(int, const void*, const long long*, const float*, const float*, void*,
                           int, int, hipStream_t);
 hipError_t arena_bn_fwd(int, const void*, const void*, void*, uint8_t*, long long, int, int, int,
@@ -1801,6 +1802,22 @@ Tensor xent_bwd(Tensor x, Tensor y, Tensor lse, Tensor gout) {
   return dx;
 }
 
+// Global-average-pool backward: g [N, C] -> channels_last [N, C, H, W] filled with g / (H W).
+Tensor gap_bwd(Tensor g, int64_t H, int64_t W) {
+  TORCH_CHECK(g.is_cuda() && g.dim() == 2 && g.is_contiguous() &&
+                  (g.scalar_type() == torch::kBFloat16 || g.scalar_type() == torch::kFloat32) &&
+                  g.size(1) % 8 == 0 && H > 0 && W > 0,
+              "gap_bwd: g must be a contiguous [N, C % 8 == 0] bf16/fp32 GPU tensor");
+  TORCH_CHECK(g.size(0) * H * W * g.size(1) < (int64_t(1) << 34), "gap_bwd: too large");
+  Tensor dx = torch::empty({g.size(0), g.size(1), H, W},
+                           g.options().memory_format(at::MemoryFormat::ChannelsLast));
+  check_hip(arena_gap_bwd(g.scalar_type() == torch::kBFloat16 ? 1 : 0, g.data_ptr(), dx.data_ptr(),
+                          (int)g.size(0), (int)(H * W), (int)g.size(1), 1.0f / (float)(H * W),
+                          cur_stream()),
+            "gap_bwd");
+  return dx;
+}
+
 std::vector<Tensor> maxpool_fwd(Tensor x, int64_t k, int64_t s, int64_t p) {
   pool_check(x, "x");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
@@ -2012,6 +2029,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("maxpool_fwd", &maxpool_fwd);
   m.def("xent_fwd", &xent_fwd);
   m.def("xent_bwd", &xent_bwd);
+  m.def("gap_bwd", &gap_bwd);
   m.def("maxpool_bwd", &maxpool_bwd);
   m.def("bn_set_fin_max_blocks", [](int64_t p) { arena_bn_set_fin_max_blocks((int)p); });
   m.def("bn_set_nt", [](int64_t on) { arena_bn_set_nt((int)on); });
