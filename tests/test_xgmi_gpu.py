@@ -526,7 +526,11 @@ def _zero_sgd(rank, world, port, q, bucket_mb=None):
                 if r == rank:
                     assert torch.equal(xr, x) and torch.equal(yr, y)
                 with torch.autocast("cuda", dtype=bf, cache_enabled=False):
-                    loss = torch.nn.functional.cross_entropy(model(xr), yr)
+                    logits = model(xr)
+                # the step's loss is fp32 softmax cross-entropy of the bf16 logits (the fused
+                # ops.pool.cross_entropy); autocast's own cross_entropy rounds the log-softmax
+                # to bf16 on this build, ~1 % gradient differences
+                loss = torch.nn.functional.cross_entropy(logits.float(), yr)
                 grads.append([g.float() for g in torch.autograd.grad(loss, params)])
             refs = []
             for i, p in enumerate(params):
