@@ -106,9 +106,9 @@ class _SoftmaxXentFn(torch.autograd.Function):
 
 def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     """``F.cross_entropy(logits, labels)`` (mean reduction, fp32 result, no ignore_index / label
-    smoothing) in two HIP launches on the GPU (``pool_kernels.hip`` xent kernels): forward loss +
-    per-row log-sum-exp, backward one elementwise pass in the logits' dtype. Anything else runs
-    the stock op."""
+    smoothing) on the GPU through the ``pool_kernels.hip`` xent kernels: forward per-row loss +
+    log-sum-exp (one wave per row) and their mean, backward one elementwise pass in the logits'
+    dtype. Anything else runs the stock op."""
     if (logits.is_cuda and logits.dim() == 2 and labels.dim() == 1
             and labels.dtype == torch.int64 and logits.dtype in (torch.bfloat16, torch.float32)):
         return _SoftmaxXentFn.apply(logits.contiguous(), labels.contiguous())

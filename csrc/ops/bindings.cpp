@@ -1777,14 +1777,15 @@ static void xent_check(const Tensor& x, const Tensor& y) {
 
 std::vector<Tensor> xent_fwd(Tensor x, Tensor y) {
   xent_check(x, y);
-  Tensor loss = torch::empty({}, x.options().dtype(torch::kFloat32));
-  Tensor lse = torch::empty({x.size(0)}, x.options().dtype(torch::kFloat32));
+  // one buffer: [0, rows) log-sum-exp, [rows, 2 rows) per-row loss
+  Tensor buf = torch::empty({2, x.size(0)}, x.options().dtype(torch::kFloat32));
+  Tensor lse = buf[0], rowloss = buf[1];
   check_hip(arena_xent_fwd(x.scalar_type() == torch::kBFloat16 ? 1 : 0, x.data_ptr(),
                            reinterpret_cast<const long long*>(y.data_ptr<int64_t>()),
-                           loss.data_ptr<float>(), lse.data_ptr<float>(),
+                           rowloss.data_ptr<float>(), lse.data_ptr<float>(),
                            (int)x.size(0), (int)x.size(1), cur_stream()),
             "xent_fwd");
-  return {loss, lse};
+  return {rowloss.mean(), lse};
 }
 
 Tensor xent_bwd(Tensor x, Tensor y, Tensor lse, Tensor gout) {

@@ -240,16 +240,14 @@ hipError_t arena_maxpool_bwd(int dtype, const void* dy, const uint8_t* pos, void
 
 // ------------------------------------------------------------------------------------------------
 // Softmax cross-entropy of the classifier head (mean over rows), fp32 arithmetic on bf16 or fp32
-// logits: F.cross_entropy's result in two launches instead of its seven (upcast copy, log_softmax,
-// nll forward, two fills, nll backward, log_softmax backward, downcast copy: ~45 us per ResNet-50
-// bs128 step, profiles/r6_kernel_neighbors.txt).
-// forward: ONE block, one wave per row at a time (row r -> wave r % 16), every sum in a fixed order
-// (deterministic); writes the mean loss and each row's log-sum-exp. backward: one elementwise pass,
+// logits: F.cross_entropy's result in three launches (forward, mean, backward) instead of its seven
+// (upcast copy, log_softmax, nll forward, two fills, nll backward, log_softmax backward, downcast
+// copy: ~45 us per ResNet-50 bs128 step, profiles/r6_kernel_neighbors.txt).
+// forward: one wave per row, every sum in a fixed order (deterministic); writes each row's loss and
+// log-sum-exp (the mean is taken by the caller, also deterministic). backward: one elementwise pass,
 // dlogits = g * (exp(x - lse) - onehot) / rows, in the logits' dtype.
 // ------------------------------------------------------------------------------------------------
 namespace {
-
-constexpr int kXentWaves = 16;
 
 template <typename T>
 __device__ __forceinline__ float xent_ld(const T* p, long long i) {
@@ -257,39 +255,50 @@ __device__ __forceinline__ float xent_ld(const T* p, long long i) {
   else return p[i];
 }
 
-template <typename T>
-__global__ __launch_bounds__(64 * kXentWaves) void xent_fwd_kernel(const T* __restrict__ x,
-                                                                   const long long* __restrict__ y,
-                                                                   float* __restrict__ loss,
-                                                                   float* __restrict__ lse,
-                                                                   int rows, int classes) {
-  __shared__ float part[kXentWaves];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  float acc = 0.f;   // this wave's rows, in row order
-  for (int r = wave; r < rows; r += kXentWaves) {
-    const T* xr = x + (long long)r * classes;
-    float m = -INFINITY;
+// One wave per row, four rows per block. NPL > 0: the row (<= 64 * NPL classes) is loaded into
+// registers once, all NPL loads in flight, and max / sum-exp run from registers; NPL == 0: any
+// width, three passes over memory. Writes the row's log-sum-exp and loss; the mean over rows is a
+// separate deterministic reduction (the caller's). (A single-block form -- one block walking all
+// rows, the mean in LDS -- took 60 us per ResNet-50 bs128 step at 1000 classes: eight rows per
+// wave, each waiting out its loads serially, profiles/r6_xent_fwd_before_after.txt.)
+template <typename T, int NPL>
+__global__ __launch_bounds__(256) void xent_fwd_kernel(const T* __restrict__ x,
+                                                       const long long* __restrict__ y,
+                                                       float* __restrict__ rowloss,
+                                                       float* __restrict__ lse, int rows,
+                                                       int classes) {
+  const int lane = threadIdx.x & 63;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (r >= rows) return;
+  const T* xr = x + (long long)r * classes;
+  float m = -INFINITY, s = 0.f;
+  if constexpr (NPL > 0) {
+    float v[NPL];
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) {
+      const int c = lane + 64 * j;
+      v[j] = c < classes ? xent_ld(xr, c) : -INFINITY;
+    }
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) m = fmaxf(m, v[j]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+#pragma unroll
+    for (int j = 0; j < NPL; ++j) s += lane + 64 * j < classes ? __expf(v[j] - m) : 0.f;
+  } else {
     for (int c = lane; c < classes; c += 64) m = fmaxf(m, xent_ld(xr, c));
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    float s = 0.f;
     for (int c = lane; c < classes; c += 64) s += __expf(xent_ld(xr, c) - m);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-    const float l = m + __logf(s);
-    if (lane == 0) {
-      long long t = y[r];
-      t = t < 0 ? 0 : (t >= classes ? classes - 1 : t);
-      lse[r] = l;
-      acc += l - xent_ld(xr, t);
-    }
   }
-  if (lane == 0) part[wave] = acc;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float tot = 0.f;
-    for (int w = 0; w < kXentWaves; ++w) tot += part[w];
-    *loss = tot / (float)rows;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if (lane == 0) {
+    const float l = m + __logf(s);
+    long long t = y[r];
+    t = t < 0 ? 0 : (t >= classes ? classes - 1 : t);
+    lse[r] = l;
+    rowloss[r] = l - xent_ld(xr, t);
   }
 }
 
@@ -318,16 +327,22 @@ __global__ __launch_bounds__(256) void xent_bwd_kernel(const T* __restrict__ x,
 
 extern "C" {
 
-// dtype: 0 = f32, 1 = bf16 logits [rows][classes]; y: int64 [rows]; loss: fp32 scalar; lse: fp32 [rows]
-hipError_t arena_xent_fwd(int dtype, const void* x, const long long* y, float* loss, float* lse,
-                          int rows, int classes, hipStream_t stream) {
+// dtype: 0 = f32, 1 = bf16 logits [rows][classes]; y: int64 [rows]; rowloss, lse: fp32 [rows]
+hipError_t arena_xent_fwd(int dtype, const void* x, const long long* y, float* rowloss,
+                          float* lse, int rows, int classes, hipStream_t stream) {
   if (rows <= 0 || classes <= 0) return hipErrorInvalidValue;
-  if (dtype == 1)
-    hipLaunchKernelGGL(xent_fwd_kernel<uint16_t>, dim3(1), dim3(64 * kXentWaves), 0, stream,
-                       static_cast<const uint16_t*>(x), y, loss, lse, rows, classes);
-  else
-    hipLaunchKernelGGL(xent_fwd_kernel<float>, dim3(1), dim3(64 * kXentWaves), 0, stream,
-                       static_cast<const float*>(x), y, loss, lse, rows, classes);
+  const dim3 grid((unsigned)((rows + 3) / 4)), block(256);
+#define XENT_LAUNCH(T, NPL)                                                                     \
+  hipLaunchKernelGGL((xent_fwd_kernel<T, NPL>), grid, block, 0, stream,                         \
+                     static_cast<const T*>(x), y, rowloss, lse, rows, classes)
+  if (dtype == 1) {
+    if (classes <= 64 * 16) XENT_LAUNCH(uint16_t, 16);
+    else XENT_LAUNCH(uint16_t, 0);
+  } else {
+    if (classes <= 64 * 16) XENT_LAUNCH(float, 16);
+    else XENT_LAUNCH(float, 0);
+  }
+#undef XENT_LAUNCH
   return hipGetLastError();
 }
 
