@@ -1676,6 +1676,9 @@ Tensor s2d_stem(Tensor x) {
                   x.is_contiguous(at::MemoryFormat::ChannelsLast) && x.size(1) <= 4 &&
                   x.size(2) % 2 == 0 && x.size(3) % 2 == 0,
               "s2d_stem: channels_last bf16/fp32 [N, C<=4, H, W] with even H, W");
+  // the kernel loads a pixel pair's 2C values as C 8-byte (fp32) / 4-byte (bf16) words
+  if (reinterpret_cast<uintptr_t>(x.data_ptr()) % (f32 ? 8 : 4))
+    x = x.clone(at::MemoryFormat::ChannelsLast);
   const int64_t N = x.size(0), C = x.size(1), H = x.size(2), W = x.size(3);
   Tensor z = torch::empty({N, 16, H / 2, W / 2}, x.options().dtype(torch::kBFloat16).memory_format(
                                                      at::MemoryFormat::ChannelsLast));

@@ -2278,32 +2278,46 @@ __device__ __forceinline__ uint16_t s2d_in(float v) {
   return (uint16_t)(__builtin_bit_cast(uint32_t, __builtin_convertvector(p, bf16x2_t)) & 0xffffu);
 }
 
-template <typename TIn>
+// x's two pixels (2j, 2j+1) of one row are 2C contiguous elements, and in z they are channels
+// dy*2C .. dy*2C + 2C-1: each thread copies two runs, as C 8-byte (fp32) or 4-byte (bf16) loads --
+// both aligned because W is even. Index math in 32 bits when the pixel count allows (two 64-bit
+// divisions per thread cost more than its loads).
+template <typename TIn, int C, typename I>
 __global__ __launch_bounds__(256) void s2d_stem_kernel(const TIn* __restrict__ x,
                                                        uint16_t* __restrict__ z, int N, int H,
-                                                       int W, int C) {
-  const int Hz = H >> 1, Wz = W >> 1;
-  const long long p = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (p >= (long long)N * Hz * Wz) return;
-  const int j = (int)(p % Wz);
-  const long long t = p / Wz;
-  const int i = (int)(t % Hz), n = (int)(t / Hz);
+                                                       int W) {
+  const I Hz = (I)(H >> 1), Wz = (I)(W >> 1);
+  const I p = (I)blockIdx.x * 256 + (I)threadIdx.x;
+  if (p >= (I)N * Hz * Wz) return;
+  const I t = p / Wz;
+  const I j = p - t * Wz;
+  const I n = t / Hz;
+  const I i = t - n * Hz;
   uint16_t v[16];
 #pragma unroll
   for (int k = 0; k < 16; ++k) v[k] = 0;
 #pragma unroll
-  for (int d = 0; d < 4; ++d) {
-    const TIn* src = x + (((size_t)n * H + 2 * i + (d >> 1)) * W + 2 * j + (d & 1)) * C;
+  for (int dy = 0; dy < 2; ++dy) {
+    const TIn* src = x + (((size_t)n * H + 2 * (size_t)i + dy) * W + 2 * (size_t)j) * C;
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
-      if (c < C) v[d * C + c] = s2d_in(src[c]);
+    for (int q = 0; q < C; ++q) {
+      if constexpr (sizeof(TIn) == 4) {
+        const float2 f = reinterpret_cast<const float2*>(src)[q];
+        v[dy * 2 * C + 2 * q] = s2d_in(f.x);
+        v[dy * 2 * C + 2 * q + 1] = s2d_in(f.y);
+      } else {
+        const uint32_t u = reinterpret_cast<const uint32_t*>(src)[q];
+        v[dy * 2 * C + 2 * q] = (uint16_t)(u & 0xffffu);
+        v[dy * 2 * C + 2 * q + 1] = (uint16_t)(u >> 16);
+      }
+    }
   }
   uint4 o0, o1;
   o0.x = v[0] | ((uint32_t)v[1] << 16); o0.y = v[2] | ((uint32_t)v[3] << 16);
   o0.z = v[4] | ((uint32_t)v[5] << 16); o0.w = v[6] | ((uint32_t)v[7] << 16);
   o1.x = v[8] | ((uint32_t)v[9] << 16); o1.y = v[10] | ((uint32_t)v[11] << 16);
   o1.z = v[12] | ((uint32_t)v[13] << 16); o1.w = v[14] | ((uint32_t)v[15] << 16);
-  uint4* dst = reinterpret_cast<uint4*>(z + p * 16);
+  uint4* dst = reinterpret_cast<uint4*>(z + (size_t)p * 16);
   dst[0] = o0;
   dst[1] = o1;
 }
@@ -2361,12 +2375,26 @@ extern "C" hipError_t arena_s2d_stem(const void* x, void* z, int N, int H, int W
   if (N <= 0 || H % 2 || W % 2 || C < 1 || C > 4) return hipErrorInvalidValue;
   const long long P = (long long)N * (H / 2) * (W / 2);
   const dim3 g((unsigned)((P + 255) / 256));
-  if (in_f32)
-    hipLaunchKernelGGL(s2d_stem_kernel<float>, g, dim3(256), 0, st, (const float*)x,
-                       (uint16_t*)z, N, H, W, C);
-  else
-    hipLaunchKernelGGL(s2d_stem_kernel<uint16_t>, g, dim3(256), 0, st, (const uint16_t*)x,
-                       (uint16_t*)z, N, H, W, C);
+  const bool small = P < (1ll << 31);
+#define S2D_LAUNCH(TIn, CC)                                                                    \
+  do {                                                                                         \
+    if (small)                                                                                 \
+      hipLaunchKernelGGL((s2d_stem_kernel<TIn, CC, unsigned>), g, dim3(256), 0, st,            \
+                         (const TIn*)x, (uint16_t*)z, N, H, W);                                \
+    else                                                                                       \
+      hipLaunchKernelGGL((s2d_stem_kernel<TIn, CC, long long>), g, dim3(256), 0, st,           \
+                         (const TIn*)x, (uint16_t*)z, N, H, W);                                \
+  } while (0)
+#define S2D_C(TIn)                  \
+  switch (C) {                      \
+    case 1: S2D_LAUNCH(TIn, 1); break; \
+    case 2: S2D_LAUNCH(TIn, 2); break; \
+    case 3: S2D_LAUNCH(TIn, 3); break; \
+    default: S2D_LAUNCH(TIn, 4); break; \
+  }
+  if (in_f32) S2D_C(float) else S2D_C(uint16_t)
+#undef S2D_C
+#undef S2D_LAUNCH
   return hipGetLastError();
 }
 

@@ -872,6 +872,27 @@ def test_s2d_stem_fp32_input_rounds_like_the_cast():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("c", [1, 2, 3, 4])
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_s2d_stem_layout_matches_torch(c, dtype):
+    """z[n, (dy*2 + dx)*C + c, i, j] = x[n, c, 2i + dy, 2j + dx], channels 4C..15 zero; also from
+    a view whose storage offset breaks the kernel's word alignment."""
+    from arena_amd.ops import _ext
+    base = torch.randn(2 * 10 * 14 * c + 1, device="cuda").to(dtype)
+    for x in (base[:-1].view(2, 10, 14, c).permute(0, 3, 1, 2),
+              base[1:].view(2, 10, 14, c).permute(0, 3, 1, 2)):
+        assert x.is_contiguous(memory_format=torch.channels_last)
+        z = _ext.load().s2d_stem(x)
+        xb = x.to(torch.bfloat16)
+        ref = torch.zeros(2, 16, 5, 7, dtype=torch.bfloat16, device="cuda")
+        for dy in range(2):
+            for dx in range(2):
+                d = dy * 2 + dx
+                ref[:, d * c:(d + 1) * c] = xb[:, :, dy::2, dx::2]
+        assert torch.equal(z, ref)
+
+
+@pytest.mark.gpu
 def test_masked_residual_join_matches_materialized():
     """Identity blocks whose last BN parks (dy, ReLU bits) in the residual join (the conv's
     backward-data epilogue adds dy where the bit is set) give the same gradients, bit for bit,
